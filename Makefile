@@ -1,0 +1,25 @@
+# Builds libsa_hip.so (the C-ABI hot-path library) for MI355X / gfx950.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH  ?= gfx950
+SRC   := $(wildcard stereoanywhere_amd/csrc/*.hip)
+HDR   := $(wildcard stereoanywhere_amd/csrc/*.h) include/stereoanywhere_hip.h
+OUT   := stereoanywhere_amd/lib/libsa_hip.so
+OBJ   := $(patsubst stereoanywhere_amd/csrc/%.hip,build/%.o,$(SRC))
+# -ffp-contract=off: keep the reference's separate fp32 multiplies and adds
+# (no fused multiply-add contraction) in the elementwise epilogues.
+FLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result
+
+all: $(OUT)
+
+build/%.o: stereoanywhere_amd/csrc/%.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(FLAGS) -c $< -o $@
+
+$(OUT): $(OBJ)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ)
+
+clean:
+	rm -rf build $(OUT)
+
+.PHONY: all clean

@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Throughput of the MI355X StereoAnywhere forward on synthetic 540x960 pairs.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Metric (BASELINE.json): stereo pairs/s at 540x960 "D=192" (a label: the reference volume
+is all-pairs over W/4), configs[1]: batch 4 per GPU, padded to 544x960
+(test.py:206-213), 22 GRU iterations, published flags, seeded weights, fp32.
+A step = one test_mode forward over the rank's batch, inputs resident in HBM.
+Weak scaling: every rank runs its own batch of 4; value = all pairs / max-over-ranks time.
+
+Also reported (rank 0):
+  roofline      the dominant hand-written kernel, timed live with HIP events on its
+                launch stream inside the timed region (libsa_hip sa_timing_*),
+                algorithmic bytes or flops per launch / mean launch time vs MI355X peak
+  cpu_baseline  the oracle CPU restatement (torch CPU + numpy, parity-pinned to the
+                reference) on one 544x960 pair, all host threads, N=1 only
+  epe_vs_reference  EPE of this build vs the reference's own disparity (golden vector,
+                544x960, 22 iterations) on identical inputs and weights
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from stereoanywhere_amd import _native as N  # noqa: E402
+from stereoanywhere_amd import dist as D  # noqa: E402
+from stereoanywhere_amd import synth  # noqa: E402
+from stereoanywhere_amd.model import StereoAnywhere  # noqa: E402
+
+PUBLISHED = dict(use_truncate_vol=True, use_aggregate_mono_vol=True, vol_n_masks=8, n_additional_hourglass=0,
+                 vol_downsample=0, mirror_conf_th=0.98, mirror_attenuation=0.9, lrc_th=1.0, normal_gain=10)
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8 TB/s spec
+FP32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_*_f32 dense peak
+
+
+def algorithmic_cost(kernel: str, B: int, H4: int, W4: int, C: int = 256):
+    """(unit, amount per launch) of the minimal traffic / work of one launch at batch B."""
+    px = B * H4 * W4
+    vol = px * W4
+    lv = [W4, W4 // 2, W4 // 4, W4 // 8]
+    if kernel == "corr_volume_pyramid":  # fp32 MFMA-bound: 2*C flops per volume cell
+        return "TFLOP/s", 2.0 * vol * C
+    if kernel == "corr_lookup":  # 2 volumes x 4 levels x 10 cells read + 72 taps written + coords
+        return "GB/s", px * (2 * 4 * 10 * 4 + 72 * 4 + 4)
+    if kernel == "mono_masked_volume":  # 8-channel fp32 volume written; normals/maps read
+        return "GB/s", 8 * vol * 4 + px * 2 * 4 * 4
+    if kernel == "softargmin_conf":  # two volumes read once, four maps written
+        return "GB/s", 2 * vol * 4 + 4 * px * 4
+    if kernel == "gru_zr":  # per level: xc(2C) + hzr(2C) + cz,cr(2C) + h(C) read, z,rh(2C) written
+        return "GB/s", None
+    if kernel == "convex_upsample":
+        return "GB/s", px * (144 + 1) * 4 + px * 16 * 4
+    return "GB/s", None
+
+
+def make_inputs(B, H, W, Hp, Wp, D, seed0, device):
+    pb = synth.synthetic_batch(B, H, W, D, seed0=seed0)
+    out = {}
+    for k in ("left", "right", "mono_left", "mono_right"):
+        x, _ = synth.pad_to_multiple(pb[k], 32)
+        assert x.shape[-2:] == (Hp, Wp)
+        out[k] = torch.from_numpy(np.ascontiguousarray(x)).to(device)
+    return out
+
+
+def cpu_baseline(iters: int, H: int, W: int):
+    """The oracle restatement on one pair (bounded sample), all host threads."""
+    from oracle import model_ref as M
+
+    torch.set_num_threads(os.cpu_count() or 1)
+    sd = M.load_state_dict_seeded(0)
+    pair = synth.synthetic_batch(1, H, W, 192.0, seed0=1)
+    t = [torch.from_numpy(pair[k]) for k in ("left", "right", "mono_left", "mono_right")]
+    t0 = time.perf_counter()
+    M.forward(sd, *t, iters=iters)
+    dt = time.perf_counter() - t0
+    return {"value": 1.0 / dt, "unit": "pairs/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"1 pair 1x{H}x{W}, {iters} iters, oracle (torch CPU convs + numpy hot path), "
+                      f"{dt:.1f} s wall"}
+
+
+def epe_vs_reference(model, device):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fixtures_util import load_fixture, regenerate_inputs  # golden data only
+
+    fix = load_fixture("cfg2_544x960_it22.npz")
+    pair = regenerate_inputs(fix, 1, 544, 960, 192.0)
+    t = [torch.from_numpy(pair[k]).to(device) for k in ("left", "right", "mono_left", "mono_right")]
+    flow_up, _ = model(*t, iters=22, test_mode=True)
+    disp = -flow_up[:, 0].cpu().numpy()
+    return float(np.abs(disp.astype(np.float64) - fix["disparity"]).mean())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=4, help="pairs per GPU (configs[1]: 4)")
+    ap.add_argument("--iters", type=int, default=22)
+    ap.add_argument("--height", type=int, default=540)
+    ap.add_argument("--width", type=int, default=960)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-epe", action="store_true")
+    args = ap.parse_args()
+
+    r = D.init_from_env("nccl")
+    device = torch.device("cuda", r.local_rank)
+    torch.cuda.set_device(device)
+    if r.world != args.gpus and r.is_main:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {r.world}", file=sys.stderr)
+
+    H, W = args.height, args.width
+    Hp, Wp = (H + 31) // 32 * 32, (W + 31) // 32 * 32
+    H4, W4 = Hp // 4, Wp // 4
+    model = StereoAnywhere(dict(PUBLISHED)).eval()
+    synth.load_seeded_weights(model, 0)
+    model = model.to(device)
+    lo, hi = D.shard_range(args.batch * r.world, r.rank, r.world)
+    inp = make_inputs(hi - lo, H, W, Hp, Wp, 192.0, seed0=1 + lo, device=device)
+    x = (inp["left"], inp["right"], inp["mono_left"], inp["mono_right"])
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            model(*x, iters=args.iters, test_mode=True)
+        torch.cuda.synchronize()
+        N.timing_enable(True)
+        D.barrier(r)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out, _ = model(*x, iters=args.iters, test_mode=True)
+        torch.cuda.synchronize()
+        D.barrier(r)
+        elapsed = time.perf_counter() - t0
+        kt = {k: N.timing_read(k) for k in N.KERNEL_IDS}
+        N.timing_enable(False)
+        elapsed = D.max_over_ranks(elapsed, r, device)
+        # per-pair metrics gathered once, after the timed region (the only collective)
+        disp = -out[:, 0]
+        local = torch.stack([disp.mean((1, 2)), disp.amin((1, 2)), disp.amax((1, 2))], 1).double()
+        allm = D.gather_metrics(local, r)
+
+    total_pairs = args.batch * r.world * args.steps
+    if not r.is_main:
+        return
+    # dominant hand-written kernel by summed time in the timed region
+    mine = {k: v for k, v in kt.items() if k != "misc" and v[1] > 0}
+    dom = max(mine, key=lambda k: mine[k][0])
+    ms_tot, n_launch = mine[dom]
+    avg_s = ms_tot / 1e3 / n_launch
+    unit, amount = algorithmic_cost(dom, hi - lo, H4, W4)
+    if unit == "TFLOP/s":
+        achieved = amount / avg_s / 1e12
+        peak, bound = FP32_MFMA_PEAK_TFS, "mfma"
+    else:
+        achieved = (amount / avg_s / 1e9) if amount else None
+        peak, bound = HBM_PEAK_GBS, "hbm"
+    roof = {"kernel": dom, "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
+            "frac": (achieved / peak) if achieved else None, "traffic": None,
+            "avg_launch_us": avg_s * 1e6, "launches": n_launch,
+            "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]}}
+    res = {
+        "metric": "stereo pairs/sec @540x960 D=192 (1/2/4/8 GPU) + EPE vs reference",
+        "value": total_pairs / elapsed, "unit": "pairs/s", "n_gpus": r.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded value-noise pairs, "
+        "seeded random weights; no dataset/checkpoint offline)",
+        "config": {"workload": f"configs[1]: batch {args.batch}/GPU x {H}x{W} (padded {Hp}x{Wp}), "
+                               f"{args.iters} GRU iters, published flags", "global_batch": args.batch * r.world,
+                   "iters": args.iters, "parallelism": f"dp{r.world} (independent pairs, metrics all_gather)"},
+        "roofline": roof,
+        "gathered_pairs": int(allm.shape[0]),
+    }
+    if not args.no_epe:
+        res["epe_vs_reference"] = epe_vs_reference(model, device)
+    if r.world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(args.iters, Hp, Wp)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

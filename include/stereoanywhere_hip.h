@@ -1,0 +1,174 @@
+/*
+ * stereoanywhere_hip.h — C ABI of the MI355X (gfx950) cost-volume hot path.
+ *
+ * One shared library, libsa_hip.so, built by hipcc from the .hip sources in
+ * stereoanywhere_amd/csrc/.
+ * Every entry point takes plain device pointers and sizes (no framework types):
+ *   - all tensors are float32, dense, row-major in the layout documented per call;
+ *   - `stream` is a hipStream_t (NULL = the default stream); calls only enqueue work
+ *     and never synchronise the host (the reference's implicit syncs at
+ *     utils/utils.py:26 and :361-368 disappear);
+ *   - the return value is SA_OK or a negative SA_E_* code; sa_last_error() gives a
+ *     message for the calling thread.  Argument checks reproduce the failures the
+ *     reference raises as Python exceptions (stereoanywhere.py:133, utils.py:26).
+ *
+ * The library replaces the torch-level operator plug-in point of the reference:
+ * `args.corr_implementation` (stereoanywhere.py:25, 128-133) and the `CorrBlock1D`
+ * class contract (corr.py:75-132) — see INTEGRATION.md for the bindings.
+ * Reference paths below are relative to the kei312/stereoanywhere root.
+ */
+#ifndef STEREOANYWHERE_HIP_H
+#define STEREOANYWHERE_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  SA_OK = 0,
+  SA_E_ARG = -1,        /* bad shape / null pointer / unsupported size           */
+  SA_E_LAUNCH = -2,     /* hipLaunchKernel or hipGetLastError failed             */
+  SA_E_RUNTIME = -3     /* other HIP runtime failure (events, memset)            */
+};
+
+int sa_abi_version(void);
+const char *sa_last_error(void);
+
+/* ----------------------------------------------------------------------------------
+ * Correlation pyramid storage.  The reference keeps num_levels+1 separate tensors
+ * [B*H*W1, 1, 1, W2>>i] (corr.py:85-91).  Here one buffer holds, for every pixel row
+ * (b,h,j), the levels back to back: [L0 (W2) | L1 (W2/2) | L2 | L3 ...] (floor at every
+ * halving), the row padded to a multiple of 4 floats.  Level `num_levels` (built but
+ * never read by the reference, corr.py:101) is not stored.
+ * ---------------------------------------------------------------------------------- */
+int  sa_pyramid_level_width(int w2, int level);
+int  sa_pyramid_level_offset(int w2, int level);
+long sa_pyramid_row_stride(int w2, int num_levels);
+
+/* a1 + a8 + a9 — replaces CorrBlock1D.corr (corr.py:117-132) followed by the
+ * truncation multiply (stereoanywhere.py:201-205, 253-254, utils.py:216-238) and
+ * CorrBlock1D.__init__ (corr.py:76-91).
+ *   fmap2 [B,C,H,W1], fmap3 [B,C,H,W2]  (NCHW, as produced by fnet)
+ *   V[b,h,j,k] = sum_c fmap2[b,c,h,j] fmap3[b,c,h,k] / sqrt_c   (fp32 MFMA, exact f32)
+ *   if trunc_disp != NULL:  V *= (1 - m) + m (sigmoid((j - d) - k)(1 - atten) + atten)
+ *     with d = trunc_disp[b,h,j], m = trunc_conf[b,h,j]   ([B,H,W1] each)
+ *   pyramid: [B*H*W1, row_stride] as above, levels 0..num_levels-1 written.
+ * num_levels = 1 gives the plain volume ([B,H,W1,W2] when row_stride == W2). */
+int sa_corr_volume_pyramid(const float *fmap2, const float *fmap3, int B, int C, int H, int W1,
+                           int W2, float sqrt_c, const float *trunc_disp, const float *trunc_conf,
+                           float atten, int num_levels, float *pyramid, long row_stride,
+                           void *stream);
+
+/* a9 alone — CorrBlock1D.__init__ (corr.py:76-91) on an existing volume.
+ *   volume: `rows` rows of W2 floats with stride in_row_stride (level 0 is copied). */
+int sa_corr_pyramid_from_volume(const float *volume, long rows, int W2, long in_row_stride,
+                                int num_levels, float *pyramid, long row_stride, void *stream);
+
+/* a10 — CorrBlock1D.__call__ (corr.py:93-115) + bilinear_sampler (utils.py:19-35).
+ *   coords_x: x channel of coords1, element (b,h,j) at coords_x[b*coords_bstride + h*W1 + j]
+ *   out: element (b, v*L*(2r+1) + l*(2r+1) + t, h, j) at
+ *        out[b*out_bstride + (v*L*(2r+1) + l*(2r+1) + t)*H*W1 + h*W1 + j]
+ *   where v = 0 for pyramid_a and 1 for pyramid_b (pyramid_b may be NULL).  Zero
+ *   padding outside [0, W_l - 1]; same normalise/unnormalise round trip as grid_sample. */
+int sa_corr_lookup(const float *pyramid_a, const float *pyramid_b, int W2, long row_stride,
+                   int num_levels, int radius, const float *coords_x, long coords_bstride,
+                   int B, int H, int W1, float *out, long out_bstride, void *stream);
+
+/* a2 — estimate_normals (utils.py:73-77) on the 1/4-res mono map.
+ *   mde [B,1,H,W] -> normals [B,3,H,W]; gain = W/normal_gain (stereoanywhere.py:113). */
+int sa_mono_normals(const float *mde, int B, int H, int W, float gain, float *normals,
+                    void *stream);
+
+/* a2 + a3 — 1.73 * corr(normals_l, normals_r) (stereoanywhere.py:136) binned by the
+ * half-open depth masks (utils.py:48-54, stereoanywhere.py:138-139, 161), written
+ * directly in the hourglass's [B, nbins, W2, H, W1] layout (hourglass.py:63).
+ *   n2 [B,3,H,W1], n3 [B,3,H,W2], m2 [B,1,H,W1], m3 [B,1,H,W2] (1/4-res mono maps). */
+int sa_mono_masked_volume(const float *n2, const float *n3, const float *m2, const float *m3,
+                          int B, int H, int W1, int W2, int nbins, float gain, float *out,
+                          void *stream);
+
+/* a5 + a6 — estimate_left/right_disparity (utils.py:112-152) and
+ * estimate_left/right_confidence (utils.py:154-170) on volumes given by strides
+ * (element (b,h,j,k) at v[b*sb + h*sh + j*sj + k*sk]; sj == 1 or sk == 1).
+ *   vol_disp -> dL [B,H,W1], dR [B,H,W2];  vol_conf -> cL [B,H,W1], cR [B,H,W2], each
+ *   output map's element (b,h,o) at out[b*out_bs + h*W + o] (out_bs = H*W for [B,1,H,W]). */
+int sa_softargmin_conf(const float *vol_disp, const float *vol_conf, int B, int H, int W1,
+                       int W2, long sb, long sh, long sj, long sk, float *dL, float *dR,
+                       float *cL, float *cR, long out_bs, void *stream);
+
+/* a7 — softlrc (utils.py:189-198) with disp_warping (utils.py:172-187); optional
+ * fuzzy_and with a confidence (utils.py:240-241, stereoanywhere.py:188-189):
+ *   s2 = softlrc_2 * (conf2 ? conf2 : 1), s3 likewise.  All maps [H,W] planes with batch
+ *   stride map_bs (H*W for [B,1,H,W]; 2*H*W for the L/R halves of a [B,2,H,W] buffer). */
+int sa_softlrc(const float *d2, const float *d3, const float *conf2, const float *conf3, int B,
+               int H, int W, long map_bs, float lrc_th, float *s2, float *s3, void *stream);
+
+/* a7 — weighted_lsq (utils.py:345-384) over the joint L+R maps of each sample:
+ *   maps [B, 2, H, W] each (mde, disp, conf); exact torch.quantile(linear) band
+ *   [q_lo, q_hi] on relu(disp) (radix select, no host sync), weighted least squares in
+ *   float64 accumulation.  Writes scale[B], shift[B] (device). */
+int sa_weighted_lsq(const float *mde, const float *disp, const float *conf, int B, int n_per_b,
+                    float q_lo, float q_hi, float *scale, float *shift, void *stream);
+
+/* a7 + a8 + a11 — scaled mono (stereoanywhere.py:194-197), its softLRC (199), the mirror
+ * detector (utils.py:255-269) and the initial coordinates (stereoanywhere.py:261-262):
+ *   sm2 = scale*m2 + shift, sm3 = scale*m3 + shift                     [B,1,H,W]
+ *   mirror = detector(dL, sm2, conf_l, softlrc(sm2, sm3))              [B,1,H,W]
+ *   coords_x = x - sm2                                                  [B,1,H,W]
+ * Inputs m2, m3, dL, conf_l are [H,W] planes with batch stride in_bs; outputs dense. */
+int sa_mono_scale_mirror(const float *m2, const float *m3, const float *scale, const float *shift,
+                         const float *dL, const float *conf_l, int B, int H, int W, long in_bs,
+                         float lrc_th, float conf_th, float *sm2, float *sm3, float *mirror,
+                         float *coords_x, void *stream);
+
+/* a12 — ConvGRU gates (update.py:53-62) with the convolution split by input
+ * (conv([h,x]) = conv_h(h) + conv_x(x)); all tensors [B, ch, H, W] with batch strides.
+ *   gru_zr: z = sigmoid(xc[0:C] + hzr[0:C] + cz), r = sigmoid(xc[C:2C] + hzr[C:2C] + cr),
+ *           writes z and rh = r*h.
+ *   gru_out: h = (1 - z) h + z tanh(xc[2C:3C] + qh + cq)   (in place on h). */
+int sa_gru_zr(const float *xc, long xc_bs, const float *hzr, long hzr_bs, const float *cz,
+              const float *cr, long c_bs, const float *h, long h_bs, int B, int C, int HW,
+              float *z, float *rh, void *stream);
+int sa_gru_out(const float *xc, long xc_bs, const float *qh, long qh_bs, const float *cq,
+               long c_bs, const float *z, int B, int C, int HW, float *h, long h_bs,
+               void *stream);
+
+/* Update-block plumbing that writes straight into channel slices of the GRU inputs
+ * (replaces the torch.cat calls of update.py:54-59, 88-90):
+ *   pool2x: avg_pool2d(3, stride 2, pad 1, count_include_pad) (update.py:124-125)
+ *   interp: bilinear, align_corners=True resize (update.py:130-132)
+ *   relu_copy: out = max(in, 0)
+ *   flow_update: coords_x += delta[:, 0] (delta may be NULL; stereoanywhere.py:277-280) and
+ *     writes the 2-plane flow [coords_x - x, 0] (stereoanywhere.py:272) into flow_a and
+ *     flow_b (either may be NULL) — the convf1 input and the tail of the motion
+ *     features (update.py:90). */
+int sa_pool2x(const float *in, long in_bs, int B, int C, int H, int W, float *out, long out_bs,
+              void *stream);
+int sa_interp_bilinear_ac(const float *in, long in_bs, int B, int C, int H, int W, int Ho, int Wo,
+                          float *out, long out_bs, void *stream);
+int sa_relu_copy(const float *in, long in_bs, int B, int C, int HW, float *out, long out_bs,
+                 void *stream);
+int sa_flow_update(float *coords_x, const float *delta, long delta_bs, int B, int H, int W,
+                   float *flow_a, long flow_a_bs, float *flow_b, long flow_b_bs, void *stream);
+
+/* a14 — convex_upflow (utils.py:97-110), factor 4: flow [B,1,H,W] (low-res x flow),
+ * mask [B, 9*f*f, H, W] -> out [B,1,f*H,f*W] (sign as given: the reference's
+ * flow_up, i.e. minus the disparity). */
+int sa_convex_upsample(const float *flow, const float *mask, long mask_bs, int B, int H, int W,
+                       int factor, float *out, void *stream);
+
+/* Live per-kernel timing for bench.py: when enabled, every launch of kernel `id`
+ * is bracketed by hipEvents on the launch stream; sa_timing_read synchronises the
+ * recorded events and returns their summed duration (ms) and count, then clears. */
+enum {
+  SA_K_CORR_PYRAMID = 0, SA_K_LOOKUP, SA_K_MONO_VOLUME, SA_K_SOFTARGMIN, SA_K_LSQ,
+  SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_COUNT
+};
+int sa_timing_enable(int on);
+int sa_timing_read(int kernel_id, double *total_ms, long *count);
+const char *sa_kernel_name(int kernel_id);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STEREOANYWHERE_HIP_H */

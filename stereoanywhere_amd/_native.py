@@ -1,0 +1,107 @@
+"""ctypes binding of libsa_hip.so (the C ABI declared in include/stereoanywhere_hip.h).
+
+The library is built in-tree (``make`` or ``stereoanywhere_amd._native.build()``) so the
+.so travels with the repo snapshot to the GPU box.  There is no fallback: if the
+library is missing every op raises, loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(_HERE, "lib", "libsa_hip.so")
+HEADER = os.path.join(ROOT, "include", "stereoanywhere_hip.h")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_long
+F = ctypes.c_float
+
+# name -> (restype, argtypes); must match include/stereoanywhere_hip.h exactly
+SIGNATURES = {
+    "sa_abi_version": (I, []),
+    "sa_last_error": (ctypes.c_char_p, []),
+    "sa_pyramid_level_width": (I, [I, I]),
+    "sa_pyramid_level_offset": (I, [I, I]),
+    "sa_pyramid_row_stride": (L, [I, I]),
+    "sa_corr_volume_pyramid": (I, [P, P, I, I, I, I, I, F, P, P, F, I, P, L, P]),
+    "sa_corr_pyramid_from_volume": (I, [P, L, I, L, I, P, L, P]),
+    "sa_corr_lookup": (I, [P, P, I, L, I, I, P, L, I, I, I, P, L, P]),
+    "sa_mono_normals": (I, [P, I, I, I, F, P, P]),
+    "sa_mono_masked_volume": (I, [P, P, P, P, I, I, I, I, I, F, P, P]),
+    "sa_softargmin_conf": (I, [P, P, I, I, I, I, L, L, L, L, P, P, P, P, L, P]),
+    "sa_softlrc": (I, [P, P, P, P, I, I, I, L, F, P, P, P]),
+    "sa_weighted_lsq": (I, [P, P, P, I, I, F, F, P, P, P]),
+    "sa_mono_scale_mirror": (I, [P, P, P, P, P, P, I, I, I, L, F, F, P, P, P, P, P]),
+    "sa_gru_zr": (I, [P, L, P, L, P, P, L, P, L, I, I, I, P, P, P]),
+    "sa_gru_out": (I, [P, L, P, L, P, L, P, I, I, I, P, L, P]),
+    "sa_pool2x": (I, [P, L, I, I, I, I, P, L, P]),
+    "sa_interp_bilinear_ac": (I, [P, L, I, I, I, I, I, I, P, L, P]),
+    "sa_relu_copy": (I, [P, L, I, I, I, P, L, P]),
+    "sa_flow_update": (I, [P, P, L, I, I, I, P, L, P, L, P]),
+    "sa_convex_upsample": (I, [P, P, L, I, I, I, I, P, P]),
+    "sa_timing_enable": (I, [I]),
+    "sa_timing_read": (I, [I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]),
+    "sa_kernel_name": (ctypes.c_char_p, [I]),
+}
+
+KERNEL_IDS = {
+    "corr_volume_pyramid": 0, "corr_lookup": 1, "mono_masked_volume": 2, "softargmin_conf": 3,
+    "weighted_lsq": 4, "gru_zr": 5, "gru_out": 6, "convex_upsample": 7, "misc": 8,
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def build(verbose: bool = False) -> str:
+    """Compile libsa_hip.so for gfx950 with hipcc (via the repo Makefile)."""
+    cmd = ["make", "-C", ROOT, "-j8"]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise NativeError(f"building libsa_hip.so failed:\n{res.stdout}\n{res.stderr}")
+    if verbose:
+        print(res.stdout)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(
+                f"{LIB_PATH} is missing: the HIP hot path has no fallback. Build it with `make` "
+                "or stereoanywhere_amd._native.build().")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().sa_last_error().decode(errors="replace")
+        raise NativeError(f"{name} failed ({rc}): {msg}")
+
+
+def timing_enable(on: bool) -> None:
+    call("sa_timing_enable", 1 if on else 0)
+
+
+def timing_read(kernel: str):
+    """(total_ms, launches) of one kernel since timing_enable / the last read."""
+    ms = ctypes.c_double()
+    n = ctypes.c_long()
+    call("sa_timing_read", KERNEL_IDS[kernel], ctypes.byref(ms), ctypes.byref(n))
+    return ms.value, n.value

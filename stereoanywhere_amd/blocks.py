@@ -1,0 +1,244 @@
+"""Dense convolution blocks that stay on PyTorch / MIOpen (fp32) in this tier.
+
+Module and parameter names reproduce the reference's state-dict layout exactly
+(tests/golden/state_dict_keys.json, 390 entries) so reference checkpoints load with
+``strict=True`` after stripping DataParallel's ``module.`` prefix (test.py:142-152):
+  * ``ResidualBlock`` / ``BasicEncoder`` / ``MultiBasicEncoder`` — extractor.py:6-300
+  * ``BasicConv`` / ``DoubleFeatureAtt`` — submodule.py:25-53, 113-140
+  * ``Hourglass`` — hourglass.py:13-91, run in its native [B, C, W2, H, W1] layout
+  * ``BasicMultiUpdateBlock`` parameters — update.py:46-197 (the forward of the
+    update step lives in model.py, where the GRU convolutions are split by input)
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _norm2d(kind: str, ch: int) -> nn.Module:
+    return {"batch": nn.BatchNorm2d, "instance": nn.InstanceNorm2d}[kind](ch)
+
+
+class ResidualBlock(nn.Module):
+    """Two 3x3 convs + norm + ReLU with an optional strided 1x1 projection (extractor.py:6-60).
+    The projection's norm is registered under both ``norm3`` and ``downsample.1``."""
+
+    def __init__(self, cin: int, cout: int, norm: str, stride: int = 1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride=stride, padding=1)
+        self.conv2 = nn.Conv2d(cout, cout, 3, padding=1)
+        self.relu = nn.ReLU(inplace=True)
+        self.norm1 = _norm2d(norm, cout)
+        self.norm2 = _norm2d(norm, cout)
+        project = stride != 1 or cin != cout
+        if project:
+            self.norm3 = _norm2d(norm, cout)
+            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride=stride), self.norm3)
+        else:
+            self.downsample = None
+
+    def forward(self, x):
+        y = self.relu(self.norm1(self.conv1(x)))
+        y = self.relu(self.norm2(self.conv2(y)))
+        skip = x if self.downsample is None else self.downsample(x)
+        return self.relu(skip + y)
+
+
+def _stage(cin: int, cout: int, norm: str, stride: int) -> nn.Sequential:
+    return nn.Sequential(ResidualBlock(cin, cout, norm, stride), ResidualBlock(cout, cout, norm, 1))
+
+
+class BasicEncoder(nn.Module):
+    """fnet: 7x7 stem + 3 residual stages to 1/4 resolution + 1x1 to 256 ch, instance norm."""
+
+    def __init__(self, output_dim: int = 256, norm_fn: str = "instance", downsample: int = 2):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=1 + (downsample > 2), padding=3)
+        self.norm1 = _norm2d(norm_fn, 64)
+        self.relu1 = nn.ReLU(inplace=True)
+        self.layer1 = _stage(64, 64, norm_fn, 1)
+        self.layer2 = _stage(64, 96, norm_fn, 1 + (downsample > 1))
+        self.layer3 = _stage(96, 128, norm_fn, 1 + (downsample > 0))
+        self.conv2 = nn.Conv2d(128, output_dim, 1)
+
+    def forward(self, x):
+        x = self.relu1(self.norm1(self.conv1(x)))
+        return self.conv2(self.layer3(self.layer2(self.layer1(x))))
+
+
+class MultiBasicEncoder(nn.Module):
+    """cnet: shared trunk, then (hidden, context) heads at 1/4, 1/8, 1/16 (batch norm)."""
+
+    def __init__(self, output_dim=([128] * 3, [128] * 3), norm_fn: str = "batch", downsample: int = 2):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=1 + (downsample > 2), padding=3)
+        self.norm1 = _norm2d(norm_fn, 64)
+        self.relu1 = nn.ReLU(inplace=True)
+        self.layer1 = _stage(64, 64, norm_fn, 1)
+        self.layer2 = _stage(64, 96, norm_fn, 1 + (downsample > 1))
+        self.layer3 = _stage(96, 128, norm_fn, 1 + (downsample > 0))
+        self.layer4 = _stage(128, 128, norm_fn, 2)
+        self.layer5 = _stage(128, 128, norm_fn, 2)
+        self.outputs08 = nn.ModuleList(
+            [nn.Sequential(ResidualBlock(128, 128, norm_fn), nn.Conv2d(128, d[2], 3, padding=1)) for d in output_dim])
+        self.outputs16 = nn.ModuleList(
+            [nn.Sequential(ResidualBlock(128, 128, norm_fn), nn.Conv2d(128, d[1], 3, padding=1)) for d in output_dim])
+        self.outputs32 = nn.ModuleList([nn.Conv2d(128, d[0], 3, padding=1) for d in output_dim])
+
+    def forward(self, x) -> List[List[torch.Tensor]]:
+        x = self.relu1(self.norm1(self.conv1(x)))
+        s08 = self.layer3(self.layer2(self.layer1(x)))
+        s16 = self.layer4(s08)
+        s32 = self.layer5(s16)
+        return [[f(s08) for f in self.outputs08], [f(s16) for f in self.outputs16],
+                [f(s32) for f in self.outputs32]]
+
+
+class BasicConv(nn.Module):
+    """conv (no bias) + InstanceNorm + LeakyReLU(0.01), 2-D or 3-D (submodule.py:25-53)."""
+
+    def __init__(self, cin: int, cout: int, is_3d: bool = False, **conv_kw):
+        super().__init__()
+        self.act_fn = nn.LeakyReLU()
+        self.norm_fn = (nn.InstanceNorm3d if is_3d else nn.InstanceNorm2d)(cout)
+        self.conv = (nn.Conv3d if is_3d else nn.Conv2d)(cin, cout, bias=False, **conv_kw)
+
+    def forward(self, x):
+        return self.act_fn(self.norm_fn(self.conv(x)))
+
+
+class DoubleFeatureAtt(nn.Module):
+    """CoEx-style excitation sigmoid(f_L) * sigmoid(f_R) of a cost volume in the
+    [B, C, W2, H, W1] layout (submodule.py:113-140)."""
+
+    def __init__(self, cv_chan: int, feat_chan: int, kernel_size: int = 3, stride: int = 1, padding: int = 1):
+        super().__init__()
+        mid = max(32, feat_chan // 2)
+
+        def branch():
+            return nn.Sequential(BasicConv(feat_chan, mid, kernel_size=kernel_size, stride=stride, padding=padding),
+                                 nn.Conv2d(mid, cv_chan, 1))
+        self.feat_att_left = branch()
+        self.feat_att_right = branch()
+
+    def forward(self, cv, feat_left, feat_right):
+        gl = self.feat_att_left(feat_left).unsqueeze(2)                     # B C 1 H W1
+        gr = self.feat_att_right(feat_right).permute(0, 1, 3, 2).unsqueeze(4)  # B C W2 H 1
+        g = torch.sigmoid(gl) * torch.sigmoid(gr)
+        if tuple(g.shape[2:]) != tuple(cv.shape[2:]):
+            g = F.interpolate(g, size=cv.shape[2:], mode="trilinear", align_corners=True)
+        return g * cv
+
+
+class HourglassIdentity(nn.Module):
+    def forward(self, x, features_left=None, features_right=None):
+        return x
+
+
+class Hourglass(nn.Module):
+    """3-scale 3-D encoder-decoder over the mono volume (hourglass.py:13-91).
+
+    Works directly on the [B, C, W2, H, W1] layout the reference permutes into
+    (hourglass.py:63) and returns that layout (the caller's classifier convs run on it
+    with permuted kernels).  The reference's first up-path step (agg_layers[0] +
+    feature_atts_up[0]) feeds nothing: hourglass.py:319 re-reads
+    ``downsampled_features`` and overwrites ``x`` — so it is skipped, exactly."""
+
+    def __init__(self, in_channels: int = 8, out_channels: int = 8, feature_channels=(1, 1, 1, 1, 1, 1),
+                 n_downsample: int = 2):
+        super().__init__()
+        fc = list(feature_channels)[n_downsample:]
+        ns = len(fc)
+        c = in_channels
+        self.down_layers = nn.ModuleList()
+        for i in range(ns - 1):
+            ci, co = c * (1 if i == 0 else 2 * i), c * 2 * (i + 1)
+            self.down_layers.append(nn.Sequential(
+                BasicConv(ci, co, True, kernel_size=3, padding=1, stride=2, dilation=1, groups=1),
+                BasicConv(co, co, True, kernel_size=3, padding=1, stride=1, dilation=1, groups=1)))
+        self.agg_layers = nn.ModuleList()
+        for i in range(ns - 2):
+            ci = c * 2 * (ns - i - 1) + c * 2 * (ns - i - 2)
+            co = c * 2 * (ns - i - 2)
+            self.agg_layers.append(nn.Sequential(
+                BasicConv(ci, co, True, kernel_size=1, padding=0, stride=1),
+                BasicConv(co, co, True, kernel_size=3, padding=1, stride=1),
+                BasicConv(co, co, True, kernel_size=3, padding=1, stride=1)))
+        self.final_agg = nn.Sequential(
+            BasicConv(c + co, c, True, kernel_size=1, padding=0, stride=1),
+            BasicConv(c, c, True, kernel_size=3, padding=1, stride=1),
+            BasicConv(c, out_channels, True, kernel_size=3, padding=1, stride=1))
+        self.feature_atts = nn.ModuleList([DoubleFeatureAtt(c * 2 * i, fc[i]) for i in range(1, ns)])
+        self.feature_atts_up = nn.ModuleList([DoubleFeatureAtt(c * 2 * (ns - i - 1), fc[ns - i - 1])
+                                              for i in range(1, ns - 1)])
+        self.final_feature_atts_up = DoubleFeatureAtt(out_channels, fc[0])
+        self.number_of_scales = ns
+
+    def forward(self, x, features_left, features_right):
+        ns = self.number_of_scales
+        orig = x
+        downs = []
+        for i in range(ns - 1):
+            x = self.down_layers[i](x)
+            x = self.feature_atts[i](x, features_left[i + 1], features_right[i + 1])
+            downs.append(x)
+        # only the last up-path step is live (see class docstring)
+        i = ns - 3
+        up = F.interpolate(downs[ns - 2 - i], size=downs[ns - 3 - i].shape[2:], mode="trilinear",
+                           align_corners=True)
+        x = self.agg_layers[i](torch.cat((up, downs[ns - 3 - i]), 1))
+        x = self.feature_atts_up[i](x, features_left[ns - 2 - i], features_right[ns - 2 - i])
+        up = F.interpolate(x, size=orig.shape[2:], mode="trilinear", align_corners=True)
+        x = self.final_agg(torch.cat((orig, up), 1))
+        return self.final_feature_atts_up(x, features_left[0], features_right[0])
+
+
+class ConvGRU(nn.Module):
+    """Parameters of update.py:46-62 (convz/convr/convq over cat(h, x))."""
+
+    def __init__(self, hidden_dim: int, input_dim: int, kernel_size: int = 3):
+        super().__init__()
+        cin = hidden_dim + input_dim
+        self.convz = nn.Conv2d(cin, hidden_dim, kernel_size, padding=kernel_size // 2)
+        self.convr = nn.Conv2d(cin, hidden_dim, kernel_size, padding=kernel_size // 2)
+        self.convq = nn.Conv2d(cin, hidden_dim, kernel_size, padding=kernel_size // 2)
+
+
+class BasicMotionEncoder(nn.Module):
+    """Parameters of update.py:64-90; convc1/convc2 are shared by the stereo and mono lookups."""
+
+    def __init__(self, corr_levels: int = 4, corr_radius: int = 4):
+        super().__init__()
+        planes = corr_levels * (2 * corr_radius + 1)
+        self.convc1 = nn.Conv2d(planes, 64, 1, padding=0)
+        self.convc2 = nn.Conv2d(64, 64, 3, padding=1)
+        self.convf1 = nn.Conv2d(2, 64, 7, padding=3)
+        self.convf2 = nn.Conv2d(64, 64, 3, padding=1)
+        self._conv = nn.Conv2d(64 + 64 + 64, 128 - 2, 3, padding=1)
+
+
+class UpdateHead(nn.Module):
+    def __init__(self, input_dim: int = 128, hidden_dim: int = 256, output_dim: int = 2):
+        super().__init__()
+        self.conv1 = nn.Conv2d(input_dim, hidden_dim, 3, padding=1)
+        self.conv2 = nn.Conv2d(hidden_dim, output_dim, 3, padding=1)
+        self.relu = nn.ReLU(inplace=True)
+
+
+class BasicMultiUpdateBlock(nn.Module):
+    """Parameters of update.py:134-162 (predict_confidence=False, 3 GRU levels)."""
+
+    def __init__(self, corr_levels=4, corr_radius=4, encoder_output_dim=128, hidden_dims=(128, 128, 128),
+                 n_downsample=2):
+        super().__init__()
+        self.encoder = BasicMotionEncoder(corr_levels, corr_radius)
+        self.gru08 = ConvGRU(hidden_dims[2], encoder_output_dim + hidden_dims[1])
+        self.gru16 = ConvGRU(hidden_dims[1], hidden_dims[0] + hidden_dims[2])
+        self.gru32 = ConvGRU(hidden_dims[0], hidden_dims[1])
+        self.flow_head = UpdateHead(hidden_dims[2], 256, 2)
+        f = 2 ** n_downsample
+        self.mask = nn.Sequential(nn.Conv2d(hidden_dims[2], 256, 3, padding=1), nn.ReLU(inplace=True),
+                                  nn.Conv2d(256, f * f * 9, 1, padding=0))

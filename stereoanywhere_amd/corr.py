@@ -1,0 +1,87 @@
+"""HIP implementation of the reference's correlation plug-in point.
+
+Reference contract (models/stereoanywhere/corr.py):
+  * ``CorrBlock1D.corr(fmap2 [B,C,H,W1], fmap3 [B,C,H,W2]) -> [B,H,W1,1,W2]`` (117-132)
+  * ``CorrBlock1D(fullcorr, num_levels=4, radius=4, pad=[0,0])`` builds the pyramid (76-91)
+  * ``block(coords [B,2,H,W]) -> [B, num_levels*(2r+1), H, W - pad0 - pad1]`` (93-115)
+selected by ``args.corr_implementation`` (stereoanywhere.py:25, 128-133).
+
+``HipCorrBlock1D`` keeps that contract; the pyramid lives in one buffer with the levels
+of a pixel row back to back (include/stereoanywhere_hip.h) and ``corr_pyramid`` exposes
+per-level views shaped like the reference's.  ``HipCorrBlock1D.from_features`` is the
+fused entry (volume + truncation + pyramid in one kernel) the model uses.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from . import ops
+
+
+class HipCorrBlock1D:
+    def __init__(self, fullcorr: Optional[torch.Tensor], num_levels: int = 4, radius: int = 4,
+                 pad: Sequence[int] = (0, 0), _pyramid: Optional[torch.Tensor] = None,
+                 _shape: Optional[tuple] = None):
+        self.num_levels = num_levels
+        self.radius = radius
+        self.pad = list(pad)
+        if _pyramid is None:
+            if fullcorr.dim() != 5 or fullcorr.shape[3] != 1:
+                raise RuntimeError(f"fullcorr must be [B,H,W1,1,W2], got {tuple(fullcorr.shape)}")
+            B, H, W1, _, W2 = fullcorr.shape
+            _pyramid = ops.pyramid_from_volume(fullcorr.reshape(B * H * W1, W2), num_levels)
+            _shape = (B, H, W1, W2)
+        self.shape = _shape
+        self.pyramid = _pyramid
+        B, H, W1, W2 = _shape
+        _, offs, wids = ops.pyramid_geometry(W2, num_levels)
+        # [B*H*W1, 1, 1, W_l] views, the reference's per-level shape (corr.py:85-91)
+        self.corr_pyramid = [_pyramid[:, o:o + w].unsqueeze(1).unsqueeze(1) for o, w in zip(offs, wids)]
+
+    @classmethod
+    def from_features(cls, fmap2: torch.Tensor, fmap3: torch.Tensor, num_levels: int = 4, radius: int = 4,
+                      trunc_disp: Optional[torch.Tensor] = None, trunc_conf: Optional[torch.Tensor] = None,
+                      attenuation: float = 0.9, pad: Sequence[int] = (0, 0)) -> "HipCorrBlock1D":
+        """corr -> x truncation volume -> pyramid fused (stereoanywhere.py:135, 201-205, 253-255)."""
+        B, _, H, W1 = fmap2.shape
+        W2 = fmap3.shape[3]
+        pyr = ops.corr_volume_pyramid(fmap2, fmap3, num_levels, trunc_disp, trunc_conf, attenuation)
+        return cls(None, num_levels, radius, pad, _pyramid=pyr, _shape=(B, H, W1, W2))
+
+    def lookup_into(self, coords_x: torch.Tensor, out: torch.Tensor, other: Optional["HipCorrBlock1D"] = None):
+        """Look up this pyramid (and ``other``'s, same geometry) at coords_x [B,1,H,W1] into
+        out [B, nvol*L*(2r+1), H, W1] — one launch for both volumes."""
+        ops.corr_lookup(self.pyramid, None if other is None else other.pyramid, self.shape[3], self.num_levels,
+                        self.radius, coords_x, out)
+        return out
+
+    def __call__(self, coords: torch.Tensor) -> torch.Tensor:
+        x = coords[:, :1]
+        if self.pad[0]:
+            x = x + self.pad[0]
+        if not x.is_contiguous() and x.stride(3) != 1:
+            x = x.contiguous()
+        out = ops.corr_lookup(self.pyramid, None, self.shape[3], self.num_levels, self.radius, x)
+        W1 = out.shape[-1]
+        if self.pad[0] or self.pad[1]:
+            out = out[..., self.pad[0]:W1 - self.pad[1]].contiguous()
+        return out
+
+    @staticmethod
+    def corr(fmap2: torch.Tensor, fmap3: torch.Tensor) -> torch.Tensor:
+        return ops.corr_volume(fmap2.float().contiguous(), fmap3.float().contiguous())
+
+
+# args.corr_implementation -> block class.  The reference's "reg" (torch) and "reg_cuda"
+# (unvendored RAFT sampler, broken at corr.py:56) both resolve to the HIP block: this
+# package IS the replacement of that plug-in point, and it has no CPU fallback.
+CORR_IMPLEMENTATIONS = {"hip": HipCorrBlock1D, "reg": HipCorrBlock1D, "reg_cuda": HipCorrBlock1D}
+
+
+def get_corr_block(name: str):
+    try:
+        return CORR_IMPLEMENTATIONS[name]
+    except KeyError:
+        raise NotImplementedError(f"corr_implementation={name!r}") from None

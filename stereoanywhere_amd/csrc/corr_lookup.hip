@@ -1,0 +1,93 @@
+// K4 — correlation-pyramid lookup (CorrBlock1D.__call__, corr.py:93-115, through
+// bilinear_sampler, utils.py:19-35).
+//
+// One thread per (volume, pixel): for each level l it reads the (2r+2) pyramid cells
+// around x = coords_x / 2^l out of its own pixel row and writes the (2r+1) linearly
+// interpolated taps; consecutive threads are consecutive pixels j, so every output
+// plane store is coalesced.  Stereo and mono pyramids share one launch (blockIdx.y).
+//
+// Arithmetic mirrors the reference's grid_sample round trip in fp32:
+//   xg = 2 (t + x/2^l) / (W_l - 1) - 1       (utils.py:25, corr.py:104)
+//   ix = (xg + 1) * ((W_l - 1) / 2)          (ATen CPU grid_sample, align_corners=True)
+//   out = v[floor] * (1 - w) + v[floor + 1] * w, zero outside [0, W_l - 1].
+#include "sa_common.h"
+
+namespace {
+
+struct LGeo {
+  int H, W1, L, r;
+  long rs, cbs, obs;
+  int off[4], wid[4];
+};
+
+__global__ __launch_bounds__(256) void lookup_kernel(const float *__restrict__ pa,
+                                                     const float *__restrict__ pb,
+                                                     const float *__restrict__ cx, LGeo g,
+                                                     long npix, float *__restrict__ out) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+  const int v = blockIdx.y;
+  const float *__restrict__ pyr = v ? pb : pa;
+  const long hw = (long)g.H * g.W1;
+  const long b = p / hw, rem = p % hw;
+  const float x = cx[b * g.cbs + rem];
+  const float *__restrict__ row = pyr + p * g.rs;
+  const int K = 2 * g.r + 1;
+  float *__restrict__ o = out + b * g.obs + (long)v * g.L * K * hw + rem;
+  for (int l = 0; l < g.L; ++l) {
+    const int Wl = g.wid[l];
+    const float *__restrict__ lv = row + g.off[l];
+    const float xl = x / (float)(1 << l);
+    const float denom = (float)(Wl - 1);
+    const float sf = (float)(Wl - 1) / 2.0f;
+    for (int t = -g.r; t <= g.r; ++t) {
+      const float x0 = (float)t + xl;
+      const float xg = 2.0f * x0 / denom - 1.0f;
+      const float ix = (xg + 1.0f) * sf;
+      float xw = floorf(ix);
+      const float w = ix - xw;
+      const float e = 1.0f - w;
+      xw = fminf(fmaxf(xw, -2.0f), (float)Wl + 1.0f);  // keep the int conversion defined
+      const int xi = (int)xw;
+      const float v0 = (xi >= 0 && xi <= Wl - 1) ? lv[xi] : 0.0f;
+      const float v1 = (xi + 1 >= 0 && xi + 1 <= Wl - 1) ? lv[xi + 1] : 0.0f;
+      o[(long)(l * K + t + g.r) * hw] = v0 * e + v1 * w;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int sa_corr_lookup(const float *pyramid_a, const float *pyramid_b, int W2, long row_stride,
+                              int num_levels, int radius, const float *coords_x, long coords_bstride,
+                              int B, int H, int W1, float *out, long out_bstride, void *stream) {
+  SA_REQUIRE(pyramid_a && coords_x && out, "sa_corr_lookup: null pointer");
+  SA_REQUIRE(B > 0 && H > 0 && W1 > 0 && W2 > 0, "sa_corr_lookup: empty shape");
+  SA_REQUIRE(num_levels >= 1 && num_levels <= 4, "sa_corr_lookup: num_levels must be 1..4");
+  SA_REQUIRE(radius >= 0 && radius <= 16, "sa_corr_lookup: radius must be 0..16");
+  SA_REQUIRE(sa_pyramid_level_width(W2, num_levels - 1) >= 2,
+             "sa_corr_lookup: level %d of width %d is too narrow to sample", num_levels - 1,
+             sa_pyramid_level_width(W2, num_levels - 1));
+  SA_REQUIRE(row_stride >= sa_pyramid_level_offset(W2, num_levels), "sa_corr_lookup: row_stride too small");
+  const int nvol = pyramid_b ? 2 : 1;
+  SA_REQUIRE(out_bstride >= (long)nvol * num_levels * (2 * radius + 1) * H * W1,
+             "sa_corr_lookup: out batch stride too small");
+  LGeo g{};
+  g.H = H;
+  g.W1 = W1;
+  g.L = num_levels;
+  g.r = radius;
+  g.rs = row_stride;
+  g.cbs = coords_bstride;
+  g.obs = out_bstride;
+  for (int i = 0; i < 4; ++i) {
+    g.off[i] = sa_pyramid_level_offset(W2, i);
+    g.wid[i] = sa_pyramid_level_width(W2, i);
+  }
+  const long npix = (long)B * H * W1;
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_LOOKUP, s);
+  dim3 grid((unsigned)((npix + 255) / 256), nvol);
+  lookup_kernel<<<grid, 256, 0, s>>>(pyramid_a, pyramid_b ? pyramid_b : pyramid_a, coords_x, g, npix, out);
+  return sa::check_launch("sa_corr_lookup");
+}

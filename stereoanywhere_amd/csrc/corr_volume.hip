@@ -1,0 +1,272 @@
+// K1 — all-pairs 1-D correlation volume on fp32 MFMA, fused with the truncation
+// volume and the 1-D average-pool pyramid.
+//
+// Reference: CorrBlock1D.corr (corr.py:117-132) = einsum('aijk,aijh->ajkh')/sqrt(C);
+// truncate_corr_volume_v2 (utils.py:216-238) applied at stereoanywhere.py:253-254;
+// CorrBlock1D.__init__ (corr.py:76-91) pyramid of avg_pool2d([1,2]).
+//
+// For every image row (b,h) the volume is a W1 x W2 GEMM with K = C (256):
+// A[j][c] = fmap2[b,c,h,j] and B[c][k] = fmap3[b,c,h,k] are both contiguous along
+// j / k in NCHW, i.e. exactly the k-major operand layout v_mfma_f32_32x32x2_f32 reads
+// (A lane l: A[l&31][l>>5], B lane l: B[l>>5][l&31]).  A block computes a 64(j) x 128(k)
+// tile with 4 waves (each 32 x 64 = two 32x32 accumulators), staging 32-channel slices
+// of both panels through LDS with one register-prefetched stage in flight.
+// f32-input MFMA is exact f32 (a k-ordered fmaf chain), so the sum differs from the
+// CPU einsum only by accumulation order.
+//
+// Epilogue: divide by sqrt(C), multiply by the analytic truncation factor
+// T = (1-m) + m (sigmoid((j-d)-k)(1-a) + a) (two per-pixel scalars, zero extra HBM
+// bytes), then write level 0 and build levels 1..3 with lane shuffles: the accumulator
+// column is the lane (col = lane&31), so pairs (k, k+1) sit in lanes (l, l^1).
+#include "sa_common.h"
+
+namespace {
+
+constexpr int TJ = 64;    // tile rows (left pixels j)
+constexpr int TK = 128;   // tile cols (right pixels k)
+constexpr int KC = 32;    // channels per LDS stage
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct Geo {
+  int C, H, W1, W2, tilesJ, tilesK, nlev;
+  long rs;
+  int off[4], wid[4];
+};
+
+template <bool VEC, bool TRUNC>
+__global__ __launch_bounds__(256) void corr_pyramid_kernel(
+    const float *__restrict__ f2, const float *__restrict__ f3, Geo g, float sqrt_c,
+    const float *__restrict__ tdisp, const float *__restrict__ tconf, float atten,
+    float *__restrict__ pyr) {
+  __shared__ float As[KC][TJ];
+  __shared__ float Bs[KC][TK];
+
+  const unsigned nwg = gridDim.x;
+  const unsigned wid = sa::xcd_remap(blockIdx.x, nwg);
+  const int tiles = g.tilesJ * g.tilesK;
+  const int bh = wid / tiles, tile = wid % tiles;
+  const int j0 = (tile / g.tilesK) * TJ, k0 = (tile % g.tilesK) * TK;
+  const int b = bh / g.H, h = bh % g.H;
+  const long cstride = (long)g.H * g.W1;  // fmap2 channel stride
+  const long cstride3 = (long)g.H * g.W2;
+  const long base2 = (long)b * g.C * cstride + (long)h * g.W1;
+  const long base3 = (long)b * g.C * cstride3 + (long)h * g.W2;
+
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wj = w & 1, wk = w >> 1;
+
+  f32x16 acc0 = {0.f}, acc1 = {0.f};
+  float4 ra[2], rb[4];
+
+  auto load = [&](int c0) {
+    // A panel
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = t + 256 * i;
+      const int c = q >> 4, j = j0 + ((q & 15) << 2);
+      const bool okc = (c0 + c) < g.C;
+      const float *p = f2 + base2 + (long)(c0 + c) * cstride + j;
+      if (VEC && okc && j + 3 < g.W1) {
+        ra[i] = *reinterpret_cast<const float4 *>(p);
+      } else {
+        ra[i].x = (okc && j + 0 < g.W1) ? p[0] : 0.f;
+        ra[i].y = (okc && j + 1 < g.W1) ? p[1] : 0.f;
+        ra[i].z = (okc && j + 2 < g.W1) ? p[2] : 0.f;
+        ra[i].w = (okc && j + 3 < g.W1) ? p[3] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = t + 256 * i;
+      const int c = q >> 5, k = k0 + ((q & 31) << 2);
+      const bool okc = (c0 + c) < g.C;
+      const float *p = f3 + base3 + (long)(c0 + c) * cstride3 + k;
+      if (VEC && okc && k + 3 < g.W2) {
+        rb[i] = *reinterpret_cast<const float4 *>(p);
+      } else {
+        rb[i].x = (okc && k + 0 < g.W2) ? p[0] : 0.f;
+        rb[i].y = (okc && k + 1 < g.W2) ? p[1] : 0.f;
+        rb[i].z = (okc && k + 2 < g.W2) ? p[2] : 0.f;
+        rb[i].w = (okc && k + 3 < g.W2) ? p[3] : 0.f;
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = t + 256 * i;
+      *reinterpret_cast<float4 *>(&As[q >> 4][(q & 15) << 2]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = t + 256 * i;
+      *reinterpret_cast<float4 *>(&Bs[q >> 5][(q & 31) << 2]) = rb[i];
+    }
+  };
+
+  load(0);
+  for (int c0 = 0; c0 < g.C; c0 += KC) {
+    __syncthreads();  // previous stage fully consumed
+    store();
+    __syncthreads();
+    if (c0 + KC < g.C) load(c0 + KC);  // prefetch next stage under the MFMAs
+    const int arow = lane >> 5, col = lane & 31;
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 2) {
+      const float a = As[kk + arow][wj * 32 + col];
+      const float b0 = Bs[kk + arow][wk * 64 + col];
+      const float b1 = Bs[kk + arow][wk * 64 + 32 + col];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc1, 0, 0, 0);
+    }
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  const int col = lane & 31, hi = lane >> 5;
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * hi;
+      const int j = j0 + wj * 32 + row;
+      const int k = k0 + wk * 64 + n * 32 + col;
+      float v = (n == 0 ? acc0[r] : acc1[r]) / sqrt_c;
+      const bool jok = j < g.W1;
+      if (TRUNC) {
+        float d = 0.f, m = 0.f;
+        if (jok) {
+          const long pix = ((long)b * g.H + h) * g.W1 + j;
+          d = tdisp[pix];
+          m = tconf[pix];
+        }
+        const float center = (float)j - d;
+        const float tv = center - (float)k;
+        const float s = sa::sigmoidf_ref(tv);
+        const float T = 1.0f * (1.0f - m) + m * (s * (1.0f - atten) + atten);
+        v = T * v;
+      }
+      float *row_ptr = pyr + (((long)b * g.H + h) * g.W1 + j) * g.rs;
+      if (jok && k < g.W2) row_ptr[k] = v;
+      if (g.nlev > 1) {
+        // level 1: (v[k] + v[k+1]) / 2 held by the even lane
+        const float v1 = (v + __shfl_xor(v, 1)) * 0.5f;
+        const int k1 = k >> 1;
+        if (jok && (col & 1) == 0 && k1 < g.wid[1]) row_ptr[g.off[1] + k1] = v1;
+        if (g.nlev > 2) {
+          const float v2 = (v1 + __shfl_xor(v1, 2)) * 0.5f;
+          const int k2 = k >> 2;
+          if (jok && (col & 3) == 0 && k2 < g.wid[2]) row_ptr[g.off[2] + k2] = v2;
+          if (g.nlev > 3) {
+            const float v3 = (v2 + __shfl_xor(v2, 4)) * 0.5f;
+            const int k3 = k >> 3;
+            if (jok && (col & 7) == 0 && k3 < g.wid[3]) row_ptr[g.off[3] + k3] = v3;
+          }
+        }
+      }
+    }
+  }
+}
+
+// Pyramid from an existing volume (mono path, stereoanywhere.py:257-259): one wave per
+// row; each lane takes 8 consecutive level-0 values and emits the 4+2+1 coarser cells.
+__global__ __launch_bounds__(256) void pyramid_from_volume_kernel(const float *__restrict__ vol,
+                                                                  long rows, int W2, long in_rs,
+                                                                  Geo g, float *__restrict__ pyr) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const float *src = vol + row * in_rs;
+  float *dst = pyr + row * g.rs;
+  // 8 consecutive level-0 values per lane-iteration -> one level-3 value
+  for (int base = lane * 8; base < W2; base += 64 * 8) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (base + i < W2) ? src[base + i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (base + i < W2) dst[base + i] = v[i];
+    float l1[4], l2[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      l1[i] = (v[2 * i] + v[2 * i + 1]) * 0.5f;
+      const int k1 = base / 2 + i;
+      if (g.nlev > 1 && k1 < g.wid[1]) dst[g.off[1] + k1] = l1[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      l2[i] = (l1[2 * i] + l1[2 * i + 1]) * 0.5f;
+      const int k2 = base / 4 + i;
+      if (g.nlev > 2 && k2 < g.wid[2]) dst[g.off[2] + k2] = l2[i];
+    }
+    const float l3 = (l2[0] + l2[1]) * 0.5f;
+    const int k3 = base / 8;
+    if (g.nlev > 3 && k3 < g.wid[3]) dst[g.off[3] + k3] = l3;
+  }
+}
+
+Geo make_geo(int C, int H, int W1, int W2, int nlev, long rs) {
+  Geo g{};
+  g.C = C;
+  g.H = H;
+  g.W1 = W1;
+  g.W2 = W2;
+  g.tilesJ = (W1 + TJ - 1) / TJ;
+  g.tilesK = (W2 + TK - 1) / TK;
+  g.nlev = nlev;
+  g.rs = rs;
+  for (int i = 0; i < 4; ++i) {
+    g.off[i] = sa_pyramid_level_offset(W2, i);
+    g.wid[i] = sa_pyramid_level_width(W2, i);
+  }
+  return g;
+}
+
+}  // namespace
+
+extern "C" int sa_corr_volume_pyramid(const float *fmap2, const float *fmap3, int B, int C, int H,
+                                      int W1, int W2, float sqrt_c, const float *trunc_disp,
+                                      const float *trunc_conf, float atten, int num_levels,
+                                      float *pyramid, long row_stride, void *stream) {
+  SA_REQUIRE(fmap2 && fmap3 && pyramid, "sa_corr_volume_pyramid: null pointer");
+  SA_REQUIRE(B > 0 && C > 0 && H > 0 && W1 > 0 && W2 > 0, "sa_corr_volume_pyramid: empty shape");
+  SA_REQUIRE(num_levels >= 1 && num_levels <= 4, "sa_corr_volume_pyramid: num_levels must be 1..4");
+  SA_REQUIRE(row_stride >= sa_pyramid_level_offset(W2, num_levels),
+             "sa_corr_volume_pyramid: row_stride %ld too small", row_stride);
+  SA_REQUIRE((trunc_disp == nullptr) == (trunc_conf == nullptr),
+             "sa_corr_volume_pyramid: trunc_disp and trunc_conf go together");
+  SA_REQUIRE((long)B * H * ((W1 + TJ - 1) / TJ) * ((W2 + TK - 1) / TK) < (1L << 31),
+             "sa_corr_volume_pyramid: grid too large");
+  Geo g = make_geo(C, H, W1, W2, num_levels, row_stride);
+  const bool vec = (W1 % 4 == 0) && (W2 % 4 == 0) &&
+                   (reinterpret_cast<uintptr_t>(fmap2) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(fmap3) % 16 == 0);
+  hipStream_t s = sa::as_stream(stream);
+  const unsigned nblk = (unsigned)((long)B * H * g.tilesJ * g.tilesK);
+  sa::TimingScope ts(SA_K_CORR_PYRAMID, s);
+  const bool tr = trunc_disp != nullptr;
+  if (vec && tr)
+    corr_pyramid_kernel<true, true><<<nblk, 256, 0, s>>>(fmap2, fmap3, g, sqrt_c, trunc_disp, trunc_conf, atten, pyramid);
+  else if (vec)
+    corr_pyramid_kernel<true, false><<<nblk, 256, 0, s>>>(fmap2, fmap3, g, sqrt_c, nullptr, nullptr, atten, pyramid);
+  else if (tr)
+    corr_pyramid_kernel<false, true><<<nblk, 256, 0, s>>>(fmap2, fmap3, g, sqrt_c, trunc_disp, trunc_conf, atten, pyramid);
+  else
+    corr_pyramid_kernel<false, false><<<nblk, 256, 0, s>>>(fmap2, fmap3, g, sqrt_c, nullptr, nullptr, atten, pyramid);
+  return sa::check_launch("sa_corr_volume_pyramid");
+}
+
+extern "C" int sa_corr_pyramid_from_volume(const float *volume, long rows, int W2, long in_row_stride,
+                                           int num_levels, float *pyramid, long row_stride,
+                                           void *stream) {
+  SA_REQUIRE(volume && pyramid, "sa_corr_pyramid_from_volume: null pointer");
+  SA_REQUIRE(rows > 0 && W2 > 0 && in_row_stride >= W2, "sa_corr_pyramid_from_volume: bad shape");
+  SA_REQUIRE(num_levels >= 1 && num_levels <= 4, "sa_corr_pyramid_from_volume: num_levels must be 1..4");
+  SA_REQUIRE(row_stride >= sa_pyramid_level_offset(W2, num_levels),
+             "sa_corr_pyramid_from_volume: row_stride too small");
+  Geo g = make_geo(1, 1, 1, W2, num_levels, row_stride);
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_MISC, s);
+  pyramid_from_volume_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(volume, rows, W2, in_row_stride, g, pyramid);
+  return sa::check_launch("sa_corr_pyramid_from_volume");
+}

@@ -1,0 +1,252 @@
+"""StereoAnywhere on MI355X: the reference model API with the cost-volume hot path on
+hand-written HIP kernels (libsa_hip.so) and the dense convolutions on MIOpen fp32.
+
+Drop-in for models/stereoanywhere/stereoanywhere.py:
+  * ``StereoAnywhere(args)`` — args is a Namespace or dict; defaults read like the
+    reference (stereoanywhere.py:21-50);
+  * ``forward(image2, image3, mde2, mde3, iters=12, test_mode=False)`` (95);
+    ``test_mode=True`` returns ``(flow_up [B,1,H,W] = -disparity, None)`` (296-297);
+  * identical parameter names (state dicts of the reference load with strict=True).
+
+Hot path, one kernel family per row:
+  a2+a3  normals + masked mono volume, written in the hourglass layout   sa_mono_*
+  a5+a6  soft-argmin and entropy confidence of the aggregated volumes    sa_softargmin_conf
+  a7     softLRC, weighted LSQ (exact quantile band, no host sync)       sa_softlrc, sa_weighted_lsq
+  a8+a11 scaled mono, mirror detector, initial coordinates               sa_mono_scale_mirror
+  a1+a8+a9 stereo volume x truncation -> pyramid, one fp32-MFMA kernel  sa_corr_volume_pyramid
+  a10    stereo + mono pyramid lookups, one launch per iteration         sa_corr_lookup
+  a12    GRU gates fused; convs split by input so no torch.cat          sa_gru_zr / sa_gru_out
+  a14    convex upsampling of the final flow                            sa_convex_upsample
+Training (test_mode=False), vol_downsample > 0 and use_aggregate_stereo_vol are outside
+this tier and raise NotImplementedError.
+"""
+from __future__ import annotations
+
+import math
+from types import SimpleNamespace
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from .blocks import BasicEncoder, BasicMultiUpdateBlock, Hourglass, HourglassIdentity, MultiBasicEncoder
+from .corr import HipCorrBlock1D, get_corr_block
+
+_DEFAULTS = dict(
+    corr_implementation="hip", n_downsample=2, corr_radius=4, corr_levels=4, n_gru_layers=3,
+    encoder_output_dim=128, context_dims=[128] * 3, n_additional_hourglass=0, volume_channels=8, vol_n_masks=8,
+    vol_aug_n_masks=4, vol_downsample=0, use_truncate_vol=True, mirror_conf_th=0.98, mirror_attenuation=0.9,
+    lrc_th=1, moving_average_decay=0.67, volume_corruption_prob=0.33, normal_gain=10, init_disparity_zero=False,
+    use_aggregate_stereo_vol=False, use_aggregate_mono_vol=True, things_to_freeze=["fnet"],
+)
+
+
+def _normalize_pair(a: torch.Tensor, b: torch.Tensor, eps: float = 1e-4):
+    """utils.py:56-71 for the C == 1 input path: joint per-(b,c) min/max of the pair."""
+    mn = torch.minimum(a.amin(dim=(2, 3), keepdim=True), b.amin(dim=(2, 3), keepdim=True))
+    mx = torch.maximum(a.amax(dim=(2, 3), keepdim=True), b.amax(dim=(2, 3), keepdim=True))
+    return (a - mn) / (mx - mn + eps), (b - mn) / (mx - mn + eps)
+
+
+class StereoAnywhere(nn.Module):
+    def __init__(self, args):
+        super().__init__()
+        if isinstance(args, dict):
+            args = SimpleNamespace(**args)
+        for k, v in _DEFAULTS.items():
+            if not hasattr(args, k):
+                setattr(args, k, v)
+        self.args = args
+        a = args
+        self.cnet = MultiBasicEncoder(output_dim=[a.context_dims, a.context_dims], norm_fn="batch",
+                                      downsample=a.n_downsample)
+        self.context_zqr_convs = nn.ModuleList(
+            [nn.Conv2d(a.context_dims[i], a.context_dims[i] * 3, 3, padding=1) for i in range(a.n_gru_layers)])
+        self.fnet = BasicEncoder(output_dim=256, norm_fn="instance", downsample=a.n_downsample)
+        self.feature_channels = [1, 1, 1, 1, 1, 1]
+        self.hourglass_mono = Hourglass(a.vol_n_masks, a.volume_channels, self.feature_channels)
+        self.hourglass_mono_stack = nn.ModuleList([HourglassIdentity()] + [
+            Hourglass(a.volume_channels, a.volume_channels, self.feature_channels)
+            for _ in range(a.n_additional_hourglass)])
+        self.classifier_mono = nn.Conv3d(a.volume_channels, 1, 3, 1, 1, bias=False)
+        self.classifier_monoconf = nn.Conv3d(a.volume_channels, 1, 3, 1, 1, bias=False)
+        self.update_block = BasicMultiUpdateBlock(a.corr_levels, a.corr_radius, a.encoder_output_dim,
+                                                  a.context_dims, a.n_downsample)
+        self._derived = None
+        self._derived_key = None
+
+    # ------------------------------------------------------------------ weights
+    def _split_gru(self, gru, hidden: int):
+        wz, wr, wq = gru.convz.weight, gru.convr.weight, gru.convq.weight
+        return dict(
+            wx=torch.cat([wz[:, hidden:], wr[:, hidden:], wq[:, hidden:]], 0).contiguous(),
+            bx=torch.cat([gru.convz.bias, gru.convr.bias, gru.convq.bias], 0).contiguous(),
+            whzr=torch.cat([wz[:, :hidden], wr[:, :hidden]], 0).contiguous(),
+            wqh=wq[:, :hidden].contiguous(),
+        )
+
+    def _weights(self):
+        """Derived tensors (split GRU kernels, permuted classifier kernels), rebuilt when
+        any parameter is modified or moved."""
+        key = tuple((p.data_ptr(), p._version) for p in self.parameters())
+        if self._derived_key != key:
+            ub = self.update_block
+            hd = self.args.context_dims
+            with torch.no_grad():
+                self._derived = dict(
+                    g08=self._split_gru(ub.gru08, hd[2]), g16=self._split_gru(ub.gru16, hd[1]),
+                    g32=self._split_gru(ub.gru32, hd[0]),
+                    # reference conv over (H, W1, W2) == conv over (W2, H, W1) with permuted kernel
+                    cls_d=self.classifier_mono.weight.permute(0, 1, 4, 2, 3).contiguous(),
+                    cls_c=self.classifier_monoconf.weight.permute(0, 1, 4, 2, 3).contiguous(),
+                )
+            self._derived_key = key
+        return self._derived
+
+    def freeze_bn(self):
+        for m in self.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.eval()
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, image2, image3, mde2, mde3, iters: int = 12, test_mode: bool = False):
+        a = self.args
+        if not test_mode:
+            raise NotImplementedError("training forward (test_mode=False) is outside the inference tier")
+        if a.vol_downsample > 0 or a.use_aggregate_stereo_vol or a.n_gru_layers != 3 or a.n_downsample != 2:
+            raise NotImplementedError("only the published configuration (vol_downsample=0, no stereo "
+                                      "aggregation, 3 GRU levels, n_downsample=2) is built")
+        get_corr_block(a.corr_implementation)
+        if image2.device.type != "cuda":
+            raise RuntimeError("StereoAnywhere (MI355X build) runs on the GPU only; move inputs to cuda")
+        with torch.no_grad():
+            return self._forward(image2, image3, mde2, mde3, iters)
+
+    def _forward(self, image2, image3, mde2, mde3, iters):
+        a = self.args
+        dw = self._weights()
+        B, C, H, W = image2.shape
+        if H % 32 or W % 32:
+            raise RuntimeError(f"H and W must be multiples of 32 (callers pad, test.py:206-213); got {H}x{W}")
+        H4, W4 = H // 4, W // 4
+        dev = image2.device
+        f32 = torch.float32
+        image2, image3 = image2.float(), image3.float()
+        if C == 1:
+            image2, image3 = _normalize_pair(image2.repeat(1, 3, 1, 1), image3.repeat(1, 3, 1, 1))
+        image2 = (image2 * 2 - 1).contiguous()
+        image3 = (image3 * 2 - 1).contiguous()
+        mde2 = mde2.float().contiguous()
+        mde3 = mde3.float().contiguous()
+
+        # ---- mono maps at 1/4 (stereoanywhere.py:109-114): both views in one [B,2,H4,W4] buffer
+        mde_lr = torch.empty((B, 2, H4, W4), device=dev, dtype=f32)
+        ops.interp(mde2, mde_lr[:, 0:1])
+        ops.interp(mde3, mde_lr[:, 1:2])
+        m2l = mde_lr[:, 0:1].contiguous()
+        m3l = mde_lr[:, 1:2].contiguous()
+        gain = W4 / a.normal_gain
+        n2 = ops.mono_normals(m2l, gain)
+        n3 = ops.mono_normals(m3l, gain)
+
+        # ---- context + feature encoders (kept on MIOpen fp32)
+        cl = self.cnet(mde2.repeat(1, 3, 1, 1))
+        hid = [torch.tanh(x[0]).contiguous() for x in cl]
+        ctx = [conv(torch.relu(x[1])) for x, conv in zip(cl, self.context_zqr_convs)]  # [B,384,..]
+        fm = self.fnet(torch.cat([image2, image3], 0))
+        fmap2, fmap3 = fm[:B].contiguous(), fm[B:].contiguous()
+        feats_l = [F.interpolate(mde2, scale_factor=1 / 2 ** i, mode="bilinear", align_corners=True)
+                   for i in range(a.n_downsample, len(self.feature_channels))]
+        feats_r = [F.interpolate(mde3, scale_factor=1 / 2 ** i, mode="bilinear", align_corners=True)
+                   for i in range(a.n_downsample, len(self.feature_channels))]
+
+        # ---- mono cost volume -> 3-D hourglass -> classifiers (native [B,C,W2,H,W1] layout)
+        masked = ops.mono_masked_volume(n2, n3, m2l, m3l, a.vol_n_masks, 1.73)
+        agg = self.hourglass_mono(masked, feats_l, feats_r)
+        for i in range(a.n_additional_hourglass):  # stack[0] is the identity (stereoanywhere.py:163-164)
+            hg = self.hourglass_mono_stack[i]
+            agg = agg if isinstance(hg, HourglassIdentity) else hg(agg, feats_l, feats_r)
+        vol_d = F.conv3d(agg, dw["cls_d"], padding=1)  # [B,1,W2,H,W1]
+        vol_c = F.conv3d(agg, dw["cls_c"], padding=1)
+        del masked, agg
+        strides = (W4 * H4 * W4, W4, 1, H4 * W4)  # (b, h, j, k) -> native layout
+        disp_lr, conf_lr = ops.softargmin_conf(vol_d, vol_c, strides, (B, H4, W4, W4))
+
+        # ---- scale/shift alignment, mirror detector, truncation inputs
+        confx = ops.softlrc_joint(disp_lr, conf_lr, float(a.lrc_th))          # fuzzy_and(conf, softlrc)
+        scale, shift = ops.weighted_lsq(mde_lr, disp_lr, confx)
+        sm2, sm3, mirror, coords_x = ops.mono_scale_mirror(mde_lr, scale, shift, disp_lr, confx,
+                                                           float(a.lrc_th), float(a.mirror_conf_th))
+        if a.init_disparity_zero:
+            coords_x = torch.arange(W4, device=dev, dtype=f32).expand(B, 1, H4, W4).contiguous()
+
+        # ---- pyramids
+        trunc = (sm2, mirror) if a.use_truncate_vol else (None, None)
+        stereo_blk = HipCorrBlock1D.from_features(fmap2, fmap3, a.corr_levels, a.corr_radius, trunc[0], trunc[1],
+                                                  float(a.mirror_attenuation))
+        del fmap2, fmap3
+        if a.use_aggregate_mono_vol:
+            mono_rows = vol_d.permute(0, 1, 3, 4, 2).contiguous()  # [B,1,H,W1,W2]
+        else:
+            raise NotImplementedError("use_aggregate_mono_vol=False is not built in this tier")
+        mono_blk = HipCorrBlock1D(None, a.corr_levels, a.corr_radius,
+                                  _pyramid=ops.pyramid_from_volume(mono_rows, a.corr_levels),
+                                  _shape=(B, H4, W4, W4))
+        del mono_rows, vol_d, vol_c
+
+        return self._iterate(dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4)
+
+    def _iterate(self, dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4):
+        ub = self.update_block
+        enc = ub.encoder
+        dev = coords_x.device
+        f32 = torch.float32
+        h08, h16, h32 = hid
+        H8, W8 = h16.shape[2:]
+        H16, W16 = h32.shape[2:]
+        K = enc.convc1.in_channels
+        corr_buf = torch.empty((B, 2 * K, H4, W4), device=dev, dtype=f32)   # [stereo | mono] lookups
+        flow = torch.empty((B, 2, H4, W4), device=dev, dtype=f32)
+        x08 = torch.empty((B, 256, H4, W4), device=dev, dtype=f32)   # [motion(126) | flow(2) | interp(h16)]
+        x16 = torch.empty((B, 256, H8, W8), device=dev, dtype=f32)   # [pool(h08) | interp(h32)]
+        x32 = torch.empty((B, 128, H16, W16), device=dev, dtype=f32)  # [pool(h16)]
+        z = {k: torch.empty_like(h) for k, h in (("08", h08), ("16", h16), ("32", h32))}
+        rh = {k: torch.empty_like(h) for k, h in (("08", h08), ("16", h16), ("32", h32))}
+        cz = [c[:, 0:128] for c in ctx]
+        cr = [c[:, 128:256] for c in ctx]
+        cq = [c[:, 256:384] for c in ctx]
+
+        def gru(level, h, x, key):
+            g = dw["g" + key]
+            xc = F.conv2d(x, g["wx"], g["bx"], padding=1)
+            hzr = F.conv2d(h, g["whzr"], None, padding=1)
+            ops.gru_zr(xc, hzr, cz[level], cr[level], h, z[key], rh[key])
+            qh = F.conv2d(rh[key], g["wqh"], None, padding=1)
+            ops.gru_out(xc, qh, cq[level], z[key], h)
+
+        ops.flow_update(coords_x, None, flow, x08[:, 126:128])
+        flow_up = None
+        for it in range(iters):
+            stereo_blk.lookup_into(coords_x, corr_buf, other=mono_blk)
+            # update.py:166-183, in order: gru32, gru16, motion encoder, gru08
+            ops.pool2x(h16, x32)
+            gru(2, h32, x32, "32")
+            ops.pool2x(h08, x16[:, :128])
+            ops.interp(h32, x16[:, 128:])
+            gru(1, h16, x16, "16")
+            # shared convc1/convc2 on the stereo and mono lookups as one 2B batch
+            c = F.relu(enc.convc1(corr_buf.view(2 * B, K, H4, W4)), inplace=True)
+            c = F.relu(enc.convc2(c), inplace=True).view(B, 128, H4, W4)
+            fl = F.relu(enc.convf1(flow), inplace=True)
+            fl = F.relu(enc.convf2(fl), inplace=True)
+            mot = enc._conv(torch.cat([c, fl], 1))
+            ops.relu_copy(mot, x08[:, :126])
+            ops.interp(h16, x08[:, 128:])
+            gru(0, h08, x08, "08")
+            delta = ub.flow_head.conv2(F.relu(ub.flow_head.conv1(h08), inplace=True))
+            ops.flow_update(coords_x, delta[:, 0:1], flow, x08[:, 126:128])
+            if it == iters - 1:
+                mask = ub.mask(h08).mul_(0.25)
+                flow_up = ops.convex_upsample(flow[:, 0:1].contiguous(), mask, 2 ** self.args.n_downsample)
+        return flow_up, None

@@ -1,0 +1,285 @@
+"""Torch-tensor front end of the C ABI (include/stereoanywhere_hip.h).
+
+Every function checks device / dtype / layout, allocates outputs with the caching
+allocator on the input's device, and enqueues the HIP kernel on torch's current
+stream through ``_native.call`` — there is no CPU or eager-torch fallback.
+PyTorch is plumbing here (device memory, streams); the arithmetic is in the .so.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Tuple
+
+import torch
+
+from . import _native as N
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _check(t: torch.Tensor, name: str, contiguous: bool = True) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name} must be on the GPU (HIP path has no CPU fallback), got {t.device}")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be float32, got {t.dtype}")
+    if contiguous and not t.is_contiguous():
+        raise RuntimeError(f"{name} must be contiguous")
+
+
+def _plane_bs(t: torch.Tensor, name: str, planes: int = 1) -> int:
+    """Batch stride of a [B, C, H, W] (possibly channel-sliced) view whose first
+    ``planes`` channels are each dense [H, W] planes laid out back to back."""
+    _check(t, name, contiguous=False)
+    B, C, H, W = t.shape
+    if t.stride(3) != 1 or t.stride(2) != W or (C > 1 and t.stride(1) != H * W):
+        raise RuntimeError(f"{name}: inner [C,H,W] block must be dense (strides {t.stride()})")
+    return t.stride(0)
+
+
+# ----------------------------------------------------------------------- pyramid geometry
+def pyramid_geometry(w2: int, num_levels: int) -> Tuple[int, List[int], List[int]]:
+    lib = N.lib()
+    rs = lib.sa_pyramid_row_stride(w2, num_levels)
+    offs = [lib.sa_pyramid_level_offset(w2, i) for i in range(num_levels)]
+    wids = [lib.sa_pyramid_level_width(w2, i) for i in range(num_levels)]
+    return int(rs), offs, wids
+
+
+# ----------------------------------------------------------------------- a1 + a8 + a9
+def corr_volume_pyramid(fmap2: torch.Tensor, fmap3: torch.Tensor, num_levels: int = 4,
+                        trunc_disp: Optional[torch.Tensor] = None, trunc_conf: Optional[torch.Tensor] = None,
+                        attenuation: float = 0.9, row_stride: Optional[int] = None) -> torch.Tensor:
+    """Stereo correlation volume (corr.py:117-132), optionally x truncation volume
+    (utils.py:216-238), and its avg-pool pyramid (corr.py:76-91) in one kernel.
+    Returns the pyramid buffer [B*H*W1, row_stride]."""
+    _check(fmap2, "fmap2")
+    _check(fmap3, "fmap3")
+    B, C, H, W1 = fmap2.shape
+    B3, C3, H3, W2 = fmap3.shape
+    if (B3, C3, H3) != (B, C, H):
+        raise RuntimeError(f"fmap shapes disagree: {tuple(fmap2.shape)} vs {tuple(fmap3.shape)}")
+    if trunc_disp is not None:
+        _check(trunc_disp, "trunc_disp")
+        _check(trunc_conf, "trunc_conf")
+        if trunc_disp.numel() != B * H * W1 or trunc_conf.numel() != B * H * W1:
+            raise RuntimeError("truncation maps must be [B,1,H,W1]")
+    rs = row_stride if row_stride is not None else pyramid_geometry(W2, num_levels)[0]
+    out = torch.empty((B * H * W1, rs), device=fmap2.device, dtype=torch.float32)
+    # torch.sqrt(torch.tensor(C)) of the reference: a float32 square root
+    sqrt_c = float(torch.sqrt(torch.tensor(float(C), dtype=torch.float32)))
+    N.call("sa_corr_volume_pyramid", fmap2.data_ptr(), fmap3.data_ptr(), B, C, H, W1, W2, sqrt_c,
+           _ptr(trunc_disp), _ptr(trunc_conf), attenuation, num_levels, out.data_ptr(), rs, _stream(fmap2))
+    return out
+
+
+def corr_volume(fmap2: torch.Tensor, fmap3: torch.Tensor) -> torch.Tensor:
+    """CorrBlock1D.corr contract: [B,C,H,W1] x [B,C,H,W2] -> [B,H,W1,1,W2]."""
+    B, C, H, W1 = fmap2.shape
+    W2 = fmap3.shape[3]
+    vol = corr_volume_pyramid(fmap2, fmap3, num_levels=1, row_stride=W2)
+    return vol.view(B, H, W1, 1, W2)
+
+
+def pyramid_from_volume(volume: torch.Tensor, num_levels: int = 4) -> torch.Tensor:
+    """CorrBlock1D.__init__ on an existing volume [..., W2] (rows contiguous along W2)."""
+    _check(volume, "volume", contiguous=False)
+    W2 = volume.shape[-1]
+    rows2d = volume.reshape(-1, W2)
+    if rows2d.stride(1) != 1:
+        raise RuntimeError("volume rows must be contiguous along the last axis")
+    rs = pyramid_geometry(W2, num_levels)[0]
+    out = torch.empty((rows2d.shape[0], rs), device=volume.device, dtype=torch.float32)
+    N.call("sa_corr_pyramid_from_volume", rows2d.data_ptr(), rows2d.shape[0], W2, rows2d.stride(0),
+           num_levels, out.data_ptr(), rs, _stream(volume))
+    return out
+
+
+# ----------------------------------------------------------------------- a10
+def corr_lookup(pyr_a: torch.Tensor, pyr_b: Optional[torch.Tensor], W2: int, num_levels: int, radius: int,
+                coords_x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Lookup of one or two pyramids at coords_x [B,1,H,W1] (any batch stride) ->
+    out [B, nvol*L*(2r+1), H, W1] (stereo channels first, then mono)."""
+    _check(pyr_a, "pyramid_a")
+    if pyr_b is not None:
+        _check(pyr_b, "pyramid_b")
+        if pyr_b.shape != pyr_a.shape:
+            raise RuntimeError("both pyramids must share a geometry")
+    cbs = _plane_bs(coords_x, "coords_x")
+    B, _, H, W1 = coords_x.shape
+    rs = pyr_a.shape[1]
+    if pyr_a.shape[0] != B * H * W1:
+        raise RuntimeError(f"pyramid rows {pyr_a.shape[0]} != B*H*W1 {B * H * W1}")
+    nvol = 2 if pyr_b is not None else 1
+    K = 2 * radius + 1
+    if out is None:
+        out = torch.empty((B, nvol * num_levels * K, H, W1), device=pyr_a.device, dtype=torch.float32)
+    obs = _plane_bs(out, "out")
+    N.call("sa_corr_lookup", pyr_a.data_ptr(), _ptr(pyr_b), W2, rs, num_levels, radius, coords_x.data_ptr(),
+           cbs, B, H, W1, out.data_ptr(), obs, _stream(pyr_a))
+    return out
+
+
+# ----------------------------------------------------------------------- a2 + a3
+def mono_normals(mde_lowres: torch.Tensor, gain: float) -> torch.Tensor:
+    _check(mde_lowres, "mde_lowres")
+    B, _, H, W = mde_lowres.shape
+    out = torch.empty((B, 3, H, W), device=mde_lowres.device, dtype=torch.float32)
+    N.call("sa_mono_normals", mde_lowres.data_ptr(), B, H, W, gain, out.data_ptr(), _stream(mde_lowres))
+    return out
+
+
+def mono_masked_volume(n2, n3, m2, m3, nbins: int = 8, gain: float = 1.73) -> torch.Tensor:
+    """-> [B, nbins, W2, H, W1] (the hourglass's working layout)."""
+    for t, nm in ((n2, "n2"), (n3, "n3"), (m2, "m2"), (m3, "m3")):
+        _check(t, nm)
+    B, _, H, W1 = n2.shape
+    W2 = n3.shape[3]
+    out = torch.empty((B, nbins, W2, H, W1), device=n2.device, dtype=torch.float32)
+    N.call("sa_mono_masked_volume", n2.data_ptr(), n3.data_ptr(), m2.data_ptr(), m3.data_ptr(), B, H, W1, W2,
+           nbins, gain, out.data_ptr(), _stream(n2))
+    return out
+
+
+# ----------------------------------------------------------------------- a5 + a6
+def softargmin_conf(vol_disp: Optional[torch.Tensor], vol_conf: Optional[torch.Tensor], strides, dims,
+                    out_disp: Optional[torch.Tensor] = None, out_conf: Optional[torch.Tensor] = None):
+    """Volumes addressed as v[b*sb + h*sh + j*sj + k*sk] with dims (B, H, W1, W2).
+    Outputs are [B, 2, H, W] buffers: channel 0 = left (over k), 1 = right (over j)."""
+    B, H, W1, W2 = dims
+    if W1 != W2:
+        raise RuntimeError("joint [B,2,H,W] outputs need W1 == W2")
+    sb, sh, sj, sk = strides
+    ref = vol_disp if vol_disp is not None else vol_conf
+    if out_disp is None and vol_disp is not None:
+        out_disp = torch.empty((B, 2, H, W1), device=ref.device, dtype=torch.float32)
+    if out_conf is None and vol_conf is not None:
+        out_conf = torch.empty((B, 2, H, W1), device=ref.device, dtype=torch.float32)
+    obs = 2 * H * W1
+    dL = dR = cL = cR = None
+    if out_disp is not None:
+        dL, dR = out_disp.data_ptr(), out_disp[:, 1].data_ptr()
+    if out_conf is not None:
+        cL, cR = out_conf.data_ptr(), out_conf[:, 1].data_ptr()
+    N.call("sa_softargmin_conf", _ptr(vol_disp), _ptr(vol_conf), B, H, W1, W2, sb, sh, sj, sk, dL, dR, cL, cR,
+           obs, _stream(ref))
+    return out_disp, out_conf
+
+
+# ----------------------------------------------------------------------- a7 + a8 + a11
+def softlrc_joint(disp: torch.Tensor, conf: Optional[torch.Tensor], lrc_th: float) -> torch.Tensor:
+    """softlrc of the L/R halves of a [B,2,H,W] disparity buffer, times conf (fuzzy_and)
+    when given -> [B,2,H,W]."""
+    _check(disp, "disp")
+    B, _, H, W = disp.shape
+    out = torch.empty_like(disp)
+    c2 = c3 = None
+    if conf is not None:
+        _check(conf, "conf")
+        c2, c3 = conf.data_ptr(), conf[:, 1].data_ptr()
+    N.call("sa_softlrc", disp.data_ptr(), disp[:, 1].data_ptr(), c2, c3, B, H, W, 2 * H * W, lrc_th,
+           out.data_ptr(), out[:, 1].data_ptr(), _stream(disp))
+    return out
+
+
+def weighted_lsq(mde: torch.Tensor, disp: torch.Tensor, conf: torch.Tensor, q_lo: float = 0.2,
+                 q_hi: float = 0.9) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-sample (scale, shift) [B] of weighted_lsq over the flattened [B, ...] maps."""
+    for t, nm in ((mde, "mde"), (disp, "disp"), (conf, "conf")):
+        _check(t, nm)
+    B = mde.shape[0]
+    n = mde.numel() // B
+    scale = torch.empty(B, device=mde.device, dtype=torch.float32)
+    shift = torch.empty(B, device=mde.device, dtype=torch.float32)
+    N.call("sa_weighted_lsq", mde.data_ptr(), disp.data_ptr(), conf.data_ptr(), B, n, q_lo, q_hi,
+           scale.data_ptr(), shift.data_ptr(), _stream(mde))
+    return scale, shift
+
+
+def mono_scale_mirror(mde_lr: torch.Tensor, scale, shift, disp: torch.Tensor, conf: torch.Tensor, lrc_th: float,
+                      conf_th: float):
+    """From [B,2,H,W] mono / disparity / confidence buffers -> sm2, sm3, mirror, coords_x [B,1,H,W]."""
+    for t, nm in ((mde_lr, "mde_lr"), (disp, "disp"), (conf, "conf")):
+        _check(t, nm)
+    B, _, H, W = mde_lr.shape
+    outs = [torch.empty((B, 1, H, W), device=mde_lr.device, dtype=torch.float32) for _ in range(4)]
+    N.call("sa_mono_scale_mirror", mde_lr.data_ptr(), mde_lr[:, 1].data_ptr(), scale.data_ptr(), shift.data_ptr(),
+           disp.data_ptr(), conf.data_ptr(), B, H, W, 2 * H * W, lrc_th, conf_th,
+           *[o.data_ptr() for o in outs], _stream(mde_lr))
+    return tuple(outs)
+
+
+# ----------------------------------------------------------------------- a12 / a13 plumbing
+def gru_zr(xc, hzr, cz, cr, h, z_out, rh_out):
+    B, C, H, W = h.shape
+    N.call("sa_gru_zr", xc.data_ptr(), _plane_bs(xc, "xc"), hzr.data_ptr(), _plane_bs(hzr, "hzr"),
+           cz.data_ptr(), cr.data_ptr(), _plane_bs(cz, "cz"), h.data_ptr(), _plane_bs(h, "h"), B, C, H * W,
+           z_out.data_ptr(), rh_out.data_ptr(), _stream(h))
+
+
+def gru_out(xc, qh, cq, z, h):
+    B, C, H, W = h.shape
+    N.call("sa_gru_out", xc.data_ptr(), _plane_bs(xc, "xc"), qh.data_ptr(), _plane_bs(qh, "qh"), cq.data_ptr(),
+           _plane_bs(cq, "cq"), z.data_ptr(), B, C, H * W, h.data_ptr(), _plane_bs(h, "h"), _stream(h))
+
+
+def pool2x(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    B, C, H, W = x.shape
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    if tuple(out.shape) != (B, C, Ho, Wo):
+        raise RuntimeError(f"pool2x: out {tuple(out.shape)} != {(B, C, Ho, Wo)}")
+    N.call("sa_pool2x", x.data_ptr(), _plane_bs(x, "x"), B, C, H, W, out.data_ptr(), _plane_bs(out, "out"),
+           _stream(x))
+    return out
+
+
+def interp(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    B, C, H, W = x.shape
+    Bo, Co, Ho, Wo = out.shape
+    if (Bo, Co) != (B, C):
+        raise RuntimeError("interp: batch/channels mismatch")
+    N.call("sa_interp_bilinear_ac", x.data_ptr(), _plane_bs(x, "x"), B, C, H, W, Ho, Wo, out.data_ptr(),
+           _plane_bs(out, "out"), _stream(x))
+    return out
+
+
+def relu_copy(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    B, C, H, W = x.shape
+    if tuple(out.shape) != (B, C, H, W):
+        raise RuntimeError("relu_copy: shape mismatch")
+    N.call("sa_relu_copy", x.data_ptr(), _plane_bs(x, "x"), B, C, H * W, out.data_ptr(), _plane_bs(out, "out"),
+           _stream(x))
+    return out
+
+
+def flow_update(coords_x: torch.Tensor, delta: Optional[torch.Tensor], flow_a: Optional[torch.Tensor],
+                flow_b: Optional[torch.Tensor]) -> None:
+    _check(coords_x, "coords_x")
+    B, _, H, W = coords_x.shape
+    N.call("sa_flow_update", coords_x.data_ptr(), _ptr(delta), 0 if delta is None else _plane_bs(delta, "delta"),
+           B, H, W, _ptr(flow_a), 0 if flow_a is None else _plane_bs(flow_a, "flow_a"), _ptr(flow_b),
+           0 if flow_b is None else _plane_bs(flow_b, "flow_b"), _stream(coords_x))
+
+
+def convex_upsample(flow_x: torch.Tensor, mask: torch.Tensor, factor: int = 4) -> torch.Tensor:
+    """flow_x [B,1,H,W] (contiguous), mask [B,9*f*f,H,W] -> [B,1,f*H,f*W]."""
+    _check(flow_x, "flow_x")
+    B, _, H, W = flow_x.shape
+    out = torch.empty((B, 1, factor * H, factor * W), device=flow_x.device, dtype=torch.float32)
+    N.call("sa_convex_upsample", flow_x.data_ptr(), mask.data_ptr(), _plane_bs(mask, "mask"), B, H, W, factor,
+           out.data_ptr(), _stream(flow_x))
+    return out
+
+
+def float32_sqrt(x: float) -> float:
+    return float(torch.sqrt(torch.tensor(float(x), dtype=torch.float32)))
+
+
+__all__ = [n for n in dir() if not n.startswith("_") and n not in ("annotations", "math", "torch")]

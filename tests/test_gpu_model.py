@@ -1,0 +1,65 @@
+"""End-to-end parity of the MI355X model against the reference's own outputs
+(tests/golden, produced by the reference on identical seeded weights and inputs).
+Gate: EPE < 1e-3 px (north_star); the fp32 floor measured here is ~1e-5."""
+import numpy as np
+import pytest
+import torch
+
+from fixtures_util import epe, load_fixture, regenerate_inputs
+from stereoanywhere_amd import synth
+from stereoanywhere_amd.model import StereoAnywhere
+
+pytestmark = pytest.mark.gpu
+PUBLISHED = dict(use_truncate_vol=True, use_aggregate_mono_vol=True, vol_n_masks=8, n_additional_hourglass=0,
+                 vol_downsample=0, mirror_conf_th=0.98, mirror_attenuation=0.9, lrc_th=1.0, normal_gain=10)
+
+
+@pytest.fixture(scope="module")
+def model():
+    torch.backends.cudnn.benchmark = False
+    m = StereoAnywhere(dict(PUBLISHED)).eval()
+    synth.load_seeded_weights(m, 0)
+    return m.cuda()
+
+
+def run(model, pair, iters):
+    t = [torch.from_numpy(pair[k]).cuda() for k in ("left", "right", "mono_left", "mono_right")]
+    flow_up, none = model(*t, iters=iters, test_mode=True)
+    assert none is None
+    return -flow_up[:, 0].cpu().numpy()
+
+
+def test_tiny_case_and_intermediates(model):
+    fix = load_fixture("tiny_64x128_it4.npz")
+    pair = regenerate_inputs(fix, 1, 64, 128, 24.0)
+    disp = run(model, pair, 4)
+    e = epe(disp, fix["disparity"])
+    print("tiny EPE", e)
+    assert e < 1e-3
+
+
+@pytest.mark.parametrize("name,H,W,D,iters", [("cfg1_256x512_it8.npz", 256, 512, 64.0, 8),
+                                               ("cfg2_544x960_it22.npz", 544, 960, 192.0, 22)])
+def test_end_to_end_vs_reference(model, name, H, W, D, iters):
+    fix = load_fixture(name)
+    pair = regenerate_inputs(fix, 1, H, W, D)
+    disp = run(model, pair, iters)
+    e = epe(disp, fix["disparity"])
+    print(name, "EPE", e, "max", float(np.abs(disp - fix["disparity"]).max()))
+    assert e < 1e-3
+
+
+def test_batch_independence(model):
+    """Pairs are independent: a B=3 batch equals three B=1 runs."""
+    pb = synth.synthetic_batch(3, 128, 256, 48.0, seed0=5)
+    batch = run(model, pb, 6)
+    for i in range(3):
+        single = run(model, {k: v[i:i + 1] for k, v in pb.items()}, 6)
+        assert epe(batch[i:i + 1], single) < 1e-4
+
+
+def test_deterministic_rerun(model):
+    pb = synth.synthetic_batch(1, 128, 256, 48.0, seed0=9)
+    a = run(model, pb, 5)
+    b = run(model, pb, 5)
+    assert np.array_equal(a, b)

@@ -1,0 +1,234 @@
+"""Per-op parity of the HIP kernels (through the C ABI) against the oracle restatement
+and the reference's own golden vectors.  Tolerances are absolute unless stated:
+volumes/lookups 1e-5·scale (fp32 accumulation-order noise), maps 1e-5, masks exact."""
+import numpy as np
+import pytest
+import torch
+
+from fixtures_util import load_fixture
+from oracle import ops_ref as R
+from stereoanywhere_amd import ops
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def g(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)
+
+
+def c(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def micro():
+    return load_fixture("micro_ops.npz")
+
+
+def levels_of(pyr, B, H, W1, W2, L=4):
+    rs, offs, wids = ops.pyramid_geometry(W2, L)
+    p = c(pyr).reshape(B, H, W1, rs)
+    return [p[..., o:o + w] for o, w in zip(offs, wids)]
+
+
+@pytest.mark.parametrize("shape", [(2, 256, 3, 37, 45), (1, 256, 5, 240, 240), (2, 64, 4, 128, 96), (1, 3, 6, 20, 20),
+                                   (1, 256, 2, 64, 300)])
+def test_corr_volume_and_pyramid(shape):
+    B, C, H, W1, W2 = shape
+    rng = np.random.default_rng(sum(shape))
+    f2 = rng.standard_normal((B, C, H, W1)).astype(np.float32)
+    f3 = rng.standard_normal((B, C, H, W2)).astype(np.float32)
+    ref = R.corr_volume(f2, f3)
+    vol = c(ops.corr_volume(g(f2), g(f3)))[:, :, :, 0]
+    tol = 2e-6 * np.abs(ref).max() + 1e-6
+    np.testing.assert_allclose(vol, ref, atol=tol)
+    pyr = ops.corr_volume_pyramid(g(f2), g(f3), 4)
+    got = levels_of(pyr, B, H, W1, W2)
+    for lv, rv in zip(got, R.corr_pyramid(ref, 4)):
+        np.testing.assert_allclose(lv, rv, atol=tol)
+
+
+def test_corr_volume_matches_reference_vector(micro):
+    vol = c(ops.corr_volume(g(micro["corr.f2"]), g(micro["corr.f3"])))
+    np.testing.assert_allclose(vol, micro["corr.out"], atol=2e-5)
+
+
+def test_truncated_pyramid():
+    B, C, H, W = 2, 256, 4, 96
+    rng = np.random.default_rng(3)
+    f2 = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    f3 = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    d = (rng.random((B, 1, H, W)) * 40).astype(np.float32)
+    m = rng.random((B, 1, H, W)).astype(np.float32)
+    ref = R.truncate_volume(d, m, 0.9) * R.corr_volume(f2, f3)
+    pyr = ops.corr_volume_pyramid(g(f2), g(f3), 4, g(d), g(m), 0.9)
+    tol = 2e-6 * np.abs(ref).max() + 1e-6
+    for lv, rv in zip(levels_of(pyr, B, H, W, W), R.corr_pyramid(ref.astype(np.float32), 4)):
+        np.testing.assert_allclose(lv, rv, atol=tol)
+
+
+def test_pyramid_from_volume_and_lookup_edges(micro):
+    vol = micro["corr.out"][:, :, :, 0]  # [2,3,37,45]
+    B, H, W1, W2 = vol.shape
+    pyr = ops.pyramid_from_volume(g(vol), 4)
+    for lv, i in zip(levels_of(pyr, B, H, W1, W2), range(4)):
+        np.testing.assert_allclose(lv, micro[f"pyr.level{i}"].reshape(lv.shape), atol=1e-6)
+    coords = g(micro["lookup.coords"])
+    out = c(ops.corr_lookup(pyr, None, W2, 4, 4, coords[:, :1]))
+    np.testing.assert_allclose(out, micro["lookup.out"], atol=1e-5)
+
+
+def test_lookup_two_volumes_one_launch():
+    rng = np.random.default_rng(5)
+    B, H, W = 2, 6, 64
+    va = rng.standard_normal((B, H, W, W)).astype(np.float32)
+    vb = rng.standard_normal((B, H, W, W)).astype(np.float32)
+    cx = (rng.random((B, 1, H, W)) * 90 - 20).astype(np.float32)
+    pa, pb = ops.pyramid_from_volume(g(va)), ops.pyramid_from_volume(g(vb))
+    out = c(ops.corr_lookup(pa, pb, W, 4, 4, g(cx)))
+    ref = np.concatenate([R.corr_lookup(R.corr_pyramid(va), cx[:, 0]), R.corr_lookup(R.corr_pyramid(vb), cx[:, 0])], 1)
+    np.testing.assert_allclose(out, ref, atol=1e-5)
+
+
+def test_hip_corr_block_contract(micro):
+    from stereoanywhere_amd.corr import HipCorrBlock1D
+    blk = HipCorrBlock1D(g(micro["corr.out"]), num_levels=4, radius=4)
+    for i in range(4):
+        np.testing.assert_allclose(c(blk.corr_pyramid[i]), micro[f"pyr.level{i}"], atol=1e-6)
+    np.testing.assert_allclose(c(blk(g(micro["lookup.coords"]))), micro["lookup.out"], atol=1e-5)
+    v = HipCorrBlock1D.corr(g(micro["corr.f2"]), g(micro["corr.f3"]))
+    assert tuple(v.shape) == micro["corr.out"].shape
+
+
+def test_normals_masks_and_masked_volume(micro):
+    mde = micro["masks.mde"]  # [2,1,6,20] incl. 1.0 and exact bin edges
+    n = c(ops.mono_normals(g(mde), 2.0))
+    np.testing.assert_allclose(n, micro["normals.out"], atol=1e-6)
+    rng = np.random.default_rng(11)
+    m3 = rng.random(mde.shape).astype(np.float32)
+    m3[0, 0, 0, :4] = [1.0, 0.0, 0.5, 0.375]
+    n3 = R.estimate_normals(m3, 2.0)
+    out = c(ops.mono_masked_volume(g(micro["normals.out"]), g(n3), g(mde), g(m3), 8, 1.73))  # [B,8,W2,H,W1]
+    ref = R.masked_mono_volume(R.mono_corr_volume(micro["normals.out"], n3), R.generate_masks(mde), R.generate_masks(m3))
+    np.testing.assert_allclose(out, ref.transpose(0, 1, 4, 2, 3), atol=1e-6)
+    # pixels with mde == 1.0 are in no bin: their whole row is zero in every channel
+    assert np.all(out[0, :, :, 0, 5] == 0)
+
+
+@pytest.mark.parametrize("layout", ["reference", "native"])
+def test_softargmin_confidence(micro, layout):
+    vol = micro["sam.vol"][:, 0]  # [B,H,W1,W2]
+    B, H, W1, W2 = vol.shape
+    if layout == "reference":
+        t = g(vol)
+        strides = (H * W1 * W2, W1 * W2, W2, 1)
+    else:
+        t = g(vol.transpose(0, 3, 1, 2))  # [B,W2,H,W1]
+        strides = (W2 * H * W1, W1, 1, H * W1)
+    d, cf = ops.softargmin_conf(t, t, strides, (B, H, W1, W2))
+    d, cf = c(d), c(cf)
+    np.testing.assert_allclose(d[:, 0:1], micro["sam.left"], atol=2e-5)
+    np.testing.assert_allclose(d[:, 1:2], micro["sam.right"], atol=2e-5)
+    np.testing.assert_allclose(cf[:, 0:1], micro["conf.left"], atol=2e-6)
+    np.testing.assert_allclose(cf[:, 1:2], micro["conf.right"], atol=2e-6)
+
+
+def test_softlrc(micro):
+    d = np.concatenate([micro["lrc.d2"], micro["lrc.d3"]], 1)
+    out = c(ops.softlrc_joint(g(d), None, 1.0))
+    np.testing.assert_allclose(out[:, 0:1], micro["lrc.s2"], atol=2e-6)
+    np.testing.assert_allclose(out[:, 1:2], micro["lrc.s3"], atol=2e-6)
+
+
+def test_weighted_lsq_matches_reference(micro):
+    sc, sh = ops.weighted_lsq(g(micro["lsq.mde"]), g(micro["lsq.disp"]), g(micro["lsq.conf"]))
+    np.testing.assert_allclose(c(sc), micro["lsq.scale"].ravel(), rtol=2e-5, atol=1e-5)
+    np.testing.assert_allclose(c(sh), micro["lsq.shift"].ravel(), rtol=2e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("n", [2, 17, 1000, 65280])
+def test_weighted_lsq_quantile_band_vs_oracle(n):
+    rng = np.random.default_rng(n)
+    B = 3
+    m = rng.random((B, n)).astype(np.float32)
+    d = (40 * m + 3 + rng.standard_normal((B, n))).astype(np.float32)
+    d[:, : n // 7] = -1.0  # relu'd to 0: ties at the bottom of the band
+    d[1, : n // 2] = 5.0    # ties inside the band
+    cf = rng.random((B, n)).astype(np.float32)
+    sc, sh = ops.weighted_lsq(g(m), g(d), g(cf))
+    rsc, rsh = R.weighted_lsq(m, d, cf)
+    np.testing.assert_allclose(c(sc), rsc, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(c(sh), rsh, rtol=1e-5, atol=1e-4)
+
+
+def test_mirror_and_coords():
+    rng = np.random.default_rng(2)
+    B, H, W = 2, 8, 40
+    mde = rng.random((B, 2, H, W)).astype(np.float32)
+    disp = (rng.random((B, 2, H, W)) * 20).astype(np.float32)
+    conf = rng.random((B, 2, H, W)).astype(np.float32)
+    scale = np.array([-3.0, 12.0], np.float32)
+    shift = np.array([20.0, 1.5], np.float32)
+    sm2, sm3, mir, cx = [c(t) for t in ops.mono_scale_mirror(g(mde), g(scale), g(shift), g(disp), g(conf), 1.0, 0.98)]
+    rsm2 = (scale[:, None, None, None] * mde[:, 0:1] + shift[:, None, None, None]).astype(np.float32)
+    rsm3 = (scale[:, None, None, None] * mde[:, 1:2] + shift[:, None, None, None]).astype(np.float32)
+    np.testing.assert_allclose(sm2, rsm2, atol=1e-5)
+    lrc, _ = R.softlrc(rsm2, rsm3, 1.0)
+    rmir = R.handcrafted_mirror_detector(disp[:, 0:1], rsm2, conf[:, 0:1], lrc, 0.98)
+    np.testing.assert_allclose(mir, rmir, atol=2e-5)
+    np.testing.assert_allclose(cx, np.arange(W, dtype=np.float32) - rsm2, atol=1e-5)
+
+
+def test_convex_upsample(micro):
+    out = c(ops.convex_upsample(g(micro["up.flow"]), g(micro["up.mask"]), 4))
+    np.testing.assert_allclose(out, micro["up.out"], atol=1e-5)
+
+
+def test_gru_gates_and_plumbing():
+    rng = np.random.default_rng(9)
+    B, C, H, W = 2, 128, 10, 12
+    xc = rng.standard_normal((B, 3 * C, H, W)).astype(np.float32)
+    hzr = rng.standard_normal((B, 2 * C, H, W)).astype(np.float32)
+    ctx = rng.standard_normal((B, 3 * C, H, W)).astype(np.float32)
+    h = np.tanh(rng.standard_normal((B, C, H, W))).astype(np.float32)
+    qh = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    gctx, gh = g(ctx), g(h)
+    z, rh = torch.empty_like(gh), torch.empty_like(gh)
+    ops.gru_zr(g(xc), g(hzr), gctx[:, :C], gctx[:, C:2 * C], gh, z, rh)
+    ops.gru_out(g(xc), g(qh), gctx[:, 2 * C:], z, gh)
+    zr = R.sigmoid(xc[:, :C] + hzr[:, :C] + ctx[:, :C])
+    rr = R.sigmoid(xc[:, C:2 * C] + hzr[:, C:] + ctx[:, C:2 * C])
+    q = np.tanh(xc[:, 2 * C:] + qh + ctx[:, 2 * C:])
+    np.testing.assert_allclose(c(z), zr, atol=1e-6)
+    np.testing.assert_allclose(c(rh), rr * h, atol=1e-6)
+    np.testing.assert_allclose(c(gh), (1 - zr) * h + zr * q, atol=2e-6)
+    # plumbing vs torch's own ops on the GPU
+    x = g(rng.standard_normal((B, C, 17, 23)))
+    buf = torch.zeros(B, 2 * C, 9, 12, device=dev)
+    ops.pool2x(x, buf[:, C:])
+    torch.testing.assert_close(buf[:, C:], torch.nn.functional.avg_pool2d(x, 3, 2, 1), atol=1e-6, rtol=0)
+    y = g(rng.standard_normal((B, C, 5, 6)))
+    ops.interp(y, buf[:, :C])
+    torch.testing.assert_close(buf[:, :C], torch.nn.functional.interpolate(y, (9, 12), mode="bilinear",
+                                                                           align_corners=True), atol=1e-6, rtol=0)
+    r = torch.empty(B, C, 17, 23, device=dev)
+    ops.relu_copy(x, r)
+    torch.testing.assert_close(r, torch.relu(x))
+
+
+def test_ops_reject_cpu_tensors():
+    with pytest.raises(RuntimeError, match="GPU"):
+        ops.corr_volume(torch.zeros(1, 4, 2, 8), torch.zeros(1, 4, 2, 8))
+
+
+def test_timing_counts_launches():
+    from stereoanywhere_amd import _native as N
+    f = torch.randn(1, 256, 8, 64, device=dev)
+    N.timing_enable(True)
+    for _ in range(3):
+        ops.corr_volume_pyramid(f, f, 4)
+    ms, n = N.timing_read("corr_volume_pyramid")
+    N.timing_enable(False)
+    assert n == 3 and ms > 0
