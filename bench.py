@@ -75,11 +75,24 @@ def make_inputs(B, H, W, Hp, Wp, D, seed0, device):
     return out
 
 
+def host_threads() -> int:
+    """CPU share of this process: OMP_NUM_THREADS if set (16 on the GPU box), else the
+    affinity mask — os.cpu_count() reports the whole machine there."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+def log(msg: str) -> None:
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(iters: int, H: int, W: int):
     """The oracle restatement on one pair (bounded sample), all host threads."""
     from oracle import model_ref as M
 
-    torch.set_num_threads(os.cpu_count() or 1)
+    torch.set_num_threads(host_threads())
     sd = M.load_state_dict_seeded(0)
     pair = synth.synthetic_batch(1, H, W, 192.0, seed0=1)
     t = [torch.from_numpy(pair[k]) for k in ("left", "right", "mono_left", "mono_right")]
@@ -133,9 +146,10 @@ def main():
     x = (inp["left"], inp["right"], inp["mono_left"], inp["mono_right"])
 
     with torch.no_grad():
-        for _ in range(args.warmup):
+        for i in range(args.warmup):
             model(*x, iters=args.iters, test_mode=True)
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            log(f"warmup {i + 1}/{args.warmup} done")
         N.timing_enable(True)
         D.barrier(r)
         torch.cuda.synchronize()
@@ -145,6 +159,7 @@ def main():
         torch.cuda.synchronize()
         D.barrier(r)
         elapsed = time.perf_counter() - t0
+        log(f"timed {args.steps} steps in {elapsed:.3f} s")
         kt = {k: N.timing_read(k) for k in N.KERNEL_IDS}
         N.timing_enable(False)
         elapsed = D.max_over_ranks(elapsed, r, device)
@@ -186,7 +201,9 @@ def main():
     }
     if not args.no_epe:
         res["epe_vs_reference"] = epe_vs_reference(model, device)
+        log(f"EPE vs reference {res['epe_vs_reference']:.3g}")
     if r.world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline (oracle, bounded sample) ...")
         res["cpu_baseline"] = cpu_baseline(args.iters, Hp, Wp)
     print(json.dumps(res))
 
