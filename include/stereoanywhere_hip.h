@@ -157,12 +157,42 @@ int sa_flow_update(float *coords_x, const float *delta, long delta_bs, int B, in
 int sa_convex_upsample(const float *flow, const float *mask, long mask_bs, int B, int H, int W,
                        int factor, float *out, void *stream);
 
+/* Hourglass full-resolution tail (hourglass.py:325-329, submodule.py:25-53, 113-140,
+ * stereoanywhere.py:165-166) as fused direct 3-D convolutions on [B, C, D, H, W]
+ * volumes (D = W2, W = W1), 3x3x3 / stride 1 / pad 1 / no bias:
+ *   out = conv(T(in)),  T(x) = [gate_l[b,c,h,w] * gate_r[b,c,h,d] *] [lrelu(] [(x - mean[b,c]) *
+ *   rstd[b,c]] [)] — the previous layer's InstanceNorm3d + LeakyReLU (+ DoubleFeatureAtt
+ *   gate) applied while the input is staged.  stats_partial (may be NULL): per-block
+ *   float64 (sum, sum^2) of every output channel, [B*Cout][parts][2] with
+ *   parts = sa_conv3d_stat_parts(D, H, W); reduce with sa_instnorm_finalize.
+ * Built for Cin = 8 -> Cout = 8 (final_agg) or 2 (both classifiers in one launch). */
+long sa_conv3d_stat_parts(int D, int H, int W);
+int sa_conv3d_k3(const float *in, int B, int Cin, int D, int H, int W, const float *weight,
+                 int Cout, const float *in_mean, const float *in_rstd, int act, float slope,
+                 const float *gate_l, const float *gate_r, float *out, double *stats_partial,
+                 void *stream);
+/* 1x1x1 conv over cat(a, trilinear_up(u)) (hourglass.py:326-328 + final_agg.0): a [B,8,D,H,W],
+ * u [B,16,Du,Hu,Wu] upsampled with align_corners=True on the fly; weight [Cout, 24]. */
+int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *u, int Cu, int Du, int Hu,
+                              int Wu, int B, int D, int H, int W, const float *weight, int Cout,
+                              float *out, double *stats_partial, void *stream);
+/* mean/rstd of each of bc_count channels from the partials (count voxels each, biased
+ * variance, rstd = 1/sqrt(var + eps)) — InstanceNorm3d statistics (affine=False). */
+int sa_instnorm_finalize(const double *partial, int bc_count, long nparts, long count, float eps,
+                         float *mean, float *rstd, void *stream);
+
+/* convf1 + ReLU of the motion encoder (update.py:76, 85): direct KxK conv, Cin <= 8,
+ * in [B,Cin,H,W] (batch stride in_bs) -> out [B,Cout,H,W] (batch stride out_bs). */
+int sa_conv2d_small(const float *in, long in_bs, int B, int Cin, int H, int W, const float *weight,
+                    const float *bias, int Cout, int ksize, int relu, float *out, long out_bs,
+                    void *stream);
+
 /* Live per-kernel timing for bench.py: when enabled, every launch of kernel `id`
  * is bracketed by hipEvents on the launch stream; sa_timing_read synchronises the
  * recorded events and returns their summed duration (ms) and count, then clears. */
 enum {
   SA_K_CORR_PYRAMID = 0, SA_K_LOOKUP, SA_K_MONO_VOLUME, SA_K_SOFTARGMIN, SA_K_LSQ,
-  SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_COUNT
+  SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_COUNT
 };
 int sa_timing_enable(int on);
 int sa_timing_read(int kernel_id, double *total_ms, long *count);

@@ -44,6 +44,11 @@ SIGNATURES = {
     "sa_relu_copy": (I, [P, L, I, I, I, P, L, P]),
     "sa_flow_update": (I, [P, P, L, I, I, I, P, L, P, L, P]),
     "sa_convex_upsample": (I, [P, P, L, I, I, I, I, P, P]),
+    "sa_conv3d_stat_parts": (L, [I, I, I]),
+    "sa_conv3d_k3": (I, [P, I, I, I, I, I, P, I, P, P, I, F, P, P, P, P, P]),
+    "sa_conv3d_pointwise_upcat": (I, [P, I, P, I, I, I, I, I, I, I, I, P, I, P, P, P]),
+    "sa_instnorm_finalize": (I, [P, I, L, L, F, P, P, P]),
+    "sa_conv2d_small": (I, [P, L, I, I, I, I, P, P, I, I, I, P, L, P]),
     "sa_timing_enable": (I, [I]),
     "sa_timing_read": (I, [I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]),
     "sa_kernel_name": (ctypes.c_char_p, [I]),
@@ -51,7 +56,7 @@ SIGNATURES = {
 
 KERNEL_IDS = {
     "corr_volume_pyramid": 0, "corr_lookup": 1, "mono_masked_volume": 2, "softargmin_conf": 3,
-    "weighted_lsq": 4, "gru_zr": 5, "gru_out": 6, "convex_upsample": 7, "misc": 8,
+    "weighted_lsq": 4, "gru_zr": 5, "gru_out": 6, "convex_upsample": 7, "misc": 8, "conv3d_fused": 9,
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -177,7 +177,10 @@ class Hourglass(nn.Module):
         self.final_feature_atts_up = DoubleFeatureAtt(out_channels, fc[0])
         self.number_of_scales = ns
 
-    def forward(self, x, features_left, features_right):
+    def forward(self, x, features_left, features_right, fused=None):
+        """``fused``: dict of pre-arranged weights (model._weights) to run the full-resolution
+        tail through the fused HIP convolutions; returns (vol_disp, vol_conf) of the two
+        classifiers then (see _fused_tail).  Without it: the plain torch/MIOpen tail."""
         ns = self.number_of_scales
         orig = x
         downs = []
@@ -191,9 +194,27 @@ class Hourglass(nn.Module):
                            align_corners=True)
         x = self.agg_layers[i](torch.cat((up, downs[ns - 3 - i]), 1))
         x = self.feature_atts_up[i](x, features_left[ns - 2 - i], features_right[ns - 2 - i])
+        if fused is not None:
+            return self._fused_tail(orig, x, features_left[0], features_right[0], fused)
         up = F.interpolate(x, size=orig.shape[2:], mode="trilinear", align_corners=True)
         x = self.final_agg(torch.cat((orig, up), 1))
         return self.final_feature_atts_up(x, features_left[0], features_right[0])
+
+    def _fused_tail(self, orig, x, feat_left, feat_right, fw):
+        """hourglass.py:325-329 + classifiers (stereoanywhere.py:165-166) at full volume
+        resolution in four HIP launches (csrc/conv3d_fused.hip): each conv applies the
+        previous InstanceNorm3d + LeakyReLU on load; the DoubleFeatureAtt gate is applied
+        on load of the classifier conv, whose two outputs are computed together."""
+        from . import ops
+        att = self.final_feature_atts_up
+        gl = torch.sigmoid(att.feat_att_left(feat_left)).contiguous()    # [B,C,H,W1]
+        gr = torch.sigmoid(att.feat_att_right(feat_right)).contiguous()  # [B,C,H,W2]
+        slope = self.final_agg[0].act_fn.negative_slope
+        t, st = ops.conv3d_pointwise_upcat(orig.contiguous(), x.contiguous(), fw["fa0"], fw["fa0"].shape[1])
+        t, st = ops.conv3d_k3(t, fw["fa1"], fw["fa1"].shape[2], norm=st, act=True, slope=slope, stats=True)
+        t, st = ops.conv3d_k3(t, fw["fa2"], fw["fa2"].shape[2], norm=st, act=True, slope=slope, stats=True)
+        vol, _ = ops.conv3d_k3(t, fw["cls"], 2, norm=st, act=True, slope=slope, gate=(gl, gr))
+        return vol[:, 0:1], vol[:, 1:2]
 
 
 class ConvGRU(nn.Module):

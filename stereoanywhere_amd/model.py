@@ -100,7 +100,18 @@ class StereoAnywhere(nn.Module):
                     # reference conv over (H, W1, W2) == conv over (W2, H, W1) with permuted kernel
                     cls_d=self.classifier_mono.weight.permute(0, 1, 4, 2, 3).contiguous(),
                     cls_c=self.classifier_monoconf.weight.permute(0, 1, 4, 2, 3).contiguous(),
+                    # convf1 [64,2,7,7] -> [ci][ky][kx][co] for sa_conv2d_small
+                    f1=ub.encoder.convf1.weight.permute(1, 2, 3, 0).contiguous(),
                 )
+                hg = self.hourglass_mono
+                cls = torch.cat([self._derived["cls_d"], self._derived["cls_c"]], 0)  # [2,8,3,3,3]
+
+                def k3(w):  # [co, ci, 3,3,3] -> [ci][27][co]
+                    return w.reshape(w.shape[0], w.shape[1], 27).permute(1, 2, 0).contiguous()
+                fa0 = hg.final_agg[0].conv.weight
+                self._derived["hg_tail"] = dict(
+                    fa0=fa0.reshape(fa0.shape[0], fa0.shape[1]).t().contiguous(),  # [cin][co]
+                    fa1=k3(hg.final_agg[1].conv.weight), fa2=k3(hg.final_agg[2].conv.weight), cls=k3(cls))
             self._derived_key = key
         return self._derived
 
@@ -163,14 +174,22 @@ class StereoAnywhere(nn.Module):
 
         # ---- mono cost volume -> 3-D hourglass -> classifiers (native [B,C,W2,H,W1] layout)
         masked = ops.mono_masked_volume(n2, n3, m2l, m3l, a.vol_n_masks, 1.73)
-        agg = self.hourglass_mono(masked, feats_l, feats_r)
-        for i in range(a.n_additional_hourglass):  # stack[0] is the identity (stereoanywhere.py:163-164)
-            hg = self.hourglass_mono_stack[i]
-            agg = agg if isinstance(hg, HourglassIdentity) else hg(agg, feats_l, feats_r)
-        vol_d = F.conv3d(agg, dw["cls_d"], padding=1)  # [B,1,W2,H,W1]
-        vol_c = F.conv3d(agg, dw["cls_c"], padding=1)
-        del masked, agg
-        strides = (W4 * H4 * W4, W4, 1, H4 * W4)  # (b, h, j, k) -> native layout
+        # stack[i] for i < n_additional (stereoanywhere.py:163-164): stack[0] is the identity,
+        # so only n_additional >= 2 puts a real hourglass after hourglass_mono
+        extra = [self.hourglass_mono_stack[i] for i in range(a.n_additional_hourglass)
+                 if not isinstance(self.hourglass_mono_stack[i], HourglassIdentity)]
+        if not extra and a.vol_n_masks == 8 and a.volume_channels == 8:
+            vol_d, vol_c = self.hourglass_mono(masked, feats_l, feats_r, fused=dw["hg_tail"])
+        else:
+            agg = self.hourglass_mono(masked, feats_l, feats_r)
+            for hg in extra:
+                agg = hg(agg, feats_l, feats_r)
+            vol_d = F.conv3d(agg, dw["cls_d"], padding=1)  # [B,1,W2,H,W1]
+            vol_c = F.conv3d(agg, dw["cls_c"], padding=1)
+            del agg
+        del masked
+        # (b, h, j, k) -> native [B, ., W2, H, W1] layout; vol_d/vol_c may be channel views
+        strides = (vol_d.stride(0), W4, 1, H4 * W4)
         disp_lr, conf_lr = ops.softargmin_conf(vol_d, vol_c, strides, (B, H4, W4, W4))
 
         # ---- scale/shift alignment, mirror detector, truncation inputs
@@ -238,7 +257,7 @@ class StereoAnywhere(nn.Module):
             # shared convc1/convc2 on the stereo and mono lookups as one 2B batch
             c = F.relu(enc.convc1(corr_buf.view(2 * B, K, H4, W4)), inplace=True)
             c = F.relu(enc.convc2(c), inplace=True).view(B, 128, H4, W4)
-            fl = F.relu(enc.convf1(flow), inplace=True)
+            fl = ops.conv2d_small(flow, dw["f1"], enc.convf1.bias, 64, 7, relu=True)
             fl = F.relu(enc.convf2(fl), inplace=True)
             mot = enc._conv(torch.cat([c, fl], 1))
             ops.relu_copy(mot, x08[:, :126])

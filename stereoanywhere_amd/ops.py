@@ -283,3 +283,60 @@ def float32_sqrt(x: float) -> float:
 
 
 __all__ = [n for n in dir() if not n.startswith("_") and n not in ("annotations", "math", "torch")]
+
+
+# ----------------------------------------------------------------------- fused hourglass tail / convf1
+def conv3d_stat_parts(D: int, H: int, W: int) -> int:
+    return int(N.lib().sa_conv3d_stat_parts(D, H, W))
+
+
+def instnorm_finalize(partial: torch.Tensor, bc: int, parts: int, count: int, eps: float = 1e-5):
+    mean = torch.empty(bc, device=partial.device, dtype=torch.float32)
+    rstd = torch.empty(bc, device=partial.device, dtype=torch.float32)
+    N.call("sa_instnorm_finalize", partial.data_ptr(), bc, parts, count, eps, mean.data_ptr(), rstd.data_ptr(),
+           _stream(partial))
+    return mean, rstd
+
+
+def conv3d_k3(x: torch.Tensor, w_t: torch.Tensor, cout: int, norm=None, act: bool = False, slope: float = 0.01,
+              gate=None, stats: bool = False):
+    """3x3x3 conv (no bias) of T(x) with T = [gate *] [lrelu] [instance-norm(mean, rstd)];
+    w_t pre-arranged [Cin][27][Cout].  Returns (out [B,Cout,D,H,W], (mean, rstd) | None)."""
+    _check(x, "x")
+    _check(w_t, "w_t")
+    B, Cin, D, H, W = x.shape
+    out = torch.empty((B, cout, D, H, W), device=x.device, dtype=torch.float32)
+    parts = conv3d_stat_parts(D, H, W)
+    partial = torch.empty((B * cout * parts * 2,), device=x.device, dtype=torch.float64) if stats else None
+    mean, rstd = norm if norm is not None else (None, None)
+    gl, gr = gate if gate is not None else (None, None)
+    N.call("sa_conv3d_k3", x.data_ptr(), B, Cin, D, H, W, w_t.data_ptr(), cout, _ptr(mean), _ptr(rstd),
+           1 if act else 0, slope, _ptr(gl), _ptr(gr), out.data_ptr(), _ptr(partial), _stream(x))
+    if not stats:
+        return out, None
+    return out, instnorm_finalize(partial, B * cout, parts, D * H * W)
+
+
+def conv3d_pointwise_upcat(a: torch.Tensor, u: torch.Tensor, w_t: torch.Tensor, cout: int):
+    """1x1x1 conv over cat(a, trilinear_up(u)) -> (out, (mean, rstd)); w_t [Ca+Cu][Cout]."""
+    _check(a, "a")
+    _check(u, "u")
+    B, Ca, D, H, W = a.shape
+    _, Cu, Du, Hu, Wu = u.shape
+    out = torch.empty((B, cout, D, H, W), device=a.device, dtype=torch.float32)
+    parts = conv3d_stat_parts(D, H, W)
+    partial = torch.empty((B * cout * parts * 2,), device=a.device, dtype=torch.float64)
+    N.call("sa_conv3d_pointwise_upcat", a.data_ptr(), Ca, u.data_ptr(), Cu, Du, Hu, Wu, B, D, H, W, w_t.data_ptr(),
+           cout, out.data_ptr(), partial.data_ptr(), _stream(a))
+    return out, instnorm_finalize(partial, B * cout, parts, D * H * W)
+
+
+def conv2d_small(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor], cout: int, ksize: int,
+                 relu: bool = True) -> torch.Tensor:
+    """Direct KxK conv (padding K//2) for few input channels; w_t pre-arranged [Cin][K][K][Cout]."""
+    bs = _plane_bs(x, "x")
+    B, Cin, H, W = x.shape
+    out = torch.empty((B, cout, H, W), device=x.device, dtype=torch.float32)
+    N.call("sa_conv2d_small", x.data_ptr(), bs, B, Cin, H, W, w_t.data_ptr(), _ptr(bias), cout, ksize,
+           1 if relu else 0, out.data_ptr(), cout * H * W, _stream(x))
+    return out
