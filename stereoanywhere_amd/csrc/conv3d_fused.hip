@@ -229,21 +229,35 @@ __global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__res
   block_stats<COUT>(s, q, red, partial, b, nparts, blk, COUT);
 }
 
-__global__ void instnorm_finalize_kernel(const double *__restrict__ partial, int bc_count, int nparts, double count,
-                                         float eps, float *__restrict__ mean, float *__restrict__ rstd) {
-  const int bc = blockIdx.x * blockDim.x + threadIdx.x;
-  if (bc >= bc_count) return;
+// one block per (b, c): fixed-shape tree reduction of the float64 partials (deterministic)
+__global__ __launch_bounds__(256) void instnorm_finalize_kernel(const double *__restrict__ partial, int nparts,
+                                                                double count, float eps, float *__restrict__ mean,
+                                                                float *__restrict__ rstd) {
+  __shared__ double rs[256], rq[256];
+  const int bc = blockIdx.x, t = threadIdx.x;
   const double *p = partial + (long)bc * nparts * 2;
   double s = 0.0, q = 0.0;
-  for (int i = 0; i < nparts; ++i) {
+  for (int i = t; i < nparts; i += 256) {
     s += p[2 * i];
     q += p[2 * i + 1];
   }
-  const double m = s / count;
-  double var = q / count - m * m;
-  if (var < 0.0) var = 0.0;
-  mean[bc] = (float)m;
-  rstd[bc] = (float)(1.0 / std::sqrt(var + (double)eps));
+  rs[t] = s;
+  rq[t] = q;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      rs[t] += rs[t + o];
+      rq[t] += rq[t + o];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double m = rs[0] / count;
+    double var = rq[0] / count - m * m;
+    if (var < 0.0) var = 0.0;
+    mean[bc] = (float)m;
+    rstd[bc] = (float)(1.0 / std::sqrt(var + (double)eps));
+  }
 }
 
 inline dim3 grid_of(int B, int D, int H, int W, int &tilesD) {
@@ -305,7 +319,6 @@ extern "C" int sa_instnorm_finalize(const double *partial, int bc_count, long np
              "sa_instnorm_finalize: bad arguments");
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_MISC, s);
-  instnorm_finalize_kernel<<<(bc_count + 63) / 64, 64, 0, s>>>(partial, bc_count, (int)nparts, (double)count, eps,
-                                                               mean, rstd);
+  instnorm_finalize_kernel<<<bc_count, 256, 0, s>>>(partial, (int)nparts, (double)count, eps, mean, rstd);
   return sa::check_launch("sa_instnorm_finalize");
 }

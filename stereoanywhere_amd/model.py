@@ -102,6 +102,11 @@ class StereoAnywhere(nn.Module):
                     cls_c=self.classifier_monoconf.weight.permute(0, 1, 4, 2, 3).contiguous(),
                     # convf1 [64,2,7,7] -> [ci][ky][kx][co] for sa_conv2d_small
                     f1=ub.encoder.convf1.weight.permute(1, 2, 3, 0).contiguous(),
+                    # encoder._conv has 126 outputs (update.py:78), which drops MIOpen off its
+                    # Winograd kernels; two zero filters make it 128 (only 0..125 are read)
+                    mot_w=torch.cat([ub.encoder._conv.weight,
+                                     ub.encoder._conv.weight.new_zeros((2,) + ub.encoder._conv.weight.shape[1:])]),
+                    mot_b=torch.cat([ub.encoder._conv.bias, ub.encoder._conv.bias.new_zeros(2)]),
                 )
                 hg = self.hourglass_mono
                 cls = torch.cat([self._derived["cls_d"], self._derived["cls_c"]], 0)  # [2,8,3,3,3]
@@ -259,8 +264,8 @@ class StereoAnywhere(nn.Module):
             c = F.relu(enc.convc2(c), inplace=True).view(B, 128, H4, W4)
             fl = ops.conv2d_small(flow, dw["f1"], enc.convf1.bias, 64, 7, relu=True)
             fl = F.relu(enc.convf2(fl), inplace=True)
-            mot = enc._conv(torch.cat([c, fl], 1))
-            ops.relu_copy(mot, x08[:, :126])
+            mot = F.conv2d(torch.cat([c, fl], 1), dw["mot_w"], dw["mot_b"], padding=1)
+            ops.relu_copy(mot[:, :126], x08[:, :126])
             ops.interp(h16, x08[:, 128:])
             gru(0, h08, x08, "08")
             delta = ub.flow_head.conv2(F.relu(ub.flow_head.conv1(h08), inplace=True))
