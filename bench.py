@@ -45,24 +45,44 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8 TB/s spec
 FP32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_*_f32 dense peak
 
 
-def algorithmic_cost(kernel: str, B: int, H4: int, W4: int, C: int = 256):
-    """(unit, amount per launch) of the minimal traffic / work of one launch at batch B."""
-    px = B * H4 * W4
-    vol = px * W4
-    lv = [W4, W4 // 2, W4 // 4, W4 // 8]
-    if kernel == "corr_volume_pyramid":  # fp32 MFMA-bound: 2*C flops per volume cell
-        return "TFLOP/s", 2.0 * vol * C
-    if kernel == "corr_lookup":  # 2 volumes x 4 levels x 10 cells read + 72 taps written + coords
-        return "GB/s", px * (2 * 4 * 10 * 4 + 72 * 4 + 4)
-    if kernel == "mono_masked_volume":  # 8-channel fp32 volume written; normals/maps read
-        return "GB/s", 8 * vol * 4 + px * 2 * 4 * 4
-    if kernel == "softargmin_conf":  # two volumes read once, four maps written
-        return "GB/s", 2 * vol * 4 + 4 * px * 4
-    if kernel == "gru_zr":  # per level: xc(2C) + hzr(2C) + cz,cr(2C) + h(C) read, z,rh(2C) written
-        return "GB/s", None
-    if kernel == "convex_upsample":
-        return "GB/s", px * (144 + 1) * 4 + px * 16 * 4
-    return "GB/s", None
+def step_costs(B: int, H4: int, W4: int, iters: int, C: int = 256):
+    """Algorithmic work of one forward step per hand-written kernel family:
+    {kernel: (unit, amount per step)} — minimal bytes each launch must move (HBM-bound
+    kernels) or flops it must do (compute-bound ones).  Derivations in DESIGN.md §4."""
+    px = B * H4 * W4                      # 1/4-res pixels
+    vol = px * W4                         # cost-volume cells
+    lv = [W4 >> i for i in range(4)]
+    gru_px = B * (H4 * W4 + ((H4 + 1) // 2) * ((W4 + 1) // 2) + ((H4 + 3) // 4) * ((W4 + 3) // 4))
+    hid = 128
+    return {
+        # fp32 MFMA: 2*C flops per volume cell (a1); epilogue work (trunc, pyramid) is free
+        "corr_volume_pyramid": ("TFLOP/s", 2.0 * vol * C),
+        # per pixel: 2 volumes x 4 levels x (2r+2) cells read, 72 taps written, coords read
+        "corr_lookup": ("GB/s", iters * px * (2 * 4 * 10 * 4 + 72 * 4 + 4)),
+        "mono_masked_volume": ("GB/s", 8 * vol * 4 + px * 2 * 4 * 4),
+        # two aggregated volumes read once, four maps written
+        "softargmin_conf": ("GB/s", 2 * vol * 4 + 4 * px * 4),
+        # three joint L/R maps read once
+        "weighted_lsq": ("GB/s", 3 * 2 * px * 4),
+        # per pixel and GRU level: xc(2C) + hzr(2C) + cz,cr(2C) + h(C) read, z, r*h (2C) written
+        "gru_zr": ("GB/s", iters * gru_px * 9 * hid * 4),
+        # xc_q, qh, cq, z, h read, h written
+        "gru_out": ("GB/s", iters * gru_px * 6 * hid * 4),
+        "convex_upsample": ("GB/s", px * (144 + 1) * 4 + px * 16 * 4),
+        # full-res hourglass tail: 1x1x1 24->8, 3x3x3 8->8 (x2), 3x3x3 8->2 (fp32 FMA)
+        "conv3d_fused": ("TFLOP/s", 2.0 * vol * (24 * 8 + 2 * 27 * 8 * 8 + 27 * 8 * 2)),
+    }
+
+
+def pmc_traffic(kernel: str, batch: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic_*.json, made by scripts/pmc_traffic.py on this bench config)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_b{batch}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        rec = json.load(f).get(kernel)
+    return None if rec is None else rec["hbm_bytes_per_launch"]
 
 
 def make_inputs(B, H, W, Hp, Wp, D, seed0, device):
@@ -127,8 +147,11 @@ def main():
     ap.add_argument("--width", type=int, default=960)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-epe", action="store_true")
+    ap.add_argument("--miopen-find", type=int, default=0,
+                    help="let MIOpen time its conv algorithms per shape (torch cudnn.benchmark)")
     args = ap.parse_args()
 
+    torch.backends.cudnn.benchmark = bool(args.miopen_find)
     r = D.init_from_env("nccl")
     device = torch.device("cuda", r.local_rank)
     torch.cuda.set_device(device)
@@ -171,22 +194,27 @@ def main():
     total_pairs = args.batch * r.world * args.steps
     if not r.is_main:
         return
-    # dominant hand-written kernel by summed time in the timed region
-    mine = {k: v for k, v in kt.items() if k != "misc" and v[1] > 0}
-    dom = max(mine, key=lambda k: mine[k][0])
-    ms_tot, n_launch = mine[dom]
-    avg_s = ms_tot / 1e3 / n_launch
-    unit, amount = algorithmic_cost(dom, hi - lo, H4, W4)
-    if unit == "TFLOP/s":
-        achieved = amount / avg_s / 1e12
-        peak, bound = FP32_MFMA_PEAK_TFS, "mfma"
-    else:
-        achieved = (amount / avg_s / 1e9) if amount else None
-        peak, bound = HBM_PEAK_GBS, "hbm"
-    roof = {"kernel": dom, "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
-            "frac": (achieved / peak) if achieved else None, "traffic": None,
-            "avg_launch_us": avg_s * 1e6, "launches": n_launch,
-            "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]}}
+    # every hand-written kernel family: algorithmic work / live event time vs MI355X peak
+    costs = step_costs(hi - lo, H4, W4, args.iters)
+    kernels = {}
+    for k, (ms_tot, n_launch) in kt.items():
+        if n_launch == 0 or k not in costs:
+            continue
+        unit, amount = costs[k]
+        secs = ms_tot / 1e3 / args.steps                      # per step
+        if unit == "TFLOP/s":
+            ach, peak, bound = amount / secs / 1e12, FP32_MFMA_PEAK_TFS, "mfma"
+        else:
+            ach, peak, bound = amount / secs / 1e9, HBM_PEAK_GBS, "hbm"
+        kernels[k] = {"bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
+                      "ms_per_step": ms_tot / args.steps, "launches_per_step": n_launch / args.steps,
+                      "avg_launch_us": ms_tot * 1e3 / n_launch}
+    dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
+    roof = dict(kernels[dom])
+    roof.update({"kernel": dom, "traffic": pmc_traffic(dom, args.batch), "kernels": kernels,
+                 "misc_ms_per_step": kt["misc"][0] / args.steps,
+                 "note": "achieved = algorithmic amount per launch / mean live HIP-event launch time; "
+                         "fp32 FMA peak 157.3 TF/s is the same for MFMA (v_mfma_f32_*_f32) and VALU"})
     res = {
         "metric": "stereo pairs/sec @540x960 D=192 (1/2/4/8 GPU) + EPE vs reference",
         "value": total_pairs / elapsed, "unit": "pairs/s", "n_gpus": r.world, "steps": args.steps,

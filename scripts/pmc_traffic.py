@@ -1,0 +1,48 @@
+"""Per-launch HBM traffic of each hand-written kernel family from two rocprofv3 --pmc
+passes (FETCH_SIZE and WRITE_SIZE, separate runs as MI355X_MICROARCH.md §HBM prescribes).
+
+FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reports half the bytes of a
+wide coalesced stream, so reads are doubled (the guide's correction; it is exact only for
+16-B-per-lane streams, and an upper bound for narrower access).
+usage: python scripts/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> out.json
+"""
+import collections
+import csv
+import json
+import sys
+
+FAMILIES = {
+    "conv3d_k3_kernel": "conv3d_fused", "pointwise_upcat_kernel": "conv3d_fused", "lookup_kernel": "corr_lookup",
+    "corr_pyramid_kernel": "corr_volume_pyramid", "masked_volume_kernel": "mono_masked_volume",
+    "sam_contig_kernel": "softargmin_conf", "sam_strided_kernel": "softargmin_conf", "lsq_kernel": "weighted_lsq",
+    "gru_zr_kernel": "gru_zr", "gru_out_kernel": "gru_out", "convex_up_kernel": "convex_upsample",
+}
+
+
+def family(name):
+    for k, v in FAMILIES.items():
+        if k in name:
+            return v
+    return None
+
+
+def per_launch(path, counter):
+    tot = collections.defaultdict(float)
+    n = collections.defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        if r.get("Counter_Name") != counter:
+            continue
+        f = family(r["Kernel_Name"])
+        if f:
+            tot[f] += float(r["Counter_Value"])
+            n[f].add(r["Dispatch_Id"])
+    return {f: tot[f] * 1024.0 / len(n[f]) for f in tot}
+
+
+if __name__ == "__main__":
+    fetch = per_launch(sys.argv[1], "FETCH_SIZE")
+    write = per_launch(sys.argv[2], "WRITE_SIZE")
+    out = {f: {"fetch_bytes_raw": fetch.get(f), "write_bytes": write.get(f),
+               "hbm_bytes_per_launch": 2.0 * fetch.get(f, 0.0) + write.get(f, 0.0)} for f in set(fetch) | set(write)}
+    json.dump(out, open(sys.argv[3], "w"), indent=1, sort_keys=True)
+    print(json.dumps(out, indent=1, sort_keys=True))

@@ -5,10 +5,12 @@ import csv
 import sys
 
 path = sys.argv[1]
+which = int(sys.argv[3]) if len(sys.argv) > 3 else -1  # which forward (by convex-upsample launch)
 rows = list(csv.DictReader(open(path)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ups = [i for i, r in enumerate(rows) if "convex_up" in r["Kernel_Name"]]
-fw = rows[ups[-2] + 1:ups[-1] + 1]
+ends = [-1] + ups
+fw = rows[ends[which - 1 if which < 0 else which] + 1:ends[which] + 1] if which != 0 else rows[:ups[0] + 1]
 
 
 def dur(r):

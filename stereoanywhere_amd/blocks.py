@@ -184,7 +184,9 @@ class Hourglass(nn.Module):
         ns = self.number_of_scales
         orig = x
         downs = []
-        for i in range(ns - 1):
+        # only downsampled_features[0 .. ns-3] feed the live up-path step (class docstring):
+        # the deepest down layer and its feature attention are dead code in the reference
+        for i in range(ns - 2):
             x = self.down_layers[i](x)
             x = self.feature_atts[i](x, features_left[i + 1], features_right[i + 1])
             downs.append(x)
