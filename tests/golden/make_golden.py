@@ -292,6 +292,43 @@ def micro_cases(ut, corr_mod):
     return {k: _np(v) for k, v in out.items()}
 
 
+def tiler_cases():
+    """The reference tiler (mapreduce_v2/tile_wrapper.py) on a deterministic mock model:
+    tile enumeration (incl. duplicate tiles), blend weights and the stitched output."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_tile_wrapper", os.path.join(REF, "mapreduce_v2", "tile_wrapper.py"))
+    tw = importlib.util.module_from_spec(spec)
+    sys.modules["ref_tile_wrapper"] = tw  # dataclasses resolve their module by name
+    spec.loader.exec_module(tw)
+
+    class Mock(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.p = torch.nn.Parameter(torch.zeros(1))
+
+        def forward(self, l, r, ml, mr, iters=1, test_mode=True):
+            H, W = l.shape[-2:]
+            ramp = torch.arange(W, dtype=torch.float32).view(1, 1, 1, W) / W
+            return -(2 * l[:, :1] - r[:, 1:2] + ml * 3 + ramp + H / 100.0), None
+
+    out = {}
+    g = torch.Generator().manual_seed(3)
+    for i, (H, W, th, tw_, ov) in enumerate([(100, 150, 96, 64, 32), (128, 128, 128, 64, 32), (200, 130, 128, 96, 64),
+                                             (96, 96, 128, 128, 32)]):
+        l, r = torch.rand(1, 3, H, W, generator=g), torch.rand(1, 3, H, W, generator=g)
+        ml, mr = torch.rand(1, 1, H, W, generator=g), torch.rand(1, 1, H, W, generator=g)
+        wrap = tw.TileWrapper(Mock(), tile_width=tw_, tile_height=th, overlap=ov)
+        tiles = wrap._enumerate_tiles(H, W)
+        with torch.no_grad():
+            st = wrap(l, r, ml, mr, iters=1, test_mode=True)
+        out[f"case{i}.geom"] = np.array([H, W, th, tw_, ov])
+        out[f"case{i}.tiles"] = np.array([[t.y_start, t.y_end, t.x_start, t.x_end] for t in tiles])
+        out[f"case{i}.weight"] = _np(tw._make_blend_weight(th, tw_, torch.device("cpu")))
+        for k, v in (("l", l), ("r", r), ("ml", ml), ("mr", mr), ("out", st)):
+            out[f"case{i}.{k}"] = _np(v)
+    return out
+
+
 def _dedupe(rec):
     """Store byte-identical captures once; ``alias.<key>`` names the kept copy."""
     seen, out = {}, {}
@@ -315,6 +352,7 @@ def main():
         json.dump(keys, f, indent=0, sort_keys=True)
 
     np.savez_compressed(os.path.join(HERE, "micro_ops.npz"), **micro_cases(ut, corr_mod))
+    np.savez_compressed(os.path.join(HERE, "tiler.npz"), **tiler_cases())
 
     # tiny end-to-end case with every intermediate
     pair = synth.synthetic_batch(1, 64, 128, 24.0, seed0=1)
