@@ -18,7 +18,8 @@ Hot path, one kernel family per row:
   a12    GRU gates fused; convs split by input so no torch.cat          sa_gru_zr / sa_gru_out
   a14    convex upsampling of the final flow                            sa_convex_upsample
 Training (test_mode=False), vol_downsample > 0 and use_aggregate_stereo_vol are outside
-this tier and raise NotImplementedError.
+this tier and raise NotImplementedError.  use_truncate_vol / use_aggregate_mono_vol may be
+off (the reference CLI's store_true defaults, test.py:94-98).
 """
 from __future__ import annotations
 
@@ -213,7 +214,8 @@ class StereoAnywhere(nn.Module):
         if a.use_aggregate_mono_vol:
             mono_rows = vol_d.permute(0, 1, 3, 4, 2).contiguous()  # [B,1,H,W1,W2]
         else:
-            raise NotImplementedError("use_aggregate_mono_vol=False is not built in this tier")
+            # raw mono volume 1.73 * corr(normals) (stereoanywhere.py:136, 210)
+            mono_rows = 1.73 * ops.corr_volume(n2, n3)
         mono_blk = HipCorrBlock1D(None, a.corr_levels, a.corr_radius,
                                   _pyramid=ops.pyramid_from_volume(mono_rows, a.corr_levels),
                                   _shape=(B, H4, W4, W4))

@@ -329,6 +329,31 @@ def tiler_cases():
     return out
 
 
+def metrics_cases():
+    """losses.guided_metrics (losses.py:273-342) on random disparities with occlusion masks,
+    including the all-zero-occlusion branch."""
+    tvf = types.ModuleType("torchvision.transforms.functional")
+    tvf.gaussian_blur = None
+    sys.modules.setdefault("torchvision.transforms", types.ModuleType("torchvision.transforms"))
+    sys.modules["torchvision.transforms.functional"] = tvf
+    import importlib
+    losses = importlib.import_module("losses")
+    rng = np.random.default_rng(4)
+    out = {}
+    for i, occ in enumerate([True, False]):
+        gt = (rng.random((1, 1, 40, 60)) * 50).astype(np.float32)
+        disp = gt + rng.standard_normal(gt.shape).astype(np.float32) * 3
+        valid = (rng.random(gt.shape) > 0.2).astype(np.uint8)
+        maskocc = (rng.random(gt.shape) > 0.7).astype(np.uint8) if occ else np.zeros(gt.shape, np.uint8)
+        res = losses.guided_metrics(disp, gt, valid, maskocc)
+        keys = sorted(k for k in res if k != "errormap")
+        out[f"case{i}.disp"], out[f"case{i}.gt"], out[f"case{i}.valid"], out[f"case{i}.occ"] = disp, gt, valid, maskocc
+        out[f"case{i}.keys"] = np.array(keys)
+        out[f"case{i}.values"] = np.array([float(res[k]) for k in keys], dtype=np.float64)
+        out[f"case{i}.errormap"] = res["errormap"].astype(np.float32)
+    return out
+
+
 def _dedupe(rec):
     """Store byte-identical captures once; ``alias.<key>`` names the kept copy."""
     seen, out = {}, {}
@@ -353,6 +378,7 @@ def main():
 
     np.savez_compressed(os.path.join(HERE, "micro_ops.npz"), **micro_cases(ut, corr_mod))
     np.savez_compressed(os.path.join(HERE, "tiler.npz"), **tiler_cases())
+    np.savez_compressed(os.path.join(HERE, "metrics.npz"), **metrics_cases())
 
     # tiny end-to-end case with every intermediate
     pair = synth.synthetic_batch(1, 64, 128, 24.0, seed0=1)
