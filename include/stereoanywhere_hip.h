@@ -157,24 +157,30 @@ int sa_flow_update(float *coords_x, const float *delta, long delta_bs, int B, in
 int sa_convex_upsample(const float *flow, const float *mask, long mask_bs, int B, int H, int W,
                        int factor, float *out, void *stream);
 
-/* Hourglass full-resolution tail (hourglass.py:325-329, submodule.py:25-53, 113-140,
- * stereoanywhere.py:165-166) as fused direct 3-D convolutions on [B, C, D, H, W]
- * volumes (D = W2, W = W1), 3x3x3 / stride 1 / pad 1 / no bias:
+/* Mono hourglass (hourglass.py:13-91, submodule.py:25-53, 113-140) and its classifiers
+ * (stereoanywhere.py:165-166) as fused direct 3-D convolutions on [B, C, D, H, W] volumes
+ * (D = W2, W = W1), 3x3x3 / pad 1 / no bias, stride 1 or 2:
  *   out = conv(T(in)),  T(x) = [gate_l[b,c,h,w] * gate_r[b,c,h,d] *] [lrelu(] [(x - mean[b,c]) *
  *   rstd[b,c]] [)] — the previous layer's InstanceNorm3d + LeakyReLU (+ DoubleFeatureAtt
- *   gate) applied while the input is staged.  stats_partial (may be NULL): per-block
- *   float64 (sum, sum^2) of every output channel, [B*Cout][parts][2] with
- *   parts = sa_conv3d_stat_parts(D, H, W); reduce with sa_instnorm_finalize.
- * Built for Cin = 8 -> Cout = 8 (final_agg) or 2 (both classifiers in one launch). */
-long sa_conv3d_stat_parts(int D, int H, int W);
-int sa_conv3d_k3(const float *in, int B, int Cin, int D, int H, int W, const float *weight,
-                 int Cout, const float *in_mean, const float *in_rstd, int act, float slope,
-                 const float *gate_l, const float *gate_r, float *out, double *stats_partial,
-                 void *stream);
-/* 1x1x1 conv over cat(a, trilinear_up(u)) (hourglass.py:326-328 + final_agg.0): a [B,8,D,H,W],
- * u [B,16,Du,Hu,Wu] upsampled with align_corners=True on the fly; weight [Cout, 24]. */
-int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *u, int Cu, int Du, int Hu,
-                              int Wu, int B, int D, int H, int W, const float *weight, int Cout,
+ *   gate, maps at the INPUT resolution) applied while the input is staged.
+ *   stats_partial (may be NULL): per-block float64 (sum, sum^2) of every output channel,
+ *   [B*Cout][parts][2] with parts = sa_conv3d_stat_parts(Cout, stride, Do, Ho, Wo);
+ *   reduce with sa_instnorm_finalize.  Output size (n - 1) / stride + 1 per axis.
+ * Built for (Cin, Cout, stride) in {(8,8,1), (8,2,1), (16,16,1), (32,32,1), (8,16,2), (16,32,2)}. */
+long sa_conv3d_stat_parts(int Cout, int stride, int Do, int Ho, int Wo);
+int sa_conv3d(const float *in, int B, int Cin, int Di, int Hi, int Wi, int stride,
+              const float *weight, int Cout, const float *in_mean, const float *in_rstd, int act,
+              float slope, const float *gate_l, const float *gate_r, float *out,
+              double *stats_partial, void *stream);
+/* 1x1x1 conv over cat(Ta(a), trilinear_up(Tu(u))) (hourglass.py:319-321, 326-328):
+ * a [B,Ca,D,H,W], u [B,Cu,Du,Hu,Wu] upsampled with align_corners=True on the fly, each
+ * corner transformed before interpolation; T as above (pass NULLs for identity); weight
+ * pre-arranged [Ca+Cu][Cout] with the a-rows first.  Built for (8,16->8) and (16,32->16). */
+int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_mean, const float *a_rstd,
+                              int a_act, const float *a_gl, const float *a_gr, const float *u,
+                              int Cu, const float *u_mean, const float *u_rstd, int u_act,
+                              const float *u_gl, const float *u_gr, int Du, int Hu, int Wu, int B,
+                              int D, int H, int W, float slope, const float *weight, int Cout,
                               float *out, double *stats_partial, void *stream);
 /* mean/rstd of each of bc_count channels from the partials (count voxels each, biased
  * variance, rstd = 1/sqrt(var + eps)) — InstanceNorm3d statistics (affine=False). */

@@ -178,10 +178,12 @@ class Hourglass(nn.Module):
         self.number_of_scales = ns
 
     def forward(self, x, features_left, features_right, fused=None):
-        """``fused``: dict of pre-arranged weights (model._weights) to run the full-resolution
-        tail through the fused HIP convolutions; returns (vol_disp, vol_conf) of the two
-        classifiers then (see _fused_tail).  Without it: the plain torch/MIOpen tail."""
+        """``fused``: pre-arranged weights (StereoAnywhere._weights()["hg"]) to run the whole
+        hourglass plus both classifiers through the fused HIP convolutions (see
+        _forward_fused); returns (vol_disp, vol_conf) then.  Without it: torch/MIOpen."""
         ns = self.number_of_scales
+        if fused is not None:
+            return self._forward_fused(x, features_left, features_right, fused)
         orig = x
         downs = []
         # only downsampled_features[0 .. ns-3] feed the live up-path step (class docstring):
@@ -196,27 +198,78 @@ class Hourglass(nn.Module):
                            align_corners=True)
         x = self.agg_layers[i](torch.cat((up, downs[ns - 3 - i]), 1))
         x = self.feature_atts_up[i](x, features_left[ns - 2 - i], features_right[ns - 2 - i])
-        if fused is not None:
-            return self._fused_tail(orig, x, features_left[0], features_right[0], fused)
         up = F.interpolate(x, size=orig.shape[2:], mode="trilinear", align_corners=True)
         x = self.final_agg(torch.cat((orig, up), 1))
         return self.final_feature_atts_up(x, features_left[0], features_right[0])
 
-    def _fused_tail(self, orig, x, feat_left, feat_right, fw):
-        """hourglass.py:325-329 + classifiers (stereoanywhere.py:165-166) at full volume
-        resolution in four HIP launches (csrc/conv3d_fused.hip): each conv applies the
-        previous InstanceNorm3d + LeakyReLU on load; the DoubleFeatureAtt gate is applied
-        on load of the classifier conv, whose two outputs are computed together."""
+    @staticmethod
+    def _gate(att, feat_left, feat_right, vol_shape):
+        """sigmoid'ed DoubleFeatureAtt maps [B,C,H,W1] and [B,C,H,W2] for a volume
+        [B,C,W2,H,W1] of the same resolution (no resize needed), else None."""
+        gl = torch.sigmoid(att.feat_att_left(feat_left)).contiguous()
+        gr = torch.sigmoid(att.feat_att_right(feat_right)).contiguous()
+        D, H, W = vol_shape[2:]
+        if tuple(gl.shape[2:]) != (H, W) or tuple(gr.shape[2:]) != (H, D):
+            return None
+        return gl, gr
+
+    def fusable(self, x, features_left) -> bool:
+        """The fused path needs the published geometry (8 channels, 4 scales) and volume
+        sizes that halve exactly onto the feature pyramids (H, W multiples of 32)."""
+        if self.number_of_scales != 4 or x.shape[1] != 8 or self.final_agg[2].conv.out_channels != 8:
+            return False
+        D, H, W = x.shape[2:]
+        return all(n % 4 == 0 for n in (D, H, W)) and tuple(features_left[0].shape[2:]) == (H, W)
+
+    def _forward_fused(self, masked, fl, fr, fw):
+        """hourglass.py:61-91 (live part) + classifiers as 12 fused HIP launches
+        (csrc/conv3d_fused.hip).  Every activation is kept raw; the consumer applies
+        InstanceNorm3d + LeakyReLU (+ DoubleFeatureAtt gate) while loading it, so no
+        normalised / gated / upsampled / concatenated volume is ever written."""
         from . import ops
-        att = self.final_feature_atts_up
-        gl = torch.sigmoid(att.feat_att_left(feat_left)).contiguous()    # [B,C,H,W1]
-        gr = torch.sigmoid(att.feat_att_right(feat_right)).contiguous()  # [B,C,H,W2]
         slope = self.final_agg[0].act_fn.negative_slope
-        t, st = ops.conv3d_pointwise_upcat(orig.contiguous(), x.contiguous(), fw["fa0"], fw["fa0"].shape[1])
-        t, st = ops.conv3d_k3(t, fw["fa1"], fw["fa1"].shape[2], norm=st, act=True, slope=slope, stats=True)
-        t, st = ops.conv3d_k3(t, fw["fa2"], fw["fa2"].shape[2], norm=st, act=True, slope=slope, stats=True)
-        vol, _ = ops.conv3d_k3(t, fw["cls"], 2, norm=st, act=True, slope=slope, gate=(gl, gr))
+
+        def gated(v, att, i):
+            g = self._gate(att, fl[i], fr[i], v.raw.shape)
+            if g is None:
+                raise RuntimeError("fused hourglass: feature pyramid does not match the volume")
+            return v.with_gate(g)
+        orig = ops.VolAct(masked)
+        r = ops.conv3d(orig, fw["d00"], 16, stride=2, slope=slope)                  # down_layers[0][0]
+        r = ops.conv3d(r, fw["d01"], 16, slope=slope)                               # down_layers[0][1]
+        down0 = gated(r, self.feature_atts[0], 1)
+        r = ops.conv3d(down0, fw["d10"], 32, stride=2, slope=slope)                 # down_layers[1][0]
+        r = ops.conv3d(r, fw["d11"], 32, slope=slope)                               # down_layers[1][1]
+        down1 = gated(r, self.feature_atts[1], 2)
+        r = ops.conv3d_pointwise_upcat(down0, down1, fw["a10"], 16, slope=slope)    # agg_layers[1][0]
+        r = ops.conv3d(r, fw["a11"], 16, slope=slope)                               # agg_layers[1][1]
+        r = ops.conv3d(r, fw["a12"], 16, slope=slope)                               # agg_layers[1][2]
+        x = gated(r, self.feature_atts_up[1], 1)
+        r = ops.conv3d_pointwise_upcat(orig, x, fw["fa0"], 8, slope=slope)          # final_agg[0]
+        r = ops.conv3d(r, fw["fa1"], 8, slope=slope)                                # final_agg[1]
+        r = ops.conv3d(r, fw["fa2"], 8, slope=slope)                                # final_agg[2]
+        r = gated(r, self.final_feature_atts_up, 0)
+        vol = ops.conv3d(r, fw["cls"], 2, slope=slope, stats=False).raw             # both classifiers
         return vol[:, 0:1], vol[:, 1:2]
+
+    def fused_weights(self, classifiers):
+        """[ci][27][co] / [cin][co] arrangements of every conv used by _forward_fused;
+        ``classifiers``: [2, 8, 3, 3, 3] kernels already in the (W2, H, W1) layout."""
+        def k3(w):
+            return w.reshape(w.shape[0], w.shape[1], 27).permute(1, 2, 0).contiguous()
+
+        def pw(w, a_cols, u_cols):  # rows: a-part first, then the upsampled part
+            w = w.reshape(w.shape[0], w.shape[1])
+            return torch.cat([w[:, a_cols].t(), w[:, u_cols].t()], 0).contiguous()
+        a10 = self.agg_layers[1][0].conv.weight  # input cat(up(down1) [32], down0 [16])
+        fa0 = self.final_agg[0].conv.weight      # input cat(orig [8], up(x) [16])
+        return dict(
+            d00=k3(self.down_layers[0][0].conv.weight), d01=k3(self.down_layers[0][1].conv.weight),
+            d10=k3(self.down_layers[1][0].conv.weight), d11=k3(self.down_layers[1][1].conv.weight),
+            a10=pw(a10, slice(32, 48), slice(0, 32)),
+            a11=k3(self.agg_layers[1][1].conv.weight), a12=k3(self.agg_layers[1][2].conv.weight),
+            fa0=pw(fa0, slice(0, 8), slice(8, 24)),
+            fa1=k3(self.final_agg[1].conv.weight), fa2=k3(self.final_agg[2].conv.weight), cls=k3(classifiers))
 
 
 class ConvGRU(nn.Module):

@@ -25,11 +25,12 @@
 
 namespace {
 
-constexpr int TW = 64;  // tile along W (one wave row)
-constexpr int TH = 4;   // tile along H (4 waves)
+// Output tiles: 256 threads = TW (along W) x TH (along H); each thread owns TD planes
+// along D.  Stride-1 tiles are one wave wide (TW 64); stride-2 tiles are 32 x 8 so the
+// (2*T+1)-wide input halo stays small.
+constexpr int TW = 64;  // default tile (stride 1) along W
+constexpr int TH = 4;   // along H
 constexpr int TD = 4;   // output planes per thread along D
-constexpr int LW = TW + 2, LH = TH + 2, LD = TD + 2;
-constexpr int LPLANE = LD * LH * LW;  // floats per input channel in LDS
 
 struct InXform {
   const float *mean, *rstd;   // per (b, ci), or null
@@ -80,21 +81,25 @@ __device__ __forceinline__ void block_stats(const double (&s)[NC], const double 
   }
 }
 
-// 3x3x3, stride 1, padding 1, no bias; CIN input channels, COUT outputs.
-template <int CIN, int COUT>
-__global__ __launch_bounds__(256) void conv3d_k3_kernel(const float *__restrict__ in, int D, int H, int W,
-                                                        const float *__restrict__ wt, InXform tx,
-                                                        float *__restrict__ out, double *__restrict__ partial,
-                                                        int tilesD) {
+// 3x3x3, stride S, padding 1, no bias; CIN input channels, COUT outputs.
+template <int CIN, int COUT, int S, int TDx, int TWx, int THx>
+__global__ __launch_bounds__(256) void conv3d_kernel(const float *__restrict__ in, int Di, int Hi, int Wi, int Do,
+                                                     int Ho, int Wo, const float *__restrict__ wt, InXform tx,
+                                                     float *__restrict__ out, double *__restrict__ partial,
+                                                     int tilesD) {
+  static_assert(TWx * THx == 256, "256 threads per block");
+  constexpr int LW = (TWx - 1) * S + 3, LH = (THx - 1) * S + 3, LD = (TDx - 1) * S + 3;
+  constexpr int LPLANE = LD * LH * LW;
   __shared__ float tile[2][LPLANE];
   __shared__ double red[COUT * 4 * 2];
-  const int tx_ = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int w0 = blockIdx.x * TW, h0 = blockIdx.y * TH;
-  const int b = blockIdx.z / tilesD, d0 = (blockIdx.z % tilesD) * TD;
-  const long vol = (long)D * H * W;
-  float acc[TD][COUT];
+  const int tx_ = threadIdx.x % TWx, ty = threadIdx.x / TWx;
+  const int w0 = blockIdx.x * TWx, h0 = blockIdx.y * THx;
+  const int b = blockIdx.z / tilesD, d0 = (blockIdx.z % tilesD) * TDx;
+  const long vol = (long)Di * Hi * Wi;
+  const int iw0 = w0 * S - 1, ih0 = h0 * S - 1, id0 = d0 * S - 1;
+  float acc[TDx][COUT];
 #pragma unroll
-  for (int i = 0; i < TD; ++i)
+  for (int i = 0; i < TDx; ++i)
 #pragma unroll
     for (int c = 0; c < COUT; ++c) acc[i][c] = 0.f;
 
@@ -103,10 +108,10 @@ __global__ __launch_bounds__(256) void conv3d_k3_kernel(const float *__restrict_
     const float *src = in + bc * vol;
     for (int i = threadIdx.x; i < LPLANE; i += 256) {
       const int ww = i % LW, r = i / LW, hh = r % LH, dd = r / LH;
-      const int w = w0 - 1 + ww, h = h0 - 1 + hh, d = d0 - 1 + dd;
+      const int w = iw0 + ww, h = ih0 + hh, d = id0 + dd;
       float v = 0.0f;
-      if (w >= 0 && w < W && h >= 0 && h < H && d >= 0 && d < D)
-        v = xform(src[((long)d * H + h) * W + w], tx, bc, d, h, w, H, W, D);
+      if (w >= 0 && w < Wi && h >= 0 && h < Hi && d >= 0 && d < Di)
+        v = xform(src[((long)d * Hi + h) * Wi + w], tx, bc, d, h, w, Hi, Wi, Di);
       tile[buf][i] = v;
     }
   };
@@ -117,7 +122,7 @@ __global__ __launch_bounds__(256) void conv3d_k3_kernel(const float *__restrict_
   for (int ci = 0; ci < CIN; ++ci) {
     const int buf = ci & 1;
     if (ci + 1 < CIN) stage(ci + 1, buf ^ 1);
-    const float *tb = tile[buf] + ty * LW + tx_;
+    const float *tb = tile[buf] + (ty * S) * LW + tx_ * S;
     const float *wc = wt + (long)ci * 27 * COUT;  // weights pre-arranged [ci][tap][co]
 #pragma unroll 1
     for (int kd = 0; kd < 3; ++kd) {
@@ -126,15 +131,15 @@ __global__ __launch_bounds__(256) void conv3d_k3_kernel(const float *__restrict_
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
           const float *tp = tb + (kd * LH + kh) * LW + kw;
-          float v[TD];
+          float v[TDx];
 #pragma unroll
-          for (int od = 0; od < TD; ++od) v[od] = tp[od * LH * LW];
+          for (int od = 0; od < TDx; ++od) v[od] = tp[od * S * LH * LW];
           const float *wp = wc + ((kd * 3 + kh) * 3 + kw) * COUT;
 #pragma unroll
           for (int co = 0; co < COUT; ++co) {
             const float wv = wp[co];
 #pragma unroll
-            for (int od = 0; od < TD; ++od) acc[od][co] += wv * v[od];
+            for (int od = 0; od < TDx; ++od) acc[od][co] += wv * v[od];
           }
         }
     }
@@ -145,14 +150,14 @@ __global__ __launch_bounds__(256) void conv3d_k3_kernel(const float *__restrict_
   double s[COUT], q[COUT];
 #pragma unroll
   for (int c = 0; c < COUT; ++c) s[c] = q[c] = 0.0;
-  if (w < W && h < H) {
+  if (w < Wo && h < Ho) {
 #pragma unroll
-    for (int od = 0; od < TD; ++od) {
+    for (int od = 0; od < TDx; ++od) {
       const int d = d0 + od;
-      if (d < D) {
+      if (d < Do) {
 #pragma unroll
         for (int co = 0; co < COUT; ++co) {
-          out[(((long)b * COUT + co) * D + d) * (long)H * W + (long)h * W + w] = acc[od][co];
+          out[(((long)b * COUT + co) * Do + d) * (long)Ho * Wo + (long)h * Wo + w] = acc[od][co];
           s[co] += (double)acc[od][co];
           q[co] += (double)acc[od][co] * acc[od][co];
         }
@@ -166,11 +171,14 @@ __global__ __launch_bounds__(256) void conv3d_k3_kernel(const float *__restrict_
   }
 }
 
-// 1x1x1 conv over cat(a, trilinear_up(u)) -> COUT channels, + IN partial statistics.
+// 1x1x1 conv over cat(Ta(a), trilinear_up(Tu(u))) -> COUT channels, + IN partial
+// statistics.  Tu (norm / LeakyReLU / gate of the low-resolution branch) is applied to each
+// of the 8 corners before interpolating, i.e. exactly upsample(T(u)).
 template <int CA, int CU, int COUT>
-__global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__restrict__ a, const float *__restrict__ u,
-                                                              int D, int H, int W, int Du, int Hu, int Wu, float sd,
-                                                              float sh, float sw, const float *__restrict__ wt,
+__global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__restrict__ a, InXform ta,
+                                                              const float *__restrict__ u, InXform tu, int D, int H,
+                                                              int W, int Du, int Hu, int Wu, float sd, float sh,
+                                                              float sw, const float *__restrict__ wt,
                                                               float *__restrict__ out, double *__restrict__ partial,
                                                               int tilesD) {
   __shared__ double red[COUT * 4 * 2];
@@ -198,21 +206,26 @@ __global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__res
       float r[COUT];
 #pragma unroll
       for (int co = 0; co < COUT; ++co) r[co] = 0.0f;
-      // weights pre-arranged [cin][co]; cat order (a, up(u)) as hourglass.py:327
+      // weights pre-arranged [cin][co] with the a-rows first
 #pragma unroll 1
       for (int c = 0; c < CA; ++c) {
-        const float xv = a[((long)b * CA + c) * vol + pos];
+        const long bc = (long)b * CA + c;
+        const float xv = xform(a[bc * vol + pos], ta, bc, d, h, w, H, W, D);
 #pragma unroll
         for (int co = 0; co < COUT; ++co) r[co] += wt[c * COUT + co] * xv;
       }
+      const int hb = h1 + h1p, wb = w1 + w1p, db = d1 + d1p;
       const long o000 = ((long)d1 * Hu + h1) * Wu + w1;
       const long od_ = (long)d1p * Hu * Wu, oh_ = (long)h1p * Wu, ow_ = w1p;
 #pragma unroll 1
       for (int c = 0; c < CU; ++c) {
-        const float *p = u + ((long)b * CU + c) * volu + o000;
-        const float xv = dl0 * (hl0 * (wl0 * p[0] + wl1 * p[ow_]) + hl1 * (wl0 * p[oh_] + wl1 * p[oh_ + ow_])) +
-                         dl1 * (hl0 * (wl0 * p[od_] + wl1 * p[od_ + ow_]) +
-                                hl1 * (wl0 * p[od_ + oh_] + wl1 * p[od_ + oh_ + ow_]));
+        const long bc = (long)b * CU + c;
+        const float *p = u + bc * volu + o000;
+        auto X = [&](long off, int dd, int hh, int ww) { return xform(p[off], tu, bc, dd, hh, ww, Hu, Wu, Du); };
+        const float xv = dl0 * (hl0 * (wl0 * X(0, d1, h1, w1) + wl1 * X(ow_, d1, h1, wb)) +
+                                hl1 * (wl0 * X(oh_, d1, hb, w1) + wl1 * X(oh_ + ow_, d1, hb, wb))) +
+                         dl1 * (hl0 * (wl0 * X(od_, db, h1, w1) + wl1 * X(od_ + ow_, db, h1, wb)) +
+                                hl1 * (wl0 * X(od_ + oh_, db, hb, w1) + wl1 * X(od_ + oh_ + ow_, db, hb, wb)));
 #pragma unroll
         for (int co = 0; co < COUT; ++co) r[co] += wt[(CA + c) * COUT + co] * xv;
       }
@@ -260,56 +273,89 @@ __global__ __launch_bounds__(256) void instnorm_finalize_kernel(const double *__
   }
 }
 
-inline dim3 grid_of(int B, int D, int H, int W, int &tilesD) {
-  tilesD = (D + TD - 1) / TD;
-  return dim3((W + TW - 1) / TW, (H + TH - 1) / TH, tilesD * B);
+struct ConvGeo {
+  int td, tw, th;
+};
+
+inline ConvGeo conv_geo(int cout, int stride) {
+  if (stride == 2) return {2, 32, 8};
+  return {cout >= 32 ? 2 : 4, 64, 4};
 }
+
+inline dim3 conv_grid(int B, int Do, int Ho, int Wo, ConvGeo g, int &tilesD) {
+  tilesD = (Do + g.td - 1) / g.td;
+  return dim3((Wo + g.tw - 1) / g.tw, (Ho + g.th - 1) / g.th, tilesD * B);
+}
+
+inline int out_size(int n, int stride) { return (n - 1) / stride + 1; }  // k3, pad 1
 
 }  // namespace
 
-extern "C" long sa_conv3d_stat_parts(int D, int H, int W) {
+extern "C" long sa_conv3d_stat_parts(int Cout, int stride, int Do, int Ho, int Wo) {
   int tilesD;
-  dim3 g = grid_of(1, D, H, W, tilesD);
+  dim3 g = conv_grid(1, Do, Ho, Wo, conv_geo(Cout, stride), tilesD);
   return (long)g.x * g.y * g.z;
 }
 
-extern "C" int sa_conv3d_k3(const float *in, int B, int Cin, int D, int H, int W, const float *weight, int Cout,
-                            const float *in_mean, const float *in_rstd, int act, float slope, const float *gate_l,
-                            const float *gate_r, float *out, double *stats_partial, void *stream) {
-  SA_REQUIRE(in && weight && out, "sa_conv3d_k3: null pointer");
-  SA_REQUIRE(B > 0 && D > 0 && H > 0 && W > 0, "sa_conv3d_k3: empty shape");
-  SA_REQUIRE(Cin == 8 && (Cout == 8 || Cout == 2), "sa_conv3d_k3: built for Cin 8 -> Cout 8 or 2 (got %d -> %d)",
-             Cin, Cout);
-  SA_REQUIRE((in_mean == nullptr) == (in_rstd == nullptr), "sa_conv3d_k3: mean and rstd go together");
-  SA_REQUIRE((gate_l == nullptr) == (gate_r == nullptr), "sa_conv3d_k3: both gate maps or none");
+extern "C" int sa_conv3d(const float *in, int B, int Cin, int Di, int Hi, int Wi, int stride, const float *weight,
+                         int Cout, const float *in_mean, const float *in_rstd, int act, float slope,
+                         const float *gate_l, const float *gate_r, float *out, double *stats_partial, void *stream) {
+  SA_REQUIRE(in && weight && out, "sa_conv3d: null pointer");
+  SA_REQUIRE(B > 0 && Di > 0 && Hi > 0 && Wi > 0, "sa_conv3d: empty shape");
+  SA_REQUIRE((in_mean == nullptr) == (in_rstd == nullptr), "sa_conv3d: mean and rstd go together");
+  SA_REQUIRE((gate_l == nullptr) == (gate_r == nullptr), "sa_conv3d: both gate maps or none");
+  const int Do = out_size(Di, stride), Ho = out_size(Hi, stride), Wo = out_size(Wi, stride);
+  const ConvGeo geo = conv_geo(Cout, stride);
   int tilesD;
-  dim3 grid = grid_of(B, D, H, W, tilesD);
+  dim3 grid = conv_grid(B, Do, Ho, Wo, geo, tilesD);
   InXform tx{in_mean, in_rstd, gate_l, gate_r, slope, act};
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV3D, s);
-  if (Cout == 8)
-    conv3d_k3_kernel<8, 8><<<grid, 256, 0, s>>>(in, D, H, W, weight, tx, out, stats_partial, tilesD);
-  else
-    conv3d_k3_kernel<8, 2><<<grid, 256, 0, s>>>(in, D, H, W, weight, tx, out, stats_partial, tilesD);
-  return sa::check_launch("sa_conv3d_k3");
+#define SA_CONV(CI, CO, S, TDV, TWV, THV)                                                                   \
+  if (Cin == CI && Cout == CO && stride == S) {                                                              \
+    conv3d_kernel<CI, CO, S, TDV, TWV, THV><<<grid, 256, 0, s>>>(in, Di, Hi, Wi, Do, Ho, Wo, weight, tx, out, \
+                                                                stats_partial, tilesD);                      \
+    return sa::check_launch("sa_conv3d");                                                                    \
+  }
+  SA_CONV(8, 8, 1, 4, 64, 4)
+  SA_CONV(8, 2, 1, 4, 64, 4)
+  SA_CONV(16, 16, 1, 4, 64, 4)
+  SA_CONV(32, 32, 1, 2, 64, 4)
+  SA_CONV(8, 16, 2, 2, 32, 8)
+  SA_CONV(16, 32, 2, 2, 32, 8)
+#undef SA_CONV
+  sa::set_error("sa_conv3d: no kernel built for Cin %d -> Cout %d, stride %d", Cin, Cout, stride);
+  return SA_E_ARG;
 }
 
-extern "C" int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *u, int Cu, int Du, int Hu, int Wu,
-                                         int B, int D, int H, int W, const float *weight, int Cout, float *out,
+extern "C" int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_mean, const float *a_rstd, int a_act,
+                                         const float *a_gl, const float *a_gr, const float *u, int Cu,
+                                         const float *u_mean, const float *u_rstd, int u_act, const float *u_gl,
+                                         const float *u_gr, int Du, int Hu, int Wu, int B, int D, int H, int W,
+                                         float slope, const float *weight, int Cout, float *out,
                                          double *stats_partial, void *stream) {
   SA_REQUIRE(a && u && weight && out && stats_partial, "sa_conv3d_pointwise_upcat: null pointer");
-  SA_REQUIRE(Ca == 8 && Cu == 16 && Cout == 8, "sa_conv3d_pointwise_upcat: built for 8 + 16 -> 8 channels");
   SA_REQUIRE(B > 0 && D > 1 && H > 1 && W > 1 && Du > 0 && Hu > 0 && Wu > 0,
              "sa_conv3d_pointwise_upcat: bad shape");
+  const ConvGeo geo = conv_geo(8, 1);
   int tilesD;
-  dim3 grid = grid_of(B, D, H, W, tilesD);
+  dim3 grid = conv_grid(B, D, H, W, geo, tilesD);
   // area_pixel_compute_scale(align_corners=True) = (in - 1) / (out - 1)
   const float sd = (float)(Du - 1) / (float)(D - 1), sh = (float)(Hu - 1) / (float)(H - 1),
               sw = (float)(Wu - 1) / (float)(W - 1);
+  InXform ta{a_mean, a_rstd, a_gl, a_gr, slope, a_act}, tu{u_mean, u_rstd, u_gl, u_gr, slope, u_act};
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV3D, s);
-  pointwise_upcat_kernel<8, 16, 8><<<grid, 256, 0, s>>>(a, u, D, H, W, Du, Hu, Wu, sd, sh, sw, weight, out,
-                                                         stats_partial, tilesD);
+  if (Ca == 8 && Cu == 16 && Cout == 8) {
+    pointwise_upcat_kernel<8, 16, 8><<<grid, 256, 0, s>>>(a, ta, u, tu, D, H, W, Du, Hu, Wu, sd, sh, sw, weight,
+                                                           out, stats_partial, tilesD);
+  } else if (Ca == 16 && Cu == 32 && Cout == 16) {
+    pointwise_upcat_kernel<16, 32, 16><<<grid, 256, 0, s>>>(a, ta, u, tu, D, H, W, Du, Hu, Wu, sd, sh, sw, weight,
+                                                             out, stats_partial, tilesD);
+  } else {
+    sa::set_error("sa_conv3d_pointwise_upcat: no kernel built for %d + %d -> %d", Ca, Cu, Cout);
+    return SA_E_ARG;
+  }
   return sa::check_launch("sa_conv3d_pointwise_upcat");
 }
 

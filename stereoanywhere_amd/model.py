@@ -109,15 +109,8 @@ class StereoAnywhere(nn.Module):
                                      ub.encoder._conv.weight.new_zeros((2,) + ub.encoder._conv.weight.shape[1:])]),
                     mot_b=torch.cat([ub.encoder._conv.bias, ub.encoder._conv.bias.new_zeros(2)]),
                 )
-                hg = self.hourglass_mono
                 cls = torch.cat([self._derived["cls_d"], self._derived["cls_c"]], 0)  # [2,8,3,3,3]
-
-                def k3(w):  # [co, ci, 3,3,3] -> [ci][27][co]
-                    return w.reshape(w.shape[0], w.shape[1], 27).permute(1, 2, 0).contiguous()
-                fa0 = hg.final_agg[0].conv.weight
-                self._derived["hg_tail"] = dict(
-                    fa0=fa0.reshape(fa0.shape[0], fa0.shape[1]).t().contiguous(),  # [cin][co]
-                    fa1=k3(hg.final_agg[1].conv.weight), fa2=k3(hg.final_agg[2].conv.weight), cls=k3(cls))
+                self._derived["hg"] = self.hourglass_mono.fused_weights(cls)
             self._derived_key = key
         return self._derived
 
@@ -184,8 +177,8 @@ class StereoAnywhere(nn.Module):
         # so only n_additional >= 2 puts a real hourglass after hourglass_mono
         extra = [self.hourglass_mono_stack[i] for i in range(a.n_additional_hourglass)
                  if not isinstance(self.hourglass_mono_stack[i], HourglassIdentity)]
-        if not extra and a.vol_n_masks == 8 and a.volume_channels == 8:
-            vol_d, vol_c = self.hourglass_mono(masked, feats_l, feats_r, fused=dw["hg_tail"])
+        if not extra and self.hourglass_mono.fusable(masked, feats_l):
+            vol_d, vol_c = self.hourglass_mono(masked, feats_l, feats_r, fused=dw["hg"])
         else:
             agg = self.hourglass_mono(masked, feats_l, feats_r)
             for hg in extra:

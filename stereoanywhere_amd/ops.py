@@ -286,8 +286,8 @@ __all__ = [n for n in dir() if not n.startswith("_") and n not in ("annotations"
 
 
 # ----------------------------------------------------------------------- fused hourglass tail / convf1
-def conv3d_stat_parts(D: int, H: int, W: int) -> int:
-    return int(N.lib().sa_conv3d_stat_parts(D, H, W))
+def conv3d_stat_parts(cout: int, stride: int, D: int, H: int, W: int) -> int:
+    return int(N.lib().sa_conv3d_stat_parts(cout, stride, D, H, W))
 
 
 def instnorm_finalize(partial: torch.Tensor, bc: int, parts: int, count: int, eps: float = 1e-5):
@@ -298,37 +298,52 @@ def instnorm_finalize(partial: torch.Tensor, bc: int, parts: int, count: int, ep
     return mean, rstd
 
 
-def conv3d_k3(x: torch.Tensor, w_t: torch.Tensor, cout: int, norm=None, act: bool = False, slope: float = 0.01,
-              gate=None, stats: bool = False):
-    """3x3x3 conv (no bias) of T(x) with T = [gate *] [lrelu] [instance-norm(mean, rstd)];
-    w_t pre-arranged [Cin][27][Cout].  Returns (out [B,Cout,D,H,W], (mean, rstd) | None)."""
-    _check(x, "x")
+class VolAct:
+    """A raw conv output plus the transform its consumers apply on load:
+    T(x) = [gate_l * gate_r *] [lrelu(] [(x - mean) * rstd] [)]."""
+
+    def __init__(self, raw: torch.Tensor, norm=None, act: bool = False, gate=None):
+        self.raw, self.norm, self.act, self.gate = raw, norm, act, gate
+
+    def args(self):
+        mean, rstd = self.norm if self.norm is not None else (None, None)
+        gl, gr = self.gate if self.gate is not None else (None, None)
+        return [_ptr(mean), _ptr(rstd), 1 if self.act else 0, _ptr(gl), _ptr(gr)]
+
+    def with_gate(self, gate) -> "VolAct":
+        return VolAct(self.raw, self.norm, self.act, gate)
+
+
+def conv3d(x: "VolAct", w_t: torch.Tensor, cout: int, stride: int = 1, slope: float = 0.01, stats: bool = True):
+    """3x3x3 conv (pad 1, no bias) of T(x.raw); w_t pre-arranged [Cin][27][Cout].
+    Returns VolAct(out, InstanceNorm stats of out if requested, act=True)."""
+    _check(x.raw, "x")
     _check(w_t, "w_t")
-    B, Cin, D, H, W = x.shape
-    out = torch.empty((B, cout, D, H, W), device=x.device, dtype=torch.float32)
-    parts = conv3d_stat_parts(D, H, W)
-    partial = torch.empty((B * cout * parts * 2,), device=x.device, dtype=torch.float64) if stats else None
-    mean, rstd = norm if norm is not None else (None, None)
-    gl, gr = gate if gate is not None else (None, None)
-    N.call("sa_conv3d_k3", x.data_ptr(), B, Cin, D, H, W, w_t.data_ptr(), cout, _ptr(mean), _ptr(rstd),
-           1 if act else 0, slope, _ptr(gl), _ptr(gr), out.data_ptr(), _ptr(partial), _stream(x))
-    if not stats:
-        return out, None
-    return out, instnorm_finalize(partial, B * cout, parts, D * H * W)
+    B, Cin, D, H, W = x.raw.shape
+    Do, Ho, Wo = (D - 1) // stride + 1, (H - 1) // stride + 1, (W - 1) // stride + 1
+    out = torch.empty((B, cout, Do, Ho, Wo), device=x.raw.device, dtype=torch.float32)
+    parts = conv3d_stat_parts(cout, stride, Do, Ho, Wo)
+    partial = torch.empty((B * cout * parts * 2,), device=out.device, dtype=torch.float64) if stats else None
+    a = x.args()
+    N.call("sa_conv3d", x.raw.data_ptr(), B, Cin, D, H, W, stride, w_t.data_ptr(), cout, a[0], a[1], a[2], slope,
+           a[3], a[4], out.data_ptr(), _ptr(partial), _stream(out))
+    norm = instnorm_finalize(partial, B * cout, parts, Do * Ho * Wo) if stats else None
+    return VolAct(out, norm, act=stats)
 
 
-def conv3d_pointwise_upcat(a: torch.Tensor, u: torch.Tensor, w_t: torch.Tensor, cout: int):
-    """1x1x1 conv over cat(a, trilinear_up(u)) -> (out, (mean, rstd)); w_t [Ca+Cu][Cout]."""
-    _check(a, "a")
-    _check(u, "u")
-    B, Ca, D, H, W = a.shape
-    _, Cu, Du, Hu, Wu = u.shape
-    out = torch.empty((B, cout, D, H, W), device=a.device, dtype=torch.float32)
-    parts = conv3d_stat_parts(D, H, W)
-    partial = torch.empty((B * cout * parts * 2,), device=a.device, dtype=torch.float64)
-    N.call("sa_conv3d_pointwise_upcat", a.data_ptr(), Ca, u.data_ptr(), Cu, Du, Hu, Wu, B, D, H, W, w_t.data_ptr(),
-           cout, out.data_ptr(), partial.data_ptr(), _stream(a))
-    return out, instnorm_finalize(partial, B * cout, parts, D * H * W)
+def conv3d_pointwise_upcat(a: "VolAct", u: "VolAct", w_t: torch.Tensor, cout: int, slope: float = 0.01):
+    """1x1x1 conv over cat(T(a), trilinear_up(T(u))) -> VolAct(out, IN stats, act=True);
+    w_t [Ca+Cu][Cout] with a-rows first."""
+    _check(a.raw, "a")
+    _check(u.raw, "u")
+    B, Ca, D, H, W = a.raw.shape
+    _, Cu, Du, Hu, Wu = u.raw.shape
+    out = torch.empty((B, cout, D, H, W), device=a.raw.device, dtype=torch.float32)
+    parts = conv3d_stat_parts(8, 1, D, H, W)
+    partial = torch.empty((B * cout * parts * 2,), device=out.device, dtype=torch.float64)
+    N.call("sa_conv3d_pointwise_upcat", a.raw.data_ptr(), Ca, *a.args(), u.raw.data_ptr(), Cu, *u.args(), Du, Hu,
+           Wu, B, D, H, W, slope, w_t.data_ptr(), cout, out.data_ptr(), partial.data_ptr(), _stream(out))
+    return VolAct(out, instnorm_finalize(partial, B * cout, parts, D * H * W), act=True)
 
 
 def conv2d_small(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor], cout: int, ksize: int,
