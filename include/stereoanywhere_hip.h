@@ -182,6 +182,10 @@ int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_mean, const
                               const float *u_gl, const float *u_gr, int Du, int Hu, int Wu, int B,
                               int D, int H, int W, float slope, const float *weight, int Cout,
                               float *out, double *stats_partial, void *stream);
+/* out = T(in) elementwise on a [B,C,D,H,W] volume (T as for sa_conv3d). */
+int sa_vol_apply(const float *in, int B, int C, int D, int H, int W, const float *mean,
+                 const float *rstd, int act, float slope, const float *gate_l, const float *gate_r,
+                 float *out, void *stream);
 /* mean/rstd of each of bc_count channels from the partials (count voxels each, biased
  * variance, rstd = 1/sqrt(var + eps)) — InstanceNorm3d statistics (affine=False). */
 int sa_instnorm_finalize(const double *partial, int bc_count, long nparts, long count, float eps,

@@ -49,6 +49,7 @@ SIGNATURES = {
     "sa_conv3d_pointwise_upcat": (I, [P, I, P, P, I, P, P, P, I, P, P, I, P, P, I, I, I, I, I, I, I, F, P, I, P,
                                       P, P]),
     "sa_instnorm_finalize": (I, [P, I, L, L, F, P, P, P]),
+    "sa_vol_apply": (I, [P, I, I, I, I, I, P, P, I, F, P, P, P, P]),
     "sa_conv2d_small": (I, [P, L, I, I, I, I, P, P, I, I, I, P, L, P]),
     "sa_timing_enable": (I, [I]),
     "sa_timing_read": (I, [I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]),

@@ -241,11 +241,12 @@ class Hourglass(nn.Module):
         r = ops.conv3d(down0, fw["d10"], 32, stride=2, slope=slope)                 # down_layers[1][0]
         r = ops.conv3d(r, fw["d11"], 32, slope=slope)                               # down_layers[1][1]
         down1 = gated(r, self.feature_atts[1], 2)
-        r = ops.conv3d_pointwise_upcat(down0, down1, fw["a10"], 16, slope=slope)    # agg_layers[1][0]
+        # the up-cat convs read the low-res branch at 8 corners per voxel: materialise T(.) once
+        r = ops.conv3d_pointwise_upcat(down0, ops.vol_apply(down1, slope), fw["a10"], 16, slope=slope)  # agg[1][0]
         r = ops.conv3d(r, fw["a11"], 16, slope=slope)                               # agg_layers[1][1]
         r = ops.conv3d(r, fw["a12"], 16, slope=slope)                               # agg_layers[1][2]
         x = gated(r, self.feature_atts_up[1], 1)
-        r = ops.conv3d_pointwise_upcat(orig, x, fw["fa0"], 8, slope=slope)          # final_agg[0]
+        r = ops.conv3d_pointwise_upcat(orig, ops.vol_apply(x, slope), fw["fa0"], 8, slope=slope)  # final_agg[0]
         r = ops.conv3d(r, fw["fa1"], 8, slope=slope)                                # final_agg[1]
         r = ops.conv3d(r, fw["fa2"], 8, slope=slope)                                # final_agg[2]
         r = gated(r, self.final_feature_atts_up, 0)

@@ -242,6 +242,20 @@ __global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__res
   block_stats<COUT>(s, q, red, partial, b, nparts, blk, COUT);
 }
 
+// T(x) materialised (for the low-resolution branch an up-cat conv reads at 8 corners)
+__global__ __launch_bounds__(256) void vol_apply_kernel(const float *__restrict__ in, InXform tx, int C, int D, int H,
+                                                        int W, long n, float *__restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int w = (int)(i % W);
+  const long r = i / W;
+  const int h = (int)(r % H);
+  const long r2 = r / H;
+  const int d = (int)(r2 % D);
+  const long bc = r2 / D;
+  out[i] = xform(in[i], tx, bc, d, h, w, H, W, D);
+}
+
 // one block per (b, c): fixed-shape tree reduction of the float64 partials (deterministic)
 __global__ __launch_bounds__(256) void instnorm_finalize_kernel(const double *__restrict__ partial, int nparts,
                                                                 double count, float eps, float *__restrict__ mean,
@@ -357,6 +371,17 @@ extern "C" int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_
     return SA_E_ARG;
   }
   return sa::check_launch("sa_conv3d_pointwise_upcat");
+}
+
+extern "C" int sa_vol_apply(const float *in, int B, int C, int D, int H, int W, const float *mean, const float *rstd,
+                            int act, float slope, const float *gate_l, const float *gate_r, float *out, void *stream) {
+  SA_REQUIRE(in && out && B > 0 && C > 0 && D > 0 && H > 0 && W > 0, "sa_vol_apply: bad arguments");
+  const long n = (long)B * C * D * H * W;
+  InXform tx{mean, rstd, gate_l, gate_r, slope, act};
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_CONV3D, s);
+  vol_apply_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(in, tx, C, D, H, W, n, out);
+  return sa::check_launch("sa_vol_apply");
 }
 
 extern "C" int sa_instnorm_finalize(const double *partial, int bc_count, long nparts, long count, float eps,

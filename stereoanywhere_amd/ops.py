@@ -314,6 +314,17 @@ class VolAct:
         return VolAct(self.raw, self.norm, self.act, gate)
 
 
+def vol_apply(x: "VolAct", slope: float = 0.01) -> "VolAct":
+    """Materialise T(x.raw) -> VolAct(out) with the identity transform."""
+    _check(x.raw, "x")
+    B, C, D, H, W = x.raw.shape
+    out = torch.empty_like(x.raw)
+    a = x.args()
+    N.call("sa_vol_apply", x.raw.data_ptr(), B, C, D, H, W, a[0], a[1], a[2], slope, a[3], a[4], out.data_ptr(),
+           _stream(out))
+    return VolAct(out)
+
+
 def conv3d(x: "VolAct", w_t: torch.Tensor, cout: int, stride: int = 1, slope: float = 0.01, stats: bool = True):
     """3x3x3 conv (pad 1, no bias) of T(x.raw); w_t pre-arranged [Cin][27][Cout].
     Returns VolAct(out, InstanceNorm stats of out if requested, act=True)."""
