@@ -172,16 +172,16 @@ int sa_conv3d(const float *in, int B, int Cin, int Di, int Hi, int Wi, int strid
               const float *weight, int Cout, const float *in_mean, const float *in_rstd, int act,
               float slope, const float *gate_l, const float *gate_r, float *out,
               double *stats_partial, void *stream);
-/* 1x1x1 conv over cat(Ta(a), trilinear_up(Tu(u))) (hourglass.py:319-321, 326-328):
- * a [B,Ca,D,H,W], u [B,Cu,Du,Hu,Wu] upsampled with align_corners=True on the fly, each
- * corner transformed before interpolation; T as above (pass NULLs for identity); weight
- * pre-arranged [Ca+Cu][Cout] with the a-rows first.  Built for (8,16->8) and (16,32->16). */
+/* 1x1x1 conv over cat(Ta(a), trilinear_up(u)) (hourglass.py:319-321, 326-328):
+ * a [B,Ca,D,H,W] with transform Ta as above (NULLs / act 0 for identity); u [B,Cu,Du,Hu,Wu]
+ * already transformed (sa_vol_apply), upsampled with align_corners=True on the fly;
+ * weight pre-arranged [Ca+Cu][Cout] with the a-rows first.
+ * Built for (8 + 16 -> 8, identity a) and (16 + 32 -> 16, transformed a). */
 int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_mean, const float *a_rstd,
                               int a_act, const float *a_gl, const float *a_gr, const float *u,
-                              int Cu, const float *u_mean, const float *u_rstd, int u_act,
-                              const float *u_gl, const float *u_gr, int Du, int Hu, int Wu, int B,
-                              int D, int H, int W, float slope, const float *weight, int Cout,
-                              float *out, double *stats_partial, void *stream);
+                              int Cu, int Du, int Hu, int Wu, int B, int D, int H, int W,
+                              float slope, const float *weight, int Cout, float *out,
+                              double *stats_partial, void *stream);
 /* out = T(in) elementwise on a [B,C,D,H,W] volume (T as for sa_conv3d). */
 int sa_vol_apply(const float *in, int B, int C, int D, int H, int W, const float *mean,
                  const float *rstd, int act, float slope, const float *gate_l, const float *gate_r,

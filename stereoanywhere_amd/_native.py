@@ -46,8 +46,7 @@ SIGNATURES = {
     "sa_convex_upsample": (I, [P, P, L, I, I, I, I, P, P]),
     "sa_conv3d_stat_parts": (L, [I, I, I, I, I]),
     "sa_conv3d": (I, [P, I, I, I, I, I, I, P, I, P, P, I, F, P, P, P, P, P]),
-    "sa_conv3d_pointwise_upcat": (I, [P, I, P, P, I, P, P, P, I, P, P, I, P, P, I, I, I, I, I, I, I, F, P, I, P,
-                                      P, P]),
+    "sa_conv3d_pointwise_upcat": (I, [P, I, P, P, I, P, P, P, I, I, I, I, I, I, I, I, F, P, I, P, P, P]),
     "sa_instnorm_finalize": (I, [P, I, L, L, F, P, P, P]),
     "sa_vol_apply": (I, [P, I, I, I, I, I, P, P, I, F, P, P, P, P]),
     "sa_conv2d_small": (I, [P, L, I, I, I, I, P, P, I, I, I, P, L, P]),

@@ -171,12 +171,12 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const float *__restrict__ i
   }
 }
 
-// 1x1x1 conv over cat(Ta(a), trilinear_up(Tu(u))) -> COUT channels, + IN partial
-// statistics.  Tu (norm / LeakyReLU / gate of the low-resolution branch) is applied to each
-// of the 8 corners before interpolating, i.e. exactly upsample(T(u)).
-template <int CA, int CU, int COUT>
+// 1x1x1 conv over cat(Ta(a), trilinear_up(u)) -> COUT channels, + IN partial statistics.
+// The low-resolution branch u arrives already transformed (sa_vol_apply): evaluating its
+// gate at all 8 corners of every voxel made this kernel load-issue bound.
+template <int CA, int CU, int COUT, bool AX>
 __global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__restrict__ a, InXform ta,
-                                                              const float *__restrict__ u, InXform tu, int D, int H,
+                                                              const float *__restrict__ u, int D, int H,
                                                               int W, int Du, int Hu, int Wu, float sd, float sh,
                                                               float sw, const float *__restrict__ wt,
                                                               float *__restrict__ out, double *__restrict__ partial,
@@ -210,22 +210,19 @@ __global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__res
 #pragma unroll 1
       for (int c = 0; c < CA; ++c) {
         const long bc = (long)b * CA + c;
-        const float xv = xform(a[bc * vol + pos], ta, bc, d, h, w, H, W, D);
+        const float av = a[bc * vol + pos];
+        const float xv = AX ? xform(av, ta, bc, d, h, w, H, W, D) : av;
 #pragma unroll
         for (int co = 0; co < COUT; ++co) r[co] += wt[c * COUT + co] * xv;
       }
-      const int hb = h1 + h1p, wb = w1 + w1p, db = d1 + d1p;
       const long o000 = ((long)d1 * Hu + h1) * Wu + w1;
       const long od_ = (long)d1p * Hu * Wu, oh_ = (long)h1p * Wu, ow_ = w1p;
 #pragma unroll 1
       for (int c = 0; c < CU; ++c) {
-        const long bc = (long)b * CU + c;
-        const float *p = u + bc * volu + o000;
-        auto X = [&](long off, int dd, int hh, int ww) { return xform(p[off], tu, bc, dd, hh, ww, Hu, Wu, Du); };
-        const float xv = dl0 * (hl0 * (wl0 * X(0, d1, h1, w1) + wl1 * X(ow_, d1, h1, wb)) +
-                                hl1 * (wl0 * X(oh_, d1, hb, w1) + wl1 * X(oh_ + ow_, d1, hb, wb))) +
-                         dl1 * (hl0 * (wl0 * X(od_, db, h1, w1) + wl1 * X(od_ + ow_, db, h1, wb)) +
-                                hl1 * (wl0 * X(od_ + oh_, db, hb, w1) + wl1 * X(od_ + oh_ + ow_, db, hb, wb)));
+        const float *p = u + ((long)b * CU + c) * volu + o000;
+        const float xv = dl0 * (hl0 * (wl0 * p[0] + wl1 * p[ow_]) + hl1 * (wl0 * p[oh_] + wl1 * p[oh_ + ow_])) +
+                         dl1 * (hl0 * (wl0 * p[od_] + wl1 * p[od_ + ow_]) +
+                                hl1 * (wl0 * p[od_ + oh_] + wl1 * p[od_ + oh_ + ow_]));
 #pragma unroll
         for (int co = 0; co < COUT; ++co) r[co] += wt[(CA + c) * COUT + co] * xv;
       }
@@ -343,11 +340,9 @@ extern "C" int sa_conv3d(const float *in, int B, int Cin, int Di, int Hi, int Wi
 }
 
 extern "C" int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_mean, const float *a_rstd, int a_act,
-                                         const float *a_gl, const float *a_gr, const float *u, int Cu,
-                                         const float *u_mean, const float *u_rstd, int u_act, const float *u_gl,
-                                         const float *u_gr, int Du, int Hu, int Wu, int B, int D, int H, int W,
-                                         float slope, const float *weight, int Cout, float *out,
-                                         double *stats_partial, void *stream) {
+                                         const float *a_gl, const float *a_gr, const float *u, int Cu, int Du, int Hu,
+                                         int Wu, int B, int D, int H, int W, float slope, const float *weight, int Cout,
+                                         float *out, double *stats_partial, void *stream) {
   SA_REQUIRE(a && u && weight && out && stats_partial, "sa_conv3d_pointwise_upcat: null pointer");
   SA_REQUIRE(B > 0 && D > 1 && H > 1 && W > 1 && Du > 0 && Hu > 0 && Wu > 0,
              "sa_conv3d_pointwise_upcat: bad shape");
@@ -357,20 +352,21 @@ extern "C" int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_
   // area_pixel_compute_scale(align_corners=True) = (in - 1) / (out - 1)
   const float sd = (float)(Du - 1) / (float)(D - 1), sh = (float)(Hu - 1) / (float)(H - 1),
               sw = (float)(Wu - 1) / (float)(W - 1);
-  InXform ta{a_mean, a_rstd, a_gl, a_gr, slope, a_act}, tu{u_mean, u_rstd, u_gl, u_gr, slope, u_act};
+  InXform ta{a_mean, a_rstd, a_gl, a_gr, slope, a_act};
+  const bool ax = a_mean || a_act || a_gl;
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV3D, s);
-  if (Ca == 8 && Cu == 16 && Cout == 8) {
-    pointwise_upcat_kernel<8, 16, 8><<<grid, 256, 0, s>>>(a, ta, u, tu, D, H, W, Du, Hu, Wu, sd, sh, sw, weight,
-                                                           out, stats_partial, tilesD);
-  } else if (Ca == 16 && Cu == 32 && Cout == 16) {
-    pointwise_upcat_kernel<16, 32, 16><<<grid, 256, 0, s>>>(a, ta, u, tu, D, H, W, Du, Hu, Wu, sd, sh, sw, weight,
-                                                             out, stats_partial, tilesD);
-  } else {
-    sa::set_error("sa_conv3d_pointwise_upcat: no kernel built for %d + %d -> %d", Ca, Cu, Cout);
-    return SA_E_ARG;
+#define SA_PW(CA, CU, CO, AXV)                                                                                     \
+  if (Ca == CA && Cu == CU && Cout == CO && ax == AXV) {                                                          \
+    pointwise_upcat_kernel<CA, CU, CO, AXV><<<grid, 256, 0, s>>>(a, ta, u, D, H, W, Du, Hu, Wu, sd, sh, sw,       \
+                                                                  weight, out, stats_partial, tilesD);             \
+    return sa::check_launch("sa_conv3d_pointwise_upcat");                                                         \
   }
-  return sa::check_launch("sa_conv3d_pointwise_upcat");
+  SA_PW(8, 16, 8, false)
+  SA_PW(16, 32, 16, true)
+#undef SA_PW
+  sa::set_error("sa_conv3d_pointwise_upcat: no kernel built for %d + %d -> %d (a transform %d)", Ca, Cu, Cout, ax);
+  return SA_E_ARG;
 }
 
 extern "C" int sa_vol_apply(const float *in, int B, int C, int D, int H, int W, const float *mean, const float *rstd,

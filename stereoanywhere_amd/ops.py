@@ -343,8 +343,10 @@ def conv3d(x: "VolAct", w_t: torch.Tensor, cout: int, stride: int = 1, slope: fl
 
 
 def conv3d_pointwise_upcat(a: "VolAct", u: "VolAct", w_t: torch.Tensor, cout: int, slope: float = 0.01):
-    """1x1x1 conv over cat(T(a), trilinear_up(T(u))) -> VolAct(out, IN stats, act=True);
-    w_t [Ca+Cu][Cout] with a-rows first."""
+    """1x1x1 conv over cat(T(a), trilinear_up(u)) -> VolAct(out, IN stats, act=True);
+    u must be materialised (identity transform, see vol_apply); w_t [Ca+Cu][Cout], a-rows first."""
+    if u.norm is not None or u.act or u.gate is not None:
+        raise RuntimeError("conv3d_pointwise_upcat: materialise u with vol_apply first")
     _check(a.raw, "a")
     _check(u.raw, "u")
     B, Ca, D, H, W = a.raw.shape
@@ -352,8 +354,8 @@ def conv3d_pointwise_upcat(a: "VolAct", u: "VolAct", w_t: torch.Tensor, cout: in
     out = torch.empty((B, cout, D, H, W), device=a.raw.device, dtype=torch.float32)
     parts = conv3d_stat_parts(8, 1, D, H, W)
     partial = torch.empty((B * cout * parts * 2,), device=out.device, dtype=torch.float64)
-    N.call("sa_conv3d_pointwise_upcat", a.raw.data_ptr(), Ca, *a.args(), u.raw.data_ptr(), Cu, *u.args(), Du, Hu,
-           Wu, B, D, H, W, slope, w_t.data_ptr(), cout, out.data_ptr(), partial.data_ptr(), _stream(out))
+    N.call("sa_conv3d_pointwise_upcat", a.raw.data_ptr(), Ca, *a.args(), u.raw.data_ptr(), Cu, Du, Hu, Wu, B, D,
+           H, W, slope, w_t.data_ptr(), cout, out.data_ptr(), partial.data_ptr(), _stream(out))
     return VolAct(out, instnorm_finalize(partial, B * cout, parts, D * H * W), act=True)
 
 
