@@ -69,8 +69,13 @@ def step_costs(B: int, H4: int, W4: int, iters: int, C: int = 256):
         # xc_q, qh, cq, z, h read, h written
         "gru_out": ("GB/s", iters * gru_px * 6 * hid * 4),
         "convex_upsample": ("GB/s", px * (144 + 1) * 4 + px * 16 * 4),
-        # full-res hourglass tail: 1x1x1 24->8, 3x3x3 8->8 (x2), 3x3x3 8->2 (fp32 FMA)
-        "conv3d_fused": ("TFLOP/s", 2.0 * vol * (24 * 8 + 2 * 27 * 8 * 8 + 27 * 8 * 2)),
+        # the whole mono hourglass + classifier (11 fused conv launches; fp32 FMA), flops
+        # per full-res volume cell: full res 1x1x1 24->8, 3x3x3 8->8 (x2), 8->2;
+        # 1/8 (stride-2 outputs) 8->16, 16->16 (x3), 1x1x1 48->16;  1/64: 16->32, 32->32.
+        # (the two vol_apply launches timed in this family move < 2% of its bytes)
+        "conv3d_fused": ("TFLOP/s", 2.0 * vol * (24 * 8 + 2 * 27 * 8 * 8 + 27 * 8 * 2
+                                                 + (27 * 8 * 16 + 3 * 27 * 16 * 16 + 48 * 16) / 8
+                                                 + (27 * 16 * 32 + 27 * 32 * 32) / 64)),
     }
 
 

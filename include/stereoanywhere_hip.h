@@ -126,10 +126,10 @@ int sa_mono_scale_mirror(const float *m2, const float *m3, const float *scale, c
  *   gru_zr: z = sigmoid(xc[0:C] + hzr[0:C] + cz), r = sigmoid(xc[C:2C] + hzr[C:2C] + cr),
  *           writes z and rh = r*h.
  *   gru_out: h = (1 - z) h + z tanh(xc[2C:3C] + qh + cq)   (in place on h). */
-int sa_gru_zr(const float *xc, long xc_bs, const float *hzr, long hzr_bs, const float *cz,
+int sa_gru_zr(const float *xc, long xc_bs, const float *bx, const float *hzr, long hzr_bs, const float *cz,
               const float *cr, long c_bs, const float *h, long h_bs, int B, int C, int HW,
               float *z, float *rh, void *stream);
-int sa_gru_out(const float *xc, long xc_bs, const float *qh, long qh_bs, const float *cq,
+int sa_gru_out(const float *xc, long xc_bs, const float *bx, const float *qh, long qh_bs, const float *cq,
                long c_bs, const float *z, int B, int C, int HW, float *h, long h_bs,
                void *stream);
 
@@ -172,16 +172,23 @@ int sa_conv3d(const float *in, int B, int Cin, int Di, int Hi, int Wi, int strid
               const float *weight, int Cout, const float *in_mean, const float *in_rstd, int act,
               float slope, const float *gate_l, const float *gate_r, float *out,
               double *stats_partial, void *stream);
-/* 1x1x1 conv over cat(Ta(a), trilinear_up(u)) (hourglass.py:319-321, 326-328):
- * a [B,Ca,D,H,W] with transform Ta as above (NULLs / act 0 for identity); u [B,Cu,Du,Hu,Wu]
- * already transformed (sa_vol_apply), upsampled with align_corners=True on the fly;
- * weight pre-arranged [Ca+Cu][Cout] with the a-rows first.
- * Built for (8 + 16 -> 8, identity a) and (16 + 32 -> 16, transformed a). */
+/* 1x1x1 conv over cat(Ta(a), trilinear_up(T(u))) (hourglass.py:319-321, 326-328), in two
+ * launches because the upsample is linear: W . cat(Ta(a), up(T(u))) = Wa . Ta(a) + up(Wu . T(u)).
+ *   sa_conv3d_pointwise: p = W . T(in) at the low resolution (transform T as for sa_conv3d,
+ *     weight [Cin][Cout]; no statistics).  Built for 16 -> 8 and 32 -> 16.
+ *   sa_conv3d_pointwise_upcat: out = Wa . Ta(a) + up(p), a [B,Ca,D,H,W], p [B,Cout,Dp,Hp,Wp]
+ *     upsampled with align_corners=True (Dp-1 <= (D-1)/2 per axis), weight [Ca][Cout],
+ *     plus InstanceNorm partials as for sa_conv3d (parts = sa_conv3d_upcat_stat_parts(D, H, W)).
+ *     Built for (8 -> 8, identity a) and (16 -> 16, transformed a). */
+long sa_conv3d_upcat_stat_parts(int D, int H, int W);
+int sa_conv3d_pointwise(const float *in, int B, int Cin, int D, int H, int W, const float *mean,
+                        const float *rstd, int act, float slope, const float *gate_l,
+                        const float *gate_r, const float *weight, int Cout, float *out, void *stream);
 int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_mean, const float *a_rstd,
-                              int a_act, const float *a_gl, const float *a_gr, const float *u,
-                              int Cu, int Du, int Hu, int Wu, int B, int D, int H, int W,
-                              float slope, const float *weight, int Cout, float *out,
-                              double *stats_partial, void *stream);
+                              int a_act, const float *a_gl, const float *a_gr, const float *p,
+                              int Dp, int Hp, int Wp, int B, int D, int H, int W, float slope,
+                              const float *weight, int Cout, float *out, double *stats_partial,
+                              void *stream);
 /* out = T(in) elementwise on a [B,C,D,H,W] volume (T as for sa_conv3d). */
 int sa_vol_apply(const float *in, int B, int C, int D, int H, int W, const float *mean,
                  const float *rstd, int act, float slope, const float *gate_l, const float *gate_r,
@@ -197,12 +204,32 @@ int sa_conv2d_small(const float *in, long in_bs, int B, int Cin, int H, int W, c
                     const float *bias, int Cout, int ksize, int relu, float *out, long out_bs,
                     void *stream);
 
+/* flow_head.conv2 (update.py:98-110): 3x3 / pad 1 conv, Cin (multiple of 4) -> Cout = 2,
+ * weight in the module's [Cout][Cin][3][3] layout, bias may be NULL. */
+int sa_conv2d_k3_narrow(const float *in, long in_bs, int B, int Cin, int H, int W, const float *weight,
+                        const float *bias, int Cout, float *out, long out_bs, void *stream);
+
+/* Epilogues of the MIOpen 2-D convs (encoders extractor.py:6-300, update block update.py:64-110).
+ * sa_plane_stats: InstanceNorm2d statistics (biased variance, eps) of each (b, c) plane of
+ *   x [B,C,hw] (batch stride x_bs) -> mean, rstd [B*C].
+ * sa_norm_act: out = act_out(act_in((x - m) * s + t) + skip_term), skip_term =
+ *   (skip - skip_m) * skip_s + skip_t (any of the three NULL = 0 / 1 / 0) or 0 without skip;
+ *   parameters per channel (pstride 0) or per (b, c) plane (pstride C); act 0 none,
+ *   1 ReLU, 2 tanh; x, skip and out may be channel-slice views (batch strides); out may
+ *   alias x. */
+int sa_plane_stats(const float *x, long x_bs, int B, int C, long hw, float eps, float *mean,
+                   float *rstd, void *stream);
+int sa_norm_act(const float *x, long x_bs, int B, int C, long hw, const float *m, const float *s,
+                const float *t, int pstride, int act_in, const float *skip, long skip_bs,
+                const float *skip_m, const float *skip_s, const float *skip_t, int skip_pstride,
+                int act_out, float *out, long out_bs, void *stream);
+
 /* Live per-kernel timing for bench.py: when enabled, every launch of kernel `id`
  * is bracketed by hipEvents on the launch stream; sa_timing_read synchronises the
  * recorded events and returns their summed duration (ms) and count, then clears. */
 enum {
   SA_K_CORR_PYRAMID = 0, SA_K_LOOKUP, SA_K_MONO_VOLUME, SA_K_SOFTARGMIN, SA_K_LSQ,
-  SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_COUNT
+  SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_NORM, SA_K_COUNT
 };
 int sa_timing_enable(int on);
 int sa_timing_read(int kernel_id, double *total_ms, long *count);

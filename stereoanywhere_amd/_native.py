@@ -13,7 +13,7 @@ from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_HERE, "lib", "libsa_hip.so")
+LIB_PATH = os.environ.get("SA_HIP_LIB") or os.path.join(_HERE, "lib", "libsa_hip.so")  # override: A/B runs
 HEADER = os.path.join(ROOT, "include", "stereoanywhere_hip.h")
 
 P = ctypes.c_void_p
@@ -37,8 +37,8 @@ SIGNATURES = {
     "sa_softlrc": (I, [P, P, P, P, I, I, I, L, F, P, P, P]),
     "sa_weighted_lsq": (I, [P, P, P, I, I, F, F, P, P, P]),
     "sa_mono_scale_mirror": (I, [P, P, P, P, P, P, I, I, I, L, F, F, P, P, P, P, P]),
-    "sa_gru_zr": (I, [P, L, P, L, P, P, L, P, L, I, I, I, P, P, P]),
-    "sa_gru_out": (I, [P, L, P, L, P, L, P, I, I, I, P, L, P]),
+    "sa_gru_zr": (I, [P, L, P, P, L, P, P, L, P, L, I, I, I, P, P, P]),
+    "sa_gru_out": (I, [P, L, P, P, L, P, L, P, I, I, I, P, L, P]),
     "sa_pool2x": (I, [P, L, I, I, I, I, P, L, P]),
     "sa_interp_bilinear_ac": (I, [P, L, I, I, I, I, I, I, P, L, P]),
     "sa_relu_copy": (I, [P, L, I, I, I, P, L, P]),
@@ -46,7 +46,12 @@ SIGNATURES = {
     "sa_convex_upsample": (I, [P, P, L, I, I, I, I, P, P]),
     "sa_conv3d_stat_parts": (L, [I, I, I, I, I]),
     "sa_conv3d": (I, [P, I, I, I, I, I, I, P, I, P, P, I, F, P, P, P, P, P]),
-    "sa_conv3d_pointwise_upcat": (I, [P, I, P, P, I, P, P, P, I, I, I, I, I, I, I, I, F, P, I, P, P, P]),
+    "sa_conv2d_k3_narrow": (I, [P, L, I, I, I, I, P, P, I, P, L, P]),
+    "sa_plane_stats": (I, [P, L, I, I, L, F, P, P, P]),
+    "sa_norm_act": (I, [P, L, I, I, L, P, P, P, I, I, P, L, P, P, P, I, I, P, L, P]),
+    "sa_conv3d_upcat_stat_parts": (L, [I, I, I]),
+    "sa_conv3d_pointwise": (I, [P, I, I, I, I, I, P, P, I, F, P, P, P, I, P, P]),
+    "sa_conv3d_pointwise_upcat": (I, [P, I, P, P, I, P, P, P, I, I, I, I, I, I, I, F, P, I, P, P, P]),
     "sa_instnorm_finalize": (I, [P, I, L, L, F, P, P, P]),
     "sa_vol_apply": (I, [P, I, I, I, I, I, P, P, I, F, P, P, P, P]),
     "sa_conv2d_small": (I, [P, L, I, I, I, I, P, P, I, I, I, P, L, P]),
@@ -58,6 +63,7 @@ SIGNATURES = {
 KERNEL_IDS = {
     "corr_volume_pyramid": 0, "corr_lookup": 1, "mono_masked_volume": 2, "softargmin_conf": 3,
     "weighted_lsq": 4, "gru_zr": 5, "gru_out": 6, "convex_upsample": 7, "misc": 8, "conv3d_fused": 9,
+    "norm_act": 10,
 }
 
 _lib: Optional[ctypes.CDLL] = None

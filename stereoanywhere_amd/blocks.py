@@ -222,7 +222,7 @@ class Hourglass(nn.Module):
         return all(n % 4 == 0 for n in (D, H, W)) and tuple(features_left[0].shape[2:]) == (H, W)
 
     def _forward_fused(self, masked, fl, fr, fw):
-        """hourglass.py:61-91 (live part) + classifiers as 12 fused HIP launches
+        """hourglass.py:61-91 (live part) + classifiers as 13 fused HIP launches
         (csrc/conv3d_fused.hip).  Every activation is kept raw; the consumer applies
         InstanceNorm3d + LeakyReLU (+ DoubleFeatureAtt gate) while loading it, so no
         normalised / gated / upsampled / concatenated volume is ever written."""
@@ -241,12 +241,12 @@ class Hourglass(nn.Module):
         r = ops.conv3d(down0, fw["d10"], 32, stride=2, slope=slope)                 # down_layers[1][0]
         r = ops.conv3d(r, fw["d11"], 32, slope=slope)                               # down_layers[1][1]
         down1 = gated(r, self.feature_atts[1], 2)
-        # the up-cat convs read the low-res branch at 8 corners per voxel: materialise T(.) once
-        r = ops.conv3d_pointwise_upcat(down0, ops.vol_apply(down1, slope), fw["a10"], 16, slope=slope)  # agg[1][0]
+        # up-cat convs: the low-res branch is projected to the output channels, then upsampled
+        r = ops.conv3d_pointwise_upcat(down0, down1, *fw["a10"], 16, slope=slope)  # agg_layers[1][0]
         r = ops.conv3d(r, fw["a11"], 16, slope=slope)                               # agg_layers[1][1]
         r = ops.conv3d(r, fw["a12"], 16, slope=slope)                               # agg_layers[1][2]
         x = gated(r, self.feature_atts_up[1], 1)
-        r = ops.conv3d_pointwise_upcat(orig, ops.vol_apply(x, slope), fw["fa0"], 8, slope=slope)  # final_agg[0]
+        r = ops.conv3d_pointwise_upcat(orig, x, *fw["fa0"], 8, slope=slope)         # final_agg[0]
         r = ops.conv3d(r, fw["fa1"], 8, slope=slope)                                # final_agg[1]
         r = ops.conv3d(r, fw["fa2"], 8, slope=slope)                                # final_agg[2]
         r = gated(r, self.final_feature_atts_up, 0)
@@ -259,9 +259,9 @@ class Hourglass(nn.Module):
         def k3(w):
             return w.reshape(w.shape[0], w.shape[1], 27).permute(1, 2, 0).contiguous()
 
-        def pw(w, a_cols, u_cols):  # rows: a-part first, then the upsampled part
+        def pw(w, a_cols, u_cols):  # ([Ca][Cout] for the full-res part, [Cu][Cout] for the upsampled)
             w = w.reshape(w.shape[0], w.shape[1])
-            return torch.cat([w[:, a_cols].t(), w[:, u_cols].t()], 0).contiguous()
+            return w[:, a_cols].t().contiguous(), w[:, u_cols].t().contiguous()
         a10 = self.agg_layers[1][0].conv.weight  # input cat(up(down1) [32], down0 [16])
         fa0 = self.final_agg[0].conv.weight      # input cat(orig [8], up(x) [16])
         return dict(

@@ -8,6 +8,11 @@
 // wave-uniform (scalar) weights; bias and ReLU are applied in the epilogue.
 #include "sa_common.h"
 
+// Convolution sums have no reference summation order to reproduce (MIOpen picks its own
+// algorithm), so let a*b+c contract to (packed) FMA here; the library builds with
+// -ffp-contract=off for the element-wise kernels that mirror torch expressions.
+#pragma clang fp contract(fast)
+
 namespace {
 
 constexpr int T = 16;
@@ -54,7 +59,87 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const float *__restri
   }
 }
 
+// 3x3 / pad 1 conv with many inputs and very few outputs (flow_head.conv2: 256 -> 2,
+// update.py:98-110), which the library runs at a few % of its arithmetic rate.  Memory
+// bound: one thread per (pixel, quarter of the input channels), taps read straight from
+// L1/L2 (neighbouring pixels share lines), the four partial sums reduced through LDS in a
+// fixed order; bias in the epilogue.  Weights in the module's own [Cout][Cin][3][3] layout.
+template <int COUT>
+__global__ __launch_bounds__(256) void conv2d_k3_narrow_kernel(const float *__restrict__ in, long in_bs, int Cin,
+                                                               int H, int W, const float *__restrict__ wt,
+                                                               const float *__restrict__ bias,
+                                                               float *__restrict__ out, long out_bs) {
+  __shared__ float red[3][COUT][64];
+  const int lane = threadIdx.x & 63;
+  const int grp = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long hw = (long)H * W;
+  const long pix = (long)blockIdx.x * 64 + lane;
+  const int b = blockIdx.y;
+  const bool ok = pix < hw;
+  const int y = ok ? (int)(pix / W) : 0, x = ok ? (int)(pix % W) : 0;
+  int off[9];
+  bool val[9];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int yy = y + ky - 1, xx = x + kx - 1;
+      val[ky * 3 + kx] = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      off[ky * 3 + kx] = min(max(yy, 0), H - 1) * W + min(max(xx, 0), W - 1);
+    }
+  const int per = Cin / 4, c0 = grp * per;
+  float acc[COUT];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) acc[co] = 0.0f;
+  const float *src = in + (long)b * in_bs + (long)c0 * hw;
+#pragma unroll 2
+  for (int ci = 0; ci < per; ++ci) {
+    float v[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) v[t] = src[off[t]];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) v[t] = val[t] ? v[t] : 0.0f;
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) {
+      const float *w = wt + ((long)co * Cin + c0 + ci) * 9;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc[co] += w[t] * v[t];
+    }
+    src += hw;
+  }
+  if (grp > 0) {
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) red[grp - 1][co][lane] = acc[co];
+  }
+  __syncthreads();
+  if (grp == 0 && ok) {
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) {
+      const float r = ((acc[co] + red[0][co][lane]) + (red[1][co][lane] + red[2][co][lane])) +
+                      (bias ? bias[co] : 0.0f);
+      out[(long)b * out_bs + co * hw + pix] = r;
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int sa_conv2d_k3_narrow(const float *in, long in_bs, int B, int Cin, int H, int W, const float *weight,
+                                   const float *bias, int Cout, float *out, long out_bs, void *stream) {
+  SA_REQUIRE(in && weight && out, "sa_conv2d_k3_narrow: null pointer");
+  SA_REQUIRE(B > 0 && B <= 65535 && Cin > 0 && Cin % 4 == 0 && H > 0 && W > 0, "sa_conv2d_k3_narrow: bad shape");
+  SA_REQUIRE((long)H * W < (1L << 31), "sa_conv2d_k3_narrow: plane too large");
+  const long hw = (long)H * W;
+  dim3 grid((unsigned)((hw + 63) / 64), (unsigned)B);
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_MISC, s);
+  if (Cout == 2) {
+    conv2d_k3_narrow_kernel<2><<<grid, 256, 0, s>>>(in, in_bs, Cin, H, W, weight, bias, out, out_bs);
+    return sa::check_launch("sa_conv2d_k3_narrow");
+  }
+  sa::set_error("sa_conv2d_k3_narrow: built for 2 outputs (got %d)", Cout);
+  return SA_E_ARG;
+}
 
 extern "C" int sa_conv2d_small(const float *in, long in_bs, int B, int Cin, int H, int W, const float *weight,
                                const float *bias, int Cout, int ksize, int relu, float *out, long out_bs,

@@ -20,17 +20,25 @@
 //   * both classifiers share one conv launch (Cout = 2).
 // Layout everywhere: [B, C, D, H, W] with D = W2 (right pixel), W = W1 (left pixel).
 #include <cmath>
+#include <type_traits>
 
 #include "sa_common.h"
 
+// Convolution sums have no reference summation order to reproduce (MIOpen picks its own
+// algorithm), so let a*b+c contract to (packed) FMA here; the library builds with
+// -ffp-contract=off for the element-wise kernels that mirror torch expressions.
+#pragma clang fp contract(fast)
+
 namespace {
 
-// Output tiles: 256 threads = TW (along W) x TH (along H); each thread owns TD planes
-// along D.  Stride-1 tiles are one wave wide (TW 64); stride-2 tiles are 32 x 8 so the
-// (2*T+1)-wide input halo stays small.
-constexpr int TW = 64;  // default tile (stride 1) along W
+// Output tiles: 256 threads = TWx (along W) x THx (along H), each thread owning TDx
+// planes along D.  A 64-lane wave stages one input row of the tile's halo per load, so
+// the halo row must fit 64 floats: stride-1 tiles use 62 of their 64 columns, stride-2
+// tiles 31 of 32 (same tile counts as 64 / 32 for the volume widths the model has).
+constexpr int TW = 64;  // pointwise tiles along W
 constexpr int TH = 4;   // along H
 constexpr int TD = 4;   // output planes per thread along D
+constexpr int ROW = 64; // LDS row pitch (floats)
 
 struct InXform {
   const float *mean, *rstd;   // per (b, ci), or null
@@ -49,14 +57,15 @@ __device__ __forceinline__ float xform(float v, const InXform &t, long bc, int d
   return v;
 }
 
-// block partial sums of (x, x^2) over the tile for each of NC channels -> partial[bc][blk]
+// block partial sums of (x, x^2) over the tile for each of NC channels -> partial[bc][blk].
+// A thread's own values (at most TD of them) are summed in fp32, everything above in fp64.
 template <int NC>
-__device__ __forceinline__ void block_stats(const double (&s)[NC], const double (&q)[NC], double *red,
+__device__ __forceinline__ void block_stats(const float (&s)[NC], const float (&q)[NC], double *red,
                                             double *partial, long b, int nparts, int blk, int Cout) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    double a = s[c], e = q[c];
+    double a = (double)s[c], e = (double)q[c];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       a += __shfl_xor(a, o);
@@ -81,76 +90,135 @@ __device__ __forceinline__ void block_stats(const double (&s)[NC], const double 
   }
 }
 
+template <int S, int TWx>
+struct ConvTile {
+  static constexpr int valid_w = TWx - (S == 1 ? 2 : 1);  // output columns per tile
+};
+
 // 3x3x3, stride S, padding 1, no bias; CIN input channels, COUT outputs.
+//   staging: the halo of input channel ci+1 is fetched into registers (one 64-lane row load
+//   per row, row coordinates wave-uniform) while channel ci is convolved out of LDS, then
+//   transformed (InstanceNorm / LeakyReLU / gate of the producer) and written to the other
+//   LDS buffer; one barrier per input channel.
+//   compute: for each (kh, kw) the thread reads the LD input planes its TDx outputs touch
+//   once and reuses them across the 3 kd taps; weights [ci][tap][co] come in as scalars.
 template <int CIN, int COUT, int S, int TDx, int TWx, int THx>
 __global__ __launch_bounds__(256) void conv3d_kernel(const float *__restrict__ in, int Di, int Hi, int Wi, int Do,
                                                      int Ho, int Wo, const float *__restrict__ wt, InXform tx,
                                                      float *__restrict__ out, double *__restrict__ partial,
                                                      int tilesD) {
   static_assert(TWx * THx == 256, "256 threads per block");
-  constexpr int LW = (TWx - 1) * S + 3, LH = (THx - 1) * S + 3, LD = (TDx - 1) * S + 3;
-  constexpr int LPLANE = LD * LH * LW;
-  __shared__ float tile[2][LPLANE];
+  constexpr int TWV = ConvTile<S, TWx>::valid_w;
+  constexpr int LW = (TWV - 1) * S + 3, LH = (THx - 1) * S + 3, LD = (TDx - 1) * S + 3;
+  static_assert(LW <= ROW, "halo row must fit one wave");
+  constexpr int ROWS = LD * LH, RPW = (ROWS + 3) / 4;  // rows per wave
+  static_assert(RPW <= 32, "row mask is 32 bits");
+  constexpr int LBUF = ROWS * ROW + 2 * ROW;            // + slack for the idle columns' reads
+  __shared__ float tile[2][LBUF];
   __shared__ double red[COUT * 4 * 2];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tx_ = threadIdx.x % TWx, ty = threadIdx.x / TWx;
-  const int w0 = blockIdx.x * TWx, h0 = blockIdx.y * THx;
+  const int w0 = blockIdx.x * TWV, h0 = blockIdx.y * THx;
   const int b = blockIdx.z / tilesD, d0 = (blockIdx.z % tilesD) * TDx;
   const long vol = (long)Di * Hi * Wi;
   const int iw0 = w0 * S - 1, ih0 = h0 * S - 1, id0 = d0 * S - 1;
+  const int wl = iw0 + lane;                              // this lane's input column
+  const bool lane_ok = lane < LW && wl >= 0 && wl < Wi;
   float acc[TDx][COUT];
 #pragma unroll
   for (int i = 0; i < TDx; ++i)
 #pragma unroll
     for (int c = 0; c < COUT; ++c) acc[i][c] = 0.f;
 
-  auto stage = [&](int ci, int buf) {
+  // branch-free staging: clamped addresses, padding selected to zero at commit (divergent
+  // branches per row would keep one saved exec mask per row live in SGPRs)
+  float pv[RPW], pg[RPW];
+  unsigned okm = 0;
+  const int wcl = min(max(wl, 0), Wi - 1);
+  auto fetch_rows = [&](auto gated, int ci) __attribute__((always_inline)) {
+    constexpr bool G = decltype(gated)::value;
     const long bc = (long)b * CIN + ci;
-    const float *src = in + bc * vol;
-    for (int i = threadIdx.x; i < LPLANE; i += 256) {
-      const int ww = i % LW, r = i / LW, hh = r % LH, dd = r / LH;
-      const int w = iw0 + ww, h = ih0 + hh, d = id0 + dd;
-      float v = 0.0f;
-      if (w >= 0 && w < Wi && h >= 0 && h < Hi && d >= 0 && d < Di)
-        v = xform(src[((long)d * Hi + h) * Wi + w], tx, bc, d, h, w, Hi, Wi, Di);
-      tile[buf][i] = v;
+    const float *src = in + bc * vol;  // plane bases in 64 bits once; offsets in a plane fit 32
+    const float *glb = G ? tx.gl + bc * Hi * Wi : nullptr;
+    const float *grb = G ? tx.gr + bc * Hi * Di : nullptr;
+    okm = 0;
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+      int r = wv + 4 * k;
+      asm volatile("" : "+s"(r));  // recompute the row math per fetch (SALU) instead of hoisting it into SGPRs
+      const int dd = r / LH, hh = r - dd * LH;
+      const int d = id0 + dd, h = ih0 + hh;
+      const bool rok = r < ROWS && d >= 0 && d < Di && h >= 0 && h < Hi;
+      const int dc = min(max(d, 0), Di - 1), hc = min(max(h, 0), Hi - 1);
+      const float *rowp = src + (unsigned)((dc * Hi + hc) * Wi);  // scalar row base, lane offset
+      pv[k] = rowp[(unsigned)wcl];
+      if (G) pg[k] = glb[(unsigned)(hc * Wi) + (unsigned)wcl] * grb[hc * Di + dc];
+      okm |= (rok && lane_ok) ? (1u << k) : 0u;
+    }
+  };
+  auto fetch = [&](int ci) __attribute__((always_inline)) {
+    if (tx.gl) fetch_rows(std::true_type{}, ci);
+    else fetch_rows(std::false_type{}, ci);
+  };
+  auto commit = [&](int ci, int buf) __attribute__((always_inline)) {
+    const long bc = (long)b * CIN + ci;
+    float mean = 0.0f, rstd = 1.0f;
+    if (tx.mean) {
+      mean = tx.mean[bc];
+      rstd = tx.rstd[bc];
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+      const int r = wv + 4 * k;
+      if (r < ROWS) {
+        float v = pv[k];
+        if (tx.mean) v = (v - mean) * rstd;
+        if (tx.act) v = v > 0.0f ? v : v * tx.slope;
+        if (tx.gl) v = pg[k] * v;
+        tile[buf][r * ROW + lane] = ((okm >> k) & 1u) ? v : 0.0f;
+      }
     }
   };
 
-  stage(0, 0);
+  fetch(0);
+  commit(0, 0);
   __syncthreads();
+  constexpr int KWU = COUT <= 8 ? 3 : 1;
 #pragma unroll 1
   for (int ci = 0; ci < CIN; ++ci) {
     const int buf = ci & 1;
-    if (ci + 1 < CIN) stage(ci + 1, buf ^ 1);
-    const float *tb = tile[buf] + (ty * S) * LW + tx_ * S;
+    if (ci + 1 < CIN) fetch(ci + 1);
+    const float *tb = tile[buf] + (ty * S) * ROW + tx_ * S;
     const float *wc = wt + (long)ci * 27 * COUT;  // weights pre-arranged [ci][tap][co]
 #pragma unroll 1
-    for (int kd = 0; kd < 3; ++kd) {
+    for (int kh = 0; kh < 3; ++kh) {
+#pragma unroll KWU
+      for (int kw = 0; kw < 3; ++kw) {
+        float v[LD];
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh)
+        for (int p = 0; p < LD; ++p) v[p] = tb[(p * LH + kh) * ROW + kw];
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          const float *tp = tb + (kd * LH + kh) * LW + kw;
-          float v[TDx];
-#pragma unroll
-          for (int od = 0; od < TDx; ++od) v[od] = tp[od * S * LH * LW];
+        for (int kd = 0; kd < 3; ++kd) {
           const float *wp = wc + ((kd * 3 + kh) * 3 + kw) * COUT;
 #pragma unroll
           for (int co = 0; co < COUT; ++co) {
-            const float wv = wp[co];
+            const float wv_ = wp[co];
 #pragma unroll
-            for (int od = 0; od < TDx; ++od) acc[od][co] += wv * v[od];
+            for (int od = 0; od < TDx; ++od) acc[od][co] += wv_ * v[od * S + kd];
           }
         }
+      }
     }
+    if (ci + 1 < CIN) commit(ci + 1, buf ^ 1);
     __syncthreads();
   }
 
   const int w = w0 + tx_, h = h0 + ty;
-  double s[COUT], q[COUT];
+  float s[COUT], q[COUT];
 #pragma unroll
-  for (int c = 0; c < COUT; ++c) s[c] = q[c] = 0.0;
-  if (w < Wo && h < Ho) {
+  for (int c = 0; c < COUT; ++c) s[c] = q[c] = 0.0f;
+  if (tx_ < TWV && w < Wo && h < Ho) {
 #pragma unroll
     for (int od = 0; od < TDx; ++od) {
       const int d = d0 + od;
@@ -158,8 +226,8 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const float *__restrict__ i
 #pragma unroll
         for (int co = 0; co < COUT; ++co) {
           out[(((long)b * COUT + co) * Do + d) * (long)Ho * Wo + (long)h * Wo + w] = acc[od][co];
-          s[co] += (double)acc[od][co];
-          q[co] += (double)acc[od][co] * acc[od][co];
+          s[co] += acc[od][co];
+          q[co] += acc[od][co] * acc[od][co];
         }
       }
     }
@@ -171,66 +239,145 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const float *__restrict__ i
   }
 }
 
-// 1x1x1 conv over cat(Ta(a), trilinear_up(u)) -> COUT channels, + IN partial statistics.
-// The low-resolution branch u arrives already transformed (sa_vol_apply): evaluating its
-// gate at all 8 corners of every voxel made this kernel load-issue bound.
-template <int CA, int CU, int COUT, bool AX>
+// 1x1x1 conv with the producer's transform on load: out = W . T(in), no statistics.
+// Projects the low-resolution branch of an up-cat conv onto the output channels before it
+// is upsampled (W_u . up(T(u)) = up(W_u . T(u)): trilinear interpolation is linear).
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void pointwise_kernel(const float *__restrict__ in, InXform tx, int D, int H, int W,
+                                                        long n, const float *__restrict__ wt,
+                                                        float *__restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long dhw = (long)D * H * W;
+  const long b = i / dhw, pos = i - b * dhw;
+  const int w = (int)(pos % W), h = (int)((pos / W) % H), d = (int)(pos / ((long)W * H));
+  float r[COUT];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) r[co] = 0.0f;
+#pragma unroll 4
+  for (int c = 0; c < CIN; ++c) {
+    const long bc = b * CIN + c;
+    const float v = xform(in[bc * dhw + pos], tx, bc, d, h, w, H, W, D);
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) r[co] += wt[c * COUT + co] * v;
+  }
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) out[(b * COUT + co) * dhw + pos] = r[co];
+}
+
+// 1x1x1 conv over cat(Ta(a), trilinear_up(u)) -> COUT channels, + IN partial statistics,
+// evaluated as Wa . Ta(a) + up(p) with p = Wu . T(u) already at the low resolution
+// (pointwise_kernel).  The block's low-resolution footprint of p (at most 4 x 4 x 34
+// voxels for an upsampling factor >= 2) is staged in LDS as [d][h][w][co], so each
+// voxel's 8 trilinear corners are COUT/4 float4 reads apiece.
+template <int CA, int COUT, bool AX>
 __global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__restrict__ a, InXform ta,
-                                                              const float *__restrict__ u, int D, int H,
-                                                              int W, int Du, int Hu, int Wu, float sd, float sh,
-                                                              float sw, const float *__restrict__ wt,
-                                                              float *__restrict__ out, double *__restrict__ partial,
-                                                              int tilesD) {
+                                                              const float *__restrict__ pu, int D, int H, int W,
+                                                              int Du, int Hu, int Wu, float sd, float sh, float sw,
+                                                              const float *__restrict__ wt, float *__restrict__ out,
+                                                              double *__restrict__ partial, int tilesD) {
+  constexpr int TWV = TW;  // no halo: full, aligned 64-wide tiles
+  constexpr int ED = 4, EH = 4, EW = 34;
+  static_assert(COUT % 4 == 0, "float4 corners");
+  __shared__ float4 pt[ED * EH * EW * (COUT / 4)];
   __shared__ double red[COUT * 4 * 2];
-  const int tx_ = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int w = blockIdx.x * TW + tx_, h = blockIdx.y * TH + ty;
+  const int tx_ = threadIdx.x & 63;
+  const int ty = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // one H row per wave
+  const int w0 = blockIdx.x * TWV, h0 = blockIdx.y * TH;
+  const int w = w0 + tx_, h = h0 + ty;
   const int b = blockIdx.z / tilesD, d0 = (blockIdx.z % tilesD) * TD;
-  const long vol = (long)D * H * W, volu = (long)Du * Hu * Wu;
-  double s[COUT], q[COUT];
+  const long vol = (long)D * H * W;
+  // upsample_trilinear3d(align_corners=True): source index floor(s * dst), monotone in dst
+  const int dlo = (int)(sd * (float)d0), hlo = (int)(sh * (float)h0), wlo = (int)(sw * (float)w0);
+  {
+    float *ptf = reinterpret_cast<float *>(pt);
+    for (int i = threadIdx.x; i < ED * EH * EW * COUT; i += 256) {
+      const int ww = i % EW, r = i / EW, hh = r % EH, r2 = r / EH, dd = r2 % ED, co = r2 / ED;
+      const int dz = dlo + dd, hy = hlo + hh, wx = wlo + ww;
+      float v = 0.0f;
+      if (dz < Du && hy < Hu && wx < Wu) v = pu[(((long)b * COUT + co) * Du + dz) * (long)Hu * Wu + (long)hy * Wu + wx];
+      ptf[((dd * EH + hh) * EW + ww) * COUT + co] = v;
+    }
+  }
+  __syncthreads();
+  float s[COUT], q[COUT];
 #pragma unroll
-  for (int c = 0; c < COUT; ++c) s[c] = q[c] = 0.0;
-  if (w < W && h < H) {
-    // upsample_trilinear3d(align_corners=True) source coordinates (h, w fixed per thread)
-    const float rh = sh * (float)h, rw = sw * (float)w;
-    const int h1 = (int)rh, w1 = (int)rw;
-    const int h1p = h1 < Hu - 1 ? 1 : 0, w1p = w1 < Wu - 1 ? 1 : 0;
-    const float hl1 = rh - (float)h1, hl0 = 1.0f - hl1, wl1 = rw - (float)w1, wl0 = 1.0f - wl1;
-    for (int od = 0; od < TD; ++od) {
-      const int d = d0 + od;
-      if (d >= D) break;
-      const float rd = sd * (float)d;
-      const int d1 = (int)rd;
-      const int d1p = d1 < Du - 1 ? 1 : 0;
-      const float dl1 = rd - (float)d1, dl0 = 1.0f - dl1;
+  for (int c = 0; c < COUT; ++c) s[c] = q[c] = 0.0f;
+  const bool col_ok = tx_ < TWV && w < W && h < H;
+  const int wc = min(w, W - 1), hc = min(h, H - 1);
+  // Wa . Ta(a): all TD planes of this (h, w) column per input channel
+  float r[TD][COUT];
+#pragma unroll
+  for (int od = 0; od < TD; ++od)
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) r[od][co] = 0.0f;
+  const long pos0 = ((long)min(d0, D - 1) * H + hc) * W + wc;
+#pragma unroll 2
+  for (int c = 0; c < CA; ++c) {
+    const long bc = (long)b * CA + c;
+    const float *ap = a + bc * vol + pos0;
+    float av[TD];
+#pragma unroll
+    for (int od = 0; od < TD; ++od) av[od] = d0 + od < D ? ap[(long)od * H * W] : 0.0f;
+    if (AX) {
+      float mean = 0.0f, rstd = 1.0f, gl = 1.0f;
+      if (ta.mean) {
+        mean = ta.mean[bc];
+        rstd = ta.rstd[bc];
+      }
+      if (ta.gl) gl = ta.gl[(bc * H + hc) * W + wc];
+#pragma unroll
+      for (int od = 0; od < TD; ++od) {
+        float v = av[od];
+        if (ta.mean) v = (v - mean) * rstd;
+        if (ta.act) v = v > 0.0f ? v : v * ta.slope;
+        if (ta.gl) v = (gl * ta.gr[(bc * H + hc) * D + min(d0 + od, D - 1)]) * v;
+        av[od] = v;
+      }
+    }
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) {
+      const float wv_ = wt[c * COUT + co];
+#pragma unroll
+      for (int od = 0; od < TD; ++od) r[od][co] += wv_ * av[od];
+    }
+  }
+  // + up(p) from the LDS footprint
+  const float rh = sh * (float)hc, rw = sw * (float)wc;
+  const int h1 = (int)rh, w1 = (int)rw;
+  const int h1p = h1 < Hu - 1 ? 1 : 0, w1p = w1 < Wu - 1 ? 1 : 0;
+  const float hl1 = rh - (float)h1, hl0 = 1.0f - hl1, wl1 = rw - (float)w1, wl0 = 1.0f - wl1;
+  const int lh = h1 - hlo, lw = w1 - wlo;
+#pragma unroll
+  for (int od = 0; od < TD; ++od) {
+    const int d = d0 + od;
+    const float rd = sd * (float)min(d, D - 1);
+    const int d1 = (int)rd;
+    const int d1p = d1 < Du - 1 ? 1 : 0;
+    const float dl1 = rd - (float)d1, dl0 = 1.0f - dl1;
+    const float4 *c000 = pt + (((d1 - dlo) * EH + lh) * EW + lw) * (COUT / 4);
+    const int od_ = d1p * EH * EW * (COUT / 4), oh_ = h1p * EW * (COUT / 4), ow_ = w1p * (COUT / 4);
+#pragma unroll
+    for (int g = 0; g < COUT / 4; ++g) {
+      const float4 p000 = c000[g], p001 = c000[ow_ + g], p010 = c000[oh_ + g], p011 = c000[oh_ + ow_ + g];
+      const float4 p100 = c000[od_ + g], p101 = c000[od_ + ow_ + g], p110 = c000[od_ + oh_ + g],
+                   p111 = c000[od_ + oh_ + ow_ + g];
+#define SA_TRI(F)                                                                                 \
+  (dl0 * (hl0 * (wl0 * p000.F + wl1 * p001.F) + hl1 * (wl0 * p010.F + wl1 * p011.F)) +            \
+   dl1 * (hl0 * (wl0 * p100.F + wl1 * p101.F) + hl1 * (wl0 * p110.F + wl1 * p111.F)))
+      r[od][4 * g + 0] += SA_TRI(x);
+      r[od][4 * g + 1] += SA_TRI(y);
+      r[od][4 * g + 2] += SA_TRI(z);
+      r[od][4 * g + 3] += SA_TRI(w);
+#undef SA_TRI
+    }
+    if (col_ok && d < D) {
       const long pos = ((long)d * H + h) * W + w;
-      float r[COUT];
-#pragma unroll
-      for (int co = 0; co < COUT; ++co) r[co] = 0.0f;
-      // weights pre-arranged [cin][co] with the a-rows first
-#pragma unroll 1
-      for (int c = 0; c < CA; ++c) {
-        const long bc = (long)b * CA + c;
-        const float av = a[bc * vol + pos];
-        const float xv = AX ? xform(av, ta, bc, d, h, w, H, W, D) : av;
-#pragma unroll
-        for (int co = 0; co < COUT; ++co) r[co] += wt[c * COUT + co] * xv;
-      }
-      const long o000 = ((long)d1 * Hu + h1) * Wu + w1;
-      const long od_ = (long)d1p * Hu * Wu, oh_ = (long)h1p * Wu, ow_ = w1p;
-#pragma unroll 1
-      for (int c = 0; c < CU; ++c) {
-        const float *p = u + ((long)b * CU + c) * volu + o000;
-        const float xv = dl0 * (hl0 * (wl0 * p[0] + wl1 * p[ow_]) + hl1 * (wl0 * p[oh_] + wl1 * p[oh_ + ow_])) +
-                         dl1 * (hl0 * (wl0 * p[od_] + wl1 * p[od_ + ow_]) +
-                                hl1 * (wl0 * p[od_ + oh_] + wl1 * p[od_ + oh_ + ow_]));
-#pragma unroll
-        for (int co = 0; co < COUT; ++co) r[co] += wt[(CA + c) * COUT + co] * xv;
-      }
 #pragma unroll
       for (int co = 0; co < COUT; ++co) {
-        out[((long)b * COUT + co) * vol + pos] = r[co];
-        s[co] += (double)r[co];
-        q[co] += (double)r[co] * r[co];
+        out[((long)b * COUT + co) * vol + pos] = r[od][co];
+        s[co] += r[od][co];
+        q[co] += r[od][co] * r[od][co];
       }
     }
   }
@@ -285,17 +432,26 @@ __global__ __launch_bounds__(256) void instnorm_finalize_kernel(const double *__
 }
 
 struct ConvGeo {
-  int td, tw, th;
+  int td, tw, th;  // tw: threads along W (valid output columns: tw - 2 at stride 1, tw - 1 at 2)
+  int stride;
+  int valid_w() const { return tw - (stride == 1 ? 2 : 1); }
 };
 
 inline ConvGeo conv_geo(int cout, int stride) {
-  if (stride == 2) return {2, 32, 8};
-  return {cout >= 32 ? 2 : 4, 64, 4};
+  if (stride == 2) return {2, 32, 8, 2};
+  if (cout <= 8) return {8, 64, 4, 1};  // few outputs: longer D columns reuse each LDS read more
+  return {cout >= 32 ? 2 : 4, 64, 4, 1};
 }
 
 inline dim3 conv_grid(int B, int Do, int Ho, int Wo, ConvGeo g, int &tilesD) {
   tilesD = (Do + g.td - 1) / g.td;
-  return dim3((Wo + g.tw - 1) / g.tw, (Ho + g.th - 1) / g.th, tilesD * B);
+  return dim3((Wo + g.valid_w() - 1) / g.valid_w(), (Ho + g.th - 1) / g.th, tilesD * B);
+}
+
+// up-cat pointwise tiles: TD x TH x TW, aligned, no halo
+inline dim3 upcat_grid(int B, int D, int H, int W, int &tilesD) {
+  tilesD = (D + TD - 1) / TD;
+  return dim3((W + TW - 1) / TW, (H + TH - 1) / TH, tilesD * B);
 }
 
 inline int out_size(int n, int stride) { return (n - 1) / stride + 1; }  // k3, pad 1
@@ -308,6 +464,12 @@ extern "C" long sa_conv3d_stat_parts(int Cout, int stride, int Do, int Ho, int W
   return (long)g.x * g.y * g.z;
 }
 
+extern "C" long sa_conv3d_upcat_stat_parts(int D, int H, int W) {
+  int tilesD;
+  dim3 g = upcat_grid(1, D, H, W, tilesD);
+  return (long)g.x * g.y * g.z;
+}
+
 extern "C" int sa_conv3d(const float *in, int B, int Cin, int Di, int Hi, int Wi, int stride, const float *weight,
                          int Cout, const float *in_mean, const float *in_rstd, int act, float slope,
                          const float *gate_l, const float *gate_r, float *out, double *stats_partial, void *stream) {
@@ -315,6 +477,7 @@ extern "C" int sa_conv3d(const float *in, int B, int Cin, int Di, int Hi, int Wi
   SA_REQUIRE(B > 0 && Di > 0 && Hi > 0 && Wi > 0, "sa_conv3d: empty shape");
   SA_REQUIRE((in_mean == nullptr) == (in_rstd == nullptr), "sa_conv3d: mean and rstd go together");
   SA_REQUIRE((gate_l == nullptr) == (gate_r == nullptr), "sa_conv3d: both gate maps or none");
+  SA_REQUIRE((long)Di * Hi * Wi < (1L << 31), "sa_conv3d: a channel plane must hold < 2^31 voxels");
   const int Do = out_size(Di, stride), Ho = out_size(Hi, stride), Wo = out_size(Wi, stride);
   const ConvGeo geo = conv_geo(Cout, stride);
   int tilesD;
@@ -328,8 +491,8 @@ extern "C" int sa_conv3d(const float *in, int B, int Cin, int Di, int Hi, int Wi
                                                                 stats_partial, tilesD);                      \
     return sa::check_launch("sa_conv3d");                                                                    \
   }
-  SA_CONV(8, 8, 1, 4, 64, 4)
-  SA_CONV(8, 2, 1, 4, 64, 4)
+  SA_CONV(8, 8, 1, 8, 64, 4)
+  SA_CONV(8, 2, 1, 8, 64, 4)
   SA_CONV(16, 16, 1, 4, 64, 4)
   SA_CONV(32, 32, 1, 2, 64, 4)
   SA_CONV(8, 16, 2, 2, 32, 8)
@@ -339,33 +502,57 @@ extern "C" int sa_conv3d(const float *in, int B, int Cin, int Di, int Hi, int Wi
   return SA_E_ARG;
 }
 
+extern "C" int sa_conv3d_pointwise(const float *in, int B, int Cin, int D, int H, int W, const float *mean,
+                                   const float *rstd, int act, float slope, const float *gate_l, const float *gate_r,
+                                   const float *weight, int Cout, float *out, void *stream) {
+  SA_REQUIRE(in && weight && out && B > 0 && D > 0 && H > 0 && W > 0, "sa_conv3d_pointwise: bad arguments");
+  SA_REQUIRE((mean == nullptr) == (rstd == nullptr), "sa_conv3d_pointwise: mean and rstd go together");
+  SA_REQUIRE((gate_l == nullptr) == (gate_r == nullptr), "sa_conv3d_pointwise: both gate maps or none");
+  const long n = (long)B * D * H * W;
+  InXform tx{mean, rstd, gate_l, gate_r, slope, act};
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_CONV3D, s);
+#define SA_PJ(CI, CO)                                                                                        \
+  if (Cin == CI && Cout == CO) {                                                                             \
+    pointwise_kernel<CI, CO><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(in, tx, D, H, W, n, weight, out);   \
+    return sa::check_launch("sa_conv3d_pointwise");                                                         \
+  }
+  SA_PJ(16, 8)
+  SA_PJ(32, 16)
+#undef SA_PJ
+  sa::set_error("sa_conv3d_pointwise: no kernel built for %d -> %d", Cin, Cout);
+  return SA_E_ARG;
+}
+
 extern "C" int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_mean, const float *a_rstd, int a_act,
-                                         const float *a_gl, const float *a_gr, const float *u, int Cu, int Du, int Hu,
-                                         int Wu, int B, int D, int H, int W, float slope, const float *weight, int Cout,
+                                         const float *a_gl, const float *a_gr, const float *p, int Dp, int Hp, int Wp,
+                                         int B, int D, int H, int W, float slope, const float *weight, int Cout,
                                          float *out, double *stats_partial, void *stream) {
-  SA_REQUIRE(a && u && weight && out && stats_partial, "sa_conv3d_pointwise_upcat: null pointer");
-  SA_REQUIRE(B > 0 && D > 1 && H > 1 && W > 1 && Du > 0 && Hu > 0 && Wu > 0,
+  SA_REQUIRE(a && p && weight && out && stats_partial, "sa_conv3d_pointwise_upcat: null pointer");
+  SA_REQUIRE(B > 0 && D > 1 && H > 1 && W > 1 && Dp > 0 && Hp > 0 && Wp > 0,
              "sa_conv3d_pointwise_upcat: bad shape");
-  const ConvGeo geo = conv_geo(8, 1);
+  // the LDS footprint assumes upsampling by at least 2 along every axis
+  SA_REQUIRE(2 * (Dp - 1) <= D - 1 && 2 * (Hp - 1) <= H - 1 && 2 * (Wp - 1) <= W - 1,
+             "sa_conv3d_pointwise_upcat: the low-resolution branch must be at most half size");
   int tilesD;
-  dim3 grid = conv_grid(B, D, H, W, geo, tilesD);
+  dim3 grid = upcat_grid(B, D, H, W, tilesD);
   // area_pixel_compute_scale(align_corners=True) = (in - 1) / (out - 1)
-  const float sd = (float)(Du - 1) / (float)(D - 1), sh = (float)(Hu - 1) / (float)(H - 1),
-              sw = (float)(Wu - 1) / (float)(W - 1);
+  const float sd = (float)(Dp - 1) / (float)(D - 1), sh = (float)(Hp - 1) / (float)(H - 1),
+              sw = (float)(Wp - 1) / (float)(W - 1);
   InXform ta{a_mean, a_rstd, a_gl, a_gr, slope, a_act};
   const bool ax = a_mean || a_act || a_gl;
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV3D, s);
-#define SA_PW(CA, CU, CO, AXV)                                                                                     \
-  if (Ca == CA && Cu == CU && Cout == CO && ax == AXV) {                                                          \
-    pointwise_upcat_kernel<CA, CU, CO, AXV><<<grid, 256, 0, s>>>(a, ta, u, D, H, W, Du, Hu, Wu, sd, sh, sw,       \
-                                                                  weight, out, stats_partial, tilesD);             \
-    return sa::check_launch("sa_conv3d_pointwise_upcat");                                                         \
+#define SA_PW(CA, CO, AXV)                                                                                    \
+  if (Ca == CA && Cout == CO && ax == AXV) {                                                                 \
+    pointwise_upcat_kernel<CA, CO, AXV><<<grid, 256, 0, s>>>(a, ta, p, D, H, W, Dp, Hp, Wp, sd, sh, sw, weight, \
+                                                             out, stats_partial, tilesD);                    \
+    return sa::check_launch("sa_conv3d_pointwise_upcat");                                                    \
   }
-  SA_PW(8, 16, 8, false)
-  SA_PW(16, 32, 16, true)
+  SA_PW(8, 8, false)
+  SA_PW(16, 16, true)
 #undef SA_PW
-  sa::set_error("sa_conv3d_pointwise_upcat: no kernel built for %d + %d -> %d (a transform %d)", Ca, Cu, Cout, ax);
+  sa::set_error("sa_conv3d_pointwise_upcat: no kernel built for %d -> %d (a transform %d)", Ca, Cout, ax);
   return SA_E_ARG;
 }
 

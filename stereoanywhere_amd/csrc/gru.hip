@@ -16,6 +16,7 @@
 namespace {
 
 __global__ __launch_bounds__(256) void gru_zr_kernel(const float *__restrict__ xc, long xc_bs,
+                                                     const float *__restrict__ bx,
                                                      const float *__restrict__ hzr, long hzr_bs,
                                                      const float *__restrict__ cz, const float *__restrict__ cr,
                                                      long c_bs, const float *__restrict__ h, long h_bs,
@@ -25,7 +26,12 @@ __global__ __launch_bounds__(256) void gru_zr_kernel(const float *__restrict__ x
   if (i >= n) return;
   const long per = (long)C * HW;
   const long b = i / per, r = i % per;
-  const float zx = xc[b * xc_bs + r], rx = xc[b * xc_bs + per + r];
+  float zx = xc[b * xc_bs + r], rx = xc[b * xc_bs + per + r];
+  if (bx) {  // conv_x bias, added as MIOpen's conv + bias would (one rounding)
+    const int c = (int)((unsigned)r / (unsigned)HW);
+    zx = zx + bx[c];
+    rx = rx + bx[C + c];
+  }
   const float zh = hzr[b * hzr_bs + r], rhh = hzr[b * hzr_bs + per + r];
   const float zz = sa::sigmoidf_ref((zx + zh) + cz[b * c_bs + r]);
   const float rr = sa::sigmoidf_ref((rx + rhh) + cr[b * c_bs + r]);
@@ -34,6 +40,7 @@ __global__ __launch_bounds__(256) void gru_zr_kernel(const float *__restrict__ x
 }
 
 __global__ __launch_bounds__(256) void gru_out_kernel(const float *__restrict__ xc, long xc_bs,
+                                                      const float *__restrict__ bx,
                                                       const float *__restrict__ qh, long qh_bs,
                                                       const float *__restrict__ cq, long c_bs,
                                                       const float *__restrict__ z, int C, long HW, long n,
@@ -42,7 +49,9 @@ __global__ __launch_bounds__(256) void gru_out_kernel(const float *__restrict__ 
   if (i >= n) return;
   const long per = (long)C * HW;
   const long b = i / per, r = i % per;
-  const float q = tanhf((xc[b * xc_bs + 2 * per + r] + qh[b * qh_bs + r]) + cq[b * c_bs + r]);
+  float qx = xc[b * xc_bs + 2 * per + r];
+  if (bx) qx = qx + bx[2 * C + (int)((unsigned)r / (unsigned)HW)];
+  const float q = tanhf((qx + qh[b * qh_bs + r]) + cq[b * c_bs + r]);
   const float zz = z[i];
   const float hv = h[b * h_bs + r];
   h[b * h_bs + r] = (1.0f - zz) * hv + zz * q;
@@ -128,26 +137,27 @@ inline unsigned nblocks(long n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace
 
-extern "C" int sa_gru_zr(const float *xc, long xc_bs, const float *hzr, long hzr_bs, const float *cz,
+extern "C" int sa_gru_zr(const float *xc, long xc_bs, const float *bx, const float *hzr, long hzr_bs, const float *cz,
                          const float *cr, long c_bs, const float *h, long h_bs, int B, int C, int HW,
                          float *z, float *rh, void *stream) {
   SA_REQUIRE(xc && hzr && cz && cr && h && z && rh, "sa_gru_zr: null pointer");
   SA_REQUIRE(B > 0 && C > 0 && HW > 0, "sa_gru_zr: empty shape");
+  SA_REQUIRE((long)C * HW < (1L << 31), "sa_gru_zr: plane too large");
   const long n = (long)B * C * HW;
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_GRU_ZR, s);
-  gru_zr_kernel<<<nblocks(n), 256, 0, s>>>(xc, xc_bs, hzr, hzr_bs, cz, cr, c_bs, h, h_bs, C, HW, n, z, rh);
+  gru_zr_kernel<<<nblocks(n), 256, 0, s>>>(xc, xc_bs, bx, hzr, hzr_bs, cz, cr, c_bs, h, h_bs, C, HW, n, z, rh);
   return sa::check_launch("sa_gru_zr");
 }
 
-extern "C" int sa_gru_out(const float *xc, long xc_bs, const float *qh, long qh_bs, const float *cq, long c_bs,
+extern "C" int sa_gru_out(const float *xc, long xc_bs, const float *bx, const float *qh, long qh_bs, const float *cq, long c_bs,
                           const float *z, int B, int C, int HW, float *h, long h_bs, void *stream) {
   SA_REQUIRE(xc && qh && cq && z && h, "sa_gru_out: null pointer");
   SA_REQUIRE(B > 0 && C > 0 && HW > 0, "sa_gru_out: empty shape");
   const long n = (long)B * C * HW;
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_GRU_OUT, s);
-  gru_out_kernel<<<nblocks(n), 256, 0, s>>>(xc, xc_bs, qh, qh_bs, cq, c_bs, z, C, HW, n, h, h_bs);
+  gru_out_kernel<<<nblocks(n), 256, 0, s>>>(xc, xc_bs, bx, qh, qh_bs, cq, c_bs, z, C, HW, n, h, h_bs);
   return sa::check_launch("sa_gru_out");
 }
 

@@ -1,0 +1,119 @@
+"""Feature (fnet) and context (cnet) encoders with fused epilogues.
+
+The reference runs extractor.py:6-300 as nn.Modules: every Conv2d adds its bias in a
+separate pass, every norm is a statistics pass plus an apply pass, then a ReLU pass, and a
+residual block ends in an add pass and a ReLU pass — on tensors of 1 GB at full resolution
+for the 8-image feature batch.  Here the convolutions stay on MIOpen (fp32, bias dropped)
+and each conv output is finished by one ``ops.norm_act`` pass (plus one ``ops.plane_stats``
+read for InstanceNorm):
+
+  ResidualBlock (extractor.py:6-60):
+      y1  = relu(N1(conv1(x) + b1))                     -> norm_act(act_in=relu)
+      out = relu(relu(N2(conv2(y1) + b2)) + skip)        -> norm_act(act_in=relu, skip, act_out=relu)
+      skip = x, or N3(convd(x) + bd) applied inside the same pass (skip affine).
+
+InstanceNorm (affine=False) subtracts the per-plane mean, so a conv bias in front of it
+cancels and is not added.  BatchNorm runs in eval mode (running statistics, as the reference
+does under model.eval()) as (x - (running_mean - b)) * gamma / sqrt(running_var + eps) + beta.
+"""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+
+
+def _conv(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    return F.conv2d(x, conv.weight, None, conv.stride, conv.padding)
+
+
+def bn_affine(norm: nn.BatchNorm2d, conv_bias) -> ops.Affine:
+    """Eval BatchNorm of (conv + bias) as one per-channel affine."""
+    with torch.no_grad():
+        m = norm.running_mean - (conv_bias if conv_bias is not None else 0.0)
+        s = norm.weight / torch.sqrt(norm.running_var + norm.eps)
+        return ops.Affine(m.contiguous(), s.contiguous(), norm.bias.detach().contiguous())
+
+
+class _Finisher:
+    """Applies a layer's norm to a raw conv output: instance statistics computed here, batch
+    statistics looked up in the folded table."""
+
+    def __init__(self, kind: str, table: Dict[str, ops.Affine]):
+        self.kind, self.table = kind, table
+
+    def affine(self, name: str, raw: torch.Tensor) -> ops.Affine:
+        if self.kind == "instance":
+            mean, rstd = ops.plane_stats(raw)
+            return ops.Affine(mean, rstd, None, per_plane=True)
+        return self.table[name]
+
+
+def residual_block(blk: nn.Module, name: str, x: torch.Tensor, fin: _Finisher) -> torch.Tensor:
+    c1 = _conv(x, blk.conv1)
+    y1 = ops.norm_act(c1, fin.affine(name + ".norm1", c1), act_in="relu", out=c1)
+    c2 = _conv(y1, blk.conv2)
+    a2 = fin.affine(name + ".norm2", c2)
+    if blk.downsample is None:
+        return ops.norm_act(c2, a2, act_in="relu", skip=x, act_out="relu", out=c2)
+    d = _conv(x, blk.downsample[0])
+    return ops.norm_act(c2, a2, act_in="relu", skip=d, skip_aff=fin.affine(name + ".norm3", d), act_out="relu",
+                        out=c2)
+
+
+def _stem(enc: nn.Module, x: torch.Tensor, fin: _Finisher) -> torch.Tensor:
+    c = _conv(x, enc.conv1)
+    return ops.norm_act(c, fin.affine("norm1", c), act_in="relu", out=c)
+
+
+def _stage(seq: nn.Sequential, name: str, x: torch.Tensor, fin: _Finisher) -> torch.Tensor:
+    for i, blk in enumerate(seq):
+        x = residual_block(blk, f"{name}.{i}", x, fin)
+    return x
+
+
+def fnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine]) -> torch.Tensor:
+    """BasicEncoder.forward (extractor.py:62-153) -> [N, 256, H/4, W/4]."""
+    fin = _Finisher("instance" if isinstance(enc.norm1, nn.InstanceNorm2d) else "batch", table)
+    x = _stem(enc, x, fin)
+    for s in ("layer1", "layer2", "layer3"):
+        x = _stage(getattr(enc, s), s, x, fin)
+    return F.conv2d(x, enc.conv2.weight, enc.conv2.bias)
+
+
+def cnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine]) -> List[List[torch.Tensor]]:
+    """MultiBasicEncoder.forward (extractor.py:156-300) up to the head convs, whose outputs
+    are returned RAW (bias not added) as [[h08, c08], [h16, c16], [h32, c32]]; the caller
+    finishes them (tanh / relu with the bias) in one pass each."""
+    fin = _Finisher("instance" if isinstance(enc.norm1, nn.InstanceNorm2d) else "batch", table)
+    x = _stem(enc, x, fin)
+    for s in ("layer1", "layer2", "layer3"):
+        x = _stage(getattr(enc, s), s, x, fin)
+    s08 = x
+    s16 = _stage(enc.layer4, "layer4", s08, fin)
+    s32 = _stage(enc.layer5, "layer5", s16, fin)
+
+    def head(seq, i, name, feat):
+        r = residual_block(seq[0], f"{name}.{i}.0", feat, fin)
+        return _conv(r, seq[1])
+    return [[head(f, i, "outputs08", s08) for i, f in enumerate(enc.outputs08)],
+            [head(f, i, "outputs16", s16) for i, f in enumerate(enc.outputs16)],
+            [_conv(s32, f) for f in enc.outputs32]]
+
+
+def bn_table(enc: nn.Module) -> Dict[str, ops.Affine]:
+    """Folded BatchNorm affines of a batch-norm encoder (empty for instance norm)."""
+    if not isinstance(enc.norm1, nn.BatchNorm2d):
+        return {}
+    t = {"norm1": bn_affine(enc.norm1, enc.conv1.bias)}
+    for name, blk in enc.named_modules():
+        if name and hasattr(blk, "conv1") and hasattr(blk, "norm2"):
+            t[name + ".norm1"] = bn_affine(blk.norm1, blk.conv1.bias)
+            t[name + ".norm2"] = bn_affine(blk.norm2, blk.conv2.bias)
+            if blk.downsample is not None:
+                t[name + ".norm3"] = bn_affine(blk.norm3, blk.downsample[0].bias)
+    return t

@@ -30,7 +30,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import ops
+from . import encoders, ops
 from .blocks import BasicEncoder, BasicMultiUpdateBlock, Hourglass, HourglassIdentity, MultiBasicEncoder
 from .corr import HipCorrBlock1D, get_corr_block
 
@@ -88,9 +88,9 @@ class StereoAnywhere(nn.Module):
         )
 
     def _weights(self):
-        """Derived tensors (split GRU kernels, permuted classifier kernels), rebuilt when
-        any parameter is modified or moved."""
-        key = tuple((p.data_ptr(), p._version) for p in self.parameters())
+        """Derived tensors (split GRU kernels, permuted classifier kernels, folded BatchNorm),
+        rebuilt when any parameter or buffer is modified or moved."""
+        key = tuple((p.data_ptr(), p._version) for p in list(self.parameters()) + list(self.buffers()))
         if self._derived_key != key:
             ub = self.update_block
             hd = self.args.context_dims
@@ -108,6 +108,17 @@ class StereoAnywhere(nn.Module):
                     mot_w=torch.cat([ub.encoder._conv.weight,
                                      ub.encoder._conv.weight.new_zeros((2,) + ub.encoder._conv.weight.shape[1:])]),
                     mot_b=torch.cat([ub.encoder._conv.bias, ub.encoder._conv.bias.new_zeros(2)]),
+                )
+                enc = ub.encoder
+                self._derived.update(
+                    # folded eval-BatchNorm affines of the encoders (encoders.py)
+                    bn_cnet=encoders.bn_table(self.cnet), bn_fnet=encoders.bn_table(self.fnet),
+                    mot_b126=ub.encoder._conv.bias[:126].contiguous(),
+                    head_b=[(self.cnet.outputs08[0][1].bias, self.cnet.outputs08[1][1].bias),
+                            (self.cnet.outputs16[0][1].bias, self.cnet.outputs16[1][1].bias),
+                            (self.cnet.outputs32[0].bias, self.cnet.outputs32[1].bias)],
+                    bias_c1=ops.Affine(t=enc.convc1.bias), bias_c2=ops.Affine(t=enc.convc2.bias),
+                    bias_f2=ops.Affine(t=enc.convf2.bias), bias_fh1=ops.Affine(t=ub.flow_head.conv1.bias),
                 )
                 cls = torch.cat([self._derived["cls_d"], self._derived["cls_c"]], 0)  # [2,8,3,3,3]
                 self._derived["hg"] = self.hourglass_mono.fused_weights(cls)
@@ -160,11 +171,19 @@ class StereoAnywhere(nn.Module):
         n2 = ops.mono_normals(m2l, gain)
         n3 = ops.mono_normals(m3l, gain)
 
-        # ---- context + feature encoders (kept on MIOpen fp32)
-        cl = self.cnet(mde2.repeat(1, 3, 1, 1))
-        hid = [torch.tanh(x[0]).contiguous() for x in cl]
-        ctx = [conv(torch.relu(x[1])) for x, conv in zip(cl, self.context_zqr_convs)]  # [B,384,..]
-        fm = self.fnet(torch.cat([image2, image3], 0))
+        # ---- context + feature encoders: convs on MIOpen fp32, epilogues fused (encoders.py)
+        if self.cnet.training or self.fnet.training:  # batch-statistics BatchNorm: module path
+            cl = self.cnet(mde2.repeat(1, 3, 1, 1))
+            hid = [torch.tanh(x[0]).contiguous() for x in cl]
+            ctx = [conv(torch.relu(x[1])) for x, conv in zip(cl, self.context_zqr_convs)]
+            fm = self.fnet(torch.cat([image2, image3], 0))
+        else:
+            cl = encoders.cnet_forward(self.cnet, mde2.repeat(1, 3, 1, 1), dw["bn_cnet"])
+            hid, ctx = [], []
+            for (h_raw, c_raw), (hb, cb), conv in zip(cl, dw["head_b"], self.context_zqr_convs):
+                hid.append(ops.norm_act(h_raw, ops.Affine(t=hb), act_in="tanh", out=h_raw))
+                ctx.append(conv(ops.norm_act(c_raw, ops.Affine(t=cb), act_in="relu", out=c_raw)))  # [B,384,..]
+            fm = encoders.fnet_forward(self.fnet, torch.cat([image2, image3], 0), dw["bn_fnet"])
         fmap2, fmap3 = fm[:B].contiguous(), fm[B:].contiguous()
         feats_l = [F.interpolate(mde2, scale_factor=1 / 2 ** i, mode="bilinear", align_corners=True)
                    for i in range(a.n_downsample, len(self.feature_channels))]
@@ -238,11 +257,11 @@ class StereoAnywhere(nn.Module):
 
         def gru(level, h, x, key):
             g = dw["g" + key]
-            xc = F.conv2d(x, g["wx"], g["bx"], padding=1)
+            xc = F.conv2d(x, g["wx"], None, padding=1)  # bias added inside the gate kernels
             hzr = F.conv2d(h, g["whzr"], None, padding=1)
-            ops.gru_zr(xc, hzr, cz[level], cr[level], h, z[key], rh[key])
+            ops.gru_zr(xc, hzr, cz[level], cr[level], h, z[key], rh[key], bx=g["bx"])
             qh = F.conv2d(rh[key], g["wqh"], None, padding=1)
-            ops.gru_out(xc, qh, cq[level], z[key], h)
+            ops.gru_out(xc, qh, cq[level], z[key], h, bx=g["bx"])
 
         ops.flow_update(coords_x, None, flow, x08[:, 126:128])
         flow_up = None
@@ -255,15 +274,21 @@ class StereoAnywhere(nn.Module):
             ops.interp(h32, x16[:, 128:])
             gru(1, h16, x16, "16")
             # shared convc1/convc2 on the stereo and mono lookups as one 2B batch
-            c = F.relu(enc.convc1(corr_buf.view(2 * B, K, H4, W4)), inplace=True)
-            c = F.relu(enc.convc2(c), inplace=True).view(B, 128, H4, W4)
+            # conv + bias + ReLU as MIOpen conv (no bias) + one norm_act pass
+            c = F.conv2d(corr_buf.view(2 * B, K, H4, W4), enc.convc1.weight)
+            c = ops.norm_act(c, dw["bias_c1"], act_in="relu", out=c)
+            c = F.conv2d(c, enc.convc2.weight, None, padding=1)
+            c = ops.norm_act(c, dw["bias_c2"], act_in="relu", out=c).view(B, 128, H4, W4)
             fl = ops.conv2d_small(flow, dw["f1"], enc.convf1.bias, 64, 7, relu=True)
-            fl = F.relu(enc.convf2(fl), inplace=True)
-            mot = F.conv2d(torch.cat([c, fl], 1), dw["mot_w"], dw["mot_b"], padding=1)
-            ops.relu_copy(mot[:, :126], x08[:, :126])
+            fl = F.conv2d(fl, enc.convf2.weight, None, padding=1)
+            fl = ops.norm_act(fl, dw["bias_f2"], act_in="relu", out=fl)
+            mot = F.conv2d(torch.cat([c, fl], 1), dw["mot_w"], None, padding=1)
+            ops.norm_act(mot[:, :126], ops.Affine(t=dw["mot_b126"]), act_in="relu", out=x08[:, :126])
             ops.interp(h16, x08[:, 128:])
             gru(0, h08, x08, "08")
-            delta = ub.flow_head.conv2(F.relu(ub.flow_head.conv1(h08), inplace=True))
+            f1 = F.conv2d(h08, ub.flow_head.conv1.weight, None, padding=1)
+            f1 = ops.norm_act(f1, dw["bias_fh1"], act_in="relu", out=f1)
+            delta = ops.conv2d_k3_narrow(f1, ub.flow_head.conv2.weight, ub.flow_head.conv2.bias)
             ops.flow_update(coords_x, delta[:, 0:1], flow, x08[:, 126:128])
             if it == iters - 1:
                 mask = ub.mask(h08).mul_(0.25)

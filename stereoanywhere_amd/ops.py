@@ -217,17 +217,20 @@ def mono_scale_mirror(mde_lr: torch.Tensor, scale, shift, disp: torch.Tensor, co
 
 
 # ----------------------------------------------------------------------- a12 / a13 plumbing
-def gru_zr(xc, hzr, cz, cr, h, z_out, rh_out):
+def gru_zr(xc, hzr, cz, cr, h, z_out, rh_out, bx: Optional[torch.Tensor] = None):
+    """z = sigmoid(xc_z + bx_z + hzr_z + cz), r*h with r = sigmoid(xc_r + bx_r + hzr_r + cr)."""
     B, C, H, W = h.shape
-    N.call("sa_gru_zr", xc.data_ptr(), _plane_bs(xc, "xc"), hzr.data_ptr(), _plane_bs(hzr, "hzr"),
+    N.call("sa_gru_zr", xc.data_ptr(), _plane_bs(xc, "xc"), _ptr(bx), hzr.data_ptr(), _plane_bs(hzr, "hzr"),
            cz.data_ptr(), cr.data_ptr(), _plane_bs(cz, "cz"), h.data_ptr(), _plane_bs(h, "h"), B, C, H * W,
            z_out.data_ptr(), rh_out.data_ptr(), _stream(h))
 
 
-def gru_out(xc, qh, cq, z, h):
+def gru_out(xc, qh, cq, z, h, bx: Optional[torch.Tensor] = None):
+    """h = (1 - z) h + z tanh(xc_q + bx_q + qh + cq), in place."""
     B, C, H, W = h.shape
-    N.call("sa_gru_out", xc.data_ptr(), _plane_bs(xc, "xc"), qh.data_ptr(), _plane_bs(qh, "qh"), cq.data_ptr(),
-           _plane_bs(cq, "cq"), z.data_ptr(), B, C, H * W, h.data_ptr(), _plane_bs(h, "h"), _stream(h))
+    N.call("sa_gru_out", xc.data_ptr(), _plane_bs(xc, "xc"), _ptr(bx), qh.data_ptr(), _plane_bs(qh, "qh"),
+           cq.data_ptr(), _plane_bs(cq, "cq"), z.data_ptr(), B, C, H * W, h.data_ptr(), _plane_bs(h, "h"),
+           _stream(h))
 
 
 def pool2x(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
@@ -282,7 +285,6 @@ def float32_sqrt(x: float) -> float:
     return float(torch.sqrt(torch.tensor(float(x), dtype=torch.float32)))
 
 
-__all__ = [n for n in dir() if not n.startswith("_") and n not in ("annotations", "math", "torch")]
 
 
 # ----------------------------------------------------------------------- fused hourglass tail / convf1
@@ -342,20 +344,31 @@ def conv3d(x: "VolAct", w_t: torch.Tensor, cout: int, stride: int = 1, slope: fl
     return VolAct(out, norm, act=stats)
 
 
-def conv3d_pointwise_upcat(a: "VolAct", u: "VolAct", w_t: torch.Tensor, cout: int, slope: float = 0.01):
-    """1x1x1 conv over cat(T(a), trilinear_up(u)) -> VolAct(out, IN stats, act=True);
-    u must be materialised (identity transform, see vol_apply); w_t [Ca+Cu][Cout], a-rows first."""
-    if u.norm is not None or u.act or u.gate is not None:
-        raise RuntimeError("conv3d_pointwise_upcat: materialise u with vol_apply first")
+def conv3d_pointwise(x: "VolAct", w_t: torch.Tensor, cout: int, slope: float = 0.01) -> torch.Tensor:
+    """1x1x1 conv of T(x.raw) (no statistics); w_t [Cin][Cout]."""
+    _check(x.raw, "x")
+    _check(w_t, "w_t")
+    B, Cin, D, H, W = x.raw.shape
+    out = torch.empty((B, cout, D, H, W), device=x.raw.device, dtype=torch.float32)
+    a = x.args()
+    N.call("sa_conv3d_pointwise", x.raw.data_ptr(), B, Cin, D, H, W, a[0], a[1], a[2], slope, a[3], a[4],
+           w_t.data_ptr(), cout, out.data_ptr(), _stream(out))
+    return out
+
+
+def conv3d_pointwise_upcat(a: "VolAct", u: "VolAct", w_a: torch.Tensor, w_u: torch.Tensor, cout: int,
+                           slope: float = 0.01) -> "VolAct":
+    """1x1x1 conv over cat(T(a), trilinear_up(T(u))) -> VolAct(out, IN stats, act=True), as
+    Wa.T(a) + up(Wu.T(u)) (two launches); w_a [Ca][Cout], w_u [Cu][Cout]."""
     _check(a.raw, "a")
-    _check(u.raw, "u")
+    p = conv3d_pointwise(u, w_u, cout, slope)
     B, Ca, D, H, W = a.raw.shape
-    _, Cu, Du, Hu, Wu = u.raw.shape
+    _, _, Dp, Hp, Wp = p.shape
     out = torch.empty((B, cout, D, H, W), device=a.raw.device, dtype=torch.float32)
-    parts = conv3d_stat_parts(8, 1, D, H, W)
+    parts = int(N.lib().sa_conv3d_upcat_stat_parts(D, H, W))
     partial = torch.empty((B * cout * parts * 2,), device=out.device, dtype=torch.float64)
-    N.call("sa_conv3d_pointwise_upcat", a.raw.data_ptr(), Ca, *a.args(), u.raw.data_ptr(), Cu, Du, Hu, Wu, B, D,
-           H, W, slope, w_t.data_ptr(), cout, out.data_ptr(), partial.data_ptr(), _stream(out))
+    N.call("sa_conv3d_pointwise_upcat", a.raw.data_ptr(), Ca, *a.args(), p.data_ptr(), Dp, Hp, Wp, B, D,
+           H, W, slope, w_a.data_ptr(), cout, out.data_ptr(), partial.data_ptr(), _stream(out))
     return VolAct(out, instnorm_finalize(partial, B * cout, parts, D * H * W), act=True)
 
 
@@ -368,3 +381,65 @@ def conv2d_small(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor
     N.call("sa_conv2d_small", x.data_ptr(), bs, B, Cin, H, W, w_t.data_ptr(), _ptr(bias), cout, ksize,
            1 if relu else 0, out.data_ptr(), cout * H * W, _stream(x))
     return out
+
+
+# ----------------------------------------------------------------------- conv epilogues
+ACT = {None: 0, "none": 0, "relu": 1, "tanh": 2}
+
+
+def plane_stats(x: torch.Tensor, eps: float = 1e-5):
+    """InstanceNorm2d statistics of every (b, c) plane -> (mean, rstd), each [B*C]."""
+    bs = _plane_bs(x, "x")
+    B, C, H, W = x.shape
+    mean = torch.empty(B * C, device=x.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    N.call("sa_plane_stats", x.data_ptr(), bs, B, C, H * W, eps, mean.data_ptr(), rstd.data_ptr(), _stream(x))
+    return mean, rstd
+
+
+class Affine:
+    """(x - m) * s + t with per-channel (``per_plane=False``) or per-(b, c) parameters;
+    any of m / s / t may be None."""
+
+    def __init__(self, m=None, s=None, t=None, per_plane: bool = False):
+        self.m, self.s, self.t, self.per_plane = m, s, t, per_plane
+
+    def args(self, C: int):
+        return [_ptr(self.m), _ptr(self.s), _ptr(self.t), C if self.per_plane else 0]
+
+
+def norm_act(x: torch.Tensor, aff: Optional[Affine] = None, act_in=None, skip: Optional[torch.Tensor] = None,
+             skip_aff: Optional[Affine] = None, act_out=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = act_out(act_in(aff(x)) + skip_aff(skip)) in one pass (out may be x or a channel slice)."""
+    xb = _plane_bs(x, "x")
+    B, C, H, W = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    if tuple(out.shape) != (B, C, H, W):
+        raise RuntimeError(f"norm_act: out {tuple(out.shape)} != {(B, C, H, W)}")
+    ob = _plane_bs(out, "out")
+    sb = 0
+    if skip is not None:
+        if tuple(skip.shape) != (B, C, H, W):
+            raise RuntimeError("norm_act: skip shape mismatch")
+        sb = _plane_bs(skip, "skip")
+    a = (aff or Affine()).args(C)
+    sa_ = (skip_aff or Affine()).args(C)
+    N.call("sa_norm_act", x.data_ptr(), xb, B, C, H * W, *a, ACT[act_in], _ptr(skip), sb, *sa_, ACT[act_out],
+           out.data_ptr(), ob, _stream(x))
+    return out
+
+
+def conv2d_k3_narrow(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    """3x3 / pad 1 conv to 2 channels (weight [2, Cin, 3, 3] as stored by nn.Conv2d)."""
+    bs = _plane_bs(x, "x")
+    _check(weight, "weight")
+    B, Cin, H, W = x.shape
+    cout = weight.shape[0]
+    out = torch.empty((B, cout, H, W), device=x.device, dtype=torch.float32)
+    N.call("sa_conv2d_k3_narrow", x.data_ptr(), bs, B, Cin, H, W, weight.data_ptr(), _ptr(bias), cout,
+           out.data_ptr(), cout * H * W, _stream(x))
+    return out
+
+
+__all__ = [n for n in dir() if not n.startswith("_") and n not in ("annotations", "math", "torch")]

@@ -1,0 +1,122 @@
+"""Conv epilogue kernels (norm_act.hip, conv2d_k3_narrow, GRU bias) and the fused encoders
+against plain PyTorch fp32 on the GPU.  Tolerances: element-wise epilogues 1e-6 (one
+rounding order apart); normalised activations 1e-5 (fp64 vs fp32 statistics); encoder
+outputs 1e-4 relative (MIOpen convs without the bias pass, different norm rounding)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from stereoanywhere_amd import encoders, ops, synth
+from stereoanywhere_amd.blocks import BasicEncoder, MultiBasicEncoder
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def rnd(*shape, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.randn(*shape, generator=g).to(dev)
+
+
+def test_norm_act_forms():
+    B, C, H, W = 2, 6, 9, 13   # odd plane: scalar path
+    for hw_shape in ((H, W), (8, 12)):   # and the float4 path
+        x = rnd(B, C, *hw_shape, seed=1)
+        sk = rnd(B, C, *hw_shape, seed=2)
+        b = rnd(C, seed=3)
+        # bias + relu
+        torch.testing.assert_close(ops.norm_act(x, ops.Affine(t=b), act_in="relu"),
+                                   torch.relu(x + b[None, :, None, None]), atol=1e-6, rtol=0)
+        # bias + tanh, in place
+        y = x.clone()
+        ops.norm_act(y, ops.Affine(t=b), act_in="tanh", out=y)
+        torch.testing.assert_close(y, torch.tanh(x + b[None, :, None, None]), atol=1e-6, rtol=0)
+        # instance norm + relu + residual (identity) + relu
+        mean, rstd = ops.plane_stats(x)
+        ref_in = F.instance_norm(x)
+        out = ops.norm_act(x, ops.Affine(mean, rstd, None, per_plane=True), act_in="relu", skip=sk, act_out="relu")
+        torch.testing.assert_close(out, torch.relu(torch.relu(ref_in) + sk), atol=1e-5, rtol=1e-5)
+        # eval batch norm on both branches
+        bn1, bn2 = torch.nn.BatchNorm2d(C).to(dev).eval(), torch.nn.BatchNorm2d(C).to(dev).eval()
+        for bn, s in ((bn1, 4), (bn2, 5)):
+            with torch.no_grad():
+                bn.running_mean.copy_(rnd(C, seed=s))
+                bn.running_var.copy_(rnd(C, seed=s + 10).abs() + 0.5)
+                bn.weight.copy_(rnd(C, seed=s + 20))
+                bn.bias.copy_(rnd(C, seed=s + 30))
+        cb1, cb2 = rnd(C, seed=6), rnd(C, seed=7)
+        with torch.no_grad():
+            ref = torch.relu(torch.relu(bn1(x + cb1[None, :, None, None])) + bn2(sk + cb2[None, :, None, None]))
+        out = ops.norm_act(x, encoders.bn_affine(bn1, cb1), act_in="relu", skip=sk,
+                           skip_aff=encoders.bn_affine(bn2, cb2), act_out="relu")
+        torch.testing.assert_close(out, ref, atol=1e-5, rtol=1e-5)
+    # channel-slice views in and out
+    big = rnd(B, 10, 8, 12, seed=8)
+    dst = torch.zeros(B, 12, 8, 12, device=dev)
+    ops.norm_act(big[:, 2:8], ops.Affine(t=b), act_in="relu", out=dst[:, 4:10])
+    torch.testing.assert_close(dst[:, 4:10], torch.relu(big[:, 2:8] + b[None, :, None, None]), atol=1e-6, rtol=0)
+    assert float(dst[:, :4].abs().sum()) == 0.0 and float(dst[:, 10:].abs().sum()) == 0.0
+
+
+def test_plane_stats_matches_instance_norm():
+    x = rnd(3, 5, 37, 41, seed=11) * 3 + 1
+    mean, rstd = ops.plane_stats(x)
+    ref_m = x.mean(dim=(2, 3)).flatten()
+    ref_v = x.var(dim=(2, 3), unbiased=False).flatten()
+    torch.testing.assert_close(mean, ref_m, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(rstd, 1 / torch.sqrt(ref_v + 1e-5), atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("shape", [(2, 256, 17, 29), (1, 64, 8, 8), (4, 256, 34, 60)])
+def test_conv2d_k3_narrow(shape):
+    B, Cin, H, W = shape
+    x = rnd(*shape, seed=12)
+    w = rnd(2, Cin, 3, 3, seed=13) * 0.05
+    b = rnd(2, seed=14)
+    out = ops.conv2d_k3_narrow(x, w, b)
+    torch.testing.assert_close(out, F.conv2d(x, w, b, padding=1), atol=2e-5, rtol=1e-5)
+
+
+def test_gru_bias_inside_gates():
+    B, C, H, W = 2, 32, 6, 10
+    xc, hzr, ctx = rnd(B, 3 * C, H, W, seed=15), rnd(B, 2 * C, H, W, seed=16), rnd(B, 3 * C, H, W, seed=17)
+    h = torch.tanh(rnd(B, C, H, W, seed=18))
+    qh = rnd(B, C, H, W, seed=19)
+    bx = rnd(3 * C, seed=20)
+    xcb = xc + bx[None, :, None, None]
+    outs = []
+    for x_in, bias in ((xc, bx), (xcb, None)):
+        hh = h.clone()
+        z, rh = torch.empty_like(h), torch.empty_like(h)
+        ops.gru_zr(x_in, hzr, ctx[:, :C], ctx[:, C:2 * C], hh, z, rh, bx=bias)
+        ops.gru_out(x_in, qh, ctx[:, 2 * C:], z, hh, bx=bias)
+        outs.append((z, rh, hh))
+    for a, b in zip(*outs):   # bias inside the kernel == bias added beforehand, bit for bit
+        assert torch.equal(a, b)
+
+
+def _encoders():
+    torch.manual_seed(0)
+    fnet = BasicEncoder(256, "instance", 2)
+    cnet = MultiBasicEncoder(([128] * 3, [128] * 3), "batch", 2)
+    for m in (fnet, cnet):
+        synth.load_seeded_weights(m, 3)
+    return fnet.to(dev).eval(), cnet.to(dev).eval()
+
+
+def test_fused_encoders_match_modules():
+    fnet, cnet = _encoders()
+    x = rnd(2, 3, 64, 96, seed=21).clamp(-1, 1)
+    with torch.no_grad():
+        ref_f = fnet(x)
+        got_f = encoders.fnet_forward(fnet, x, encoders.bn_table(fnet))
+        torch.testing.assert_close(got_f, ref_f, atol=1e-4, rtol=1e-4)
+        ref_c = cnet(x)
+        got_c = encoders.cnet_forward(cnet, x, encoders.bn_table(cnet))
+        heads = [cnet.outputs08, cnet.outputs16, cnet.outputs32]
+        for lvl in range(3):
+            for j in range(2):
+                conv = heads[lvl][j][1] if lvl < 2 else heads[lvl][j]
+                got = got_c[lvl][j] + conv.bias[None, :, None, None]
+                torch.testing.assert_close(got, ref_c[lvl][j], atol=1e-4, rtol=1e-4)
