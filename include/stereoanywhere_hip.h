@@ -209,6 +209,16 @@ int sa_conv2d_small(const float *in, long in_bs, int B, int Cin, int H, int W, c
 int sa_conv2d_k3_narrow(const float *in, long in_bs, int B, int Cin, int H, int W, const float *weight,
                         const float *bias, int Cout, float *out, long out_bs, void *stream);
 
+/* 3x3 / stride 1 / pad 1 conv (encoders extractor.py:6-300, update block update.py:46-110)
+ * as fused Winograd F(2x2,3x3) on fp32 MFMA.  sa_conv2d_wino_weights transforms a
+ * [Cout][Cin][3][3] kernel (Cin % 8 == 0) once into U, 16*Cin*Cout floats laid out
+ * [16][Cin/8][4][Cout][2] (16-byte aligned); sa_conv2d_k3_wino:
+ * in [N,Cin,H,W] (batch stride in_bs) -> out [N,Cout,H,W] (batch stride out_bs), + bias
+ * (may be NULL), ReLU if relu != 0.  Needs Cin % 8 == 0 and Cout % 32 == 0. */
+int sa_conv2d_wino_weights(const float *weight, int Cout, int Cin, float *U, void *stream);
+int sa_conv2d_k3_wino(const float *in, long in_bs, int N, int Cin, int H, int W, const float *U,
+                      int Cout, const float *bias, int relu, float *out, long out_bs, void *stream);
+
 /* Epilogues of the MIOpen 2-D convs (encoders extractor.py:6-300, update block update.py:64-110).
  * sa_plane_stats: InstanceNorm2d statistics (biased variance, eps) of each (b, c) plane of
  *   x [B,C,hw] (batch stride x_bs) -> mean, rstd [B*C].
@@ -229,7 +239,7 @@ int sa_norm_act(const float *x, long x_bs, int B, int C, long hw, const float *m
  * recorded events and returns their summed duration (ms) and count, then clears. */
 enum {
   SA_K_CORR_PYRAMID = 0, SA_K_LOOKUP, SA_K_MONO_VOLUME, SA_K_SOFTARGMIN, SA_K_LSQ,
-  SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_NORM, SA_K_COUNT
+  SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_NORM, SA_K_CONV2D, SA_K_COUNT
 };
 int sa_timing_enable(int on);
 int sa_timing_read(int kernel_id, double *total_ms, long *count);

@@ -1,0 +1,298 @@
+// 3x3 / stride 1 / pad 1 convolution as fused Winograd F(2x2, 3x3) on fp32 MFMA.
+//
+// The 2-D convolutions of the encoders and the update block (extractor.py:6-300,
+// update.py:46-110) are ~3/4 of the forward's time; MIOpen runs them as its assembly
+// Winograd f2x3 kernels or NHWC implicit GEMM (+ layout transposes) at ~110 TF/s
+// direct-equivalent.  This kernel does the whole Winograd pipeline per block:
+//
+//   block  = 8 waves, output tile 8 x 32 pixels (64 Winograd tiles of 2x2) x 32 channels
+//   chunk  = 8 input channels: the 10 x 34 input patch -> LDS, input transform
+//            V = B^T d B (one (channel, tile) per thread) -> LDS as V[xi][ci][tile],
+//            transformed filters U[xi][ci][co] (sa_conv2d_wino_weights) -> LDS;
+//            the next chunk's global loads are in flight while this one multiplies
+//   MFMA   = v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulate): wave w owns
+//            16 tiles (one tile row) x 16 output channels for all 16 transform points,
+//            so the output transform Y = A^T M A runs in registers
+//   store  = + bias, optional ReLU, through LDS as 32-float rows (coalesced)
+//
+// 16 multiplies per 2x2 outputs instead of 36: the MFMA peak (157 TF/s fp32) is 354 TF/s
+// direct-equivalent.  Numerics: the same algorithm as MIOpen's f2x3 path (transform
+// coefficients 0, +-1, +-1/2); filters are transformed in fp64 and rounded once.
+// Block -> XCD: the 2-D grid is walked with a bijective XCD remap so that the output-channel
+// blocks of one spatial tile (which read the same input patch) share an XCD's L2.
+#include "sa_common.h"
+
+#pragma clang fp contract(fast)
+
+namespace {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+constexpr int OTH = 8, OTW = 32;             // output tile (pixels)
+constexpr int TR = OTH / 2, TC = OTW / 2;    // Winograd tiles: 4 rows x 16 cols
+constexpr int NT = TR * TC;                  // 64
+constexpr int KC = 8;                        // input channels per chunk
+constexpr int CO = 32;                       // output channels per block
+constexpr int PH = OTH + 2, PW = OTW + 2;    // input patch 10 x 34
+constexpr int XS = 36;                       // LDS row pitch of the patch
+constexpr int XCP = 384;                     // LDS channel-plane pitch (>= PH * XS, multiple of 64:
+                                             // channels c and c + 4 load as one ds_read2st64_b32)
+constexpr int NX = KC * PH * PW;             // 2720 patch values per chunk
+constexpr int XPT = (NX + 511) / 512;        // per thread (6)
+constexpr int NU4 = 16 * KC * CO / 4;        // 1024 float4 of U per chunk
+constexpr int UPT = NU4 / 512;               // 2
+// LDS images hold the two k-steps of an MFMA pair side by side (channel ci and ci + 4 of a
+// chunk), so one ds_read_b64 feeds two MFMAs.  Row pitches (in pairs) are 16 mod 32 so the
+// two k-rows a half-wave reads fall in disjoint bank halves (b64 bank = dword addr mod 64).
+constexpr int VP = NT + 16;                  // V[xi][ci%4][tile][ci/4]: 80 pairs per row
+constexpr int UP = CO + 16;                  // U[xi][ci%4][co][ci/4]:  48 pairs per row
+constexpr int COP = CO + 2;                  // output staging O[row][x][co]: 8*COP = 16 mod 32 banks
+
+// double-buffered: chunk k multiplies out of (v, u)[k & 1] while chunk k+1 is transformed
+// into (v)[(k+1) & 1]
+struct Smem {
+  float x[2][KC * XCP];           // input patch [ci][row][col]
+  float v[2][16 * 4 * VP * 2];    // V pairs; v[0] reused as the output tile O[co][row][col]
+  float u[2][16 * 4 * UP * 2];    // U pairs
+};
+static_assert(OTH * OTW * COP <= 16 * 4 * VP * 2, "output staging fits one V buffer");
+static_assert(sizeof(Smem) <= 160 * 1024, "LDS budget");
+
+#ifndef SA_WINO_WAVES_PER_EU
+#define SA_WINO_WAVES_PER_EU 2
+#endif
+
+__global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
+    const float *__restrict__ in, long in_bs, int Cin, int H, int W, const float *__restrict__ U, int Cout,
+    const float *__restrict__ bias, int relu, float *__restrict__ out, long out_bs, int tiles_w, int tiles_hw,
+    int co_blocks) {
+  __shared__ Smem sm;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // XCD-aware work order: consecutive work ids = the co blocks of one spatial tile
+  const unsigned wid = sa::xcd_remap(blockIdx.x, gridDim.x);
+  const int cb = wid % co_blocks;
+  const int st = (wid / co_blocks) % tiles_hw;
+  const int n = wid / (co_blocks * tiles_hw);
+  const int y0 = (st / tiles_w) * OTH, x0 = (st % tiles_w) * OTW;
+  const int co0 = cb * CO;
+  const float *src = in + (long)n * in_bs;
+  const long hw = (long)H * W;
+
+  // ---- per-thread load slots, fixed for all chunks: 32-bit byte offsets from the chunk's
+  // channel-0 plane (clamped inside the image; padding selected at commit), read with buffer
+  // loads (scalar base + chunk offset, no per-load address arithmetic)
+  const __amdgpu_buffer_rsrc_t xin = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(src), (short)0, (int)((long)Cin * hw * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t uin = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(U), (short)0, (int)(16L * Cin * Cout * 4), 0x00020000);
+  int xo[XPT], xl[XPT];   // global byte offset, LDS slot (-1: no slot)
+  unsigned xpad = 0;
+#pragma unroll
+  for (int j = 0; j < XPT; ++j) {
+    const int i = min(tid + 512 * j, NX - 1);
+    const int ci = i / (PH * PW), r = (i / PW) % PH, cc = i % PW;
+    const int y = y0 - 1 + r, x = x0 - 1 + cc;
+    xo[j] = (ci * (int)hw + min(max(y, 0), H - 1) * W + min(max(x, 0), W - 1)) * 4;
+    xl[j] = tid + 512 * j < NX ? ci * XCP + r * XS + cc : -1;
+    if (y < 0 || y >= H || x < 0 || x >= W) xpad |= 1u << j;
+  }
+  // U chunk image: global [xi][Cin/8][4][Cout][2] -> rows of 32 co pairs (64 floats)
+  int uo[UPT];
+#pragma unroll
+  for (int j = 0; j < UPT; ++j) {
+    const int i4 = tid + 512 * j;               // 1024 float4 = 16 xi x 4 ci4 x 16 (co pair halves)
+    const int q = i4 & 15, ci4 = (i4 >> 4) & 3, xi = i4 >> 6;
+    uo[j] = (((xi * (Cin / KC)) * 4 + ci4) * Cout * 2 + co0 * 2 + q * 4) * 4;
+  }
+  float xr[XPT];
+  f32x4 ur[UPT];
+  auto fetch = [&](int chunk) __attribute__((always_inline)) {
+    const int xs = chunk * KC * (int)hw * 4, us = chunk * 4 * Cout * 2 * 4;
+#pragma unroll
+    for (int j = 0; j < XPT; ++j) xr[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xin, xo[j], xs, 0));
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+      const auto w = __builtin_amdgcn_raw_buffer_load_b128(uin, uo[j], us, 0);
+      ur[j] = f32x4{__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3])};
+    }
+  };
+  auto commit = [&](int buf) __attribute__((always_inline)) {
+    float *xs = sm.x[buf];
+#pragma unroll
+    for (int j = 0; j < XPT; ++j)
+      if (xl[j] >= 0) xs[xl[j]] = ((xpad >> j) & 1u) ? 0.0f : xr[j];
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+      const int i4 = tid + 512 * j;
+      const int q = i4 & 15, row = i4 >> 4;  // row = xi * 4 + ci4
+      *reinterpret_cast<f32x4 *>(sm.u[buf] + row * UP * 2 + q * 4) = ur[j];
+    }
+  };
+  // input transform V = B^T d B of (channel tid >> 6, tile tid & 63) into its slot of the
+  // (c, c + 4) pair image; every thread has one job per chunk
+  auto transform = [&](int buf) __attribute__((always_inline)) {
+    const int ci = tid >> 6, t = tid & 63;
+    const int ty = t / TC, tx = t % TC;
+    const float *p = sm.x[buf] + ci * XCP + 2 * ty * XS + 2 * tx;
+    float d[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) d[r][c] = p[r * XS + c];
+    // B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]
+    float w[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      w[0][c] = d[0][c] - d[2][c];
+      w[1][c] = d[1][c] + d[2][c];
+      w[2][c] = d[2][c] - d[1][c];
+      w[3][c] = d[1][c] - d[3][c];
+    }
+    float *o = sm.v[buf] + ((ci & 3) * VP + t) * 2 + (ci >> 2);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      o[((r * 4 + 0) * 4) * VP * 2] = w[r][0] - w[r][2];
+      o[((r * 4 + 1) * 4) * VP * 2] = w[r][1] + w[r][2];
+      o[((r * 4 + 2) * 4) * VP * 2] = w[r][2] - w[r][1];
+      o[((r * 4 + 3) * 4) * VP * 2] = w[r][1] - w[r][3];
+    }
+  };
+
+  f32x4 acc[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int tg = wv & 3, cg = wv >> 2;                 // tile row, co half
+  const int ak = lane >> 4, am = lane & 15;            // operand lane map (16x16x4)
+  const int a_off = ak * VP + tg * TC + am, b_off = ak * UP + cg * 16 + am;
+
+  // software pipeline: iteration k = [sync, commit chunk k+1, issue loads of chunk k+2, sync,
+  // MFMA chunk k || transform chunk k+1]
+  const int nchunks = Cin / KC;
+  fetch(0);
+  commit(0);
+  if (nchunks > 1) fetch(1);
+  __syncthreads();
+  transform(0);
+#pragma unroll 1
+  for (int k = 0; k < nchunks; ++k) {
+    const int cur = k & 1, nxt = cur ^ 1;
+    __syncthreads();                     // chunk k transformed; chunk k-1's buffers free
+    if (k + 1 < nchunks) commit(nxt);    // registers hold chunk k+1
+    if (k + 2 < nchunks) fetch(k + 2);
+    __syncthreads();
+    const float2 *va = reinterpret_cast<const float2 *>(sm.v[cur]) + a_off;
+    const float2 *ubp = reinterpret_cast<const float2 *>(sm.u[cur]) + b_off;
+    float2 a[16], b[16];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) {
+      a[xi] = va[xi * 4 * VP];
+      b[xi] = ubp[xi * 4 * UP];
+    }
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) acc[xi] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[xi].x, b[xi].x, acc[xi], 0, 0, 0);
+    transform(nxt);  // unconditional (the last one fills an idle buffer) so it shares the MFMAs' block
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) acc[xi] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[xi].y, b[xi].y, acc[xi], 0, 0, 0);
+  }
+  __syncthreads();
+
+  // ---- output transform in registers: lane holds tiles (tg, 4*(lane>>4) + r), channel cg*16 + (lane&15)
+  float *ot = sm.v[0];  // reuse: O[row][x][co]
+  const int col = cg * 16 + (lane & 15);
+  const float bv = bias ? bias[co0 + col] : 0.0f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int tx = 4 * (lane >> 4) + r;
+    float m[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) m[a][b] = acc[a * 4 + b][r];
+    // A^T = [[1,1,1,0],[0,1,-1,-1]]
+    float t0[4], t1[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      t0[b] = m[0][b] + m[1][b] + m[2][b];
+      t1[b] = m[1][b] - m[2][b] - m[3][b];
+    }
+    float y[2][2];
+    y[0][0] = t0[0] + t0[1] + t0[2];
+    y[0][1] = t0[1] - t0[2] - t0[3];
+    y[1][0] = t1[0] + t1[1] + t1[2];
+    y[1][1] = t1[1] - t1[2] - t1[3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        float v = y[i][j] + bv;
+        if (relu) v = fmaxf(v, 0.0f);
+        ot[((2 * tg + i) * OTW + 2 * tx + j) * COP + col] = v;
+      }
+  }
+  __syncthreads();
+  // 32 channels x 8 rows x 32 columns, one row-segment of 32 floats per half-wave
+  float *dst = out + (long)n * out_bs;
+#pragma unroll
+  for (int j = 0; j < (CO * OTH * OTW) / 512; ++j) {
+    const int i = tid + 512 * j;
+    const int cx = i % OTW, r = (i / OTW) % OTH, c = i / (OTW * OTH);
+    const int y = y0 + r, x = x0 + cx;
+    if (y < H && x < W) dst[(long)(co0 + c) * hw + (long)y * W + x] = ot[(r * OTW + cx) * COP + c];
+  }
+}
+
+// U = (G g G^T) for g = w[co][ci] (3x3), in fp64, rounded once
+__global__ __launch_bounds__(256) void wino_weights_kernel(const float *__restrict__ w, int Cout, int Cin,
+                                                           float *__restrict__ U) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)Cout * Cin) return;
+  const int co = (int)(i / Cin), ci = (int)(i % Cin);
+  const float *g = w + i * 9;
+  // G = [[1,0,0],[1/2,1/2,1/2],[1/2,-1/2,1/2],[0,0,1]]
+  double t[4][3];
+  for (int c = 0; c < 3; ++c) {
+    const double g0 = g[c], g1 = g[3 + c], g2 = g[6 + c];
+    t[0][c] = g0;
+    t[1][c] = 0.5 * (g0 + g1 + g2);
+    t[2][c] = 0.5 * (g0 - g1 + g2);
+    t[3][c] = g2;
+  }
+  for (int r = 0; r < 4; ++r) {
+    const double u0 = t[r][0], u1 = 0.5 * (t[r][0] + t[r][1] + t[r][2]), u2 = 0.5 * (t[r][0] - t[r][1] + t[r][2]),
+                 u3 = t[r][2];
+    const double u[4] = {u0, u1, u2, u3};
+    // layout [xi][Cin/8][ci%4][Cout][(ci%8)/4]: the chunk image the conv kernel stages
+    for (int c = 0; c < 4; ++c)
+      U[((((long)(r * 4 + c) * (Cin / 8) + ci / 8) * 4 + (ci % 4)) * Cout + co) * 2 + (ci % 8) / 4] = (float)u[c];
+  }
+}
+
+}  // namespace
+
+extern "C" int sa_conv2d_wino_weights(const float *weight, int Cout, int Cin, float *U, void *stream) {
+  SA_REQUIRE(weight && U && Cout > 0 && Cin > 0 && Cin % 8 == 0, "sa_conv2d_wino_weights: bad arguments (Cin %% 8)");
+  const long n = (long)Cout * Cin;
+  hipStream_t s = sa::as_stream(stream);
+  wino_weights_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(weight, Cout, Cin, U);
+  return sa::check_launch("sa_conv2d_wino_weights");
+}
+
+extern "C" int sa_conv2d_k3_wino(const float *in, long in_bs, int N, int Cin, int H, int W, const float *U, int Cout,
+                                 const float *bias, int relu, float *out, long out_bs, void *stream) {
+  SA_REQUIRE(in && U && out && N > 0 && H > 0 && W > 0, "sa_conv2d_k3_wino: bad arguments");
+  SA_REQUIRE(Cin % KC == 0 && Cout % CO == 0, "sa_conv2d_k3_wino: needs Cin %% 8 == 0 and Cout %% 32 == 0 (got %d, %d)",
+             Cin, Cout);
+  SA_REQUIRE((reinterpret_cast<uintptr_t>(U) & 15) == 0, "sa_conv2d_k3_wino: U must be 16-byte aligned");
+  SA_REQUIRE((long)Cin * H * W * 4 < (1L << 31) && 16L * Cin * Cout * 4 < (1L << 31),
+             "sa_conv2d_k3_wino: an image or the filter bank exceeds the 2 GB buffer-descriptor range");
+  const int tiles_w = (W + OTW - 1) / OTW, tiles_h = (H + OTH - 1) / OTH;
+  const int co_blocks = Cout / CO;
+  const long nblk = (long)N * tiles_w * tiles_h * co_blocks;
+  SA_REQUIRE(nblk < (1L << 31), "sa_conv2d_k3_wino: grid too large");
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_CONV2D, s);
+  wino_f2k3_kernel<<<(unsigned)nblk, 512, 0, s>>>(in, in_bs, Cin, H, W, U, Cout, bias, relu, out, out_bs, tiles_w,
+                                                  tiles_w * tiles_h, co_blocks);
+  return sa::check_launch("sa_conv2d_k3_wino");
+}

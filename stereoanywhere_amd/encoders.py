@@ -27,7 +27,31 @@ import torch.nn.functional as F
 from . import ops
 
 
+# Winograd-transformed filters of the eligible 3x3 convs (ops.conv2d_k3), keyed by the
+# module's weight storage; filled by StereoAnywhere._weights()
+WinoTable = Dict[int, torch.Tensor]
+
+
+def wino_eligible(conv: nn.Conv2d) -> bool:
+    """3x3 / stride 1 / pad 1 / dense convs with Cin % 8 == 0 and Cout % 32 == 0."""
+    return (conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.in_channels % 8 == 0
+            and conv.out_channels % 32 == 0)
+
+
+def wino_table(*modules: nn.Module) -> WinoTable:
+    return {m.weight.data_ptr(): ops.wino_weights(m.weight.detach().contiguous())
+            for mod in modules for m in mod.modules() if isinstance(m, nn.Conv2d) and wino_eligible(m)}
+
+
+_WINO: WinoTable = {}
+
+
 def _conv(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    """conv without bias: fused Winograd when the layer qualifies, else MIOpen."""
+    U = _WINO.get(conv.weight.data_ptr())
+    if U is not None:
+        return ops.conv2d_k3(x, U)
     return F.conv2d(x, conv.weight, None, conv.stride, conv.padding)
 
 
@@ -76,8 +100,11 @@ def _stage(seq: nn.Sequential, name: str, x: torch.Tensor, fin: _Finisher) -> to
     return x
 
 
-def fnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine]) -> torch.Tensor:
+def fnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
+                 wino: WinoTable = None) -> torch.Tensor:
     """BasicEncoder.forward (extractor.py:62-153) -> [N, 256, H/4, W/4]."""
+    _WINO.clear()
+    _WINO.update(wino or {})
     fin = _Finisher("instance" if isinstance(enc.norm1, nn.InstanceNorm2d) else "batch", table)
     x = _stem(enc, x, fin)
     for s in ("layer1", "layer2", "layer3"):
@@ -85,10 +112,13 @@ def fnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine]) 
     return F.conv2d(x, enc.conv2.weight, enc.conv2.bias)
 
 
-def cnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine]) -> List[List[torch.Tensor]]:
+def cnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
+                 wino: WinoTable = None) -> List[List[torch.Tensor]]:
     """MultiBasicEncoder.forward (extractor.py:156-300) up to the head convs, whose outputs
     are returned RAW (bias not added) as [[h08, c08], [h16, c16], [h32, c32]]; the caller
     finishes them (tanh / relu with the bias) in one pass each."""
+    _WINO.clear()
+    _WINO.update(wino or {})
     fin = _Finisher("instance" if isinstance(enc.norm1, nn.InstanceNorm2d) else "batch", table)
     x = _stem(enc, x, fin)
     for s in ("layer1", "layer2", "layer3"):

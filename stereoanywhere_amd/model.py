@@ -120,6 +120,18 @@ class StereoAnywhere(nn.Module):
                     bias_c1=ops.Affine(t=enc.convc1.bias), bias_c2=ops.Affine(t=enc.convc2.bias),
                     bias_f2=ops.Affine(t=enc.convf2.bias), bias_fh1=ops.Affine(t=ub.flow_head.conv1.bias),
                 )
+                # Winograd F(2x2,3x3) filters (ops.conv2d_k3) of every eligible 3x3 conv
+                d = self._derived
+                d["wino"] = encoders.wino_table(self.cnet, self.fnet)
+                for key in ("g08", "g16", "g32"):
+                    g = d[key]
+                    g.update(Ux=ops.wino_weights(g["wx"]), Uhzr=ops.wino_weights(g["whzr"]),
+                             Uqh=ops.wino_weights(g["wqh"]))
+                d.update(U_c2=ops.wino_weights(enc.convc2.weight.detach().contiguous()),
+                         U_f2=ops.wino_weights(enc.convf2.weight.detach().contiguous()),
+                         U_mot=ops.wino_weights(d["mot_w"]),
+                         U_fh1=ops.wino_weights(ub.flow_head.conv1.weight.detach().contiguous()),
+                         U_ctx=[ops.wino_weights(c.weight.detach().contiguous()) for c in self.context_zqr_convs])
                 cls = torch.cat([self._derived["cls_d"], self._derived["cls_c"]], 0)  # [2,8,3,3,3]
                 self._derived["hg"] = self.hourglass_mono.fused_weights(cls)
             self._derived_key = key
@@ -178,12 +190,13 @@ class StereoAnywhere(nn.Module):
             ctx = [conv(torch.relu(x[1])) for x, conv in zip(cl, self.context_zqr_convs)]
             fm = self.fnet(torch.cat([image2, image3], 0))
         else:
-            cl = encoders.cnet_forward(self.cnet, mde2.repeat(1, 3, 1, 1), dw["bn_cnet"])
+            cl = encoders.cnet_forward(self.cnet, mde2.repeat(1, 3, 1, 1), dw["bn_cnet"], dw["wino"])
             hid, ctx = [], []
-            for (h_raw, c_raw), (hb, cb), conv in zip(cl, dw["head_b"], self.context_zqr_convs):
+            for (h_raw, c_raw), (hb, cb), conv, U in zip(cl, dw["head_b"], self.context_zqr_convs, dw["U_ctx"]):
                 hid.append(ops.norm_act(h_raw, ops.Affine(t=hb), act_in="tanh", out=h_raw))
-                ctx.append(conv(ops.norm_act(c_raw, ops.Affine(t=cb), act_in="relu", out=c_raw)))  # [B,384,..]
-            fm = encoders.fnet_forward(self.fnet, torch.cat([image2, image3], 0), dw["bn_fnet"])
+                c = ops.norm_act(c_raw, ops.Affine(t=cb), act_in="relu", out=c_raw)
+                ctx.append(ops.conv2d_k3(c, U, conv.bias))  # [B,384,..]
+            fm = encoders.fnet_forward(self.fnet, torch.cat([image2, image3], 0), dw["bn_fnet"], dw["wino"])
         fmap2, fmap3 = fm[:B].contiguous(), fm[B:].contiguous()
         feats_l = [F.interpolate(mde2, scale_factor=1 / 2 ** i, mode="bilinear", align_corners=True)
                    for i in range(a.n_downsample, len(self.feature_channels))]
@@ -257,10 +270,10 @@ class StereoAnywhere(nn.Module):
 
         def gru(level, h, x, key):
             g = dw["g" + key]
-            xc = F.conv2d(x, g["wx"], None, padding=1)  # bias added inside the gate kernels
-            hzr = F.conv2d(h, g["whzr"], None, padding=1)
+            xc = ops.conv2d_k3(x, g["Ux"])  # bias added inside the gate kernels
+            hzr = ops.conv2d_k3(h, g["Uhzr"])
             ops.gru_zr(xc, hzr, cz[level], cr[level], h, z[key], rh[key], bx=g["bx"])
-            qh = F.conv2d(rh[key], g["wqh"], None, padding=1)
+            qh = ops.conv2d_k3(rh[key], g["Uqh"])
             ops.gru_out(xc, qh, cq[level], z[key], h, bx=g["bx"])
 
         ops.flow_update(coords_x, None, flow, x08[:, 126:128])
@@ -277,19 +290,19 @@ class StereoAnywhere(nn.Module):
             # conv + bias + ReLU as MIOpen conv (no bias) + one norm_act pass
             c = F.conv2d(corr_buf.view(2 * B, K, H4, W4), enc.convc1.weight)
             c = ops.norm_act(c, dw["bias_c1"], act_in="relu", out=c)
-            c = F.conv2d(c, enc.convc2.weight, None, padding=1)
-            c = ops.norm_act(c, dw["bias_c2"], act_in="relu", out=c).view(B, 128, H4, W4)
+            # 3x3 convs with bias + ReLU in the Winograd epilogue
+            c = ops.conv2d_k3(c, dw["U_c2"], enc.convc2.bias, relu=True).view(B, 128, H4, W4)
             fl = ops.conv2d_small(flow, dw["f1"], enc.convf1.bias, 64, 7, relu=True)
-            fl = F.conv2d(fl, enc.convf2.weight, None, padding=1)
-            fl = ops.norm_act(fl, dw["bias_f2"], act_in="relu", out=fl)
-            mot = F.conv2d(torch.cat([c, fl], 1), dw["mot_w"], None, padding=1)
-            ops.norm_act(mot[:, :126], ops.Affine(t=dw["mot_b126"]), act_in="relu", out=x08[:, :126])
+            fl = ops.conv2d_k3(fl, dw["U_f2"], enc.convf2.bias, relu=True)
+            # _conv (126 outputs, padded to 128) writes x08[:, :128]; channels 126-127 (the flow)
+            # are rewritten right after from the coordinates
+            ops.conv2d_k3(torch.cat([c, fl], 1), dw["U_mot"], dw["mot_b"], relu=True, out=x08[:, :128])
+            ops.flow_update(coords_x, None, None, x08[:, 126:128])
             ops.interp(h16, x08[:, 128:])
             gru(0, h08, x08, "08")
-            f1 = F.conv2d(h08, ub.flow_head.conv1.weight, None, padding=1)
-            f1 = ops.norm_act(f1, dw["bias_fh1"], act_in="relu", out=f1)
+            f1 = ops.conv2d_k3(h08, dw["U_fh1"], ub.flow_head.conv1.bias, relu=True)
             delta = ops.conv2d_k3_narrow(f1, ub.flow_head.conv2.weight, ub.flow_head.conv2.bias)
-            ops.flow_update(coords_x, delta[:, 0:1], flow, x08[:, 126:128])
+            ops.flow_update(coords_x, delta[:, 0:1], flow, None)
             if it == iters - 1:
                 mask = ub.mask(h08).mul_(0.25)
                 flow_up = ops.convex_upsample(flow[:, 0:1].contiguous(), mask, 2 ** self.args.n_downsample)

@@ -442,4 +442,32 @@ def conv2d_k3_narrow(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch
     return out
 
 
+def wino_weights(weight: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, 3, 3] -> Winograd F(2x2,3x3) filters U (fp64 transform), a [16, Cin, Cout]
+    container whose storage is the kernel's chunk layout [16][Cin/8][4][Cout][2]."""
+    _check(weight, "weight")
+    Cout, Cin = weight.shape[:2]
+    U = torch.empty((16, Cin, Cout), device=weight.device, dtype=torch.float32)
+    N.call("sa_conv2d_wino_weights", weight.data_ptr(), Cout, Cin, U.data_ptr(), _stream(weight))
+    return U
+
+
+def conv2d_k3(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = None, relu: bool = False,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """3x3 / pad 1 conv via fused Winograd (U from wino_weights); + bias, optional ReLU."""
+    bs = _plane_bs(x, "x")
+    _check(U, "U")
+    B, Cin, H, W = x.shape
+    Cout = U.shape[2]
+    if U.shape[1] != Cin:
+        raise RuntimeError(f"conv2d_k3: U has {U.shape[1]} input channels, x has {Cin}")
+    if out is None:
+        out = torch.empty((B, Cout, H, W), device=x.device, dtype=torch.float32)
+    if tuple(out.shape) != (B, Cout, H, W):
+        raise RuntimeError("conv2d_k3: out shape mismatch")
+    N.call("sa_conv2d_k3_wino", x.data_ptr(), bs, B, Cin, H, W, U.data_ptr(), Cout, _ptr(bias), 1 if relu else 0,
+           out.data_ptr(), _plane_bs(out, "out"), _stream(x))
+    return out
+
+
 __all__ = [n for n in dir() if not n.startswith("_") and n not in ("annotations", "math", "torch")]

@@ -1,0 +1,46 @@
+"""Fused Winograd F(2x2,3x3) conv (conv2d_wino.hip) against torch's fp32 conv (MIOpen).
+Tolerance: Winograd rounding (transform coefficients +-1, 1/2) over Cin*9-term sums of
+unit-scale data, 2e-5 relative to the output's RMS."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from stereoanywhere_amd import ops
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def rnd(*shape, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.randn(*shape, generator=g).to(dev)
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(1, 8, 32, 8, 32), (2, 16, 64, 9, 37), (1, 64, 96, 17, 50),
+                                            (2, 128, 256, 34, 60), (1, 256, 384, 20, 33), (3, 192, 128, 6, 7)])
+def test_wino_matches_conv2d(N, Cin, Cout, H, W):
+    x = rnd(N, Cin, H, W, seed=Cin)
+    w = rnd(Cout, Cin, 3, 3, seed=Cout) / (3 * Cin ** 0.5)
+    b = rnd(Cout, seed=7)
+    U = ops.wino_weights(w)
+    for bias, relu in ((None, False), (b, False), (b, True)):
+        got = ops.conv2d_k3(x, U, bias, relu)
+        ref = F.conv2d(x, w, bias, padding=1)
+        if relu:
+            ref = torch.relu(ref)
+        scale = float(ref.pow(2).mean().sqrt())
+        assert float((got - ref).abs().max()) < 2e-5 * max(scale, 1.0) * 10, float((got - ref).abs().max())
+        assert float((got - ref).pow(2).mean().sqrt()) < 2e-6 * max(scale, 1.0) * 10
+
+
+def test_wino_views_and_errors():
+    x = rnd(2, 40, 12, 64, seed=1)
+    w = rnd(32, 16, 3, 3, seed=2) * 0.1
+    U = ops.wino_weights(w)
+    out = torch.zeros(2, 96, 12, 64, device=dev)
+    ops.conv2d_k3(x[:, 8:24], U, out=out[:, 32:64])     # channel-slice input and output
+    ref = F.conv2d(x[:, 8:24], w, padding=1)
+    torch.testing.assert_close(out[:, 32:64], ref, atol=2e-5, rtol=1e-5)
+    assert float(out[:, :32].abs().sum()) == 0.0 and float(out[:, 64:].abs().sum()) == 0.0
+    with pytest.raises(RuntimeError):
+        ops.conv2d_k3(rnd(1, 12, 8, 8), ops.wino_weights(rnd(32, 12, 3, 3)))   # Cin % 8 != 0
