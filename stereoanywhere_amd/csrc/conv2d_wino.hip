@@ -32,41 +32,45 @@ constexpr int OTH = 8, OTW = 32;             // output tile (pixels)
 constexpr int TR = OTH / 2, TC = OTW / 2;    // Winograd tiles: 4 rows x 16 cols
 constexpr int NT = TR * TC;                  // 64
 constexpr int KC = 8;                        // input channels per chunk
-constexpr int CO = 32;                       // output channels per block
 constexpr int PH = OTH + 2, PW = OTW + 2;    // input patch 10 x 34
 constexpr int XS = 36;                       // LDS row pitch of the patch
-constexpr int XCP = 384;                     // LDS channel-plane pitch (>= PH * XS, multiple of 64:
-                                             // channels c and c + 4 load as one ds_read2st64_b32)
+constexpr int XCP = 384;                     // LDS channel-plane pitch (>= PH * XS)
 constexpr int NX = KC * PH * PW;             // 2720 patch values per chunk
 constexpr int XPT = (NX + 511) / 512;        // per thread (6)
-constexpr int NU4 = 16 * KC * CO / 4;        // 1024 float4 of U per chunk
-constexpr int UPT = NU4 / 512;               // 2
-// LDS images hold the two k-steps of an MFMA pair side by side (channel ci and ci + 4 of a
-// chunk), so one ds_read_b64 feeds two MFMAs.  Row pitches (in pairs) are 16 mod 32 so the
-// two k-rows a half-wave reads fall in disjoint bank halves (b64 bank = dword addr mod 64).
-constexpr int VP = NT + 16;                  // V[xi][ci%4][tile][ci/4]: 80 pairs per row
-constexpr int UP = CO + 16;                  // U[xi][ci%4][co][ci/4]:  48 pairs per row
-constexpr int COP = CO + 2;                  // output staging O[row][x][co]: 8*COP = 16 mod 32 banks
 
-// double-buffered: chunk k multiplies out of (v, u)[k & 1] while chunk k+1 is transformed
-// into (v)[(k+1) & 1]
-struct Smem {
-  float x[2][KC * XCP];           // input patch [ci][row][col]
-  float v[2][16 * 4 * VP * 2];    // V pairs; v[0] reused as the output tile O[co][row][col]
-  float u[2][16 * 4 * UP * 2];    // U pairs
+// V and U live in LDS as rows of float2 pairs (channel c and c + 4 of a chunk: the two
+// k-steps of an MFMA pair, one ds_read_b64).  An operand read puts rows r and r + 1 in one
+// half-wave, so odd rows are stored with column ^ 16: the two rows then fall in disjoint
+// bank halves without padding (b64 bank = dword address mod 64).
+__device__ __forceinline__ int swz(int row, int col, int ncol) { return row * ncol + (col ^ ((row & 1) << 4)); }
+
+// CG output-channel groups of 16 per wave; a block has 4 tile rows x 2 channel halves of waves
+// and 32 * CG output channels.  CG = 2 halves the transform work and V traffic per FMA and
+// reuses each A fragment for two MFMAs.
+template <int CG>
+struct Wino {
+  static constexpr int CO = 32 * CG;
+  static constexpr int UPT = (16 * 4 * CO / 2) / 512;   // float4 of U per thread per chunk
+  static constexpr int COP = CO + 2;                    // output staging O[row][x][co] pitch
+  static constexpr int X_OFF = 0, V_OFF = KC * XCP, VSZ = 16 * 4 * NT * 2, U_OFF = V_OFF + 2 * VSZ,
+                       USZ = 16 * 4 * CO * 2, SMEM = U_OFF + 2 * USZ;
+  static_assert(OTH * OTW * COP <= 2 * VSZ + 2 * USZ, "output staging fits V + U");
+  static_assert(SMEM * 4 <= 160 * 1024, "LDS budget");
 };
-static_assert(OTH * OTW * COP <= 16 * 4 * VP * 2, "output staging fits one V buffer");
-static_assert(sizeof(Smem) <= 160 * 1024, "LDS budget");
 
 #ifndef SA_WINO_WAVES_PER_EU
 #define SA_WINO_WAVES_PER_EU 2
 #endif
 
+template <int CG>
 __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
     const float *__restrict__ in, long in_bs, int Cin, int H, int W, const float *__restrict__ U, int Cout,
     const float *__restrict__ bias, int relu, float *__restrict__ out, long out_bs, int tiles_w, int tiles_hw,
     int co_blocks) {
-  __shared__ Smem sm;
+  using Cfg = Wino<CG>;
+  constexpr int CO = Cfg::CO, UPT = Cfg::UPT;
+  __shared__ float smem[Cfg::SMEM];
+  float *const sx = smem + Cfg::X_OFF;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware work order: consecutive work ids = the co blocks of one spatial tile
@@ -97,13 +101,14 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
     xl[j] = tid + 512 * j < NX ? ci * XCP + r * XS + cc : -1;
     if (y < 0 || y >= H || x < 0 || x >= W) xpad |= 1u << j;
   }
-  // U chunk image: global [xi][Cin/8][4][Cout][2] -> rows of 32 co pairs (64 floats)
-  int uo[UPT];
+  // U chunk image: global [xi][Cin/8][4][Cout][2] -> LDS rows (xi, ci4) of CO swizzled pairs
+  int uo[UPT], ul[UPT];
 #pragma unroll
   for (int j = 0; j < UPT; ++j) {
-    const int i4 = tid + 512 * j;               // 1024 float4 = 16 xi x 4 ci4 x 16 (co pair halves)
-    const int q = i4 & 15, ci4 = (i4 >> 4) & 3, xi = i4 >> 6;
-    uo[j] = (((xi * (Cin / KC)) * 4 + ci4) * Cout * 2 + co0 * 2 + q * 4) * 4;
+    const int i4 = tid + 512 * j;
+    const int q = i4 % (CO / 2), row = i4 / (CO / 2);   // row = xi * 4 + ci4
+    uo[j] = (((row >> 2) * (Cin / KC) * 4 + (row & 3)) * Cout * 2 + co0 * 2 + q * 4) * 4;
+    ul[j] = swz(row, 2 * q, CO) * 2;
   }
   float xr[XPT];
   f32x4 ur[UPT];
@@ -118,23 +123,19 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
     }
   };
   auto commit = [&](int buf) __attribute__((always_inline)) {
-    float *xs = sm.x[buf];
 #pragma unroll
     for (int j = 0; j < XPT; ++j)
-      if (xl[j] >= 0) xs[xl[j]] = ((xpad >> j) & 1u) ? 0.0f : xr[j];
+      if (xl[j] >= 0) sx[xl[j]] = ((xpad >> j) & 1u) ? 0.0f : xr[j];
+    float *su = smem + Cfg::U_OFF + buf * Cfg::USZ;
 #pragma unroll
-    for (int j = 0; j < UPT; ++j) {
-      const int i4 = tid + 512 * j;
-      const int q = i4 & 15, row = i4 >> 4;  // row = xi * 4 + ci4
-      *reinterpret_cast<f32x4 *>(sm.u[buf] + row * UP * 2 + q * 4) = ur[j];
-    }
+    for (int j = 0; j < UPT; ++j) *reinterpret_cast<f32x4 *>(su + ul[j]) = ur[j];
   };
   // input transform V = B^T d B of (channel tid >> 6, tile tid & 63) into its slot of the
   // (c, c + 4) pair image; every thread has one job per chunk
   auto transform = [&](int buf) __attribute__((always_inline)) {
     const int ci = tid >> 6, t = tid & 63;
     const int ty = t / TC, tx = t % TC;
-    const float *p = sm.x[buf] + ci * XCP + 2 * ty * XS + 2 * tx;
+    const float *p = sx + ci * XCP + 2 * ty * XS + 2 * tx;
     float d[4][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -149,25 +150,33 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
       w[2][c] = d[2][c] - d[1][c];
       w[3][c] = d[1][c] - d[3][c];
     }
-    float *o = sm.v[buf] + ((ci & 3) * VP + t) * 2 + (ci >> 2);
+    // rows xi * 4 + (ci & 3) all have the parity of ci & 3: one swizzled column for all xi
+    float *o = smem + Cfg::V_OFF + buf * Cfg::VSZ + swz(ci & 3, t, NT) * 2 + (ci >> 2);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      o[((r * 4 + 0) * 4) * VP * 2] = w[r][0] - w[r][2];
-      o[((r * 4 + 1) * 4) * VP * 2] = w[r][1] + w[r][2];
-      o[((r * 4 + 2) * 4) * VP * 2] = w[r][2] - w[r][1];
-      o[((r * 4 + 3) * 4) * VP * 2] = w[r][1] - w[r][3];
+      o[((r * 4 + 0) * 4) * NT * 2] = w[r][0] - w[r][2];
+      o[((r * 4 + 1) * 4) * NT * 2] = w[r][1] + w[r][2];
+      o[((r * 4 + 2) * 4) * NT * 2] = w[r][2] - w[r][1];
+      o[((r * 4 + 3) * 4) * NT * 2] = w[r][1] - w[r][3];
     }
   };
 
-  f32x4 acc[16];
+  f32x4 acc[16][CG];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int tg = wv & 3, cg = wv >> 2;                 // tile row, co half
+  for (int k = 0; k < 16; ++k)
+#pragma unroll
+    for (int g = 0; g < CG; ++g) acc[k][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int tg = wv & 3, ch = wv >> 2;                 // tile row, output-channel half
   const int ak = lane >> 4, am = lane & 15;            // operand lane map (16x16x4)
-  const int a_off = ak * VP + tg * TC + am, b_off = ak * UP + cg * 16 + am;
+  // operand slots (float2 units) of row xi * 4 + ak: the swizzle depends on ak's parity only
+  const int a_slot = swz(ak, tg * TC + am, NT);
+  int b_slot[CG];
+#pragma unroll
+  for (int g = 0; g < CG; ++g) b_slot[g] = swz(ak, (ch * CG + g) * 16 + am, CO);
 
   // software pipeline: iteration k = [sync, commit chunk k+1, issue loads of chunk k+2, sync,
-  // MFMA chunk k || transform chunk k+1]
+  // MFMA chunk k || transform chunk k+1].  The patch buffer is single: its commit and the
+  // transform that reads it are separated by the first barrier of the next iteration.
   const int nchunks = Cin / KC;
   fetch(0);
   commit(0);
@@ -181,57 +190,72 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
     if (k + 1 < nchunks) commit(nxt);    // registers hold chunk k+1
     if (k + 2 < nchunks) fetch(k + 2);
     __syncthreads();
-    const float2 *va = reinterpret_cast<const float2 *>(sm.v[cur]) + a_off;
-    const float2 *ubp = reinterpret_cast<const float2 *>(sm.u[cur]) + b_off;
-    float2 a[16], b[16];
+    const float2 *va = reinterpret_cast<const float2 *>(smem + Cfg::V_OFF + cur * Cfg::VSZ) + a_slot;
+    const float2 *vb = reinterpret_cast<const float2 *>(smem + Cfg::U_OFF + cur * Cfg::USZ);
 #pragma unroll
-    for (int xi = 0; xi < 16; ++xi) {
-      a[xi] = va[xi * 4 * VP];
-      b[xi] = ubp[xi * 4 * UP];
+    for (int h = 0; h < 2; ++h) {        // transform points 8h .. 8h+7
+      float2 a[8], b[8][CG];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        a[i] = va[(8 * h + i) * 4 * NT];
+#pragma unroll
+        for (int g = 0; g < CG; ++g) b[i][g] = vb[(8 * h + i) * 4 * CO + b_slot[g]];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int g = 0; g < CG; ++g)
+          acc[8 * h + i][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b[i][g].x, acc[8 * h + i][g], 0, 0, 0);
+      if (h == 0) transform(nxt);  // unconditional (the last one fills an idle buffer): same block as the MFMAs
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int g = 0; g < CG; ++g)
+          acc[8 * h + i][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b[i][g].y, acc[8 * h + i][g], 0, 0, 0);
     }
-#pragma unroll
-    for (int xi = 0; xi < 16; ++xi) acc[xi] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[xi].x, b[xi].x, acc[xi], 0, 0, 0);
-    transform(nxt);  // unconditional (the last one fills an idle buffer) so it shares the MFMAs' block
-#pragma unroll
-    for (int xi = 0; xi < 16; ++xi) acc[xi] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[xi].y, b[xi].y, acc[xi], 0, 0, 0);
   }
   __syncthreads();
 
-  // ---- output transform in registers: lane holds tiles (tg, 4*(lane>>4) + r), channel cg*16 + (lane&15)
-  float *ot = sm.v[0];  // reuse: O[row][x][co]
-  const int col = cg * 16 + (lane & 15);
-  const float bv = bias ? bias[co0 + col] : 0.0f;
+  // ---- output transform in registers: lane holds tiles (tg, 4*(lane>>4) + r) of channel
+  // (ch * CG + g) * 16 + (lane & 15); staged as O[row][x][co] for row-contiguous stores
+  float *ot = smem + Cfg::V_OFF;
+  constexpr int COP = Cfg::COP;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int tx = 4 * (lane >> 4) + r;
-    float m[4][4];
+  for (int g = 0; g < CG; ++g) {
+    const int col = (ch * CG + g) * 16 + (lane & 15);
+    const float bv = bias ? bias[co0 + col] : 0.0f;
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int r = 0; r < 4; ++r) {
+      const int tx = 4 * (lane >> 4) + r;
+      float m[4][4];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) m[a][b] = acc[a * 4 + b][r];
-    // A^T = [[1,1,1,0],[0,1,-1,-1]]
-    float t0[4], t1[4];
+      for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      t0[b] = m[0][b] + m[1][b] + m[2][b];
-      t1[b] = m[1][b] - m[2][b] - m[3][b];
-    }
-    float y[2][2];
-    y[0][0] = t0[0] + t0[1] + t0[2];
-    y[0][1] = t0[1] - t0[2] - t0[3];
-    y[1][0] = t1[0] + t1[1] + t1[2];
-    y[1][1] = t1[1] - t1[2] - t1[3];
+        for (int b = 0; b < 4; ++b) m[a][b] = acc[a * 4 + b][g][r];
+      // A^T = [[1,1,1,0],[0,1,-1,-1]]
+      float t0[4], t1[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        float v = y[i][j] + bv;
-        if (relu) v = fmaxf(v, 0.0f);
-        ot[((2 * tg + i) * OTW + 2 * tx + j) * COP + col] = v;
+      for (int b = 0; b < 4; ++b) {
+        t0[b] = m[0][b] + m[1][b] + m[2][b];
+        t1[b] = m[1][b] - m[2][b] - m[3][b];
       }
+      float y[2][2];
+      y[0][0] = t0[0] + t0[1] + t0[2];
+      y[0][1] = t0[1] - t0[2] - t0[3];
+      y[1][0] = t1[0] + t1[1] + t1[2];
+      y[1][1] = t1[1] - t1[2] - t1[3];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float v = y[i][j] + bv;
+          if (relu) v = fmaxf(v, 0.0f);
+          ot[((2 * tg + i) * OTW + 2 * tx + j) * COP + col] = v;
+        }
+    }
   }
   __syncthreads();
-  // 32 channels x 8 rows x 32 columns, one row-segment of 32 floats per half-wave
+  // CO channels x 8 rows x 32 columns, one row-segment of 32 floats per half-wave
   float *dst = out + (long)n * out_bs;
 #pragma unroll
   for (int j = 0; j < (CO * OTH * OTW) / 512; ++j) {
@@ -281,18 +305,23 @@ extern "C" int sa_conv2d_wino_weights(const float *weight, int Cout, int Cin, fl
 extern "C" int sa_conv2d_k3_wino(const float *in, long in_bs, int N, int Cin, int H, int W, const float *U, int Cout,
                                  const float *bias, int relu, float *out, long out_bs, void *stream) {
   SA_REQUIRE(in && U && out && N > 0 && H > 0 && W > 0, "sa_conv2d_k3_wino: bad arguments");
-  SA_REQUIRE(Cin % KC == 0 && Cout % CO == 0, "sa_conv2d_k3_wino: needs Cin %% 8 == 0 and Cout %% 32 == 0 (got %d, %d)",
+  SA_REQUIRE(Cin % KC == 0 && Cout % 32 == 0, "sa_conv2d_k3_wino: needs Cin %% 8 == 0 and Cout %% 32 == 0 (got %d, %d)",
              Cin, Cout);
   SA_REQUIRE((reinterpret_cast<uintptr_t>(U) & 15) == 0, "sa_conv2d_k3_wino: U must be 16-byte aligned");
   SA_REQUIRE((long)Cin * H * W * 4 < (1L << 31) && 16L * Cin * Cout * 4 < (1L << 31),
              "sa_conv2d_k3_wino: an image or the filter bank exceeds the 2 GB buffer-descriptor range");
+  const int cg = Cout % 64 == 0 ? 2 : 1;
   const int tiles_w = (W + OTW - 1) / OTW, tiles_h = (H + OTH - 1) / OTH;
-  const int co_blocks = Cout / CO;
+  const int co_blocks = Cout / (32 * cg);
   const long nblk = (long)N * tiles_w * tiles_h * co_blocks;
   SA_REQUIRE(nblk < (1L << 31), "sa_conv2d_k3_wino: grid too large");
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV2D, s);
-  wino_f2k3_kernel<<<(unsigned)nblk, 512, 0, s>>>(in, in_bs, Cin, H, W, U, Cout, bias, relu, out, out_bs, tiles_w,
-                                                  tiles_w * tiles_h, co_blocks);
+  if (cg == 2)
+    wino_f2k3_kernel<2><<<(unsigned)nblk, 512, 0, s>>>(in, in_bs, Cin, H, W, U, Cout, bias, relu, out, out_bs,
+                                                       tiles_w, tiles_w * tiles_h, co_blocks);
+  else
+    wino_f2k3_kernel<1><<<(unsigned)nblk, 512, 0, s>>>(in, in_bs, Cin, H, W, U, Cout, bias, relu, out, out_bs,
+                                                       tiles_w, tiles_w * tiles_h, co_blocks);
   return sa::check_launch("sa_conv2d_k3_wino");
 }

@@ -123,8 +123,8 @@ class StereoAnywhere(nn.Module):
                 # Winograd F(2x2,3x3) filters (ops.conv2d_k3) of every eligible 3x3 conv
                 d = self._derived
                 d["wino"] = encoders.wino_table(self.cnet, self.fnet)
-                for key in ("g08", "g16", "g32"):
-                    g = d[key]
+                for gk in ("g08", "g16", "g32"):
+                    g = d[gk]
                     g.update(Ux=ops.wino_weights(g["wx"]), Uhzr=ops.wino_weights(g["whzr"]),
                              Uqh=ops.wino_weights(g["wqh"]))
                 d.update(U_c2=ops.wino_weights(enc.convc2.weight.detach().contiguous()),

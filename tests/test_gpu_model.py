@@ -65,3 +65,15 @@ def test_rerun_stability(model):
     a = run(model, pb, 5)
     b = run(model, pb, 5)
     assert epe(a, b) < 1e-5
+
+
+def test_derived_weights_cached_across_forwards(model):
+    """The transformed / folded weights are built once per weight version, not per forward."""
+    pb = synth.synthetic_batch(1, 64, 128, 16.0, seed0=5)
+    x = [torch.from_numpy(pb[k]).cuda() for k in ("left", "right", "mono_left", "mono_right")]
+    with torch.no_grad():
+        model(*x, iters=1, test_mode=True)
+        d1 = model._derived
+        model(*x, iters=1, test_mode=True)
+    assert model._derived is d1
+    assert isinstance(model._derived_key, tuple)
