@@ -178,6 +178,13 @@ def main():
             model(*x, iters=args.iters, test_mode=True)
             torch.cuda.synchronize()
             log(f"warmup {i + 1}/{args.warmup} done")
+        # price the layer-mix-dependent families (Winograd convs, norm epilogues) on one
+        # untimed forward
+        from stereoanywhere_amd import ops as O
+        O.WORK = {}
+        model(*x, iters=args.iters, test_mode=True)
+        work, O.WORK = O.WORK, None
+        torch.cuda.synchronize()
         N.timing_enable(True)
         D.barrier(r)
         torch.cuda.synchronize()
@@ -201,6 +208,8 @@ def main():
         return
     # every hand-written kernel family: algorithmic work / live event time vs MI355X peak
     costs = step_costs(hi - lo, H4, W4, args.iters)
+    costs["conv2d_wino"] = ("TFLOP/s", work.get("conv2d_wino", 0.0))
+    costs["norm_act"] = ("GB/s", work.get("norm_act", 0.0))
     kernels = {}
     for k, (ms_tot, n_launch) in kt.items():
         if n_launch == 0 or k not in costs:
@@ -219,7 +228,9 @@ def main():
     roof.update({"kernel": dom, "traffic": pmc_traffic(dom, args.batch), "kernels": kernels,
                  "misc_ms_per_step": kt["misc"][0] / args.steps,
                  "note": "achieved = algorithmic amount per launch / mean live HIP-event launch time; "
-                         "fp32 FMA peak 157.3 TF/s is the same for MFMA (v_mfma_f32_*_f32) and VALU"})
+                         "fp32 FMA peak 157.3 TF/s is the same for MFMA (v_mfma_f32_*_f32) and VALU; "
+                         "conv2d_wino counts the Winograd-domain products it executes (16/36 of the "
+                         "direct convolution's), so its direct-equivalent rate is 2.25x achieved"})
     res = {
         "metric": "stereo pairs/sec @540x960 D=192 (1/2/4/8 GPU) + EPE vs reference",
         "value": total_pairs / elapsed, "unit": "pairs/s", "n_gpus": r.world, "steps": args.steps,

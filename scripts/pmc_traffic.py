@@ -12,10 +12,12 @@ import json
 import sys
 
 FAMILIES = {
-    "conv3d_k3_kernel": "conv3d_fused", "pointwise_upcat_kernel": "conv3d_fused", "lookup_kernel": "corr_lookup",
+    "conv3d_kernel": "conv3d_fused", "pointwise_upcat_kernel": "conv3d_fused", "pointwise_kernel": "conv3d_fused",
+    "vol_apply_kernel": "conv3d_fused", "lookup_kernel": "corr_lookup",
     "corr_pyramid_kernel": "corr_volume_pyramid", "masked_volume_kernel": "mono_masked_volume",
     "sam_contig_kernel": "softargmin_conf", "sam_strided_kernel": "softargmin_conf", "lsq_kernel": "weighted_lsq",
     "gru_zr_kernel": "gru_zr", "gru_out_kernel": "gru_out", "convex_up_kernel": "convex_upsample",
+    "wino_f2k3_kernel": "conv2d_wino", "norm_act_kernel": "norm_act", "plane_stats_kernel": "norm_act",
 }
 
 

@@ -52,7 +52,7 @@ struct Wino {
   static constexpr int CO = 32 * CG;
   static constexpr int UPT = (16 * 4 * CO / 2) / 512;   // float4 of U per thread per chunk
   static constexpr int COP = CO + 2;                    // output staging O[row][x][co] pitch
-  static constexpr int X_OFF = 0, V_OFF = KC * XCP, VSZ = 16 * 4 * NT * 2, U_OFF = V_OFF + 2 * VSZ,
+  static constexpr int XSZ = KC * XCP, X_OFF = 0, V_OFF = 2 * XSZ, VSZ = 16 * 4 * NT * 2, U_OFF = V_OFF + 2 * VSZ,
                        USZ = 16 * 4 * CO * 2, SMEM = U_OFF + 2 * USZ;
   static_assert(OTH * OTW * COP <= 2 * VSZ + 2 * USZ, "output staging fits V + U");
   static_assert(SMEM * 4 <= 160 * 1024, "LDS budget");
@@ -70,7 +70,6 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
   using Cfg = Wino<CG>;
   constexpr int CO = Cfg::CO, UPT = Cfg::UPT;
   __shared__ float smem[Cfg::SMEM];
-  float *const sx = smem + Cfg::X_OFF;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware work order: consecutive work ids = the co blocks of one spatial tile
@@ -112,20 +111,26 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
   }
   float xr[XPT];
   f32x4 ur[UPT];
-  auto fetch = [&](int chunk) __attribute__((always_inline)) {
-    const int xs = chunk * KC * (int)hw * 4, us = chunk * 4 * Cout * 2 * 4;
+  auto fetch_x = [&](int chunk) __attribute__((always_inline)) {
+    const int xs = chunk * KC * (int)hw * 4;
 #pragma unroll
     for (int j = 0; j < XPT; ++j) xr[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xin, xo[j], xs, 0));
+  };
+  auto fetch_u = [&](int chunk) __attribute__((always_inline)) {
+    const int us = chunk * 4 * Cout * 2 * 4;
 #pragma unroll
     for (int j = 0; j < UPT; ++j) {
       const auto w = __builtin_amdgcn_raw_buffer_load_b128(uin, uo[j], us, 0);
       ur[j] = f32x4{__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3])};
     }
   };
-  auto commit = [&](int buf) __attribute__((always_inline)) {
+  auto commit_x = [&](int buf) __attribute__((always_inline)) {
+    float *sx = smem + Cfg::X_OFF + buf * Cfg::XSZ;
 #pragma unroll
     for (int j = 0; j < XPT; ++j)
       if (xl[j] >= 0) sx[xl[j]] = ((xpad >> j) & 1u) ? 0.0f : xr[j];
+  };
+  auto commit_u = [&](int buf) __attribute__((always_inline)) {
     float *su = smem + Cfg::U_OFF + buf * Cfg::USZ;
 #pragma unroll
     for (int j = 0; j < UPT; ++j) *reinterpret_cast<f32x4 *>(su + ul[j]) = ur[j];
@@ -135,7 +140,7 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
   auto transform = [&](int buf) __attribute__((always_inline)) {
     const int ci = tid >> 6, t = tid & 63;
     const int ty = t / TC, tx = t % TC;
-    const float *p = sx + ci * XCP + 2 * ty * XS + 2 * tx;
+    const float *p = smem + Cfg::X_OFF + buf * Cfg::XSZ + ci * XCP + 2 * ty * XS + 2 * tx;
     float d[4][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -174,21 +179,26 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
 #pragma unroll
   for (int g = 0; g < CG; ++g) b_slot[g] = swz(ak, (ch * CG + g) * 16 + am, CO);
 
-  // software pipeline: iteration k = [sync, commit chunk k+1, issue loads of chunk k+2, sync,
-  // MFMA chunk k || transform chunk k+1].  The patch buffer is single: its commit and the
-  // transform that reads it are separated by the first barrier of the next iteration.
+  // software pipeline, one barrier per chunk.  Chunk c lives in X[c & 1], V[c & 1], U[c & 1].
+  // Iteration k: barrier | MFMA(k) || transform(k+1) | commit U(k+1), X(k+2) | loads U(k+2), X(k+3).
+  // Every buffer written in iteration k was last read in iteration k-1 (before the barrier),
+  // every buffer read in iteration k was written in iteration k-1.
   const int nchunks = Cin / KC;
-  fetch(0);
-  commit(0);
-  if (nchunks > 1) fetch(1);
+  fetch_x(0);
+  fetch_u(0);
+  commit_x(0);
+  commit_u(0);
+  if (nchunks > 1) {
+    fetch_x(1);
+    fetch_u(1);
+    commit_x(1);
+  }
+  if (nchunks > 2) fetch_x(2);
   __syncthreads();
   transform(0);
 #pragma unroll 1
   for (int k = 0; k < nchunks; ++k) {
     const int cur = k & 1, nxt = cur ^ 1;
-    __syncthreads();                     // chunk k transformed; chunk k-1's buffers free
-    if (k + 1 < nchunks) commit(nxt);    // registers hold chunk k+1
-    if (k + 2 < nchunks) fetch(k + 2);
     __syncthreads();
     const float2 *va = reinterpret_cast<const float2 *>(smem + Cfg::V_OFF + cur * Cfg::VSZ) + a_slot;
     const float2 *vb = reinterpret_cast<const float2 *>(smem + Cfg::U_OFF + cur * Cfg::USZ);
@@ -206,7 +216,14 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
 #pragma unroll
         for (int g = 0; g < CG; ++g)
           acc[8 * h + i][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b[i][g].x, acc[8 * h + i][g], 0, 0, 0);
-      if (h == 0) transform(nxt);  // unconditional (the last one fills an idle buffer): same block as the MFMAs
+      if (h == 0) {
+        // every chunk index past the end reads / writes only idle buffers
+        transform(nxt);
+        commit_u(nxt);
+        commit_x(cur);
+        if (k + 2 < nchunks) fetch_u(k + 2);
+        if (k + 3 < nchunks) fetch_x(k + 3);
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll

@@ -15,6 +15,16 @@ import torch
 from . import _native as N
 
 
+# algorithmic work per kernel family, accumulated while a dict is installed here (bench.py
+# runs one untimed forward with it to price the families whose work depends on the layer mix)
+WORK: Optional[dict] = None
+
+
+def _account(kernel: str, amount: float) -> None:
+    if WORK is not None:
+        WORK[kernel] = WORK.get(kernel, 0.0) + amount
+
+
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
@@ -394,6 +404,7 @@ def plane_stats(x: torch.Tensor, eps: float = 1e-5):
     mean = torch.empty(B * C, device=x.device, dtype=torch.float32)
     rstd = torch.empty_like(mean)
     N.call("sa_plane_stats", x.data_ptr(), bs, B, C, H * W, eps, mean.data_ptr(), rstd.data_ptr(), _stream(x))
+    _account("norm_act", 4.0 * B * C * H * W)
     return mean, rstd
 
 
@@ -427,6 +438,7 @@ def norm_act(x: torch.Tensor, aff: Optional[Affine] = None, act_in=None, skip: O
     sa_ = (skip_aff or Affine()).args(C)
     N.call("sa_norm_act", x.data_ptr(), xb, B, C, H * W, *a, ACT[act_in], _ptr(skip), sb, *sa_, ACT[act_out],
            out.data_ptr(), ob, _stream(x))
+    _account("norm_act", 4.0 * B * C * H * W * (3 if skip is not None else 2))
     return out
 
 
@@ -467,6 +479,8 @@ def conv2d_k3(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = N
         raise RuntimeError("conv2d_k3: out shape mismatch")
     N.call("sa_conv2d_k3_wino", x.data_ptr(), bs, B, Cin, H, W, U.data_ptr(), Cout, _ptr(bias), 1 if relu else 0,
            out.data_ptr(), _plane_bs(out, "out"), _stream(x))
+    # Winograd-domain products actually executed: 16 per 2x2 tile per (Cin, Cout) pair
+    _account("conv2d_wino", 2.0 * 16 * Cin * Cout * B * ((H + 1) // 2) * ((W + 1) // 2))
     return out
 
 
