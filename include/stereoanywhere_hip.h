@@ -218,6 +218,17 @@ int sa_conv2d_k3_narrow(const float *in, long in_bs, int B, int Cin, int H, int 
 int sa_conv2d_wino_weights(const float *weight, int Cout, int Cin, float *U, void *stream);
 int sa_conv2d_k3_wino(const float *in, long in_bs, int N, int Cin, int H, int W, const float *U,
                       int Cout, const float *bias, int relu, float *out, long out_bs, void *stream);
+/* As sa_conv2d_k3_wino, plus the producer's epilogue applied while the input is loaded,
+ * x -> act((x - m) * s + t) (m, s, t per channel with in_pstride 0 or per (image, channel)
+ * with in_pstride Cin; NULL = 0 / 1 / 0; in_act 1 = ReLU; zero padding applies to the
+ * result; Cin <= 512), and, if stats_partial != NULL, per-block float64 (sum, sum^2) of every
+ * output channel, [N*Cout][parts][2] with parts = sa_conv2d_k3_wino_stat_parts(H, W), for
+ * sa_instnorm_finalize. */
+long sa_conv2d_k3_wino_stat_parts(int H, int W);
+int sa_conv2d_k3_wino_ex(const float *in, long in_bs, int N, int Cin, int H, int W, const float *U,
+                         int Cout, const float *bias, int relu, const float *in_m, const float *in_s,
+                         const float *in_t, int in_pstride, int in_act, float *out, long out_bs,
+                         double *stats_partial, void *stream);
 
 /* Epilogues of the MIOpen 2-D convs (encoders extractor.py:6-300, update block update.py:64-110).
  * sa_plane_stats: InstanceNorm2d statistics (biased variance, eps) of each (b, c) plane of

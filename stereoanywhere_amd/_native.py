@@ -49,6 +49,8 @@ SIGNATURES = {
     "sa_conv2d_k3_narrow": (I, [P, L, I, I, I, I, P, P, I, P, L, P]),
     "sa_conv2d_wino_weights": (I, [P, I, I, P, P]),
     "sa_conv2d_k3_wino": (I, [P, L, I, I, I, I, P, I, P, I, P, L, P]),
+    "sa_conv2d_k3_wino_stat_parts": (L, [I, I]),
+    "sa_conv2d_k3_wino_ex": (I, [P, L, I, I, I, I, P, I, P, I, P, P, P, I, I, P, L, P, P]),
     "sa_plane_stats": (I, [P, L, I, I, L, F, P, P, P]),
     "sa_norm_act": (I, [P, L, I, I, L, P, P, P, I, I, P, L, P, P, P, I, I, P, L, P]),
     "sa_conv3d_upcat_stat_parts": (L, [I, I, I]),

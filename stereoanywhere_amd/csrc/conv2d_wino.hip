@@ -62,14 +62,30 @@ struct Wino {
 #define SA_WINO_WAVES_PER_EU 2
 #endif
 
+constexpr int MAX_CIN_AFFINE = 512;
+
+// Optional producer epilogue applied on load and statistics of the output:
+//   input  v -> act(v * scale[c] + shift[c]), scale = s, shift = t - m * s, with (m, s, t)
+//          per channel (pstride 0) or per (image, channel) (pstride Cin), any of them NULL =
+//          0 / 1 / 0 — the previous layer's bias / BatchNorm / InstanceNorm + ReLU; zero
+//          padding applies to the activated input
+//   stats  per-block float64 (sum, sum^2) of every output channel for the next
+//          InstanceNorm: partial[(n * Cout + co) * tiles_hw + spatial tile][2]
+struct WinoIO {
+  const float *m, *s, *t;
+  int pstride, act;
+  double *partial;
+};
+
 template <int CG>
 __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
     const float *__restrict__ in, long in_bs, int Cin, int H, int W, const float *__restrict__ U, int Cout,
     const float *__restrict__ bias, int relu, float *__restrict__ out, long out_bs, int tiles_w, int tiles_hw,
-    int co_blocks) {
+    int co_blocks, WinoIO io) {
   using Cfg = Wino<CG>;
   constexpr int CO = Cfg::CO, UPT = Cfg::UPT;
   __shared__ float smem[Cfg::SMEM];
+  __shared__ float2 tab[MAX_CIN_AFFINE];   // input (scale, shift) of this image's channels
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware work order: consecutive work ids = the co blocks of one spatial tile
@@ -89,13 +105,22 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
       const_cast<float *>(src), (short)0, (int)((long)Cin * hw * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t uin = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float *>(U), (short)0, (int)(16L * Cin * Cout * 4), 0x00020000);
-  int xo[XPT], xl[XPT];   // global byte offset, LDS slot (-1: no slot)
+  const bool in_aff = io.m || io.s || io.t || io.act;
+  if (in_aff) {
+    for (int c = tid; c < Cin; c += 512) {
+      const int pi = n * io.pstride + c;
+      const float m = io.m ? io.m[pi] : 0.0f, sc = io.s ? io.s[pi] : 1.0f, t = io.t ? io.t[pi] : 0.0f;
+      tab[c] = make_float2(sc, t - m * sc);
+    }
+  }
+  int xo[XPT], xl[XPT], xc[XPT];   // global byte offset, LDS slot (-1: no slot), channel in chunk
   unsigned xpad = 0;
 #pragma unroll
   for (int j = 0; j < XPT; ++j) {
     const int i = min(tid + 512 * j, NX - 1);
     const int ci = i / (PH * PW), r = (i / PW) % PH, cc = i % PW;
     const int y = y0 - 1 + r, x = x0 - 1 + cc;
+    xc[j] = ci;
     xo[j] = (ci * (int)hw + min(max(y, 0), H - 1) * W + min(max(x, 0), W - 1)) * 4;
     xl[j] = tid + 512 * j < NX ? ci * XCP + r * XS + cc : -1;
     if (y < 0 || y >= H || x < 0 || x >= W) xpad |= 1u << j;
@@ -124,11 +149,18 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
       ur[j] = f32x4{__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3])};
     }
   };
-  auto commit_x = [&](int buf) __attribute__((always_inline)) {
+  auto commit_x = [&](int buf, int chunk) __attribute__((always_inline)) {
     float *sx = smem + Cfg::X_OFF + buf * Cfg::XSZ;
 #pragma unroll
-    for (int j = 0; j < XPT; ++j)
-      if (xl[j] >= 0) sx[xl[j]] = ((xpad >> j) & 1u) ? 0.0f : xr[j];
+    for (int j = 0; j < XPT; ++j) {
+      float v = xr[j];
+      if (in_aff) {
+        const float2 p = tab[chunk * KC + xc[j]];
+        v = v * p.x + p.y;
+        if (io.act) v = fmaxf(v, 0.0f);
+      }
+      if (xl[j] >= 0) sx[xl[j]] = ((xpad >> j) & 1u) ? 0.0f : v;
+    }
   };
   auto commit_u = [&](int buf) __attribute__((always_inline)) {
     float *su = smem + Cfg::U_OFF + buf * Cfg::USZ;
@@ -184,14 +216,15 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
   // Every buffer written in iteration k was last read in iteration k-1 (before the barrier),
   // every buffer read in iteration k was written in iteration k-1.
   const int nchunks = Cin / KC;
+  if (in_aff) __syncthreads();  // the (scale, shift) table
   fetch_x(0);
   fetch_u(0);
-  commit_x(0);
+  commit_x(0, 0);
   commit_u(0);
   if (nchunks > 1) {
     fetch_x(1);
     fetch_u(1);
-    commit_x(1);
+    commit_x(1, 1);
   }
   if (nchunks > 2) fetch_x(2);
   __syncthreads();
@@ -220,7 +253,7 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
         // every chunk index past the end reads / writes only idle buffers
         transform(nxt);
         commit_u(nxt);
-        commit_x(cur);
+        commit_x(cur, k + 2);
         if (k + 2 < nchunks) fetch_u(k + 2);
         if (k + 3 < nchunks) fetch_x(k + 3);
       }
@@ -272,6 +305,31 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
     }
   }
   __syncthreads();
+  if (io.partial) {
+    // InstanceNorm partials of the block: TPC threads per channel, fixed-order reduction
+    constexpr int TPC = 512 / CO, PPT = OTH * OTW / TPC;
+    const int c = tid / TPC, part = tid % TPC;
+    double ssum = 0.0, ssq = 0.0;
+#pragma unroll 4
+    for (int p = part * PPT; p < (part + 1) * PPT; ++p) {
+      const int r = p / OTW, cx = p % OTW;
+      if (y0 + r < H && x0 + cx < W) {
+        const double v = ot[(r * OTW + cx) * COP + c];
+        ssum += v;
+        ssq += v * v;
+      }
+    }
+#pragma unroll
+    for (int o = TPC / 2; o > 0; o >>= 1) {
+      ssum += __shfl_xor(ssum, o);
+      ssq += __shfl_xor(ssq, o);
+    }
+    if (part == 0) {
+      double *pp = io.partial + (((long)n * Cout + co0 + c) * tiles_hw + st) * 2;
+      pp[0] = ssum;
+      pp[1] = ssq;
+    }
+  }
   // CO channels x 8 rows x 32 columns, one row-segment of 32 floats per half-wave
   float *dst = out + (long)n * out_bs;
 #pragma unroll
@@ -319,26 +377,42 @@ extern "C" int sa_conv2d_wino_weights(const float *weight, int Cout, int Cin, fl
   return sa::check_launch("sa_conv2d_wino_weights");
 }
 
-extern "C" int sa_conv2d_k3_wino(const float *in, long in_bs, int N, int Cin, int H, int W, const float *U, int Cout,
-                                 const float *bias, int relu, float *out, long out_bs, void *stream) {
+extern "C" long sa_conv2d_k3_wino_stat_parts(int H, int W) {
+  return (long)((W + OTW - 1) / OTW) * ((H + OTH - 1) / OTH);
+}
+
+extern "C" int sa_conv2d_k3_wino_ex(const float *in, long in_bs, int N, int Cin, int H, int W, const float *U,
+                                    int Cout, const float *bias, int relu, const float *in_m, const float *in_s,
+                                    const float *in_t, int in_pstride, int in_act, float *out, long out_bs,
+                                    double *stats_partial, void *stream) {
   SA_REQUIRE(in && U && out && N > 0 && H > 0 && W > 0, "sa_conv2d_k3_wino: bad arguments");
   SA_REQUIRE(Cin % KC == 0 && Cout % 32 == 0, "sa_conv2d_k3_wino: needs Cin %% 8 == 0 and Cout %% 32 == 0 (got %d, %d)",
              Cin, Cout);
   SA_REQUIRE((reinterpret_cast<uintptr_t>(U) & 15) == 0, "sa_conv2d_k3_wino: U must be 16-byte aligned");
   SA_REQUIRE((long)Cin * H * W * 4 < (1L << 31) && 16L * Cin * Cout * 4 < (1L << 31),
              "sa_conv2d_k3_wino: an image or the filter bank exceeds the 2 GB buffer-descriptor range");
+  const bool aff = in_m || in_s || in_t || in_act;
+  SA_REQUIRE(!aff || Cin <= MAX_CIN_AFFINE, "sa_conv2d_k3_wino: input transform needs Cin <= %d", MAX_CIN_AFFINE);
+  SA_REQUIRE(in_pstride == 0 || in_pstride == Cin, "sa_conv2d_k3_wino: in_pstride must be 0 or Cin");
   const int cg = Cout % 64 == 0 ? 2 : 1;
   const int tiles_w = (W + OTW - 1) / OTW, tiles_h = (H + OTH - 1) / OTH;
   const int co_blocks = Cout / (32 * cg);
   const long nblk = (long)N * tiles_w * tiles_h * co_blocks;
   SA_REQUIRE(nblk < (1L << 31), "sa_conv2d_k3_wino: grid too large");
+  const WinoIO io{in_m, in_s, in_t, in_pstride, in_act, stats_partial};
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV2D, s);
   if (cg == 2)
     wino_f2k3_kernel<2><<<(unsigned)nblk, 512, 0, s>>>(in, in_bs, Cin, H, W, U, Cout, bias, relu, out, out_bs,
-                                                       tiles_w, tiles_w * tiles_h, co_blocks);
+                                                       tiles_w, tiles_w * tiles_h, co_blocks, io);
   else
     wino_f2k3_kernel<1><<<(unsigned)nblk, 512, 0, s>>>(in, in_bs, Cin, H, W, U, Cout, bias, relu, out, out_bs,
-                                                       tiles_w, tiles_w * tiles_h, co_blocks);
+                                                       tiles_w, tiles_w * tiles_h, co_blocks, io);
   return sa::check_launch("sa_conv2d_k3_wino");
+}
+
+extern "C" int sa_conv2d_k3_wino(const float *in, long in_bs, int N, int Cin, int H, int W, const float *U, int Cout,
+                                 const float *bias, int relu, float *out, long out_bs, void *stream) {
+  return sa_conv2d_k3_wino_ex(in, in_bs, N, Cin, H, W, U, Cout, bias, relu, nullptr, nullptr, nullptr, 0, 0, out,
+                              out_bs, nullptr, stream);
 }

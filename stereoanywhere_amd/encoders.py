@@ -64,24 +64,45 @@ def bn_affine(norm: nn.BatchNorm2d, conv_bias) -> ops.Affine:
 
 
 class _Finisher:
-    """Applies a layer's norm to a raw conv output: instance statistics computed here, batch
-    statistics looked up in the folded table."""
+    """Applies a layer's norm to a raw conv output: instance statistics computed here (or
+    taken from the conv epilogue), batch statistics looked up in the folded table."""
 
     def __init__(self, kind: str, table: Dict[str, ops.Affine]):
         self.kind, self.table = kind, table
 
-    def affine(self, name: str, raw: torch.Tensor) -> ops.Affine:
-        if self.kind == "instance":
-            mean, rstd = ops.plane_stats(raw)
+    @property
+    def instance(self) -> bool:
+        return self.kind == "instance"
+
+    def affine(self, name: str, raw: torch.Tensor, stats=None) -> ops.Affine:
+        if self.instance:
+            mean, rstd = stats if stats is not None else ops.plane_stats(raw)
             return ops.Affine(mean, rstd, None, per_plane=True)
         return self.table[name]
 
 
+def _conv_k3(x: torch.Tensor, conv: nn.Conv2d, fin: _Finisher, in_aff=None):
+    """Winograd conv of a qualifying 3x3 layer -> (raw out, IN stats or None); with in_aff the
+    producer's norm + ReLU is applied while x is loaded."""
+    U = _WINO[conv.weight.data_ptr()]
+    r = ops.conv2d_k3(x, U, in_aff=in_aff, in_act="relu" if in_aff is not None else None, stats=fin.instance)
+    return r if fin.instance else (r, None)
+
+
 def residual_block(blk: nn.Module, name: str, x: torch.Tensor, fin: _Finisher) -> torch.Tensor:
-    c1 = _conv(x, blk.conv1)
-    y1 = ops.norm_act(c1, fin.affine(name + ".norm1", c1), act_in="relu", out=c1)
-    c2 = _conv(y1, blk.conv2)
-    a2 = fin.affine(name + ".norm2", c2)
+    w1, w2 = blk.conv1.weight.data_ptr(), blk.conv2.weight.data_ptr()
+    if w1 in _WINO and w2 in _WINO:
+        # y1 = relu(N1(c1)) is never written: conv2 applies it while loading c1
+        c1, s1 = _conv_k3(x, blk.conv1, fin)
+        c2, s2 = _conv_k3(c1, blk.conv2, fin, in_aff=fin.affine(name + ".norm1", c1, s1))
+    else:
+        c1 = _conv(x, blk.conv1)
+        y1 = ops.norm_act(c1, fin.affine(name + ".norm1", c1), act_in="relu", out=c1)
+        if w2 in _WINO:
+            c2, s2 = _conv_k3(y1, blk.conv2, fin)
+        else:
+            c2, s2 = _conv(y1, blk.conv2), None
+    a2 = fin.affine(name + ".norm2", c2, s2)
     if blk.downsample is None:
         return ops.norm_act(c2, a2, act_in="relu", skip=x, act_out="relu", out=c2)
     d = _conv(x, blk.downsample[0])

@@ -465,8 +465,11 @@ def wino_weights(weight: torch.Tensor) -> torch.Tensor:
 
 
 def conv2d_k3(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = None, relu: bool = False,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """3x3 / pad 1 conv via fused Winograd (U from wino_weights); + bias, optional ReLU."""
+              out: Optional[torch.Tensor] = None, in_aff: Optional[Affine] = None, in_act=None,
+              stats: bool = False):
+    """3x3 / pad 1 conv via fused Winograd (U from wino_weights); + bias, optional ReLU.
+    in_aff / in_act: the producer's norm + activation applied to x while it is loaded.
+    stats: also return the output's InstanceNorm (mean, rstd) per (image, channel)."""
     bs = _plane_bs(x, "x")
     _check(U, "U")
     B, Cin, H, W = x.shape
@@ -477,10 +480,15 @@ def conv2d_k3(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = N
         out = torch.empty((B, Cout, H, W), device=x.device, dtype=torch.float32)
     if tuple(out.shape) != (B, Cout, H, W):
         raise RuntimeError("conv2d_k3: out shape mismatch")
-    N.call("sa_conv2d_k3_wino", x.data_ptr(), bs, B, Cin, H, W, U.data_ptr(), Cout, _ptr(bias), 1 if relu else 0,
-           out.data_ptr(), _plane_bs(out, "out"), _stream(x))
+    a = (in_aff or Affine()).args(Cin)
+    parts = int(N.lib().sa_conv2d_k3_wino_stat_parts(H, W)) if stats else 0
+    partial = torch.empty((B * Cout * parts * 2,), device=x.device, dtype=torch.float64) if stats else None
+    N.call("sa_conv2d_k3_wino_ex", x.data_ptr(), bs, B, Cin, H, W, U.data_ptr(), Cout, _ptr(bias),
+           1 if relu else 0, *a, ACT[in_act], out.data_ptr(), _plane_bs(out, "out"), _ptr(partial), _stream(x))
     # Winograd-domain products actually executed: 16 per 2x2 tile per (Cin, Cout) pair
     _account("conv2d_wino", 2.0 * 16 * Cin * Cout * B * ((H + 1) // 2) * ((W + 1) // 2))
+    if stats:
+        return out, instnorm_finalize(partial, B * Cout, parts, H * W)
     return out
 
 

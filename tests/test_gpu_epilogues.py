@@ -105,18 +105,46 @@ def _encoders():
     return fnet.to(dev).eval(), cnet.to(dev).eval()
 
 
-def test_fused_encoders_match_modules():
+@pytest.mark.parametrize("use_wino", [False, True])
+def test_fused_encoders_match_modules(use_wino):
+    """Module forward vs the fused encoders: epilogue passes only (MIOpen convs), and with the
+    Winograd convs applying norm + ReLU on load and producing the InstanceNorm statistics."""
     fnet, cnet = _encoders()
     x = rnd(2, 3, 64, 96, seed=21).clamp(-1, 1)
     with torch.no_grad():
+        wino = encoders.wino_table(fnet, cnet) if use_wino else None
         ref_f = fnet(x)
-        got_f = encoders.fnet_forward(fnet, x, encoders.bn_table(fnet))
+        got_f = encoders.fnet_forward(fnet, x, encoders.bn_table(fnet), wino)
         torch.testing.assert_close(got_f, ref_f, atol=1e-4, rtol=1e-4)
         ref_c = cnet(x)
-        got_c = encoders.cnet_forward(cnet, x, encoders.bn_table(cnet))
+        got_c = encoders.cnet_forward(cnet, x, encoders.bn_table(cnet), wino)
         heads = [cnet.outputs08, cnet.outputs16, cnet.outputs32]
         for lvl in range(3):
             for j in range(2):
                 conv = heads[lvl][j][1] if lvl < 2 else heads[lvl][j]
                 got = got_c[lvl][j] + conv.bias[None, :, None, None]
                 torch.testing.assert_close(got, ref_c[lvl][j], atol=1e-4, rtol=1e-4)
+
+
+def test_wino_input_affine_and_stats():
+    """conv2d_k3 with the producer's norm + ReLU on load and fused InstanceNorm statistics vs
+    torch: relu(instance_norm(x)) -> conv -> instance-norm statistics of the output."""
+    N, Cin, Cout, H, W = 2, 16, 64, 19, 45
+    x = rnd(N, Cin, H, W, seed=30) * 2 + 0.5
+    w = rnd(Cout, Cin, 3, 3, seed=31) / (3 * Cin ** 0.5)
+    mean, rstd = ops.plane_stats(x)
+    y, (m2, r2) = ops.conv2d_k3(x, ops.wino_weights(w), in_aff=ops.Affine(mean, rstd, None, per_plane=True),
+                                in_act="relu", stats=True)
+    ref = F.conv2d(torch.relu(F.instance_norm(x)), w, padding=1)
+    torch.testing.assert_close(y, ref, atol=2e-5, rtol=1e-4)
+    torch.testing.assert_close(m2, ref.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(r2, 1 / torch.sqrt(ref.var(dim=(2, 3), unbiased=False).flatten() + 1e-5),
+                               atol=1e-4, rtol=1e-4)
+    # per-channel affine (eval BatchNorm) on load, 32-channel blocks
+    bn = torch.nn.BatchNorm2d(Cin).to(dev).eval()
+    with torch.no_grad():
+        bn.running_mean.copy_(rnd(Cin, seed=32))
+        bn.running_var.copy_(rnd(Cin, seed=33).abs() + 0.5)
+        w2 = rnd(96, Cin, 3, 3, seed=34) / (3 * Cin ** 0.5)
+        got = ops.conv2d_k3(x, ops.wino_weights(w2), in_aff=encoders.bn_affine(bn, None), in_act="relu")
+        torch.testing.assert_close(got, F.conv2d(torch.relu(bn(x)), w2, padding=1), atol=2e-5, rtol=1e-4)
