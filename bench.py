@@ -57,8 +57,9 @@ def step_costs(B: int, H4: int, W4: int, iters: int, C: int = 256):
     return {
         # fp32 MFMA: 2*C flops per volume cell (a1); epilogue work (trunc, pyramid) is free
         "corr_volume_pyramid": ("TFLOP/s", 2.0 * vol * C),
-        # per pixel: 2 volumes x 4 levels x (2r+2) cells read, 72 taps written, coords read
-        "corr_lookup": ("GB/s", iters * px * (2 * 4 * 10 * 4 + 72 * 4 + 4)),
+        # per pixel: 2 volumes x 4 levels x (2r+2) cells read, coords read, and (convc1 fused)
+        # 2 x 64 channels of relu(convc1(taps)) written
+        "corr_lookup": ("GB/s", iters * px * (2 * 4 * 10 * 4 + 4 + 2 * 64 * 4)),
         "mono_masked_volume": ("GB/s", 8 * vol * 4 + px * 2 * 4 * 4),
         # two aggregated volumes read once, four maps written
         "softargmin_conf": ("GB/s", 2 * vol * 4 + 4 * px * 4),

@@ -151,6 +151,15 @@ int sa_relu_copy(const float *in, long in_bs, int B, int C, int HW, float *out, 
 int sa_flow_update(float *coords_x, const float *delta, long delta_bs, int B, int H, int W,
                    float *flow_a, long flow_a_bs, float *flow_b, long flow_b_bs, void *stream);
 
+/* a10 + update.py:75, 84 — the lookup of sa_corr_lookup fused with the motion encoder's convc1
+ * (1x1 conv of the L*(2r+1) taps -> Cout, + bias, ReLU): weight_kc [L*(2r+1)][Cout] (the
+ * module's [Cout][K][1][1] transposed), out [B*nvol, Cout, H, W1] with sample b*nvol + v
+ * (v = 0 for pyramid_a, 1 for pyramid_b).  Built for 4 levels, radius 4, Cout 64. */
+int sa_corr_lookup_conv1x1(const float *pyramid_a, const float *pyramid_b, int W2, long row_stride,
+                           int num_levels, int radius, const float *coords_x, long coords_bstride,
+                           int B, int H, int W1, const float *weight_kc, const float *bias, int Cout,
+                           float *out, void *stream);
+
 /* a14 — convex_upflow (utils.py:97-110), factor 4: flow [B,1,H,W] (low-res x flow),
  * mask [B, 9*f*f, H, W] -> out [B,1,f*H,f*W] (sign as given: the reference's
  * flow_up, i.e. minus the disparity). */

@@ -57,6 +57,13 @@ class HipCorrBlock1D:
                         self.radius, coords_x, out)
         return out
 
+    def lookup_conv1x1_into(self, coords_x: torch.Tensor, weight_kc: torch.Tensor, bias: torch.Tensor,
+                            out: torch.Tensor, other: Optional["HipCorrBlock1D"] = None):
+        """Lookup of this pyramid (and ``other``'s) followed, in the same kernel, by a 1x1 conv
+        + bias + ReLU of the taps -> out [B*nvol, Cout, H, W1] (sample b*nvol + v)."""
+        return ops.corr_lookup_conv1x1(self.pyramid, None if other is None else other.pyramid, self.shape[3],
+                                       self.num_levels, self.radius, coords_x, weight_kc, bias, out)
+
     def __call__(self, coords: torch.Tensor) -> torch.Tensor:
         x = coords[:, :1]
         if self.pad[0]:

@@ -56,7 +56,100 @@ __global__ __launch_bounds__(256) void lookup_kernel(const float *__restrict__ p
   }
 }
 
+// Lookup fused with the motion encoder's first layer (update.py:75, 84): convc1 is a 1x1
+// conv of the L*(2r+1) taps to COUT channels + bias + ReLU, applied by the thread that
+// sampled them, so the taps never leave registers.  Weights [K][COUT] are wave-uniform
+// (scalar loads); consecutive output channels pair up for packed FMAs.
+// out: [B * nvol, COUT, H, W1], sample b * nvol + v (the reference's stereo / mono batch).
+template <int L, int R, int COUT>
+__global__ __launch_bounds__(256) void lookup_c1_kernel(const float *__restrict__ pa, const float *__restrict__ pb,
+                                                        const float *__restrict__ cx, LGeo g, long npix,
+                                                        const float *__restrict__ wt,
+                                                        const float *__restrict__ bias, int nvol,
+                                                        float *__restrict__ out) {
+  constexpr int K = 2 * R + 1, NT = L * K;
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+  const int v = blockIdx.y;
+  const float *__restrict__ pyr = v ? pb : pa;
+  const long hw = (long)g.H * g.W1;
+  const long b = p / hw, rem = p % hw;
+  const float x = cx[b * g.cbs + rem];
+  const float *__restrict__ row = pyr + p * g.rs;
+  float f[NT];
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    const int Wl = g.wid[l];
+    const float *__restrict__ lv = row + g.off[l];
+    const float xl = x / (float)(1 << l);
+    const float denom = (float)(Wl - 1);
+    const float sf = (float)(Wl - 1) / 2.0f;
+#pragma unroll
+    for (int t = -R; t <= R; ++t) {
+      const float x0 = (float)t + xl;
+      const float xg = 2.0f * x0 / denom - 1.0f;
+      const float ix = (xg + 1.0f) * sf;
+      float xw = floorf(ix);
+      const float w = ix - xw;
+      const float e = 1.0f - w;
+      xw = fminf(fmaxf(xw, -2.0f), (float)Wl + 1.0f);
+      const int xi = (int)xw;
+      const float v0 = (xi >= 0 && xi <= Wl - 1) ? lv[xi] : 0.0f;
+      const float v1 = (xi + 1 >= 0 && xi + 1 <= Wl - 1) ? lv[xi + 1] : 0.0f;
+      f[l * K + t + R] = v0 * e + v1 * w;
+    }
+  }
+  float *__restrict__ o = out + (b * nvol + v) * COUT * hw + rem;
+#pragma unroll 4
+  for (int c0 = 0; c0 < COUT; c0 += 8) {
+    float acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = bias[c0 + c];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[c] = fmaf(wt[k * COUT + c0 + c], f[k], acc[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) o[(long)(c0 + c) * hw] = fmaxf(acc[c], 0.0f);
+  }
+}
+
 }  // namespace
+
+extern "C" int sa_corr_lookup_conv1x1(const float *pyramid_a, const float *pyramid_b, int W2, long row_stride,
+                                      int num_levels, int radius, const float *coords_x, long coords_bstride,
+                                      int B, int H, int W1, const float *weight_kc, const float *bias, int Cout,
+                                      float *out, void *stream) {
+  SA_REQUIRE(pyramid_a && coords_x && out && weight_kc && bias, "sa_corr_lookup_conv1x1: null pointer");
+  SA_REQUIRE(B > 0 && H > 0 && W1 > 0 && W2 > 0, "sa_corr_lookup_conv1x1: empty shape");
+  SA_REQUIRE(num_levels == 4 && radius == 4 && Cout == 64,
+             "sa_corr_lookup_conv1x1: built for 4 levels, radius 4, 64 outputs (got %d, %d, %d)", num_levels, radius,
+             Cout);
+  SA_REQUIRE(sa_pyramid_level_width(W2, num_levels - 1) >= 2,
+             "sa_corr_lookup_conv1x1: level %d of width %d is too narrow to sample", num_levels - 1,
+             sa_pyramid_level_width(W2, num_levels - 1));
+  SA_REQUIRE(row_stride >= sa_pyramid_level_offset(W2, num_levels), "sa_corr_lookup_conv1x1: row_stride too small");
+  const int nvol = pyramid_b ? 2 : 1;
+  LGeo g{};
+  g.H = H;
+  g.W1 = W1;
+  g.L = num_levels;
+  g.r = radius;
+  g.rs = row_stride;
+  g.cbs = coords_bstride;
+  for (int i = 0; i < 4; ++i) {
+    g.off[i] = sa_pyramid_level_offset(W2, i);
+    g.wid[i] = sa_pyramid_level_width(W2, i);
+  }
+  const long npix = (long)B * H * W1;
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_LOOKUP, s);
+  dim3 grid((unsigned)((npix + 255) / 256), nvol);
+  lookup_c1_kernel<4, 4, 64><<<grid, 256, 0, s>>>(pyramid_a, pyramid_b ? pyramid_b : pyramid_a, coords_x, g, npix,
+                                                  weight_kc, bias, nvol, out);
+  return sa::check_launch("sa_corr_lookup_conv1x1");
+}
 
 extern "C" int sa_corr_lookup(const float *pyramid_a, const float *pyramid_b, int W2, long row_stride,
                               int num_levels, int radius, const float *coords_x, long coords_bstride,

@@ -113,12 +113,9 @@ class StereoAnywhere(nn.Module):
                 self._derived.update(
                     # folded eval-BatchNorm affines of the encoders (encoders.py)
                     bn_cnet=encoders.bn_table(self.cnet), bn_fnet=encoders.bn_table(self.fnet),
-                    mot_b126=ub.encoder._conv.bias[:126].contiguous(),
                     head_b=[(self.cnet.outputs08[0][1].bias, self.cnet.outputs08[1][1].bias),
                             (self.cnet.outputs16[0][1].bias, self.cnet.outputs16[1][1].bias),
                             (self.cnet.outputs32[0].bias, self.cnet.outputs32[1].bias)],
-                    bias_c1=ops.Affine(t=enc.convc1.bias), bias_c2=ops.Affine(t=enc.convc2.bias),
-                    bias_f2=ops.Affine(t=enc.convf2.bias), bias_fh1=ops.Affine(t=ub.flow_head.conv1.bias),
                 )
                 # Winograd F(2x2,3x3) filters (ops.conv2d_k3) of every eligible 3x3 conv
                 d = self._derived
@@ -127,7 +124,8 @@ class StereoAnywhere(nn.Module):
                     g = d[gk]
                     g.update(Ux=ops.wino_weights(g["wx"]), Uhzr=ops.wino_weights(g["whzr"]),
                              Uqh=ops.wino_weights(g["wqh"]))
-                d.update(U_c2=ops.wino_weights(enc.convc2.weight.detach().contiguous()),
+                d.update(c1_kc=enc.convc1.weight.detach().reshape(enc.convc1.out_channels, -1).t().contiguous(),
+                         U_c2=ops.wino_weights(enc.convc2.weight.detach().contiguous()),
                          U_f2=ops.wino_weights(enc.convf2.weight.detach().contiguous()),
                          U_mot=ops.wino_weights(d["mot_w"]),
                          U_fh1=ops.wino_weights(ub.flow_head.conv1.weight.detach().contiguous()),
@@ -256,8 +254,8 @@ class StereoAnywhere(nn.Module):
         h08, h16, h32 = hid
         H8, W8 = h16.shape[2:]
         H16, W16 = h32.shape[2:]
-        K = enc.convc1.in_channels
-        corr_buf = torch.empty((B, 2 * K, H4, W4), device=dev, dtype=f32)   # [stereo | mono] lookups
+        c1 = torch.empty((2 * B, enc.convc1.out_channels, H4, W4), device=dev, dtype=f32)  # convc1(lookups)
+        motin = torch.empty((B, 192, H4, W4), device=dev, dtype=f32)  # [convc2 stereo | mono | convf2]
         flow = torch.empty((B, 2, H4, W4), device=dev, dtype=f32)
         x08 = torch.empty((B, 256, H4, W4), device=dev, dtype=f32)   # [motion(126) | flow(2) | interp(h16)]
         x16 = torch.empty((B, 256, H8, W8), device=dev, dtype=f32)   # [pool(h08) | interp(h32)]
@@ -279,7 +277,8 @@ class StereoAnywhere(nn.Module):
         ops.flow_update(coords_x, None, flow, x08[:, 126:128])
         flow_up = None
         for it in range(iters):
-            stereo_blk.lookup_into(coords_x, corr_buf, other=mono_blk)
+            # lookup of both pyramids + convc1 + ReLU in one kernel (sample 2b: stereo, 2b+1: mono)
+            stereo_blk.lookup_conv1x1_into(coords_x, dw["c1_kc"], enc.convc1.bias, c1, other=mono_blk)
             # update.py:166-183, in order: gru32, gru16, motion encoder, gru08
             ops.pool2x(h16, x32)
             gru(2, h32, x32, "32")
@@ -287,16 +286,16 @@ class StereoAnywhere(nn.Module):
             ops.interp(h32, x16[:, 128:])
             gru(1, h16, x16, "16")
             # shared convc1/convc2 on the stereo and mono lookups as one 2B batch
-            # conv + bias + ReLU as MIOpen conv (no bias) + one norm_act pass
-            c = F.conv2d(corr_buf.view(2 * B, K, H4, W4), enc.convc1.weight)
-            c = ops.norm_act(c, dw["bias_c1"], act_in="relu", out=c)
-            # 3x3 convs with bias + ReLU in the Winograd epilogue
-            c = ops.conv2d_k3(c, dw["U_c2"], enc.convc2.bias, relu=True).view(B, 128, H4, W4)
+            # 3x3 convs with bias + ReLU in the Winograd epilogue, written straight into the
+            # motion conv's input: cat(convc2(stereo), convc2(mono), convf2(convf1(flow)))
+            c1v = c1.view(B, 2, c1.shape[1], H4, W4)
+            for v in range(2):
+                ops.conv2d_k3(c1v[:, v], dw["U_c2"], enc.convc2.bias, relu=True, out=motin[:, 64 * v:64 * v + 64])
             fl = ops.conv2d_small(flow, dw["f1"], enc.convf1.bias, 64, 7, relu=True)
-            fl = ops.conv2d_k3(fl, dw["U_f2"], enc.convf2.bias, relu=True)
+            ops.conv2d_k3(fl, dw["U_f2"], enc.convf2.bias, relu=True, out=motin[:, 128:192])
             # _conv (126 outputs, padded to 128) writes x08[:, :128]; channels 126-127 (the flow)
             # are rewritten right after from the coordinates
-            ops.conv2d_k3(torch.cat([c, fl], 1), dw["U_mot"], dw["mot_b"], relu=True, out=x08[:, :128])
+            ops.conv2d_k3(motin, dw["U_mot"], dw["mot_b"], relu=True, out=x08[:, :128])
             ops.flow_update(coords_x, None, None, x08[:, 126:128])
             ops.interp(h16, x08[:, 128:])
             gru(0, h08, x08, "08")

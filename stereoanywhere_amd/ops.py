@@ -137,6 +137,35 @@ def corr_lookup(pyr_a: torch.Tensor, pyr_b: Optional[torch.Tensor], W2: int, num
     return out
 
 
+def corr_lookup_conv1x1(pyr_a: torch.Tensor, pyr_b: Optional[torch.Tensor], W2: int, num_levels: int, radius: int,
+                        coords_x: torch.Tensor, weight_kc: torch.Tensor, bias: torch.Tensor,
+                        out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Lookup fused with a 1x1 conv + bias + ReLU of the taps (the motion encoder's convc1):
+    weight_kc [L*(2r+1), Cout] -> out [B*nvol, Cout, H, W1], sample b*nvol + v."""
+    _check(pyr_a, "pyramid_a")
+    if pyr_b is not None:
+        _check(pyr_b, "pyramid_b")
+        if pyr_b.shape != pyr_a.shape:
+            raise RuntimeError("both pyramids must share a geometry")
+    _check(weight_kc, "weight_kc")
+    _check(bias, "bias")
+    cbs = _plane_bs(coords_x, "coords_x")
+    B, _, H, W1 = coords_x.shape
+    if pyr_a.shape[0] != B * H * W1:
+        raise RuntimeError(f"pyramid rows {pyr_a.shape[0]} != B*H*W1 {B * H * W1}")
+    nvol = 2 if pyr_b is not None else 1
+    Cout = weight_kc.shape[1]
+    if weight_kc.shape[0] != num_levels * (2 * radius + 1):
+        raise RuntimeError("weight_kc must be [L*(2r+1), Cout]")
+    if out is None:
+        out = torch.empty((B * nvol, Cout, H, W1), device=pyr_a.device, dtype=torch.float32)
+    _check(out, "out")
+    N.call("sa_corr_lookup_conv1x1", pyr_a.data_ptr(), _ptr(pyr_b), W2, pyr_a.shape[1], num_levels, radius,
+           coords_x.data_ptr(), cbs, B, H, W1, weight_kc.data_ptr(), bias.data_ptr(), Cout, out.data_ptr(),
+           _stream(pyr_a))
+    return out
+
+
 # ----------------------------------------------------------------------- a2 + a3
 def mono_normals(mde_lowres: torch.Tensor, gain: float) -> torch.Tensor:
     _check(mde_lowres, "mde_lowres")

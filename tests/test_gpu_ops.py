@@ -92,6 +92,24 @@ def test_lookup_two_volumes_one_launch():
     np.testing.assert_allclose(out, ref, atol=1e-5)
 
 
+def test_lookup_fused_convc1():
+    """Lookup + 1x1 conv (36 -> 64) + bias + ReLU in one kernel vs the oracle lookup followed by
+    the conv in numpy; sample 2b is the stereo pyramid, 2b + 1 the mono one."""
+    rng = np.random.default_rng(6)
+    B, H, W = 2, 5, 72
+    va = rng.standard_normal((B, H, W, W)).astype(np.float32)
+    vb = rng.standard_normal((B, H, W, W)).astype(np.float32)
+    cx = (rng.random((B, 1, H, W)) * 100 - 20).astype(np.float32)
+    wt = (rng.standard_normal((64, 36)) / 6).astype(np.float32)
+    bias = rng.standard_normal(64).astype(np.float32)
+    pa, pb = ops.pyramid_from_volume(g(va)), ops.pyramid_from_volume(g(vb))
+    out = c(ops.corr_lookup_conv1x1(pa, pb, W, 4, 4, g(cx), g(wt.T.copy()), g(bias)))
+    for v, vol in enumerate((va, vb)):
+        taps = R.corr_lookup(R.corr_pyramid(vol), cx[:, 0])               # [B, 36, H, W]
+        ref = np.maximum(np.einsum("ok,bkhw->bohw", wt.astype(np.float64), taps) + bias[None, :, None, None], 0)
+        np.testing.assert_allclose(out[v::2], ref, atol=2e-5)
+
+
 def test_hip_corr_block_contract(micro):
     from stereoanywhere_amd.corr import HipCorrBlock1D
     blk = HipCorrBlock1D(g(micro["corr.out"]), num_levels=4, radius=4)
