@@ -77,7 +77,7 @@ struct WinoIO {
   double *partial;
 };
 
-template <int CG>
+template <int CG, bool AFF>
 __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
     const float *__restrict__ in, long in_bs, int Cin, int H, int W, const float *__restrict__ U, int Cout,
     const float *__restrict__ bias, int relu, float *__restrict__ out, long out_bs, int tiles_w, int tiles_hw,
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
       const_cast<float *>(src), (short)0, (int)((long)Cin * hw * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t uin = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float *>(U), (short)0, (int)(16L * Cin * Cout * 4), 0x00020000);
-  const bool in_aff = io.m || io.s || io.t || io.act;
+  constexpr bool in_aff = AFF;  // producer epilogue on load (a template flag: free when off)
   if (in_aff) {
     for (int c = tid; c < Cin; c += 512) {
       const int pi = n * io.pstride + c;
@@ -402,12 +402,15 @@ extern "C" int sa_conv2d_k3_wino_ex(const float *in, long in_bs, int N, int Cin,
   const WinoIO io{in_m, in_s, in_t, in_pstride, in_act, stats_partial};
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV2D, s);
-  if (cg == 2)
-    wino_f2k3_kernel<2><<<(unsigned)nblk, 512, 0, s>>>(in, in_bs, Cin, H, W, U, Cout, bias, relu, out, out_bs,
-                                                       tiles_w, tiles_w * tiles_h, co_blocks, io);
-  else
-    wino_f2k3_kernel<1><<<(unsigned)nblk, 512, 0, s>>>(in, in_bs, Cin, H, W, U, Cout, bias, relu, out, out_bs,
-                                                       tiles_w, tiles_w * tiles_h, co_blocks, io);
+#define SA_WINO(CGV, AFFV)                                                                                   \
+  wino_f2k3_kernel<CGV, AFFV><<<(unsigned)nblk, 512, 0, s>>>(in, in_bs, Cin, H, W, U, Cout, bias, relu, out, out_bs, \
+                                                             tiles_w, tiles_w * tiles_h, co_blocks, io)
+  if (cg == 2) {
+    if (aff) SA_WINO(2, true); else SA_WINO(2, false);
+  } else {
+    if (aff) SA_WINO(1, true); else SA_WINO(1, false);
+  }
+#undef SA_WINO
   return sa::check_launch("sa_conv2d_k3_wino");
 }
 
