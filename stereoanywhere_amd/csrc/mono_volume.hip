@@ -43,16 +43,17 @@ __device__ __forceinline__ int depth_bin(float m, int nbins) {
   return -1;
 }
 
-// one thread = 4 consecutive j of one (b, k, h): float4 stores into each of the nbins planes
-template <int NB>
+// one thread = VEC consecutive j of one (b, k, h): VEC-wide stores into each of the nbins
+// planes (VEC = 4 when W1 % 4 == 0, else 1)
+template <int NB, int VEC>
 __global__ __launch_bounds__(256) void masked_volume_kernel(
     const float *__restrict__ n2, const float *__restrict__ n3, const float *__restrict__ m2,
     const float *__restrict__ m3, int H, int W1, int W2, float gain, long nthreads,
     float *__restrict__ out) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nthreads) return;
-  const int q = W1 / 4;
-  const int j0 = (int)(t % q) * 4;
+  const int q = W1 / VEC;
+  const int j0 = (int)(t % q) * VEC;
   const long r1 = t / q;
   const int h = (int)(r1 % H);
   const long r2 = r1 / H;
@@ -63,25 +64,42 @@ __global__ __launch_bounds__(256) void masked_volume_kernel(
   const long pk = b * 3 * hw2 + (long)h * W2 + k;
   const float c0 = n3[pk], c1 = n3[pk + hw2], c2 = n3[pk + 2 * hw2];
   const int bk = depth_bin(m3[b * hw2 + (long)h * W2 + k], NB);
-  const float4 a0 = *reinterpret_cast<const float4 *>(nl);
-  const float4 a1 = *reinterpret_cast<const float4 *>(nl + hw1);
-  const float4 a2 = *reinterpret_cast<const float4 *>(nl + 2 * hw1);
-  const float4 ml = *reinterpret_cast<const float4 *>(m2 + b * hw1 + (long)h * W1 + j0);
+  float a0[VEC], a1[VEC], a2[VEC], ml[VEC];
+  if constexpr (VEC == 4) {
+    const float4 x0 = *reinterpret_cast<const float4 *>(nl);
+    const float4 x1 = *reinterpret_cast<const float4 *>(nl + hw1);
+    const float4 x2 = *reinterpret_cast<const float4 *>(nl + 2 * hw1);
+    const float4 mm = *reinterpret_cast<const float4 *>(m2 + b * hw1 + (long)h * W1 + j0);
+    a0[0] = x0.x; a0[1] = x0.y; a0[2] = x0.z; a0[3] = x0.w;
+    a1[0] = x1.x; a1[1] = x1.y; a1[2] = x1.z; a1[3] = x1.w;
+    a2[0] = x2.x; a2[1] = x2.y; a2[2] = x2.z; a2[3] = x2.w;
+    ml[0] = mm.x; ml[1] = mm.y; ml[2] = mm.z; ml[3] = mm.w;
+  } else {
+    a0[0] = nl[0];
+    a1[0] = nl[hw1];
+    a2[0] = nl[2 * hw1];
+    ml[0] = m2[b * hw1 + (long)h * W1 + j0];
+  }
   const float sq3 = sqrtf(3.0f);
-  auto cell = [&](float x0, float x1, float x2) { return gain * ((x0 * c0 + x1 * c1 + x2 * c2) / sq3); };
-  const float v[4] = {cell(a0.x, a1.x, a2.x), cell(a0.y, a1.y, a2.y), cell(a0.z, a1.z, a2.z),
-                      cell(a0.w, a1.w, a2.w)};
-  const int bj[4] = {depth_bin(ml.x, NB), depth_bin(ml.y, NB), depth_bin(ml.z, NB), depth_bin(ml.w, NB)};
+  float v[VEC];
+  int bj[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    v[e] = gain * ((a0[e] * c0 + a1[e] * c1 + a2[e] * c2) / sq3);
+    bj[e] = depth_bin(ml[e], NB);
+  }
   float *o = out + ((b * NB) * W2 + k) * hw1 + (long)h * W1 + j0;
   const long plane = (long)W2 * hw1;
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
-    float4 r;
-    r.x = (bk == n && bj[0] == n) ? v[0] : 0.0f;
-    r.y = (bk == n && bj[1] == n) ? v[1] : 0.0f;
-    r.z = (bk == n && bj[2] == n) ? v[2] : 0.0f;
-    r.w = (bk == n && bj[3] == n) ? v[3] : 0.0f;
-    *reinterpret_cast<float4 *>(o + n * plane) = r;
+    float r[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) r[e] = (bk == n && bj[e] == n) ? v[e] : 0.0f;
+    if constexpr (VEC == 4) {
+      *reinterpret_cast<float4 *>(o + n * plane) = make_float4(r[0], r[1], r[2], r[3]);
+    } else {
+      o[n * plane] = r[0];
+    }
   }
 }
 
@@ -103,14 +121,16 @@ extern "C" int sa_mono_masked_volume(const float *n2, const float *n3, const flo
                                      void *stream) {
   SA_REQUIRE(n2 && n3 && m2 && m3 && out, "sa_mono_masked_volume: null pointer");
   SA_REQUIRE(B > 0 && H > 0 && W1 > 0 && W2 > 0, "sa_mono_masked_volume: empty shape");
-  SA_REQUIRE(W1 % 4 == 0, "sa_mono_masked_volume: W1 must be a multiple of 4 (got %d)", W1);
   SA_REQUIRE(nbins == 8, "sa_mono_masked_volume: only vol_n_masks == 8 is built (got %d)", nbins);
-  SA_REQUIRE(((uintptr_t)n2 | (uintptr_t)m2 | (uintptr_t)out) % 16 == 0,
-             "sa_mono_masked_volume: n2/m2/out must be 16-byte aligned");
-  const long nthreads = (long)B * W2 * H * (W1 / 4);
+  const bool vec = W1 % 4 == 0 && ((uintptr_t)n2 | (uintptr_t)m2 | (uintptr_t)out) % 16 == 0;
+  const long nthreads = (long)B * W2 * H * (vec ? W1 / 4 : W1);
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_MONO_VOLUME, s);
-  masked_volume_kernel<8><<<(unsigned)((nthreads + 255) / 256), 256, 0, s>>>(n2, n3, m2, m3, H, W1, W2, gain,
-                                                                          nthreads, out);
+  const unsigned grid = (unsigned)((nthreads + 255) / 256);
+  if (vec) {
+    masked_volume_kernel<8, 4><<<grid, 256, 0, s>>>(n2, n3, m2, m3, H, W1, W2, gain, nthreads, out);
+  } else {
+    masked_volume_kernel<8, 1><<<grid, 256, 0, s>>>(n2, n3, m2, m3, H, W1, W2, gain, nthreads, out);
+  }
   return sa::check_launch("sa_mono_masked_volume");
 }

@@ -158,8 +158,10 @@ class StereoAnywhere(nn.Module):
         a = self.args
         dw = self._weights()
         B, C, H, W = image2.shape
-        if H % 32 or W % 32:
-            raise RuntimeError(f"H and W must be multiples of 32 (callers pad, test.py:206-213); got {H}x{W}")
+        if H % 4 or W % 4:
+            # the reference fails on these too (its hourglass skip shapes stop matching);
+            # callers pad to x32 (test.py:206-213)
+            raise RuntimeError(f"H and W must be multiples of 4; got {H}x{W}")
         H4, W4 = H // 4, W // 4
         dev = image2.device
         f32 = torch.float32

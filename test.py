@@ -10,6 +10,7 @@ Same flags, same per-sample procedure:
 DAv2 is outside this tier: --monomodel DAv2 needs precomputed maps (--mono_tag) as written
 by mono_sceneflow-style preprocessing.  Datasets: `middlebury` (folder layout of
 middlebury_dataset.py) and `synthetic` (seeded pairs with true disparity).
+The tiled harness (configs 3 and 5) is test_mapreduce_v2.py.
 Multi-GPU: run under torchrun; samples are split across ranks and the per-sample metric
 rows are all-gathered to rank 0 (the only exchange).
 """
@@ -77,7 +78,6 @@ def build_parser():
     p.add_argument("--iters", type=int, default=32)
     # build-specific
     p.add_argument("--mono_tag", default="dav2", help="file tag of precomputed mono maps (im0_<tag>.png)")
-    p.add_argument("--tile_preset", default=None, help="run through the tiler with a mapreduce_v2 preset")
     p.add_argument("--synthetic_size", default="540x960", help="HxW of --dataset synthetic")
     p.add_argument("--synthetic_count", type=int, default=4)
     return p
@@ -114,17 +114,14 @@ def run(net, sample, args, device):
         m2, m3 = (m2 - lo) / (hi - lo), (m3 - lo) / (hi - lo)  # joint min-max (test.py:198)
     else:
         m2, m3 = torch.zeros_like(im2[:, :1]), torch.zeros_like(im3[:, :1])
-    if args.tile_preset:
-        pred = tiler.from_preset(net, args.tile_preset)(im2, im3, m2, m3, iters=args.iters)[:, 0]
-    else:
-        pad = tiler.pad32(*im2.shape[-2:])
+    pad = tiler.pad32(*im2.shape[-2:])
 
-        def P(x):
-            return F.pad(x, pad, mode="replicate")
-        flow_up, _ = net(P(im2), P(im3), P(m2), P(m3), test_mode=True, iters=args.iters)
-        pred = -flow_up[:, 0]
-        hd, wd = pred.shape[-2:]
-        pred = pred[..., pad[2]:hd - pad[3], pad[0]:wd - pad[1]]
+    def P(x):
+        return F.pad(x, pad, mode="replicate")
+    flow_up, _ = net(P(im2), P(im3), P(m2), P(m3), test_mode=True, iters=args.iters)
+    pred = -flow_up[:, 0]
+    hd, wd = pred.shape[-2:]
+    pred = pred[..., pad[2]:hd - pad[3], pad[0]:wd - pad[1]]
     if args.iscale != 1 and args.iscale / args.oscale != 1:
         pred = F.interpolate(pred[None], t["gt"].shape[-2:], mode="nearest")[0] * args.iscale / args.oscale
     res = metrics.guided_metrics(pred.cpu().numpy(), t["gt"][:, 0].numpy(), t["validgt"][:, 0].numpy(),

@@ -28,6 +28,7 @@ import json
 import os
 import sys
 import types
+import warnings
 
 import numpy as np
 import torch
@@ -329,6 +330,70 @@ def tiler_cases():
     return out
 
 
+def mapreduce_cases():
+    """The reference's MapReduceInference (mapreduce_v2/tiled_inference.py:25-336) on the
+    same mock model: uint8 inputs, bilinear iscale, nearest oscale, post_scale and an
+    explicit global-guidance map (the automatic guidance pass needs cv2, absent here).
+    The package __init__ imports cv2 (non_lambertian.py), so the three modules are loaded
+    as members of a bare package object."""
+    import importlib
+    pkg = types.ModuleType("ref_mr")
+    pkg.__path__ = [os.path.join(REF, "mapreduce_v2")]
+    sys.modules["ref_mr"] = pkg
+    ti = importlib.import_module("ref_mr.tiled_inference")
+
+    class Mock(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.p = torch.nn.Parameter(torch.zeros(1))
+
+        def forward(self, l, r, ml, mr, iters=1, test_mode=True):
+            H, W = l.shape[-2:]
+            ramp = torch.arange(W, dtype=torch.float32).view(1, 1, 1, W) / W
+            return -(40 * l[:, :1] - 10 * r[:, 1:2] + ml * 3 + ramp + H / 100.0), None
+
+    rng = np.random.default_rng(7)
+    out = {}
+    cases = [  # H, W, tile_w, tile_h, overlap, iscale, oscale, post_scale, guidance (None / "half" / "full"), weight
+        (150, 230, 96, 64, 20, 1.0, 1.0, 1.0, None, 0.3),
+        (150, 230, 96, 64, 20, 2.0, 1.0, 1.0, None, 0.3),
+        (128, 192, 64, 64, 32, 1.0, 2.0, 1.5, "half", 0.5),
+        (128, 192, 64, 64, 32, 1.0, 1.0, 1.0, "full", 0.3),
+        (100, 120, 128, 128, 32, 1.0, 1.0, 2.0, "half", 0.5),   # one tile: guidance unused
+        (96, 160, 0, 0, 0, 1.0, 1.0, 1.0, None, 0.3),           # square tiles (tile_size 64, overlap 16 -> 32)
+    ]
+    for i, (H, W, tw_, th, ov, isc, osc, ps, gmode, gw) in enumerate(cases):
+        l = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        r = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        ml = torch.from_numpy(rng.random((1, 1, H, W), dtype=np.float32))
+        mr = torch.from_numpy(rng.random((1, 1, H, W), dtype=np.float32))
+        if tw_:
+            inf = ti.MapReduceInference(Mock(), tile_width=tw_, tile_height=th, overlap=ov, guidance_weight=0.2)
+        else:
+            inf = ti.MapReduceInference(Mock(), tile_size=64, overlap=16, guidance_weight=0.2)
+        g = None
+        ht, wt = round(H / isc), round(W / isc)
+        if gmode == "half":
+            g = (rng.random((ht // 2, wt // 2), dtype=np.float32) * 30).astype(np.float32)
+        elif gmode == "full":
+            g = torch.from_numpy((rng.random((1, 1, ht, wt), dtype=np.float32) * 30).astype(np.float32))
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            d = inf.infer(l, r, iscale=isc, oscale=osc, post_scale=ps, mono_pair=(ml, mr), global_guidance=g,
+                          guidance_weight=gw, iters=1, test_mode=True)
+        out[f"case{i}.geom"] = np.array([H, W, tw_, th, ov], np.int64)
+        out[f"case{i}.scales"] = np.array([isc, osc, ps, gw], np.float64)
+        out[f"case{i}.l"], out[f"case{i}.r"] = l, r
+        out[f"case{i}.ml"], out[f"case{i}.mr"] = _np(ml), _np(mr)
+        if g is not None:
+            out[f"case{i}.guide"] = g if isinstance(g, np.ndarray) else _np(g)
+            out[f"case{i}.guide_is_tensor"] = np.array(not isinstance(g, np.ndarray))
+        out[f"case{i}.wrapper"] = np.array([inf.tile_wrapper.tile_width, inf.tile_wrapper.tile_height,
+                                            inf.tile_wrapper.overlap])
+        out[f"case{i}.out"] = np.asarray(d, np.float32)
+    return out
+
+
 def metrics_cases():
     """losses.guided_metrics (losses.py:273-342) on random disparities with occlusion masks,
     including the all-zero-occlusion branch."""
@@ -351,6 +416,23 @@ def metrics_cases():
         out[f"case{i}.keys"] = np.array(keys)
         out[f"case{i}.values"] = np.array([float(res[k]) for k in keys], dtype=np.float64)
         out[f"case{i}.errormap"] = res["errormap"].astype(np.float32)
+    return out
+
+
+def odd_size_cases(model):
+    """The reference model on sizes that are multiples of 4 but not of 32 — what it accepts
+    unpadded (the tiled harness's guidance pass feeds it such sizes, tiled_inference.py:
+    199-207): 64x100 (W/4 odd) and 120x168, cropped from one synthetic pair, 4 iterations."""
+    base = synth.synthetic_batch(1, 128, 192, 24.0, seed0=5)
+    out = {}
+    for i, (H, W) in enumerate([(64, 100), (120, 168)]):
+        t = [torch.from_numpy(np.ascontiguousarray(base[k][..., :H, :W])) for k in
+             ("left", "right", "mono_left", "mono_right")]
+        with torch.no_grad():
+            flow_up = model(*t, iters=4, test_mode=True)[0]
+        for k, v in zip(("left", "right", "mono_left", "mono_right"), t):
+            out[f"case{i}.{k}"] = _np(v)
+        out[f"case{i}.disparity"] = -_np(flow_up)[:, 0]
     return out
 
 
@@ -378,7 +460,9 @@ def main():
 
     np.savez_compressed(os.path.join(HERE, "micro_ops.npz"), **micro_cases(ut, corr_mod))
     np.savez_compressed(os.path.join(HERE, "tiler.npz"), **tiler_cases())
+    np.savez_compressed(os.path.join(HERE, "mapreduce.npz"), **mapreduce_cases())
     np.savez_compressed(os.path.join(HERE, "metrics.npz"), **metrics_cases())
+    np.savez_compressed(os.path.join(HERE, "odd_sizes.npz"), **odd_size_cases(model))
 
     # tiny end-to-end case with every intermediate
     pair = synth.synthetic_batch(1, 64, 128, 24.0, seed0=1)

@@ -49,6 +49,26 @@ def test_end_to_end_vs_reference(model, name, H, W, D, iters):
     assert e < 1e-3
 
 
+@pytest.mark.parametrize("i,H,W", [(0, 64, 100), (1, 120, 168)])
+def test_unpadded_sizes_vs_reference(model, i, H, W):
+    """Sizes that are multiples of 4 but not 32 run unpadded, as in the reference (the tiled
+    harness's guidance pass does this): W/4 odd, non-power-of-two pyramid levels, and the
+    hourglass on its general (unfused) path."""
+    fix = load_fixture("odd_sizes.npz")
+    pair = {k: fix[f"case{i}.{k}"] for k in ("left", "right", "mono_left", "mono_right")}
+    assert pair["left"].shape[-2:] == (H, W)
+    disp = run(model, pair, 4)
+    e = epe(disp, fix[f"case{i}.disparity"])
+    print("unpadded", H, W, "EPE", e)
+    assert e < 1e-3
+
+
+def test_size_not_multiple_of_4_is_rejected(model):
+    t = [torch.zeros(1, c, 66, 98, device="cuda") for c in (3, 3, 1, 1)]
+    with pytest.raises(RuntimeError):
+        model(*t, iters=1, test_mode=True)
+
+
 def test_batch_independence(model):
     """Pairs are independent: a B=3 batch equals three B=1 runs."""
     pb = synth.synthetic_batch(3, 128, 256, 48.0, seed0=5)

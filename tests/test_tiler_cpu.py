@@ -10,6 +10,10 @@ from stereoanywhere_amd import tiler
 
 
 class Mock(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.p = torch.nn.Parameter(torch.zeros(1))   # TileWrapper.device reads the model's parameters
+
     def forward(self, l, r, ml, mr, iters=1, test_mode=True):
         H, W = l.shape[-2:]
         ramp = torch.arange(W, dtype=torch.float32).view(1, 1, 1, W) / W
@@ -30,7 +34,7 @@ def test_tiles_weights_and_stitch_match_reference(fix, i):
     t = {k: torch.from_numpy(fix[f"case{i}.{k}"]) for k in ("l", "r", "ml", "mr")}
     for batch in (False, True):
         wrap = tiler.TileWrapper(Mock(), tile_width=tw, tile_height=th, overlap=ov, batch_tiles=batch)
-        out = wrap(t["l"], t["r"], t["ml"], t["mr"], iters=1)
+        out = wrap(t["l"], t["r"], t["ml"], t["mr"], iters=1, test_mode=True)
         np.testing.assert_allclose(out.numpy(), fix[f"case{i}.out"], atol=1e-6)
 
 
