@@ -33,7 +33,10 @@ def timeit(fn, reps=10):
 def main():
     torch.backends.cudnn.benchmark = "--find" in sys.argv
     dev = torch.device("cuda", 0)
+    only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--shape=")]
     for name, N, Cin, Cout, H, W in SHAPES:
+        if only and name not in only:
+            continue
         x = torch.randn(N, Cin, H, W, device=dev)
         w = torch.randn(Cout, Cin, 3, 3, device=dev) / (3 * Cin ** 0.5)
         U = ops.wino_weights(w)

@@ -58,6 +58,10 @@ struct Wino {
   static_assert(SMEM * 4 <= 160 * 1024, "LDS budget");
 };
 
+#ifndef SA_WINO_SCHED
+#define SA_WINO_SCHED 0
+#endif
+
 #ifndef SA_WINO_WAVES_PER_EU
 #define SA_WINO_WAVES_PER_EU 2
 #endif
@@ -122,7 +126,11 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
     const int y = y0 - 1 + r, x = x0 - 1 + cc;
     xc[j] = ci;
     xo[j] = (ci * (int)hw + min(max(y, 0), H - 1) * W + min(max(x, 0), W - 1)) * 4;
-    xl[j] = tid + 512 * j < NX ? ci * XCP + r * XS + cc : -1;
+    // without an input transform, padding taps read past the buffer's range: the load
+    // returns 0 (raw buffer range check on the VGPR offset), so no select is needed
+    if (!AFF && (y < 0 || y >= H || x < 0 || x >= W)) xo[j] = 0x7ffffff0;
+    // threads without a slot store into the unused tail of channel 0's plane (branch-free)
+    xl[j] = tid + 512 * j < NX ? ci * XCP + r * XS + cc : XCP - 1;
     if (y < 0 || y >= H || x < 0 || x >= W) xpad |= 1u << j;
   }
   // U chunk image: global [xi][Cin/8][4][Cout][2] -> LDS rows (xi, ci4) of CO swizzled pairs
@@ -149,17 +157,19 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
       ur[j] = f32x4{__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3])};
     }
   };
+  const float act_floor = io.act ? 0.0f : -INFINITY;   // ReLU or identity, branch-free
   auto commit_x = [&](int buf, int chunk) __attribute__((always_inline)) {
     float *sx = smem + Cfg::X_OFF + buf * Cfg::XSZ;
+    const int cb = min(chunk, Cin / KC - 1) * KC;
 #pragma unroll
     for (int j = 0; j < XPT; ++j) {
       float v = xr[j];
       if (in_aff) {
-        const float2 p = tab[chunk * KC + xc[j]];
-        v = v * p.x + p.y;
-        if (io.act) v = fmaxf(v, 0.0f);
+        const float2 p = tab[cb + xc[j]];
+        v = fmaxf(v * p.x + p.y, act_floor);
       }
-      if (xl[j] >= 0) sx[xl[j]] = ((xpad >> j) & 1u) ? 0.0f : v;
+      if (in_aff) v = ((xpad >> j) & 1u) ? 0.0f : v;
+      sx[xl[j]] = v;
     }
   };
   auto commit_u = [&](int buf) __attribute__((always_inline)) {
@@ -168,8 +178,11 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
     for (int j = 0; j < UPT; ++j) *reinterpret_cast<f32x4 *>(su + ul[j]) = ur[j];
   };
   // input transform V = B^T d B of (channel tid >> 6, tile tid & 63) into its slot of the
-  // (c, c + 4) pair image; every thread has one job per chunk
-  auto transform = [&](int buf) __attribute__((always_inline)) {
+  // (c, c + 4) pair image; every thread has one job per chunk.  Split in three parts so the
+  // work spreads over a chunk's MFMAs: read + row pass, then the column pass and writes of
+  // transform rows 0-1 and 2-3.
+  float tw[4][4];
+  auto transform_read = [&](int buf) __attribute__((always_inline)) {
     const int ci = tid >> 6, t = tid & 63;
     const int ty = t / TC, tx = t % TC;
     const float *p = smem + Cfg::X_OFF + buf * Cfg::XSZ + ci * XCP + 2 * ty * XS + 2 * tx;
@@ -179,23 +192,30 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
 #pragma unroll
       for (int c = 0; c < 4; ++c) d[r][c] = p[r * XS + c];
     // B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]
-    float w[4][4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      w[0][c] = d[0][c] - d[2][c];
-      w[1][c] = d[1][c] + d[2][c];
-      w[2][c] = d[2][c] - d[1][c];
-      w[3][c] = d[1][c] - d[3][c];
+      tw[0][c] = d[0][c] - d[2][c];
+      tw[1][c] = d[1][c] + d[2][c];
+      tw[2][c] = d[2][c] - d[1][c];
+      tw[3][c] = d[1][c] - d[3][c];
     }
+  };
+  auto transform_write = [&](int buf, int r0) __attribute__((always_inline)) {
+    const int ci = tid >> 6, t = tid & 63;
     // rows xi * 4 + (ci & 3) all have the parity of ci & 3: one swizzled column for all xi
     float *o = smem + Cfg::V_OFF + buf * Cfg::VSZ + swz(ci & 3, t, NT) * 2 + (ci >> 2);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      o[((r * 4 + 0) * 4) * NT * 2] = w[r][0] - w[r][2];
-      o[((r * 4 + 1) * 4) * NT * 2] = w[r][1] + w[r][2];
-      o[((r * 4 + 2) * 4) * NT * 2] = w[r][2] - w[r][1];
-      o[((r * 4 + 3) * 4) * NT * 2] = w[r][1] - w[r][3];
+    for (int r = r0; r < r0 + 2; ++r) {
+      o[((r * 4 + 0) * 4) * NT * 2] = tw[r][0] - tw[r][2];
+      o[((r * 4 + 1) * 4) * NT * 2] = tw[r][1] + tw[r][2];
+      o[((r * 4 + 2) * 4) * NT * 2] = tw[r][2] - tw[r][1];
+      o[((r * 4 + 3) * 4) * NT * 2] = tw[r][1] - tw[r][3];
     }
+  };
+  auto transform = [&](int buf) __attribute__((always_inline)) {
+    transform_read(buf);
+    transform_write(buf, 0);
+    transform_write(buf, 2);
   };
 
   f32x4 acc[16][CG];
@@ -214,55 +234,84 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
   // software pipeline, one barrier per chunk.  Chunk c lives in X[c & 1], V[c & 1], U[c & 1].
   // Iteration k: barrier | MFMA(k) || transform(k+1) | commit U(k+1), X(k+2) | loads U(k+2), X(k+3).
   // Every buffer written in iteration k was last read in iteration k-1 (before the barrier),
-  // every buffer read in iteration k was written in iteration k-1.
+  // every buffer read in iteration k was written in iteration k-1.  Past the last chunk the
+  // fetches re-read the last chunk (clamped: branch-free) into buffers nobody reads again.
+  // The chunk's MFMAs run as 4 groups of 4 transform points (16 MFMAs); operands are read one
+  // group ahead and the side work is spread over the groups, so the matrix pipe is fed while
+  // both waves of a SIMD do their share of it.
   const int nchunks = Cin / KC;
   if (in_aff) __syncthreads();  // the (scale, shift) table
+  // static priority for the second half of the waves (the arbitration losers of each SIMD pair)
+  if (wv >= 4) __builtin_amdgcn_s_setprio(1);
   fetch_x(0);
   fetch_u(0);
   commit_x(0, 0);
   commit_u(0);
-  if (nchunks > 1) {
-    fetch_x(1);
-    fetch_u(1);
-    commit_x(1, 1);
-  }
-  if (nchunks > 2) fetch_x(2);
+  fetch_x(min(1, nchunks - 1));
+  fetch_u(min(1, nchunks - 1));
+  commit_x(1, 1);
+  fetch_x(min(2, nchunks - 1));
   __syncthreads();
   transform(0);
+#ifndef SA_WINO_DIAG
+#define SA_WINO_DIAG 0   // timing diagnostics only (wrong results): 1 no side work, 2 also no barrier
+#endif
 #pragma unroll 1
   for (int k = 0; k < nchunks; ++k) {
     const int cur = k & 1, nxt = cur ^ 1;
-    __syncthreads();
+    if (SA_WINO_DIAG < 2) __syncthreads();
     const float2 *va = reinterpret_cast<const float2 *>(smem + Cfg::V_OFF + cur * Cfg::VSZ) + a_slot;
     const float2 *vb = reinterpret_cast<const float2 *>(smem + Cfg::U_OFF + cur * Cfg::USZ);
+    float2 a[2][4], b[2][4][CG];
+    auto load_ops = [&](int q, int slot) __attribute__((always_inline)) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {        // transform points 8h .. 8h+7
-      float2 a[8], b[8][CG];
+      for (int i = 0; i < 4; ++i) {
+        a[slot][i] = va[(4 * q + i) * 4 * NT];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        a[i] = va[(8 * h + i) * 4 * NT];
-#pragma unroll
-        for (int g = 0; g < CG; ++g) b[i][g] = vb[(8 * h + i) * 4 * CO + b_slot[g]];
+        for (int g = 0; g < CG; ++g) b[slot][i][g] = vb[(4 * q + i) * 4 * CO + b_slot[g]];
       }
+    };
+    auto mfma_group = [&](int q, int slot) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int g = 0; g < CG; ++g)
-          acc[8 * h + i][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b[i][g].x, acc[8 * h + i][g], 0, 0, 0);
-      if (h == 0) {
-        // every chunk index past the end reads / writes only idle buffers
-        transform(nxt);
+          acc[4 * q + i][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[slot][i].x, b[slot][i][g].x, acc[4 * q + i][g], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int g = 0; g < CG; ++g)
+          acc[4 * q + i][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[slot][i].y, b[slot][i][g].y, acc[4 * q + i][g], 0, 0, 0);
+    };
+    load_ops(0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q < 3) load_ops(q + 1, (q + 1) & 1);
+      if (SA_WINO_DIAG == 0) {
+      if (q == 0) transform_read(nxt);
+      if (q == 1) transform_write(nxt, 0);
+      if (q == 2) transform_write(nxt, 2);
+      if (q == 3) {
         commit_u(nxt);
         commit_x(cur, k + 2);
-        if (k + 2 < nchunks) fetch_u(k + 2);
-        if (k + 3 < nchunks) fetch_x(k + 3);
+        fetch_u(min(k + 2, nchunks - 1));
+        fetch_x(min(k + 3, nchunks - 1));
       }
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int g = 0; g < CG; ++g)
-          acc[8 * h + i][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b[i][g].y, acc[8 * h + i][g], 0, 0, 0);
+      }
+      mfma_group(q, q & 1);
     }
+#if SA_WINO_SCHED
+    // issue order of the iteration: the first group's operand reads, then every MFMA
+    // followed by one LDS access and one VALU op; the global loads sit in the last quarter
+    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x300, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+      if (i >= 48 && i < 58) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+#endif
   }
   __syncthreads();
 
