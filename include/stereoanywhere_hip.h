@@ -238,6 +238,25 @@ int sa_conv2d_k3_wino_ex(const float *in, long in_bs, int N, int Cin, int H, int
                          int Cout, const float *bias, int relu, const float *in_m, const float *in_s,
                          const float *in_t, int in_pstride, int in_act, float *out, long out_bs,
                          double *stats_partial, void *stream);
+/* Up to 4 independent sa_conv2d_k3_wino_ex convolutions in one launch (their blocks share
+ * one grid, so a small conv's last, partly filled round of blocks is filled by the others).
+ * All problems must have the same Cout % 64 == 0 outcome and either all or none carry an
+ * input transform. */
+typedef struct SaWinoProblem {
+  const float *in;
+  long in_bs;
+  int N, Cin, H, W;
+  const float *U;
+  int Cout;
+  const float *bias;
+  int relu;
+  const float *in_m, *in_s, *in_t;
+  int in_pstride, in_act;
+  float *out;
+  long out_bs;
+  double *stats_partial;
+} SaWinoProblem;
+int sa_conv2d_k3_wino_multi(int nprob, const SaWinoProblem *probs, void *stream);
 
 /* Epilogues of the MIOpen 2-D convs (encoders extractor.py:6-300, update block update.py:64-110).
  * sa_plane_stats: InstanceNorm2d statistics (biased variance, eps) of each (b, c) plane of

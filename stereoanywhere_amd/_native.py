@@ -22,6 +22,13 @@ L = ctypes.c_long
 F = ctypes.c_float
 
 # name -> (restype, argtypes); must match include/stereoanywhere_hip.h exactly
+class SaWinoProblem(ctypes.Structure):
+    """include/stereoanywhere_hip.h: one convolution of sa_conv2d_k3_wino_multi."""
+    _fields_ = [("in_", P), ("in_bs", L), ("N", I), ("Cin", I), ("H", I), ("W", I), ("U", P), ("Cout", I),
+                ("bias", P), ("relu", I), ("in_m", P), ("in_s", P), ("in_t", P), ("in_pstride", I),
+                ("in_act", I), ("out", P), ("out_bs", L), ("stats_partial", P)]
+
+
 SIGNATURES = {
     "sa_abi_version": (I, []),
     "sa_last_error": (ctypes.c_char_p, []),
@@ -52,6 +59,7 @@ SIGNATURES = {
     "sa_conv2d_k3_wino": (I, [P, L, I, I, I, I, P, I, P, I, P, L, P]),
     "sa_conv2d_k3_wino_stat_parts": (L, [I, I]),
     "sa_conv2d_k3_wino_ex": (I, [P, L, I, I, I, I, P, I, P, I, P, P, P, I, I, P, L, P, P]),
+    "sa_conv2d_k3_wino_multi": (I, [I, P, P]),
     "sa_plane_stats": (I, [P, L, I, I, L, F, P, P, P]),
     "sa_norm_act": (I, [P, L, I, I, L, P, P, P, I, I, P, L, P, P, P, I, I, P, L, P]),
     "sa_conv3d_upcat_stat_parts": (L, [I, I, I]),

@@ -81,19 +81,49 @@ struct WinoIO {
   double *partial;
 };
 
+// one convolution of a launch; a launch carries up to MAX_PROB independent convolutions
+// with the same template configuration (their blocks share the grid, so one conv's tail
+// round fills with another's blocks)
+struct WinoProb {
+  const float *in;
+  long in_bs;
+  int Cin, H, W;
+  const float *U;
+  int Cout;
+  const float *bias;
+  int relu;
+  float *out;
+  long out_bs;
+  int tiles_w, tiles_hw, co_blocks;
+  WinoIO io;
+};
+constexpr int MAX_PROB = 4;
+struct WinoLaunch {
+  WinoProb p[MAX_PROB];
+  unsigned end[MAX_PROB];   // end of each problem's block range, ranges padded to multiples of 8
+  unsigned nblk[MAX_PROB];  // the problem's own block count
+  int nprob;
+};
+
 template <int CG, bool AFF>
-__global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
-    const float *__restrict__ in, long in_bs, int Cin, int H, int W, const float *__restrict__ U, int Cout,
-    const float *__restrict__ bias, int relu, float *__restrict__ out, long out_bs, int tiles_w, int tiles_hw,
-    int co_blocks, WinoIO io) {
+__device__ __forceinline__ void wino_body(const WinoProb &P, const unsigned wid) {
+  const float *__restrict__ in = P.in;
+  const long in_bs = P.in_bs;
+  const int Cin = P.Cin, H = P.H, W = P.W, Cout = P.Cout, relu = P.relu;
+  const float *__restrict__ U = P.U;
+  const float *__restrict__ bias = P.bias;
+  float *__restrict__ out = P.out;
+  const long out_bs = P.out_bs;
+  const int tiles_w = P.tiles_w, tiles_hw = P.tiles_hw, co_blocks = P.co_blocks;
+  const WinoIO io = P.io;
   using Cfg = Wino<CG>;
   constexpr int CO = Cfg::CO, UPT = Cfg::UPT;
   __shared__ float smem[Cfg::SMEM];
   __shared__ float2 tab[MAX_CIN_AFFINE];   // input (scale, shift) of this image's channels
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // XCD-aware work order: consecutive work ids = the co blocks of one spatial tile
-  const unsigned wid = sa::xcd_remap(blockIdx.x, gridDim.x);
+  // XCD-aware work order (the launch remaps block ids): consecutive work ids = the co
+  // blocks of one spatial tile
   const int cb = wid % co_blocks;
   const int st = (wid / co_blocks) % tiles_hw;
   const int n = wid / (co_blocks * tiles_hw);
@@ -390,6 +420,28 @@ __global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(
   }
 }
 
+template <int CG, bool AFF>
+__global__ __launch_bounds__(512, SA_WINO_WAVES_PER_EU) void wino_f2k3_kernel(const WinoLaunch L) {
+  // The block's problem from its raw id: blocks are dealt to the 8 XCDs round-robin and every
+  // problem's range starts at a multiple of 8, so each XCD gets an equal share of each
+  // problem (problems differ in work per block); the L2-locality remap applies within it.
+  // Uniform selects with constant indices (a dynamic index into the kernel-argument struct
+  // would copy it to scratch).
+  const unsigned g = blockIdx.x;
+  WinoProb P = L.p[0];
+  unsigned base = 0, n = L.nblk[0];
+#pragma unroll
+  for (int i = 1; i < MAX_PROB; ++i) {
+    if (i < L.nprob && g >= L.end[i - 1]) {
+      P = L.p[i];
+      base = L.end[i - 1];
+      n = L.nblk[i];
+    }
+  }
+  if (g - base >= n) return;   // padding block (before any barrier)
+  wino_body<CG, AFF>(P, sa::xcd_remap(g - base, n));
+}
+
 // U = (G g G^T) for g = w[co][ci] (3x3), in fp64, rounded once
 __global__ __launch_bounds__(256) void wino_weights_kernel(const float *__restrict__ w, int Cout, int Cin,
                                                            float *__restrict__ U) {
@@ -430,30 +482,58 @@ extern "C" long sa_conv2d_k3_wino_stat_parts(int H, int W) {
   return (long)((W + OTW - 1) / OTW) * ((H + OTH - 1) / OTH);
 }
 
-extern "C" int sa_conv2d_k3_wino_ex(const float *in, long in_bs, int N, int Cin, int H, int W, const float *U,
-                                    int Cout, const float *bias, int relu, const float *in_m, const float *in_s,
-                                    const float *in_t, int in_pstride, int in_act, float *out, long out_bs,
-                                    double *stats_partial, void *stream) {
-  SA_REQUIRE(in && U && out && N > 0 && H > 0 && W > 0, "sa_conv2d_k3_wino: bad arguments");
-  SA_REQUIRE(Cin % KC == 0 && Cout % 32 == 0, "sa_conv2d_k3_wino: needs Cin %% 8 == 0 and Cout %% 32 == 0 (got %d, %d)",
-             Cin, Cout);
-  SA_REQUIRE((reinterpret_cast<uintptr_t>(U) & 15) == 0, "sa_conv2d_k3_wino: U must be 16-byte aligned");
-  SA_REQUIRE((long)Cin * H * W * 4 < (1L << 31) && 16L * Cin * Cout * 4 < (1L << 31),
+namespace {
+
+// validate one problem and fill its kernel descriptor; returns its CG (0 on error)
+int wino_prob(const SaWinoProblem &q, WinoProb &P, bool &aff) {
+  SA_REQUIRE(q.in && q.U && q.out && q.N > 0 && q.H > 0 && q.W > 0, "sa_conv2d_k3_wino: bad arguments");
+  SA_REQUIRE(q.Cin % KC == 0 && q.Cout % 32 == 0,
+             "sa_conv2d_k3_wino: needs Cin %% 8 == 0 and Cout %% 32 == 0 (got %d, %d)", q.Cin, q.Cout);
+  SA_REQUIRE((reinterpret_cast<uintptr_t>(q.U) & 15) == 0, "sa_conv2d_k3_wino: U must be 16-byte aligned");
+  SA_REQUIRE((long)q.Cin * q.H * q.W * 4 < (1L << 31) && 16L * q.Cin * q.Cout * 4 < (1L << 31),
              "sa_conv2d_k3_wino: an image or the filter bank exceeds the 2 GB buffer-descriptor range");
-  const bool aff = in_m || in_s || in_t || in_act;
-  SA_REQUIRE(!aff || Cin <= MAX_CIN_AFFINE, "sa_conv2d_k3_wino: input transform needs Cin <= %d", MAX_CIN_AFFINE);
-  SA_REQUIRE(in_pstride == 0 || in_pstride == Cin, "sa_conv2d_k3_wino: in_pstride must be 0 or Cin");
-  const int cg = Cout % 64 == 0 ? 2 : 1;
-  const int tiles_w = (W + OTW - 1) / OTW, tiles_h = (H + OTH - 1) / OTH;
-  const int co_blocks = Cout / (32 * cg);
-  const long nblk = (long)N * tiles_w * tiles_h * co_blocks;
-  SA_REQUIRE(nblk < (1L << 31), "sa_conv2d_k3_wino: grid too large");
-  const WinoIO io{in_m, in_s, in_t, in_pstride, in_act, stats_partial};
+  aff = q.in_m || q.in_s || q.in_t || q.in_act;
+  SA_REQUIRE(!aff || q.Cin <= MAX_CIN_AFFINE, "sa_conv2d_k3_wino: input transform needs Cin <= %d", MAX_CIN_AFFINE);
+  SA_REQUIRE(q.in_pstride == 0 || q.in_pstride == q.Cin, "sa_conv2d_k3_wino: in_pstride must be 0 or Cin");
+  const int cg = q.Cout % 64 == 0 ? 2 : 1;
+  const int tiles_w = (q.W + OTW - 1) / OTW, tiles_h = (q.H + OTH - 1) / OTH;
+  P = WinoProb{q.in, q.in_bs, q.Cin, q.H, q.W, q.U, q.Cout, q.bias, q.relu, q.out, q.out_bs, tiles_w,
+               tiles_w * tiles_h, q.Cout / (32 * cg),
+               WinoIO{q.in_m, q.in_s, q.in_t, q.in_pstride, q.in_act, q.stats_partial}};
+  return cg;
+}
+
+}  // namespace
+
+extern "C" int sa_conv2d_k3_wino_multi(int nprob, const SaWinoProblem *probs, void *stream) {
+  SA_REQUIRE(nprob >= 1 && nprob <= MAX_PROB && probs, "sa_conv2d_k3_wino_multi: 1..%d problems", MAX_PROB);
+  WinoLaunch L{};
+  int cg = 0;
+  bool aff = false;
+  long total = 0;
+  for (int i = 0; i < nprob; ++i) {
+    bool a = false;
+    const int c = wino_prob(probs[i], L.p[i], a);
+    if (c == 0) return SA_E_ARG;
+    SA_REQUIRE(i == 0 || (c == cg && a == aff),
+               "sa_conv2d_k3_wino_multi: problems must share the output-channel grouping (Cout %% 64) and "
+               "the presence of an input transform");
+    cg = c;
+    aff = a;
+    const long nb = (long)probs[i].N * L.p[i].tiles_hw * L.p[i].co_blocks;
+    total = (i + 1 < nprob ? (total + nb + 7) / 8 * 8 : total + nb);
+    SA_REQUIRE(total < (1L << 31), "sa_conv2d_k3_wino: grid too large");
+    L.end[i] = (unsigned)total;
+    L.nblk[i] = (unsigned)nb;
+  }
+  for (int i = nprob; i < MAX_PROB; ++i) {
+    L.end[i] = (unsigned)total;
+    L.nblk[i] = 0;
+  }
+  L.nprob = nprob;
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV2D, s);
-#define SA_WINO(CGV, AFFV)                                                                                   \
-  wino_f2k3_kernel<CGV, AFFV><<<(unsigned)nblk, 512, 0, s>>>(in, in_bs, Cin, H, W, U, Cout, bias, relu, out, out_bs, \
-                                                             tiles_w, tiles_w * tiles_h, co_blocks, io)
+#define SA_WINO(CGV, AFFV) wino_f2k3_kernel<CGV, AFFV><<<(unsigned)total, 512, 0, s>>>(L)
   if (cg == 2) {
     if (aff) SA_WINO(2, true); else SA_WINO(2, false);
   } else {
@@ -461,6 +541,15 @@ extern "C" int sa_conv2d_k3_wino_ex(const float *in, long in_bs, int N, int Cin,
   }
 #undef SA_WINO
   return sa::check_launch("sa_conv2d_k3_wino");
+}
+
+extern "C" int sa_conv2d_k3_wino_ex(const float *in, long in_bs, int N, int Cin, int H, int W, const float *U,
+                                    int Cout, const float *bias, int relu, const float *in_m, const float *in_s,
+                                    const float *in_t, int in_pstride, int in_act, float *out, long out_bs,
+                                    double *stats_partial, void *stream) {
+  const SaWinoProblem q{in, in_bs, N, Cin, H, W, U, Cout, bias, relu, in_m, in_s, in_t, in_pstride, in_act,
+                        out, out_bs, stats_partial};
+  return sa_conv2d_k3_wino_multi(1, &q, stream);
 }
 
 extern "C" int sa_conv2d_k3_wino(const float *in, long in_bs, int N, int Cin, int H, int W, const float *U, int Cout,

@@ -23,6 +23,8 @@ off (the reference CLI's store_true defaults, test.py:94-98).
 """
 from __future__ import annotations
 
+import os
+
 import math
 from types import SimpleNamespace
 
@@ -49,6 +51,11 @@ def _normalize_pair(a: torch.Tensor, b: torch.Tensor, eps: float = 1e-4):
     mx = torch.maximum(a.amax(dim=(2, 3), keepdim=True), b.amax(dim=(2, 3), keepdim=True))
     return (a - mn) / (mx - mn + eps), (b - mn) / (mx - mn + eps)
 
+
+
+# independent 3x3 convs of the update block share one launch (ops.conv2d_k3_multi);
+# SA_GROUP_CONVS=0 launches them one by one (A/B timing)
+_GROUP_CONVS = os.environ.get("SA_GROUP_CONVS", "1") != "0"
 
 class StereoAnywhere(nn.Module):
     def __init__(self, args):
@@ -270,8 +277,11 @@ class StereoAnywhere(nn.Module):
 
         def gru(level, h, x, key):
             g = dw["g" + key]
-            xc = ops.conv2d_k3(x, g["Ux"])  # bias added inside the gate kernels
-            hzr = ops.conv2d_k3(h, g["Uhzr"])
+            # x and h halves of convz/convr/convq in one launch; bias added inside the gate kernels
+            if _GROUP_CONVS:
+                xc, hzr = ops.conv2d_k3_multi(dict(x=x, U=g["Ux"]), dict(x=h, U=g["Uhzr"]))
+            else:
+                xc, hzr = ops.conv2d_k3(x, g["Ux"]), ops.conv2d_k3(h, g["Uhzr"])
             ops.gru_zr(xc, hzr, cz[level], cr[level], h, z[key], rh[key], bx=g["bx"])
             qh = ops.conv2d_k3(rh[key], g["Uqh"])
             ops.gru_out(xc, qh, cq[level], z[key], h, bx=g["bx"])
@@ -291,10 +301,15 @@ class StereoAnywhere(nn.Module):
             # 3x3 convs with bias + ReLU in the Winograd epilogue, written straight into the
             # motion conv's input: cat(convc2(stereo), convc2(mono), convf2(convf1(flow)))
             c1v = c1.view(B, 2, c1.shape[1], H4, W4)
-            for v in range(2):
-                ops.conv2d_k3(c1v[:, v], dw["U_c2"], enc.convc2.bias, relu=True, out=motin[:, 64 * v:64 * v + 64])
             fl = ops.conv2d_small(flow, dw["f1"], enc.convf1.bias, 64, 7, relu=True)
-            ops.conv2d_k3(fl, dw["U_f2"], enc.convf2.bias, relu=True, out=motin[:, 128:192])
+            mconv = [dict(x=c1v[:, v], U=dw["U_c2"], bias=enc.convc2.bias, relu=True,
+                          out=motin[:, 64 * v:64 * v + 64]) for v in range(2)]
+            mconv.append(dict(x=fl, U=dw["U_f2"], bias=enc.convf2.bias, relu=True, out=motin[:, 128:192]))
+            if _GROUP_CONVS:
+                ops.conv2d_k3_multi(*mconv)
+            else:
+                for p in mconv:
+                    ops.conv2d_k3(**p)
             # _conv (126 outputs, padded to 128) writes x08[:, :128]; channels 126-127 (the flow)
             # are rewritten right after from the coordinates
             ops.conv2d_k3(motin, dw["U_mot"], dw["mot_b"], relu=True, out=x08[:, :128])

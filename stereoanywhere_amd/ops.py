@@ -7,6 +7,7 @@ PyTorch is plumbing here (device memory, streams); the arithmetic is in the .so.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import List, Optional, Tuple
 
@@ -493,12 +494,9 @@ def wino_weights(weight: torch.Tensor) -> torch.Tensor:
     return U
 
 
-def conv2d_k3(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = None, relu: bool = False,
-              out: Optional[torch.Tensor] = None, in_aff: Optional[Affine] = None, in_act=None,
-              stats: bool = False):
-    """3x3 / pad 1 conv via fused Winograd (U from wino_weights); + bias, optional ReLU.
-    in_aff / in_act: the producer's norm + activation applied to x while it is loaded.
-    stats: also return the output's InstanceNorm (mean, rstd) per (image, channel)."""
+def _wino_problem(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = None, relu: bool = False,
+                  out: Optional[torch.Tensor] = None, in_aff: Optional[Affine] = None, in_act=None,
+                  stats: bool = False):
     bs = _plane_bs(x, "x")
     _check(U, "U")
     B, Cin, H, W = x.shape
@@ -509,16 +507,37 @@ def conv2d_k3(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = N
         out = torch.empty((B, Cout, H, W), device=x.device, dtype=torch.float32)
     if tuple(out.shape) != (B, Cout, H, W):
         raise RuntimeError("conv2d_k3: out shape mismatch")
-    a = (in_aff or Affine()).args(Cin)
+    m, s, t, ps = (in_aff or Affine()).args(Cin)
     parts = int(N.lib().sa_conv2d_k3_wino_stat_parts(H, W)) if stats else 0
     partial = torch.empty((B * Cout * parts * 2,), device=x.device, dtype=torch.float64) if stats else None
-    N.call("sa_conv2d_k3_wino_ex", x.data_ptr(), bs, B, Cin, H, W, U.data_ptr(), Cout, _ptr(bias),
-           1 if relu else 0, *a, ACT[in_act], out.data_ptr(), _plane_bs(out, "out"), _ptr(partial), _stream(x))
+    prob = N.SaWinoProblem(x.data_ptr(), bs, B, Cin, H, W, U.data_ptr(), Cout, _ptr(bias), 1 if relu else 0,
+                           m, s, t, ps, ACT[in_act], out.data_ptr(), _plane_bs(out, "out"), _ptr(partial))
     # Winograd-domain products actually executed: 16 per 2x2 tile per (Cin, Cout) pair
     _account("conv2d_wino", 2.0 * 16 * Cin * Cout * B * ((H + 1) // 2) * ((W + 1) // 2))
-    if stats:
-        return out, instnorm_finalize(partial, B * Cout, parts, H * W)
-    return out
+    fin = (lambda: (out, instnorm_finalize(partial, B * Cout, parts, H * W))) if stats else (lambda: out)
+    return prob, fin
 
 
-__all__ = [n for n in dir() if not n.startswith("_") and n not in ("annotations", "math", "torch")]
+def conv2d_k3_multi(*problems) -> list:
+    """Independent conv2d_k3 calls (each a dict of conv2d_k3's keyword arguments) in ONE launch:
+    their blocks share the grid, so each conv's partly filled last round of blocks is filled by
+    the others.  All must agree on Cout % 64 == 0 and on having an input transform or not."""
+    if not 1 <= len(problems) <= 4:
+        raise RuntimeError("conv2d_k3_multi: 1..4 convolutions per launch")
+    built = [_wino_problem(**p) for p in problems]
+    arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
+    N.call("sa_conv2d_k3_wino_multi", len(built), ctypes.addressof(arr), _stream(problems[0]["x"]))
+    return [b[1]() for b in built]
+
+
+def conv2d_k3(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = None, relu: bool = False,
+              out: Optional[torch.Tensor] = None, in_aff: Optional[Affine] = None, in_act=None,
+              stats: bool = False):
+    """3x3 / pad 1 conv via fused Winograd (U from wino_weights); + bias, optional ReLU.
+    in_aff / in_act: the producer's norm + activation applied to x while it is loaded.
+    stats: also return the output's InstanceNorm (mean, rstd) per (image, channel)."""
+    return conv2d_k3_multi(dict(x=x, U=U, bias=bias, relu=relu, out=out, in_aff=in_aff, in_act=in_act,
+                                stats=stats))[0]
+
+
+__all__ = [n for n in dir() if not n.startswith("_") and n not in ("annotations", "ctypes", "math", "torch")]

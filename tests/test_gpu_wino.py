@@ -44,3 +44,29 @@ def test_wino_views_and_errors():
     assert float(out[:, :32].abs().sum()) == 0.0 and float(out[:, 64:].abs().sum()) == 0.0
     with pytest.raises(RuntimeError):
         ops.conv2d_k3(rnd(1, 12, 8, 8), ops.wino_weights(rnd(32, 12, 3, 3)))   # Cin % 8 != 0
+
+
+def test_multi_launch_matches_separate_convs():
+    """sa_conv2d_k3_wino_multi: three convolutions of different shapes (and a channel-slice
+    output) in one grid equal torch's convs; mixed Cout % 64 groupings are rejected."""
+    g = torch.Generator(device="cpu").manual_seed(40)
+
+    def rnd(*s):
+        return torch.randn(*s, generator=g).cuda()
+    xa, xb, xc = rnd(2, 64, 20, 50), rnd(3, 128, 11, 37), rnd(2, 32, 34, 60)
+    wa, wb, wc = (rnd(64, 64, 3, 3) / 24, rnd(128, 128, 3, 3) / 34, rnd(64, 32, 3, 3) / 17)
+    ba = rnd(64)
+    big = torch.zeros(2, 192, 20, 50, device="cuda")
+    ya, yb, yc = ops.conv2d_k3_multi(
+        dict(x=xa, U=ops.wino_weights(wa), bias=ba, relu=True, out=big[:, 64:128]),
+        dict(x=xb, U=ops.wino_weights(wb)),
+        dict(x=xc, U=ops.wino_weights(wc), stats=True))
+    torch.testing.assert_close(ya, torch.relu(F.conv2d(xa, wa, ba, padding=1)), atol=2e-5, rtol=1e-4)
+    assert float(big[:, :64].abs().sum()) == 0 and float(big[:, 128:].abs().sum()) == 0
+    torch.testing.assert_close(yb, F.conv2d(xb, wb, padding=1), atol=2e-5, rtol=1e-4)
+    out_c, (mean, rstd) = yc
+    ref_c = F.conv2d(xc, wc, padding=1)
+    torch.testing.assert_close(out_c, ref_c, atol=2e-5, rtol=1e-4)
+    torch.testing.assert_close(mean, ref_c.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
+    with pytest.raises(RuntimeError):
+        ops.conv2d_k3_multi(dict(x=xa, U=ops.wino_weights(wa)), dict(x=xa, U=ops.wino_weights(rnd(96, 64, 3, 3))))
