@@ -238,7 +238,7 @@ int sa_conv2d_k3_wino_ex(const float *in, long in_bs, int N, int Cin, int H, int
                          int Cout, const float *bias, int relu, const float *in_m, const float *in_s,
                          const float *in_t, int in_pstride, int in_act, float *out, long out_bs,
                          double *stats_partial, void *stream);
-/* Up to 4 independent sa_conv2d_k3_wino_ex convolutions in one launch (their blocks share
+/* Up to 8 independent sa_conv2d_k3_wino_ex convolutions in one launch (their blocks share
  * one grid, so a small conv's last, partly filled round of blocks is filled by the others).
  * All problems must have the same Cout % 64 == 0 outcome and either all or none carry an
  * input transform. */

@@ -97,7 +97,7 @@ struct WinoProb {
   int tiles_w, tiles_hw, co_blocks;
   WinoIO io;
 };
-constexpr int MAX_PROB = 4;
+constexpr int MAX_PROB = 8;
 struct WinoLaunch {
   WinoProb p[MAX_PROB];
   unsigned end[MAX_PROB];   // end of each problem's block range, ranges padded to multiples of 8

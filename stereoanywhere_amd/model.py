@@ -275,47 +275,56 @@ class StereoAnywhere(nn.Module):
         cr = [c[:, 128:256] for c in ctx]
         cq = [c[:, 256:384] for c in ctx]
 
-        def gru(level, h, x, key):
-            g = dw["g" + key]
-            # x and h halves of convz/convr/convq in one launch; bias added inside the gate kernels
+        def conv_group(*probs):
+            """Independent 3x3 convs in one launch (SA_GROUP_CONVS=0: one launch each)."""
             if _GROUP_CONVS:
-                xc, hzr = ops.conv2d_k3_multi(dict(x=x, U=g["Ux"]), dict(x=h, U=g["Uhzr"]))
-            else:
-                xc, hzr = ops.conv2d_k3(x, g["Ux"]), ops.conv2d_k3(h, g["Uhzr"])
-            ops.gru_zr(xc, hzr, cz[level], cr[level], h, z[key], rh[key], bx=g["bx"])
-            qh = ops.conv2d_k3(rh[key], g["Uqh"])
-            ops.gru_out(xc, qh, cq[level], z[key], h, bx=g["bx"])
+                return ops.conv2d_k3_multi(*probs)
+            return [ops.conv2d_k3(**p) for p in probs]
+
+        def gate_x_h(key, x, h):
+            g = dw["g" + key]   # x and h halves of convz/convr/convq; bias added in the gate kernels
+            return [dict(x=x, U=g["Ux"]), dict(x=h, U=g["Uhzr"])]
+
+        def gru_zr(level, key, h, xc, hzr):
+            ops.gru_zr(xc, hzr, cz[level], cr[level], h, z[key], rh[key], bx=dw["g" + key]["bx"])
+
+        def gru_out(level, key, h, xc, qh):
+            ops.gru_out(xc, qh, cq[level], z[key], h, bx=dw["g" + key]["bx"])
 
         ops.flow_update(coords_x, None, flow, x08[:, 126:128])
         flow_up = None
+        c1v = c1.view(B, 2, c1.shape[1], H4, W4)
         for it in range(iters):
+            # update.py:166-183 runs gru32, gru16, the motion encoder, gru08.  The motion
+            # encoder depends on neither GRU state, so its convs share launches with gru32's
+            # (every op is deterministic: the result is identical to the reference order).
             # lookup of both pyramids + convc1 + ReLU in one kernel (sample 2b: stereo, 2b+1: mono)
             stereo_blk.lookup_conv1x1_into(coords_x, dw["c1_kc"], enc.convc1.bias, c1, other=mono_blk)
-            # update.py:166-183, in order: gru32, gru16, motion encoder, gru08
-            ops.pool2x(h16, x32)
-            gru(2, h32, x32, "32")
-            ops.pool2x(h08, x16[:, :128])
-            ops.interp(h32, x16[:, 128:])
-            gru(1, h16, x16, "16")
-            # shared convc1/convc2 on the stereo and mono lookups as one 2B batch
-            # 3x3 convs with bias + ReLU in the Winograd epilogue, written straight into the
-            # motion conv's input: cat(convc2(stereo), convc2(mono), convf2(convf1(flow)))
-            c1v = c1.view(B, 2, c1.shape[1], H4, W4)
             fl = ops.conv2d_small(flow, dw["f1"], enc.convf1.bias, 64, 7, relu=True)
+            ops.pool2x(h16, x32)
+            # gru32's x/h convs + the motion encoder's 3x3 convs (bias + ReLU in the epilogue,
+            # written straight into the motion conv's input cat(convc2(stereo), convc2(mono),
+            # convf2(convf1(flow))))
             mconv = [dict(x=c1v[:, v], U=dw["U_c2"], bias=enc.convc2.bias, relu=True,
                           out=motin[:, 64 * v:64 * v + 64]) for v in range(2)]
             mconv.append(dict(x=fl, U=dw["U_f2"], bias=enc.convf2.bias, relu=True, out=motin[:, 128:192]))
-            if _GROUP_CONVS:
-                ops.conv2d_k3_multi(*mconv)
-            else:
-                for p in mconv:
-                    ops.conv2d_k3(**p)
-            # _conv (126 outputs, padded to 128) writes x08[:, :128]; channels 126-127 (the flow)
-            # are rewritten right after from the coordinates
-            ops.conv2d_k3(motin, dw["U_mot"], dw["mot_b"], relu=True, out=x08[:, :128])
+            xc32, hzr32 = conv_group(*gate_x_h("32", x32, h32), *mconv)[:2]
+            gru_zr(2, "32", h32, xc32, hzr32)
+            # gru32's r*h conv + the motion conv (_conv: 126 outputs, padded to 128, into
+            # x08[:, :128]; channels 126-127 (the flow) are rewritten right after)
+            qh32 = conv_group(dict(x=rh["32"], U=dw["g32"]["Uqh"]),
+                              dict(x=motin, U=dw["U_mot"], bias=dw["mot_b"], relu=True, out=x08[:, :128]))[0]
+            gru_out(2, "32", h32, xc32, qh32)
             ops.flow_update(coords_x, None, None, x08[:, 126:128])
+            ops.pool2x(h08, x16[:, :128])
+            ops.interp(h32, x16[:, 128:])
+            xc16, hzr16 = conv_group(*gate_x_h("16", x16, h16))
+            gru_zr(1, "16", h16, xc16, hzr16)
+            gru_out(1, "16", h16, xc16, ops.conv2d_k3(rh["16"], dw["g16"]["Uqh"]))
             ops.interp(h16, x08[:, 128:])
-            gru(0, h08, x08, "08")
+            xc08, hzr08 = conv_group(*gate_x_h("08", x08, h08))
+            gru_zr(0, "08", h08, xc08, hzr08)
+            gru_out(0, "08", h08, xc08, ops.conv2d_k3(rh["08"], dw["g08"]["Uqh"]))
             f1 = ops.conv2d_k3(h08, dw["U_fh1"], ub.flow_head.conv1.bias, relu=True)
             delta = ops.conv2d_k3_narrow(f1, ub.flow_head.conv2.weight, ub.flow_head.conv2.bias)
             ops.flow_update(coords_x, delta[:, 0:1], flow, None)

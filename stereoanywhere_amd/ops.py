@@ -522,8 +522,8 @@ def conv2d_k3_multi(*problems) -> list:
     """Independent conv2d_k3 calls (each a dict of conv2d_k3's keyword arguments) in ONE launch:
     their blocks share the grid, so each conv's partly filled last round of blocks is filled by
     the others.  All must agree on Cout % 64 == 0 and on having an input transform or not."""
-    if not 1 <= len(problems) <= 4:
-        raise RuntimeError("conv2d_k3_multi: 1..4 convolutions per launch")
+    if not 1 <= len(problems) <= 8:
+        raise RuntimeError("conv2d_k3_multi: 1..8 convolutions per launch")
     built = [_wino_problem(**p) for p in problems]
     arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
     N.call("sa_conv2d_k3_wino_multi", len(built), ctypes.addressof(arr), _stream(problems[0]["x"]))
