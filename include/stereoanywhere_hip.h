@@ -213,7 +213,7 @@ int sa_conv2d_small(const float *in, long in_bs, int B, int Cin, int H, int W, c
                     const float *bias, int Cout, int ksize, int relu, float *out, long out_bs,
                     void *stream);
 
-/* flow_head.conv2 (update.py:98-110): 3x3 / pad 1 conv, Cin (multiple of 4) -> Cout = 2,
+/* flow_head.conv2 (update.py:98-110): 3x3 / pad 1 conv, Cin (multiple of 8) -> Cout = 2,
  * weight in the module's [Cout][Cin][3][3] layout, bias may be NULL. */
 int sa_conv2d_k3_narrow(const float *in, long in_bs, int B, int Cin, int H, int W, const float *weight,
                         const float *bias, int Cout, float *out, long out_bs, void *stream);

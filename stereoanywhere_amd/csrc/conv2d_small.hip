@@ -61,64 +61,103 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const float *__restri
 
 // 3x3 / pad 1 conv with many inputs and very few outputs (flow_head.conv2: 256 -> 2,
 // update.py:98-110), which the library runs at a few % of its arithmetic rate.  Memory
-// bound: one thread per (pixel, quarter of the input channels), taps read straight from
-// L1/L2 (neighbouring pixels share lines), the four partial sums reduced through LDS in a
-// fixed order; bias in the epilogue.  Weights in the module's own [Cout][Cin][3][3] layout.
+// bound.  A block is 62 output columns x NR rows x all outputs; its 8 waves split the input
+// channels.  Per channel a lane loads one column (NR + 2 rows, coalesced across lanes) and
+// takes its x-1 / x+1 neighbours from the adjacent lanes with DPP wave shifts (lanes 0 and
+// 63 load the halo columns), so every input value is read from memory once per block;
+// loads run UNR channels ahead.  The 8 partial sums are reduced through LDS in a fixed
+// order; bias in the epilogue.  Weights in the module's own [Cout][Cin][3][3] layout
+// (wave-uniform scalar loads).
+constexpr int NW = 8, NR = 4, NCOL = 62;
+
+__device__ __forceinline__ float lane_prev(float v) {   // lane i <- lane i - 1 (DPP wave_shr:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float lane_next(float v) {   // lane i <- lane i + 1 (DPP wave_shl:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+
 template <int COUT>
-__global__ __launch_bounds__(256) void conv2d_k3_narrow_kernel(const float *__restrict__ in, long in_bs, int Cin,
+__global__ __launch_bounds__(512) void conv2d_k3_narrow_kernel(const float *__restrict__ in, long in_bs, int Cin,
                                                                int H, int W, const float *__restrict__ wt,
                                                                const float *__restrict__ bias,
                                                                float *__restrict__ out, long out_bs) {
-  __shared__ float red[3][COUT][64];
+  __shared__ float red[NW - 1][COUT][NR][64];
   const int lane = threadIdx.x & 63;
   const int grp = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const long hw = (long)H * W;
-  const long pix = (long)blockIdx.x * 64 + lane;
-  const int b = blockIdx.y;
-  const bool ok = pix < hw;
-  const int y = ok ? (int)(pix / W) : 0, x = ok ? (int)(pix % W) : 0;
-  int off[9];
-  bool val[9];
+  const int x = blockIdx.x * NCOL + lane - 1;   // the column this lane loads
+  const int y0 = blockIdx.y * NR;
+  const int b = blockIdx.z;
+  const bool xin = x >= 0 && x < W;
+  int roff[NR + 2];
+  bool rok[NR + 2];
 #pragma unroll
-  for (int ky = 0; ky < 3; ++ky)
+  for (int r = 0; r < NR + 2; ++r) {
+    const int yy = y0 - 1 + r;
+    rok[r] = xin && yy >= 0 && yy < H;
+    roff[r] = rok[r] ? yy * W + x : 0;
+  }
+  const int per = Cin / NW, c0 = grp * per;
+  float acc[NR][COUT];
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int yy = y + ky - 1, xx = x + kx - 1;
-      val[ky * 3 + kx] = yy >= 0 && yy < H && xx >= 0 && xx < W;
-      off[ky * 3 + kx] = min(max(yy, 0), H - 1) * W + min(max(xx, 0), W - 1);
-    }
-  const int per = Cin / 4, c0 = grp * per;
-  float acc[COUT];
+  for (int i = 0; i < NR; ++i)
 #pragma unroll
-  for (int co = 0; co < COUT; ++co) acc[co] = 0.0f;
+    for (int co = 0; co < COUT; ++co) acc[i][co] = 0.0f;
   const float *src = in + (long)b * in_bs + (long)c0 * hw;
-#pragma unroll 2
-  for (int ci = 0; ci < per; ++ci) {
-    float v[9];
+  constexpr int UNR = 4;
+  for (int cb = 0; cb < per; cb += UNR) {
+    float col[UNR][NR + 2];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) v[t] = src[off[t]];
+    for (int u = 0; u < UNR; ++u)
 #pragma unroll
-    for (int t = 0; t < 9; ++t) v[t] = val[t] ? v[t] : 0.0f;
+      for (int r = 0; r < NR + 2; ++r) col[u][r] = (cb + u < per && rok[r]) ? src[(long)(cb + u) * hw + roff[r]] : 0.0f;
 #pragma unroll
-    for (int co = 0; co < COUT; ++co) {
-      const float *w = wt + ((long)co * Cin + c0 + ci) * 9;
+    for (int u = 0; u < UNR; ++u) {
+      if (cb + u >= per) break;
+      float lft[NR + 2], rgt[NR + 2];
 #pragma unroll
-      for (int t = 0; t < 9; ++t) acc[co] += w[t] * v[t];
+      for (int r = 0; r < NR + 2; ++r) {
+        lft[r] = lane_prev(col[u][r]);
+        rgt[r] = lane_next(col[u][r]);
+      }
+      const int ci = c0 + cb + u;
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) {
+        const float *w = wt + ((long)co * Cin + ci) * 9;
+        float wk[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wk[t] = w[t];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) {
+            acc[i][co] += wk[ky * 3 + 0] * lft[i + ky];
+            acc[i][co] += wk[ky * 3 + 1] * col[u][i + ky];
+            acc[i][co] += wk[ky * 3 + 2] * rgt[i + ky];
+          }
+        }
+      }
     }
-    src += hw;
   }
   if (grp > 0) {
 #pragma unroll
-    for (int co = 0; co < COUT; ++co) red[grp - 1][co][lane] = acc[co];
+    for (int co = 0; co < COUT; ++co)
+#pragma unroll
+      for (int i = 0; i < NR; ++i) red[grp - 1][co][i][lane] = acc[i][co];
   }
   __syncthreads();
-  if (grp == 0 && ok) {
+  if (grp == 0 && lane >= 1 && lane <= NCOL && x < W) {
 #pragma unroll
-    for (int co = 0; co < COUT; ++co) {
-      const float r = ((acc[co] + red[0][co][lane]) + (red[1][co][lane] + red[2][co][lane])) +
-                      (bias ? bias[co] : 0.0f);
-      out[(long)b * out_bs + co * hw + pix] = r;
-    }
+    for (int co = 0; co < COUT; ++co)
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        if (y0 + i >= H) break;
+        float r = acc[i][co];
+#pragma unroll
+        for (int g = 0; g < NW - 1; ++g) r += red[g][co][i][lane];
+        out[(long)b * out_bs + co * hw + (long)(y0 + i) * W + x] = r + (bias ? bias[co] : 0.0f);
+      }
   }
 }
 
@@ -127,14 +166,13 @@ __global__ __launch_bounds__(256) void conv2d_k3_narrow_kernel(const float *__re
 extern "C" int sa_conv2d_k3_narrow(const float *in, long in_bs, int B, int Cin, int H, int W, const float *weight,
                                    const float *bias, int Cout, float *out, long out_bs, void *stream) {
   SA_REQUIRE(in && weight && out, "sa_conv2d_k3_narrow: null pointer");
-  SA_REQUIRE(B > 0 && B <= 65535 && Cin > 0 && Cin % 4 == 0 && H > 0 && W > 0, "sa_conv2d_k3_narrow: bad shape");
+  SA_REQUIRE(B > 0 && B <= 65535 && Cin > 0 && Cin % NW == 0 && H > 0 && W > 0, "sa_conv2d_k3_narrow: bad shape");
   SA_REQUIRE((long)H * W < (1L << 31), "sa_conv2d_k3_narrow: plane too large");
-  const long hw = (long)H * W;
-  dim3 grid((unsigned)((hw + 63) / 64), (unsigned)B);
+  dim3 grid((unsigned)((W + NCOL - 1) / NCOL), (unsigned)((H + NR - 1) / NR), (unsigned)B);
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_MISC, s);
   if (Cout == 2) {
-    conv2d_k3_narrow_kernel<2><<<grid, 256, 0, s>>>(in, in_bs, Cin, H, W, weight, bias, out, out_bs);
+    conv2d_k3_narrow_kernel<2><<<grid, 512, 0, s>>>(in, in_bs, Cin, H, W, weight, bias, out, out_bs);
     return sa::check_launch("sa_conv2d_k3_narrow");
   }
   sa::set_error("sa_conv2d_k3_narrow: built for 2 outputs (got %d)", Cout);

@@ -204,9 +204,10 @@ def test_convex_upsample(micro):
     np.testing.assert_allclose(out, micro["up.out"], atol=1e-5)
 
 
-def test_gru_gates_and_plumbing():
+@pytest.mark.parametrize("H,W", [(10, 12), (9, 13)])   # float4 and scalar (H*W % 4 != 0) paths
+def test_gru_gates_and_plumbing(H, W):
     rng = np.random.default_rng(9)
-    B, C, H, W = 2, 128, 10, 12
+    B, C = 2, 128
     xc = rng.standard_normal((B, 3 * C, H, W)).astype(np.float32)
     hzr = rng.standard_normal((B, 2 * C, H, W)).astype(np.float32)
     ctx = rng.standard_normal((B, 3 * C, H, W)).astype(np.float32)
