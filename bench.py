@@ -219,6 +219,7 @@ def main():
     # every hand-written kernel family: algorithmic work / live event time vs MI355X peak
     costs = step_costs(hi - lo, H4, W4, args.iters)
     costs["conv2d_wino"] = ("TFLOP/s", work.get("conv2d_wino", 0.0))
+    costs["conv2d_direct"] = ("TFLOP/s", work.get("conv2d_direct", 0.0))
     costs["norm_act"] = ("GB/s", work.get("norm_act", 0.0))
     kernels = {}
     for k, (ms_tot, n_launch) in kt.items():

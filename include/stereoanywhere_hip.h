@@ -258,6 +258,23 @@ typedef struct SaWinoProblem {
 } SaWinoProblem;
 int sa_conv2d_k3_wino_multi(int nprob, const SaWinoProblem *probs, void *stream);
 
+/* Direct KxK convolution (padding K/2, no bias) on fp32 MFMA for the encoder convs the
+ * Winograd kernel does not cover (extractor.py:22-40, 91, 208):
+ *   K = 7, S = 1, Cout % 64 == 0, Cin <= 4 (the 7x7 stems), and
+ *   K = 3, S = 2, Cout 96 or a multiple of 128, Cin % 8 == 0, with the residual block's 1x1
+ *   stride-2 downsample (weights wd, output out_ds) computed in the same launch.
+ * sa_conv_direct_weights arranges a [Cout][Cin][K][K] kernel (K = 1 for the downsample, with
+ * with_ds = 1 and the 3x3 conv's S) into sa_conv_direct_weights_size floats.  part / part_ds:
+ * optional float64 InstanceNorm partials [N*Cout][sa_conv_direct_stat_parts(Ho, Wo)][2] for
+ * sa_instnorm_finalize. */
+long sa_conv_direct_weights_size(int Cout, int Cin, int K, int S, int with_ds);
+int sa_conv_direct_weights(const float *weight, int Cout, int Cin, int K, int S, int with_ds, float *out,
+                           void *stream);
+long sa_conv_direct_stat_parts(int Ho, int Wo);
+int sa_conv_direct(const float *in, long in_bs, int N, int Cin, int H, int W, int K, int S, const float *wg,
+                   const float *wd, int Cout, float *out, long out_bs, float *out_ds, long out_ds_bs,
+                   double *part, double *part_ds, void *stream);
+
 /* Epilogues of the MIOpen 2-D convs (encoders extractor.py:6-300, update block update.py:64-110).
  * sa_plane_stats: InstanceNorm2d statistics (biased variance, eps) of each (b, c) plane of
  *   x [B,C,hw] (batch stride x_bs) -> mean, rstd [B*C].
@@ -278,7 +295,7 @@ int sa_norm_act(const float *x, long x_bs, int B, int C, long hw, const float *m
  * recorded events and returns their summed duration (ms) and count, then clears. */
 enum {
   SA_K_CORR_PYRAMID = 0, SA_K_LOOKUP, SA_K_MONO_VOLUME, SA_K_SOFTARGMIN, SA_K_LSQ,
-  SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_NORM, SA_K_CONV2D, SA_K_COUNT
+  SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_NORM, SA_K_CONV2D, SA_K_CONV_DIRECT, SA_K_COUNT
 };
 int sa_timing_enable(int on);
 int sa_timing_read(int kernel_id, double *total_ms, long *count);

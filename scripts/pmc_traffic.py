@@ -17,7 +17,7 @@ FAMILIES = {
     "corr_pyramid_kernel": "corr_volume_pyramid", "masked_volume_kernel": "mono_masked_volume",
     "sam_contig_kernel": "softargmin_conf", "sam_strided_kernel": "softargmin_conf", "lsq_kernel": "weighted_lsq",
     "gru_zr_kernel": "gru_zr", "gru_out_kernel": "gru_out", "convex_up_kernel": "convex_upsample",
-    "wino_f2k3_kernel": "conv2d_wino", "norm_act_kernel": "norm_act", "plane_stats_kernel": "norm_act",
+    "wino_f2k3_kernel": "conv2d_wino", "conv_direct_kernel": "conv2d_direct", "norm_act_kernel": "norm_act", "plane_stats_kernel": "norm_act",
 }
 
 

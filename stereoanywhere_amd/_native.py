@@ -60,6 +60,10 @@ SIGNATURES = {
     "sa_conv2d_k3_wino_stat_parts": (L, [I, I]),
     "sa_conv2d_k3_wino_ex": (I, [P, L, I, I, I, I, P, I, P, I, P, P, P, I, I, P, L, P, P]),
     "sa_conv2d_k3_wino_multi": (I, [I, P, P]),
+    "sa_conv_direct_weights": (I, [P, I, I, I, I, I, P, P]),
+    "sa_conv_direct_weights_size": (L, [I, I, I, I, I]),
+    "sa_conv_direct_stat_parts": (L, [I, I]),
+    "sa_conv_direct": (I, [P, L, I, I, I, I, I, I, P, P, I, P, L, P, L, P, P, P]),
     "sa_plane_stats": (I, [P, L, I, I, L, F, P, P, P]),
     "sa_norm_act": (I, [P, L, I, I, L, P, P, P, I, I, P, L, P, P, P, I, I, P, L, P]),
     "sa_conv3d_upcat_stat_parts": (L, [I, I, I]),
@@ -76,7 +80,7 @@ SIGNATURES = {
 KERNEL_IDS = {
     "corr_volume_pyramid": 0, "corr_lookup": 1, "mono_masked_volume": 2, "softargmin_conf": 3,
     "weighted_lsq": 4, "gru_zr": 5, "gru_out": 6, "convex_upsample": 7, "misc": 8, "conv3d_fused": 9,
-    "norm_act": 10, "conv2d_wino": 11,
+    "norm_act": 10, "conv2d_wino": 11, "conv2d_direct": 12,
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -1,0 +1,346 @@
+// Direct convolution on fp32 MFMA (implicit GEMM) for the encoder convs that the Winograd
+// kernel does not cover (extractor.py:62-300):
+//   * the 7x7 stems, 3 -> 64 channels at full resolution (fnet / cnet conv1), and
+//   * the stride-2 3x3 conv of each stage's first residual block together with that block's
+//     1x1 stride-2 downsample (extractor.py:22-40): both read the same input pixels (the 1x1
+//     conv's input is the 3x3 conv's centre tap), so one launch computes both.
+// MIOpen runs these as NHWC implicit GEMMs plus layout transposes, 5-7x slower than this.
+//
+//   block  = 8 waves; output tile 8 rows (one per wave) x 32 columns x NC = 16*NTL channels
+//   chunk  = KC input channels: the stride-aware input patch ((8-1)*S+K rows x (32-1)*S+K
+//            columns, zero padded) and the chunk's weights [tap][ci][NC] are staged in LDS;
+//            the next chunk's global loads are in flight while this one multiplies
+//   MFMA   = v_mfma_f32_16x16x4_f32 (exact fp32 products): K runs tap-major over the chunk,
+//            so every LDS offset of a K-step is a compile-time immediate; each wave owns 2
+//            row segments of 16 pixels x all NC channels (+ NC downsample channels)
+//   output = raw conv (no bias: the encoders fold it into the following norm) and optional
+//            float64 InstanceNorm partials per (image, channel, block), as the Winograd conv
+//            writes them (sa_instnorm_finalize)
+#include "sa_common.h"
+
+#pragma clang fp contract(fast)
+
+namespace {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+constexpr int DOTH = 8, DOTW = 32, MT = 2;   // output tile; row segments of 16 pixels per wave
+
+template <int K, int S, int KC, int NTL, bool DS>
+struct DCfg {
+  static constexpr int PH = (DOTH - 1) * S + K, PW = (DOTW - 1) * S + K;
+  static constexpr int PWP = PW;
+  // plane pitch: the A read's two 16-lane k-rows of a half-wave fall in disjoint banks
+  // (stride 1: 16 consecutive columns -> offset 16 mod 32; stride 2: even columns -> odd offset)
+  static constexpr int PL0 = PH * PWP, PR = S == 1 ? 16 : 17;
+  static constexpr int PLANE = PL0 + ((PR - PL0 % 32) + 32) % 32;
+  static constexpr int XN = KC * PLANE;                    // patch floats per chunk
+  static constexpr int NC = 16 * NTL;                      // conv output channels per block
+  static constexpr int KK = K * K;
+  static constexpr int WN = KC * KK * NC;                  // conv weights per chunk, [tap*KC + ci][NC]
+  static constexpr int DN = DS ? KC * NC : 0;              // downsample weights per chunk, [ci][NC]
+  static constexpr int NCP = NC + 16;                      // LDS row pitch of the weights (bank halves)
+  static constexpr int WROWS = KC * KK + (DS ? KC : 0);    // conv rows then downsample rows
+  static constexpr int XPT = (XN + 511) / 512, WPT = (WN + DN) / 4 / 512 + (((WN + DN) / 4) % 512 ? 1 : 0);
+  static constexpr int KSTEPS = KC * KK / 4;
+  static constexpr int NACC = NTL * (DS ? 2 : 1);
+  static constexpr int SMEM = XN + WROWS * NCP + 4;   // + a spare float4 for slot-less commits
+  static_assert(KC % 4 == 0, "a K-step of 4 must stay inside one tap");
+  static_assert((WN + DN) % 4 == 0, "weights are staged as float4");
+  static_assert(SMEM * 4 <= 160 * 1024, "LDS budget");
+  static_assert(8 * 2 * NACC * 16 * 2 <= SMEM, "the stats reduction reuses the staging LDS");
+};
+
+struct DirArgs {
+  const float *in;
+  long in_bs;
+  int Cin, H, W, Ho, Wo;
+  const float *wg, *wd;   // arranged weights (sa_conv_direct_weights layout)
+  int Cout, co_blocks, tiles_w, tiles, nchunks;
+  float *out, *out_ds;
+  long out_bs, out_ds_bs;
+  double *part, *part_ds;
+};
+
+template <int K, int S, int KC, int NTL, bool DS>
+__global__ __launch_bounds__(512, DS ? 2 : 4) void conv_direct_kernel(const DirArgs a) {
+  using C = DCfg<K, S, KC, NTL, DS>;
+  constexpr int NC = C::NC, NCP = C::NCP, PLANE = C::PLANE, PWP = C::PWP;
+  __shared__ __attribute__((aligned(16))) float sm[C::SMEM];
+  float *sx = sm, *sw = sm + C::XN, *sd = sw + KC * C::KK * NCP;
+  constexpr int SPARE = C::SMEM - 4;   // slot-less threads commit here (never read)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const unsigned wid = sa::xcd_remap(blockIdx.x, gridDim.x);   // co blocks of a tile together
+  const int cb = wid % a.co_blocks;
+  const int st = (wid / a.co_blocks) % a.tiles;
+  const int n = wid / (a.co_blocks * a.tiles);
+  const int oy0 = (st / a.tiles_w) * DOTH, ox0 = (st % a.tiles_w) * DOTW;
+  const int iy0 = oy0 * S - K / 2, ix0 = ox0 * S - K / 2;
+  const long hw = (long)a.H * a.W;
+  const float *src = a.in + (long)n * a.in_bs;
+
+  // staging slots, fixed for all chunks: patch element -> image offset.  Channels past Cin
+  // (only a single-chunk stem pads Cin = 3 to KC = 4) read a real channel: their weights are
+  // zero, so any finite value gives the exact result.
+  // Branch-free staging: buffer loads whose out-of-range VGPR offset returns 0 give the zero
+  // padding, and threads without a slot commit to a spare LDS float4.
+  constexpr int OOB = 0x7ffffff0;
+  const __amdgpu_buffer_rsrc_t xin = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(src), (short)0, (int)((long)a.Cin * hw * 4), 0x00020000);
+  int xoff[C::XPT], xl[C::XPT];
+#pragma unroll
+  for (int j = 0; j < C::XPT; ++j) {
+    const int i = tid + 512 * j;
+    const int ci = i / PLANE, rem = i % PLANE, r = rem / PWP, c = rem % PWP;
+    const int y = iy0 + r, x = ix0 + c;
+    const bool ok = i < C::XN && rem < C::PH * PWP && c < C::PW && y >= 0 && y < a.H && x >= 0 && x < a.W;
+    xoff[j] = ok ? (int)((min(ci, a.Cin - 1) * hw + (long)y * a.W + x) * 4) : OOB;
+    xl[j] = i < C::XN ? i : SPARE;
+  }
+  // weights: conv rows then downsample rows, float4 units; LDS slot with the padded pitch
+  constexpr int WQ = (C::WN + C::DN) / 4;
+  const __amdgpu_buffer_rsrc_t win = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(a.wg) + (long)cb * a.nchunks * C::WN, (short)0, (int)((long)a.nchunks * C::WN * 4),
+      0x00020000);
+  const __amdgpu_buffer_rsrc_t din = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(DS ? a.wd + (long)cb * a.nchunks * C::DN : a.wg), (short)0,
+      (int)((long)a.nchunks * (DS ? C::DN : 0) * 4), 0x00020000);
+  int woff[C::WPT], wl[C::WPT];
+  bool wds[C::WPT];
+#pragma unroll
+  for (int j = 0; j < C::WPT; ++j) {
+    const int i = tid + 512 * j;
+    wds[j] = i >= C::WN / 4;
+    woff[j] = i < WQ ? (wds[j] ? (i - C::WN / 4) * 16 : i * 16) : OOB;
+    const int row = (4 * i) / NC, col = (4 * i) % NC;
+    wl[j] = i < WQ ? row * NCP + col : SPARE;
+  }
+  float xr[C::XPT];
+  f32x4 wr[C::WPT];
+  auto fetch = [&](int chunk) __attribute__((always_inline)) {
+    const int xs = chunk * KC * (int)hw * 4;
+#pragma unroll
+    for (int j = 0; j < C::XPT; ++j) xr[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xin, xoff[j], xs, 0));
+#pragma unroll
+    for (int j = 0; j < C::WPT; ++j) {
+      const auto v = wds[j] ? __builtin_amdgcn_raw_buffer_load_b128(din, woff[j], chunk * C::DN * 4, 0)
+                            : __builtin_amdgcn_raw_buffer_load_b128(win, woff[j], chunk * C::WN * 4, 0);
+      wr[j] = f32x4{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3])};
+    }
+  };
+  auto commit = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < C::XPT; ++j) sx[xl[j]] = xr[j];
+#pragma unroll
+    for (int j = 0; j < C::WPT; ++j) *reinterpret_cast<f32x4 *>(sw + wl[j]) = wr[j];
+  };
+
+  f32x4 acc[MT][C::NACC];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int t = 0; t < C::NACC; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // operand lanes (16x16x4): A[m = lane & 15][k = lane >> 4], B[k = lane >> 4][n = lane & 15]
+  const int kq = lane >> 4, ml = lane & 15;
+  int abase[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) abase[m] = kq * PLANE + (wv * S) * PWP + (m * 16 + ml) * S;
+  const int bbase = kq * NCP + ml;
+
+  fetch(0);
+  commit();
+  __syncthreads();
+#pragma unroll 1
+  for (int chunk = 0; chunk < a.nchunks; ++chunk) {
+    if (chunk + 1 < a.nchunks) fetch(chunk + 1);
+#pragma unroll
+    for (int s = 0; s < C::KSTEPS; ++s) {
+      const int tap = (4 * s) / KC, ci0 = (4 * s) % KC;
+      const int koff = ci0 * PLANE + (tap / K) * PWP + (tap % K);
+      float av[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) av[m] = sx[abase[m] + koff];
+#pragma unroll
+      for (int t = 0; t < NTL; ++t) {
+        const float bv = sw[bbase + 4 * s * NCP + t * 16];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv, acc[m][t], 0, 0, 0);
+      }
+      if (DS && tap == (K / 2) * K + K / 2) {
+#pragma unroll
+        for (int t = 0; t < NTL; ++t) {
+          const float bv = sd[bbase + ci0 * NCP + t * 16];
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            acc[m][NTL + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv, acc[m][NTL + t], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+    if (chunk + 1 < a.nchunks) {
+      commit();
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: lane holds channel t*16 + (lane & 15), pixels 4*(lane>>4) + r of segment m.
+  // The stats reduction reuses the staging LDS (free after the loop's last barrier).
+  double *red = reinterpret_cast<double *>(sm);   // [8 waves][2][NACC * 16]
+  constexpr int RC = C::NACC * 16;
+  const int oy = oy0 + wv;
+  const bool stats = a.part != nullptr;
+  const bool interior = oy0 + DOTH <= a.Ho && ox0 + DOTW <= a.Wo && (a.Wo & 3) == 0;
+#pragma unroll
+  for (int t = 0; t < C::NACC; ++t) {
+    const bool ds = DS && t >= NTL;
+    const int co = cb * NC + (ds ? t - NTL : t) * 16 + ml;
+    float *dst = (ds ? a.out_ds + (long)n * a.out_ds_bs : a.out + (long)n * a.out_bs) + (long)co * a.Ho * a.Wo;
+    double s1 = 0.0, s2 = 0.0;
+    if (interior) {   // block-uniform: every output in range, rows float4-aligned
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int ox = ox0 + m * 16 + 4 * kq;   // 4 consecutive pixels of one row
+        *reinterpret_cast<float4 *>(dst + (long)oy * a.Wo + ox) =
+            make_float4(acc[m][t][0], acc[m][t][1], acc[m][t][2], acc[m][t][3]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double v = acc[m][t][r];
+          s1 += v;
+          s2 += v * v;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int ox = ox0 + m * 16 + 4 * kq;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (oy < a.Ho && ox + r < a.Wo) {
+            const float v = acc[m][t][r];
+            dst[(long)oy * a.Wo + ox + r] = v;
+            s1 += (double)v;
+            s2 += (double)v * v;
+          }
+        }
+      }
+    }
+    if (stats) {
+      s1 += __shfl_xor(s1, 16);
+      s2 += __shfl_xor(s2, 16);
+      s1 += __shfl_xor(s1, 32);
+      s2 += __shfl_xor(s2, 32);
+      if (kq == 0) {
+        red[(wv * 2 + 0) * RC + t * 16 + ml] = s1;
+        red[(wv * 2 + 1) * RC + t * 16 + ml] = s2;
+      }
+    }
+  }
+  if (stats) {
+    __syncthreads();
+    for (int c = tid; c < RC; c += 512) {
+      double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        s1 += red[(w * 2 + 0) * RC + c];
+        s2 += red[(w * 2 + 1) * RC + c];
+      }
+      const bool ds = DS && c >= NC;
+      double *pp = ds ? a.part_ds : a.part;
+      if (pp) {
+        const int co = cb * NC + (ds ? c - NC : c);
+        pp += (((long)n * a.Cout + co) * a.tiles + st) * 2;
+        pp[0] = s1;
+        pp[1] = s2;
+      }
+    }
+  }
+}
+
+// weight arrangement: w [Cout][Cin][K][K] -> [co block][chunk][tap][ci in chunk][NC], Cin padded
+// with zeros to a multiple of KC; downsample wd [Cout][Cin] -> [co block][chunk][ci][NC]
+__global__ void direct_weights_kernel(const float *__restrict__ w, int Cout, int Cin, int K, int KC, int NC,
+                                      int nchunks, int ds, float *__restrict__ out) {
+  const long total = (long)Cout * nchunks * KC * K * K;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  // output index decomposition
+  const int n = (int)(i % NC);
+  long r = i / NC;
+  const int ci = (int)(r % KC);
+  r /= KC;
+  const int tap = (int)(r % (K * K));
+  r /= K * K;
+  const int chunk = (int)(r % nchunks);
+  const int cblk = (int)(r / nchunks);
+  const int co = cblk * NC + n, cin = chunk * KC + ci;
+  (void)ds;
+  out[i] = cin < Cin ? w[((long)co * Cin + cin) * K * K + tap] : 0.0f;
+}
+
+// the built configurations: (K, S, Cout) -> channel chunk KC and output tile NTL * 16; the
+// stride-2 3x3 launches always carry the 1x1 downsample (K = 1 arranges its weights)
+bool pick(int K, int S, int Cout, int &KC, int &NTL) {
+  KC = K == 7 ? 4 : 8;
+  if (K == 7 && S == 1 && Cout % 64 == 0) { NTL = 4; return true; }
+  if ((K == 3 || K == 1) && S == 2 && Cout == 96) { NTL = 6; return true; }
+  if ((K == 3 || K == 1) && S == 2 && Cout % 128 == 0) { NTL = 8; return true; }
+  return false;
+}
+
+}  // namespace
+
+extern "C" int sa_conv_direct_weights(const float *weight, int Cout, int Cin, int K, int S, int with_ds,
+                                      float *out, void *stream) {
+  int KC = 0, NTL = 0;
+  SA_REQUIRE(weight && out && Cout > 0 && Cin > 0, "sa_conv_direct_weights: bad arguments");
+  SA_REQUIRE(pick(K, S, Cout, KC, NTL) && (K != 1 || with_ds), "sa_conv_direct_weights: no kernel for K=%d S=%d Cout=%d",
+             K, S, Cout);
+  const int NC = 16 * NTL, nchunks = (Cin + KC - 1) / KC;
+  const long total = (long)Cout * nchunks * KC * K * K;
+  hipStream_t s = sa::as_stream(stream);
+  direct_weights_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(weight, Cout, Cin, K, KC, NC, nchunks, 0,
+                                                                       out);
+  return sa::check_launch("sa_conv_direct_weights");
+}
+
+extern "C" long sa_conv_direct_weights_size(int Cout, int Cin, int K, int S, int with_ds) {
+  int KC = 0, NTL = 0;
+  if (!pick(K, S, Cout, KC, NTL) || (K == 1 && !with_ds)) return -1;
+  return (long)Cout * ((Cin + KC - 1) / KC) * KC * K * K;
+}
+
+extern "C" long sa_conv_direct_stat_parts(int Ho, int Wo) {
+  return (long)((Wo + DOTW - 1) / DOTW) * ((Ho + DOTH - 1) / DOTH);
+}
+
+extern "C" int sa_conv_direct(const float *in, long in_bs, int N, int Cin, int H, int W, int K, int S,
+                              const float *wg, const float *wd, int Cout, float *out, long out_bs, float *out_ds,
+                              long out_ds_bs, double *part, double *part_ds, void *stream) {
+  int KC = 0, NTL = 0;
+  const bool ds = wd != nullptr;
+  SA_REQUIRE(in && wg && out && N > 0 && Cin > 0 && H > 0 && W > 0, "sa_conv_direct: bad arguments");
+  SA_REQUIRE(!ds || out_ds, "sa_conv_direct: downsample weights without an output");
+  SA_REQUIRE(K != 1 && pick(K, S, Cout, KC, NTL) && ds == (S == 2),
+             "sa_conv_direct: no kernel for K=%d S=%d Cout=%d ds=%d", K, S, Cout, (int)ds);
+  SA_REQUIRE((long)Cin * H * W < (1L << 31), "sa_conv_direct: image too large");
+  SA_REQUIRE(Cin % KC == 0 || Cin <= KC, "sa_conv_direct: Cin must be a multiple of %d (or at most %d)", KC, KC);
+  const int p = K / 2;
+  const int Ho = (H + 2 * p - K) / S + 1, Wo = (W + 2 * p - K) / S + 1;
+  const int tiles_w = (Wo + DOTW - 1) / DOTW, tiles = tiles_w * ((Ho + DOTH - 1) / DOTH);
+  const int co_blocks = Cout / (16 * NTL);
+  const DirArgs a{in, in_bs, Cin, H, W, Ho, Wo, wg, wd, Cout, co_blocks, tiles_w, tiles, (Cin + KC - 1) / KC,
+                  out, out_ds, out_bs, out_ds_bs, part, part_ds};
+  const long nblk = (long)N * tiles * co_blocks;
+  SA_REQUIRE(nblk < (1L << 31), "sa_conv_direct: grid too large");
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_CONV_DIRECT, s);
+  if (K == 7) {
+    conv_direct_kernel<7, 1, 4, 4, false><<<(unsigned)nblk, 512, 0, s>>>(a);
+  } else if (NTL == 6) {
+    conv_direct_kernel<3, 2, 8, 6, true><<<(unsigned)nblk, 512, 0, s>>>(a);
+  } else {
+    conv_direct_kernel<3, 2, 8, 8, true><<<(unsigned)nblk, 512, 0, s>>>(a);
+  }
+  return sa::check_launch("sa_conv_direct");
+}

@@ -18,7 +18,7 @@ does under model.eval()) as (x - (running_mean - b)) * gamma / sqrt(running_var 
 """
 from __future__ import annotations
 
-from typing import Dict, List
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -45,6 +45,53 @@ def wino_table(*modules: nn.Module) -> WinoTable:
 
 
 _WINO: WinoTable = {}
+
+# arranged weights of the convs on the direct fp32-MFMA kernel (ops.conv_direct), keyed by the
+# 3x3 / 7x7 conv's weight storage: (conv weights, fused 1x1 downsample weights or None)
+DirectTable = Dict[int, Tuple[torch.Tensor, Optional[torch.Tensor]]]
+_DIRECT: DirectTable = {}
+
+
+def stem_direct(conv: nn.Conv2d) -> bool:
+    """7x7 / stride 1 / pad 3 stems with <= 4 inputs and Cout % 64 == 0."""
+    return (conv.kernel_size == (7, 7) and conv.stride == (1, 1) and conv.padding == (3, 3)
+            and conv.groups == 1 and conv.in_channels <= 4 and conv.out_channels % 64 == 0)
+
+
+def block_direct(blk: nn.Module) -> bool:
+    """A residual block whose conv1 is 3x3 / stride 2 / pad 1 with a 1x1 / stride 2 downsample,
+    Cin % 8 == 0 and Cout 96 or a multiple of 128."""
+    c1 = getattr(blk, "conv1", None)
+    ds = getattr(blk, "downsample", None)
+    if c1 is None or ds is None or not isinstance(ds[0], nn.Conv2d):
+        return False
+    d = ds[0]
+    return (c1.kernel_size == (3, 3) and c1.stride == (2, 2) and c1.padding == (1, 1) and c1.groups == 1
+            and d.kernel_size == (1, 1) and d.stride == (2, 2) and d.padding == (0, 0)
+            and c1.in_channels % 8 == 0 and (c1.out_channels == 96 or c1.out_channels % 128 == 0)
+            and d.out_channels == c1.out_channels)
+
+
+def _direct_fills_chip(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    """The direct kernel runs one 8x32-output block per CU; below one block per CU (cnet's
+    1/16 and 1/32 stages) MIOpen's finer grid is faster."""
+    B, _, H, W = x.shape
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    nc = 96 if conv.out_channels == 96 else 128
+    return B * -(-Ho // 8) * -(-Wo // 32) * (conv.out_channels // nc) >= 256
+
+
+def direct_table(*modules: nn.Module) -> DirectTable:
+    t: DirectTable = {}
+    for mod in modules:
+        if stem_direct(mod.conv1):
+            t[mod.conv1.weight.data_ptr()] = (ops.conv_direct_weights(mod.conv1.weight.detach().contiguous(), 1), None)
+        for blk in mod.modules():
+            if block_direct(blk):
+                t[blk.conv1.weight.data_ptr()] = (
+                    ops.conv_direct_weights(blk.conv1.weight.detach().contiguous(), 2),
+                    ops.conv_direct_weights(blk.downsample[0].weight.detach().contiguous(), 2, with_ds=True))
+    return t
 
 
 def _conv(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
@@ -91,6 +138,16 @@ def _conv_k3(x: torch.Tensor, conv: nn.Conv2d, fin: _Finisher, in_aff=None):
 
 def residual_block(blk: nn.Module, name: str, x: torch.Tensor, fin: _Finisher) -> torch.Tensor:
     w1, w2 = blk.conv1.weight.data_ptr(), blk.conv2.weight.data_ptr()
+    direct = _DIRECT.get(w1)
+    if direct is not None and w2 in _WINO and _direct_fills_chip(x, blk.conv1):
+        # stride-2 conv1 and the 1x1 downsample in one direct-MFMA launch (raw outputs, IN
+        # statistics in its epilogue); conv2 applies norm1 + ReLU while loading conv1's output
+        r = ops.conv_direct(x, direct[0], 3, 2, blk.conv1.out_channels, wd=direct[1], stats=fin.instance)
+        c1, d = r[0], r[1]
+        s1, sd = r[2] if fin.instance else (None, None)
+        c2, s2 = _conv_k3(c1, blk.conv2, fin, in_aff=fin.affine(name + ".norm1", c1, s1))
+        return ops.norm_act(c2, fin.affine(name + ".norm2", c2, s2), act_in="relu", skip=d,
+                            skip_aff=fin.affine(name + ".norm3", d, sd), act_out="relu", out=c2)
     if w1 in _WINO and w2 in _WINO:
         # y1 = relu(N1(c1)) is never written: conv2 applies it while loading c1
         c1, s1 = _conv_k3(x, blk.conv1, fin)
@@ -111,8 +168,15 @@ def residual_block(blk: nn.Module, name: str, x: torch.Tensor, fin: _Finisher) -
 
 
 def _stem(enc: nn.Module, x: torch.Tensor, fin: _Finisher) -> torch.Tensor:
-    c = _conv(x, enc.conv1)
-    return ops.norm_act(c, fin.affine("norm1", c), act_in="relu", out=c)
+    direct = _DIRECT.get(enc.conv1.weight.data_ptr())
+    stats = None
+    if direct is not None:
+        r = ops.conv_direct(x, direct[0], 7, 1, enc.conv1.out_channels, stats=fin.instance)
+        c = r[0]
+        stats = r[1][0] if fin.instance else None
+    else:
+        c = _conv(x, enc.conv1)
+    return ops.norm_act(c, fin.affine("norm1", c, stats), act_in="relu", out=c)
 
 
 def _stage(seq: nn.Sequential, name: str, x: torch.Tensor, fin: _Finisher) -> torch.Tensor:
@@ -121,11 +185,17 @@ def _stage(seq: nn.Sequential, name: str, x: torch.Tensor, fin: _Finisher) -> to
     return x
 
 
-def fnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
-                 wino: WinoTable = None) -> torch.Tensor:
-    """BasicEncoder.forward (extractor.py:62-153) -> [N, 256, H/4, W/4]."""
+def _install(wino: Optional[WinoTable], direct: Optional[DirectTable]) -> None:
     _WINO.clear()
     _WINO.update(wino or {})
+    _DIRECT.clear()
+    _DIRECT.update(direct or {})
+
+
+def fnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
+                 wino: WinoTable = None, direct: DirectTable = None) -> torch.Tensor:
+    """BasicEncoder.forward (extractor.py:62-153) -> [N, 256, H/4, W/4]."""
+    _install(wino, direct)
     fin = _Finisher("instance" if isinstance(enc.norm1, nn.InstanceNorm2d) else "batch", table)
     x = _stem(enc, x, fin)
     for s in ("layer1", "layer2", "layer3"):
@@ -134,12 +204,11 @@ def fnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
 
 
 def cnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
-                 wino: WinoTable = None) -> List[List[torch.Tensor]]:
+                 wino: WinoTable = None, direct: DirectTable = None) -> List[List[torch.Tensor]]:
     """MultiBasicEncoder.forward (extractor.py:156-300) up to the head convs, whose outputs
     are returned RAW (bias not added) as [[h08, c08], [h16, c16], [h32, c32]]; the caller
     finishes them (tanh / relu with the bias) in one pass each."""
-    _WINO.clear()
-    _WINO.update(wino or {})
+    _install(wino, direct)
     fin = _Finisher("instance" if isinstance(enc.norm1, nn.InstanceNorm2d) else "batch", table)
     x = _stem(enc, x, fin)
     for s in ("layer1", "layer2", "layer3"):

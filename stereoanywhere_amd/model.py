@@ -127,6 +127,10 @@ class StereoAnywhere(nn.Module):
                 # Winograd F(2x2,3x3) filters (ops.conv2d_k3) of every eligible 3x3 conv
                 d = self._derived
                 d["wino"] = encoders.wino_table(self.cnet, self.fnet)
+                # the stems and the stride-2 blocks on the direct fp32-MFMA conv (ops.conv_direct)
+                # (SA_DIRECT_CONV=0 leaves them on MIOpen, for A/B timing)
+                d["direct"] = (encoders.direct_table(self.cnet, self.fnet)
+                               if os.environ.get("SA_DIRECT_CONV", "1") != "0" else {})
                 for gk in ("g08", "g16", "g32"):
                     g = d[gk]
                     g.update(Ux=ops.wino_weights(g["wx"]), Uhzr=ops.wino_weights(g["whzr"]),
@@ -197,13 +201,14 @@ class StereoAnywhere(nn.Module):
             ctx = [conv(torch.relu(x[1])) for x, conv in zip(cl, self.context_zqr_convs)]
             fm = self.fnet(torch.cat([image2, image3], 0))
         else:
-            cl = encoders.cnet_forward(self.cnet, mde2.repeat(1, 3, 1, 1), dw["bn_cnet"], dw["wino"])
+            cl = encoders.cnet_forward(self.cnet, mde2.repeat(1, 3, 1, 1), dw["bn_cnet"], dw["wino"], dw["direct"])
             hid, ctx = [], []
             for (h_raw, c_raw), (hb, cb), conv, U in zip(cl, dw["head_b"], self.context_zqr_convs, dw["U_ctx"]):
                 hid.append(ops.norm_act(h_raw, ops.Affine(t=hb), act_in="tanh", out=h_raw))
                 c = ops.norm_act(c_raw, ops.Affine(t=cb), act_in="relu", out=c_raw)
                 ctx.append(ops.conv2d_k3(c, U, conv.bias))  # [B,384,..]
-            fm = encoders.fnet_forward(self.fnet, torch.cat([image2, image3], 0), dw["bn_fnet"], dw["wino"])
+            fm = encoders.fnet_forward(self.fnet, torch.cat([image2, image3], 0), dw["bn_fnet"], dw["wino"],
+                                       dw["direct"])
         fmap2, fmap3 = fm[:B].contiguous(), fm[B:].contiguous()
         feats_l = [F.interpolate(mde2, scale_factor=1 / 2 ** i, mode="bilinear", align_corners=True)
                    for i in range(a.n_downsample, len(self.feature_channels))]

@@ -540,4 +540,47 @@ def conv2d_k3(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = N
                                 stats=stats))[0]
 
 
+def conv_direct_weights(weight: torch.Tensor, stride: int, with_ds: bool = False) -> torch.Tensor:
+    """[Cout, Cin, K, K] -> the direct-conv kernel's chunked layout (sa_conv_direct_weights).
+    with_ds: the weight is the 1x1 downsample fused into a stride-``stride`` 3x3 launch."""
+    _check(weight, "weight")
+    Cout, Cin, K, _ = weight.shape
+    n = int(N.lib().sa_conv_direct_weights_size(Cout, Cin, K, stride, 1 if with_ds else 0))
+    if n < 0:
+        raise RuntimeError(f"conv_direct_weights: no kernel for K={K} stride={stride} Cout={Cout}")
+    out = torch.empty((n,), device=weight.device, dtype=torch.float32)
+    N.call("sa_conv_direct_weights", weight.data_ptr(), Cout, Cin, K, stride, 1 if with_ds else 0, out.data_ptr(),
+           _stream(weight))
+    return out
+
+
+def conv_direct(x: torch.Tensor, wg: torch.Tensor, K: int, stride: int, Cout: int,
+                wd: Optional[torch.Tensor] = None, stats: bool = False):
+    """KxK conv (padding K//2, no bias) on fp32 MFMA: the 7x7 stems and the stride-2 3x3 conv
+    with its fused 1x1 stride-2 downsample (wd).  Returns [out, (out_ds)] and, with stats,
+    the InstanceNorm (mean, rstd) of each output after it."""
+    bs = _plane_bs(x, "x")
+    _check(wg, "wg")
+    B, Cin, H, W = x.shape
+    p = K // 2
+    Ho, Wo = (H + 2 * p - K) // stride + 1, (W + 2 * p - K) // stride + 1
+    out = torch.empty((B, Cout, Ho, Wo), device=x.device, dtype=torch.float32)
+    out_ds = torch.empty_like(out) if wd is not None else None
+    parts = int(N.lib().sa_conv_direct_stat_parts(Ho, Wo)) if stats else 0
+
+    def part():
+        return torch.empty((B * Cout * parts * 2,), device=x.device, dtype=torch.float64) if stats else None
+    pa, pd = part(), (part() if wd is not None else None)
+    N.call("sa_conv_direct", x.data_ptr(), bs, B, Cin, H, W, K, stride, wg.data_ptr(), _ptr(wd), Cout,
+           out.data_ptr(), Cout * Ho * Wo, _ptr(out_ds), Cout * Ho * Wo, _ptr(pa), _ptr(pd), _stream(x))
+    # products executed: the stem's channels padded to the kernel's chunk of 4
+    cin_x = -(-Cin // 4) * 4 if K == 7 else Cin
+    _account("conv2d_direct", 2.0 * B * Cout * cin_x * K * K * Ho * Wo
+             + (2.0 * B * Cout * Cin * Ho * Wo if wd is not None else 0))
+    res = [out] + ([out_ds] if wd is not None else [])
+    if stats:
+        res.append([instnorm_finalize(q, B * Cout, parts, Ho * Wo) for q in (pa, pd) if q is not None])
+    return res
+
+
 __all__ = [n for n in dir() if not n.startswith("_") and n not in ("annotations", "ctypes", "math", "torch")]

@@ -1,0 +1,51 @@
+"""The direct fp32-MFMA conv (csrc/conv_direct.hip) against torch fp32 convs: 7x7 stems and
+stride-2 3x3 convs with the fused 1x1 stride-2 downsample, odd sizes, InstanceNorm stats.
+Tolerance 2e-5 abs / 1e-4 rel (fp32 products, a different summation order)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from stereoanywhere_amd import ops
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def rnd(*shape, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.randn(*shape, generator=g).to(dev)
+
+
+@pytest.mark.parametrize("B,Cin,H,W", [(2, 3, 40, 70), (1, 3, 33, 29), (2, 1, 16, 64)])
+def test_stem_7x7(B, Cin, H, W):
+    x = rnd(B, Cin, H, W, seed=1)
+    w = rnd(64, Cin, 7, 7, seed=2) / 10
+    out, (stats,) = ops.conv_direct(x, ops.conv_direct_weights(w, 1), 7, 1, 64, stats=True)
+    ref = F.conv2d(x, w, padding=3)
+    torch.testing.assert_close(out, ref, atol=2e-5, rtol=1e-4)
+    mean, rstd = stats
+    torch.testing.assert_close(mean, ref.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(rstd, 1 / torch.sqrt(ref.var(dim=(2, 3), unbiased=False).flatten() + 1e-5),
+                               atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("B,Cin,Cout,H,W", [(2, 64, 96, 34, 70), (1, 96, 128, 27, 45), (2, 128, 128, 16, 30),
+                                            (1, 32, 256, 20, 66)])
+def test_stride2_with_downsample(B, Cin, Cout, H, W):
+    x = rnd(B, Cin, H, W, seed=3)
+    w = rnd(Cout, Cin, 3, 3, seed=4) / (3 * Cin ** 0.5)
+    wd = rnd(Cout, Cin, 1, 1, seed=5) / Cin ** 0.5
+    out, ds, (s1, sd) = ops.conv_direct(x, ops.conv_direct_weights(w, 2), 3, 2, Cout,
+                                        wd=ops.conv_direct_weights(wd, 2, with_ds=True), stats=True)
+    ref = F.conv2d(x, w, stride=2, padding=1)
+    ref_d = F.conv2d(x, wd, stride=2)
+    torch.testing.assert_close(out, ref, atol=2e-5, rtol=1e-4)
+    torch.testing.assert_close(ds, ref_d, atol=2e-5, rtol=1e-4)
+    torch.testing.assert_close(s1[0], ref.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(sd[0], ref_d.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
+
+
+def test_unsupported_shapes_raise():
+    x = rnd(1, 12, 16, 16)
+    with pytest.raises(RuntimeError):
+        ops.conv_direct_weights(rnd(80, 12, 3, 3), 2, with_ds=False)

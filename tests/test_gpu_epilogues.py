@@ -105,19 +105,22 @@ def _encoders():
     return fnet.to(dev).eval(), cnet.to(dev).eval()
 
 
-@pytest.mark.parametrize("use_wino", [False, True])
-def test_fused_encoders_match_modules(use_wino):
+@pytest.mark.parametrize("use_wino,use_direct", [(False, False), (True, False), (True, True)])
+def test_fused_encoders_match_modules(use_wino, use_direct):
     """Module forward vs the fused encoders: epilogue passes only (MIOpen convs), and with the
     Winograd convs applying norm + ReLU on load and producing the InstanceNorm statistics."""
     fnet, cnet = _encoders()
     x = rnd(2, 3, 64, 96, seed=21).clamp(-1, 1)
     with torch.no_grad():
         wino = encoders.wino_table(fnet, cnet) if use_wino else None
+        direct = encoders.direct_table(fnet, cnet) if use_direct else None
+        if use_direct:
+            assert len(direct) == 2 + 2 + 4   # two stems, fnet layer2/3, cnet layer2-5
         ref_f = fnet(x)
-        got_f = encoders.fnet_forward(fnet, x, encoders.bn_table(fnet), wino)
+        got_f = encoders.fnet_forward(fnet, x, encoders.bn_table(fnet), wino, direct)
         torch.testing.assert_close(got_f, ref_f, atol=1e-4, rtol=1e-4)
         ref_c = cnet(x)
-        got_c = encoders.cnet_forward(cnet, x, encoders.bn_table(cnet), wino)
+        got_c = encoders.cnet_forward(cnet, x, encoders.bn_table(cnet), wino, direct)
         heads = [cnet.outputs08, cnet.outputs16, cnet.outputs32]
         for lvl in range(3):
             for j in range(2):
