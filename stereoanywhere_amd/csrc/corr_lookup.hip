@@ -115,6 +115,101 @@ __global__ __launch_bounds__(256) void lookup_c1_kernel(const float *__restrict_
   }
 }
 
+// The same, with each level's taps gathered from four aligned float4 buffer loads instead
+// of 2 * (2R+1) scalar loads: one thread per pixel used to touch ~2 cache lines per tap load
+// across 64 rows, which thrashes L1 and re-fetches every line from L2 for every tap.  The
+// float4s cover [x_-R - 1, x_-R + 2R + 3] of the level (the floor of every tap's own grid
+// position lies within 1 of x_-R + t; its fp32 rounding is reproduced exactly per tap), the
+// alignment shift is undone with selects, and every tap picks its two cells with 3-way
+// selects.  Loads past the buffer return 0 (cells outside [0, W_l - 1] are zeroed anyway).
+template <int L, int R, int COUT>
+__global__ __launch_bounds__(256) void lookup_c1_vec_kernel(const float *__restrict__ pa, const float *__restrict__ pb,
+                                                            const float *__restrict__ cx, LGeo g, int npix,
+                                                            int pyr_bytes, const float *__restrict__ wt,
+                                                            const float *__restrict__ bias, int nvol,
+                                                            float *__restrict__ out) {
+  constexpr int K = 2 * R + 1, NT = L * K, WIN = 2 * R + 4;   // cells x_-R - 1 .. x_-R + 2R + 2
+  static_assert(WIN + 3 <= 16, "four float4s cover the window at any alignment");
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= npix) return;
+  const int v = blockIdx.y;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(v ? pb : pa), (short)0, pyr_bytes, 0x00020000);
+  const int hw = g.H * g.W1;
+  const int b = p / hw, rem = p - b * hw;
+  const float x = cx[(long)b * g.cbs + rem];
+  float f[NT];
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    const int Wl = g.wid[l];
+    const float xl = x / (float)(1 << l);
+    const float denom = (float)(Wl - 1);
+    const float sf = (float)(Wl - 1) / 2.0f;
+    int xi[K];
+    float wgt[K];
+#pragma unroll
+    for (int t = -R; t <= R; ++t) {
+      const float x0 = (float)t + xl;
+      const float xg = 2.0f * x0 / denom - 1.0f;
+      const float ix = (xg + 1.0f) * sf;
+      float xw = floorf(ix);
+      wgt[t + R] = ix - xw;
+      // a wide clamp only keeps the int conversion defined: consecutive taps then stay
+      // within 1 of x_-R + t (a tight clamp to [-2, W_l + 1] would break that), and a
+      // cell's in/out-of-range status is the same as the reference's
+      xw = fminf(fmaxf(xw, -16777216.0f), 16777216.0f);
+      xi[t + R] = (int)xw;
+    }
+    // window start (float index in the buffer) and its float4-aligned base
+    const long start = (long)p * g.rs + g.off[l] + xi[0] - 1;
+    float cell[WIN];   // cell[k] = level value at x_-R - 1 + k
+    if (start >= 0) {
+      const long abase = start & ~3L;
+      const int sh = (int)(start - abase);
+      float wv[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const auto u = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (unsigned)(abase * 4) + 16 * q, 0, 0);
+        wv[4 * q + 0] = __uint_as_float(u[0]);
+        wv[4 * q + 1] = __uint_as_float(u[1]);
+        wv[4 * q + 2] = __uint_as_float(u[2]);
+        wv[4 * q + 3] = __uint_as_float(u[3]);
+      }
+#pragma unroll
+      for (int k = 0; k < WIN; ++k)
+        cell[k] = sh == 0 ? wv[k] : sh == 1 ? wv[k + 1] : sh == 2 ? wv[k + 2] : wv[k + 3];
+    } else {   // only the buffer's first row, level 0, with x_-R <= 0: cells before it are unused
+      const float *q = v ? pb : pa;
+#pragma unroll
+      for (int k = 0; k < WIN; ++k) cell[k] = start + k >= 0 ? q[start + k] : 0.0f;
+    }
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const int d = xi[t] - xi[0] - t;   // -1, 0 or +1 (fp32 rounding of the grid position)
+      const float c0 = d == 0 ? cell[t + 1] : d < 0 ? cell[t] : cell[t + 2];
+      const float c1 = d == 0 ? cell[t + 2] : d < 0 ? cell[t + 1] : cell[t + 3 < WIN ? t + 3 : WIN - 1];
+      const float v0 = (xi[t] >= 0 && xi[t] <= Wl - 1) ? c0 : 0.0f;
+      const float v1 = (xi[t] + 1 >= 0 && xi[t] + 1 <= Wl - 1) ? c1 : 0.0f;
+      const float w = wgt[t];
+      f[l * K + t] = v0 * (1.0f - w) + v1 * w;
+    }
+  }
+  float *__restrict__ o = out + ((long)b * nvol + v) * COUT * hw + rem;
+#pragma unroll 4
+  for (int c0 = 0; c0 < COUT; c0 += 8) {
+    float acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = bias[c0 + c];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[c] = fmaf(wt[k * COUT + c0 + c], f[k], acc[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) o[(long)(c0 + c) * hw] = fmaxf(acc[c], 0.0f);
+  }
+}
+
 }  // namespace
 
 extern "C" int sa_corr_lookup_conv1x1(const float *pyramid_a, const float *pyramid_b, int W2, long row_stride,
@@ -146,6 +241,12 @@ extern "C" int sa_corr_lookup_conv1x1(const float *pyramid_a, const float *pyram
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_LOOKUP, s);
   dim3 grid((unsigned)((npix + 255) / 256), nvol);
+  const long pyr_bytes = npix * row_stride * 4;
+  if (pyr_bytes < (1L << 31) - 64 && row_stride % 4 == 0 && (long)H * W1 < (1L << 30)) {
+    lookup_c1_vec_kernel<4, 4, 64><<<grid, 256, 0, s>>>(pyramid_a, pyramid_b ? pyramid_b : pyramid_a, coords_x, g,
+                                                        (int)npix, (int)pyr_bytes, weight_kc, bias, nvol, out);
+    return sa::check_launch("sa_corr_lookup_conv1x1");
+  }
   lookup_c1_kernel<4, 4, 64><<<grid, 256, 0, s>>>(pyramid_a, pyramid_b ? pyramid_b : pyramid_a, coords_x, g, npix,
                                                   weight_kc, bias, nvol, out);
   return sa::check_launch("sa_corr_lookup_conv1x1");

@@ -140,6 +140,7 @@ class StereoAnywhere(nn.Module):
                          U_f2=ops.wino_weights(enc.convf2.weight.detach().contiguous()),
                          U_mot=ops.wino_weights(d["mot_w"]),
                          U_fh1=ops.wino_weights(ub.flow_head.conv1.weight.detach().contiguous()),
+                         U_mask=ops.wino_weights(ub.mask[0].weight.detach().contiguous()),
                          U_ctx=[ops.wino_weights(c.weight.detach().contiguous()) for c in self.context_zqr_convs])
                 cls = torch.cat([self._derived["cls_d"], self._derived["cls_c"]], 0)  # [2,8,3,3,3]
                 self._derived["hg"] = self.hourglass_mono.fused_weights(cls)
@@ -334,6 +335,9 @@ class StereoAnywhere(nn.Module):
             delta = ops.conv2d_k3_narrow(f1, ub.flow_head.conv2.weight, ub.flow_head.conv2.bias)
             ops.flow_update(coords_x, delta[:, 0:1], flow, None)
             if it == iters - 1:
-                mask = ub.mask(h08).mul_(0.25)
+                # mask head (update.py:185-191): 3x3 conv + bias + ReLU on the Winograd kernel,
+                # then the 1x1 conv; x 0.25 as the reference scales it
+                m1 = ops.conv2d_k3(h08, dw["U_mask"], ub.mask[0].bias, relu=True)
+                mask = F.conv2d(m1, ub.mask[2].weight, ub.mask[2].bias).mul_(0.25)
                 flow_up = ops.convex_upsample(flow[:, 0:1].contiguous(), mask, 2 ** self.args.n_downsample)
         return flow_up, None

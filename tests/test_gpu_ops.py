@@ -110,6 +110,30 @@ def test_lookup_fused_convc1():
         np.testing.assert_allclose(out[v::2], ref, atol=2e-5)
 
 
+def test_lookup_fused_taps_bit_exact():
+    """The fused lookup's taps equal the standalone lookup's bit for bit: identity convc1
+    weights (fmaf(1, tap, 0) = tap) and zero bias make the output relu(tap).  Coordinates
+    include integers, values a rounding step off an integer, negatives and past the width."""
+    rng = np.random.default_rng(8)
+    B, H, W = 2, 7, 96
+    va = rng.standard_normal((B, H, W, W)).astype(np.float32)
+    vb = rng.standard_normal((B, H, W, W)).astype(np.float32)
+    base = np.concatenate([np.arange(-6, W + 6, dtype=np.float32),
+                           np.nextafter(np.arange(0, 40, dtype=np.float32), np.float32(-1)),
+                           np.nextafter(np.arange(0, 40, dtype=np.float32), np.float32(100)),
+                           (rng.random(B * H * W) * 110 - 10).astype(np.float32)])
+    cx = base[:B * H * W].reshape(B, 1, H, W).copy()
+    rng.shuffle(cx.reshape(-1))
+    wt = np.zeros((36, 64), np.float32)
+    wt[np.arange(36), np.arange(36)] = 1.0
+    pa, pb = ops.pyramid_from_volume(g(va)), ops.pyramid_from_volume(g(vb))
+    fused = c(ops.corr_lookup_conv1x1(pa, pb, W, 4, 4, g(cx), g(wt), g(np.zeros(64, np.float32))))
+    taps = c(ops.corr_lookup(pa, pb, W, 4, 4, g(cx)))                     # [B, 72, H, W]
+    for v in range(2):
+        np.testing.assert_array_equal(fused[v::2, :36], np.maximum(taps[:, 36 * v:36 * v + 36], 0))
+        assert np.all(fused[v::2, 36:] == 0)
+
+
 def test_hip_corr_block_contract(micro):
     from stereoanywhere_amd.corr import HipCorrBlock1D
     blk = HipCorrBlock1D(g(micro["corr.out"]), num_levels=4, radius=4)
