@@ -4,7 +4,12 @@
   sign = endianness, rows flipped.
 * ``read_mono16`` — frame_utils.read_mono (136-137): 16-bit PNG / 65535.
 * ``MiddleburyFolder`` — middlebury_dataset.py:10-88 layout: <scene>/im0.png, im1*.png,
-  disp0GT.pfm, mask0nocc.png and precomputed mono maps im0_<mono>.png / im1_<mono>.png.
+  disp0GT.pfm, mask0nocc.png (occluded where == 128) and precomputed mono maps
+  im0_<mono>.png / im1_<mono>.png; also ETH3D (the same reader) and Middlebury 2021
+  (middlebury2021_dataset.py:10-60: disp0.pfm, im1 only).
+* ``BoosterFolder`` — booster_dataset.py:10-60 layout: balanced/<scene>/camera_00|02/*.png,
+  <scene>/disp_00.npy (valid where > 0), mask_00.png (occluded where == 0), mono maps in
+  camera_00_<mono>/ and camera_02_<mono>/.
 * ``SyntheticPairs`` — the seeded synthetic pairs of the benchmark, with the true
   disparity as ground truth (no dataset is reachable offline).
 Samples are dicts of float32 numpy arrays in CHW like the reference loaders deliver them.
@@ -63,11 +68,12 @@ def _rgb(img: np.ndarray) -> np.ndarray:
 
 
 class MiddleburyFolder:
-    def __init__(self, root: str, mono: str | None = None):
-        self.mono = mono
+    def __init__(self, root: str, mono: str | None = None, gt_name: str = "disp0GT.pfm",
+                 right_views=("im1", "im1E", "im1L")):
+        self.mono, self.gt_name = mono, gt_name
         self.items = []
         for im0 in sorted(glob(os.path.join(root, "*", "im0.png"))):
-            for im1 in ("im1", "im1E", "im1L"):
+            for im1 in right_views:
                 p1 = im0.replace("im0", im1)
                 if os.path.exists(p1):
                     self.items.append((im0, p1, im1))
@@ -80,17 +86,57 @@ class MiddleburyFolder:
         d = os.path.dirname(im0)
         s = {"im2": _rgb(_read_png(im0)).astype(np.float32).transpose(2, 0, 1) / 255.0,
              "im3": _rgb(_read_png(im1)).astype(np.float32).transpose(2, 0, 1) / 255.0}
-        gt = read_pfm(os.path.join(d, "disp0GT.pfm"))[None]
+        gt = read_pfm(os.path.join(d, self.gt_name))[None]
         s["gt"] = gt.astype(np.float32)
         s["validgt"] = ((gt < 5000) & (gt > 0)).astype(np.uint8)
         occ = os.path.join(d, "mask0nocc.png")
         if os.path.exists(occ):
-            s["maskocc"] = (_read_png(occ) != 255).astype(np.uint8)[None]
+            s["maskocc"] = (_read_png(occ) == 128).astype(np.uint8)[None]   # 1 = occluded
         if self.mono:
             s["im2_mono"] = read_mono16(os.path.join(d, f"im0_{self.mono}.png"))[None]
             s["im3_mono"] = read_mono16(os.path.join(d, f"{tag}_{self.mono}.png"))[None]
         s["name"] = os.path.basename(d)
         return s
+
+
+class BoosterFolder:
+    def __init__(self, root: str, mono: str | None = None):
+        self.mono = mono
+        left = sorted(glob(os.path.join(root, "balanced", "*", "camera_00", "*.png")))
+        right = sorted(glob(os.path.join(root, "balanced", "*", "camera_02", "*.png")))
+        if len(left) != len(right):
+            raise ValueError("Different number of images")
+        self.items = list(zip(left, right))
+
+    def __len__(self):
+        return len(self.items)
+
+    def __getitem__(self, i):
+        im0, im1 = self.items[i]
+        scene = os.path.dirname(os.path.dirname(im0))
+        s = {"im2": _rgb(_read_png(im0)).astype(np.float32).transpose(2, 0, 1) / 255.0,
+             "im3": _rgb(_read_png(im1)).astype(np.float32).transpose(2, 0, 1) / 255.0}
+        gt = np.load(os.path.join(scene, "disp_00.npy")).astype(np.float32)   # numeric array, no pickle
+        s["gt"] = gt[None]
+        s["validgt"] = (gt > 0).astype(np.uint8)[None]
+        s["maskocc"] = (_read_png(os.path.join(scene, "mask_00.png")) == 0).astype(np.uint8)[None]
+        if self.mono:
+            s["im2_mono"] = read_mono16(im0.replace("camera_00", f"camera_00_{self.mono}"))[None]
+            s["im3_mono"] = read_mono16(im1.replace("camera_02", f"camera_02_{self.mono}"))[None]
+        s["name"] = f"{os.path.basename(scene)}_{os.path.splitext(os.path.basename(im0))[0]}"
+        return s
+
+
+def dataset_for(name: str, root: str, mono: str | None):
+    """The harness's dataset switch (dataloaders/__init__.py:22-33) for the real sets this
+    tier evaluates."""
+    if name in ("middlebury", "eth3d"):
+        return MiddleburyFolder(root, mono)
+    if name == "middlebury2021":
+        return MiddleburyFolder(root, mono, gt_name="disp0.pfm", right_views=("im1",))
+    if name == "booster":
+        return BoosterFolder(root, mono)
+    raise NotImplementedError(f"dataset {name!r} is not built in this tier")
 
 
 class SyntheticPairs:

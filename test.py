@@ -87,9 +87,7 @@ def build_dataset(args):
     if args.dataset == "synthetic":
         h, w = map(int, args.synthetic_size.split("x"))
         return data.SyntheticPairs(args.synthetic_count, h, w, float(args.maxdisp))
-    if args.dataset in ("middlebury", "middlebury2014", "middlebury2021", "eth3d", "booster"):
-        return data.MiddleburyFolder(args.datapath, None if args.monomodel == "none" else args.mono_tag)
-    raise NotImplementedError(f"dataset {args.dataset!r} is not built in this tier")
+    return data.dataset_for(args.dataset, args.datapath, None if args.monomodel == "none" else args.mono_tag)
 
 
 @torch.no_grad()
