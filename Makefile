@@ -11,6 +11,10 @@ FLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wn
 
 all: $(OUT)
 
+# packed-f32 SLP vectorisation of the transform math costs register moves and spills beside
+# the 144 MFMA accumulators (and packed VALU is no faster next to MFMAs)
+build/conv2d_wino4.o: FLAGS += -fno-slp-vectorize
+
 build/%.o: stereoanywhere_amd/csrc/%.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(FLAGS) -c $< -o $@

@@ -258,6 +258,17 @@ typedef struct SaWinoProblem {
 } SaWinoProblem;
 int sa_conv2d_k3_wino_multi(int nprob, const SaWinoProblem *probs, void *stream);
 
+/* The same 3x3 convolutions as fused Winograd F(4x4,3x3) on fp32 MFMA (2.25 products per
+ * output instead of 4).  sa_conv2d_wino4_weights transforms [Cout][Cin][3][3] (Cin % 8 == 0,
+ * Cout % 32 == 0) once into U4, 36*Cin*Cout floats laid out [Cout/32][Cin/8][36][2][4][32]
+ * (16-byte aligned).  sa_conv2d_k3_wino4_multi takes SaWinoProblem with U = U4 and needs
+ * W % 4 == 0, 16-byte aligned input planes (in, in_bs % 4 == 0) and no input transform
+ * (in_m / in_s / in_t NULL, in_act 0); bias, ReLU and the InstanceNorm partials
+ * ([N*Cout][parts][2], parts = sa_conv2d_k3_wino4_stat_parts(H, W)) as sa_conv2d_k3_wino_ex. */
+int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, float *U4, void *stream);
+long sa_conv2d_k3_wino4_stat_parts(int H, int W);
+int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, void *stream);
+
 /* Direct KxK convolution (padding K/2, no bias) on fp32 MFMA for the encoder convs the
  * Winograd kernel does not cover (extractor.py:22-40, 91, 208):
  *   K = 7, S = 1, Cout % 64 == 0, Cin <= 4 (the 7x7 stems), and
@@ -295,7 +306,8 @@ int sa_norm_act(const float *x, long x_bs, int B, int C, long hw, const float *m
  * recorded events and returns their summed duration (ms) and count, then clears. */
 enum {
   SA_K_CORR_PYRAMID = 0, SA_K_LOOKUP, SA_K_MONO_VOLUME, SA_K_SOFTARGMIN, SA_K_LSQ,
-  SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_NORM, SA_K_CONV2D, SA_K_CONV_DIRECT, SA_K_COUNT
+  SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_NORM, SA_K_CONV2D, SA_K_CONV_DIRECT,
+  SA_K_CONV2D_W4, SA_K_COUNT
 };
 int sa_timing_enable(int on);
 int sa_timing_read(int kernel_id, double *total_ms, long *count);

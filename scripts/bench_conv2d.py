@@ -41,10 +41,15 @@ def main():
         w = torch.randn(Cout, Cin, 3, 3, device=dev) / (3 * Cin ** 0.5)
         U = ops.wino_weights(w)
         out = torch.empty(N, Cout, H, W, device=dev)
+        ops._WINO4 = False
         t_w = timeit(lambda: ops.conv2d_k3(x, U, out=out))
+        ops._WINO4 = True
+        t_4 = timeit(lambda: ops.conv2d_k3(x, U, out=out))
+        f4 = float((ops.conv2d_k3(x, U) - F.conv2d(x, w, None, padding=1)).abs().max())
         if "--only-wino" in sys.argv:
-            print(f"{name:12s} wino {t_w:8.1f} us ({2.0 * N * Cout * Cin * 9 * H * W / t_w / 1e6:6.1f} TF-eq)",
-                  flush=True)
+            fl = 2.0 * N * Cout * Cin * 9 * H * W
+            print(f"{name:12s} wino {t_w:8.1f} us ({fl / t_w / 1e6:6.1f} TF-eq)  wino4 {t_4:8.1f} us "
+                  f"({fl / t_4 / 1e6:6.1f} TF-eq, {fl / 4 / t_4 / 1e6:5.1f} TF executed) max|d| {f4:.2e}", flush=True)
             continue
         t_m = timeit(lambda: F.conv2d(x, w, None, padding=1))
         ref = F.conv2d(x, w, None, padding=1)

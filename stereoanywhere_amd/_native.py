@@ -60,6 +60,9 @@ SIGNATURES = {
     "sa_conv2d_k3_wino_stat_parts": (L, [I, I]),
     "sa_conv2d_k3_wino_ex": (I, [P, L, I, I, I, I, P, I, P, I, P, P, P, I, I, P, L, P, P]),
     "sa_conv2d_k3_wino_multi": (I, [I, P, P]),
+    "sa_conv2d_wino4_weights": (I, [P, I, I, P, P]),
+    "sa_conv2d_k3_wino4_stat_parts": (L, [I, I]),
+    "sa_conv2d_k3_wino4_multi": (I, [I, P, P]),
     "sa_conv_direct_weights": (I, [P, I, I, I, I, I, P, P]),
     "sa_conv_direct_weights_size": (L, [I, I, I, I, I]),
     "sa_conv_direct_stat_parts": (L, [I, I]),
@@ -80,7 +83,7 @@ SIGNATURES = {
 KERNEL_IDS = {
     "corr_volume_pyramid": 0, "corr_lookup": 1, "mono_masked_volume": 2, "softargmin_conf": 3,
     "weighted_lsq": 4, "gru_zr": 5, "gru_out": 6, "convex_upsample": 7, "misc": 8, "conv3d_fused": 9,
-    "norm_act": 10, "conv2d_wino": 11, "conv2d_direct": 12,
+    "norm_act": 10, "conv2d_wino": 11, "conv2d_direct": 12, "conv2d_wino4": 13,
 }
 
 _lib: Optional[ctypes.CDLL] = None

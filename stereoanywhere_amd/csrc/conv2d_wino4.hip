@@ -1,0 +1,438 @@
+// 3x3 / stride 1 / pad 1 convolution as fused Winograd F(4x4, 3x3) on fp32 MFMA.
+//
+// Same role as conv2d_wino.hip (the encoder and update-block 3x3 convs, extractor.py:6-300,
+// update.py:46-110) with 36 products per 4x4 outputs instead of 16 per 2x2: 2.25 products
+// per output against 4, so the fp32 MFMA peak is 629 TF/s direct-equivalent.  Transform
+// points 0, +-1, +-2, inf (B^T, G, A^T below; filters transformed in fp64, rounded once).
+//
+//   block  = 8 waves, 64 Winograd tiles (16 x 64 or 8 x 128 output pixels, chosen per conv
+//            to waste the fewest padded pixels) x 32 output channels
+//   wave   = 16 tiles (one MFMA M-block) x 32 output channels x one half of the 36 transform
+//            points (columns 0-2 or 3-5 of the 6 x 6 point grid): 144 fp32 accumulators, each
+//            transformed input feeding two MFMAs.  The output transform runs in registers as
+//            far as each half allows; the two halves' partial outputs meet in LDS.
+//   chunk  = 8 input channels.  The input patch and the chunk's transformed filters are
+//            copied global -> LDS by LDS-DMA (buffer_load ... lds, no staging registers),
+//            one chunk ahead, one barrier per chunk.  Zero padding = out-of-range loads
+//            (the patch is staged 16-byte aligned, so every 4-float group is wholly inside
+//            or outside the image; needs W % 4 == 0).
+//   input transform straight into MFMA operands: lane (k, m) of a v_mfma_f32_16x16x4_f32
+//            holds A[tile m][channel k], which is exactly one (tile, channel) transform job,
+//            so V = B^T d B never goes through LDS: the lane reads its 6 patch rows (all in
+//            flight together), runs its half of the row pass (3 of 6 outputs per row), then
+//            each of its 3 column passes yields the A operands of 6 x 2 MFMAs
+//   filters B operands of the two output-channel halves as one float2 per lane (U[point][channel]
+//            [co % 16][co / 16]: conflict-free ds_read_b64)
+//
+// No transform work is duplicated: each (tile, channel, point) value is computed once, by the
+// lane that feeds it to its two MFMAs (about 2 VALU operations per MFMA).
+#include "sa_common.h"
+
+#pragma clang fp contract(fast)
+
+namespace {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+
+constexpr int KC = 8;                     // input channels per chunk (two MFMA k-steps of 4)
+constexpr int NPT = 36;                   // transform points
+constexpr int CO = 32;                    // output channels per block
+constexpr int PS_MAX = 340;               // patch float4 groups per channel, largest geometry (10 x 34)
+constexpr int PBUF = (KC * PS_MAX + 32) * 4;   // floats per patch buffer (+ the last DMA's idle lanes)
+constexpr int UBUF = NPT * KC * CO;       // 9216 floats of filters per chunk
+constexpr int U_OFF = 2 * PBUF;
+constexpr int SMEM = 2 * PBUF + 2 * UBUF;
+constexpr int COP = CO + 1;               // output staging pitch
+constexpr int NWAVE = 8, NTHR = 64 * NWAVE;
+constexpr int PDMA = 6;                   // patch DMA wave-instructions per wave per chunk (<= ceil(43 / 8))
+constexpr int UDMA = UBUF / 256;          // 36 filter DMA wave-instructions (1 KiB each) per chunk
+static_assert(SMEM * 4 <= 160 * 1024, "LDS budget");
+static_assert(64 * 16 * COP <= SMEM, "output staging fits");
+
+struct W4Prob {
+  const float *in;
+  long in_bs;
+  int Cin, H, W;
+  const float *U;
+  int Cout;
+  const float *bias;
+  int relu;
+  float *out;
+  long out_bs;
+  int ltw;                 // log2 of Winograd tiles per block row: 4 (16 x 64 px) or 5 (8 x 128 px)
+  int tiles_w, tiles_hw, co_blocks;
+  double *partial;
+};
+constexpr int MAX_PROB = 8;
+struct W4Launch {
+  W4Prob p[MAX_PROB];
+  unsigned end[MAX_PROB];
+  unsigned nblk[MAX_PROB];
+  int nprob;
+};
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, float *lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)lds, 16, voff, soff, 0, 0);
+}
+
+// B^T x for x = 6 samples (rows of B^T: [4,0,-5,0,1,0] [0,-4,-4,1,1,0] [0,4,-4,-1,1,0]
+// [0,-2,-1,2,1,0] [0,2,-1,-2,1,0] [0,4,0,-5,0,1])
+__device__ __forceinline__ void bt6(const float x0, const float x1, const float x2, const float x3, const float x4,
+                                    const float x5, float *o) {
+  const float a = x4 - 4.0f * x2, b = x3 - 4.0f * x1, c = x4 - x2, e = x3 - x1;
+  o[0] = 4.0f * x0 - 5.0f * x2 + x4;
+  o[1] = a + b;
+  o[2] = a - b;
+  o[3] = c + 2.0f * e;
+  o[4] = c - 2.0f * e;
+  o[5] = 4.0f * x1 - 5.0f * x3 + x5;
+}
+
+// A^T m for m = 6 points (rows [1,1,1,1,1,0] [0,1,-1,2,-2,0] [0,1,1,4,4,0] [0,1,-1,8,-8,1])
+__device__ __forceinline__ void at6(const float *m, float *o) {
+  const float a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], e = m[3] - m[4];
+  o[0] = m[0] + a + c;
+  o[1] = b + 2.0f * e;
+  o[2] = a + 4.0f * c;
+  o[3] = b + 8.0f * e + m[5];
+}
+
+// half HF of B^T x: outputs 0-2 (HF = 0) or 3-5 (HF = 1)
+template <int HF>
+__device__ __forceinline__ void bt6h(const float x0, const float x1, const float x2, const float x3, const float x4,
+                                     const float x5, float *o) {
+  if (HF == 0) {
+    const float a = x4 - 4.0f * x2, b = x3 - 4.0f * x1;
+    o[0] = 4.0f * x0 - 5.0f * x2 + x4;
+    o[1] = a + b;
+    o[2] = a - b;
+  } else {
+    const float c = x4 - x2, e = x3 - x1;
+    o[0] = c + 2.0f * e;
+    o[1] = c - 2.0f * e;
+    o[2] = 4.0f * x1 - 5.0f * x3 + x5;
+  }
+}
+
+template <int HF>
+__device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, float *smem) {
+  const int Cin = P.Cin, H = P.H, W = P.W, Cout = P.Cout;
+  const int ltw = P.ltw, tw = 1 << ltw, tr = 64 >> ltw;
+  const int BH = 4 * tr, BW = 4 * tw, PG = tw + 2, PR = BH + 2, PS = PR * PG;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int co_blocks = P.co_blocks, tiles_hw = P.tiles_hw, tiles_w = P.tiles_w;
+  const int cb = wid % co_blocks;
+  const int st = (wid / co_blocks) % tiles_hw;
+  const int n = wid / (co_blocks * tiles_hw);
+  const int y0 = (st / tiles_w) * BH, x0 = (st % tiles_w) * BW;
+  const int co0 = cb * CO;
+  const int hw = H * W;
+  const int nchunks = Cin / KC;
+
+  const __amdgpu_buffer_rsrc_t xin = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(P.in + (long)n * P.in_bs), (short)0, Cin * hw * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t uin = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(P.U + (long)cb * nchunks * UBUF), (short)0, nchunks * UBUF * 4, 0x00020000);
+
+  // patch DMA: the chunk's image is [channel][PR rows][PG groups of 4 floats], dense, starting
+  // at (y0 - 1, x0 - 4); wave-instruction gi fills groups 64 gi .. 64 gi + 63 (lane-linear)
+  const int npi = (KC * PS + 63) >> 6;
+  int po[PDMA];
+#pragma unroll
+  for (int j = 0; j < PDMA; ++j) {
+    const int s = (wv + NWAVE * j) * 64 + lane;
+    const int ci = s / PS, rem = s - ci * PS, r = rem / PG, g = rem - r * PG;
+    const int y = y0 - 1 + r, x = x0 - 4 + 4 * g;
+    const bool ok = s < KC * PS && y >= 0 && y < H && x >= 0 && x < W;
+    po[j] = ok ? (ci * hw + y * W + x) * 4 : 0x7ffffff0;   // out of range: the load returns 0
+  }
+  auto issue = [&](int chunk, int buf) __attribute__((always_inline)) {
+    float *pb = smem + buf * PBUF;
+    const int xs = chunk * KC * hw * 4;
+#pragma unroll
+    for (int j = 0; j < PDMA; ++j)
+      if (wv + NWAVE * j < npi) dma16(xin, pb + (wv + NWAVE * j) * 256, po[j], xs);
+    float *ub = smem + U_OFF + buf * UBUF;
+    const int us = chunk * UBUF * 4;
+#pragma unroll
+    for (int j = 0; j < (UDMA + NWAVE - 1) / NWAVE; ++j)
+      if (wv + NWAVE * j < UDMA) dma16(uin, ub + (wv + NWAVE * j) * 256, ((wv + NWAVE * j) * 64 + lane) * 16, us);
+  };
+
+  // lane roles: MFMA A operand A[m][k] = (tile m, channel k); B operands B[k][n] = (channel k,
+  // output channel n of each 16-channel half)
+  const int tg = wv & 3;
+  const int k = lane >> 4, m = lane & 15;
+  const int tidx = tg * 16 + m, trow = tidx >> ltw, tcol = tidx & (tw - 1);
+  // patch row 0 of the tile (input row y0 + 4 trow - 1), columns 4 tcol + 2 .. 4 tcol + 9
+  // (input x0 + 4 tcol - 2 ...): the tile's 6 inputs are columns 3..8 of that span
+  const int pread = k * PS * 4 + 4 * trow * PG * 4 + 4 * tcol + 2;
+  const int uread = k * 32 + 2 * m;
+
+  // acc[i][jj][g]: point (row i, column 3 HF + jj) of output-channel half g
+  f32x4 acc[6][3][2];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) acc[i][jj][0] = acc[i][jj][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#ifndef SA_W4_DIAG
+#define SA_W4_DIAG 0   // timing diagnostics only (wrong results): 1 no DMA in the loop, 2 no
+                       // transform / MFMA, 3 no DMA and no barrier in the loop
+#endif
+  issue(0, 0);
+#pragma unroll 1
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const int cur = kc & 1;
+    if (SA_W4_DIAG != 3) __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
+    if (SA_W4_DIAG == 0 || SA_W4_DIAG == 2)
+      if (kc + 1 < nchunks) issue(kc + 1, cur ^ 1);
+    if (SA_W4_DIAG == 2) continue;
+    const float *pb = smem + cur * PBUF + pread;
+    const float *ub = smem + U_OFF + cur * UBUF + uread;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {   // channel k, then k + 4
+      // the lane's 6 patch rows, read 3 at a time (the reads of a group in flight together);
+      // the tile's inputs are a.y, b.xyzw, c.x of each.  This half of the row pass:
+      // t[r][jj] = (B^T d_r)[3 HF + jj]
+      const float *p = pb + s * 4 * PS * 4;
+      float t[6][3];
+#pragma unroll
+      for (int r0 = 0; r0 < 6; r0 += 3) {
+        f32x2 ra[3], rc[3];
+        f32x4 rb[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          ra[r] = *reinterpret_cast<const f32x2 *>(p + (r0 + r) * PG * 4);
+          rb[r] = *reinterpret_cast<const f32x4 *>(p + (r0 + r) * PG * 4 + 2);
+          rc[r] = *reinterpret_cast<const f32x2 *>(p + (r0 + r) * PG * 4 + 6);
+        }
+#pragma unroll
+        for (int r = 0; r < 3; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t[r0 + r]);
+      }
+      // column passes: V[i][3 HF + jj] = (B^T t)[i][jj], each feeding 6 x 2 MFMAs
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) {
+        float v[6];
+        bt6(t[0][jj], t[1][jj], t[2][jj], t[3][jj], t[4][jj], t[5][jj], v);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const int pt = 6 * i + 3 * HF + jj;
+          const f32x2 b = *reinterpret_cast<const f32x2 *>(ub + (pt * 2 + s) * 4 * 32);
+          acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], b.x, acc[i][jj][0], 0, 0, 0);
+          acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], b.y, acc[i][jj][1], 0, 0, 0);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- output transform.  Lane holds tiles tg * 16 + 4 (lane >> 4) + i of output channels
+  // g * 16 + (lane & 15), points of columns 3 HF .. 3 HF + 2.  Y = A^T M A: the column-wise
+  // A^T runs per column, the row-wise A^T only over this half's columns (a partial sum).  Half
+  // 1 stages its partials in O[row][x][co]; half 0 adds its own, the bias and the ReLU.
+  float *ot = smem;
+  const int relu = P.relu;
+#pragma unroll
+  for (int phase = 0; phase < 2; ++phase) {
+    if (phase == 1 - HF) {   // half 1 first
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const int col = g * 16 + (lane & 15);
+        const float bv = (HF == 0 && P.bias) ? P.bias[co0 + col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ti = tg * 16 + 4 * (lane >> 4) + i, orow = (ti >> ltw) * 4, ocol = (ti & (tw - 1)) * 4;
+          float u[4][3];
+#pragma unroll
+          for (int jj = 0; jj < 3; ++jj) {
+            float mcol[6], o[4];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) mcol[a] = acc[a][jj][g][i];
+            at6(mcol, o);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) u[a][jj] = o[a];
+          }
+#pragma unroll
+          for (int a = 0; a < 4; ++a) {
+            // A^T rows restricted to columns 0-2: [1,1,1] [0,1,-1] [0,1,1] [0,1,-1];
+            // columns 3-5: [1,1,0] [2,-2,0] [4,4,0] [8,-8,1]
+            float y[4];
+            if (HF == 0) {
+              const float p = u[a][1] + u[a][2], q = u[a][1] - u[a][2];
+              y[0] = u[a][0] + p;
+              y[1] = q;
+              y[2] = p;
+              y[3] = q;
+            } else {
+              const float p = u[a][0] + u[a][1], q = u[a][0] - u[a][1];
+              y[0] = p;
+              y[1] = 2.0f * q;
+              y[2] = 4.0f * p;
+              y[3] = 8.0f * q + u[a][2];
+            }
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              float *o = ot + ((orow + a) * BW + ocol + b) * COP + col;
+              if (HF == 1) {
+                *o = y[b];
+              } else {
+                float v = (*o + y[b]) + bv;
+                if (relu) v = fmaxf(v, 0.0f);
+                *o = v;
+              }
+            }
+          }
+        }
+      }
+    }
+    if (phase == 0) __syncthreads();
+  }
+  __syncthreads();
+  const int lbw = ltw + 2, lbh = 6 - ltw + 2;   // log2 BW, log2 BH
+  if (P.partial) {
+    // InstanceNorm partials of the block: 16 threads per channel, fixed-order reduction
+    constexpr int TPC = NTHR / CO, PPT = 64 * 16 / TPC;
+    const int c = tid / TPC, part = tid % TPC;
+    double ssum = 0.0, ssq = 0.0;
+#pragma unroll 4
+    for (int p = part * PPT; p < (part + 1) * PPT; ++p) {
+      const int r = p >> lbw, cx = p & (BW - 1);
+      if (y0 + r < H && x0 + cx < W) {
+        const double v = ot[p * COP + c];
+        ssum += v;
+        ssq += v * v;
+      }
+    }
+#pragma unroll
+    for (int o = TPC / 2; o > 0; o >>= 1) {
+      ssum += __shfl_xor(ssum, o);
+      ssq += __shfl_xor(ssq, o);
+    }
+    if (part == 0) {
+      double *pp = P.partial + (((long)n * Cout + co0 + c) * tiles_hw + st) * 2;
+      pp[0] = ssum;
+      pp[1] = ssq;
+    }
+  }
+  float *dst = P.out + (long)n * P.out_bs;
+#pragma unroll 8
+  for (int j = 0; j < (CO * 64 * 16) / NTHR; ++j) {
+    const int i = tid + NTHR * j;
+    const int cx = i & (BW - 1), r = (i >> lbw) & (BH - 1), c = i >> (lbw + lbh);
+    const int y = y0 + r, x = x0 + cx;
+    if (y < H && x < W) dst[(long)(co0 + c) * hw + (long)y * W + x] = ot[((r << lbw) + cx) * COP + c];
+  }
+}
+
+__global__ __launch_bounds__(NTHR) void wino_f4k3_kernel(const W4Launch L) {
+  // problem of the block from its raw id (ranges padded to multiples of 8: every XCD gets an
+  // equal share of each problem), then the L2-locality remap within it (conv2d_wino.hip)
+  const unsigned g = blockIdx.x;
+  W4Prob P = L.p[0];
+  unsigned base = 0, nb = L.nblk[0];
+#pragma unroll
+  for (int i = 1; i < MAX_PROB; ++i) {
+    if (i < L.nprob && g >= L.end[i - 1]) {
+      P = L.p[i];
+      base = L.end[i - 1];
+      nb = L.nblk[i];
+    }
+  }
+  if (g - base >= nb) return;
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
+  // waves 0-3 take point columns 0-2, waves 4-7 columns 3-5 (wave-uniform branch)
+  if (threadIdx.x < 256)
+    w4_body<0>(P, sa::xcd_remap(g - base, nb), smem);
+  else
+    w4_body<1>(P, sa::xcd_remap(g - base, nb), smem);
+}
+
+// U = G g G^T for g = w[co][ci] (3x3), fp64, rounded once.  Layout
+// [Cout/32][Cin/8][36][2][4][16][2]: per (output block, chunk) one contiguous 36 KiB image of
+// the LDS filter buffer; channel ci = 8 chunk + 4 s + k, output co = 32 cb + 16 h + n at
+// [n][h].
+__global__ __launch_bounds__(256) void wino4_weights_kernel(const float *__restrict__ w, int Cout, int Cin,
+                                                            float *__restrict__ U) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)Cout * Cin) return;
+  const int co = (int)(i / Cin), ci = (int)(i % Cin);
+  const float *g = w + i * 9;
+  const double G[6][3] = {{0.25, 0.0, 0.0},
+                          {-1.0 / 6, -1.0 / 6, -1.0 / 6},
+                          {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                          {1.0 / 24, 1.0 / 12, 1.0 / 6},
+                          {1.0 / 24, -1.0 / 12, 1.0 / 6},
+                          {0.0, 0.0, 1.0}};
+  double t[6][3];
+  for (int a = 0; a < 6; ++a)
+    for (int c = 0; c < 3; ++c) t[a][c] = G[a][0] * g[c] + G[a][1] * g[3 + c] + G[a][2] * g[6 + c];
+  const int chunk = ci / 8, s = (ci % 8) / 4, k = ci % 4, cb = co / 32, c = co % 32;
+  for (int a = 0; a < 6; ++a)
+    for (int b = 0; b < 6; ++b) {
+      const double u = t[a][0] * G[b][0] + t[a][1] * G[b][1] + t[a][2] * G[b][2];
+      const int pt = 6 * a + b;
+      U[(((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 2 + s) * 4 + k) * 32 + (c & 15) * 2 + (c >> 4)] = (float)u;
+    }
+}
+
+// geometry with the fewest padded output pixels (ties: 16 x 64, the smaller halo)
+int w4_ltw(int H, int W) {
+  const long a16 = (long)((W + 63) / 64) * 64 * ((H + 15) / 16) * 16;
+  const long a32 = (long)((W + 127) / 128) * 128 * ((H + 7) / 8) * 8;
+  return a32 < a16 ? 5 : 4;
+}
+
+}  // namespace
+
+extern "C" int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, float *U, void *stream) {
+  SA_REQUIRE(weight && U && Cout > 0 && Cin > 0 && Cin % 8 == 0 && Cout % 32 == 0,
+             "sa_conv2d_wino4_weights: bad arguments (Cin %% 8, Cout %% 32)");
+  const long n = (long)Cout * Cin;
+  hipStream_t s = sa::as_stream(stream);
+  wino4_weights_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(weight, Cout, Cin, U);
+  return sa::check_launch("sa_conv2d_wino4_weights");
+}
+
+extern "C" long sa_conv2d_k3_wino4_stat_parts(int H, int W) {
+  const int ltw = w4_ltw(H, W), bw = 4 << ltw, bh = 4 * (64 >> ltw);
+  return (long)((W + bw - 1) / bw) * ((H + bh - 1) / bh);
+}
+
+extern "C" int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, void *stream) {
+  SA_REQUIRE(nprob >= 1 && nprob <= MAX_PROB && probs, "sa_conv2d_k3_wino4_multi: 1..%d problems", MAX_PROB);
+  W4Launch L{};
+  long total = 0;
+  for (int i = 0; i < nprob; ++i) {
+    const SaWinoProblem &q = probs[i];
+    SA_REQUIRE(q.in && q.U && q.out && q.N > 0 && q.H > 0 && q.W > 0, "sa_conv2d_k3_wino4: bad arguments");
+    SA_REQUIRE(q.Cin % KC == 0 && q.Cout % CO == 0,
+               "sa_conv2d_k3_wino4: needs Cin %% 8 == 0 and Cout %% 32 == 0 (got %d, %d)", q.Cin, q.Cout);
+    SA_REQUIRE(q.W % 4 == 0 && (reinterpret_cast<uintptr_t>(q.in) & 15) == 0 && q.in_bs % 4 == 0 &&
+                   (reinterpret_cast<uintptr_t>(q.U) & 15) == 0,
+               "sa_conv2d_k3_wino4: needs W %% 4 == 0 and 16-byte aligned input planes and filters");
+    SA_REQUIRE(!q.in_m && !q.in_s && !q.in_t && !q.in_act, "sa_conv2d_k3_wino4: no input transform");
+    SA_REQUIRE((long)q.Cin * q.H * q.W * 4 < (1L << 31) - 64 && 36L * q.Cin * q.Cout * 4 < (1L << 31),
+               "sa_conv2d_k3_wino4: an image or the filter bank exceeds the 2 GB buffer-descriptor range");
+    const int ltw = w4_ltw(q.H, q.W), bw = 4 << ltw, bh = 4 * (64 >> ltw);
+    const int tiles_w = (q.W + bw - 1) / bw, tiles_h = (q.H + bh - 1) / bh;
+    L.p[i] = W4Prob{q.in, q.in_bs, q.Cin, q.H, q.W, q.U, q.Cout, q.bias, q.relu, q.out, q.out_bs,
+                    ltw, tiles_w, tiles_w * tiles_h, q.Cout / CO, q.stats_partial};
+    const long nb = (long)q.N * L.p[i].tiles_hw * L.p[i].co_blocks;
+    total = (i + 1 < nprob ? (total + nb + 7) / 8 * 8 : total + nb);
+    SA_REQUIRE(total < (1L << 31), "sa_conv2d_k3_wino4: grid too large");
+    L.end[i] = (unsigned)total;
+    L.nblk[i] = (unsigned)nb;
+  }
+  for (int i = nprob; i < MAX_PROB; ++i) {
+    L.end[i] = (unsigned)total;
+    L.nblk[i] = 0;
+  }
+  L.nprob = nprob;
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_CONV2D_W4, s);
+  wino_f4k3_kernel<<<(unsigned)total, NTHR, 0, s>>>(L);
+  return sa::check_launch("sa_conv2d_k3_wino4");
+}

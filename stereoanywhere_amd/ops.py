@@ -8,6 +8,7 @@ PyTorch is plumbing here (device memory, streams); the arithmetic is in the .so.
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from typing import List, Optional, Tuple
 
@@ -484,36 +485,79 @@ def conv2d_k3_narrow(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch
     return out
 
 
-def wino_weights(weight: torch.Tensor) -> torch.Tensor:
-    """[Cout, Cin, 3, 3] -> Winograd F(2x2,3x3) filters U (fp64 transform), a [16, Cin, Cout]
-    container whose storage is the kernel's chunk layout [16][Cin/8][4][Cout][2]."""
+class WinoFilters:
+    """Transformed filters of one 3x3 conv for both fused Winograd kernels: ``u2`` for
+    F(2x2,3x3) (conv2d_wino.hip) and ``u4`` for F(4x4,3x3) (conv2d_wino4.hip)."""
+    __slots__ = ("u2", "u4", "cin", "cout")
+
+    def __init__(self, u2: torch.Tensor, u4: torch.Tensor, cin: int, cout: int):
+        self.u2, self.u4, self.cin, self.cout = u2, u4, cin, cout
+
+
+# SA_WINO4=0 keeps every 3x3 conv on the F(2x2,3x3) kernel (A/B runs)
+_WINO4 = os.environ.get("SA_WINO4", "1") != "0"
+
+
+def wino_weights(weight: torch.Tensor) -> WinoFilters:
+    """[Cout, Cin, 3, 3] -> Winograd filters (fp64 transforms, rounded once): U2 [16][Cin/8][4][Cout][2]
+    and U4 [Cout/32][Cin/8][36][2][4][32], each in a flat container."""
     _check(weight, "weight")
     Cout, Cin = weight.shape[:2]
-    U = torch.empty((16, Cin, Cout), device=weight.device, dtype=torch.float32)
-    N.call("sa_conv2d_wino_weights", weight.data_ptr(), Cout, Cin, U.data_ptr(), _stream(weight))
-    return U
+    u2 = torch.empty((16 * Cin * Cout,), device=weight.device, dtype=torch.float32)
+    N.call("sa_conv2d_wino_weights", weight.data_ptr(), Cout, Cin, u2.data_ptr(), _stream(weight))
+    u4 = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.float32)
+    N.call("sa_conv2d_wino4_weights", weight.data_ptr(), Cout, Cin, u4.data_ptr(), _stream(weight))
+    return WinoFilters(u2, u4, Cin, Cout)
 
 
-def _wino_problem(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = None, relu: bool = False,
+def _wino4_ok(x: torch.Tensor, in_aff=None, in_act=None, **_) -> bool:
+    """F(4x4,3x3) kernel preconditions: no input transform, W % 4 == 0, 16-byte aligned planes."""
+    return (in_aff is None and in_act is None and x.shape[3] % 4 == 0 and x.data_ptr() % 16 == 0
+            and x.stride(0) % 4 == 0)
+
+
+def _wino4_blocks(x: torch.Tensor, U: "WinoFilters", **_) -> int:
+    """Workgroups of the F(4x4,3x3) launch for one conv (conv2d_wino4.hip's geometry chooser:
+    16 x 64 or 8 x 128 output pixels per block, whichever pads less; 32 channels per block)."""
+    B, _, H, W = x.shape
+    a16 = -(-W // 64) * 64 * -(-H // 16) * 16
+    a32 = -(-W // 128) * 128 * -(-H // 8) * 8
+    bh, bw = (8, 128) if a32 < a16 else (16, 64)
+    return B * -(-H // bh) * -(-W // bw) * (U.cout // 32)
+
+
+# below this many workgroups per launch (1.5 per CU) the F(2x2) kernel's four times as many,
+# smaller blocks fill the chip better than F(4x4)'s (measured on the update block's convs)
+_WINO4_MIN_BLOCKS = 384
+
+
+def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] = None, relu: bool = False,
                   out: Optional[torch.Tensor] = None, in_aff: Optional[Affine] = None, in_act=None,
-                  stats: bool = False):
+                  stats: bool = False, f4: bool = False):
     bs = _plane_bs(x, "x")
-    _check(U, "U")
+    if not isinstance(U, WinoFilters):
+        raise RuntimeError("conv2d_k3: U must come from ops.wino_weights")
     B, Cin, H, W = x.shape
-    Cout = U.shape[2]
-    if U.shape[1] != Cin:
-        raise RuntimeError(f"conv2d_k3: U has {U.shape[1]} input channels, x has {Cin}")
+    Cout = U.cout
+    if U.cin != Cin:
+        raise RuntimeError(f"conv2d_k3: U has {U.cin} input channels, x has {Cin}")
     if out is None:
         out = torch.empty((B, Cout, H, W), device=x.device, dtype=torch.float32)
     if tuple(out.shape) != (B, Cout, H, W):
         raise RuntimeError("conv2d_k3: out shape mismatch")
     m, s, t, ps = (in_aff or Affine()).args(Cin)
-    parts = int(N.lib().sa_conv2d_k3_wino_stat_parts(H, W)) if stats else 0
+    parts_fn = N.lib().sa_conv2d_k3_wino4_stat_parts if f4 else N.lib().sa_conv2d_k3_wino_stat_parts
+    parts = int(parts_fn(H, W)) if stats else 0
     partial = torch.empty((B * Cout * parts * 2,), device=x.device, dtype=torch.float64) if stats else None
-    prob = N.SaWinoProblem(x.data_ptr(), bs, B, Cin, H, W, U.data_ptr(), Cout, _ptr(bias), 1 if relu else 0,
-                           m, s, t, ps, ACT[in_act], out.data_ptr(), _plane_bs(out, "out"), _ptr(partial))
-    # Winograd-domain products actually executed: 16 per 2x2 tile per (Cin, Cout) pair
-    _account("conv2d_wino", 2.0 * 16 * Cin * Cout * B * ((H + 1) // 2) * ((W + 1) // 2))
+    prob = N.SaWinoProblem(x.data_ptr(), bs, B, Cin, H, W, (U.u4 if f4 else U.u2).data_ptr(), Cout, _ptr(bias),
+                           1 if relu else 0, m, s, t, ps, ACT[in_act], out.data_ptr(), _plane_bs(out, "out"),
+                           _ptr(partial))
+    # Winograd-domain products actually executed: 36 per 4x4 tile (F4) or 16 per 2x2 tile (F2)
+    # per (Cin, Cout) pair
+    if f4:
+        _account("conv2d_wino4", 2.0 * 36 * Cin * Cout * B * ((H + 3) // 4) * ((W + 3) // 4))
+    else:
+        _account("conv2d_wino", 2.0 * 16 * Cin * Cout * B * ((H + 1) // 2) * ((W + 1) // 2))
     fin = (lambda: (out, instnorm_finalize(partial, B * Cout, parts, H * W))) if stats else (lambda: out)
     return prob, fin
 
@@ -521,12 +565,16 @@ def _wino_problem(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor]
 def conv2d_k3_multi(*problems) -> list:
     """Independent conv2d_k3 calls (each a dict of conv2d_k3's keyword arguments) in ONE launch:
     their blocks share the grid, so each conv's partly filled last round of blocks is filled by
-    the others.  All must agree on Cout % 64 == 0 and on having an input transform or not."""
+    the others.  On the F(4x4,3x3) kernel when every problem meets its preconditions, else on
+    F(2x2,3x3), where all must agree on Cout % 64 == 0 and on having an input transform or not."""
     if not 1 <= len(problems) <= 8:
         raise RuntimeError("conv2d_k3_multi: 1..8 convolutions per launch")
-    built = [_wino_problem(**p) for p in problems]
+    f4 = (_WINO4 and all(_wino4_ok(**p) for p in problems)
+          and sum(_wino4_blocks(**p) for p in problems) >= _WINO4_MIN_BLOCKS)
+    built = [_wino_problem(**p, f4=f4) for p in problems]
     arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
-    N.call("sa_conv2d_k3_wino_multi", len(built), ctypes.addressof(arr), _stream(problems[0]["x"]))
+    N.call("sa_conv2d_k3_wino4_multi" if f4 else "sa_conv2d_k3_wino_multi", len(built), ctypes.addressof(arr),
+           _stream(problems[0]["x"]))
     return [b[1]() for b in built]
 
 

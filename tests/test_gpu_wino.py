@@ -1,4 +1,4 @@
-"""Fused Winograd F(2x2,3x3) conv (conv2d_wino.hip) against torch's fp32 conv (MIOpen).
+"""Fused Winograd F(2x2,3x3) (conv2d_wino.hip) and F(4x4,3x3) (conv2d_wino4.hip) convs against torch's fp32 conv (MIOpen).
 Tolerance: Winograd rounding (transform coefficients +-1, 1/2) over Cin*9-term sums of
 unit-scale data, 2e-5 relative to the output's RMS."""
 import pytest
@@ -18,7 +18,8 @@ def rnd(*shape, seed=0):
 
 @pytest.mark.parametrize("N,Cin,Cout,H,W", [(1, 8, 32, 8, 32), (2, 16, 64, 9, 37), (1, 64, 96, 17, 50),
                                             (2, 128, 256, 34, 60), (1, 256, 384, 20, 33), (3, 192, 128, 6, 7)])
-def test_wino_matches_conv2d(N, Cin, Cout, H, W):
+def test_wino_matches_conv2d(monkeypatch, N, Cin, Cout, H, W):
+    monkeypatch.setattr(ops, "_WINO4", False)   # the F(2x2,3x3) kernel
     x = rnd(N, Cin, H, W, seed=Cin)
     w = rnd(Cout, Cin, 3, 3, seed=Cout) / (3 * Cin ** 0.5)
     b = rnd(Cout, seed=7)
@@ -33,7 +34,8 @@ def test_wino_matches_conv2d(N, Cin, Cout, H, W):
         assert float((got - ref).pow(2).mean().sqrt()) < 2e-6 * max(scale, 1.0) * 10
 
 
-def test_wino_views_and_errors():
+def test_wino_views_and_errors(monkeypatch):
+    monkeypatch.setattr(ops, "_WINO4", False)
     x = rnd(2, 40, 12, 64, seed=1)
     w = rnd(32, 16, 3, 3, seed=2) * 0.1
     U = ops.wino_weights(w)
@@ -46,9 +48,10 @@ def test_wino_views_and_errors():
         ops.conv2d_k3(rnd(1, 12, 8, 8), ops.wino_weights(rnd(32, 12, 3, 3)))   # Cin % 8 != 0
 
 
-def test_multi_launch_matches_separate_convs():
+def test_multi_launch_matches_separate_convs(monkeypatch):
     """sa_conv2d_k3_wino_multi: three convolutions of different shapes (and a channel-slice
     output) in one grid equal torch's convs; mixed Cout % 64 groupings are rejected."""
+    monkeypatch.setattr(ops, "_WINO4", False)
     g = torch.Generator(device="cpu").manual_seed(40)
 
     def rnd(*s):
@@ -70,3 +73,71 @@ def test_multi_launch_matches_separate_convs():
     torch.testing.assert_close(mean, ref_c.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
     with pytest.raises(RuntimeError):
         ops.conv2d_k3_multi(dict(x=xa, U=ops.wino_weights(wa)), dict(x=xa, U=ops.wino_weights(rnd(96, 64, 3, 3))))
+
+
+# ---- F(4x4,3x3) kernel (conv2d_wino4.hip).  Tolerance: transform coefficients up to 8 and
+# 1/24 round more than F(2x2)'s; measured RMS error ~1e-6 and max ~1e-5 of unit-scale outputs,
+# gated at 1e-5 RMS / 1e-4 max (relative to the output's RMS).
+
+def _run(monkeypatch, on, *probs):
+    monkeypatch.setattr(ops, "_WINO4", on)
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)   # small test shapes still take the F(4x4) path
+    ops.WORK = {}
+    try:
+        res = ops.conv2d_k3_multi(*probs)
+        work = dict(ops.WORK)
+    finally:
+        ops.WORK = None
+    return res, work
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(1, 8, 32, 8, 32), (2, 16, 64, 9, 36), (1, 64, 96, 17, 52),
+                                            (2, 128, 256, 34, 60), (1, 256, 384, 20, 240), (3, 192, 128, 6, 8),
+                                            (4, 128, 128, 68, 120), (2, 256, 128, 136, 240)])
+def test_wino4_matches_conv2d(monkeypatch, N, Cin, Cout, H, W):
+    x = rnd(N, Cin, H, W, seed=Cin + 1)
+    w = rnd(Cout, Cin, 3, 3, seed=Cout + 1) / (3 * Cin ** 0.5)
+    b = rnd(Cout, seed=8)
+    U = ops.wino_weights(w)
+    for bias, relu in ((None, False), (b, True)):
+        (got,), work = _run(monkeypatch, True, dict(x=x, U=U, bias=bias, relu=relu))
+        assert "conv2d_wino4" in work and "conv2d_wino" not in work
+        ref = F.conv2d(x, w, bias, padding=1)
+        if relu:
+            ref = torch.relu(ref)
+        scale = max(float(ref.pow(2).mean().sqrt()), 1.0)
+        err_max, err_rms = float((got - ref).abs().max()), float((got - ref).pow(2).mean().sqrt())
+        print(f"wino4 {N}x{Cin}->{Cout} {H}x{W}: max {err_max:.2e} rms {err_rms:.2e} (scale {scale:.2f})")
+        assert err_max < 1e-4 * scale and err_rms < 1e-5 * scale, (err_max, err_rms)
+
+
+def test_wino4_multi_stats_views(monkeypatch):
+    """Three convolutions of different geometries in one F(4x4) launch (8 x 128 and 16 x 64
+    blocks), a channel-slice input and output, InstanceNorm statistics; an ineligible problem
+    (W % 4 != 0) sends the whole launch to the F(2x2) kernel."""
+    g = torch.Generator(device="cpu").manual_seed(41)
+
+    def r(*s):
+        return torch.randn(*s, generator=g).cuda()
+    xa, xb, xc = r(2, 96, 136, 240), r(3, 128, 34, 60), r(2, 32, 20, 52)
+    wa, wb, wc = r(64, 64, 3, 3) / 24, r(128, 128, 3, 3) / 34, r(96, 32, 3, 3) / 17
+    ba = r(64)
+    big = torch.zeros(2, 192, 136, 240, device="cuda")
+    (ya, yb, yc), work = _run(monkeypatch, True,
+                              dict(x=xa[:, 16:80], U=ops.wino_weights(wa), bias=ba, relu=True, out=big[:, 64:128]),
+                              dict(x=xb, U=ops.wino_weights(wb)),
+                              dict(x=xc, U=ops.wino_weights(wc), stats=True))
+    assert "conv2d_wino4" in work
+    torch.testing.assert_close(ya, torch.relu(F.conv2d(xa[:, 16:80], wa, ba, padding=1)), atol=1e-4, rtol=1e-4)
+    assert float(big[:, :64].abs().sum()) == 0 and float(big[:, 128:].abs().sum()) == 0
+    torch.testing.assert_close(yb, F.conv2d(xb, wb, padding=1), atol=1e-4, rtol=1e-4)
+    out_c, (mean, rstd) = yc
+    ref_c = F.conv2d(xc, wc, padding=1)
+    torch.testing.assert_close(out_c, ref_c, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(mean, ref_c.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(rstd, torch.rsqrt(ref_c.var(dim=(2, 3), unbiased=False) + 1e-5).flatten(),
+                               atol=1e-4, rtol=1e-4)
+    (yd, ye), work = _run(monkeypatch, True, dict(x=xb, U=ops.wino_weights(wb)),
+                          dict(x=r(1, 128, 9, 37), U=ops.wino_weights(wb)))
+    assert "conv2d_wino" in work and "conv2d_wino4" not in work
+    torch.testing.assert_close(yd, F.conv2d(xb, wb, padding=1), atol=2e-5, rtol=1e-4)
