@@ -80,13 +80,14 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, float *lds, int 
 // [0,-2,-1,2,1,0] [0,2,-1,-2,1,0] [0,4,0,-5,0,1])
 __device__ __forceinline__ void bt6(const float x0, const float x1, const float x2, const float x3, const float x4,
                                     const float x5, float *o) {
-  const float a = x4 - 4.0f * x2, b = x3 - 4.0f * x1, c = x4 - x2, e = x3 - x1;
-  o[0] = 4.0f * x0 - 5.0f * x2 + x4;
+  // 12 FMA-unit operations (explicit fmaf: no separate multiplies)
+  const float a = fmaf(-4.0f, x2, x4), b = fmaf(-4.0f, x1, x3), c = x4 - x2, e = x3 - x1;
+  o[0] = fmaf(4.0f, x0, fmaf(-5.0f, x2, x4));
   o[1] = a + b;
   o[2] = a - b;
-  o[3] = c + 2.0f * e;
-  o[4] = c - 2.0f * e;
-  o[5] = 4.0f * x1 - 5.0f * x3 + x5;
+  o[3] = fmaf(2.0f, e, c);
+  o[4] = fmaf(-2.0f, e, c);
+  o[5] = fmaf(4.0f, x1, fmaf(-5.0f, x3, x5));
 }
 
 // A^T m for m = 6 points (rows [1,1,1,1,1,0] [0,1,-1,2,-2,0] [0,1,1,4,4,0] [0,1,-1,8,-8,1])
@@ -103,15 +104,15 @@ template <int HF>
 __device__ __forceinline__ void bt6h(const float x0, const float x1, const float x2, const float x3, const float x4,
                                      const float x5, float *o) {
   if (HF == 0) {
-    const float a = x4 - 4.0f * x2, b = x3 - 4.0f * x1;
-    o[0] = 4.0f * x0 - 5.0f * x2 + x4;
+    const float a = fmaf(-4.0f, x2, x4), b = fmaf(-4.0f, x1, x3);
+    o[0] = fmaf(4.0f, x0, fmaf(-5.0f, x2, x4));
     o[1] = a + b;
     o[2] = a - b;
   } else {
     const float c = x4 - x2, e = x3 - x1;
-    o[0] = c + 2.0f * e;
-    o[1] = c - 2.0f * e;
-    o[2] = 4.0f * x1 - 5.0f * x3 + x5;
+    o[0] = fmaf(2.0f, e, c);
+    o[1] = fmaf(-2.0f, e, c);
+    o[2] = fmaf(4.0f, x1, fmaf(-5.0f, x3, x5));
   }
 }
 
@@ -178,6 +179,9 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
 #pragma unroll
     for (int jj = 0; jj < 3; ++jj) acc[i][jj][0] = acc[i][jj][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+#ifndef SA_W4_FENCE
+#define SA_W4_FENCE 1
+#endif
 #ifndef SA_W4_DIAG
 #define SA_W4_DIAG 0   // timing diagnostics only (wrong results): 1 no DMA in the loop, 2 no
                        // transform / MFMA, 3 no DMA and no barrier in the loop
@@ -186,44 +190,58 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
 #pragma unroll 1
   for (int kc = 0; kc < nchunks; ++kc) {
     const int cur = kc & 1;
-    if (SA_W4_DIAG != 3) __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
+    if (SA_W4_DIAG < 3) __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
     if (SA_W4_DIAG == 0 || SA_W4_DIAG == 2)
       if (kc + 1 < nchunks) issue(kc + 1, cur ^ 1);
     if (SA_W4_DIAG == 2) continue;
     const float *pb = smem + cur * PBUF + pread;
     const float *ub = smem + U_OFF + cur * UBUF + uread;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {   // channel k, then k + 4
-      // the lane's 6 patch rows, read 3 at a time (the reads of a group in flight together);
-      // the tile's inputs are a.y, b.xyzw, c.x of each.  This half of the row pass:
-      // t[r][jj] = (B^T d_r)[3 HF + jj]
+    // Per job s (channel k, then k + 4) the lane reads its tile's 6 patch rows (8 floats each;
+    // the inputs are a.y, b.xyzw, c.x), runs its half of the row pass t[r][jj] =
+    // (B^T d_r)[3 HF + jj], then 3 column passes V[i][3 HF + jj] = (B^T t)[i][jj] that feed
+    // 6 x 2 MFMAs each.  Software pipeline (the scheduler is fenced per column to bound its
+    // register use): the filter operands of the next column and rows 0-2 of the next job are
+    // read under the current column's MFMAs.
+    f32x2 ra[6], rc[6];
+    f32x4 rb[6];
+    auto load_rows = [&](int s, int r0, int r1) __attribute__((always_inline)) {
       const float *p = pb + s * 4 * PS * 4;
+#pragma unroll
+      for (int r = r0; r < r1; ++r) {
+        ra[r] = *reinterpret_cast<const f32x2 *>(p + r * PG * 4);
+        rb[r] = *reinterpret_cast<const f32x4 *>(p + r * PG * 4 + 2);
+        rc[r] = *reinterpret_cast<const f32x2 *>(p + r * PG * 4 + 6);
+      }
+    };
+    f32x2 bc[6], bn[6];
+    auto load_b = [&](int s, int jj, f32x2 *b) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) b[i] = *reinterpret_cast<const f32x2 *>(ub + ((6 * i + 3 * HF + jj) * 2 + s) * 4 * 32);
+    };
+    load_rows(0, 0, 6);
+    load_b(0, 0, bc);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (s == 1) load_rows(1, 3, 6);
       float t[6][3];
 #pragma unroll
-      for (int r0 = 0; r0 < 6; r0 += 3) {
-        f32x2 ra[3], rc[3];
-        f32x4 rb[3];
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          ra[r] = *reinterpret_cast<const f32x2 *>(p + (r0 + r) * PG * 4);
-          rb[r] = *reinterpret_cast<const f32x4 *>(p + (r0 + r) * PG * 4 + 2);
-          rc[r] = *reinterpret_cast<const f32x2 *>(p + (r0 + r) * PG * 4 + 6);
-        }
-#pragma unroll
-        for (int r = 0; r < 3; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t[r0 + r]);
-      }
-      // column passes: V[i][3 HF + jj] = (B^T t)[i][jj], each feeding 6 x 2 MFMAs
+      for (int r = 0; r < 6; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t[r]);
+      if (s == 0) load_rows(1, 0, 3);
 #pragma unroll
       for (int jj = 0; jj < 3; ++jj) {
+        if (s == 0 || jj < 2) load_b(jj < 2 ? s : s + 1, jj < 2 ? jj + 1 : 0, bn);
         float v[6];
         bt6(t[0][jj], t[1][jj], t[2][jj], t[3][jj], t[4][jj], t[5][jj], v);
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-          const int pt = 6 * i + 3 * HF + jj;
-          const f32x2 b = *reinterpret_cast<const f32x2 *>(ub + (pt * 2 + s) * 4 * 32);
-          acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], b.x, acc[i][jj][0], 0, 0, 0);
-          acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], b.y, acc[i][jj][1], 0, 0, 0);
+          acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], bc[i].x, acc[i][jj][0], 0, 0, 0);
+          acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], bc[i].y, acc[i][jj][1], 0, 0, 0);
         }
+#if SA_W4_FENCE
+        __builtin_amdgcn_sched_barrier(0);   // bound the scheduler's hoisting (register pressure)
+#endif
+#pragma unroll
+        for (int i = 0; i < 6; ++i) bc[i] = bn[i];
       }
     }
   }
