@@ -161,6 +161,21 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
     for (int j = 0; j < (UDMA + NWAVE - 1) / NWAVE; ++j)
       if (wv + NWAVE * j < UDMA) dma16(uin, ub + (wv + NWAVE * j) * 256, ((wv + NWAVE * j) * 64 + lane) * 16, us);
   };
+  // the same DMAs in three parts, spread over the first job's three column phases (each piece
+  // costs tens of issue cycles; clustered after the barrier they would delay the first reads)
+  auto issue_part = [&](int chunk, int buf, int part) __attribute__((always_inline)) {
+    float *pb = smem + buf * PBUF;
+    const int xs = chunk * KC * hw * 4;
+#pragma unroll
+    for (int j = 2 * part; j < 2 * part + 2; ++j)
+      if (wv + NWAVE * j < npi) dma16(xin, pb + (wv + NWAVE * j) * 256, po[j], xs);
+    float *ub = smem + U_OFF + buf * UBUF;
+    const int us = chunk * UBUF * 4;
+#pragma unroll
+    for (int j = 2 * part; j < 2 * part + 2 && j < (UDMA + NWAVE - 1) / NWAVE; ++j)
+      if (wv + NWAVE * j < UDMA) dma16(uin, ub + (wv + NWAVE * j) * 256, ((wv + NWAVE * j) * 64 + lane) * 16, us);
+  };
+  static_assert(PDMA == 6 && (UDMA + NWAVE - 1) / NWAVE <= 6, "three DMA parts of two pieces");
 
   // lane roles: MFMA A operand A[m][k] = (tile m, channel k); B operands B[k][n] = (channel k,
   // output channel n of each 16-channel half)
@@ -179,6 +194,9 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
 #pragma unroll
     for (int jj = 0; jj < 3; ++jj) acc[i][jj][0] = acc[i][jj][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+#ifndef SA_W4_SPREAD
+#define SA_W4_SPREAD 1
+#endif
 #ifndef SA_W4_FENCE
 #define SA_W4_FENCE 1
 #endif
@@ -186,12 +204,16 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
 #define SA_W4_DIAG 0   // timing diagnostics only (wrong results): 1 no DMA in the loop, 2 no
                        // transform / MFMA, 3 no DMA and no barrier in the loop
 #endif
+#ifndef SA_W4_PRIO
+#define SA_W4_PRIO 0
+#endif
+  if (SA_W4_PRIO && HF == 1) __builtin_amdgcn_s_setprio(1);   // static priority for waves 4-7
   issue(0, 0);
 #pragma unroll 1
   for (int kc = 0; kc < nchunks; ++kc) {
     const int cur = kc & 1;
     if (SA_W4_DIAG < 3) __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
-    if (SA_W4_DIAG == 0 || SA_W4_DIAG == 2)
+    if (SA_W4_DIAG == 2 || (SA_W4_DIAG == 0 && !SA_W4_SPREAD))
       if (kc + 1 < nchunks) issue(kc + 1, cur ^ 1);
     if (SA_W4_DIAG == 2) continue;
     const float *pb = smem + cur * PBUF + pread;
@@ -240,6 +262,12 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
 #if SA_W4_FENCE
         __builtin_amdgcn_sched_barrier(0);   // bound the scheduler's hoisting (register pressure)
 #endif
+        if (SA_W4_DIAG == 0 && SA_W4_SPREAD && s == 0 && kc + 1 < nchunks) {
+          issue_part(kc + 1, cur ^ 1, jj);
+#if SA_W4_FENCE
+          __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
 #pragma unroll
         for (int i = 0; i < 6; ++i) bc[i] = bn[i];
       }
