@@ -130,8 +130,13 @@ class _Finisher:
 
 def _conv_k3(x: torch.Tensor, conv: nn.Conv2d, fin: _Finisher, in_aff=None):
     """Winograd conv of a qualifying 3x3 layer -> (raw out, IN stats or None); with in_aff the
-    producer's norm + ReLU is applied while x is loaded."""
+    producer's norm + ReLU is applied while x is loaded (F(2x2) kernel), or, where the faster
+    F(4x4) kernel takes the conv, by one norm_act pass over x (in place: x is the producer's
+    raw output, read by nothing else) before it."""
     U = _WINO[conv.weight.data_ptr()]
+    if in_aff is not None and ops.wino4_applies(x, U):
+        x = ops.norm_act(x, in_aff, act_in="relu", out=x)
+        in_aff = None
     r = ops.conv2d_k3(x, U, in_aff=in_aff, in_act="relu" if in_aff is not None else None, stats=fin.instance)
     return r if fin.instance else (r, None)
 

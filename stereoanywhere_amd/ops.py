@@ -562,6 +562,11 @@ def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] 
     return prob, fin
 
 
+def wino4_applies(x: torch.Tensor, U: "WinoFilters") -> bool:
+    """Whether a conv2d_k3 of x without an input transform runs on the F(4x4,3x3) kernel."""
+    return _WINO4 and _wino4_ok(x) and _wino4_blocks(x, U) >= _WINO4_MIN_BLOCKS
+
+
 def conv2d_k3_multi(*problems) -> list:
     """Independent conv2d_k3 calls (each a dict of conv2d_k3's keyword arguments) in ONE launch:
     their blocks share the grid, so each conv's partly filled last round of blocks is filled by
