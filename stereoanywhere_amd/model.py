@@ -300,37 +300,55 @@ class StereoAnywhere(nn.Module):
         ops.flow_update(coords_x, None, flow, x08[:, 126:128])
         flow_up = None
         c1v = c1.view(B, 2, c1.shape[1], H4, W4)
+        # update.py:164-197 runs, per iteration, gru32 -> gru16 -> motion encoder -> gru08 -> flow
+        # head.  gru32 of iteration k+1 reads only h16 and h32 as they are after gru16 of
+        # iteration k, so it runs one iteration early, in the launches of gru08's convs; the
+        # motion encoder reads neither GRU state, so its convs share gru16's launches.  Every op
+        # is deterministic and reads the same inputs as in the reference order: the result is
+        # identical, with fewer and fuller conv launches.
+        ops.pool2x(h16, x32)
+        xc32, hzr32 = conv_group(*gate_x_h("32", x32, h32))
+        gru_zr(2, "32", h32, xc32, hzr32)
+        gru_out(2, "32", h32, xc32, ops.conv2d_k3(rh["32"], dw["g32"]["Uqh"]))
         for it in range(iters):
-            # update.py:166-183 runs gru32, gru16, the motion encoder, gru08.  The motion
-            # encoder depends on neither GRU state, so its convs share launches with gru32's
-            # (every op is deterministic: the result is identical to the reference order).
+            last = it == iters - 1
             # lookup of both pyramids + convc1 + ReLU in one kernel (sample 2b: stereo, 2b+1: mono)
             stereo_blk.lookup_conv1x1_into(coords_x, dw["c1_kc"], enc.convc1.bias, c1, other=mono_blk)
             fl = ops.conv2d_small(flow, dw["f1"], enc.convf1.bias, 64, 7, relu=True)
-            ops.pool2x(h16, x32)
-            # gru32's x/h convs + the motion encoder's 3x3 convs (bias + ReLU in the epilogue,
+            ops.pool2x(h08, x16[:, :128])
+            ops.interp(h32, x16[:, 128:])
+            # gru16's x/h convs + the motion encoder's 3x3 convs (bias + ReLU in the epilogue,
             # written straight into the motion conv's input cat(convc2(stereo), convc2(mono),
             # convf2(convf1(flow))))
             mconv = [dict(x=c1v[:, v], U=dw["U_c2"], bias=enc.convc2.bias, relu=True,
                           out=motin[:, 64 * v:64 * v + 64]) for v in range(2)]
             mconv.append(dict(x=fl, U=dw["U_f2"], bias=enc.convf2.bias, relu=True, out=motin[:, 128:192]))
-            xc32, hzr32 = conv_group(*gate_x_h("32", x32, h32), *mconv)[:2]
-            gru_zr(2, "32", h32, xc32, hzr32)
-            # gru32's r*h conv + the motion conv (_conv: 126 outputs, padded to 128, into
-            # x08[:, :128]; channels 126-127 (the flow) are rewritten right after)
-            qh32 = conv_group(dict(x=rh["32"], U=dw["g32"]["Uqh"]),
-                              dict(x=motin, U=dw["U_mot"], bias=dw["mot_b"], relu=True, out=x08[:, :128]))[0]
-            gru_out(2, "32", h32, xc32, qh32)
-            ops.flow_update(coords_x, None, None, x08[:, 126:128])
-            ops.pool2x(h08, x16[:, :128])
-            ops.interp(h32, x16[:, 128:])
-            xc16, hzr16 = conv_group(*gate_x_h("16", x16, h16))
+            xc16, hzr16 = conv_group(*gate_x_h("16", x16, h16), *mconv)[:2]
             gru_zr(1, "16", h16, xc16, hzr16)
-            gru_out(1, "16", h16, xc16, ops.conv2d_k3(rh["16"], dw["g16"]["Uqh"]))
+            # gru16's r*h conv + the motion conv (_conv: 126 outputs, padded to 128, into
+            # x08[:, :128]; channels 126-127 (the flow) are rewritten right after)
+            qh16 = conv_group(dict(x=rh["16"], U=dw["g16"]["Uqh"]),
+                              dict(x=motin, U=dw["U_mot"], bias=dw["mot_b"], relu=True, out=x08[:, :128]))[0]
+            gru_out(1, "16", h16, xc16, qh16)
+            ops.flow_update(coords_x, None, None, x08[:, 126:128])
             ops.interp(h16, x08[:, 128:])
-            xc08, hzr08 = conv_group(*gate_x_h("08", x08, h08))
+            # gru08's x/h convs (+ gru32's of the next iteration), then the r*h convs
+            probs = gate_x_h("08", x08, h08)
+            if not last:
+                ops.pool2x(h16, x32)
+                probs += gate_x_h("32", x32, h32)
+            res = conv_group(*probs)
+            xc08, hzr08 = res[:2]
             gru_zr(0, "08", h08, xc08, hzr08)
-            gru_out(0, "08", h08, xc08, ops.conv2d_k3(rh["08"], dw["g08"]["Uqh"]))
+            probs = [dict(x=rh["08"], U=dw["g08"]["Uqh"])]
+            if not last:
+                xc32, hzr32 = res[2:]
+                gru_zr(2, "32", h32, xc32, hzr32)
+                probs.append(dict(x=rh["32"], U=dw["g32"]["Uqh"]))
+            qh = conv_group(*probs)
+            gru_out(0, "08", h08, xc08, qh[0])
+            if not last:
+                gru_out(2, "32", h32, xc32, qh[1])
             f1 = ops.conv2d_k3(h08, dw["U_fh1"], ub.flow_head.conv1.bias, relu=True)
             delta = ops.conv2d_k3_narrow(f1, ub.flow_head.conv2.weight, ub.flow_head.conv2.bias)
             ops.flow_update(coords_x, delta[:, 0:1], flow, None)
