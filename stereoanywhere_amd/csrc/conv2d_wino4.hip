@@ -43,12 +43,12 @@ constexpr int PBUF = (KC * PS_MAX + 32) * 4;   // floats per patch buffer (+ the
 constexpr int UBUF = NPT * KC * CO;       // 9216 floats of filters per chunk
 constexpr int U_OFF = 2 * PBUF;
 constexpr int SMEM = 2 * PBUF + 2 * UBUF;
-constexpr int COP = CO + 1;               // output staging pitch
+constexpr int OPP = 64 * 16 + 4;          // output staging: channel-plane pitch (4 mod 32)
 constexpr int NWAVE = 8, NTHR = 64 * NWAVE;
 constexpr int PDMA = 6;                   // patch DMA wave-instructions per wave per chunk (<= ceil(43 / 8))
 constexpr int UDMA = UBUF / 256;          // 36 filter DMA wave-instructions (1 KiB each) per chunk
 static_assert(SMEM * 4 <= 160 * 1024, "LDS budget");
-static_assert(64 * 16 * COP <= SMEM, "output staging fits");
+static_assert(CO * OPP <= SMEM, "output staging fits");
 
 struct W4Prob {
   const float *in;
@@ -278,7 +278,9 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
   // ---- output transform.  Lane holds tiles tg * 16 + 4 (lane >> 4) + i of output channels
   // g * 16 + (lane & 15), points of columns 3 HF .. 3 HF + 2.  Y = A^T M A: the column-wise
   // A^T runs per column, the row-wise A^T only over this half's columns (a partial sum).  Half
-  // 1 stages its partials in O[row][x][co]; half 0 adds its own, the bias and the ReLU.
+  // 1 stages its partials in O[co][row][x] (one float4 per output row of a tile); half 0 adds
+  // its own, the bias and the ReLU.  Plane pitch OPP = 4 (mod 32) floats: the 8 lanes of a
+  // ds_write_b128 group (8 output channels) hit disjoint banks.
   float *ot = smem;
   const int relu = P.relu;
 #pragma unroll
@@ -305,30 +307,21 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
           for (int a = 0; a < 4; ++a) {
             // A^T rows restricted to columns 0-2: [1,1,1] [0,1,-1] [0,1,1] [0,1,-1];
             // columns 3-5: [1,1,0] [2,-2,0] [4,4,0] [8,-8,1]
-            float y[4];
+            f32x4 y;
             if (HF == 0) {
               const float p = u[a][1] + u[a][2], q = u[a][1] - u[a][2];
-              y[0] = u[a][0] + p;
-              y[1] = q;
-              y[2] = p;
-              y[3] = q;
+              y = f32x4{u[a][0] + p, q, p, q};
             } else {
               const float p = u[a][0] + u[a][1], q = u[a][0] - u[a][1];
-              y[0] = p;
-              y[1] = 2.0f * q;
-              y[2] = 4.0f * p;
-              y[3] = 8.0f * q + u[a][2];
+              y = f32x4{p, 2.0f * q, 4.0f * p, 8.0f * q + u[a][2]};
             }
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-              float *o = ot + ((orow + a) * BW + ocol + b) * COP + col;
-              if (HF == 1) {
-                *o = y[b];
-              } else {
-                float v = (*o + y[b]) + bv;
-                if (relu) v = fmaxf(v, 0.0f);
-                *o = v;
-              }
+            f32x4 *o = reinterpret_cast<f32x4 *>(ot + col * OPP + (orow + a) * BW + ocol);
+            if (HF == 1) {
+              *o = y;
+            } else {
+              f32x4 v = (*o + y) + bv;
+              if (relu) v = f32x4{fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f)};
+              *o = v;
             }
           }
         }
@@ -337,19 +330,24 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
     if (phase == 0) __syncthreads();
   }
   __syncthreads();
-  const int lbw = ltw + 2, lbh = 6 - ltw + 2;   // log2 BW, log2 BH
+  const int lbw = ltw + 2;   // log2 BW
   if (P.partial) {
-    // InstanceNorm partials of the block: 16 threads per channel, fixed-order reduction
+    // InstanceNorm partials of the block: 16 threads per channel, each over 64 consecutive
+    // pixels of the channel's plane, fixed-order reduction
     constexpr int TPC = NTHR / CO, PPT = 64 * 16 / TPC;
     const int c = tid / TPC, part = tid % TPC;
     double ssum = 0.0, ssq = 0.0;
-#pragma unroll 4
-    for (int p = part * PPT; p < (part + 1) * PPT; ++p) {
+#pragma unroll 2
+    for (int p = part * PPT; p < (part + 1) * PPT; p += 4) {
       const int r = p >> lbw, cx = p & (BW - 1);
-      if (y0 + r < H && x0 + cx < W) {
-        const double v = ot[p * COP + c];
-        ssum += v;
-        ssq += v * v;
+      if (y0 + r < H && x0 + cx < W) {   // W % 4 == 0: a float4 is wholly inside or outside
+        const f32x4 v = *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const double d = v[e];
+          ssum += d;
+          ssq += d * d;
+        }
       }
     }
 #pragma unroll
@@ -363,13 +361,16 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
       pp[1] = ssq;
     }
   }
+  // float4 stores: 256 per channel plane of the block
   float *dst = P.out + (long)n * P.out_bs;
-#pragma unroll 8
-  for (int j = 0; j < (CO * 64 * 16) / NTHR; ++j) {
-    const int i = tid + NTHR * j;
-    const int cx = i & (BW - 1), r = (i >> lbw) & (BH - 1), c = i >> (lbw + lbh);
+#pragma unroll 4
+  for (int j = 0; j < (CO * 64 * 16) / (4 * NTHR); ++j) {
+    const int i4 = tid + NTHR * j;
+    const int c = i4 >> 8, p = (i4 & 255) * 4, r = p >> lbw, cx = p & (BW - 1);
     const int y = y0 + r, x = x0 + cx;
-    if (y < H && x < W) dst[(long)(co0 + c) * hw + (long)y * W + x] = ot[((r << lbw) + cx) * COP + c];
+    if (y < H && x < W)
+      *reinterpret_cast<f32x4 *>(dst + (long)(co0 + c) * hw + (long)y * W + x) =
+          *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
   }
 }
 
@@ -457,8 +458,9 @@ extern "C" int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, v
     SA_REQUIRE(q.Cin % KC == 0 && q.Cout % CO == 0,
                "sa_conv2d_k3_wino4: needs Cin %% 8 == 0 and Cout %% 32 == 0 (got %d, %d)", q.Cin, q.Cout);
     SA_REQUIRE(q.W % 4 == 0 && (reinterpret_cast<uintptr_t>(q.in) & 15) == 0 && q.in_bs % 4 == 0 &&
+                   (reinterpret_cast<uintptr_t>(q.out) & 15) == 0 && q.out_bs % 4 == 0 &&
                    (reinterpret_cast<uintptr_t>(q.U) & 15) == 0,
-               "sa_conv2d_k3_wino4: needs W %% 4 == 0 and 16-byte aligned input planes and filters");
+               "sa_conv2d_k3_wino4: needs W %% 4 == 0 and 16-byte aligned input / output planes and filters");
     SA_REQUIRE(!q.in_m && !q.in_s && !q.in_t && !q.in_act, "sa_conv2d_k3_wino4: no input transform");
     SA_REQUIRE((long)q.Cin * q.H * q.W * 4 < (1L << 31) - 64 && 36L * q.Cin * q.Cout * 4 < (1L << 31),
                "sa_conv2d_k3_wino4: an image or the filter bank exceeds the 2 GB buffer-descriptor range");

@@ -510,10 +510,10 @@ def wino_weights(weight: torch.Tensor) -> WinoFilters:
     return WinoFilters(u2, u4, Cin, Cout)
 
 
-def _wino4_ok(x: torch.Tensor, in_aff=None, in_act=None, **_) -> bool:
+def _wino4_ok(x: torch.Tensor, in_aff=None, in_act=None, out: Optional[torch.Tensor] = None, **_) -> bool:
     """F(4x4,3x3) kernel preconditions: no input transform, W % 4 == 0, 16-byte aligned planes."""
     return (in_aff is None and in_act is None and x.shape[3] % 4 == 0 and x.data_ptr() % 16 == 0
-            and x.stride(0) % 4 == 0)
+            and x.stride(0) % 4 == 0 and (out is None or (out.data_ptr() % 16 == 0 and out.stride(0) % 4 == 0)))
 
 
 def _wino4_blocks(x: torch.Tensor, U: "WinoFilters", **_) -> int:
