@@ -132,6 +132,11 @@ int sa_gru_zr(const float *xc, long xc_bs, const float *bx, const float *hzr, lo
 int sa_gru_out(const float *xc, long xc_bs, const float *bx, const float *qh, long qh_bs, const float *cq,
                long c_bs, const float *z, int B, int C, int HW, float *h, long h_bs,
                void *stream);
+/* As sa_gru_out with the r*h conv split over its input channels: the gate reads qh + qh2
+ * (both with batch stride qh_bs; qh2 may be NULL). */
+int sa_gru_out_split(const float *xc, long xc_bs, const float *bx, const float *qh, const float *qh2, long qh_bs,
+                     const float *cq, long c_bs, const float *z, int B, int C, int HW, float *h, long h_bs,
+                     void *stream);
 
 /* Update-block plumbing that writes straight into channel slices of the GRU inputs
  * (replaces the torch.cat calls of update.py:54-59, 88-90):

@@ -47,6 +47,7 @@ SIGNATURES = {
     "sa_mono_scale_mirror": (I, [P, P, P, P, P, P, I, I, I, L, F, F, P, P, P, P, P]),
     "sa_gru_zr": (I, [P, L, P, P, L, P, P, L, P, L, I, I, I, P, P, P]),
     "sa_gru_out": (I, [P, L, P, P, L, P, L, P, I, I, I, P, L, P]),
+    "sa_gru_out_split": (I, [P, L, P, P, P, L, P, L, P, I, I, I, P, L, P]),
     "sa_pool2x": (I, [P, L, I, I, I, I, P, L, P]),
     "sa_interp_bilinear_ac": (I, [P, L, I, I, I, I, I, I, P, L, P]),
     "sa_relu_copy": (I, [P, L, I, I, I, P, L, P]),

@@ -69,10 +69,13 @@ __global__ __launch_bounds__(256) void gru_zr_kernel(const float *__restrict__ x
   stv<VEC>(rh + b * per + r, ro);
 }
 
+// qh2 (may be NULL): the second half of the r*h conv split over its input channels (the two
+// partial sums are added here, qh + qh2)
 template <int VEC>
 __global__ __launch_bounds__(256) void gru_out_kernel(const float *__restrict__ xc, long xc_bs,
                                                       const float *__restrict__ bx,
-                                                      const float *__restrict__ qh, long qh_bs,
+                                                      const float *__restrict__ qh, const float *__restrict__ qh2,
+                                                      long qh_bs,
                                                       const float *__restrict__ cq, long c_bs,
                                                       const float *__restrict__ z, int C, unsigned HW, unsigned per,
                                                       float *__restrict__ h, long h_bs) {
@@ -82,6 +85,12 @@ __global__ __launch_bounds__(256) void gru_out_kernel(const float *__restrict__ 
   float qx[VEC], qv[VEC], cv[VEC], zv[VEC], hv[VEC];
   ldv<VEC>(xc + b * xc_bs + 2 * (long)per + r, qx);
   ldv<VEC>(qh + b * qh_bs + r, qv);
+  if (qh2) {
+    float q2[VEC];
+    ldv<VEC>(qh2 + b * qh_bs + r, q2);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) qv[j] += q2[j];
+  }
   ldv<VEC>(cq + b * c_bs + r, cv);
   ldv<VEC>(z + b * per + r, zv);
   ldv<VEC>(h + b * h_bs + r, hv);
@@ -192,24 +201,30 @@ extern "C" int sa_gru_zr(const float *xc, long xc_bs, const float *bx, const flo
   return sa::check_launch("sa_gru_zr");
 }
 
-extern "C" int sa_gru_out(const float *xc, long xc_bs, const float *bx, const float *qh, long qh_bs, const float *cq, long c_bs,
-                          const float *z, int B, int C, int HW, float *h, long h_bs, void *stream) {
+extern "C" int sa_gru_out_split(const float *xc, long xc_bs, const float *bx, const float *qh, const float *qh2,
+                                long qh_bs, const float *cq, long c_bs, const float *z, int B, int C, int HW, float *h,
+                                long h_bs, void *stream) {
   SA_REQUIRE(xc && qh && cq && z && h, "sa_gru_out: null pointer");
   SA_REQUIRE(B > 0 && B <= 65535 && C > 0 && HW > 0, "sa_gru_out: empty shape");
   SA_REQUIRE((long)C * HW < (1L << 31), "sa_gru_out: plane too large");
   const unsigned per = (unsigned)((long)C * HW);
-  const bool v4 = HW % 4 == 0 && al16(xc) && al16(qh) && al16(cq) && al16(z) && al16(h) && xc_bs % 4 == 0 &&
-                  qh_bs % 4 == 0 && c_bs % 4 == 0 && h_bs % 4 == 0;
+  const bool v4 = HW % 4 == 0 && al16(xc) && al16(qh) && (!qh2 || al16(qh2)) && al16(cq) && al16(z) && al16(h) &&
+                  xc_bs % 4 == 0 && qh_bs % 4 == 0 && c_bs % 4 == 0 && h_bs % 4 == 0;
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_GRU_OUT, s);
   if (v4) {
-    gru_out_kernel<4><<<dim3((per / 4 + 255) / 256, B), 256, 0, s>>>(xc, xc_bs, bx, qh, qh_bs, cq, c_bs, z, C, HW, per,
-                                                                      h, h_bs);
+    gru_out_kernel<4><<<dim3((per / 4 + 255) / 256, B), 256, 0, s>>>(xc, xc_bs, bx, qh, qh2, qh_bs, cq, c_bs, z, C, HW,
+                                                                      per, h, h_bs);
   } else {
-    gru_out_kernel<1><<<dim3((per + 255) / 256, B), 256, 0, s>>>(xc, xc_bs, bx, qh, qh_bs, cq, c_bs, z, C, HW, per, h,
-                                                                  h_bs);
+    gru_out_kernel<1><<<dim3((per + 255) / 256, B), 256, 0, s>>>(xc, xc_bs, bx, qh, qh2, qh_bs, cq, c_bs, z, C, HW, per,
+                                                                  h, h_bs);
   }
   return sa::check_launch("sa_gru_out");
+}
+
+extern "C" int sa_gru_out(const float *xc, long xc_bs, const float *bx, const float *qh, long qh_bs, const float *cq, long c_bs,
+                          const float *z, int B, int C, int HW, float *h, long h_bs, void *stream) {
+  return sa_gru_out_split(xc, xc_bs, bx, qh, nullptr, qh_bs, cq, c_bs, z, B, C, HW, h, h_bs, stream);
 }
 
 extern "C" int sa_pool2x(const float *in, long in_bs, int B, int C, int H, int W, float *out, long out_bs,

@@ -133,8 +133,13 @@ class StereoAnywhere(nn.Module):
                                if os.environ.get("SA_DIRECT_CONV", "1") != "0" else {})
                 for gk in ("g08", "g16", "g32"):
                     g = d[gk]
+                    half = g["wqh"].shape[1] // 2
                     g.update(Ux=ops.wino_weights(g["wx"]), Uhzr=ops.wino_weights(g["whzr"]),
-                             Uqh=ops.wino_weights(g["wqh"]))
+                             Uqh=ops.wino_weights(g["wqh"]),
+                             # the r*h conv split over its input channels (two half-K launches'
+                             # worth of blocks; gru_out adds the partial sums)
+                             Uqh_k=[ops.wino_weights(g["wqh"][:, :half].contiguous()),
+                                    ops.wino_weights(g["wqh"][:, half:].contiguous())])
                 d.update(c1_kc=enc.convc1.weight.detach().reshape(enc.convc1.out_channels, -1).t().contiguous(),
                          U_c2=ops.wino_weights(enc.convc2.weight.detach().contiguous()),
                          U_f2=ops.wino_weights(enc.convf2.weight.detach().contiguous()),
@@ -294,8 +299,15 @@ class StereoAnywhere(nn.Module):
         def gru_zr(level, key, h, xc, hzr):
             ops.gru_zr(xc, hzr, cz[level], cr[level], h, z[key], rh[key], bx=dw["g" + key]["bx"])
 
-        def gru_out(level, key, h, xc, qh):
-            ops.gru_out(xc, qh, cq[level], z[key], h, bx=dw["g" + key]["bx"])
+        def gru_out(level, key, h, xc, qh, qh2=None):
+            ops.gru_out(xc, qh, cq[level], z[key], h, bx=dw["g" + key]["bx"], qh2=qh2)
+
+        def qh_split(key):
+            """r*h conv of one GRU as two half-Cin problems (more, shorter blocks: the launch's
+            last round of blocks costs less)."""
+            r, Uk = rh[key], dw["g" + key]["Uqh_k"]
+            c = r.shape[1] // 2
+            return [dict(x=r[:, :c], U=Uk[0]), dict(x=r[:, c:], U=Uk[1])]
 
         ops.flow_update(coords_x, None, flow, x08[:, 126:128])
         flow_up = None
@@ -340,15 +352,15 @@ class StereoAnywhere(nn.Module):
             res = conv_group(*probs)
             xc08, hzr08 = res[:2]
             gru_zr(0, "08", h08, xc08, hzr08)
-            probs = [dict(x=rh["08"], U=dw["g08"]["Uqh"])]
+            probs = qh_split("08")
             if not last:
                 xc32, hzr32 = res[2:]
                 gru_zr(2, "32", h32, xc32, hzr32)
-                probs.append(dict(x=rh["32"], U=dw["g32"]["Uqh"]))
+                probs += qh_split("32")
             qh = conv_group(*probs)
-            gru_out(0, "08", h08, xc08, qh[0])
+            gru_out(0, "08", h08, xc08, qh[0], qh[1])
             if not last:
-                gru_out(2, "32", h32, xc32, qh[1])
+                gru_out(2, "32", h32, xc32, qh[2], qh[3])
             f1 = ops.conv2d_k3(h08, dw["U_fh1"], ub.flow_head.conv1.bias, relu=True)
             delta = ops.conv2d_k3_narrow(f1, ub.flow_head.conv2.weight, ub.flow_head.conv2.bias)
             ops.flow_update(coords_x, delta[:, 0:1], flow, None)

@@ -266,12 +266,15 @@ def gru_zr(xc, hzr, cz, cr, h, z_out, rh_out, bx: Optional[torch.Tensor] = None)
            z_out.data_ptr(), rh_out.data_ptr(), _stream(h))
 
 
-def gru_out(xc, qh, cq, z, h, bx: Optional[torch.Tensor] = None):
-    """h = (1 - z) h + z tanh(xc_q + bx_q + qh + cq), in place."""
+def gru_out(xc, qh, cq, z, h, bx: Optional[torch.Tensor] = None, qh2: Optional[torch.Tensor] = None):
+    """h = (1 - z) h + z tanh(xc_q + bx_q + qh (+ qh2) + cq), in place; qh2: the second partial sum
+    of an r*h conv split over its input channels (same layout as qh)."""
     B, C, H, W = h.shape
-    N.call("sa_gru_out", xc.data_ptr(), _plane_bs(xc, "xc"), _ptr(bx), qh.data_ptr(), _plane_bs(qh, "qh"),
-           cq.data_ptr(), _plane_bs(cq, "cq"), z.data_ptr(), B, C, H * W, h.data_ptr(), _plane_bs(h, "h"),
-           _stream(h))
+    if qh2 is not None and (qh2.shape != qh.shape or _plane_bs(qh2, "qh2") != _plane_bs(qh, "qh")):
+        raise RuntimeError("gru_out: qh2 must match qh's shape and batch stride")
+    N.call("sa_gru_out_split", xc.data_ptr(), _plane_bs(xc, "xc"), _ptr(bx), qh.data_ptr(), _ptr(qh2),
+           _plane_bs(qh, "qh"), cq.data_ptr(), _plane_bs(cq, "cq"), z.data_ptr(), B, C, H * W, h.data_ptr(),
+           _plane_bs(h, "h"), _stream(h))
 
 
 def pool2x(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:

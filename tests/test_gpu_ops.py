@@ -247,6 +247,11 @@ def test_gru_gates_and_plumbing(H, W):
     np.testing.assert_allclose(c(z), zr, atol=1e-6)
     np.testing.assert_allclose(c(rh), rr * h, atol=1e-6)
     np.testing.assert_allclose(c(gh), (1 - zr) * h + zr * q, atol=2e-6)
+    # the r*h conv split over its input channels: the gate adds the two partial sums
+    gh2 = g(h)
+    qa = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    ops.gru_out(g(xc), g(qa), gctx[:, 2 * C:], z, gh2, qh2=g(qh - qa))
+    np.testing.assert_allclose(c(gh2), (1 - zr) * h + zr * q, atol=2e-6)
     # plumbing vs torch's own ops on the GPU
     x = g(rng.standard_normal((B, C, 17, 23)))
     buf = torch.zeros(B, 2 * C, 9, 12, device=dev)
