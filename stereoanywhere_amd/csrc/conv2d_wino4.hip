@@ -374,6 +374,11 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
   }
 }
 
+#ifdef SA_W4_CLOCK
+// diagnostic build only: per block (s_memtime, s_memrealtime) at the start and the end of wave 0
+__device__ unsigned long long g_w4_clock[65536][4];
+#endif
+
 __global__ __launch_bounds__(NTHR) void wino_f4k3_kernel(const W4Launch L) {
   // problem of the block from its raw id (ranges padded to multiples of 8: every XCD gets an
   // equal share of each problem), then the L2-locality remap within it (conv2d_wino.hip)
@@ -390,11 +395,22 @@ __global__ __launch_bounds__(NTHR) void wino_f4k3_kernel(const W4Launch L) {
   }
   if (g - base >= nb) return;
   __shared__ __attribute__((aligned(16))) float smem[SMEM];
+#ifdef SA_W4_CLOCK
+  unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   // waves 0-3 take point columns 0-2, waves 4-7 columns 3-5 (wave-uniform branch)
   if (threadIdx.x < 256)
     w4_body<0>(P, sa::xcd_remap(g - base, nb), smem);
   else
     w4_body<1>(P, sa::xcd_remap(g - base, nb), smem);
+#ifdef SA_W4_CLOCK
+  if (threadIdx.x == 0 && g < 65536) {
+    g_w4_clock[g][0] = t0;
+    g_w4_clock[g][1] = r0;
+    g_w4_clock[g][2] = __builtin_amdgcn_s_memtime();
+    g_w4_clock[g][3] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 // U = G g G^T for g = w[co][ci] (3x3), fp64, rounded once.  Layout
@@ -442,6 +458,12 @@ extern "C" int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, f
   wino4_weights_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(weight, Cout, Cin, U);
   return sa::check_launch("sa_conv2d_wino4_weights");
 }
+
+#ifdef SA_W4_CLOCK
+extern "C" int sa_w4_clock_read(unsigned long long *out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4_clock), sizeof(unsigned long long) * 4 * n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" long sa_conv2d_k3_wino4_stat_parts(int H, int W) {
   const int ltw = w4_ltw(H, W), bw = 4 << ltw, bh = 4 * (64 >> ltw);
