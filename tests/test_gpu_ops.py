@@ -261,6 +261,16 @@ def test_gru_gates_and_plumbing(H, W):
     ops.interp(y, buf[:, :C])
     torch.testing.assert_close(buf[:, :C], torch.nn.functional.interpolate(y, (9, 12), mode="bilinear",
                                                                            align_corners=True), atol=1e-6, rtol=0)
+    # the update block's map sizes (pool2x: the 4-wide float4 variant, W % 8 == 0)
+    for (hi, wi), (ho, wo) in (((136, 240), (68, 120)), ((68, 120), (34, 60))):
+        xs = g(rng.standard_normal((B, C, hi, wi)))
+        pooled = torch.zeros(B, 2 * C, ho, wo, device=dev)
+        ops.pool2x(xs, pooled[:, C:])
+        torch.testing.assert_close(pooled[:, C:], torch.nn.functional.avg_pool2d(xs, 3, 2, 1), atol=1e-6, rtol=0)
+        up = torch.zeros(B, 2 * C, hi, wi, device=dev)
+        ops.interp(pooled[:, C:], up[:, C:])
+        torch.testing.assert_close(up[:, C:], torch.nn.functional.interpolate(
+            pooled[:, C:], (hi, wi), mode="bilinear", align_corners=True), atol=1e-6, rtol=0)
     r = torch.empty(B, C, 17, 23, device=dev)
     ops.relu_copy(x, r)
     torch.testing.assert_close(r, torch.relu(x))
