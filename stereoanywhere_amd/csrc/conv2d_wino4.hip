@@ -116,6 +116,12 @@ __device__ __forceinline__ void bt6h(const float x0, const float x1, const float
   }
 }
 
+#ifdef SA_W4_CLOCK
+// diagnostic build only: per block (s_memtime, s_memrealtime) at the start and the end of wave 0,
+// then s_memtime after the first chunk's barrier and after the main loop
+__device__ unsigned long long g_w4_clock[65536][6];
+#endif
+
 template <int HF>
 __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, float *smem) {
   const int Cin = P.Cin, H = P.H, W = P.W, Cout = P.Cout;
@@ -202,17 +208,21 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
 #endif
 #ifndef SA_W4_DIAG
 #define SA_W4_DIAG 0   // timing diagnostics only (wrong results): 1 no DMA in the loop, 2 no
-                       // transform / MFMA, 3 no DMA and no barrier in the loop
+                       // transform / MFMA, 3 no DMA and no barrier in the loop, 4 as 3 and no
+                       // DMA at all
 #endif
 #ifndef SA_W4_PRIO
 #define SA_W4_PRIO 0
 #endif
   if (SA_W4_PRIO && HF == 1) __builtin_amdgcn_s_setprio(1);   // static priority for waves 4-7
-  issue(0, 0);
+  if (SA_W4_DIAG != 4) issue(0, 0);
 #pragma unroll 1
   for (int kc = 0; kc < nchunks; ++kc) {
     const int cur = kc & 1;
     if (SA_W4_DIAG < 3) __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
+#ifdef SA_W4_CLOCK
+    if (kc == 0 && HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][4] = __builtin_amdgcn_s_memtime();
+#endif
     if (SA_W4_DIAG == 2 || (SA_W4_DIAG == 0 && !SA_W4_SPREAD))
       if (kc + 1 < nchunks) issue(kc + 1, cur ^ 1);
     if (SA_W4_DIAG == 2) continue;
@@ -274,56 +284,58 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
     }
   }
   __syncthreads();
+#ifdef SA_W4_CLOCK
+  if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][5] = __builtin_amdgcn_s_memtime();
+#endif
 
   // ---- output transform.  Lane holds tiles tg * 16 + 4 (lane >> 4) + i of output channels
   // g * 16 + (lane & 15), points of columns 3 HF .. 3 HF + 2.  Y = A^T M A: the column-wise
-  // A^T runs per column, the row-wise A^T only over this half's columns (a partial sum).  Half
-  // 1 stages its partials in O[co][row][x] (one float4 per output row of a tile); half 0 adds
-  // its own, the bias and the ReLU.  Plane pitch OPP = 4 (mod 32) floats: the 8 lanes of a
-  // ds_write_b128 group (8 output channels) hit disjoint banks.
+  // A^T runs per column, the row-wise A^T only over this half's columns (a partial sum).  The
+  // halves meet in LDS, O[co][row][x] (one float4 per output row of a tile), balanced: in
+  // phase 0 each half stages its partials of the OTHER half's channel group (g = 1 - HF); in
+  // phase 1 it adds its own partials of group g = HF, the bias and the ReLU.  Plane pitch OPP =
+  // 4 (mod 32) floats: the 8 lanes of a ds_write_b128 group (8 output channels) hit disjoint
+  // banks.
   float *ot = smem;
   const int relu = P.relu;
 #pragma unroll
   for (int phase = 0; phase < 2; ++phase) {
-    if (phase == 1 - HF) {   // half 1 first
+    const int g = phase == 0 ? 1 - HF : HF;
+    const int col = g * 16 + (lane & 15);
+    const float bv = (phase == 1 && P.bias) ? P.bias[co0 + col] : 0.0f;
 #pragma unroll
-      for (int g = 0; g < 2; ++g) {
-        const int col = g * 16 + (lane & 15);
-        const float bv = (HF == 0 && P.bias) ? P.bias[co0 + col] : 0.0f;
+    for (int i = 0; i < 4; ++i) {
+      const int ti = tg * 16 + 4 * (lane >> 4) + i, orow = (ti >> ltw) * 4, ocol = (ti & (tw - 1)) * 4;
+      float u[4][3];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int ti = tg * 16 + 4 * (lane >> 4) + i, orow = (ti >> ltw) * 4, ocol = (ti & (tw - 1)) * 4;
-          float u[4][3];
+      for (int jj = 0; jj < 3; ++jj) {
+        float mcol[6], o[4];
 #pragma unroll
-          for (int jj = 0; jj < 3; ++jj) {
-            float mcol[6], o[4];
+        for (int a = 0; a < 6; ++a) mcol[a] = phase == 0 ? acc[a][jj][1 - HF][i] : acc[a][jj][HF][i];
+        at6(mcol, o);
 #pragma unroll
-            for (int a = 0; a < 6; ++a) mcol[a] = acc[a][jj][g][i];
-            at6(mcol, o);
+        for (int a = 0; a < 4; ++a) u[a][jj] = o[a];
+      }
 #pragma unroll
-            for (int a = 0; a < 4; ++a) u[a][jj] = o[a];
-          }
-#pragma unroll
-          for (int a = 0; a < 4; ++a) {
-            // A^T rows restricted to columns 0-2: [1,1,1] [0,1,-1] [0,1,1] [0,1,-1];
-            // columns 3-5: [1,1,0] [2,-2,0] [4,4,0] [8,-8,1]
-            f32x4 y;
-            if (HF == 0) {
-              const float p = u[a][1] + u[a][2], q = u[a][1] - u[a][2];
-              y = f32x4{u[a][0] + p, q, p, q};
-            } else {
-              const float p = u[a][0] + u[a][1], q = u[a][0] - u[a][1];
-              y = f32x4{p, 2.0f * q, 4.0f * p, 8.0f * q + u[a][2]};
-            }
-            f32x4 *o = reinterpret_cast<f32x4 *>(ot + col * OPP + (orow + a) * BW + ocol);
-            if (HF == 1) {
-              *o = y;
-            } else {
-              f32x4 v = (*o + y) + bv;
-              if (relu) v = f32x4{fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f)};
-              *o = v;
-            }
-          }
+      for (int a = 0; a < 4; ++a) {
+        // A^T rows restricted to columns 0-2: [1,1,1] [0,1,-1] [0,1,1] [0,1,-1];
+        // columns 3-5: [1,1,0] [2,-2,0] [4,4,0] [8,-8,1]
+        f32x4 y;
+        if (HF == 0) {
+          const float p = u[a][1] + u[a][2], q = u[a][1] - u[a][2];
+          y = f32x4{u[a][0] + p, q, p, q};
+        } else {
+          const float p = u[a][0] + u[a][1], q = u[a][0] - u[a][1];
+          y = f32x4{p, 2.0f * q, 4.0f * p, 8.0f * q + u[a][2]};
+        }
+        f32x4 *o = reinterpret_cast<f32x4 *>(ot + col * OPP + (orow + a) * BW + ocol);
+        if (phase == 0) {
+          *o = y;
+        } else {
+          // half 1's partial + half 0's: (p1 + p0) + bias for either finishing half
+          f32x4 v = (HF == 0 ? (*o + y) : (y + *o)) + bv;
+          if (relu) v = f32x4{fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f)};
+          *o = v;
         }
       }
     }
@@ -373,11 +385,6 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
           *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
   }
 }
-
-#ifdef SA_W4_CLOCK
-// diagnostic build only: per block (s_memtime, s_memrealtime) at the start and the end of wave 0
-__device__ unsigned long long g_w4_clock[65536][4];
-#endif
 
 __global__ __launch_bounds__(NTHR) void wino_f4k3_kernel(const W4Launch L) {
   // problem of the block from its raw id (ranges padded to multiples of 8: every XCD gets an
@@ -461,7 +468,7 @@ extern "C" int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, f
 
 #ifdef SA_W4_CLOCK
 extern "C" int sa_w4_clock_read(unsigned long long *out, int n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4_clock), sizeof(unsigned long long) * 4 * n) == hipSuccess ? 0 : -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4_clock), sizeof(unsigned long long) * 6 * n) == hipSuccess ? 0 : -1;
 }
 #endif
 
