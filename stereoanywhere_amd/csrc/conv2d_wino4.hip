@@ -28,6 +28,8 @@
 // lane that feeds it to its two MFMAs (about 2 VALU operations per MFMA).
 #include "sa_common.h"
 
+#include <cstdlib>
+
 #pragma clang fp contract(fast)
 
 namespace {
@@ -35,20 +37,33 @@ namespace {
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f32x2 = __attribute__((ext_vector_type(2))) float;
 
-constexpr int KC = 8;                     // input channels per chunk (two MFMA k-steps of 4)
 constexpr int NPT = 36;                   // transform points
 constexpr int CO = 32;                    // output channels per block
-constexpr int PS_MAX = 340;               // patch float4 groups per channel, largest geometry (10 x 34)
-constexpr int PBUF = (KC * PS_MAX + 32) * 4;   // floats per patch buffer (+ the last DMA's idle lanes)
-constexpr int UBUF = NPT * KC * CO;       // 9216 floats of filters per chunk
-constexpr int U_OFF = 2 * PBUF;
-constexpr int SMEM = 2 * PBUF + 2 * UBUF;
-constexpr int OPP = 64 * 16 + 4;          // output staging: channel-plane pitch (4 mod 32)
-constexpr int NWAVE = 8, NTHR = 64 * NWAVE;
-constexpr int PDMA = 6;                   // patch DMA wave-instructions per wave per chunk (<= ceil(43 / 8))
-constexpr int UDMA = UBUF / 256;          // 36 filter DMA wave-instructions (1 KiB each) per chunk
-static_assert(SMEM * 4 <= 160 * 1024, "LDS budget");
-static_assert(CO * OPP <= SMEM, "output staging fits");
+
+// Two block shapes of the same algorithm.  Large (the default): 8 waves, 64 tiles, 8-channel
+// chunks, one block per CU (158 KiB of LDS).  Small (SA_W4_SHAPE=small): 4 waves, 32 tiles,
+// 4-channel chunks, 66 KiB, two blocks per CU, so one block's first DMA wait and epilogue
+// overlap the other's MFMAs (per block ~6-8k cycles until the first chunk lands and ~9k of
+// epilogue around 6.8k per chunk, scripts/w4_clock.py); it is not faster in the forward.
+template <int NW_, int KC_>
+struct W4Cfg {
+  static constexpr int NW = NW_, NTHR = 64 * NW_, TG = NW_ / 2, NT = 16 * TG, KC = KC_, JPC = KC_ / 4;
+  static constexpr int PS_MAX = NT == 64 ? 340 : 204;       // (BH + 2)(BW / 4 + 2), largest geometry
+  static constexpr int PBUF = (KC * PS_MAX + 32) * 4;       // + the last DMA's idle lanes
+  static constexpr int UBUF = NPT * KC * CO;                // filters per chunk
+  static constexpr int BUF = PBUF + UBUF;                   // one buffer: patch, then filters
+  static constexpr int OPP = NT * 16 + 4;                   // output staging plane pitch (4 mod 32)
+  static constexpr int SMEM = 2 * BUF > CO * OPP ? 2 * BUF : CO * OPP;
+  static constexpr int PDMA = ((KC * PS_MAX + 63) / 64 + NW - 1) / NW;   // patch DMA pieces per wave
+  static constexpr int UDMA = UBUF / 256;                   // filter DMA pieces (1 KiB) per chunk
+  static constexpr int UPW = (UDMA + NW - 1) / NW;          // per wave
+  static_assert(SMEM * 4 <= 160 * 1024, "LDS budget");
+  static_assert(PDMA <= 6 && UPW <= 6, "three DMA parts of two pieces");
+  static_assert(OPP % 32 == 4, "conflict-free staging");
+};
+using W4Big = W4Cfg<8, 8>;
+using W4Small = W4Cfg<4, 4>;
+static_assert(2 * W4Small::SMEM * 4 <= 160 * 1024, "two small blocks per CU");
 
 struct W4Prob {
   const float *in;
@@ -119,13 +134,15 @@ __device__ __forceinline__ void bt6h(const float x0, const float x1, const float
 #ifdef SA_W4_CLOCK
 // diagnostic build only: per block (s_memtime, s_memrealtime) at the start and the end of wave 0,
 // then s_memtime after the first chunk's barrier and after the main loop
-__device__ unsigned long long g_w4_clock[65536][6];
+__device__ unsigned long long g_w4_clock[65536][8];
 #endif
 
-template <int HF>
+template <class C, int HF>
 __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, float *smem) {
+  constexpr int NWAVE = C::NW, NTHR = C::NTHR, KC = C::KC, JPC = C::JPC, NT = C::NT, PDMA = C::PDMA,
+                UDMA = C::UDMA, UPW = C::UPW, UBUF = C::UBUF, BUF = C::BUF, PBUF = C::PBUF, OPP = C::OPP;
   const int Cin = P.Cin, H = P.H, W = P.W, Cout = P.Cout;
-  const int ltw = P.ltw, tw = 1 << ltw, tr = 64 >> ltw;
+  const int ltw = P.ltw, tw = 1 << ltw, tr = NT >> ltw;
   const int BH = 4 * tr, BW = 4 * tw, PG = tw + 2, PR = BH + 2, PS = PR * PG;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -140,8 +157,17 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
 
   const __amdgpu_buffer_rsrc_t xin = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float *>(P.in + (long)n * P.in_bs), (short)0, Cin * hw * 4, 0x00020000);
+  // the filters' global layout has 8-channel chunks (sa_conv2d_wino4_weights); a 4-channel
+  // chunk is every other 512-byte piece of one (the DMA gathers it by its source addresses)
   const __amdgpu_buffer_rsrc_t uin = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float *>(P.U + (long)cb * nchunks * UBUF), (short)0, nchunks * UBUF * 4, 0x00020000);
+      const_cast<float *>(P.U + (long)cb * Cin * NPT * CO), (short)0, Cin * NPT * CO * 4, 0x00020000);
+  auto u_src = [&](int piece) {   // byte offset of this lane's 16 bytes of filter DMA piece `piece`
+    const int f = piece * 256 + lane * 4;
+    return (JPC == 2 ? f : f + (f >> 7) * 128) * 4;
+  };
+  auto u_chunk = [&](int chunk) {   // byte offset of a chunk's filters
+    return JPC == 2 ? chunk * UBUF * 4 : (chunk >> 1) * 2 * UBUF * 4 + (chunk & 1) * 512;
+  };
 
   // patch DMA: the chunk's image is [channel][PR rows][PG groups of 4 floats], dense, starting
   // at (y0 - 1, x0 - 4); wave-instruction gi fills groups 64 gi .. 64 gi + 63 (lane-linear)
@@ -155,37 +181,27 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
     const bool ok = s < KC * PS && y >= 0 && y < H && x >= 0 && x < W;
     po[j] = ok ? (ci * hw + y * W + x) * 4 : 0x7ffffff0;   // out of range: the load returns 0
   }
-  auto issue = [&](int chunk, int buf) __attribute__((always_inline)) {
-    float *pb = smem + buf * PBUF;
+  // the chunk's DMAs in three parts (part -1: all at once), spread over the first job's three
+  // column phases (each piece costs tens of issue cycles; clustered after the barrier they
+  // would delay the first reads)
+  auto issue_part = [&](int chunk, int buf, int part) __attribute__((always_inline)) {
+    float *pb = smem + buf * BUF;
     const int xs = chunk * KC * hw * 4;
 #pragma unroll
     for (int j = 0; j < PDMA; ++j)
-      if (wv + NWAVE * j < npi) dma16(xin, pb + (wv + NWAVE * j) * 256, po[j], xs);
-    float *ub = smem + U_OFF + buf * UBUF;
-    const int us = chunk * UBUF * 4;
+      if ((part < 0 || j / 2 == part) && wv + NWAVE * j < npi) dma16(xin, pb + (wv + NWAVE * j) * 256, po[j], xs);
+    float *ub = pb + PBUF;
+    const int us = u_chunk(chunk);
 #pragma unroll
-    for (int j = 0; j < (UDMA + NWAVE - 1) / NWAVE; ++j)
-      if (wv + NWAVE * j < UDMA) dma16(uin, ub + (wv + NWAVE * j) * 256, ((wv + NWAVE * j) * 64 + lane) * 16, us);
+    for (int j = 0; j < UPW; ++j)
+      if ((part < 0 || j / 2 == part) && wv + NWAVE * j < UDMA)
+        dma16(uin, ub + (wv + NWAVE * j) * 256, u_src(wv + NWAVE * j), us);
   };
-  // the same DMAs in three parts, spread over the first job's three column phases (each piece
-  // costs tens of issue cycles; clustered after the barrier they would delay the first reads)
-  auto issue_part = [&](int chunk, int buf, int part) __attribute__((always_inline)) {
-    float *pb = smem + buf * PBUF;
-    const int xs = chunk * KC * hw * 4;
-#pragma unroll
-    for (int j = 2 * part; j < 2 * part + 2; ++j)
-      if (wv + NWAVE * j < npi) dma16(xin, pb + (wv + NWAVE * j) * 256, po[j], xs);
-    float *ub = smem + U_OFF + buf * UBUF;
-    const int us = chunk * UBUF * 4;
-#pragma unroll
-    for (int j = 2 * part; j < 2 * part + 2 && j < (UDMA + NWAVE - 1) / NWAVE; ++j)
-      if (wv + NWAVE * j < UDMA) dma16(uin, ub + (wv + NWAVE * j) * 256, ((wv + NWAVE * j) * 64 + lane) * 16, us);
-  };
-  static_assert(PDMA == 6 && (UDMA + NWAVE - 1) / NWAVE <= 6, "three DMA parts of two pieces");
+  auto issue = [&](int chunk, int buf) __attribute__((always_inline)) { issue_part(chunk, buf, -1); };
 
   // lane roles: MFMA A operand A[m][k] = (tile m, channel k); B operands B[k][n] = (channel k,
   // output channel n of each 16-channel half)
-  const int tg = wv & 3;
+  const int tg = wv % C::TG;
   const int k = lane >> 4, m = lane & 15;
   const int tidx = tg * 16 + m, trow = tidx >> ltw, tcol = tidx & (tw - 1);
   // patch row 0 of the tile (input row y0 + 4 trow - 1), columns 4 tcol + 2 .. 4 tcol + 9
@@ -226,8 +242,8 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
     if (SA_W4_DIAG == 2 || (SA_W4_DIAG == 0 && !SA_W4_SPREAD))
       if (kc + 1 < nchunks) issue(kc + 1, cur ^ 1);
     if (SA_W4_DIAG == 2) continue;
-    const float *pb = smem + cur * PBUF + pread;
-    const float *ub = smem + U_OFF + cur * UBUF + uread;
+    const float *pb = smem + cur * BUF + pread;
+    const float *ub = smem + cur * BUF + PBUF + uread;
     // Per job s (channel k, then k + 4) the lane reads its tile's 6 patch rows (8 floats each;
     // the inputs are a.y, b.xyzw, c.x), runs its half of the row pass t[r][jj] =
     // (B^T d_r)[3 HF + jj], then 3 column passes V[i][3 HF + jj] = (B^T t)[i][jj] that feed
@@ -248,20 +264,20 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
     f32x2 bc[6], bn[6];
     auto load_b = [&](int s, int jj, f32x2 *b) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < 6; ++i) b[i] = *reinterpret_cast<const f32x2 *>(ub + ((6 * i + 3 * HF + jj) * 2 + s) * 4 * 32);
+      for (int i = 0; i < 6; ++i) b[i] = *reinterpret_cast<const f32x2 *>(ub + ((6 * i + 3 * HF + jj) * JPC + s) * 4 * 32);
     };
     load_rows(0, 0, 6);
     load_b(0, 0, bc);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < JPC; ++s) {
       if (s == 1) load_rows(1, 3, 6);
       float t[6][3];
 #pragma unroll
       for (int r = 0; r < 6; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t[r]);
-      if (s == 0) load_rows(1, 0, 3);
+      if (s + 1 < JPC) load_rows(1, 0, 3);
 #pragma unroll
       for (int jj = 0; jj < 3; ++jj) {
-        if (s == 0 || jj < 2) load_b(jj < 2 ? s : s + 1, jj < 2 ? jj + 1 : 0, bn);
+        if (s + 1 < JPC || jj < 2) load_b(jj < 2 ? s : s + 1, jj < 2 ? jj + 1 : 0, bn);
         float v[6];
         bt6(t[0][jj], t[1][jj], t[2][jj], t[3][jj], t[4][jj], t[5][jj], v);
 #pragma unroll
@@ -341,16 +357,22 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
     }
     if (phase == 0) __syncthreads();
   }
+#ifdef SA_W4_CLOCK
+  if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][6] = __builtin_amdgcn_s_memtime();
+#endif
   __syncthreads();
   const int lbw = ltw + 2;   // log2 BW
   if (P.partial) {
-    // InstanceNorm partials of the block: 16 threads per channel, each over 64 consecutive
-    // pixels of the channel's plane, fixed-order reduction
-    constexpr int TPC = NTHR / CO, PPT = 64 * 16 / TPC;
-    const int c = tid / TPC, part = tid % TPC;
+    // InstanceNorm partials, indexed by the small blocks' tiling (BH rows of a large block = 2
+    // small tiles), so both block shapes fill the same [N * Cout][parts][2] array: TPC threads
+    // per (channel, small tile), each over consecutive pixels of it, fixed-order reduction
+    constexpr int NSUB = NT / 32, TPC = NTHR / (CO * NSUB), PPT = 32 * 16 / TPC;
+    const int c = tid / (TPC * NSUB), sub = (tid / TPC) % NSUB, part = tid % TPC;
+    const int sub_rows = BH / NSUB, fine_h = (H + sub_rows - 1) / sub_rows;
+    const int frow = (st / tiles_w) * NSUB + sub;
     double ssum = 0.0, ssq = 0.0;
 #pragma unroll 2
-    for (int p = part * PPT; p < (part + 1) * PPT; p += 4) {
+    for (int p = sub * 512 + part * PPT; p < sub * 512 + (part + 1) * PPT; p += 4) {
       const int r = p >> lbw, cx = p & (BW - 1);
       if (y0 + r < H && x0 + cx < W) {   // W % 4 == 0: a float4 is wholly inside or outside
         const f32x4 v = *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
@@ -367,18 +389,22 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
       ssum += __shfl_xor(ssum, o);
       ssq += __shfl_xor(ssq, o);
     }
-    if (part == 0) {
-      double *pp = P.partial + (((long)n * Cout + co0 + c) * tiles_hw + st) * 2;
+    if (part == 0 && frow < fine_h) {
+      const long fst = (long)frow * tiles_w + st % tiles_w;
+      double *pp = P.partial + (((long)n * Cout + co0 + c) * ((long)fine_h * tiles_w) + fst) * 2;
       pp[0] = ssum;
       pp[1] = ssq;
     }
   }
-  // float4 stores: 256 per channel plane of the block
+#ifdef SA_W4_CLOCK
+  if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][7] = __builtin_amdgcn_s_memtime();
+#endif
+  // float4 stores: NT * 4 per channel plane of the block
   float *dst = P.out + (long)n * P.out_bs;
 #pragma unroll 4
-  for (int j = 0; j < (CO * 64 * 16) / (4 * NTHR); ++j) {
+  for (int j = 0; j < (CO * NT * 16) / (4 * NTHR); ++j) {
     const int i4 = tid + NTHR * j;
-    const int c = i4 >> 8, p = (i4 & 255) * 4, r = p >> lbw, cx = p & (BW - 1);
+    const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
     const int y = y0 + r, x = x0 + cx;
     if (y < H && x < W)
       *reinterpret_cast<f32x4 *>(dst + (long)(co0 + c) * hw + (long)y * W + x) =
@@ -386,7 +412,8 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
   }
 }
 
-__global__ __launch_bounds__(NTHR) void wino_f4k3_kernel(const W4Launch L) {
+template <class C>
+__global__ __launch_bounds__(C::NTHR, C::NW == 8 ? 1 : 2) void wino_f4k3_kernel(const W4Launch L) {
   // problem of the block from its raw id (ranges padded to multiples of 8: every XCD gets an
   // equal share of each problem), then the L2-locality remap within it (conv2d_wino.hip)
   const unsigned g = blockIdx.x;
@@ -401,15 +428,15 @@ __global__ __launch_bounds__(NTHR) void wino_f4k3_kernel(const W4Launch L) {
     }
   }
   if (g - base >= nb) return;
-  __shared__ __attribute__((aligned(16))) float smem[SMEM];
+  __shared__ __attribute__((aligned(16))) float smem[C::SMEM];
 #ifdef SA_W4_CLOCK
   unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  // waves 0-3 take point columns 0-2, waves 4-7 columns 3-5 (wave-uniform branch)
-  if (threadIdx.x < 256)
-    w4_body<0>(P, sa::xcd_remap(g - base, nb), smem);
+  // the first half of the waves takes point columns 0-2, the second half 3-5 (wave-uniform)
+  if (threadIdx.x < C::NTHR / 2)
+    w4_body<C, 0>(P, sa::xcd_remap(g - base, nb), smem);
   else
-    w4_body<1>(P, sa::xcd_remap(g - base, nb), smem);
+    w4_body<C, 1>(P, sa::xcd_remap(g - base, nb), smem);
 #ifdef SA_W4_CLOCK
   if (threadIdx.x == 0 && g < 65536) {
     g_w4_clock[g][0] = t0;
@@ -444,7 +471,7 @@ __global__ __launch_bounds__(256) void wino4_weights_kernel(const float *__restr
     for (int b = 0; b < 6; ++b) {
       const double u = t[a][0] * G[b][0] + t[a][1] * G[b][1] + t[a][2] * G[b][2];
       const int pt = 6 * a + b;
-      U[(((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 2 + s) * 4 + k) * 32 + (c & 15) * 2 + (c >> 4)] = (float)u;
+      U[(((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 2 + s) * 4 + k) * CO + (c & 15) * 2 + (c >> 4)] = (float)u;
     }
 }
 
@@ -468,23 +495,33 @@ extern "C" int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, f
 
 #ifdef SA_W4_CLOCK
 extern "C" int sa_w4_clock_read(unsigned long long *out, int n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4_clock), sizeof(unsigned long long) * 6 * n) == hipSuccess ? 0 : -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4_clock), sizeof(unsigned long long) * 8 * n) == hipSuccess ? 0 : -1;
 }
 #endif
 
+// InstanceNorm partial count: the small blocks' tiling (a large block writes its two halves)
 extern "C" long sa_conv2d_k3_wino4_stat_parts(int H, int W) {
-  const int ltw = w4_ltw(H, W), bw = 4 << ltw, bh = 4 * (64 >> ltw);
+  const int ltw = w4_ltw(H, W), bw = 4 << ltw, bh = 4 * (32 >> ltw);
   return (long)((W + bw - 1) / bw) * ((H + bh - 1) / bh);
 }
 
 extern "C" int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, void *stream) {
   SA_REQUIRE(nprob >= 1 && nprob <= MAX_PROB && probs, "sa_conv2d_k3_wino4_multi: 1..%d problems", MAX_PROB);
+  static const int shape = [] {   // SA_W4_SHAPE=big|small forces one block shape (A/B runs)
+    const char *e = getenv("SA_W4_SHAPE");
+    return e && e[0] == 's' ? 2 : e && e[0] == 'b' ? 1 : 0;
+  }();
+  // Large blocks by default.  The small shape measured 2-8% faster on standalone launches of
+  // Cin <= 128 with a few rounds of blocks (qh08, convc2) but not faster in the forward (91.7
+  // vs 91.0 ms/step with it on those launches), so it is an A/B option only.
+  const bool small = shape == 2;
+  const int nt = small ? W4Small::NT : W4Big::NT;
   W4Launch L{};
   long total = 0;
   for (int i = 0; i < nprob; ++i) {
     const SaWinoProblem &q = probs[i];
     SA_REQUIRE(q.in && q.U && q.out && q.N > 0 && q.H > 0 && q.W > 0, "sa_conv2d_k3_wino4: bad arguments");
-    SA_REQUIRE(q.Cin % KC == 0 && q.Cout % CO == 0,
+    SA_REQUIRE(q.Cin % 8 == 0 && q.Cout % CO == 0,
                "sa_conv2d_k3_wino4: needs Cin %% 8 == 0 and Cout %% 32 == 0 (got %d, %d)", q.Cin, q.Cout);
     SA_REQUIRE(q.W % 4 == 0 && (reinterpret_cast<uintptr_t>(q.in) & 15) == 0 && q.in_bs % 4 == 0 &&
                    (reinterpret_cast<uintptr_t>(q.out) & 15) == 0 && q.out_bs % 4 == 0 &&
@@ -493,7 +530,7 @@ extern "C" int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, v
     SA_REQUIRE(!q.in_m && !q.in_s && !q.in_t && !q.in_act, "sa_conv2d_k3_wino4: no input transform");
     SA_REQUIRE((long)q.Cin * q.H * q.W * 4 < (1L << 31) - 64 && 36L * q.Cin * q.Cout * 4 < (1L << 31),
                "sa_conv2d_k3_wino4: an image or the filter bank exceeds the 2 GB buffer-descriptor range");
-    const int ltw = w4_ltw(q.H, q.W), bw = 4 << ltw, bh = 4 * (64 >> ltw);
+    const int ltw = w4_ltw(q.H, q.W), bw = 4 << ltw, bh = 4 * (nt >> ltw);
     const int tiles_w = (q.W + bw - 1) / bw, tiles_h = (q.H + bh - 1) / bh;
     L.p[i] = W4Prob{q.in, q.in_bs, q.Cin, q.H, q.W, q.U, q.Cout, q.bias, q.relu, q.out, q.out_bs,
                     ltw, tiles_w, tiles_w * tiles_h, q.Cout / CO, q.stats_partial};
@@ -510,6 +547,9 @@ extern "C" int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, v
   L.nprob = nprob;
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV2D_W4, s);
-  wino_f4k3_kernel<<<(unsigned)total, NTHR, 0, s>>>(L);
+  if (small)
+    wino_f4k3_kernel<W4Small><<<(unsigned)total, W4Small::NTHR, 0, s>>>(L);
+  else
+    wino_f4k3_kernel<W4Big><<<(unsigned)total, W4Big::NTHR, 0, s>>>(L);
   return sa::check_launch("sa_conv2d_k3_wino4");
 }
