@@ -172,6 +172,37 @@ def residual_block(blk: nn.Module, name: str, x: torch.Tensor, fin: _Finisher) -
                         out=c2)
 
 
+def residual_blocks_grouped(blks, names, xs, fin: _Finisher) -> List[torch.Tensor]:
+    """Independent stride-1 residual blocks without downsample (the context encoder's heads,
+    extractor.py:232-244): each conv stage of all of them in one conv2d_k3_multi launch (fuller
+    launches than one block at a time), the same ops per block as residual_block."""
+    if not all(b.conv1.weight.data_ptr() in _WINO and b.conv2.weight.data_ptr() in _WINO
+               and b.downsample is None and b.conv1.stride == (1, 1) for b in blks):
+        return [residual_block(b, n, x, fin) for b, n, x in zip(blks, names, xs)]
+
+    def stage(convs, inputs, affs):
+        Us = [_WINO[c.weight.data_ptr()] for c in convs]
+        if affs[0] is not None and ops.wino4_applies(inputs[0], Us[0], *zip(inputs[1:], Us[1:])):
+            inputs = [ops.norm_act(x, a, act_in="relu", out=x) for x, a in zip(inputs, affs)]
+            affs = [None] * len(affs)
+        res = ops.conv2d_k3_multi(*[dict(x=x, U=U, in_aff=a, in_act="relu" if a is not None else None,
+                                         stats=fin.instance) for x, U, a in zip(inputs, Us, affs)])
+        return [r if fin.instance else (r, None) for r in res]
+
+    r1 = stage([b.conv1 for b in blks], list(xs), [None] * len(blks))
+    a1 = [fin.affine(n + ".norm1", c, st) for n, (c, st) in zip(names, r1)]
+    r2 = stage([b.conv2 for b in blks], [c for c, _ in r1], a1)
+    return [ops.norm_act(c2, fin.affine(n + ".norm2", c2, s2), act_in="relu", skip=x, act_out="relu", out=c2)
+            for n, (c2, s2), x in zip(names, r2, xs)]
+
+
+def _convs_grouped(convs, xs) -> List[torch.Tensor]:
+    """Bias-free convs of independent inputs: one launch where all qualify for Winograd."""
+    if all(c.weight.data_ptr() in _WINO for c in convs):
+        return ops.conv2d_k3_multi(*[dict(x=x, U=_WINO[c.weight.data_ptr()]) for c, x in zip(convs, xs)])
+    return [_conv(x, c) for c, x in zip(convs, xs)]
+
+
 def _stem(enc: nn.Module, x: torch.Tensor, fin: _Finisher) -> torch.Tensor:
     direct = _DIRECT.get(enc.conv1.weight.data_ptr())
     stats = None
@@ -222,12 +253,14 @@ def cnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
     s16 = _stage(enc.layer4, "layer4", s08, fin)
     s32 = _stage(enc.layer5, "layer5", s16, fin)
 
-    def head(seq, i, name, feat):
-        r = residual_block(seq[0], f"{name}.{i}.0", feat, fin)
-        return _conv(r, seq[1])
-    return [[head(f, i, "outputs08", s08) for i, f in enumerate(enc.outputs08)],
-            [head(f, i, "outputs16", s16) for i, f in enumerate(enc.outputs16)],
-            [_conv(s32, f) for f in enc.outputs32]]
+    def heads(seqs, name, feat):
+        # the heads of one level (hidden state, context) read the same features: each of their
+        # conv stages runs as one launch
+        rs = residual_blocks_grouped([q[0] for q in seqs], [f"{name}.{i}.0" for i in range(len(seqs))],
+                                     [feat] * len(seqs), fin)
+        return _convs_grouped([q[1] for q in seqs], rs)
+    return [heads(enc.outputs08, "outputs08", s08), heads(enc.outputs16, "outputs16", s16),
+            _convs_grouped(list(enc.outputs32), [s32] * len(enc.outputs32))]
 
 
 def bn_table(enc: nn.Module) -> Dict[str, ops.Affine]:

@@ -208,11 +208,13 @@ class StereoAnywhere(nn.Module):
             fm = self.fnet(torch.cat([image2, image3], 0))
         else:
             cl = encoders.cnet_forward(self.cnet, mde2.repeat(1, 3, 1, 1), dw["bn_cnet"], dw["wino"], dw["direct"])
-            hid, ctx = [], []
-            for (h_raw, c_raw), (hb, cb), conv, U in zip(cl, dw["head_b"], self.context_zqr_convs, dw["U_ctx"]):
+            hid, cs = [], []
+            for (h_raw, c_raw), (hb, cb) in zip(cl, dw["head_b"]):
                 hid.append(ops.norm_act(h_raw, ops.Affine(t=hb), act_in="tanh", out=h_raw))
-                c = ops.norm_act(c_raw, ops.Affine(t=cb), act_in="relu", out=c_raw)
-                ctx.append(ops.conv2d_k3(c, U, conv.bias))  # [B,384,..]
+                cs.append(ops.norm_act(c_raw, ops.Affine(t=cb), act_in="relu", out=c_raw))
+            # the three context_zqr convs ([B,384,..] per level) in one launch
+            ctx = ops.conv2d_k3_multi(*[dict(x=c, U=U, bias=conv.bias)
+                                        for c, U, conv in zip(cs, dw["U_ctx"], self.context_zqr_convs)])
             fm = encoders.fnet_forward(self.fnet, torch.cat([image2, image3], 0), dw["bn_fnet"], dw["wino"],
                                        dw["direct"])
         fmap2, fmap3 = fm[:B].contiguous(), fm[B:].contiguous()

@@ -565,9 +565,12 @@ def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] 
     return prob, fin
 
 
-def wino4_applies(x: torch.Tensor, U: "WinoFilters") -> bool:
-    """Whether a conv2d_k3 of x without an input transform runs on the F(4x4,3x3) kernel."""
-    return _WINO4 and _wino4_ok(x) and _wino4_blocks(x, U) >= _WINO4_MIN_BLOCKS
+def wino4_applies(x: torch.Tensor, U: "WinoFilters", *more) -> bool:
+    """Whether conv2d_k3 of x (and of the further (x, U) pairs in ``more``, in one
+    conv2d_k3_multi launch) without an input transform runs on the F(4x4,3x3) kernel."""
+    pairs = [(x, U)] + list(more)
+    return (_WINO4 and all(_wino4_ok(a) for a, _ in pairs)
+            and sum(_wino4_blocks(a, u) for a, u in pairs) >= _WINO4_MIN_BLOCKS)
 
 
 def conv2d_k3_multi(*problems) -> list:
