@@ -7,12 +7,16 @@
 //   C = 1 - (-sum p log2(p + 1e-6)) / log2(W).
 // p is formed like ATen's CPU softmax: e = exp(x - max), p = e * (1 / sum e).
 //
-// Each output reduces one line of the volume.  If that line is contiguous (stride 1)
-// one wave owns it and the lanes stride along it (wave shuffles for the reductions);
-// otherwise one thread owns it and consecutive threads own consecutive (contiguous)
-// lines, so every load instruction of the wave is still one coalesced row segment.
-// Two passes per line (max/sum, then p-weighted sums) — the second is an L2 hit.
+// Each output reduces one line of the volume, read from HBM once and held in registers
+// while the max, the sum of exponentials and the p-weighted sum are formed:
+//   sam_row_kernel — the line is contiguous (stride 1): one wave per line, up to 4
+//     elements per lane (one float4 where aligned), wave shuffles for the reductions;
+//   sam_col_kernel — the line is strided: a lane per line, consecutive lanes on
+//     consecutive (contiguous) lines so each load is one coalesced row segment, and the
+//     block's 4 waves split the line's length (partials combined through LDS).
+// Lines longer than 256 take the generic kernels below them (re-read per pass).
 #include <cmath>
+#include <cstdint>
 
 #include "sa_common.h"
 
@@ -44,6 +48,126 @@ struct LineJob {
   float *out;
   int mode;
 };
+
+constexpr int SAM_NMAX = 256;  // register-resident line length limit
+
+__device__ __forceinline__ float sam_final(int mode, int left, int o, float acc, const SGeo &g) {
+  if (mode == 0) return left ? ((float)o - acc) : (acc - (float)o);
+  return 1.0f - (-acc) / (left ? g.log2W2 : g.log2W1);
+}
+
+// one wave per contiguous line of n <= 256 elements; V4: element 4*lane+i (float4 loads),
+// else element lane+64*i
+template <bool V4>
+__global__ __launch_bounds__(256) void sam_row_kernel(LineJob jd, LineJob jc, SGeo g, int left, long nlines) {
+  const long line = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (line >= nlines) return;
+  const int lane = threadIdx.x & 63;
+  const int nout = left ? g.W1 : g.W2;
+  const int n = left ? g.W2 : g.W1;
+  const long bh = line / nout;
+  const int o = (int)(line % nout);
+  const long b = bh / g.H, h = bh % g.H;
+  const long base = b * g.sb + h * g.sh + (long)o * (left ? g.sj : g.sk);
+  const LineJob jobs[2] = {jd, jc};
+  float v[2][4];
+  int idx[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) idx[i] = V4 ? 4 * lane + i : lane + 64 * i;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (!jobs[q].vol) continue;
+    const float *src = jobs[q].vol + base;
+    if (V4) {
+      if (4 * lane < n) {
+        const float4 t = *reinterpret_cast<const float4 *>(src + 4 * lane);
+        v[q][0] = t.x, v[q][1] = t.y, v[q][2] = t.z, v[q][3] = t.w;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[q][i] = -INFINITY;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[q][i] = idx[i] < n ? src[idx[i]] : -INFINITY;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const LineJob &J = jobs[q];
+    if (!J.vol) continue;
+    const float m = wave_max(fmaxf(fmaxf(v[q][0], v[q][1]), fmaxf(v[q][2], v[q][3])));
+    float e[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) e[i] = idx[i] < n ? expf(v[q][i] - m) : 0.f;
+    const float inv = 1.0f / wave_sum((e[0] + e[1]) + (e[2] + e[3]));
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float p = e[i] * inv;
+      if (idx[i] < n) acc += J.mode == 0 ? p * (float)idx[i] : p * log2f(p + 1e-6f);
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) J.out[b * g.obs + h * nout + o] = sam_final(J.mode, left, o, acc, g);
+  }
+}
+
+// a lane per strided line of n <= 256 elements, 64 lines per block; wave w holds the
+// line's elements [w*per, (w+1)*per), per = ceil(n/4) <= 64
+__global__ __launch_bounds__(256) void sam_col_kernel(LineJob jd, LineJob jc, SGeo g, int left, long nlines) {
+  __shared__ float red[3][4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long line = (long)blockIdx.x * 64 + lane;
+  const bool valid = line < nlines;
+  const int nout = left ? g.W1 : g.W2;
+  const int n = left ? g.W2 : g.W1;
+  const long es = left ? g.sk : g.sj;
+  const long bh = valid ? line / nout : 0;
+  const int o = valid ? (int)(line % nout) : 0;
+  const long b = bh / g.H, h = bh % g.H;
+  const int per = (n + 3) >> 2, k0 = w * per;
+  const int cnt = valid ? max(0, min(per, n - k0)) : 0;
+  const long base = b * g.sb + h * g.sh + (long)o * (left ? g.sj : g.sk) + (long)k0 * es;
+  const LineJob jobs[2] = {jd, jc};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const LineJob &J = jobs[q];
+    if (!J.vol) continue;
+    const float *src = J.vol + base;
+    float v[64];
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      v[i] = i < cnt ? src[(long)i * es] : -INFINITY;
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) m = fmaxf(m, v[i]);
+    red[0][w][lane] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0][0][lane], red[0][1][lane]), fmaxf(red[0][2][lane], red[0][3][lane]));
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      v[i] = i < cnt ? expf(v[i] - m) : 0.f;
+      s += v[i];
+    }
+    red[1][w][lane] = s;
+    __syncthreads();
+    const float inv = 1.0f / ((red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]));
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      const float p = v[i] * inv;
+      if (i < cnt) acc += J.mode == 0 ? p * (float)(k0 + i) : p * log2f(p + 1e-6f);
+    }
+    red[2][w][lane] = acc;
+    __syncthreads();
+    if (w == 0 && valid) {
+      acc = (red[2][0][lane] + red[2][1][lane]) + (red[2][2][lane] + red[2][3][lane]);
+      J.out[b * g.obs + h * nout + o] = sam_final(J.mode, left, o, acc, g);
+    }
+    __syncthreads();  // red is reused by the next volume
+  }
+}
 
 // one wave per line (contiguous reduction axis)
 __global__ __launch_bounds__(256) void sam_contig_kernel(LineJob jd, LineJob jc, SGeo g, int left,
@@ -131,7 +255,19 @@ __global__ __launch_bounds__(256) void sam_strided_kernel(LineJob jd, LineJob jc
 int launch_side(LineJob jd, LineJob jc, const SGeo &g, int B, int left, hipStream_t s) {
   const long nlines = (long)B * g.H * (left ? g.W1 : g.W2);
   const long red_stride = left ? g.sk : g.sj;
-  if (red_stride == 1) {
+  const int n = left ? g.W2 : g.W1;
+  if (n <= SAM_NMAX) {
+    if (red_stride == 1) {
+      // float4 rows: every line start 16-byte aligned
+      auto al = [](const float *p) { return !p || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+      const long os = left ? g.sj : g.sk;
+      const bool v4 = n % 4 == 0 && g.sb % 4 == 0 && g.sh % 4 == 0 && os % 4 == 0 && al(jd.vol) && al(jc.vol);
+      if (v4) sam_row_kernel<true><<<(unsigned)((nlines + 3) / 4), 256, 0, s>>>(jd, jc, g, left, nlines);
+      else sam_row_kernel<false><<<(unsigned)((nlines + 3) / 4), 256, 0, s>>>(jd, jc, g, left, nlines);
+    } else {
+      sam_col_kernel<<<(unsigned)((nlines + 63) / 64), 256, 0, s>>>(jd, jc, g, left, nlines);
+    }
+  } else if (red_stride == 1) {
     sam_contig_kernel<<<(unsigned)((nlines + 3) / 4), 256, 0, s>>>(jd, jc, g, left, nlines);
   } else {
     sam_strided_kernel<<<(unsigned)((nlines + 255) / 256), 256, 0, s>>>(jd, jc, g, left, nlines);

@@ -177,6 +177,30 @@ def test_softargmin_confidence(micro, layout):
     np.testing.assert_allclose(cf[:, 1:2], micro["conf.right"], atol=2e-6)
 
 
+@pytest.mark.parametrize("n", [64, 240, 250, 300])
+@pytest.mark.parametrize("layout", ["reference", "native"])
+def test_softargmin_confidence_lines(n, layout):
+    """Register-resident kernels (line length <= 256: float4 rows, ragged rows, strided
+    columns split over 4 waves) and the generic ones (n = 300), on two different volumes
+    that are channel views of one tensor, as the model passes them."""
+    rng = np.random.default_rng(n)
+    B, H = 2, 3
+    vols = (rng.standard_normal((B, 2, H, n, n)) * 4).astype(np.float32)  # [B,2,H,W1,W2]
+    if layout == "reference":
+        t = g(vols)
+        strides = (2 * H * n * n, n * n, n, 1)
+    else:
+        t = g(vols.transpose(0, 1, 4, 2, 3))  # [B,2,W2,H,W1]
+        strides = (2 * n * H * n, n, 1, H * n)
+    d, cf = ops.softargmin_conf(t[:, 0], t[:, 1], strides, (B, H, n, n))
+    d, cf = c(d), c(cf)
+    vd, vc = vols[:, 0], vols[:, 1]
+    np.testing.assert_allclose(d[:, 0:1], R.estimate_left_disparity(vd), atol=5e-4)
+    np.testing.assert_allclose(d[:, 1:2], R.estimate_right_disparity(vd), atol=5e-4)
+    np.testing.assert_allclose(cf[:, 0:1], R.estimate_left_confidence(vc), atol=2e-6)
+    np.testing.assert_allclose(cf[:, 1:2], R.estimate_right_confidence(vc), atol=2e-6)
+
+
 def test_softlrc(micro):
     d = np.concatenate([micro["lrc.d2"], micro["lrc.d3"]], 1)
     out = c(ops.softlrc_joint(g(d), None, 1.0))
