@@ -110,6 +110,13 @@ int sa_softlrc(const float *d2, const float *d3, const float *conf2, const float
 int sa_weighted_lsq(const float *mde, const float *disp, const float *conf, int B, int n_per_b,
                     float q_lo, float q_hi, float *scale, float *shift, void *stream);
 
+/* a7 — the same result spread over the whole GPU (n_per_b / 2048 blocks per sample, five
+ * launches: one per radix digit, then the normal equations).  ws: sa_weighted_lsq_ws_size
+ * bytes of device memory, 16-byte aligned, ZEROED before the call (left zeroed after it). */
+long sa_weighted_lsq_ws_size(int B, int n_per_b);
+int sa_weighted_lsq_ws(const float *mde, const float *disp, const float *conf, int B, int n_per_b,
+                       float q_lo, float q_hi, float *scale, float *shift, void *ws, void *stream);
+
 /* a7 + a8 + a11 — scaled mono (stereoanywhere.py:194-197), its softLRC (199), the mirror
  * detector (utils.py:255-269) and the initial coordinates (stereoanywhere.py:261-262):
  *   sm2 = scale*m2 + shift, sm3 = scale*m3 + shift                     [B,1,H,W]

@@ -44,6 +44,8 @@ SIGNATURES = {
     "sa_softargmin_conf": (I, [P, P, I, I, I, I, L, L, L, L, P, P, P, P, L, P]),
     "sa_softlrc": (I, [P, P, P, P, I, I, I, L, F, P, P, P]),
     "sa_weighted_lsq": (I, [P, P, P, I, I, F, F, P, P, P]),
+    "sa_weighted_lsq_ws_size": (L, [I, I]),
+    "sa_weighted_lsq_ws": (I, [P, P, P, I, I, F, F, P, P, P, P]),
     "sa_mono_scale_mirror": (I, [P, P, P, P, P, P, I, I, I, L, F, F, P, P, P, P, P]),
     "sa_gru_zr": (I, [P, L, P, P, L, P, P, L, P, L, I, I, I, P, P, P]),
     "sa_gru_out": (I, [P, L, P, P, L, P, L, P, I, I, I, P, L, P]),

@@ -12,6 +12,7 @@
 // non-negative, so their bit patterns order like the values), then accumulates the
 // 2x2 weighted normal equations in float64 and solves them — no host round trip.
 #include <cmath>
+#include <cstdint>
 
 #include "sa_common.h"
 
@@ -102,6 +103,28 @@ __device__ __forceinline__ double block_sum(double v, double *red) {
   return t;
 }
 
+// LDS histogram add of one key per lane.  Keys of a wave often share a few bins (the
+// high digits: sign and exponent; clustered values): the lanes of each of the first few
+// distinct bins are counted with one atomic of their number instead of a many-way
+// same-address conflict; lanes left after that add one each.
+__device__ __forceinline__ void hist_add(unsigned *h, unsigned bin, bool count) {
+  unsigned long long act = __ballot(count);
+  const unsigned long long me = 1ull << (threadIdx.x & 63);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    if (!act) return;
+    const int leader = __ffsll((long long)act) - 1;
+    const unsigned lb = __shfl(bin, leader);
+    const unsigned long long same = __ballot((act & me) && bin == lb);
+    if ((int)(threadIdx.x & 63) == leader) atomicAdd(&h[lb], (unsigned)__popcll(same));
+    act &= ~same;
+  }
+  if (act & me) atomicAdd(&h[bin], 1u);
+}
+
+// KPT > 0: the sample's keys (n <= KPT * LSQ_THREADS) stay in registers over the four
+// radix passes; KPT == 0: they are re-read from memory each pass.
+template <int KPT>
 __global__ __launch_bounds__(LSQ_THREADS) void lsq_kernel(const float *__restrict__ mde, const float *__restrict__ disp,
                                                           const float *__restrict__ conf, int n, float q_lo,
                                                           float q_hi, float *__restrict__ scale,
@@ -113,7 +136,16 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq_kernel(const float *__restric
   __shared__ float qv[2];
   const int b = blockIdx.x;
   const float *md = mde + (long)b * n, *dd = disp + (long)b * n, *cd = conf + (long)b * n;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+
+  unsigned keys[KPT > 0 ? KPT : 1];
+  if (KPT > 0) {
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      const int j = t + i * LSQ_THREADS;
+      keys[i] = j < n ? key_of(dd[j]) : 0u;
+    }
+  }
 
   // ranks of torch.quantile(linear): rank = q * (n - 1) in fp32
   const float r_lo = q_lo * (float)(n - 1), r_hi = q_hi * (float)(n - 1);
@@ -127,31 +159,62 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq_kernel(const float *__restric
     const int shift_ = 24 - 8 * pass;
     for (int i = t; i < 4 * 256; i += LSQ_THREADS) (&hist[0][0])[i] = 0u;
     __syncthreads();
+    // ranks whose selected prefix so far equals an earlier rank's share its histogram
     unsigned pre[4];
+    int src[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) pre[r] = prefix[r];
-    for (int i = t; i < n; i += LSQ_THREADS) {
-      const unsigned k = key_of(dd[i]);
+    for (int r = 0; r < 4; ++r) {
+      pre[r] = prefix[r];
+      src[r] = r;
+      for (int q = r - 1; q >= 0; --q)
+        if (pre[q] == pre[r]) src[r] = q;
+    }
+    auto count = [&](unsigned k, bool valid) {
       const unsigned bin = (k >> shift_) & 255u;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const bool match = pass == 0 || ((k ^ pre[r]) >> (shift_ + 8)) == 0u;
-        if (match) atomicAdd(&hist[r][bin], 1u);
+        if (src[r] != r) continue;  // uniform
+        const bool match = valid && (pass == 0 || ((k ^ pre[r]) >> (shift_ + 8)) == 0u);
+        hist_add(hist[r], bin, match);
+      }
+    };
+    if (KPT > 0) {
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) count(keys[i], t + i * LSQ_THREADS < n);
+    } else {
+      for (int i0 = 0; i0 < n; i0 += LSQ_THREADS) {
+        const int i = i0 + t;
+        count(i < n ? key_of(dd[i]) : 0u, i < n);
       }
     }
     __syncthreads();
-    if (t < 4) {
-      unsigned rem = remain[t], acc = 0u, sel = 255u;
-      for (unsigned bin = 0; bin < 256u; ++bin) {
-        const unsigned c = hist[t][bin];
-        if (acc + c > rem) {
-          sel = bin;
-          break;
-        }
-        acc += c;
+    if (wv < 4) {
+      // wave wv selects rank wv's digit: lane l owns bins 4l..4l+3; inclusive scan of the
+      // lane totals, the first lane whose running count passes the rank holds the digit
+      const unsigned *hr = hist[src[wv]];
+      const unsigned rem = remain[wv];
+      const unsigned c0 = hr[4 * lane], c1 = hr[4 * lane + 1], c2 = hr[4 * lane + 2], c3 = hr[4 * lane + 3];
+      unsigned inc = c0 + c1 + c2 + c3;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned u = __shfl_up(inc, o);
+        if (lane >= o) inc += u;
       }
-      remain[t] = rem - acc;
-      prefix[t] |= sel << shift_;
+      const unsigned long long past = __ballot(inc > rem);
+      const int L = past ? __ffsll((long long)past) - 1 : 63;
+      if (lane == L) {
+        unsigned acc = inc - (c0 + c1 + c2 + c3), sel = 4u * L + 3u;
+        const unsigned cs[4] = {c0, c1, c2, c3};
+        for (int k = 0; k < 4; ++k) {
+          if (acc + cs[k] > rem) {
+            sel = 4u * L + k;
+            break;
+          }
+          acc += cs[k];
+        }
+        remain[wv] = rem - acc;
+        prefix[wv] = pre[wv] | (sel << shift_);
+      }
     }
     __syncthreads();
   }
@@ -163,8 +226,8 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq_kernel(const float *__restric
   __syncthreads();
   const float qlo = qv[0], qhi = qv[1];
   double s11 = 0, s12 = 0, s22 = 0, t1 = 0, t2 = 0;
-  for (int i = t; i < n; i += LSQ_THREADS) {
-    const float d = __uint_as_float(key_of(dd[i]));
+  auto accum = [&](int i, unsigned k) {
+    const float d = __uint_as_float(k);
     if (qlo <= d && d <= qhi) {
       const float m = fabsf(md[i]);
       const float c = fabsf(cd[i]) * 0.9f + 0.1f;
@@ -176,6 +239,13 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq_kernel(const float *__restric
       t1 += (double)a1 * y;
       t2 += (double)w * y;
     }
+  };
+  if (KPT > 0) {
+#pragma unroll
+    for (int u = 0; u < KPT; ++u)
+      if (t + u * LSQ_THREADS < n) accum(t + u * LSQ_THREADS, keys[u]);
+  } else {
+    for (int i = t; i < n; i += LSQ_THREADS) accum(i, key_of(dd[i]));
   }
   s11 = block_sum(s11, red);
   s12 = block_sum(s12, red);
@@ -200,6 +270,192 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq_kernel(const float *__restric
     scale[b] = (float)sc;
     shift[b] = (float)sh;
   }
+}
+
+// ---------------------------------------------------- weighted LSQ, grid-wide variant
+// The same radix select and normal equations spread over LSQ_NB(n) blocks per sample:
+// one launch per 8-bit digit, each block histograms its slice in LDS and adds the
+// non-zero bins to the sample's global histogram; the block that finishes last (an
+// arrival counter) selects the digit for the next launch and clears the histogram.  The
+// final launch forms per-block float64 partials that the last block sums in block order
+// (deterministic) before solving.  Workspace per sample, zeroed before the first launch:
+//   LsqState (64 B) | hist[4][256] u32 | part[nb][5] f64.
+constexpr int LSQ_BT = 256, LSQ_EPT = 8, LSQ_CH = LSQ_BT * LSQ_EPT;
+
+struct LsqState {
+  unsigned prefix[4], remain[4], count, pad[7];
+};
+
+inline int lsq_nb(int n) { return (n + LSQ_CH - 1) / LSQ_CH; }
+inline long lsq_ws_stride(int n) { return ((64 + 4096 + (long)lsq_nb(n) * 40) + 255) / 256 * 256; }
+
+__device__ __forceinline__ unsigned ld_agent(const unsigned *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void lsq_initial_ranks(int n, float q_lo, float q_hi, int r, unsigned &rem) {
+  const float rk = (r < 2 ? q_lo : q_hi) * (float)(n - 1);
+  rem = (unsigned)((r & 1) ? ceilf(rk) : truncf(rk));
+}
+
+__global__ __launch_bounds__(LSQ_BT) void lsq_hist_kernel(const float *__restrict__ disp, int n, int nb, float q_lo,
+                                                          float q_hi, int pass, char *__restrict__ ws, long wss) {
+  __shared__ unsigned hist[4][256];
+  __shared__ unsigned s_pre[4], s_rem[4];
+  __shared__ int s_last;
+  const int b = blockIdx.x / nb, j = blockIdx.x % nb;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  LsqState *st = reinterpret_cast<LsqState *>(ws + b * wss);
+  unsigned *gh = reinterpret_cast<unsigned *>(ws + b * wss + 64);
+  if (t < 4) {
+    if (pass == 0) {
+      lsq_initial_ranks(n, q_lo, q_hi, t, s_rem[t]);
+      s_pre[t] = 0u;
+    } else {
+      s_pre[t] = st->prefix[t];
+      s_rem[t] = st->remain[t];
+    }
+  }
+  for (int i = t; i < 4 * 256; i += LSQ_BT) (&hist[0][0])[i] = 0u;
+  __syncthreads();
+  const int shift_ = 24 - 8 * pass;
+  unsigned pre[4];
+  int src[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    pre[r] = s_pre[r];
+    src[r] = r;
+    for (int q = r - 1; q >= 0; --q)
+      if (pre[q] == pre[r]) src[r] = q;
+  }
+  const float *dd = disp + (long)b * n + (long)j * LSQ_CH;
+  const int cnt = min(LSQ_CH, n - j * LSQ_CH);
+  unsigned keys[LSQ_EPT];
+#pragma unroll
+  for (int i = 0; i < LSQ_EPT; ++i) keys[i] = t + i * LSQ_BT < cnt ? key_of(dd[t + i * LSQ_BT]) : 0u;
+#pragma unroll
+  for (int i = 0; i < LSQ_EPT; ++i) {
+    const bool valid = t + i * LSQ_BT < cnt;
+    const unsigned bin = (keys[i] >> shift_) & 255u;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (src[r] != r) continue;
+      const bool match = valid && (pass == 0 || ((keys[i] ^ pre[r]) >> (shift_ + 8)) == 0u);
+      hist_add(hist[r], bin, match);
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < 4 * 256; i += LSQ_BT) {
+    const unsigned c = (&hist[0][0])[i];
+    if (c && src[i >> 8] == (i >> 8)) atomicAdd(&gh[i], c);
+  }
+  __threadfence();
+  __syncthreads();
+  if (t == 0) s_last = atomicAdd(&st->count, 1u) == (unsigned)(nb - 1);
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  if (wv < 4) {
+    const unsigned *hr = gh + 256 * src[wv];
+    const unsigned rem = s_rem[wv];
+    const unsigned c0 = ld_agent(hr + 4 * lane), c1 = ld_agent(hr + 4 * lane + 1);
+    const unsigned c2 = ld_agent(hr + 4 * lane + 2), c3 = ld_agent(hr + 4 * lane + 3);
+    unsigned inc = c0 + c1 + c2 + c3;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned u = __shfl_up(inc, o);
+      if (lane >= o) inc += u;
+    }
+    const unsigned long long past = __ballot(inc > rem);
+    const int L = past ? __ffsll((long long)past) - 1 : 63;
+    if (lane == L) {
+      unsigned acc = inc - (c0 + c1 + c2 + c3), sel = 4u * L + 3u;
+      const unsigned cs[4] = {c0, c1, c2, c3};
+      for (int k = 0; k < 4; ++k) {
+        if (acc + cs[k] > rem) {
+          sel = 4u * L + k;
+          break;
+        }
+        acc += cs[k];
+      }
+      st->remain[wv] = rem - acc;
+      st->prefix[wv] = pre[wv] | (sel << shift_);
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < 4 * 256; i += LSQ_BT) gh[i] = 0u;
+  if (t == 0) st->count = 0u;
+}
+
+__global__ __launch_bounds__(LSQ_BT) void lsq_solve_kernel(const float *__restrict__ mde, const float *__restrict__ disp,
+                                                           const float *__restrict__ conf, int n, int nb, float q_lo,
+                                                           float q_hi, char *__restrict__ ws, long wss,
+                                                           float *__restrict__ scale, float *__restrict__ shift) {
+  __shared__ double red[5][LSQ_BT / 64];
+  __shared__ int s_last;
+  const int b = blockIdx.x / nb, j = blockIdx.x % nb;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  LsqState *st = reinterpret_cast<LsqState *>(ws + b * wss);
+  double *part = reinterpret_cast<double *>(ws + b * wss + 64 + 4096);
+  const float r_lo = q_lo * (float)(n - 1), r_hi = q_hi * (float)(n - 1);
+  const float qlo = lerp_ref(__uint_as_float(st->prefix[0]), __uint_as_float(st->prefix[1]), r_lo - truncf(r_lo));
+  const float qhi = lerp_ref(__uint_as_float(st->prefix[2]), __uint_as_float(st->prefix[3]), r_hi - truncf(r_hi));
+  const long off = (long)b * n + (long)j * LSQ_CH;
+  const int cnt = min(LSQ_CH, n - j * LSQ_CH);
+  double acc[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < LSQ_EPT; ++i) {
+    const int e = t + i * LSQ_BT;
+    if (e >= cnt) continue;
+    const float d = __uint_as_float(key_of(disp[off + e]));
+    if (qlo <= d && d <= qhi) {
+      const float m = fabsf(mde[off + e]);
+      const float c = fabsf(conf[off + e]) * 0.9f + 0.1f;
+      const float w = sqrtf(c);
+      const float a1 = m * w, y = fabsf(d) * w;
+      acc[0] += (double)a1 * a1;
+      acc[1] += (double)a1 * w;
+      acc[2] += (double)w * w;
+      acc[3] += (double)a1 * y;
+      acc[4] += (double)w * y;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    double v = acc[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) red[q][wv] = v;
+  }
+  __syncthreads();
+  if (t < 5) part[j * 5 + t] = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
+  __threadfence();
+  __syncthreads();
+  if (t == 0) s_last = atomicAdd(&st->count, 1u) == (unsigned)(nb - 1);
+  __syncthreads();
+  if (!s_last || t != 0) return;
+  __threadfence();
+  double s[5] = {0, 0, 0, 0, 0};
+  for (int k = 0; k < nb; ++k)
+    for (int q = 0; q < 5; ++q)
+      s[q] += __hip_atomic_load(part + k * 5 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  st->count = 0u;
+  const double s11 = s[0], s12 = s[1], s22 = s[2], t1 = s[3], t2 = s[4];
+  const double det = s11 * s22 - s12 * s12;
+  double sc, sh;
+  if (s22 > 0 && fabs(det) > 1e-12 * s11 * s22) {
+    sc = (s22 * t1 - s12 * t2) / det;
+    sh = (s11 * t2 - s12 * t1) / det;
+  } else if (s22 > 0) {
+    const double m0 = s12 / s22, c0 = t2 / s22;
+    sc = c0 * m0 / (m0 * m0 + 1.0);
+    sh = c0 / (m0 * m0 + 1.0);
+  } else {
+    sc = 0.0;
+    sh = 0.0;
+  }
+  scale[b] = (float)sc;
+  shift[b] = (float)sh;
 }
 
 // ------------------------------------------------------------------ scaled mono + mirror
@@ -260,8 +516,37 @@ extern "C" int sa_weighted_lsq(const float *mde, const float *disp, const float 
   SA_REQUIRE(q_lo >= 0.f && q_lo <= q_hi && q_hi <= 1.f, "sa_weighted_lsq: quantiles out of order");
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_LSQ, s);
-  lsq_kernel<<<B, LSQ_THREADS, 0, s>>>(mde, disp, conf, n_per_b, q_lo, q_hi, scale, shift);
+  if (n_per_b <= 32 * LSQ_THREADS)
+    lsq_kernel<32><<<B, LSQ_THREADS, 0, s>>>(mde, disp, conf, n_per_b, q_lo, q_hi, scale, shift);
+  else
+    lsq_kernel<0><<<B, LSQ_THREADS, 0, s>>>(mde, disp, conf, n_per_b, q_lo, q_hi, scale, shift);
   return sa::check_launch("sa_weighted_lsq");
+}
+
+extern "C" long sa_weighted_lsq_ws_size(int B, int n_per_b) {
+  if (B <= 0 || n_per_b <= 0) return -1;
+  return (long)B * lsq_ws_stride(n_per_b);
+}
+
+extern "C" int sa_weighted_lsq_ws(const float *mde, const float *disp, const float *conf, int B, int n_per_b,
+                                  float q_lo, float q_hi, float *scale, float *shift, void *ws, void *stream) {
+  SA_REQUIRE(mde && disp && conf && scale && shift && ws, "sa_weighted_lsq_ws: null pointer");
+  SA_REQUIRE(B > 0 && n_per_b > 0, "sa_weighted_lsq_ws: empty input");
+  SA_REQUIRE(q_lo >= 0.f && q_lo <= q_hi && q_hi <= 1.f, "sa_weighted_lsq_ws: quantiles out of order");
+  SA_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0, "sa_weighted_lsq_ws: workspace not 16-byte aligned");
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_LSQ, s);
+  const int nb = lsq_nb(n_per_b);
+  const long wss = lsq_ws_stride(n_per_b);
+  char *w = static_cast<char *>(ws);
+  for (int pass = 0; pass < 4; ++pass) {
+    lsq_hist_kernel<<<(unsigned)(B * nb), LSQ_BT, 0, s>>>(disp, n_per_b, nb, q_lo, q_hi, pass, w, wss);
+    const int rc = sa::check_launch("sa_weighted_lsq_ws/hist");
+    if (rc) return rc;
+  }
+  lsq_solve_kernel<<<(unsigned)(B * nb), LSQ_BT, 0, s>>>(mde, disp, conf, n_per_b, nb, q_lo, q_hi, w, wss, scale,
+                                                         shift);
+  return sa::check_launch("sa_weighted_lsq_ws/solve");
 }
 
 extern "C" int sa_mono_scale_mirror(const float *m2, const float *m3, const float *scale, const float *shift,

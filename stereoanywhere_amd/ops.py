@@ -231,16 +231,26 @@ def softlrc_joint(disp: torch.Tensor, conf: Optional[torch.Tensor], lrc_th: floa
 
 
 def weighted_lsq(mde: torch.Tensor, disp: torch.Tensor, conf: torch.Tensor, q_lo: float = 0.2,
-                 q_hi: float = 0.9) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Per-sample (scale, shift) [B] of weighted_lsq over the flattened [B, ...] maps."""
+                 q_hi: float = 0.9, single_block: Optional[bool] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-sample (scale, shift) [B] of weighted_lsq over the flattened [B, ...] maps.
+    Spread over the GPU (sa_weighted_lsq_ws) or one workgroup per sample (single_block);
+    by default the former for up to 16 samples (B=4 at 2x136x240: 84 vs 156 us), the latter
+    above (B=64: 182 vs 709 us, where the global histogram atomics contend)."""
     for t, nm in ((mde, "mde"), (disp, "disp"), (conf, "conf")):
         _check(t, nm)
     B = mde.shape[0]
     n = mde.numel() // B
     scale = torch.empty(B, device=mde.device, dtype=torch.float32)
     shift = torch.empty(B, device=mde.device, dtype=torch.float32)
-    N.call("sa_weighted_lsq", mde.data_ptr(), disp.data_ptr(), conf.data_ptr(), B, n, q_lo, q_hi,
-           scale.data_ptr(), shift.data_ptr(), _stream(mde))
+    if single_block is None:
+        single_block = B > 16
+    if single_block:
+        N.call("sa_weighted_lsq", mde.data_ptr(), disp.data_ptr(), conf.data_ptr(), B, n, q_lo, q_hi,
+               scale.data_ptr(), shift.data_ptr(), _stream(mde))
+    else:
+        ws = torch.zeros(int(N.lib().sa_weighted_lsq_ws_size(B, n)), device=mde.device, dtype=torch.uint8)
+        N.call("sa_weighted_lsq_ws", mde.data_ptr(), disp.data_ptr(), conf.data_ptr(), B, n, q_lo, q_hi,
+               scale.data_ptr(), shift.data_ptr(), ws.data_ptr(), _stream(mde))
     return scale, shift
 
 

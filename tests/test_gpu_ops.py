@@ -208,14 +208,17 @@ def test_softlrc(micro):
     np.testing.assert_allclose(out[:, 1:2], micro["lrc.s3"], atol=2e-6)
 
 
-def test_weighted_lsq_matches_reference(micro):
-    sc, sh = ops.weighted_lsq(g(micro["lsq.mde"]), g(micro["lsq.disp"]), g(micro["lsq.conf"]))
+@pytest.mark.parametrize("single_block", [False, True])
+def test_weighted_lsq_matches_reference(micro, single_block):
+    sc, sh = ops.weighted_lsq(g(micro["lsq.mde"]), g(micro["lsq.disp"]), g(micro["lsq.conf"]),
+                              single_block=single_block)
     np.testing.assert_allclose(c(sc), micro["lsq.scale"].ravel(), rtol=2e-5, atol=1e-5)
     np.testing.assert_allclose(c(sh), micro["lsq.shift"].ravel(), rtol=2e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("n", [2, 17, 1000, 65280])
-def test_weighted_lsq_quantile_band_vs_oracle(n):
+@pytest.mark.parametrize("single_block", [False, True])
+@pytest.mark.parametrize("n", [2, 17, 1000, 2048, 2049, 32640, 32768, 32769, 65280])
+def test_weighted_lsq_quantile_band_vs_oracle(n, single_block):
     rng = np.random.default_rng(n)
     B = 3
     m = rng.random((B, n)).astype(np.float32)
@@ -223,7 +226,7 @@ def test_weighted_lsq_quantile_band_vs_oracle(n):
     d[:, : n // 7] = -1.0  # relu'd to 0: ties at the bottom of the band
     d[1, : n // 2] = 5.0    # ties inside the band
     cf = rng.random((B, n)).astype(np.float32)
-    sc, sh = ops.weighted_lsq(g(m), g(d), g(cf))
+    sc, sh = ops.weighted_lsq(g(m), g(d), g(cf), single_block=single_block)
     rsc, rsh = R.weighted_lsq(m, d, cf)
     np.testing.assert_allclose(c(sc), rsc, rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(c(sh), rsh, rtol=1e-5, atol=1e-4)
