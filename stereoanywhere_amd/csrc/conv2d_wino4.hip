@@ -32,6 +32,22 @@
 
 #pragma clang fp contract(fast)
 
+// diagnostic / A-B switches (build-time)
+#ifndef SA_W4_SPREAD
+#define SA_W4_SPREAD 1
+#endif
+#ifndef SA_W4_FENCE
+#define SA_W4_FENCE 1
+#endif
+#ifndef SA_W4_DIAG
+#define SA_W4_DIAG 0   // timing diagnostics only (wrong results): 1 no DMA in the loop, 2 no
+                       // transform / MFMA, 3 no DMA and no barrier in the loop, 4 as 3 and no
+                       // DMA at all
+#endif
+#ifndef SA_W4_PRIO
+#define SA_W4_PRIO 0
+#endif
+
 namespace {
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
@@ -134,16 +150,17 @@ __device__ __forceinline__ void bt6h(const float x0, const float x1, const float
 #ifdef SA_W4_CLOCK
 // diagnostic build only: per block (s_memtime, s_memrealtime) at the start and the end of wave 0,
 // then s_memtime after the first chunk's barrier and after the main loop
-__device__ unsigned long long g_w4_clock[65536][8];
+__device__ unsigned long long g_w4_clock[65536][10];   // + [8] chunk 0 issued, [9] last wave's start
 #endif
 
-template <class C, int HF>
+template <class C, int HF, int LTW>
 __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, float *smem) {
   constexpr int NWAVE = C::NW, NTHR = C::NTHR, KC = C::KC, JPC = C::JPC, NT = C::NT, PDMA = C::PDMA,
                 UDMA = C::UDMA, UPW = C::UPW, UBUF = C::UBUF, BUF = C::BUF, PBUF = C::PBUF, OPP = C::OPP;
   const int Cin = P.Cin, H = P.H, W = P.W, Cout = P.Cout;
-  const int ltw = P.ltw, tw = 1 << ltw, tr = NT >> ltw;
-  const int BH = 4 * tr, BW = 4 * tw, PG = tw + 2, PR = BH + 2, PS = PR * PG;
+  // block geometry as compile-time constants (the patch offsets divide by PS and PG)
+  constexpr int ltw = LTW, tw = 1 << ltw, tr = NT >> ltw;
+  constexpr int BH = 4 * tr, BW = 4 * tw, PG = tw + 2, PR = BH + 2, PS = PR * PG;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int co_blocks = P.co_blocks, tiles_hw = P.tiles_hw, tiles_w = P.tiles_w;
@@ -171,6 +188,12 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
 
   // patch DMA: the chunk's image is [channel][PR rows][PG groups of 4 floats], dense, starting
   // at (y0 - 1, x0 - 4); wave-instruction gi fills groups 64 gi .. 64 gi + 63 (lane-linear)
+  // chunk 0's filters first: their offsets need no patch geometry
+  if (SA_W4_DIAG != 4) {
+#pragma unroll
+    for (int j = 0; j < UPW; ++j)
+      if (wv + NWAVE * j < UDMA) dma16(uin, smem + PBUF + (wv + NWAVE * j) * 256, u_src(wv + NWAVE * j), u_chunk(0));
+  }
   const int npi = (KC * PS + 63) >> 6;
   int po[PDMA];
 #pragma unroll
@@ -198,6 +221,11 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
         dma16(uin, ub + (wv + NWAVE * j) * 256, u_src(wv + NWAVE * j), us);
   };
   auto issue = [&](int chunk, int buf) __attribute__((always_inline)) { issue_part(chunk, buf, -1); };
+  auto issue_p0 = [&]() __attribute__((always_inline)) {   // chunk 0's patch (its filters went first)
+#pragma unroll
+    for (int j = 0; j < PDMA; ++j)
+      if (wv + NWAVE * j < npi) dma16(xin, smem + (wv + NWAVE * j) * 256, po[j], 0);
+  };
 
   // lane roles: MFMA A operand A[m][k] = (tile m, channel k); B operands B[k][n] = (channel k,
   // output channel n of each 16-channel half)
@@ -206,7 +234,11 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
   const int tidx = tg * 16 + m, trow = tidx >> ltw, tcol = tidx & (tw - 1);
   // patch row 0 of the tile (input row y0 + 4 trow - 1), columns 4 tcol + 2 .. 4 tcol + 9
   // (input x0 + 4 tcol - 2 ...): the tile's 6 inputs are columns 3..8 of that span
-  const int pread = k * PS * 4 + 4 * trow * PG * 4 + 4 * tcol + 2;
+  // the main loop addresses the patch with run-time PS / PG (as before the geometry became a
+  // template argument: with immediate offsets its schedule measured ~1% slower)
+  int PSv = PS, PGv = PG;
+  asm volatile("" : "+s"(PSv), "+s"(PGv));
+  const int pread = k * PSv * 4 + 4 * trow * PGv * 4 + 4 * tcol + 2;
   const int uread = k * 32 + 2 * m;
 
   // acc[i][jj][g]: point (row i, column 3 HF + jj) of output-channel half g
@@ -216,22 +248,11 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
 #pragma unroll
     for (int jj = 0; jj < 3; ++jj) acc[i][jj][0] = acc[i][jj][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#ifndef SA_W4_SPREAD
-#define SA_W4_SPREAD 1
-#endif
-#ifndef SA_W4_FENCE
-#define SA_W4_FENCE 1
-#endif
-#ifndef SA_W4_DIAG
-#define SA_W4_DIAG 0   // timing diagnostics only (wrong results): 1 no DMA in the loop, 2 no
-                       // transform / MFMA, 3 no DMA and no barrier in the loop, 4 as 3 and no
-                       // DMA at all
-#endif
-#ifndef SA_W4_PRIO
-#define SA_W4_PRIO 0
-#endif
   if (SA_W4_PRIO && HF == 1) __builtin_amdgcn_s_setprio(1);   // static priority for waves 4-7
-  if (SA_W4_DIAG != 4) issue(0, 0);
+  if (SA_W4_DIAG != 4) issue_p0();
+#ifdef SA_W4_CLOCK
+  if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][8] = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll 1
   for (int kc = 0; kc < nchunks; ++kc) {
     const int cur = kc & 1;
@@ -253,12 +274,12 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
     f32x2 ra[6], rc[6];
     f32x4 rb[6];
     auto load_rows = [&](int s, int r0, int r1) __attribute__((always_inline)) {
-      const float *p = pb + s * 4 * PS * 4;
+      const float *p = pb + s * 4 * PSv * 4;
 #pragma unroll
       for (int r = r0; r < r1; ++r) {
-        ra[r] = *reinterpret_cast<const f32x2 *>(p + r * PG * 4);
-        rb[r] = *reinterpret_cast<const f32x4 *>(p + r * PG * 4 + 2);
-        rc[r] = *reinterpret_cast<const f32x2 *>(p + r * PG * 4 + 6);
+        ra[r] = *reinterpret_cast<const f32x2 *>(p + r * PGv * 4);
+        rb[r] = *reinterpret_cast<const f32x4 *>(p + r * PGv * 4 + 2);
+        rc[r] = *reinterpret_cast<const f32x2 *>(p + r * PGv * 4 + 6);
       }
     };
     f32x2 bc[6], bn[6];
@@ -431,12 +452,17 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 ? 1 : 2) void wino_f4k3_kernel(
   __shared__ __attribute__((aligned(16))) float smem[C::SMEM];
 #ifdef SA_W4_CLOCK
   unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == C::NTHR - 64 && blockIdx.x < 65536) g_w4_clock[blockIdx.x][9] = t0;
 #endif
   // the first half of the waves takes point columns 0-2, the second half 3-5 (wave-uniform)
-  if (threadIdx.x < C::NTHR / 2)
-    w4_body<C, 0>(P, sa::xcd_remap(g - base, nb), smem);
-  else
-    w4_body<C, 1>(P, sa::xcd_remap(g - base, nb), smem);
+  const unsigned wid = sa::xcd_remap(g - base, nb);
+  if (threadIdx.x < C::NTHR / 2) {
+    if (P.ltw == 4) w4_body<C, 0, 4>(P, wid, smem);
+    else w4_body<C, 0, 5>(P, wid, smem);
+  } else {
+    if (P.ltw == 4) w4_body<C, 1, 4>(P, wid, smem);
+    else w4_body<C, 1, 5>(P, wid, smem);
+  }
 #ifdef SA_W4_CLOCK
   if (threadIdx.x == 0 && g < 65536) {
     g_w4_clock[g][0] = t0;
@@ -495,7 +521,7 @@ extern "C" int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, f
 
 #ifdef SA_W4_CLOCK
 extern "C" int sa_w4_clock_read(unsigned long long *out, int n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4_clock), sizeof(unsigned long long) * 8 * n) == hipSuccess ? 0 : -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4_clock), sizeof(unsigned long long) * 10 * n) == hipSuccess ? 0 : -1;
 }
 #endif
 
