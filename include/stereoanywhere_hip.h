@@ -280,6 +280,28 @@ int sa_conv2d_k3_wino_multi(int nprob, const SaWinoProblem *probs, void *stream)
 int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, float *U4, void *stream);
 long sa_conv2d_k3_wino4_stat_parts(int H, int W);
 int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, void *stream);
+/* ConvGRU gates in the epilogue (update.py:16-27), per problem (gates[i].mode 0 = plain; gates
+ * may be NULL).  v = conv + bias (no ReLU, no statistics), c = ctx plane of the same output
+ * channel (ctx + co*H*W, batch stride ctx_bs), all planes 16-byte aligned:
+ *   mode 1, conv over cat(h, x) with Cout = 2*Ch output channels (convz | convr):
+ *           co < Ch: out[co] = sigmoid(v + c);  co >= Ch: out2[co - Ch] = sigmoid(v + c) * h[co - Ch]
+ *   mode 2, conv over r*h (convq's r*h part): out[co] = (1 - z) h + z tanh((add + v) + c) with
+ *           z, h, add (convq's x part) planes of channel co; out may be h itself (in place). */
+typedef struct SaGateEpilogue {
+  int mode;
+  const float *ctx;
+  long ctx_bs;
+  const float *h;
+  long h_bs;
+  const float *z;
+  long z_bs;
+  const float *add;
+  long add_bs;
+  float *out2;
+  long out2_bs;
+} SaGateEpilogue;
+int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
+                                  void *stream);
 
 /* Direct KxK convolution (padding K/2, no bias) on fp32 MFMA for the encoder convs the
  * Winograd kernel does not cover (extractor.py:22-40, 91, 208):

@@ -29,6 +29,12 @@ class SaWinoProblem(ctypes.Structure):
                 ("in_act", I), ("out", P), ("out_bs", L), ("stats_partial", P)]
 
 
+class SaGateEpilogue(ctypes.Structure):
+    """include/stereoanywhere_hip.h: ConvGRU gate epilogue of sa_conv2d_k3_wino4_multi_gate."""
+    _fields_ = [("mode", I), ("ctx", P), ("ctx_bs", L), ("h", P), ("h_bs", L), ("z", P), ("z_bs", L),
+                ("add", P), ("add_bs", L), ("out2", P), ("out2_bs", L)]
+
+
 SIGNATURES = {
     "sa_abi_version": (I, []),
     "sa_last_error": (ctypes.c_char_p, []),
@@ -66,6 +72,7 @@ SIGNATURES = {
     "sa_conv2d_wino4_weights": (I, [P, I, I, P, P]),
     "sa_conv2d_k3_wino4_stat_parts": (L, [I, I]),
     "sa_conv2d_k3_wino4_multi": (I, [I, P, P]),
+    "sa_conv2d_k3_wino4_multi_gate": (I, [I, P, P, P]),
     "sa_conv_direct_weights": (I, [P, I, I, I, I, I, P, P]),
     "sa_conv_direct_weights_size": (L, [I, I, I, I, I]),
     "sa_conv_direct_stat_parts": (L, [I, I]),

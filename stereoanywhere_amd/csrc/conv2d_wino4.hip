@@ -96,8 +96,23 @@ struct W4Prob {
   double *partial;
 };
 constexpr int MAX_PROB = 8;
+// GRU gate epilogues (SaGateEpilogue in the header), read by the store loop only
+struct W4Gate {
+  int mode;
+  const float *ctx;
+  long ctx_bs;
+  const float *h;
+  long h_bs;
+  const float *z;
+  long z_bs;
+  const float *add;
+  long add_bs;
+  float *out2;
+  long out2_bs;
+};
 struct W4Launch {
   W4Prob p[MAX_PROB];
+  W4Gate gate[MAX_PROB];
   unsigned end[MAX_PROB];
   unsigned nblk[MAX_PROB];
   int nprob;
@@ -154,7 +169,7 @@ __device__ unsigned long long g_w4_clock[65536][10];   // + [8] chunk 0 issued, 
 #endif
 
 template <class C, int HF, int LTW>
-__device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, float *smem) {
+__device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate &GT, const unsigned wid, float *smem) {
   constexpr int NWAVE = C::NW, NTHR = C::NTHR, KC = C::KC, JPC = C::JPC, NT = C::NT, PDMA = C::PDMA,
                 UDMA = C::UDMA, UPW = C::UPW, UBUF = C::UBUF, BUF = C::BUF, PBUF = C::PBUF, OPP = C::OPP;
   const int Cin = P.Cin, H = P.H, W = P.W, Cout = P.Cout;
@@ -422,14 +437,58 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const unsigned wid, flo
 #endif
   // float4 stores: NT * 4 per channel plane of the block
   float *dst = P.out + (long)n * P.out_bs;
+  if (GT.mode == 0) {
 #pragma unroll 4
+    for (int j = 0; j < (CO * NT * 16) / (4 * NTHR); ++j) {
+      const int i4 = tid + NTHR * j;
+      const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
+      const int y = y0 + r, x = x0 + cx;
+      if (y < H && x < W)
+        *reinterpret_cast<f32x4 *>(dst + (long)(co0 + c) * hw + (long)y * W + x) =
+            *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
+    }
+    return;
+  }
+  // GRU gates (update.py:16-27): conv (+ bias, staged) + context, then
+  //   mode 1 (z | r over cat(h, x)): z = sigmoid(.) -> out, r * h -> out2 (block-uniform half)
+  //   mode 2 (q over r*h):           h' = (1 - z) h + z tanh(. + add) -> out (in place on h)
+  const int half = Cout / 2;
+  const bool rhalf = co0 >= half;
+  const float *ctxb = GT.ctx + (long)n * GT.ctx_bs;
+#pragma unroll 2
   for (int j = 0; j < (CO * NT * 16) / (4 * NTHR); ++j) {
     const int i4 = tid + NTHR * j;
     const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
     const int y = y0 + r, x = x0 + cx;
-    if (y < H && x < W)
-      *reinterpret_cast<f32x4 *>(dst + (long)(co0 + c) * hw + (long)y * W + x) =
-          *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
+    if (y < H && x < W) {
+      const int co = co0 + c;
+      const long px = (long)y * W + x;
+      const f32x4 v = *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
+      const f32x4 cv = *reinterpret_cast<const f32x4 *>(ctxb + (long)co * hw + px);
+      f32x4 o;
+      if (GT.mode == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = sa::sigmoidf_ref(v[e] + cv[e]);
+        if (!rhalf) {
+          *reinterpret_cast<f32x4 *>(dst + (long)co * hw + px) = o;
+        } else {
+          const f32x4 hv = *reinterpret_cast<const f32x4 *>(GT.h + (long)n * GT.h_bs + (long)(co - half) * hw + px);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = o[e] * hv[e];
+          *reinterpret_cast<f32x4 *>(GT.out2 + (long)n * GT.out2_bs + (long)(co - half) * hw + px) = o;
+        }
+      } else {
+        const f32x4 av = *reinterpret_cast<const f32x4 *>(GT.add + (long)n * GT.add_bs + (long)co * hw + px);
+        const f32x4 zv = *reinterpret_cast<const f32x4 *>(GT.z + (long)n * GT.z_bs + (long)co * hw + px);
+        const f32x4 hv = *reinterpret_cast<const f32x4 *>(GT.h + (long)n * GT.h_bs + (long)co * hw + px);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float q = tanhf((av[e] + v[e]) + cv[e]);
+          o[e] = (1.0f - zv[e]) * hv[e] + zv[e] * q;
+        }
+        *reinterpret_cast<f32x4 *>(dst + (long)co * hw + px) = o;
+      }
+    }
   }
 }
 
@@ -440,12 +499,14 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 ? 1 : 2) void wino_f4k3_kernel(
   const unsigned g = blockIdx.x;
   W4Prob P = L.p[0];
   unsigned base = 0, nb = L.nblk[0];
+  int pi = 0;
 #pragma unroll
   for (int i = 1; i < MAX_PROB; ++i) {
     if (i < L.nprob && g >= L.end[i - 1]) {
       P = L.p[i];
       base = L.end[i - 1];
       nb = L.nblk[i];
+      pi = i;
     }
   }
   if (g - base >= nb) return;
@@ -457,11 +518,11 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 ? 1 : 2) void wino_f4k3_kernel(
   // the first half of the waves takes point columns 0-2, the second half 3-5 (wave-uniform)
   const unsigned wid = sa::xcd_remap(g - base, nb);
   if (threadIdx.x < C::NTHR / 2) {
-    if (P.ltw == 4) w4_body<C, 0, 4>(P, wid, smem);
-    else w4_body<C, 0, 5>(P, wid, smem);
+    if (P.ltw == 4) w4_body<C, 0, 4>(P, L.gate[pi], wid, smem);
+    else w4_body<C, 0, 5>(P, L.gate[pi], wid, smem);
   } else {
-    if (P.ltw == 4) w4_body<C, 1, 4>(P, wid, smem);
-    else w4_body<C, 1, 5>(P, wid, smem);
+    if (P.ltw == 4) w4_body<C, 1, 4>(P, L.gate[pi], wid, smem);
+    else w4_body<C, 1, 5>(P, L.gate[pi], wid, smem);
   }
 #ifdef SA_W4_CLOCK
   if (threadIdx.x == 0 && g < 65536) {
@@ -532,6 +593,11 @@ extern "C" long sa_conv2d_k3_wino4_stat_parts(int H, int W) {
 }
 
 extern "C" int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, void *stream) {
+  return sa_conv2d_k3_wino4_multi_gate(nprob, probs, nullptr, stream);
+}
+
+extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
+                                             void *stream) {
   SA_REQUIRE(nprob >= 1 && nprob <= MAX_PROB && probs, "sa_conv2d_k3_wino4_multi: 1..%d problems", MAX_PROB);
   static const int shape = [] {   // SA_W4_SHAPE=big|small forces one block shape (A/B runs)
     const char *e = getenv("SA_W4_SHAPE");
@@ -560,6 +626,22 @@ extern "C" int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, v
     const int tiles_w = (q.W + bw - 1) / bw, tiles_h = (q.H + bh - 1) / bh;
     L.p[i] = W4Prob{q.in, q.in_bs, q.Cin, q.H, q.W, q.U, q.Cout, q.bias, q.relu, q.out, q.out_bs,
                     ltw, tiles_w, tiles_w * tiles_h, q.Cout / CO, q.stats_partial};
+    L.gate[i] = W4Gate{};
+    if (gates && gates[i].mode != 0) {
+      const SaGateEpilogue &e = gates[i];
+      auto a16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+      SA_REQUIRE(e.mode == 1 || e.mode == 2, "sa_conv2d_k3_wino4: gate mode %d", e.mode);
+      SA_REQUIRE(!q.relu && !q.stats_partial, "sa_conv2d_k3_wino4: a gate epilogue takes no ReLU / statistics");
+      SA_REQUIRE(e.ctx && e.h && a16(e.ctx) && a16(e.h) && e.ctx_bs % 4 == 0 && e.h_bs % 4 == 0,
+                 "sa_conv2d_k3_wino4: gate needs 16-byte aligned ctx and h planes");
+      if (e.mode == 1)
+        SA_REQUIRE(q.Cout % 64 == 0 && e.out2 && a16(e.out2) && e.out2_bs % 4 == 0,
+                   "sa_conv2d_k3_wino4: z/r gate needs Cout %% 64 == 0 and an aligned r*h output");
+      else
+        SA_REQUIRE(e.z && e.add && a16(e.z) && a16(e.add) && e.z_bs % 4 == 0 && e.add_bs % 4 == 0,
+                   "sa_conv2d_k3_wino4: state gate needs aligned z and addend planes");
+      L.gate[i] = W4Gate{e.mode, e.ctx, e.ctx_bs, e.h, e.h_bs, e.z, e.z_bs, e.add, e.add_bs, e.out2, e.out2_bs};
+    }
     const long nb = (long)q.N * L.p[i].tiles_hw * L.p[i].co_blocks;
     total = (i + 1 < nprob ? (total + nb + 7) / 8 * 8 : total + nb);
     SA_REQUIRE(total < (1L << 31), "sa_conv2d_k3_wino4: grid too large");

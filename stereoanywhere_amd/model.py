@@ -56,6 +56,12 @@ def _normalize_pair(a: torch.Tensor, b: torch.Tensor, eps: float = 1e-4):
 # independent 3x3 convs of the update block share one launch (ops.conv2d_k3_multi);
 # SA_GROUP_CONVS=0 launches them one by one (A/B timing)
 _GROUP_CONVS = os.environ.get("SA_GROUP_CONVS", "1") != "0"
+# GRU z/r gates in the F(4x4) conv epilogue (ops.conv2d_k3_multi gate=...) where its
+# preconditions hold; SA_FUSE_GATES=0 keeps the separate gate kernels (A/B timing)
+_FUSE_GATES = os.environ.get("SA_FUSE_GATES", "1") != "0"
+# ... and the state update in the r*h conv's epilogue (SA_FUSE_OUT=0: gru_out kernel, r*h conv
+# split over its input channels)
+_FUSE_OUT = os.environ.get("SA_FUSE_OUT", "1") != "0"
 
 class StereoAnywhere(nn.Module):
     def __init__(self, args):
@@ -92,6 +98,11 @@ class StereoAnywhere(nn.Module):
             bx=torch.cat([gru.convz.bias, gru.convr.bias, gru.convq.bias], 0).contiguous(),
             whzr=torch.cat([wz[:, :hidden], wr[:, :hidden]], 0).contiguous(),
             wqh=wq[:, :hidden].contiguous(),
+            # gates in the conv epilogue: convz | convr over cat(h, x) as the reference has them,
+            # and convq's x part
+            wzr=torch.cat([wz, wr], 0).contiguous(),
+            bzr=torch.cat([gru.convz.bias, gru.convr.bias], 0).contiguous(),
+            wqx=wq[:, hidden:].contiguous(),
         )
 
     def _weights(self):
@@ -136,6 +147,7 @@ class StereoAnywhere(nn.Module):
                     half = g["wqh"].shape[1] // 2
                     g.update(Ux=ops.wino_weights(g["wx"]), Uhzr=ops.wino_weights(g["whzr"]),
                              Uqh=ops.wino_weights(g["wqh"]),
+                             Uzr=ops.wino_weights(g["wzr"]), Uqx=ops.wino_weights(g["wqx"]),
                              # the r*h conv split over its input channels (two half-K launches'
                              # worth of blocks; gru_out adds the partial sums)
                              Uqh_k=[ops.wino_weights(g["wqh"][:, :half].contiguous()),
@@ -279,14 +291,35 @@ class StereoAnywhere(nn.Module):
         c1 = torch.empty((2 * B, enc.convc1.out_channels, H4, W4), device=dev, dtype=f32)  # convc1(lookups)
         motin = torch.empty((B, 192, H4, W4), device=dev, dtype=f32)  # [convc2 stereo | mono | convf2]
         flow = torch.empty((B, 2, H4, W4), device=dev, dtype=f32)
-        x08 = torch.empty((B, 256, H4, W4), device=dev, dtype=f32)   # [motion(126) | flow(2) | interp(h16)]
-        x16 = torch.empty((B, 256, H8, W8), device=dev, dtype=f32)   # [pool(h08) | interp(h32)]
-        x32 = torch.empty((B, 128, H16, W16), device=dev, dtype=f32)  # [pool(h16)]
-        z = {k: torch.empty_like(h) for k, h in (("08", h08), ("16", h16), ("32", h32))}
-        rh = {k: torch.empty_like(h) for k, h in (("08", h08), ("16", h16), ("32", h32))}
+        # x08 = [motion(126) | flow(2) | interp(h16)], x16 = [pool(h08) | interp(h32)], x32 = [pool(h16)]
+        xdims = {"08": 256, "16": 256, "32": 128}
+        shapes = {"08": (H4, W4), "16": (H8, W8), "32": (H16, W16)}
+        hd = h08.shape[1]
+        # the F(4x4) kernel's preconditions at every level (W % 4; planes then stay 16-byte aligned)
+        fused = _FUSE_GATES and ops.gate_f4_ok() and all(s[1] % 4 == 0 for s in shapes.values())
+        if fused:
+            # one buffer per level, [h | x | r*h]: the z/r conv reads cat(h, x) and the r*h conv
+            # reads r*h as channel views of it (no torch.cat)
+            hxr = {k: torch.empty((B, 2 * hd + xdims[k], *shapes[k]), device=dev, dtype=f32) for k in shapes}
+            for k, h in zip(("08", "16", "32"), hid):
+                hxr[k][:, :hd].copy_(h)
+            h08, h16, h32 = (hxr[k][:, :hd] for k in ("08", "16", "32"))
+            x08, x16, x32 = (hxr[k][:, hd:hd + xdims[k]] for k in ("08", "16", "32"))
+            rh = {k: hxr[k][:, hd + xdims[k]:] for k in shapes}
+            # convq's x part lands in channels 2*hd.. of a [B, 3*hd] buffer: gru_out reads it there
+            xq = {k: torch.empty((B, 3 * hd, *shapes[k]), device=dev, dtype=f32) for k in shapes}
+        else:
+            x08 = torch.empty((B, xdims["08"], H4, W4), device=dev, dtype=f32)
+            x16 = torch.empty((B, xdims["16"], H8, W8), device=dev, dtype=f32)
+            x32 = torch.empty((B, xdims["32"], H16, W16), device=dev, dtype=f32)
+            rh = {k: torch.empty_like(h) for k, h in (("08", h08), ("16", h16), ("32", h32))}
+        hs = {"08": h08, "16": h16, "32": h32}
+        fuse_out = fused and _FUSE_OUT
+        z = {k: torch.empty(h.shape, device=dev, dtype=f32) for k, h in hs.items()}
         cz = [c[:, 0:128] for c in ctx]
         cr = [c[:, 128:256] for c in ctx]
         cq = [c[:, 256:384] for c in ctx]
+        lvl = {"08": 0, "16": 1, "32": 2}
 
         def conv_group(*probs):
             """Independent 3x3 convs in one launch (SA_GROUP_CONVS=0: one launch each)."""
@@ -295,14 +328,23 @@ class StereoAnywhere(nn.Module):
             return [ops.conv2d_k3(**p) for p in probs]
 
         def gate_x_h(key, x, h):
-            g = dw["g" + key]   # x and h halves of convz/convr/convq; bias added in the gate kernels
+            g = dw["g" + key]
+            if fused:
+                # convz | convr over cat(h, x) (+ bias) with z = sigmoid(. + cz) and r*h = sigmoid(. + cr) * h
+                # in the epilogue (update.py:24-25); convq's x part (bias added in gru_out)
+                hx = hxr[key][:, :hd + xdims[key]]
+                return [dict(x=hx, U=g["Uzr"], bias=g["bzr"], out=z[key],
+                             gate=dict(mode=1, ctx=ctx[lvl[key]], h=h, out2=rh[key])),
+                        dict(x=x, U=g["Uqx"], out=xq[key][:, 2 * hd:])]
+            # x and h halves of convz/convr/convq; bias added in the gate kernels
             return [dict(x=x, U=g["Ux"]), dict(x=h, U=g["Uhzr"])]
 
         def gru_zr(level, key, h, xc, hzr):
-            ops.gru_zr(xc, hzr, cz[level], cr[level], h, z[key], rh[key], bx=dw["g" + key]["bx"])
+            if not fused:   # else done in the conv epilogue
+                ops.gru_zr(xc, hzr, cz[level], cr[level], h, z[key], rh[key], bx=dw["g" + key]["bx"])
 
         def gru_out(level, key, h, xc, qh, qh2=None):
-            ops.gru_out(xc, qh, cq[level], z[key], h, bx=dw["g" + key]["bx"], qh2=qh2)
+            ops.gru_out(xq[key] if fused else xc, qh, cq[level], z[key], h, bx=dw["g" + key]["bx"], qh2=qh2)
 
         def qh_split(key):
             """r*h conv of one GRU as two half-Cin problems (more, shorter blocks: the launch's
@@ -310,6 +352,20 @@ class StereoAnywhere(nn.Module):
             r, Uk = rh[key], dw["g" + key]["Uqh_k"]
             c = r.shape[1] // 2
             return [dict(x=r[:, :c], U=Uk[0]), dict(x=r[:, c:], U=Uk[1])]
+
+        def q_probs(key, split):
+            """convq's r*h part: with the state update h = (1 - z) h + z tanh(. + x part + cq) in
+            its epilogue (one problem, in place on h), else plain problem(s) (split over Cin when
+            ``split``) whose sums q_finish hands to gru_out."""
+            if fuse_out:
+                g = dw["g" + key]
+                return [dict(x=rh[key], U=g["Uqh"], bias=g["bx"][2 * hd:], out=hs[key],
+                             gate=dict(mode=2, ctx=cq[lvl[key]], h=hs[key], z=z[key], add=xq[key][:, 2 * hd:]))]
+            return qh_split(key) if split else [dict(x=rh[key], U=dw["g" + key]["Uqh"])]
+
+        def q_finish(level, key, xc, res):
+            if not fuse_out:
+                gru_out(level, key, hs[key], xc, *res)
 
         ops.flow_update(coords_x, None, flow, x08[:, 126:128])
         flow_up = None
@@ -323,7 +379,7 @@ class StereoAnywhere(nn.Module):
         ops.pool2x(h16, x32)
         xc32, hzr32 = conv_group(*gate_x_h("32", x32, h32))
         gru_zr(2, "32", h32, xc32, hzr32)
-        gru_out(2, "32", h32, xc32, ops.conv2d_k3(rh["32"], dw["g32"]["Uqh"]))
+        q_finish(2, "32", xc32, conv_group(*q_probs("32", False)))
         for it in range(iters):
             last = it == iters - 1
             # lookup of both pyramids + convc1 + ReLU in one kernel (sample 2b: stereo, 2b+1: mono)
@@ -341,9 +397,9 @@ class StereoAnywhere(nn.Module):
             gru_zr(1, "16", h16, xc16, hzr16)
             # gru16's r*h conv + the motion conv (_conv: 126 outputs, padded to 128, into
             # x08[:, :128]; channels 126-127 (the flow) are rewritten right after)
-            qh16 = conv_group(dict(x=rh["16"], U=dw["g16"]["Uqh"]),
-                              dict(x=motin, U=dw["U_mot"], bias=dw["mot_b"], relu=True, out=x08[:, :128]))[0]
-            gru_out(1, "16", h16, xc16, qh16)
+            qp = q_probs("16", False)
+            res = conv_group(*qp, dict(x=motin, U=dw["U_mot"], bias=dw["mot_b"], relu=True, out=x08[:, :128]))
+            q_finish(1, "16", xc16, res[:len(qp)])
             ops.flow_update(coords_x, None, None, x08[:, 126:128])
             ops.interp(h16, x08[:, 128:])
             # gru08's x/h convs (+ gru32's of the next iteration), then the r*h convs
@@ -354,15 +410,16 @@ class StereoAnywhere(nn.Module):
             res = conv_group(*probs)
             xc08, hzr08 = res[:2]
             gru_zr(0, "08", h08, xc08, hzr08)
-            probs = qh_split("08")
+            qp = q_probs("08", True)
+            probs = list(qp)
             if not last:
                 xc32, hzr32 = res[2:]
                 gru_zr(2, "32", h32, xc32, hzr32)
-                probs += qh_split("32")
+                probs += q_probs("32", True)
             qh = conv_group(*probs)
-            gru_out(0, "08", h08, xc08, qh[0], qh[1])
+            q_finish(0, "08", xc08, qh[:len(qp)])
             if not last:
-                gru_out(2, "32", h32, xc32, qh[2], qh[3])
+                q_finish(2, "32", xc32, qh[len(qp):])
             f1 = ops.conv2d_k3(h08, dw["U_fh1"], ub.flow_head.conv1.bias, relu=True)
             delta = ops.conv2d_k3_narrow(f1, ub.flow_head.conv2.weight, ub.flow_head.conv2.bias)
             ops.flow_update(coords_x, delta[:, 0:1], flow, None)

@@ -546,7 +546,8 @@ _WINO4_MIN_BLOCKS = 384
 
 def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] = None, relu: bool = False,
                   out: Optional[torch.Tensor] = None, in_aff: Optional[Affine] = None, in_act=None,
-                  stats: bool = False, f4: bool = False):
+                  stats: bool = False, f4: bool = False, out_cout: Optional[int] = None):
+    """out_cout: channels of ``out`` when the epilogue writes fewer than Cout there (gate mode 1)."""
     bs = _plane_bs(x, "x")
     if not isinstance(U, WinoFilters):
         raise RuntimeError("conv2d_k3: U must come from ops.wino_weights")
@@ -555,8 +556,8 @@ def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] 
     if U.cin != Cin:
         raise RuntimeError(f"conv2d_k3: U has {U.cin} input channels, x has {Cin}")
     if out is None:
-        out = torch.empty((B, Cout, H, W), device=x.device, dtype=torch.float32)
-    if tuple(out.shape) != (B, Cout, H, W):
+        out = torch.empty((B, out_cout or Cout, H, W), device=x.device, dtype=torch.float32)
+    if tuple(out.shape) != (B, out_cout or Cout, H, W):
         raise RuntimeError("conv2d_k3: out shape mismatch")
     m, s, t, ps = (in_aff or Affine()).args(Cin)
     parts_fn = N.lib().sa_conv2d_k3_wino4_stat_parts if f4 else N.lib().sa_conv2d_k3_wino_stat_parts
@@ -583,20 +584,72 @@ def wino4_applies(x: torch.Tensor, U: "WinoFilters", *more) -> bool:
             and sum(_wino4_blocks(a, u) for a, u in pairs) >= _WINO4_MIN_BLOCKS)
 
 
+def _gate_epilogue(p: dict) -> "N.SaGateEpilogue":
+    """ConvGRU gate epilogue of one problem (sa_conv2d_k3_wino4_multi_gate):
+    gate=dict(mode=1, ctx=, h=, out2=): out = z, out2 = r*h for a conv over cat(h, x) with
+    Cout = 2*Ch (convz | convr); gate=dict(mode=2, ctx=, h=, z=, add=): out = the new state
+    (1 - z) h + z tanh(add + conv + ctx) for convq's r*h part (out may be h itself)."""
+    g = p["gate"]
+    mode = g["mode"]
+    B, _, H, W = p["x"].shape
+    Cout = p["U"].cout
+    Ch = Cout // 2 if mode == 1 else Cout
+    ctx, h = g["ctx"], g["h"]
+    if ctx.shape[0] != B or ctx.shape[1] < Cout or tuple(ctx.shape[2:]) != (H, W):
+        raise RuntimeError("gate: ctx must be [B, >= Cout, H, W]")
+    if tuple(h.shape) != (B, Ch, H, W):
+        raise RuntimeError(f"gate: h must be {(B, Ch, H, W)}")
+    e = N.SaGateEpilogue(mode, ctx.data_ptr(), _plane_bs(ctx, "ctx"), h.data_ptr(), _plane_bs(h, "h"))
+    if mode == 1:
+        o2 = g["out2"]
+        if tuple(o2.shape) != (B, Ch, H, W):
+            raise RuntimeError("gate: out2 shape mismatch")
+        e.out2, e.out2_bs = o2.data_ptr(), _plane_bs(o2, "out2")
+    elif mode == 2:
+        for k in ("z", "add"):
+            t = g[k]
+            if tuple(t.shape) != (B, Ch, H, W):
+                raise RuntimeError(f"gate: {k} shape mismatch")
+            setattr(e, k, t.data_ptr())
+            setattr(e, k + "_bs", _plane_bs(t, k))
+    else:
+        raise RuntimeError(f"gate: mode {mode}")
+    return e
+
+
 def conv2d_k3_multi(*problems) -> list:
     """Independent conv2d_k3 calls (each a dict of conv2d_k3's keyword arguments) in ONE launch:
     their blocks share the grid, so each conv's partly filled last round of blocks is filled by
     the others.  On the F(4x4,3x3) kernel when every problem meets its preconditions, else on
-    F(2x2,3x3), where all must agree on Cout % 64 == 0 and on having an input transform or not."""
+    F(2x2,3x3), where all must agree on Cout % 64 == 0 and on having an input transform or not.
+    A problem with a ``gate`` (_gate_epilogue) puts the launch on F(4x4,3x3) whatever its size."""
     if not 1 <= len(problems) <= 8:
         raise RuntimeError("conv2d_k3_multi: 1..8 convolutions per launch")
-    f4 = (_WINO4 and all(_wino4_ok(**p) for p in problems)
-          and sum(_wino4_blocks(**p) for p in problems) >= _WINO4_MIN_BLOCKS)
-    built = [_wino_problem(**p, f4=f4) for p in problems]
+    gated = any(p.get("gate") for p in problems)
+    plain = [{k: v for k, v in p.items() if k != "gate"} for p in problems]
+    for p, q in zip(problems, plain):
+        if p.get("gate") and p["gate"]["mode"] == 1:
+            q["out_cout"] = p["U"].cout // 2   # z only: r*h goes to the gate's out2
+    ok4 = _WINO4 and all(_wino4_ok(**p) for p in plain)
+    if gated and not ok4:
+        raise RuntimeError("conv2d_k3_multi: gate epilogues need the F(4x4,3x3) kernel (gate_f4_ok)")
+    f4 = ok4 and (gated or sum(_wino4_blocks(**p) for p in plain) >= _WINO4_MIN_BLOCKS)
+    built = [_wino_problem(**p, f4=f4) for p in plain]
     arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
-    N.call("sa_conv2d_k3_wino4_multi" if f4 else "sa_conv2d_k3_wino_multi", len(built), ctypes.addressof(arr),
-           _stream(problems[0]["x"]))
+    if gated:
+        gates = (N.SaGateEpilogue * len(built))(*[_gate_epilogue(p) if p.get("gate") else N.SaGateEpilogue()
+                                                  for p in problems])
+        N.call("sa_conv2d_k3_wino4_multi_gate", len(built), ctypes.addressof(arr), ctypes.addressof(gates),
+               _stream(problems[0]["x"]))
+    else:
+        N.call("sa_conv2d_k3_wino4_multi" if f4 else "sa_conv2d_k3_wino_multi", len(built), ctypes.addressof(arr),
+               _stream(problems[0]["x"]))
     return [b[1]() for b in built]
+
+
+def gate_f4_ok(*xs: torch.Tensor) -> bool:
+    """Whether GRU gate epilogues can run on convs of these inputs (F(4x4,3x3) preconditions)."""
+    return _WINO4 and all(_wino4_ok(x) for x in xs)
 
 
 def conv2d_k3(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = None, relu: bool = False,

@@ -143,6 +143,51 @@ def test_wino4_multi_stats_views(monkeypatch):
     torch.testing.assert_close(yd, F.conv2d(xb, wb, padding=1), atol=2e-5, rtol=1e-4)
 
 
+def test_wino4_gru_gate_epilogues(monkeypatch):
+    """ConvGRU gates in the F(4x4) epilogue (update.py:16-27) against the reference's expressions
+    in torch fp32: mode 1 (convz | convr over cat(h, x) -> z, r*h) on channel views of one
+    [h | x | r*h] buffer, beside a plain problem in the same launch; mode 2 (convq's r*h part ->
+    the new state, in place on h).  Two levels' shapes (8 x 128 and 16 x 64 blocks)."""
+    g = torch.Generator(device="cpu").manual_seed(42)
+
+    def r(*s):
+        return torch.randn(*s, generator=g).cuda()
+    for B, hd, xd, H, W in ((2, 128, 256, 40, 240), (1, 128, 128, 34, 60)):
+        hxr = r(B, 2 * hd + xd, H, W)
+        h, x, rh_out = hxr[:, :hd], hxr[:, hd:hd + xd], hxr[:, hd + xd:]
+        ctx = r(B, 3 * hd, H, W)
+        wz, wr, wq = (r(hd, hd + xd, 3, 3) / (3 * (hd + xd) ** 0.5) for _ in range(3))
+        bz, br, bq = r(hd), r(hd), r(hd)
+        z = torch.empty(B, hd, H, W, device=dev)
+        qx = torch.empty(B, hd, H, W, device=dev)
+        (zo, qxo), work = _run(monkeypatch, True,
+                               dict(x=hxr[:, :hd + xd], U=ops.wino_weights(torch.cat([wz, wr]).contiguous()),
+                                    bias=torch.cat([bz, br]), out=z,
+                                    gate=dict(mode=1, ctx=ctx, h=h, out2=rh_out)),
+                               dict(x=x, U=ops.wino_weights(wq[:, hd:].contiguous()), out=qx))
+        assert "conv2d_wino4" in work and zo is z and qxo is qx
+        hx = torch.cat([h, x], 1)
+        z_ref = torch.sigmoid(F.conv2d(hx, wz, bz, padding=1) + ctx[:, :hd])
+        r_ref = torch.sigmoid(F.conv2d(hx, wr, br, padding=1) + ctx[:, hd:2 * hd])
+        torch.testing.assert_close(z, z_ref, atol=3e-5, rtol=1e-4)
+        torch.testing.assert_close(rh_out, r_ref * h, atol=3e-5, rtol=1e-4)
+        torch.testing.assert_close(qx, F.conv2d(x, wq[:, hd:], padding=1), atol=1e-4, rtol=1e-4)
+        # mode 2: h <- (1 - z) h + z tanh(convq(cat(r*h, x)) + cq), the x part given as the addend
+        h0 = h.clone()
+        q_ref = torch.tanh(F.conv2d(torch.cat([rh_out, x], 1), wq, bq, padding=1) + ctx[:, 2 * hd:])
+        h_ref = (1 - z) * h0 + z * q_ref
+        (ho,), work = _run(monkeypatch, True,
+                           dict(x=rh_out, U=ops.wino_weights(wq[:, :hd].contiguous()), bias=bq, out=h,
+                                gate=dict(mode=2, ctx=ctx[:, 2 * hd:], h=h, z=z, add=qx)))
+        assert ho is h
+        torch.testing.assert_close(h, h_ref, atol=1e-4, rtol=1e-4)
+    with pytest.raises(RuntimeError):   # W % 4 != 0: no F(4x4) kernel, so no gate epilogue
+        xx = r(1, 16, 8, 10)
+        ops.conv2d_k3_multi(dict(x=xx, U=ops.wino_weights(r(64, 16, 3, 3)), out=torch.empty(1, 32, 8, 10, device=dev),
+                                 gate=dict(mode=1, ctx=r(1, 64, 8, 10), h=r(1, 32, 8, 10),
+                                           out2=torch.empty(1, 32, 8, 10, device=dev))))
+
+
 _SMALL_SHAPE_CHECK = r"""
 import torch, torch.nn.functional as F
 from stereoanywhere_amd import ops
