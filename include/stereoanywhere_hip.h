@@ -300,8 +300,10 @@ typedef struct SaGateEpilogue {
   float *out2;
   long out2_bs;
 } SaGateEpilogue;
+/* block_shape: 0 / 1 large blocks (8 waves, 64 Winograd tiles, one per CU), 2 small blocks (4
+ * waves, 32 tiles, two per CU: shorter launches of few rounds fill the chip better). */
 int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
-                                  void *stream);
+                                  int block_shape, void *stream);
 
 /* Direct KxK convolution (padding K/2, no bias) on fp32 MFMA for the encoder convs the
  * Winograd kernel does not cover (extractor.py:22-40, 91, 208):

@@ -72,7 +72,7 @@ SIGNATURES = {
     "sa_conv2d_wino4_weights": (I, [P, I, I, P, P]),
     "sa_conv2d_k3_wino4_stat_parts": (L, [I, I]),
     "sa_conv2d_k3_wino4_multi": (I, [I, P, P]),
-    "sa_conv2d_k3_wino4_multi_gate": (I, [I, P, P, P]),
+    "sa_conv2d_k3_wino4_multi_gate": (I, [I, P, P, I, P]),
     "sa_conv_direct_weights": (I, [P, I, I, I, I, I, P, P]),
     "sa_conv_direct_weights_size": (L, [I, I, I, I, I]),
     "sa_conv_direct_stat_parts": (L, [I, I]),

@@ -593,19 +593,21 @@ extern "C" long sa_conv2d_k3_wino4_stat_parts(int H, int W) {
 }
 
 extern "C" int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, void *stream) {
-  return sa_conv2d_k3_wino4_multi_gate(nprob, probs, nullptr, stream);
+  return sa_conv2d_k3_wino4_multi_gate(nprob, probs, nullptr, 0, stream);
 }
 
 extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
-                                             void *stream) {
+                                             int block_shape, void *stream) {
   SA_REQUIRE(nprob >= 1 && nprob <= MAX_PROB && probs, "sa_conv2d_k3_wino4_multi: 1..%d problems", MAX_PROB);
-  static const int shape = [] {   // SA_W4_SHAPE=big|small forces one block shape (A/B runs)
+  SA_REQUIRE(block_shape >= 0 && block_shape <= 2, "sa_conv2d_k3_wino4_multi: block_shape 0..2");
+  static const int env_shape = [] {   // SA_W4_SHAPE=big|small forces one block shape (A/B runs)
     const char *e = getenv("SA_W4_SHAPE");
     return e && e[0] == 's' ? 2 : e && e[0] == 'b' ? 1 : 0;
   }();
-  // Large blocks by default.  The small shape measured 2-8% faster on standalone launches of
-  // Cin <= 128 with a few rounds of blocks (qh08, convc2) but not faster in the forward (91.7
-  // vs 91.0 ms/step with it on those launches), so it is an A/B option only.
+  // Large blocks unless the caller asks for small ones (block_shape 2).  The small shape
+  // measured 2-8% faster on standalone launches of Cin <= 128 with a few rounds of blocks
+  // (qh08, convc2) but not faster in the forward as a blanket choice.
+  const int shape = env_shape ? env_shape : block_shape;
   const bool small = shape == 2;
   const int nt = small ? W4Small::NT : W4Big::NT;
   W4Launch L{};

@@ -62,6 +62,9 @@ _FUSE_GATES = os.environ.get("SA_FUSE_GATES", "1") != "0"
 # ... and the state update in the r*h conv's epilogue (SA_FUSE_OUT=0: gru_out kernel, r*h conv
 # split over its input channels)
 _FUSE_OUT = os.environ.get("SA_FUSE_OUT", "1") != "0"
+# launches of the update block on F(4x4)'s small blocks (two per CU), by name: "q16" (gru16's
+# r*h conv + the motion conv), "q08" (gru08's + gru32's r*h convs), "zr16", "zr08", "pro32"
+_SMALL_LAUNCHES = set(filter(None, os.environ.get("SA_SMALL_LAUNCHES", "").split(",")))
 
 class StereoAnywhere(nn.Module):
     def __init__(self, args):
@@ -321,10 +324,10 @@ class StereoAnywhere(nn.Module):
         cq = [c[:, 256:384] for c in ctx]
         lvl = {"08": 0, "16": 1, "32": 2}
 
-        def conv_group(*probs):
+        def conv_group(*probs, name=None):
             """Independent 3x3 convs in one launch (SA_GROUP_CONVS=0: one launch each)."""
             if _GROUP_CONVS:
-                return ops.conv2d_k3_multi(*probs)
+                return ops.conv2d_k3_multi(*probs, small_blocks=name in _SMALL_LAUNCHES)
             return [ops.conv2d_k3(**p) for p in probs]
 
         def gate_x_h(key, x, h):
@@ -377,9 +380,9 @@ class StereoAnywhere(nn.Module):
         # is deterministic and reads the same inputs as in the reference order: the result is
         # identical, with fewer and fuller conv launches.
         ops.pool2x(h16, x32)
-        xc32, hzr32 = conv_group(*gate_x_h("32", x32, h32))
+        xc32, hzr32 = conv_group(*gate_x_h("32", x32, h32), name="pro32")
         gru_zr(2, "32", h32, xc32, hzr32)
-        q_finish(2, "32", xc32, conv_group(*q_probs("32", False)))
+        q_finish(2, "32", xc32, conv_group(*q_probs("32", False), name="pro32"))
         for it in range(iters):
             last = it == iters - 1
             # lookup of both pyramids + convc1 + ReLU in one kernel (sample 2b: stereo, 2b+1: mono)
@@ -393,12 +396,13 @@ class StereoAnywhere(nn.Module):
             mconv = [dict(x=c1v[:, v], U=dw["U_c2"], bias=enc.convc2.bias, relu=True,
                           out=motin[:, 64 * v:64 * v + 64]) for v in range(2)]
             mconv.append(dict(x=fl, U=dw["U_f2"], bias=enc.convf2.bias, relu=True, out=motin[:, 128:192]))
-            xc16, hzr16 = conv_group(*gate_x_h("16", x16, h16), *mconv)[:2]
+            xc16, hzr16 = conv_group(*gate_x_h("16", x16, h16), *mconv, name="zr16")[:2]
             gru_zr(1, "16", h16, xc16, hzr16)
             # gru16's r*h conv + the motion conv (_conv: 126 outputs, padded to 128, into
             # x08[:, :128]; channels 126-127 (the flow) are rewritten right after)
             qp = q_probs("16", False)
-            res = conv_group(*qp, dict(x=motin, U=dw["U_mot"], bias=dw["mot_b"], relu=True, out=x08[:, :128]))
+            res = conv_group(*qp, dict(x=motin, U=dw["U_mot"], bias=dw["mot_b"], relu=True, out=x08[:, :128]),
+                             name="q16")
             q_finish(1, "16", xc16, res[:len(qp)])
             ops.flow_update(coords_x, None, None, x08[:, 126:128])
             ops.interp(h16, x08[:, 128:])
@@ -407,7 +411,7 @@ class StereoAnywhere(nn.Module):
             if not last:
                 ops.pool2x(h16, x32)
                 probs += gate_x_h("32", x32, h32)
-            res = conv_group(*probs)
+            res = conv_group(*probs, name="zr08")
             xc08, hzr08 = res[:2]
             gru_zr(0, "08", h08, xc08, hzr08)
             qp = q_probs("08", True)
@@ -416,7 +420,7 @@ class StereoAnywhere(nn.Module):
                 xc32, hzr32 = res[2:]
                 gru_zr(2, "32", h32, xc32, hzr32)
                 probs += q_probs("32", True)
-            qh = conv_group(*probs)
+            qh = conv_group(*probs, name="q08")
             q_finish(0, "08", xc08, qh[:len(qp)])
             if not last:
                 q_finish(2, "32", xc32, qh[len(qp):])

@@ -617,12 +617,13 @@ def _gate_epilogue(p: dict) -> "N.SaGateEpilogue":
     return e
 
 
-def conv2d_k3_multi(*problems) -> list:
+def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     """Independent conv2d_k3 calls (each a dict of conv2d_k3's keyword arguments) in ONE launch:
     their blocks share the grid, so each conv's partly filled last round of blocks is filled by
     the others.  On the F(4x4,3x3) kernel when every problem meets its preconditions, else on
     F(2x2,3x3), where all must agree on Cout % 64 == 0 and on having an input transform or not.
-    A problem with a ``gate`` (_gate_epilogue) puts the launch on F(4x4,3x3) whatever its size."""
+    A problem with a ``gate`` (_gate_epilogue) puts the launch on F(4x4,3x3) whatever its size.
+    small_blocks: F(4x4)'s small block shape (two blocks per CU) for this launch."""
     if not 1 <= len(problems) <= 8:
         raise RuntimeError("conv2d_k3_multi: 1..8 convolutions per launch")
     gated = any(p.get("gate") for p in problems)
@@ -636,11 +637,11 @@ def conv2d_k3_multi(*problems) -> list:
     f4 = ok4 and (gated or sum(_wino4_blocks(**p) for p in plain) >= _WINO4_MIN_BLOCKS)
     built = [_wino_problem(**p, f4=f4) for p in plain]
     arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
-    if gated:
+    if f4 and (gated or small_blocks):
         gates = (N.SaGateEpilogue * len(built))(*[_gate_epilogue(p) if p.get("gate") else N.SaGateEpilogue()
                                                   for p in problems])
         N.call("sa_conv2d_k3_wino4_multi_gate", len(built), ctypes.addressof(arr), ctypes.addressof(gates),
-               _stream(problems[0]["x"]))
+               2 if small_blocks else 0, _stream(problems[0]["x"]))
     else:
         N.call("sa_conv2d_k3_wino4_multi" if f4 else "sa_conv2d_k3_wino_multi", len(built), ctypes.addressof(arr),
                _stream(problems[0]["x"]))
