@@ -15,7 +15,7 @@ Hot path, one kernel family per row:
   a8+a11 scaled mono, mirror detector, initial coordinates               sa_mono_scale_mirror
   a1+a8+a9 stereo volume x truncation -> pyramid, one fp32-MFMA kernel  sa_corr_volume_pyramid
   a10    stereo + mono pyramid lookups, one launch per iteration         sa_corr_lookup
-  a12    GRU gates fused; convs split by input so no torch.cat          sa_gru_zr / sa_gru_out
+  a12    GRU gates in the conv epilogues over [h | x | r*h] buffers    sa_conv2d_k3_wino4_multi_gate
   a14    convex upsampling of the final flow                            sa_convex_upsample
 Training (test_mode=False), vol_downsample > 0 and use_aggregate_stereo_vol are outside
 this tier and raise NotImplementedError.  use_truncate_vol / use_aggregate_mono_vol may be
