@@ -168,8 +168,8 @@ __device__ __forceinline__ void bt6h(const float x0, const float x1, const float
 __device__ unsigned long long g_w4_clock[65536][10];   // + [8] chunk 0 issued, [9] last wave's start
 #endif
 
-template <class C, int HF, int LTW>
-__device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate &GT, const unsigned wid, float *smem) {
+template <class C, int HF, int LTW, bool GATED>
+__device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, const unsigned wid, float *smem) {
   constexpr int NWAVE = C::NW, NTHR = C::NTHR, KC = C::KC, JPC = C::JPC, NT = C::NT, PDMA = C::PDMA,
                 UDMA = C::UDMA, UPW = C::UPW, UBUF = C::UBUF, BUF = C::BUF, PBUF = C::PBUF, OPP = C::OPP;
   const int Cin = P.Cin, H = P.H, W = P.W, Cout = P.Cout;
@@ -437,6 +437,24 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate &GT, const
 #endif
   // float4 stores: NT * 4 per channel plane of the block
   float *dst = P.out + (long)n * P.out_bs;
+  if constexpr (!GATED) {
+#pragma unroll 4
+    for (int j = 0; j < (CO * NT * 16) / (4 * NTHR); ++j) {
+      const int i4 = tid + NTHR * j;
+      const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
+      const int y = y0 + r, x = x0 + cx;
+      if (y < H && x < W)
+        *reinterpret_cast<f32x4 *>(dst + (long)(co0 + c) * hw + (long)y * W + x) =
+            *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
+    }
+    return;
+  } else {
+  // GRU gates (update.py:16-27): conv (+ bias, staged) + context, then
+  //   mode 1 (z | r over cat(h, x)): z = sigmoid(.) -> out, r * h -> out2 (block-uniform half)
+  //   mode 2 (q over r*h):           h' = (1 - z) h + z tanh(. + add) -> out (in place on h)
+  // the gate parameters are read here, not at the kernel's start (they would lengthen the
+  // prologue before chunk 0's DMA)
+  const W4Gate &GT = *gate;
   if (GT.mode == 0) {
 #pragma unroll 4
     for (int j = 0; j < (CO * NT * 16) / (4 * NTHR); ++j) {
@@ -449,9 +467,6 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate &GT, const
     }
     return;
   }
-  // GRU gates (update.py:16-27): conv (+ bias, staged) + context, then
-  //   mode 1 (z | r over cat(h, x)): z = sigmoid(.) -> out, r * h -> out2 (block-uniform half)
-  //   mode 2 (q over r*h):           h' = (1 - z) h + z tanh(. + add) -> out (in place on h)
   const int half = Cout / 2;
   const bool rhalf = co0 >= half;
   const float *ctxb = GT.ctx + (long)n * GT.ctx_bs;
@@ -490,25 +505,22 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate &GT, const
       }
     }
   }
+  }
 }
 
-template <class C>
+template <class C, bool GATED>
 __global__ __launch_bounds__(C::NTHR, C::NW == 8 ? 1 : 2) void wino_f4k3_kernel(const W4Launch L) {
   // problem of the block from its raw id (ranges padded to multiples of 8: every XCD gets an
   // equal share of each problem), then the L2-locality remap within it (conv2d_wino.hip)
   const unsigned g = blockIdx.x;
-  W4Prob P = L.p[0];
-  unsigned base = 0, nb = L.nblk[0];
+  // the problem index from the range ends alone, then only that problem's fields are loaded
+  // (selecting among all eight by value loaded every one of them: ~70 scalar loads before the
+  // first DMA)
   int pi = 0;
 #pragma unroll
-  for (int i = 1; i < MAX_PROB; ++i) {
-    if (i < L.nprob && g >= L.end[i - 1]) {
-      P = L.p[i];
-      base = L.end[i - 1];
-      nb = L.nblk[i];
-      pi = i;
-    }
-  }
+  for (int i = 1; i < MAX_PROB; ++i) pi += (i < L.nprob && g >= L.end[i - 1]) ? 1 : 0;
+  const W4Prob &P = L.p[pi];
+  const unsigned base = pi ? L.end[pi - 1] : 0u, nb = L.nblk[pi];
   if (g - base >= nb) return;
   __shared__ __attribute__((aligned(16))) float smem[C::SMEM];
 #ifdef SA_W4_CLOCK
@@ -518,11 +530,11 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 ? 1 : 2) void wino_f4k3_kernel(
   // the first half of the waves takes point columns 0-2, the second half 3-5 (wave-uniform)
   const unsigned wid = sa::xcd_remap(g - base, nb);
   if (threadIdx.x < C::NTHR / 2) {
-    if (P.ltw == 4) w4_body<C, 0, 4>(P, L.gate[pi], wid, smem);
-    else w4_body<C, 0, 5>(P, L.gate[pi], wid, smem);
+    if (P.ltw == 4) w4_body<C, 0, 4, GATED>(P, GATED ? &L.gate[pi] : nullptr, wid, smem);
+    else w4_body<C, 0, 5, GATED>(P, GATED ? &L.gate[pi] : nullptr, wid, smem);
   } else {
-    if (P.ltw == 4) w4_body<C, 1, 4>(P, L.gate[pi], wid, smem);
-    else w4_body<C, 1, 5>(P, L.gate[pi], wid, smem);
+    if (P.ltw == 4) w4_body<C, 1, 4, GATED>(P, GATED ? &L.gate[pi] : nullptr, wid, smem);
+    else w4_body<C, 1, 5, GATED>(P, GATED ? &L.gate[pi] : nullptr, wid, smem);
   }
 #ifdef SA_W4_CLOCK
   if (threadIdx.x == 0 && g < 65536) {
@@ -612,6 +624,7 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
   const int nt = small ? W4Small::NT : W4Big::NT;
   W4Launch L{};
   long total = 0;
+  bool gated = false;
   for (int i = 0; i < nprob; ++i) {
     const SaWinoProblem &q = probs[i];
     SA_REQUIRE(q.in && q.U && q.out && q.N > 0 && q.H > 0 && q.W > 0, "sa_conv2d_k3_wino4: bad arguments");
@@ -643,6 +656,7 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
         SA_REQUIRE(e.z && e.add && a16(e.z) && a16(e.add) && e.z_bs % 4 == 0 && e.add_bs % 4 == 0,
                    "sa_conv2d_k3_wino4: state gate needs aligned z and addend planes");
       L.gate[i] = W4Gate{e.mode, e.ctx, e.ctx_bs, e.h, e.h_bs, e.z, e.z_bs, e.add, e.add_bs, e.out2, e.out2_bs};
+      gated = true;
     }
     const long nb = (long)q.N * L.p[i].tiles_hw * L.p[i].co_blocks;
     total = (i + 1 < nprob ? (total + nb + 7) / 8 * 8 : total + nb);
@@ -658,8 +672,10 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV2D_W4, s);
   if (small)
-    wino_f4k3_kernel<W4Small><<<(unsigned)total, W4Small::NTHR, 0, s>>>(L);
+    gated ? wino_f4k3_kernel<W4Small, true><<<(unsigned)total, W4Small::NTHR, 0, s>>>(L)
+          : wino_f4k3_kernel<W4Small, false><<<(unsigned)total, W4Small::NTHR, 0, s>>>(L);
   else
-    wino_f4k3_kernel<W4Big><<<(unsigned)total, W4Big::NTHR, 0, s>>>(L);
+    gated ? wino_f4k3_kernel<W4Big, true><<<(unsigned)total, W4Big::NTHR, 0, s>>>(L)
+          : wino_f4k3_kernel<W4Big, false><<<(unsigned)total, W4Big::NTHR, 0, s>>>(L);
   return sa::check_launch("sa_conv2d_k3_wino4");
 }
