@@ -46,6 +46,12 @@ def wino_table(*modules: nn.Module) -> WinoTable:
 
 _WINO: WinoTable = {}
 
+# BatchNorm encoders: a residual block's conv1 with its eval norm1 folded in, keyed by conv1's
+# weight storage: (Winograd filters of s * W1, bias t - s * m), so ReLU(N1(conv1(x))) is one
+# conv with a bias + ReLU epilogue (fold_table)
+FoldTable = Dict[int, Tuple["ops.WinoFilters", torch.Tensor]]
+_FOLD: FoldTable = {}
+
 # arranged weights of the convs on the direct fp32-MFMA kernel (ops.conv_direct), keyed by the
 # 3x3 / 7x7 conv's weight storage: (conv weights, fused 1x1 downsample weights or None)
 DirectTable = Dict[int, Tuple[torch.Tensor, Optional[torch.Tensor]]]
@@ -153,7 +159,13 @@ def residual_block(blk: nn.Module, name: str, x: torch.Tensor, fin: _Finisher) -
         c2, s2 = _conv_k3(c1, blk.conv2, fin, in_aff=fin.affine(name + ".norm1", c1, s1))
         return ops.norm_act(c2, fin.affine(name + ".norm2", c2, s2), act_in="relu", skip=d,
                             skip_aff=fin.affine(name + ".norm3", d, sd), act_out="relu", out=c2)
-    if w1 in _WINO and w2 in _WINO:
+    fold = _FOLD.get(w1)
+    if fold is not None and w2 in _WINO and blk.conv1.stride == (1, 1) and ops.wino4_applies(x, _WINO[w2]):
+        # eval BatchNorm: norm1 + ReLU in conv1's epilogue (folded weights), so conv2 reads y1
+        # on the F(4x4) kernel without a norm_act pass in between
+        y1 = ops.conv2d_k3(x, fold[0], fold[1], relu=True)
+        c2, s2 = _conv_k3(y1, blk.conv2, fin)
+    elif w1 in _WINO and w2 in _WINO:
         # y1 = relu(N1(c1)) is never written: conv2 applies it while loading c1
         c1, s1 = _conv_k3(x, blk.conv1, fin)
         c2, s2 = _conv_k3(c1, blk.conv2, fin, in_aff=fin.affine(name + ".norm1", c1, s1))
@@ -189,9 +201,16 @@ def residual_blocks_grouped(blks, names, xs, fin: _Finisher) -> List[torch.Tenso
                                          stats=fin.instance) for x, U, a in zip(inputs, Us, affs)])
         return [r if fin.instance else (r, None) for r in res]
 
-    r1 = stage([b.conv1 for b in blks], list(xs), [None] * len(blks))
-    a1 = [fin.affine(n + ".norm1", c, st) for n, (c, st) in zip(names, r1)]
-    r2 = stage([b.conv2 for b in blks], [c for c, _ in r1], a1)
+    folds = [_FOLD.get(b.conv1.weight.data_ptr()) for b in blks]
+    U2 = [_WINO[b.conv2.weight.data_ptr()] for b in blks]
+    if all(f is not None for f in folds) and ops.wino4_applies(xs[0], U2[0], *zip(xs[1:], U2[1:])):
+        # eval BatchNorm folded into conv1 (residual_block): y1 straight from the epilogue
+        y1 = ops.conv2d_k3_multi(*[dict(x=x, U=f[0], bias=f[1], relu=True) for x, f in zip(xs, folds)])
+        r2 = stage([b.conv2 for b in blks], y1, [None] * len(blks))
+    else:
+        r1 = stage([b.conv1 for b in blks], list(xs), [None] * len(blks))
+        a1 = [fin.affine(n + ".norm1", c, st) for n, (c, st) in zip(names, r1)]
+        r2 = stage([b.conv2 for b in blks], [c for c, _ in r1], a1)
     return [ops.norm_act(c2, fin.affine(n + ".norm2", c2, s2), act_in="relu", skip=x, act_out="relu", out=c2)
             for n, (c2, s2), x in zip(names, r2, xs)]
 
@@ -221,11 +240,13 @@ def _stage(seq: nn.Sequential, name: str, x: torch.Tensor, fin: _Finisher) -> to
     return x
 
 
-def _install(wino: Optional[WinoTable], direct: Optional[DirectTable]) -> None:
+def _install(wino: Optional[WinoTable], direct: Optional[DirectTable], fold: Optional[FoldTable] = None) -> None:
     _WINO.clear()
     _WINO.update(wino or {})
     _DIRECT.clear()
     _DIRECT.update(direct or {})
+    _FOLD.clear()
+    _FOLD.update(fold or {})
 
 
 def fnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
@@ -240,11 +261,12 @@ def fnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
 
 
 def cnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
-                 wino: WinoTable = None, direct: DirectTable = None) -> List[List[torch.Tensor]]:
+                 wino: WinoTable = None, direct: DirectTable = None,
+                 fold: FoldTable = None) -> List[List[torch.Tensor]]:
     """MultiBasicEncoder.forward (extractor.py:156-300) up to the head convs, whose outputs
     are returned RAW (bias not added) as [[h08, c08], [h16, c16], [h32, c32]]; the caller
     finishes them (tanh / relu with the bias) in one pass each."""
-    _install(wino, direct)
+    _install(wino, direct, fold)
     fin = _Finisher("instance" if isinstance(enc.norm1, nn.InstanceNorm2d) else "batch", table)
     x = _stem(enc, x, fin)
     for s in ("layer1", "layer2", "layer3"):
@@ -261,6 +283,23 @@ def cnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
         return _convs_grouped([q[1] for q in seqs], rs)
     return [heads(enc.outputs08, "outputs08", s08), heads(enc.outputs16, "outputs16", s16),
             _convs_grouped(list(enc.outputs32), [s32] * len(enc.outputs32))]
+
+
+def fold_table(enc: nn.Module) -> FoldTable:
+    """conv1 of every residual block of a BatchNorm encoder whose conv1 qualifies for Winograd,
+    with its eval norm1 folded in: y = (c + b - mu) g / sqrt(var + eps) + beta = conv(x; s W) +
+    (t - s m), s = g / sqrt(var + eps), m = mu - b, t = beta (bn_affine)."""
+    if not isinstance(enc.norm1, nn.BatchNorm2d):
+        return {}
+    t: FoldTable = {}
+    with torch.no_grad():
+        for blk in enc.modules():
+            if hasattr(blk, "conv1") and hasattr(blk, "norm2") and isinstance(blk.norm1, nn.BatchNorm2d) \
+                    and wino_eligible(blk.conv1):
+                a = bn_affine(blk.norm1, blk.conv1.bias)
+                w = (blk.conv1.weight * a.s[:, None, None, None]).contiguous()
+                t[blk.conv1.weight.data_ptr()] = (ops.wino_weights(w), (a.t - a.s * a.m).contiguous())
+    return t
 
 
 def bn_table(enc: nn.Module) -> Dict[str, ops.Affine]:

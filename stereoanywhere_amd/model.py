@@ -141,6 +141,8 @@ class StereoAnywhere(nn.Module):
                 # Winograd F(2x2,3x3) filters (ops.conv2d_k3) of every eligible 3x3 conv
                 d = self._derived
                 d["wino"] = encoders.wino_table(self.cnet, self.fnet)
+                # eval-BatchNorm norm1 folded into the context encoder's conv1s
+                d["fold_cnet"] = encoders.fold_table(self.cnet)
                 # the stems and the stride-2 blocks on the direct fp32-MFMA conv (ops.conv_direct)
                 # (SA_DIRECT_CONV=0 leaves them on MIOpen, for A/B timing)
                 d["direct"] = (encoders.direct_table(self.cnet, self.fnet)
@@ -222,7 +224,8 @@ class StereoAnywhere(nn.Module):
             ctx = [conv(torch.relu(x[1])) for x, conv in zip(cl, self.context_zqr_convs)]
             fm = self.fnet(torch.cat([image2, image3], 0))
         else:
-            cl = encoders.cnet_forward(self.cnet, mde2.repeat(1, 3, 1, 1), dw["bn_cnet"], dw["wino"], dw["direct"])
+            cl = encoders.cnet_forward(self.cnet, mde2.repeat(1, 3, 1, 1), dw["bn_cnet"], dw["wino"], dw["direct"],
+                                       dw["fold_cnet"])
             hid, cs = [], []
             for (h_raw, c_raw), (hb, cb) in zip(cl, dw["head_b"]):
                 hid.append(ops.norm_act(h_raw, ops.Affine(t=hb), act_in="tanh", out=h_raw))
