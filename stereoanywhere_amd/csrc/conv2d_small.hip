@@ -8,6 +8,8 @@
 // wave-uniform (scalar) weights; bias and ReLU are applied in the epilogue.
 #include "sa_common.h"
 
+#include <cstdint>
+
 // Convolution sums have no reference summation order to reproduce (MIOpen picks its own
 // algorithm), so let a*b+c contract to (packed) FMA here; the library builds with
 // -ffp-contract=off for the element-wise kernels that mirror torch expressions.
@@ -55,6 +57,89 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const float *__restri
       float r = acc[co] + (bias ? bias[co] : 0.0f);
       if (relu) r = fmaxf(r, 0.0f);
       out[(long)b * out_bs + (long)co * H * W + (long)y * W + x] = r;
+    }
+  }
+}
+
+// The flow stem (Cin 2, 7x7, 64 outputs) as an implicit GEMM on fp32 MFMA: M = pixels, N = 64
+// output channels, K = 2 * 49 taps (padded to 100).  Block = 16 x 16 pixels, its halo staged in
+// LDS once; wave w owns rows 4w .. 4w + 3 (four 16-pixel M-tiles).  v_mfma_f32_16x16x4_f32 lane
+// (m = l % 16, k = l / 16) reads A = the tile pixel m's tap 4 j + k (one ds_read feeds the
+// MFMAs of all four 16-channel blocks); the B operands (weights, tap 4 j + k, channel 16 cb +
+// l % 16) stay in 100 VGPRs for the block's lifetime.  Accumulator lane l holds pixels
+// 4 (l / 16) .. + 3 of channel l % 16: one float4 store per (M-tile, channel block).
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+constexpr int F1_K = 7, F1_CIN = 2, F1_TAPS = F1_CIN * F1_K * F1_K, F1_KS = (F1_TAPS + 3) / 4, F1_L = T + F1_K - 1;
+
+__global__ __launch_bounds__(256) void conv2d_f1_mfma_kernel(const float *__restrict__ in, long in_bs, int H, int W,
+                                                             const float *__restrict__ wt,
+                                                             const float *__restrict__ bias, int relu,
+                                                             float *__restrict__ out, long out_bs) {
+  __shared__ float tile[F1_CIN * F1_L * F1_L + 4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int x0 = blockIdx.x * T, y0 = blockIdx.y * T, b = blockIdx.z;
+  const int m = lane & 15, kq = lane >> 4;
+  // weights -> B operands: tap 4 j + kq, channel 16 cb + m (taps >= 98 are zero)
+  float wb[F1_KS][4];
+#pragma unroll
+  for (int j = 0; j < F1_KS; ++j) {
+    const int tap = 4 * j + kq;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) wb[j][cb] = tap < F1_TAPS ? wt[tap * 64 + 16 * cb + m] : 0.0f;
+  }
+  // LDS offsets of each tap (ci, ky, kx) relative to the pixel's window origin
+  int toff[F1_KS];
+#pragma unroll
+  for (int j = 0; j < F1_KS; ++j) {
+    const int tap = min(4 * j + kq, F1_TAPS - 1);
+    const int ci = tap / (F1_K * F1_K), r = tap % (F1_K * F1_K);
+    toff[j] = ci * F1_L * F1_L + (r / F1_K) * F1_L + r % F1_K;
+  }
+  const float *src = in + (long)b * in_bs;
+  for (int i = threadIdx.x; i < F1_CIN * F1_L * F1_L; i += 256) {
+    const int ci = i / (F1_L * F1_L), r = i % (F1_L * F1_L);
+    const int yy = y0 - 3 + r / F1_L, xx = x0 - 3 + r % F1_L;
+    tile[i] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? src[(long)ci * H * W + (long)yy * W + xx] : 0.0f;
+  }
+  __syncthreads();
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) acc[t][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < F1_KS; ++j) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float a = tile[toff[j] + (4 * wv + t) * F1_L + m];
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) acc[t][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[j][cb], acc[t][cb], 0, 0, 0);
+    }
+  }
+  // D lane layout: pixel 4 kq + i of the M-tile row, channel 16 cb + m
+  const long hw = (long)H * W;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int y = y0 + 4 * wv + t, x = x0 + 4 * kq;
+    if (y >= H) continue;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int co = 16 * cb + m;
+      const float bv = bias ? bias[co] : 0.0f;
+      f32x4 v = acc[t][cb];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] += bv;
+        if (relu) v[e] = fmaxf(v[e], 0.0f);
+      }
+      float *dst = out + (long)b * out_bs + co * hw + (long)y * W + x;
+      if (x + 3 < W && (W & 3) == 0) {
+        *reinterpret_cast<f32x4 *>(dst) = v;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (x + e < W) dst[e] = v[e];
+      }
     }
   }
 }
@@ -189,6 +274,10 @@ extern "C" int sa_conv2d_small(const float *in, long in_bs, int B, int Cin, int 
   dim3 grid((W + T - 1) / T, (H + T - 1) / T, B);
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_MISC, s);
-  conv2d_small_kernel<7, 64><<<grid, 256, 0, s>>>(in, in_bs, Cin, H, W, weight, bias, relu, out, out_bs);
+  const bool aligned = (reinterpret_cast<uintptr_t>(out) & 15) == 0 && out_bs % 4 == 0;
+  if (Cin == F1_CIN && aligned)
+    conv2d_f1_mfma_kernel<<<grid, 256, 0, s>>>(in, in_bs, H, W, weight, bias, relu, out, out_bs);
+  else
+    conv2d_small_kernel<7, 64><<<grid, 256, 0, s>>>(in, in_bs, Cin, H, W, weight, bias, relu, out, out_bs);
   return sa::check_launch("sa_conv2d_small");
 }

@@ -320,8 +320,13 @@ def test_timing_counts_launches():
 
 
 def test_conv2d_small_matches_torch():
+    """convf1 (2 -> 64, 7x7): the MFMA implicit-GEMM kernel at ragged and model sizes."""
+    for (B, H, W) in ((2, 37, 53), (4, 136, 240), (1, 16, 16)):
+        _conv2d_small_case(B, H, W)
+
+
+def _conv2d_small_case(B, H, W):
     rng = np.random.default_rng(21)
-    B, H, W = 2, 37, 53
     x = g(rng.standard_normal((B, 2, H, W)))
     w = g(rng.standard_normal((64, 2, 7, 7)) * 0.1)
     b = g(rng.standard_normal(64) * 0.1)
