@@ -63,6 +63,12 @@ int sa_corr_volume_pyramid(const float *fmap2, const float *fmap3, int B, int C,
  *   volume: `rows` rows of W2 floats with stride in_row_stride (level 0 is copied). */
 int sa_corr_pyramid_from_volume(const float *volume, long rows, int W2, long in_row_stride,
                                 int num_levels, float *pyramid, long row_stride, void *stream);
+/* The same pyramid from a volume whose element (b, h, j, k) sits at volume + b*sb + h*sh + j +
+ * k*sk (W1 contiguous, W2 <= 256: the hourglass's [B, 1, W2, H, W1] classifier output, used as
+ * the mono volume with use_aggregate_mono_vol, stereoanywhere.py:168, 210); pyramid rows in
+ * (b, h, j) order as above. */
+int sa_corr_pyramid_from_volume_strided(const float *volume, int B, int H, int W1, int W2, long sb, long sh, long sk,
+                                        int num_levels, float *pyramid, long row_stride, void *stream);
 
 /* a10 — CorrBlock1D.__call__ (corr.py:93-115) + bilinear_sampler (utils.py:19-35).
  *   coords_x: x channel of coords1, element (b,h,j) at coords_x[b*coords_bstride + h*W1 + j]

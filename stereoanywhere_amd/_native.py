@@ -43,6 +43,7 @@ SIGNATURES = {
     "sa_pyramid_row_stride": (L, [I, I]),
     "sa_corr_volume_pyramid": (I, [P, P, I, I, I, I, I, F, P, P, F, I, P, L, P]),
     "sa_corr_pyramid_from_volume": (I, [P, L, I, L, I, P, L, P]),
+    "sa_corr_pyramid_from_volume_strided": (I, [P, I, I, I, I, L, L, L, I, P, L, P]),
     "sa_corr_lookup": (I, [P, P, I, L, I, I, P, L, I, I, I, P, L, P]),
     "sa_corr_lookup_conv1x1": (I, [P, P, I, L, I, I, P, L, I, I, I, P, P, I, P, P]),
     "sa_mono_normals": (I, [P, I, I, I, F, P, P]),

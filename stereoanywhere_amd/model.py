@@ -275,7 +275,7 @@ class StereoAnywhere(nn.Module):
                                                   float(a.mirror_attenuation))
         del fmap2, fmap3
         if a.use_aggregate_mono_vol:
-            mono_rows = vol_d.permute(0, 1, 3, 4, 2).contiguous()  # [B,1,H,W1,W2]
+            mono_rows = vol_d.permute(0, 1, 3, 4, 2)  # [B,1,H,W1,W2] view (transposed by the pyramid kernel)
         else:
             # raw mono volume 1.73 * corr(normals) (stereoanywhere.py:136, 210)
             mono_rows = 1.73 * ops.corr_volume(n2, n3)

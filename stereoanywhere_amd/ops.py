@@ -101,9 +101,18 @@ def corr_volume(fmap2: torch.Tensor, fmap3: torch.Tensor) -> torch.Tensor:
 
 
 def pyramid_from_volume(volume: torch.Tensor, num_levels: int = 4) -> torch.Tensor:
-    """CorrBlock1D.__init__ on an existing volume [..., W2] (rows contiguous along W2)."""
+    """CorrBlock1D.__init__ on an existing volume [..., W2] (rows contiguous along W2), or on a
+    [B, 1, H, W1, W2] view whose W1 axis is the contiguous one (W2 <= 256)."""
     _check(volume, "volume", contiguous=False)
     W2 = volume.shape[-1]
+    if volume.dim() == 5 and volume.shape[1] == 1 and volume.stride(-1) != 1 and volume.stride(3) == 1:
+        # [B, 1, H, W1, W2] view of a [B, 1, W2, H, W1] volume: transposed while staging
+        B, _, H, W1, _ = volume.shape
+        rs = pyramid_geometry(W2, num_levels)[0]
+        out = torch.empty((B * H * W1, rs), device=volume.device, dtype=torch.float32)
+        N.call("sa_corr_pyramid_from_volume_strided", volume.data_ptr(), B, H, W1, W2, volume.stride(0),
+               volume.stride(2), volume.stride(4), num_levels, out.data_ptr(), rs, _stream(volume))
+        return out
     rows2d = volume.reshape(-1, W2)
     if rows2d.stride(1) != 1:
         raise RuntimeError("volume rows must be contiguous along the last axis")

@@ -69,6 +69,20 @@ def test_truncated_pyramid():
         np.testing.assert_allclose(lv, rv, atol=tol)
 
 
+@pytest.mark.parametrize("B,H,W1,W2", [(2, 3, 70, 61), (1, 2, 64, 256), (4, 5, 240, 240)])
+def test_pyramid_from_strided_volume(B, H, W1, W2):
+    """The hourglass layout [B,1,W2,H,W1] viewed as [B,1,H,W1,W2] (W1 contiguous) gives the
+    same pyramid, bit for bit, as its contiguous permute (the LDS-transposing kernel)."""
+    rng = np.random.default_rng(W1 + W2)
+    v = g(rng.standard_normal((B, 1, W2, H, W1)))
+    view = v.permute(0, 1, 3, 4, 2)
+    got = c(ops.pyramid_from_volume(view, 4))
+    ref = c(ops.pyramid_from_volume(view.contiguous(), 4))
+    _, offs, wids = ops.pyramid_geometry(W2, 4)
+    used = offs[-1] + wids[-1]   # the row's padding to 4 floats is never written
+    np.testing.assert_array_equal(got[:, :used], ref[:, :used])
+
+
 def test_pyramid_from_volume_and_lookup_edges(micro):
     vol = micro["corr.out"][:, :, :, 0]  # [2,3,37,45]
     B, H, W1, W2 = vol.shape
