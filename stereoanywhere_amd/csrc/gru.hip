@@ -143,6 +143,34 @@ __global__ __launch_bounds__(256) void interp_kernel(const float *__restrict__ i
   out[b * out_bs + (long)c * Ho * Wo + y * Wo + x] = v;
 }
 
+// interp_kernel with 4 consecutive outputs per thread and one float4 store (Wo % 4 == 0,
+// 16-byte aligned output planes: the update block's maps); per-output arithmetic identical
+// to interp_kernel. grid: x over quads of output columns (64 per block), y over rows (4)
+__global__ __launch_bounds__(256) void interp_v4_kernel(const float *__restrict__ in, long in_bs, int C, int H,
+                                                        int W, int Ho, int Wo, float sh, float sw,
+                                                        float *__restrict__ out, long out_bs) {
+  const int xq = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (4 * xq >= Wo || y >= Ho) return;
+  const int b = blockIdx.z / C, c = blockIdx.z % C;
+  const float *p = in + b * in_bs + (long)c * H * W;
+  const float ry = sh * (float)y;
+  const int y0 = (int)ry;
+  const int yp = y0 < H - 1 ? 1 : 0;
+  const float ly1 = ry - (float)y0, ly0 = 1.0f - ly1;
+  const float *r0 = p + y0 * W, *r1 = p + (y0 + yp) * W;
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float rx = sw * (float)(4 * xq + j);
+    const int x0 = (int)rx;
+    const int xp = x0 < W - 1 ? 1 : 0;
+    const float lx1 = rx - (float)x0, lx0 = 1.0f - lx1;
+    v[j] = ly0 * (lx0 * r0[x0] + lx1 * r0[x0 + xp]) + ly1 * (lx0 * r1[x0] + lx1 * r1[x0 + xp]);
+  }
+  *reinterpret_cast<float4 *>(out + b * out_bs + (long)c * Ho * Wo + y * Wo + 4 * xq) =
+      make_float4(v[0], v[1], v[2], v[3]);
+}
+
 // pool2x with 4 consecutive outputs per thread and one float4 store (W % 8 == 0, 16-byte
 // aligned planes: the update block's maps): the window columns of outputs 4q .. 4q + 3 are
 // 8q - 1 .. 8q + 7, one scalar and two float4 loads per input row instead of 12 scalar loads.
@@ -281,8 +309,12 @@ extern "C" int sa_interp_bilinear_ac(const float *in, long in_bs, int B, int C, 
   const float sw = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.0f;
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_MISC, s);
-  interp_kernel<<<dim3((Wo + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, sh, sw, out,
-                                                                          out_bs);
+  if (Wo % 4 == 0 && al16(out) && out_bs % 4 == 0)
+    interp_v4_kernel<<<dim3((Wo / 4 + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, sh, sw,
+                                                                                   out, out_bs);
+  else
+    interp_kernel<<<dim3((Wo + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, sh, sw, out,
+                                                                            out_bs);
   return sa::check_launch("sa_interp_bilinear_ac");
 }
 

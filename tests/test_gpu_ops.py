@@ -302,6 +302,10 @@ def test_gru_gates_and_plumbing(H, W):
     ops.interp(y, buf[:, :C])
     torch.testing.assert_close(buf[:, :C], torch.nn.functional.interpolate(y, (9, 12), mode="bilinear",
                                                                            align_corners=True), atol=1e-6, rtol=0)
+    odd = torch.zeros(B, C, 9, 13, device=dev)   # Wo % 4 != 0: the one-output-per-thread kernel
+    ops.interp(y, odd)
+    torch.testing.assert_close(odd, torch.nn.functional.interpolate(y, (9, 13), mode="bilinear",
+                                                                    align_corners=True), atol=1e-6, rtol=0)
     # the update block's map sizes (pool2x: the 4-wide float4 variant, W % 8 == 0)
     for (hi, wi), (ho, wo) in (((136, 240), (68, 120)), ((68, 120), (34, 60))):
         xs = g(rng.standard_normal((B, C, hi, wi)))
