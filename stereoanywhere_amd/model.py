@@ -62,6 +62,10 @@ _FUSE_GATES = os.environ.get("SA_FUSE_GATES", "1") != "0"
 # ... and the state update in the r*h conv's epilogue (SA_FUSE_OUT=0: gru_out kernel, r*h conv
 # split over its input channels)
 _FUSE_OUT = os.environ.get("SA_FUSE_OUT", "1") != "0"
+# mono branch on a second stream beside the encoders (SA_MONO_STREAM=0: one stream)
+_MONO_STREAM = os.environ.get("SA_MONO_STREAM", "1") != "0"
+# ... followed there by the context encoder (SA_CNET_SIDE=0: context encoder on the main stream)
+_CNET_SIDE = os.environ.get("SA_CNET_SIDE", "1") != "0"
 # launches of the update block on F(4x4)'s small blocks (two per CU), by name: "q16" (gru16's
 # r*h conv + the motion conv), "q08" (gru08's + gru32's r*h convs), "zr16", "zr08", "pro32"
 _SMALL_LAUNCHES = set(filter(None, os.environ.get("SA_SMALL_LAUNCHES", "").split(",")))
@@ -217,6 +221,17 @@ class StereoAnywhere(nn.Module):
         n2 = ops.mono_normals(m2l, gain)
         n3 = ops.mono_normals(m3l, gain)
 
+        # The mono branch (volume -> hourglass -> alignment) reads only the mono maps, so it can
+        # run on a second HIP stream beside the encoders, filling their launch tails and
+        # HBM-bound passes with the hourglass's compute (SA_MONO_STREAM=0 turns it off).  The main stream
+        # waits for it before the pyramids; tensors it hands over are recorded on the main
+        # stream so the caching allocator does not reuse them early.
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev) if _MONO_STREAM else None
+        if side is not None:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                mono = self._mono_branch(dw, mde2, mde3, mde_lr, m2l, m3l, n2, n3, B, H4, W4)
         # ---- context + feature encoders: convs on MIOpen fp32, epilogues fused (encoders.py)
         if self.cnet.training or self.fnet.training:  # batch-statistics BatchNorm: module path
             cl = self.cnet(mde2.repeat(1, 3, 1, 1))
@@ -224,18 +239,68 @@ class StereoAnywhere(nn.Module):
             ctx = [conv(torch.relu(x[1])) for x, conv in zip(cl, self.context_zqr_convs)]
             fm = self.fnet(torch.cat([image2, image3], 0))
         else:
-            cl = encoders.cnet_forward(self.cnet, mde2.repeat(1, 3, 1, 1), dw["bn_cnet"], dw["wino"], dw["direct"],
-                                       dw["fold_cnet"])
-            hid, cs = [], []
-            for (h_raw, c_raw), (hb, cb) in zip(cl, dw["head_b"]):
-                hid.append(ops.norm_act(h_raw, ops.Affine(t=hb), act_in="tanh", out=h_raw))
-                cs.append(ops.norm_act(c_raw, ops.Affine(t=cb), act_in="relu", out=c_raw))
-            # the three context_zqr convs ([B,384,..] per level) in one launch
-            ctx = ops.conv2d_k3_multi(*[dict(x=c, U=U, bias=conv.bias)
-                                        for c, U, conv in zip(cs, dw["U_ctx"], self.context_zqr_convs)])
+            if side is not None and _CNET_SIDE:
+                # the context encoder after the mono branch on the side stream (it reads only
+                # mde2), so the main stream runs the feature encoder alone
+                with torch.cuda.stream(side):
+                    hid, ctx = self._context(dw, mde2)
+            else:
+                hid, ctx = self._context(dw, mde2)
             fm = encoders.fnet_forward(self.fnet, torch.cat([image2, image3], 0), dw["bn_fnet"], dw["wino"],
                                        dw["direct"])
         fmap2, fmap3 = fm[:B].contiguous(), fm[B:].contiguous()
+        if side is not None:
+            main.wait_stream(side)
+            for t in list(mono) + list(hid) + list(ctx):
+                t.record_stream(main)
+        else:
+            mono = self._mono_branch(dw, mde2, mde3, mde_lr, m2l, m3l, n2, n3, B, H4, W4)
+        vol_d, vol_c, sm2, mirror, coords_x = mono
+        del mono
+
+        # ---- pyramids
+        trunc = (sm2, mirror) if a.use_truncate_vol else (None, None)
+        stereo_blk = HipCorrBlock1D.from_features(fmap2, fmap3, a.corr_levels, a.corr_radius, trunc[0], trunc[1],
+                                                  float(a.mirror_attenuation))
+        del fmap2, fmap3
+        if a.use_aggregate_mono_vol:
+            mono_rows = vol_d.permute(0, 1, 3, 4, 2)  # [B,1,H,W1,W2] view (transposed by the pyramid kernel)
+        else:
+            # raw mono volume 1.73 * corr(normals) (stereoanywhere.py:136, 210)
+            mono_rows = 1.73 * ops.corr_volume(n2, n3)
+        mono_blk = HipCorrBlock1D(None, a.corr_levels, a.corr_radius,
+                                  _pyramid=ops.pyramid_from_volume(mono_rows, a.corr_levels),
+                                  _shape=(B, H4, W4, W4))
+        del mono_rows, vol_d, vol_c
+
+        return self._iterate(dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4)
+
+    def _context(self, dw, mde2):
+        """Context encoder (eval BatchNorm folded) -> tanh hidden states and the context_zqr
+        convs (stereoanywhere.py:116-121)."""
+        cl = encoders.cnet_forward(self.cnet, mde2.repeat(1, 3, 1, 1), dw["bn_cnet"], dw["wino"], dw["direct"],
+                                   dw["fold_cnet"])
+        hid, cs = [], []
+        for (h_raw, c_raw), (hb, cb) in zip(cl, dw["head_b"]):
+            hid.append(ops.norm_act(h_raw, ops.Affine(t=hb), act_in="tanh", out=h_raw))
+            cs.append(ops.norm_act(c_raw, ops.Affine(t=cb), act_in="relu", out=c_raw))
+        # the three context_zqr convs ([B,384,..] per level) in one launch
+        ctx = ops.conv2d_k3_multi(*[dict(x=c, U=U, bias=conv.bias)
+                                    for c, U, conv in zip(cs, dw["U_ctx"], self.context_zqr_convs)])
+        return hid, ctx
+
+    def _side_stream(self, dev):
+        s = getattr(self, "_side", None)
+        if s is None or s.device != dev:
+            s = self._side = torch.cuda.Stream(dev)
+        return s
+
+    def _mono_branch(self, dw, mde2, mde3, mde_lr, m2l, m3l, n2, n3, B, H4, W4):
+        """Mono cost volume -> hourglass -> classifiers -> soft-argmin / confidence -> scale-shift
+        alignment and mirror detector (stereoanywhere.py:136-205); returns (vol_d, vol_c, scaled
+        mono left, mirror map, initial coords_x)."""
+        a = self.args
+        dev, f32 = mde2.device, torch.float32
         feats_l = [F.interpolate(mde2, scale_factor=1 / 2 ** i, mode="bilinear", align_corners=True)
                    for i in range(a.n_downsample, len(self.feature_channels))]
         feats_r = [F.interpolate(mde3, scale_factor=1 / 2 ** i, mode="bilinear", align_corners=True)
@@ -268,23 +333,7 @@ class StereoAnywhere(nn.Module):
                                                            float(a.lrc_th), float(a.mirror_conf_th))
         if a.init_disparity_zero:
             coords_x = torch.arange(W4, device=dev, dtype=f32).expand(B, 1, H4, W4).contiguous()
-
-        # ---- pyramids
-        trunc = (sm2, mirror) if a.use_truncate_vol else (None, None)
-        stereo_blk = HipCorrBlock1D.from_features(fmap2, fmap3, a.corr_levels, a.corr_radius, trunc[0], trunc[1],
-                                                  float(a.mirror_attenuation))
-        del fmap2, fmap3
-        if a.use_aggregate_mono_vol:
-            mono_rows = vol_d.permute(0, 1, 3, 4, 2)  # [B,1,H,W1,W2] view (transposed by the pyramid kernel)
-        else:
-            # raw mono volume 1.73 * corr(normals) (stereoanywhere.py:136, 210)
-            mono_rows = 1.73 * ops.corr_volume(n2, n3)
-        mono_blk = HipCorrBlock1D(None, a.corr_levels, a.corr_radius,
-                                  _pyramid=ops.pyramid_from_volume(mono_rows, a.corr_levels),
-                                  _shape=(B, H4, W4, W4))
-        del mono_rows, vol_d, vol_c
-
-        return self._iterate(dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4)
+        return vol_d, vol_c, sm2, mirror, coords_x
 
     def _iterate(self, dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4):
         ub = self.update_block
