@@ -64,8 +64,9 @@ _FUSE_GATES = os.environ.get("SA_FUSE_GATES", "1") != "0"
 _FUSE_OUT = os.environ.get("SA_FUSE_OUT", "1") != "0"
 # mono branch on a second stream beside the encoders (SA_MONO_STREAM=0: one stream)
 _MONO_STREAM = os.environ.get("SA_MONO_STREAM", "1") != "0"
-# ... followed there by the context encoder (SA_CNET_SIDE=0: context encoder on the main stream)
-_CNET_SIDE = os.environ.get("SA_CNET_SIDE", "1") != "0"
+# the context encoder on a third stream (SA_CNET_SIDE=1: after the mono branch on the second,
+# 0: on the main stream)
+_CNET_SIDE = int(os.environ.get("SA_CNET_SIDE", "2"))
 # launches of the update block on F(4x4)'s small blocks (two per CU), by name: "q16" (gru16's
 # r*h conv + the motion conv), "q08" (gru08's + gru32's r*h convs), "zr16", "zr08", "pro32"
 _SMALL_LAUNCHES = set(filter(None, os.environ.get("SA_SMALL_LAUNCHES", "").split(",")))
@@ -241,9 +242,16 @@ class StereoAnywhere(nn.Module):
         else:
             if side is not None and _CNET_SIDE:
                 # the context encoder after the mono branch on the side stream (it reads only
-                # mde2), so the main stream runs the feature encoder alone
-                with torch.cuda.stream(side):
+                # mde2), so the main stream runs the feature encoder alone (SA_CNET_SIDE=2: on
+                # a third stream of its own)
+                cs = side
+                if _CNET_SIDE == 2:
+                    cs = self._side_stream(dev, 1)
+                    cs.wait_stream(main)
+                with torch.cuda.stream(cs):
                     hid, ctx = self._context(dw, mde2)
+                if cs is not side:
+                    side.wait_stream(cs)
             else:
                 hid, ctx = self._context(dw, mde2)
             fm = encoders.fnet_forward(self.fnet, torch.cat([image2, image3], 0), dw["bn_fnet"], dw["wino"],
@@ -289,11 +297,11 @@ class StereoAnywhere(nn.Module):
                                     for c, U, conv in zip(cs, dw["U_ctx"], self.context_zqr_convs)])
         return hid, ctx
 
-    def _side_stream(self, dev):
-        s = getattr(self, "_side", None)
-        if s is None or s.device != dev:
-            s = self._side = torch.cuda.Stream(dev)
-        return s
+    def _side_stream(self, dev, i: int = 0):
+        ss = getattr(self, "_sides", None)
+        if ss is None or ss[0].device != dev:
+            ss = self._sides = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        return ss[i]
 
     def _mono_branch(self, dw, mde2, mde3, mde_lr, m2l, m3l, n2, n3, B, H4, W4):
         """Mono cost volume -> hourglass -> classifiers -> soft-argmin / confidence -> scale-shift
