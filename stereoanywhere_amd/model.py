@@ -241,9 +241,9 @@ class StereoAnywhere(nn.Module):
             fm = self.fnet(torch.cat([image2, image3], 0))
         else:
             if side is not None and _CNET_SIDE:
-                # the context encoder after the mono branch on the side stream (it reads only
-                # mde2), so the main stream runs the feature encoder alone (SA_CNET_SIDE=2: on
-                # a third stream of its own)
+                # the context encoder (it reads only mde2) on a third stream (SA_CNET_SIDE=2)
+                # or after the mono branch on the second (1), so the main stream runs the
+                # feature encoder alone
                 cs = side
                 if _CNET_SIDE == 2:
                     cs = self._side_stream(dev, 1)
