@@ -197,6 +197,9 @@ def main():
         D.barrier(r)
         elapsed = time.perf_counter() - t0
         log(f"timed {args.steps} steps in {elapsed:.3f} s")
+        # per-launch times of one kernel at a time: the side streams' overlap (model.py) would
+        # stretch each launch by the work running beside it
+        model.stream_overlap = False
         N.timing_enable(True)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
@@ -206,6 +209,7 @@ def main():
         elapsed_ev = time.perf_counter() - t1
         kt = {k: N.timing_read(k) for k in N.KERNEL_IDS}
         N.timing_enable(False)
+        model.stream_overlap = True
         log(f"instrumented {args.steps} steps in {elapsed_ev:.3f} s")
         elapsed = D.max_over_ranks(elapsed, r, device)
         # per-pair metrics gathered once, after the timed region (the only collective)
@@ -242,7 +246,9 @@ def main():
                  "instrumented_ms_per_step": elapsed_ev / args.steps * 1e3,
                  "note": "achieved = algorithmic amount per launch / mean live HIP-event launch time, "
                          "events recorded around every launch over K steps run right after the K "
-                         "plain timed steps (the events cost ~6 % of a step); "
+                         "plain timed steps (the events cost ~6 % of a step), in the one-stream order "
+                         "(model.stream_overlap = False: the plain steps overlap the mono branch and the "
+                         "context encoder with the feature encoder on side streams); "
                          "fp32 FMA peak 157.3 TF/s is the same for MFMA (v_mfma_f32_*_f32) and VALU; "
                          "conv2d_wino / conv2d_wino4 count the Winograd-domain products they execute "
                          "(16/36 resp. 36/144 of the direct convolution's), so their direct-equivalent "

@@ -97,6 +97,9 @@ class StereoAnywhere(nn.Module):
                                                   a.context_dims, a.n_downsample)
         self._derived = None
         self._derived_key = None
+        # side streams before the update loop (_forward); False runs everything on the
+        # caller's stream (bench.py's per-launch event timing)
+        self.stream_overlap = True
 
     # ------------------------------------------------------------------ weights
     def _split_gru(self, gru, hidden: int):
@@ -228,7 +231,7 @@ class StereoAnywhere(nn.Module):
         # waits for it before the pyramids; tensors it hands over are recorded on the main
         # stream so the caching allocator does not reuse them early.
         main = torch.cuda.current_stream(dev)
-        side = self._side_stream(dev) if _MONO_STREAM else None
+        side = self._side_stream(dev) if _MONO_STREAM and self.stream_overlap else None
         if side is not None:
             side.wait_stream(main)
             with torch.cuda.stream(side):
