@@ -97,3 +97,20 @@ def test_derived_weights_cached_across_forwards(model):
         model(*x, iters=1, test_mode=True)
     assert model._derived is d1
     assert isinstance(model._derived_key, tuple)
+
+
+def test_side_streams_match_one_stream(model):
+    """The mono branch and the context encoder on side streams (model.stream_overlap, the
+    default) give the one-stream result; back-to-back forwards without a host sync exercise
+    the hand-over of side-stream tensors to the main stream (record_stream)."""
+    pb = synth.synthetic_batch(2, 256, 512, 64.0, seed0=11)
+    x = [torch.from_numpy(pb[k]).cuda() for k in ("left", "right", "mono_left", "mono_right")]
+    with torch.no_grad():
+        model.stream_overlap = False
+        ref = -model(*x, iters=6, test_mode=True)[0][:, 0].cpu().numpy()
+        model.stream_overlap = True
+        outs = [model(*x, iters=6, test_mode=True)[0] for _ in range(3)]
+        outs = [-o[:, 0].cpu().numpy() for o in outs]
+    for o in outs:
+        assert np.isfinite(o).all()
+        assert epe(o, ref) < 1e-5
