@@ -64,7 +64,7 @@ int sa_corr_volume_pyramid(const float *fmap2, const float *fmap3, int B, int C,
 int sa_corr_pyramid_from_volume(const float *volume, long rows, int W2, long in_row_stride,
                                 int num_levels, float *pyramid, long row_stride, void *stream);
 /* The same pyramid from a volume whose element (b, h, j, k) sits at volume + b*sb + h*sh + j +
- * k*sk (W1 contiguous, W2 <= 256: the hourglass's [B, 1, W2, H, W1] classifier output, used as
+ * k*sk (W1 contiguous, any W2, staged in 256-wide chunks: the hourglass's [B, 1, W2, H, W1] classifier output, used as
  * the mono volume with use_aggregate_mono_vol, stereoanywhere.py:168, 210); pyramid rows in
  * (b, h, j) order as above. */
 int sa_corr_pyramid_from_volume_strided(const float *volume, int B, int H, int W1, int W2, long sb, long sh, long sk,

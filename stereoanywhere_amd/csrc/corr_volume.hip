@@ -207,48 +207,55 @@ __global__ __launch_bounds__(256) void pyramid_from_volume_kernel(const float *_
 
 // The same pyramid from a volume stored with W1 contiguous and W2 strided (the hourglass's
 // [B, ., W2, H, W1] layout, a5 -> a8 with use_aggregate_mono_vol), without materialising the
-// [B, H, W1, W2] permute: a block stages 64 pixels x W2 (<= 256) of one (b, h) in LDS with
-// loads coalesced along W1, then writes each pixel's pyramid row from LDS.
-constexpr int PT_J = 64, PT_MAXW2 = 256;
+// [B, H, W1, W2] permute: a block stages 64 pixels x a 256-wide W2 chunk of one (b, h) in LDS
+// with loads coalesced along W1, then writes each pixel's pyramid row segment from LDS.  Any
+// W2 is handled chunk by chunk: a chunk starts at a multiple of 8, so every level-1/2/3 cell
+// (a pair / quad / octet of level-0 cells) lies inside one chunk.
+constexpr int PT_J = 64, PT_CHUNK = 256;
 
 __global__ __launch_bounds__(256) void pyramid_from_strided_kernel(const float *__restrict__ vol, long sb, long sh,
                                                                    long sk, int H, int W1, int W2, Geo g,
                                                                    float *__restrict__ pyr) {
-  __shared__ float tile[PT_J][PT_MAXW2 + 1];
+  __shared__ float tile[PT_J][PT_CHUNK + 1];
   const int j0 = blockIdx.x * PT_J, h = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const float *src = vol + b * sb + h * sh + j0;
   const bool jok = j0 + lane < W1;
-  for (int k = wv; k < W2; k += 4) tile[lane][k] = jok ? src[(long)k * sk + lane] : 0.0f;
-  __syncthreads();
-  for (int jj = wv; jj < PT_J; jj += 4) {
-    const int j = j0 + jj;
-    if (j >= W1) break;
-    float *dst = pyr + (((long)b * H + h) * W1 + j) * g.rs;
-    const float *row = tile[jj];
-    for (int base = lane * 8; base < W2; base += 64 * 8) {
-      float v[8];
+  for (int c0 = 0; c0 < W2; c0 += PT_CHUNK) {
+    const int cw = min(PT_CHUNK, W2 - c0);
+    if (c0 > 0) __syncthreads();  // the previous chunk's rows have been read
+    for (int k = wv; k < cw; k += 4) tile[lane][k] = jok ? src[(long)(c0 + k) * sk + lane] : 0.0f;
+    __syncthreads();
+    for (int jj = wv; jj < PT_J; jj += 4) {
+      const int j = j0 + jj;
+      if (j >= W1) break;
+      float *dst = pyr + (((long)b * H + h) * W1 + j) * g.rs;
+      const float *row = tile[jj];
+      for (int lb = lane * 8; lb < cw; lb += 64 * 8) {
+        const int base = c0 + lb;
+        float v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = (base + i < W2) ? row[base + i] : 0.f;
+        for (int i = 0; i < 8; ++i) v[i] = (base + i < W2) ? row[lb + i] : 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (base + i < W2) dst[base + i] = v[i];
-      float l1[4], l2[2];
+        for (int i = 0; i < 8; ++i)
+          if (base + i < W2) dst[base + i] = v[i];
+        float l1[4], l2[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        l1[i] = (v[2 * i] + v[2 * i + 1]) * 0.5f;
-        const int k1 = base / 2 + i;
-        if (g.nlev > 1 && k1 < g.wid[1]) dst[g.off[1] + k1] = l1[i];
+        for (int i = 0; i < 4; ++i) {
+          l1[i] = (v[2 * i] + v[2 * i + 1]) * 0.5f;
+          const int k1 = base / 2 + i;
+          if (g.nlev > 1 && k1 < g.wid[1]) dst[g.off[1] + k1] = l1[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          l2[i] = (l1[2 * i] + l1[2 * i + 1]) * 0.5f;
+          const int k2 = base / 4 + i;
+          if (g.nlev > 2 && k2 < g.wid[2]) dst[g.off[2] + k2] = l2[i];
+        }
+        const float l3 = (l2[0] + l2[1]) * 0.5f;
+        const int k3 = base / 8;
+        if (g.nlev > 3 && k3 < g.wid[3]) dst[g.off[3] + k3] = l3;
       }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        l2[i] = (l1[2 * i] + l1[2 * i + 1]) * 0.5f;
-        const int k2 = base / 4 + i;
-        if (g.nlev > 2 && k2 < g.wid[2]) dst[g.off[2] + k2] = l2[i];
-      }
-      const float l3 = (l2[0] + l2[1]) * 0.5f;
-      const int k3 = base / 8;
-      if (g.nlev > 3 && k3 < g.wid[3]) dst[g.off[3] + k3] = l3;
     }
   }
 }
@@ -323,8 +330,8 @@ extern "C" int sa_corr_pyramid_from_volume_strided(const float *volume, int B, i
                                                    long sk, int num_levels, float *pyramid, long row_stride,
                                                    void *stream) {
   SA_REQUIRE(volume && pyramid, "sa_corr_pyramid_from_volume_strided: null pointer");
-  SA_REQUIRE(B > 0 && B <= 65535 && H > 0 && H <= 65535 && W1 > 0 && W2 > 0 && W2 <= PT_MAXW2,
-             "sa_corr_pyramid_from_volume_strided: bad shape (W2 <= %d)", PT_MAXW2);
+  SA_REQUIRE(B > 0 && B <= 65535 && H > 0 && H <= 65535 && W1 > 0 && W2 > 0,
+             "sa_corr_pyramid_from_volume_strided: bad shape");
   SA_REQUIRE(num_levels >= 1 && num_levels <= 4, "sa_corr_pyramid_from_volume_strided: num_levels must be 1..4");
   SA_REQUIRE(row_stride >= sa_pyramid_level_offset(W2, num_levels),
              "sa_corr_pyramid_from_volume_strided: row_stride too small");

@@ -102,7 +102,7 @@ def corr_volume(fmap2: torch.Tensor, fmap3: torch.Tensor) -> torch.Tensor:
 
 def pyramid_from_volume(volume: torch.Tensor, num_levels: int = 4) -> torch.Tensor:
     """CorrBlock1D.__init__ on an existing volume [..., W2] (rows contiguous along W2), or on a
-    [B, 1, H, W1, W2] view whose W1 axis is the contiguous one (W2 <= 256)."""
+    [B, 1, H, W1, W2] view whose W1 axis is the contiguous one (any W2)."""
     _check(volume, "volume", contiguous=False)
     W2 = volume.shape[-1]
     if volume.dim() == 5 and volume.shape[1] == 1 and volume.stride(-1) != 1 and volume.stride(3) == 1:

@@ -6,7 +6,10 @@ Same flags, same per-sample procedure:
   iscale / oscale nearest resampling (test.py:169-176) -> mono maps (precomputed files,
   zeros for --monomodel none, or the synthetic set's own) -> replicate pad to ×32 (left/top
   get pad//2, 206-213) -> forward(test_mode=True) -> negate -> unpad -> rescale (238-240)
-  -> guided_metrics (losses.py:273-342) -> CSV row (251-274).
+  -> guided_metrics (losses.py:273-342); a ground truth without points gives the metrics of
+  an all-zero prediction (182-187); --stereomodel skip_pred predicts zeros (219-228).
+Over --tries: per-try sample means, then mean / std over tries, printed as the reference's
+MEAN / STD tables and written with its write_csv_header / write_csv_row (251-274, 347-403).
 DAv2 is outside this tier: --monomodel DAv2 needs precomputed maps (--mono_tag) as written
 by mono_sceneflow-style preprocessing.  Datasets: `middlebury` (folder layout of
 middlebury_dataset.py) and `synthetic` (seeded pairs with true disparity).
@@ -17,7 +20,6 @@ rows are all-gathered to rank 0 (the only exchange).
 from __future__ import annotations
 
 import argparse
-import csv
 import os
 import sys
 
@@ -28,13 +30,9 @@ import torch.nn.functional as F
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from stereoanywhere_amd import data, dist, metrics, synth, tiler  # noqa: E402
+from stereoanywhere_amd import data, dist, harness, metrics, synth, tiler  # noqa: E402
 from stereoanywhere_amd.checkpoint import load_reference_checkpoint  # noqa: E402
 from stereoanywhere_amd.model import StereoAnywhere  # noqa: E402
-
-METRIC_KEYS = ["bad 1.0", "bad 2.0", "bad 3.0", "bad 4.0", "bad 5.0", "bad 6.0", "bad 7.0", "bad 8.0", "avgerr",
-               "rms"]
-
 
 def build_parser():
     p = argparse.ArgumentParser(description="StereoAnywhere (MI355X build)")
@@ -102,6 +100,12 @@ def run(net, sample, args, device):
         t["gt"] = F.interpolate(t["gt"], scale_factor=1.0 / args.oscale, mode="nearest") / args.oscale
         t["validgt"] = F.interpolate(t["validgt"].float(), scale_factor=1.0 / args.oscale, mode="nearest")
         t["maskocc"] = F.interpolate(t["maskocc"].float(), scale_factor=1.0 / args.oscale, mode="nearest")
+    if t["gt"].max() == 0:
+        # test.py:182-187: no ground-truth point -> metrics of an all-zero prediction
+        res = metrics.guided_metrics(torch.zeros_like(t["gt"]).numpy(), t["gt"].numpy(), t["validgt"].numpy(),
+                                     t["maskocc"].numpy())
+        res["disp"] = torch.ones_like(t["gt"]).squeeze(1)
+        return res
     im2, im3 = t["im2"].to(device), t["im3"].to(device)
     if "im2_mono" in t and args.monomodel != "none":
         m2, m3 = t["im2_mono"].to(device), t["im3_mono"].to(device)
@@ -116,8 +120,11 @@ def run(net, sample, args, device):
 
     def P(x):
         return F.pad(x, pad, mode="replicate")
-    flow_up, _ = net(P(im2), P(im3), P(m2), P(m3), test_mode=True, iters=args.iters)
-    pred = -flow_up[:, 0]
+    if args.stereomodel == "skip_pred":   # test.py:219-220, 227-228: zero prediction, no network
+        pred = torch.zeros_like(P(im2))[:, 0]
+    else:
+        flow_up, _ = net(P(im2), P(im3), P(m2), P(m3), test_mode=True, iters=args.iters)
+        pred = -flow_up[:, 0]
     hd, wd = pred.shape[-2:]
     pred = pred[..., pad[2]:hd - pad[3], pad[0]:wd - pad[1]]
     if args.iscale != 1 and args.iscale / args.oscale != 1:
@@ -129,46 +136,42 @@ def run(net, sample, args, device):
 
 
 def main(argv=None):
+    """test.py:276-403: every try walks the (sharded) samples; metrics are aggregated over
+    samples per try, then over tries (harness.aggregate_tries); CSV as write_csv_row."""
     args = build_parser().parse_args(argv)
+    assert args.iscale > 0 and args.oscale > 0
     if args.no_cuda or not torch.cuda.is_available():
         raise SystemExit("the MI355X build runs on the GPU only (no CPU path)")
+    if args.stereomodel not in ("stereoanywhere", "skip_pred"):
+        raise SystemExit("no model")
     torch.manual_seed(args.seed)
     r = dist.init_from_env("nccl")
     device = torch.device("cuda", r.local_rank)
-    net = StereoAnywhere(vars(args)).eval()
-    if args.loadstereomodel:
-        load_reference_checkpoint(net, args.loadstereomodel)
-    else:
-        synth.load_seeded_weights(net, 0)
-    net = net.to(device)
+    net = None
+    if args.stereomodel == "stereoanywhere":
+        net = StereoAnywhere(vars(args)).eval()
+        if args.loadstereomodel:
+            load_reference_checkpoint(net, args.loadstereomodel)
+        else:
+            synth.load_seeded_weights(net, 0)
+        net = net.to(device)
     ds = build_dataset(args)
     n = len(ds) if args.valsize <= 0 else min(args.valsize, len(ds))
-    lo, hi = dist.shard_range(n, r.rank, r.world)
-    rows = []
-    for i in range(lo, hi):
-        for _ in range(args.tries):
-            res = run(net, ds[i], args, device)
-        rows.append([i] + [float(res[k]) for k in METRIC_KEYS])
-        if args.outdir:
+
+    def on_result(attempt, i, res):
+        if args.outdir and attempt == 0:
             os.makedirs(args.outdir, exist_ok=True)
             data.write_pfm(os.path.join(args.outdir, f"{ds[i]['name']}_disp.pfm"), res["disp"][0].cpu().numpy())
         if args.verbose:
-            print(ds[i]["name"], {k: round(float(res[k]), 4) for k in METRIC_KEYS})
-    local = torch.tensor(rows, dtype=torch.float64, device=device).reshape(-1, 1 + len(METRIC_KEYS))
-    allrows = dist.gather_metrics(local, r).cpu().numpy()
-    if not r.is_main:
-        return
-    allrows = allrows[np.argsort(allrows[:, 0])]
-    mean = {k: float(np.nanmean(allrows[:, 1 + j])) for j, k in enumerate(METRIC_KEYS)}
-    print(f"{args.dataset}: {len(allrows)} samples", {k: round(v, 4) for k, v in mean.items()})
-    if args.csv_path:
-        new = not os.path.exists(args.csv_path)
-        with open(args.csv_path, "a", newline="") as f:
-            w = csv.writer(f)
-            if new:
-                w.writerow(["dataset", "model", "iters", "maxdisp"] + METRIC_KEYS)
-            w.writerow([args.dataset, args.stereomodel, args.iters, args.maxdisp] + [mean[k] for k in METRIC_KEYS])
-    return mean
+            print(f"{i}) " + ", ".join(f"{k}: {float(res[k])}" for k in harness.METRIC_ORDER))
+    out = harness.evaluate(lambda i: run(net, ds[i], args, device), n, args.tries, r, device, on_result)
+    if out is None:
+        return None
+    acc_mean, acc_std = out
+    print("\n".join(harness.summary_lines(acc_mean, acc_std)))
+    if args.csv_path is not None:
+        harness.append_csv(args.csv_path, args, acc_mean)
+    return acc_mean
 
 
 if __name__ == "__main__":

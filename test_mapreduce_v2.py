@@ -19,7 +19,6 @@ are all-gathered to rank 0.
 from __future__ import annotations
 
 import argparse
-import csv
 import os
 import sys
 
@@ -30,13 +29,10 @@ import torch.nn.functional as F
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from stereoanywhere_amd import data, dist, metrics, synth, tiler  # noqa: E402
+from stereoanywhere_amd import data, dist, harness, metrics, synth, tiler  # noqa: E402
 from stereoanywhere_amd.checkpoint import load_reference_checkpoint  # noqa: E402
 from stereoanywhere_amd.model import StereoAnywhere  # noqa: E402
-
-METRIC_KEYS = ["bad 1.0", "bad 2.0", "bad 3.0", "bad 4.0", "bad 5.0", "bad 6.0", "bad 7.0", "bad 8.0", "avgerr",
-               "rms"]
-
+from stereoanywhere_amd.offload import CPUOffloadWrapper  # noqa: E402
 
 def build_parser():
     p = argparse.ArgumentParser(description="StereoAnywhere MapReduce evaluation (MI355X build)")
@@ -88,6 +84,8 @@ def build_parser():
     p.add_argument("--mono_tag", default="dav2", help="file tag of precomputed mono maps (im0_<tag>.png)")
     p.add_argument("--synthetic_size", default="540x960", help="HxW of --dataset synthetic")
     p.add_argument("--synthetic_count", type=int, default=4)
+    p.add_argument("--cpu_offload", action="store_true",
+                   help="run the tiler under CPUOffloadWrapper (cpu_offload_wrapper.py:28-83; config 5)")
     return p
 
 
@@ -201,34 +199,29 @@ def main(argv=None):
         synth.load_seeded_weights(net, 0)
     net = net.to(device)
     inferencer = build_inferencer(net, args)
+    if args.cpu_offload:
+        # config 5: the tiler runs under the offload wrapper (HBM-resident on MI355X, offload.py)
+        inferencer.tile_wrapper = CPUOffloadWrapper(inferencer.tile_wrapper)
     ds = build_dataset(args)
     n = len(ds) if args.valsize <= 0 else min(args.valsize, len(ds))
-    lo, hi = dist.shard_range(n, r.rank, r.world)
-    rows = []
-    for i in range(lo, hi):
-        for _ in range(args.tries):
-            res = run_mapreduce(ds[i], args, device, inferencer)
-        rows.append([i] + [float(res[k]) for k in METRIC_KEYS])
-        if args.outdir:
+
+    def on_result(attempt, i, res):
+        if args.outdir and attempt == 0:
             os.makedirs(args.outdir, exist_ok=True)
             data.write_pfm(os.path.join(args.outdir, f"{ds[i]['name']}_disp.pfm"), res["disp"][0].cpu().numpy())
         if args.verbose:
-            print(ds[i]["name"], {k: round(float(res[k]), 4) for k in METRIC_KEYS})
-    local = torch.tensor(rows, dtype=torch.float64, device=device).reshape(-1, 1 + len(METRIC_KEYS))
-    allrows = dist.gather_metrics(local, r).cpu().numpy()
-    if not r.is_main:
+            print(ds[i]["name"], {k: round(float(res[k]), 4) for k in harness.METRIC_ORDER[:10]})
+    out = harness.evaluate(lambda i: run_mapreduce(ds[i], args, device, inferencer), n, args.tries, r, device,
+                           on_result)
+    if out is None:
         return None
-    allrows = allrows[np.argsort(allrows[:, 0])]
-    mean = {k: float(np.nanmean(allrows[:, 1 + j])) for j, k in enumerate(METRIC_KEYS)}
-    print(f"{args.dataset}: {len(allrows)} samples", {k: round(v, 4) for k, v in mean.items()})
-    if args.csv_path:
-        new = not os.path.exists(args.csv_path)
-        with open(args.csv_path, "a", newline="") as f:
-            w = csv.writer(f)
-            if new:
-                w.writerow(["dataset", "model", "iters", "maxdisp"] + METRIC_KEYS)
-            w.writerow([args.dataset, args.stereomodel, args.iters, args.maxdisp] + [mean[k] for k in METRIC_KEYS])
-    return mean
+    # test_mapreduce_v2.py:531-588: same aggregation as test.py, tables in guided_metrics order
+    acc_mean, acc_std = out
+    print("\n".join(harness.summary_lines(acc_mean, acc_std, harness.METRIC_ORDER)))
+    if args.csv_path is not None:
+        # the reference accepts --csv_path here but writes nothing; the build writes test.py's row
+        harness.append_csv(args.csv_path, args, acc_mean)
+    return acc_mean
 
 
 if __name__ == "__main__":

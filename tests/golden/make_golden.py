@@ -436,6 +436,162 @@ def odd_size_cases(model):
     return out
 
 
+def _pair_record(pair, prefix=""):
+    return {f"{prefix}inputs_sha256": np.array(synth.digest([pair[k] for k in ("left", "right", "mono_left",
+                                                                               "mono_right")]))}
+
+
+def wide_case(sa_mod, ut, corr_mod, model):
+    """96x1152 (W/4 = 288 > 256, the width class of the booster / kitti / high_memory tile
+    presets, tile_presets.py:53-101), 4 iterations: final disparity."""
+    pair = synth.synthetic_batch(1, 96, 1152, 64.0, seed0=1)
+    rec = run_capture(sa_mod, ut, corr_mod, model, pair, iters=4, capture_all=False)
+    return dict(disparity=rec["disparity"].astype(np.float32), **_pair_record(pair))
+
+
+# (name, H, W, tile_w, tile_h, overlap, D, iters): the presets' tile sides after
+# MapReduceInference's rounding (tiled_inference.py:56-69; middlebury overlap 112 -> 128),
+# on images sized for two tiles and no duplicate rectangle
+TILED_CASES = [
+    ("middlebury", 992, 1088, 672, 1120, 128, 256.0, 3),
+    ("booster", 672, 1792, 1120, 896, 224, 512.0, 3),
+]
+ROW_STEP = 4   # stored outputs keep every 4th row (all columns: the tile seams are vertical)
+
+
+def _single_thread_lsq(sa_mod):
+    """Pin the reference's weighted_lsq to the single-threaded (deterministic) solve, as
+    run_capture does; returns the restore function."""
+    orig = sa_mod.weighted_lsq
+
+    def lsq_1t(*a, **k):
+        nt = torch.get_num_threads()
+        torch.set_num_threads(1)
+        try:
+            return orig(*a, **k)
+        finally:
+            torch.set_num_threads(nt)
+    sa_mod.weighted_lsq = lsq_1t
+    return lambda: setattr(sa_mod, "weighted_lsq", orig)
+
+
+def tiled_model_cases(sa_mod, model):
+    """The reference TileWrapper (mapreduce_v2/tile_wrapper.py:122-186) driving the
+    reference model on seeded weights: a two-tile stitch per preset, plus one full
+    Booster-preset tile (896x1120, W/4 = 280) through the model alone.  Outputs keep
+    every ROW_STEP-th row to stay small."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_tile_wrapper", os.path.join(REF, "mapreduce_v2", "tile_wrapper.py"))
+    tw = importlib.util.module_from_spec(spec)
+    sys.modules["ref_tile_wrapper"] = tw
+    spec.loader.exec_module(tw)
+    restore = _single_thread_lsq(sa_mod)
+    out = {"row_step": np.array(ROW_STEP)}
+    for i, (name, H, W, tw_, th, ov, D, iters) in enumerate(TILED_CASES):
+        pair = synth.synthetic_batch(1, H, W, D, seed0=11 + i)
+        t = [torch.from_numpy(pair[k]) for k in ("left", "right", "mono_left", "mono_right")]
+        wrap = tw.TileWrapper(model, tile_width=tw_, tile_height=th, overlap=ov)
+        tiles = wrap._enumerate_tiles(H, W)
+        with torch.no_grad():
+            st = wrap(*t, iters=iters, test_mode=True)
+        out[f"{name}.geom"] = np.array([H, W, tw_, th, ov, iters], np.int64)
+        out[f"{name}.D"] = np.array(D)
+        out[f"{name}.tiles"] = np.array([[s.y_start, s.y_end, s.x_start, s.x_end] for s in tiles])
+        out[f"{name}.out"] = _np(st)[0, 0, ::ROW_STEP].astype(np.float32)
+        out.update(_pair_record(pair, f"{name}."))
+        print(name, "tiles", len(tiles), "range", float(st.min()), float(st.max()))
+    pair = synth.synthetic_batch(1, 896, 1120, 512.0, seed0=13)
+    t = [torch.from_numpy(pair[k]) for k in ("left", "right", "mono_left", "mono_right")]
+    with torch.no_grad():
+        d = -model(*t, iters=3, test_mode=True)[0]
+    out["booster_tile.geom"] = np.array([896, 1120, 3], np.int64)
+    out["booster_tile.out"] = _np(d)[0, 0, ::ROW_STEP].astype(np.float32)
+    out.update(_pair_record(pair, "booster_tile."))
+    restore()
+    return out
+
+
+def harness_csv_cases():
+    """The reference test.py's write_csv_header / write_csv_row (test.py:251-274) on fixed
+    metric dicts.  test.py parses argv and builds models at import, so only those two
+    functions are taken from its source (ast) and executed; the CSV text is the fixture."""
+    import ast
+    src = open(os.path.join(REF, "test.py")).read()
+    tree = ast.parse(src)
+    fns = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in ("write_csv_header", "write_csv_row")]
+    ns = {}
+    exec(compile(ast.Module(body=fns, type_ignores=[]), "reference_test_py", "exec"), ns)
+    import io
+    rng = np.random.default_rng(9)
+    keys = ([f"bad {t}.0" for t in range(1, 9)] + ["avgerr", "rms"] + [f"occ bad {t}.0" for t in range(1, 9)]
+            + ["occ avgerr", "occ rms"] + [f"noc bad {t}.0" for t in range(1, 9)] + ["noc avgerr", "noc rms"])
+    cases = []
+    for j, args in enumerate([
+        dict(dataset="middlebury", datapath="dataset/oak_dataset/", monomodel="DAv2", loadmonomodel=None,
+             stereomodel="stereoanywhere", loadstereomodel="weights/sceneflow.tar", tries=1, iscale=1.0,
+             maxdisp=192, normalize=False),
+        dict(dataset="booster", datapath="/data/booster", monomodel="none", loadmonomodel="dav2.pth",
+             stereomodel="skip_pred", loadstereomodel="x.tar", tries=3, iscale=2.0, maxdisp=512, normalize=True),
+    ]):
+        vals = {k: float(np.float32(rng.random() * (1 if "bad" in k else 20))) for k in keys}
+        if j == 1:
+            vals.update({k: float("nan") for k in keys if k.startswith("occ")})
+            vals["occ rms"] = 0.0
+        ns_args = types.SimpleNamespace(**args)
+        f = io.StringIO()
+        ns["write_csv_header"](f, ns_args, vals)
+        ns["write_csv_row"](f, ns_args, vals)
+        cases.append(dict(args=args, metrics=[[k, vals[k]] for k in keys], text=f.getvalue()))
+    return cases
+
+
+def offload_cases():
+    """The reference CPUOffloadWrapper (mapreduce_v2/cpu_offload_wrapper.py:28-83) on CPU
+    with a mock stereo model and a mock mono model: mono given, mono computed (offloaded
+    to the host and back, or kept), and the error without either."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_offload", os.path.join(REF, "mapreduce_v2",
+                                                                              "cpu_offload_wrapper.py"))
+    off = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(off)
+
+    class Stereo(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.p = torch.nn.Parameter(torch.ones(1))
+
+        def forward(self, l, r, ml, mr, iters=1, test_mode=True):
+            return -(l[:, :1] * 2 - r[:, 2:3] + 3 * ml - mr * 0.5 + iters), None
+
+    class Mono(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.p = torch.nn.Parameter(torch.ones(1))
+
+        def forward(self, l, r):
+            return l.mean(1, keepdim=True) * self.p, r.amax(1, keepdim=True)
+
+    g = torch.Generator().manual_seed(21)
+    l, r = torch.rand(1, 3, 8, 12, generator=g), torch.rand(1, 3, 8, 12, generator=g)
+    ml, mr = torch.rand(1, 1, 8, 12, generator=g), torch.rand(1, 1, 8, 12, generator=g)
+    out = {"l": l, "r": r, "ml": ml, "mr": mr}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        with torch.no_grad():
+            out["given"] = off.CPUOffloadWrapper(Stereo(), Mono())(l, r, ml, mr, iters=4, test_mode=True)[0]
+            out["computed"] = off.CPUOffloadWrapper(Stereo(), Mono())(l, r, iters=2, test_mode=True)[0]
+            out["computed_kept"] = off.CPUOffloadWrapper(Stereo(), Mono(), offload_mono=False)(
+                l, r, None, None, 3, True)[0]
+            try:
+                off.CPUOffloadWrapper(Stereo())(l, r)
+                msg = ""
+            except ValueError as e:
+                msg = str(e)
+    out = {k: _np(v) for k, v in out.items()}
+    out["error_message"] = np.array(msg)
+    return out
+
+
 def _dedupe(rec):
     """Store byte-identical captures once; ``alias.<key>`` names the kept copy."""
     seen, out = {}, {}
@@ -450,10 +606,28 @@ def _dedupe(rec):
     return out
 
 
-def main():
+def main(only=None):
+    """``python tests/golden/make_golden.py [wide] [tiled] [csv] [offload]`` regenerates
+    just the named round-2 fixtures; no argument regenerates everything."""
     torch.set_num_threads(8)
     sa_mod, ut, corr_mod = _load_reference()
     model = build_model(sa_mod)
+    if only:
+        if "wide" in only:
+            np.savez_compressed(os.path.join(HERE, "wide_96x1152_it4.npz"), **wide_case(sa_mod, ut, corr_mod, model))
+        if "tiled" in only:
+            np.savez_compressed(os.path.join(HERE, "tiled_model.npz"), **tiled_model_cases(sa_mod, model))
+        if "csv" in only:
+            with open(os.path.join(HERE, "harness_csv.json"), "w") as f:
+                json.dump(harness_csv_cases(), f, indent=1)
+        if "offload" in only:
+            np.savez_compressed(os.path.join(HERE, "offload.npz"), **offload_cases())
+        return
+    np.savez_compressed(os.path.join(HERE, "wide_96x1152_it4.npz"), **wide_case(sa_mod, ut, corr_mod, model))
+    np.savez_compressed(os.path.join(HERE, "tiled_model.npz"), **tiled_model_cases(sa_mod, model))
+    with open(os.path.join(HERE, "harness_csv.json"), "w") as f:
+        json.dump(harness_csv_cases(), f, indent=1)
+    np.savez_compressed(os.path.join(HERE, "offload.npz"), **offload_cases())
     keys = {k: list(v.shape) for k, v in model.state_dict().items()}
     with open(os.path.join(HERE, "state_dict_keys.json"), "w") as f:
         json.dump(keys, f, indent=0, sort_keys=True)
@@ -483,4 +657,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

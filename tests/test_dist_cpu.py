@@ -54,3 +54,77 @@ def test_shard_range_covers_exactly():
             assert spans[0][0] == 0 and spans[-1][1] == gb
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+class _TileMock(torch.nn.Module):
+    """Deterministic per-tile 'model' (negated disparity, tile-size dependent like a real one)."""
+
+    def __init__(self):
+        super().__init__()
+        self.p = torch.nn.Parameter(torch.zeros(1))
+
+    def forward(self, l, r, ml, mr, iters=1, test_mode=True):
+        H, W = l.shape[-2:]
+        ramp = torch.arange(W, dtype=torch.float32).view(1, 1, 1, W) / W
+        return -(40 * l[:, :1] - 10 * r[:, 1:2] + ml * 3 + ramp + H / 100.0), None
+
+
+def _tile_inputs():
+    g = torch.Generator().manual_seed(5)
+    return [torch.rand(1, c, 200, 330, generator=g) for c in (3, 3, 1, 1)]
+
+
+def _eval_sample(i):
+    """A deterministic guided_metrics dict per sample index (what run(...) returns)."""
+    import numpy as np
+    from stereoanywhere_amd import metrics
+    rng = np.random.default_rng(100 + i)
+    gt = (rng.random((1, 1, 16, 24)) * 30).astype(np.float32)
+    occ = (rng.random(gt.shape) > 0.7).astype(np.float32) if i % 2 else np.zeros_like(gt)
+    return metrics.guided_metrics(gt + rng.standard_normal(gt.shape).astype(np.float32) * (1 + i), gt,
+                                  (rng.random(gt.shape) > 0.1).astype(np.float32), occ)
+
+
+def _worker_harness(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from stereoanywhere_amd import harness, tiler
+    r = D.init_from_env("gloo")
+    # test.py / test_mapreduce_v2.py sample sharding + metric gather (5 samples, 2 tries)
+    out = harness.evaluate(_eval_sample, 5, 2, r, "cpu")
+    # TileWrapper(rank, world): tiles r, r+world, ...; partial maps summed by one all_reduce
+    with torch.no_grad():
+        st = tiler.TileWrapper(_TileMock(), tile_width=128, tile_height=96, overlap=32, rank=r.rank,
+                               world=r.world)(*_tile_inputs(), iters=1, test_mode=True)
+    q.put((rank, out, st.numpy()))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_harness_and_tiles_sharded_equal_single_rank(world):
+    """The multi-rank harness (sample shards, all_gather of metric rows) and the tile-sharded
+    TileWrapper (all_reduce of the partial stitched / weight maps) give the single-rank
+    results: the same aggregated metrics and the same stitched disparity."""
+    import numpy as np
+    from stereoanywhere_amd import harness, tiler
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_harness, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    mean1, std1 = harness.evaluate(_eval_sample, 5, 2, D.Rank(), "cpu")
+    mean, std = res[0][1]
+    assert all(x[1] is None for x in res[1:])
+    assert list(mean) == harness.METRIC_ORDER
+    for k in harness.METRIC_ORDER:
+        np.testing.assert_equal(mean[k], mean1[k])
+        np.testing.assert_equal(std[k], std1[k])
+    with torch.no_grad():
+        st1 = tiler.TileWrapper(_TileMock(), tile_width=128, tile_height=96, overlap=32)(*_tile_inputs(), iters=1,
+                                                                                          test_mode=True).numpy()
+    for _, _, st in res:
+        np.testing.assert_allclose(st, st1, rtol=1e-6, atol=1e-6)

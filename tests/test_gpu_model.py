@@ -49,6 +49,18 @@ def test_end_to_end_vs_reference(model, name, H, W, D, iters):
     assert e < 1e-3
 
 
+def test_wide_input_vs_reference(model):
+    """96x1152: W/4 = 288 > 256, the width class of the booster (1120), high_memory (1280) and
+    kitti (1344) tiles; the mono pyramid is read from the hourglass layout in 256-wide
+    chunks and the softargmin / lookup take their long-line paths."""
+    fix = load_fixture("wide_96x1152_it4.npz")
+    pair = regenerate_inputs(fix, 1, 96, 1152, 64.0)
+    disp = run(model, pair, 4)
+    e = epe(disp, fix["disparity"])
+    print("wide 96x1152 EPE", e, "max", float(np.abs(disp - fix["disparity"]).max()))
+    assert e < 1e-3
+
+
 @pytest.mark.parametrize("i,H,W", [(0, 64, 100), (1, 120, 168)])
 def test_unpadded_sizes_vs_reference(model, i, H, W):
     """Sizes that are multiples of 4 but not 32 run unpadded, as in the reference (the tiled

@@ -69,10 +69,13 @@ def test_truncated_pyramid():
         np.testing.assert_allclose(lv, rv, atol=tol)
 
 
-@pytest.mark.parametrize("B,H,W1,W2", [(2, 3, 70, 61), (1, 2, 64, 256), (4, 5, 240, 240)])
+@pytest.mark.parametrize("B,H,W1,W2", [(2, 3, 70, 61), (1, 2, 64, 256), (4, 5, 240, 240), (1, 3, 72, 280),
+                                        (2, 2, 65, 300), (1, 2, 40, 517), (1, 1, 280, 280)])
 def test_pyramid_from_strided_volume(B, H, W1, W2):
     """The hourglass layout [B,1,W2,H,W1] viewed as [B,1,H,W1,W2] (W1 contiguous) gives the
-    same pyramid, bit for bit, as its contiguous permute (the LDS-transposing kernel)."""
+    same pyramid, bit for bit, as its contiguous permute (the LDS-transposing kernel), and
+    matches the oracle's avg-pool pyramid (corr.py:88-91).  W2 > 256 is the Booster / KITTI /
+    high_memory tile width class (W/4 = 280, 336, 320): the kernel walks W2 in 256-wide chunks."""
     rng = np.random.default_rng(W1 + W2)
     v = g(rng.standard_normal((B, 1, W2, H, W1)))
     view = v.permute(0, 1, 3, 4, 2)
@@ -81,6 +84,9 @@ def test_pyramid_from_strided_volume(B, H, W1, W2):
     _, offs, wids = ops.pyramid_geometry(W2, 4)
     used = offs[-1] + wids[-1]   # the row's padding to 4 floats is never written
     np.testing.assert_array_equal(got[:, :used], ref[:, :used])
+    vol = c(view.contiguous()).reshape(B * H * W1, W2)
+    for i, lv in enumerate(R.corr_pyramid(vol, 4)[:4]):
+        np.testing.assert_allclose(got[:, offs[i]:offs[i] + wids[i]], lv, atol=1e-6)
 
 
 def test_pyramid_from_volume_and_lookup_edges(micro):
