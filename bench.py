@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Throughput of the MI355X StereoAnywhere forward on synthetic 540x960 pairs.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W] [--config cfg2|cfg3|cfg5]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -16,7 +16,17 @@ Also reported (rank 0):
                 launch stream inside the timed region (libsa_hip sa_timing_*),
                 algorithmic bytes or flops per launch / mean launch time vs MI355X peak
   cpu_baseline  the oracle CPU restatement (torch CPU + numpy, parity-pinned to the
-                reference) on one 544x960 pair, all host threads, N=1 only
+                reference) on one 544x960 pair, all host threads, N=1 only: one warm-up
+                run, then the median of 3; cfg1 (256x512, 8 iters) the same
+                way beside it; the CPU model string and the thread count are reported
+
+Tiled configs (separate lines, not the headline):
+  --config cfg3  Middlebury-H-sized synthetic pair 1000x1400 (padded 1024x1408), middlebury
+                 preset (672x1120 tiles, overlap 112 -> 128): 3 tiles, 32 iterations
+  --config cfg5  Booster full-res synthetic pair 3008x4112 (padded 3008x4128), booster preset
+                 (1120x896 tiles, overlap 224) under CPUOffloadWrapper: 25 tiles, 32 iterations
+  A step = one image through the tiler (TileWrapper with batch_tiles, the reference's own
+  option: every tile has the preset's size, so the tiles run as one batch), stitched.
   epe_vs_reference  EPE of this build vs the reference's own disparity (golden vector,
                 544x960, 22 iterations) on identical inputs and weights
 """
@@ -114,20 +124,68 @@ def log(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(iters: int, H: int, W: int):
-    """The oracle restatement on one pair (bounded sample), all host threads."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _time_oracle(sd, H, W, iters, D, runs):
+    """One warm-up forward, then ``runs`` timed ones; returns the sorted wall times."""
+    from oracle import model_ref as M
+
+    pair = synth.synthetic_batch(1, H, W, D, seed0=1)
+    t = [torch.from_numpy(pair[k]) for k in ("left", "right", "mono_left", "mono_right")]
+    M.forward(sd, *t, iters=iters)
+    times = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        M.forward(sd, *t, iters=iters)
+        times.append(time.perf_counter() - t0)
+    return sorted(times)
+
+
+def cpu_baseline(iters: int, H: int, W: int, runs: int = 3):
+    """The oracle restatement (parity-pinned to the reference) on the box's host threads:
+    one warm-up, then the median of ``runs`` single-pair forwards, at the bench shape and
+    at cfg1 (256x512, 8 iterations)."""
     from oracle import model_ref as M
 
     torch.set_num_threads(host_threads())
     sd = M.load_state_dict_seeded(0)
-    pair = synth.synthetic_batch(1, H, W, 192.0, seed0=1)
+    ts = _time_oracle(sd, H, W, iters, 192.0, runs)
+    t1 = _time_oracle(sd, 256, 512, 8, 64.0, runs)
+    med, med1 = ts[len(ts) // 2], t1[len(t1) // 2]
+    return {"value": 1.0 / med, "unit": "pairs/s", "cores": torch.get_num_threads(), "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"1 pair 1x{H}x{W}, {iters} iters, oracle (torch CPU convs + numpy hot path); "
+                      f"1 warm-up + median of {runs}: {', '.join(f'{x:.2f}' for x in ts)} s",
+            "cfg1": {"value": 1.0 / med1, "unit": "pairs/s",
+                     "sample": f"1 pair 1x256x512, 8 iters; 1 warm-up + median of {runs}: "
+                               f"{', '.join(f'{x:.2f}' for x in t1)} s"}}
+
+
+def cpu_baseline_tile(cfg, iters: int):
+    """Tiled configs: the oracle on ONE tile of the config (bounded sample), one run."""
+    from oracle import model_ref as M
+
+    torch.set_num_threads(host_threads())
+    sd = M.load_state_dict_seeded(0)
+    th, tw = cfg["tile_hw"]
+    pair = synth.synthetic_batch(1, th, tw, cfg["D"], seed0=1)
     t = [torch.from_numpy(pair[k]) for k in ("left", "right", "mono_left", "mono_right")]
     t0 = time.perf_counter()
     M.forward(sd, *t, iters=iters)
     dt = time.perf_counter() - t0
-    return {"value": 1.0 / dt, "unit": "pairs/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"1 pair 1x{H}x{W}, {iters} iters, oracle (torch CPU convs + numpy hot path), "
-                      f"{dt:.1f} s wall"}
+    return {"value": 1.0 / dt, "unit": "tiles/s", "cores": torch.get_num_threads(), "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"1 tile 1x{th}x{tw}, {iters} iters, oracle, one run: {dt:.1f} s "
+                      f"(one image = {cfg['tiles']} tiles -> {1.0 / (dt * cfg['tiles']):.4f} images/s)"}
 
 
 def epe_vs_reference(model, device):
@@ -142,13 +200,39 @@ def epe_vs_reference(model, device):
     return float(np.abs(disp.astype(np.float64) - fix["disparity"]).mean())
 
 
+def epe_vs_reference_tiled(model, device, preset: str):
+    """The reference TileWrapper + reference model's two-tile stitch at the preset's tile size
+    (tests/golden/tiled_model.npz, 3 iterations) against this build's tiler + model."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fixtures_util import load_fixture  # golden data only
+    from stereoanywhere_amd import tiler
+
+    fix = load_fixture("tiled_model.npz")
+    H, W, tw, th, ov, iters = (int(v) for v in fix[f"{preset}.geom"])
+    seed = 11 + [c for c in ("middlebury", "booster")].index(preset)
+    pair = synth.synthetic_batch(1, H, W, float(fix[f"{preset}.D"]), seed0=seed)
+    t = [torch.from_numpy(pair[k]).to(device) for k in ("left", "right", "mono_left", "mono_right")]
+    st = tiler.TileWrapper(model, tile_width=tw, tile_height=th, overlap=ov)(*t, iters=iters, test_mode=True)
+    got = st[0, 0, ::int(fix["row_step"])].cpu().numpy()
+    return float(np.abs(got.astype(np.float64) - fix[f"{preset}.out"]).mean())
+
+
+# the tiled BASELINE configs (SURVEY §8(d)): padded image, preset, iterations
+TILED = {
+    "cfg3": dict(index=2, image=(1000, 1400), preset="middlebury", iters=32, D=256.0, offload=False),
+    "cfg5": dict(index=4, image=(3008, 4112), preset="booster", iters=32, D=512.0, offload=True),
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg5"],
+                    help="cfg2 = the headline (configs[1]); cfg3 / cfg5 = the tiled configs")
     ap.add_argument("--batch", type=int, default=4, help="pairs per GPU (configs[1]: 4)")
-    ap.add_argument("--iters", type=int, default=22)
+    ap.add_argument("--iters", type=int, default=None, help="GRU iterations (default: the config's)")
     ap.add_argument("--height", type=int, default=540)
     ap.add_argument("--width", type=int, default=960)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -164,26 +248,47 @@ def main():
     if r.world != args.gpus and r.is_main:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {r.world}", file=sys.stderr)
 
-    H, W = args.height, args.width
-    Hp, Wp = (H + 31) // 32 * 32, (W + 31) // 32 * 32
-    H4, W4 = Hp // 4, Wp // 4
     model = StereoAnywhere(dict(PUBLISHED)).eval()
     synth.load_seeded_weights(model, 0)
     model = model.to(device)
-    lo, hi = D.shard_range(args.batch * r.world, r.rank, r.world)
-    inp = make_inputs(hi - lo, H, W, Hp, Wp, 192.0, seed0=1 + lo, device=device)
-    x = (inp["left"], inp["right"], inp["mono_left"], inp["mono_right"])
+    tiled = TILED.get(args.config)
+    if tiled is None:
+        iters = args.iters or 22
+        H, W = args.height, args.width
+        Hp, Wp = (H + 31) // 32 * 32, (W + 31) // 32 * 32
+        lo, hi = D.shard_range(args.batch * r.world, r.rank, r.world)
+        inp = make_inputs(hi - lo, H, W, Hp, Wp, 192.0, seed0=1 + lo, device=device)
+        x = (inp["left"], inp["right"], inp["mono_left"], inp["mono_right"])
+        runner, units, shape = model, hi - lo, (hi - lo, Hp // 4, Wp // 4)
+    else:
+        from stereoanywhere_amd import tiler
+        from stereoanywhere_amd.offload import CPUOffloadWrapper
+        iters = args.iters or tiled["iters"]
+        H, W = tiled["image"]
+        Hp, Wp = (H + 31) // 32 * 32, (W + 31) // 32 * 32
+        # weak scaling over images: every rank tiles its own image
+        inp = make_inputs(1, H, W, Hp, Wp, tiled["D"], seed0=1 + r.rank, device=device)
+        x = (inp["left"], inp["right"], inp["mono_left"], inp["mono_right"])
+        wrap = tiler.from_preset(model, tiled["preset"], batch_tiles=True)
+        tiles = wrap._enumerate_tiles(Hp, Wp)
+        th, tw = min(wrap.tile_height, Hp), min(wrap.tile_width, Wp)
+        tiled["tiles"], tiled["tile_hw"] = len(tiles), (th, tw)
+        runner = CPUOffloadWrapper(wrap) if tiled["offload"] else wrap
+        units, shape = 1, (len(tiles), th // 4, tw // 4)
+
+    def step():
+        return runner(*x, iters=iters, test_mode=True)
 
     with torch.no_grad():
         for i in range(args.warmup):
-            model(*x, iters=args.iters, test_mode=True)
+            step()
             torch.cuda.synchronize()
             log(f"warmup {i + 1}/{args.warmup} done")
         # price the layer-mix-dependent families (Winograd convs, norm epilogues) on one
         # untimed forward
         from stereoanywhere_amd import ops as O
         O.WORK = {}
-        model(*x, iters=args.iters, test_mode=True)
+        step()
         work, O.WORK = O.WORK, None
         torch.cuda.synchronize()
         # timed region: K plain steps -> value.  The per-launch HIP events of the roofline
@@ -192,19 +297,26 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            out, _ = model(*x, iters=args.iters, test_mode=True)
+            out = step()
         torch.cuda.synchronize()
         D.barrier(r)
         elapsed = time.perf_counter() - t0
         log(f"timed {args.steps} steps in {elapsed:.3f} s")
+        # one-stream plain steps: the schedule the per-launch times below are measured in
+        model.stream_overlap = False
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        elapsed_1s = time.perf_counter() - t2
         # per-launch times of one kernel at a time: the side streams' overlap (model.py) would
         # stretch each launch by the work running beside it
-        model.stream_overlap = False
         N.timing_enable(True)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for _ in range(args.steps):
-            model(*x, iters=args.iters, test_mode=True)
+            step()
         torch.cuda.synchronize()
         elapsed_ev = time.perf_counter() - t1
         kt = {k: N.timing_read(k) for k in N.KERNEL_IDS}
@@ -212,16 +324,17 @@ def main():
         model.stream_overlap = True
         log(f"instrumented {args.steps} steps in {elapsed_ev:.3f} s")
         elapsed = D.max_over_ranks(elapsed, r, device)
-        # per-pair metrics gathered once, after the timed region (the only collective)
-        disp = -out[:, 0]
+        # per-unit metrics gathered once, after the timed region (the only collective)
+        disp = out[0] if isinstance(out, tuple) else out
+        disp = -disp[:, 0] if tiled is None else disp[:, 0]
         local = torch.stack([disp.mean((1, 2)), disp.amin((1, 2)), disp.amax((1, 2))], 1).double()
         allm = D.gather_metrics(local, r)
 
-    total_pairs = args.batch * r.world * args.steps
+    total_units = units * r.world * args.steps
     if not r.is_main:
         return
     # every hand-written kernel family: algorithmic work / live event time vs MI355X peak
-    costs = step_costs(hi - lo, H4, W4, args.iters)
+    costs = step_costs(shape[0], shape[1], shape[2], iters)
     costs["conv2d_wino"] = ("TFLOP/s", work.get("conv2d_wino", 0.0))
     costs["conv2d_wino4"] = ("TFLOP/s", work.get("conv2d_wino4", 0.0))
     costs["conv2d_direct"] = ("TFLOP/s", work.get("conv2d_direct", 0.0))
@@ -241,36 +354,50 @@ def main():
                       "avg_launch_us": ms_tot * 1e3 / n_launch}
     dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
     roof = dict(kernels[dom])
-    roof.update({"kernel": dom, "traffic": pmc_traffic(dom, args.batch), "kernels": kernels,
-                 "misc_ms_per_step": kt["misc"][0] / args.steps,
+    roof.update({"kernel": dom, "traffic": pmc_traffic(dom, args.batch) if tiled is None else None,
+                 "kernels": kernels, "misc_ms_per_step": kt["misc"][0] / args.steps,
+                 "schedule": "one-stream (model.stream_overlap = False)",
+                 "one_stream_ms_per_step": elapsed_1s / args.steps * 1e3,
                  "instrumented_ms_per_step": elapsed_ev / args.steps * 1e3,
                  "note": "achieved = algorithmic amount per launch / mean live HIP-event launch time, "
                          "events recorded around every launch over K steps run right after the K "
                          "plain timed steps (the events cost ~6 % of a step), in the one-stream order "
-                         "(model.stream_overlap = False: the plain steps overlap the mono branch and the "
-                         "context encoder with the feature encoder on side streams); "
+                         "(model.stream_overlap = False; its plain time is one_stream_ms_per_step; the "
+                         "headline steps overlap the mono branch and the context encoder with the "
+                         "feature encoder on side streams); "
                          "fp32 FMA peak 157.3 TF/s is the same for MFMA (v_mfma_f32_*_f32) and VALU; "
                          "conv2d_wino / conv2d_wino4 count the Winograd-domain products they execute "
                          "(16/36 resp. 36/144 of the direct convolution's), so their direct-equivalent "
                          "rates are 2.25x resp. 4x achieved"})
+    if tiled is None:
+        metric, unit = "stereo pairs/sec @540x960 D=192 (1/2/4/8 GPU) + EPE vs reference", "pairs/s"
+        config = {"workload": f"configs[1]: batch {args.batch}/GPU x {H}x{W} (padded {Hp}x{Wp}), "
+                              f"{iters} GRU iters, published flags", "global_batch": args.batch * r.world,
+                  "iters": iters, "parallelism": f"dp{r.world} (independent pairs, metrics all_gather)"}
+    else:
+        metric, unit = f"stereo images/sec, tiled ({args.config}) + EPE vs reference", "images/s"
+        config = {"workload": f"configs[{tiled['index']}]: 1 image/GPU {H}x{W} (padded {Hp}x{Wp}), preset "
+                              f"{tiled['preset']} -> {tiled['tiles']} tiles of {th}x{tw} (batch_tiles), "
+                              f"{iters} GRU iters, published flags"
+                              + (", CPUOffloadWrapper (HBM-resident)" if tiled["offload"] else ""),
+                  "global_batch": r.world, "tiles_per_image": tiled["tiles"], "iters": iters,
+                  "parallelism": f"dp{r.world} (independent images)"}
     res = {
-        "metric": "stereo pairs/sec @540x960 D=192 (1/2/4/8 GPU) + EPE vs reference",
-        "value": total_pairs / elapsed, "unit": "pairs/s", "n_gpus": r.world, "steps": args.steps,
+        "metric": metric, "value": total_units / elapsed, "unit": unit, "n_gpus": r.world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded value-noise pairs, "
         "seeded random weights; no dataset/checkpoint offline)",
-        "config": {"workload": f"configs[1]: batch {args.batch}/GPU x {H}x{W} (padded {Hp}x{Wp}), "
-                               f"{args.iters} GRU iters, published flags", "global_batch": args.batch * r.world,
-                   "iters": args.iters, "parallelism": f"dp{r.world} (independent pairs, metrics all_gather)"},
-        "roofline": roof,
-        "gathered_pairs": int(allm.shape[0]),
+        "config": config, "roofline": roof, "gathered_units": int(allm.shape[0]),
     }
+    if tiled is not None:
+        res["tiles_per_s"] = total_units * tiled["tiles"] / elapsed
     if not args.no_epe:
-        res["epe_vs_reference"] = epe_vs_reference(model, device)
+        res["epe_vs_reference"] = (epe_vs_reference(model, device) if tiled is None
+                                   else epe_vs_reference_tiled(model, device, tiled["preset"]))
         log(f"EPE vs reference {res['epe_vs_reference']:.3g}")
     if r.world == 1 and not args.no_cpu_baseline:
         log("cpu baseline (oracle, bounded sample) ...")
-        res["cpu_baseline"] = cpu_baseline(args.iters, Hp, Wp)
+        res["cpu_baseline"] = cpu_baseline(iters, Hp, Wp) if tiled is None else cpu_baseline_tile(tiled, iters)
     print(json.dumps(res))
 
 
