@@ -35,10 +35,27 @@ class HipCorrBlock1D:
             _shape = (B, H, W1, W2)
         self.shape = _shape
         self.pyramid = _pyramid
-        B, H, W1, W2 = _shape
-        _, offs, wids = ops.pyramid_geometry(W2, num_levels)
-        # [B*H*W1, 1, 1, W_l] views, the reference's per-level shape (corr.py:85-91)
-        self.corr_pyramid = [_pyramid[:, o:o + w].unsqueeze(1).unsqueeze(1) for o, w in zip(offs, wids)]
+        self._views = None
+
+    @property
+    def corr_pyramid(self):
+        """The reference's ``corr_pyramid`` list (corr.py:85-91): num_levels + 1 tensors of
+        shape [B*H*W1, 1, 1, W2 >> i].  Levels 0..num_levels-1 are views of the lookup's
+        buffer; the last level, which the reference builds and never reads, is pooled from
+        the one before it on first access (one HIP pyramid launch), not in the forward."""
+        if self._views is None:
+            B, H, W1, W2 = self.shape
+            _, offs, wids = ops.pyramid_geometry(W2, self.num_levels)
+            views = [self.pyramid[:, o:o + w].unsqueeze(1).unsqueeze(1) for o, w in zip(offs, wids)]
+            last = views[-1].reshape(-1, wids[-1])
+            if wids[-1] >= 2:
+                extra = ops.pyramid_from_volume(last.contiguous(), 2)
+                w = wids[-1] // 2
+                views.append(extra[:, wids[-1]:wids[-1] + w].unsqueeze(1).unsqueeze(1))
+            else:   # avg_pool2d of a width-1 (or 0) row is empty
+                views.append(last.new_empty((last.shape[0], 1, 1, 0)))
+            self._views = views
+        return self._views
 
     @classmethod
     def from_features(cls, fmap2: torch.Tensor, fmap3: torch.Tensor, num_levels: int = 4, radius: int = 4,
@@ -79,6 +96,23 @@ class HipCorrBlock1D:
     @staticmethod
     def corr(fmap2: torch.Tensor, fmap3: torch.Tensor) -> torch.Tensor:
         return ops.corr_volume(fmap2.float().contiguous(), fmap3.float().contiguous())
+
+
+class CorrSampler(torch.autograd.Function):
+    """Replacement of the reference's native-sampler hook (corr.py:17-29,
+    ``corr_sampler.forward(volume [B,H,W1,W_i], coords [B,1,H,W1], radius)`` -> the 2r+1 taps
+    of one pyramid level at x = coords, linear interpolation, zero outside [0, W_i - 1]).
+    Forward only (the inference tier): one HIP lookup over a one-level pyramid."""
+
+    @staticmethod
+    def forward(ctx, volume, coords, radius):
+        B, H, W1, Wi = volume.shape
+        pyr = ops.pyramid_from_volume(volume.contiguous().reshape(B * H * W1, Wi), 1)
+        return ops.corr_lookup(pyr, None, Wi, 1, int(radius), coords[:, :1].contiguous())
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        raise NotImplementedError("CorrSampler.backward: training is outside this tier")
 
 
 # args.corr_implementation -> block class.  The reference's "reg" (torch) and "reg_cuda"

@@ -57,7 +57,7 @@ constexpr int NPT = 36;                   // transform points
 constexpr int CO = 32;                    // output channels per block
 
 // Two block shapes of the same algorithm.  Large (the default): 8 waves, 64 tiles, 8-channel
-// chunks, one block per CU (158 KiB of LDS).  Small (SA_W4_SHAPE=small): 4 waves, 32 tiles,
+// chunks, one block per CU (158 KiB of LDS).  Small (block_shape 2): 4 waves, 32 tiles,
 // 4-channel chunks, 66 KiB, two blocks per CU, so one block's first DMA wait and epilogue
 // overlap the other's MFMAs (per block ~6-8k cycles until the first chunk lands and ~9k of
 // epilogue around 6.8k per chunk, scripts/w4_clock.py); it is not faster in the forward.
@@ -612,15 +612,10 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
                                              int block_shape, void *stream) {
   SA_REQUIRE(nprob >= 1 && nprob <= MAX_PROB && probs, "sa_conv2d_k3_wino4_multi: 1..%d problems", MAX_PROB);
   SA_REQUIRE(block_shape >= 0 && block_shape <= 2, "sa_conv2d_k3_wino4_multi: block_shape 0..2");
-  static const int env_shape = [] {   // SA_W4_SHAPE=big|small forces one block shape (A/B runs)
-    const char *e = getenv("SA_W4_SHAPE");
-    return e && e[0] == 's' ? 2 : e && e[0] == 'b' ? 1 : 0;
-  }();
   // Large blocks unless the caller asks for small ones (block_shape 2).  The small shape
   // measured 2-8% faster on standalone launches of Cin <= 128 with a few rounds of blocks
   // (qh08, convc2) but not faster in the forward as a blanket choice.
-  const int shape = env_shape ? env_shape : block_shape;
-  const bool small = shape == 2;
+  const bool small = block_shape == 2;
   const int nt = small ? W4Small::NT : W4Big::NT;
   W4Launch L{};
   long total = 0;

@@ -23,9 +23,8 @@ off (the reference CLI's store_true defaults, test.py:94-98).
 """
 from __future__ import annotations
 
-import os
-
 import math
+from dataclasses import dataclass, field
 from types import SimpleNamespace
 
 import torch
@@ -53,23 +52,31 @@ def _normalize_pair(a: torch.Tensor, b: torch.Tensor, eps: float = 1e-4):
 
 
 
-# independent 3x3 convs of the update block share one launch (ops.conv2d_k3_multi);
-# SA_GROUP_CONVS=0 launches them one by one (A/B timing)
-_GROUP_CONVS = os.environ.get("SA_GROUP_CONVS", "1") != "0"
-# GRU z/r gates in the F(4x4) conv epilogue (ops.conv2d_k3_multi gate=...) where its
-# preconditions hold; SA_FUSE_GATES=0 keeps the separate gate kernels (A/B timing)
-_FUSE_GATES = os.environ.get("SA_FUSE_GATES", "1") != "0"
-# ... and the state update in the r*h conv's epilogue (SA_FUSE_OUT=0: gru_out kernel, r*h conv
-# split over its input channels)
-_FUSE_OUT = os.environ.get("SA_FUSE_OUT", "1") != "0"
-# mono branch on a second stream beside the encoders (SA_MONO_STREAM=0: one stream)
-_MONO_STREAM = os.environ.get("SA_MONO_STREAM", "1") != "0"
-# the context encoder on a third stream (SA_CNET_SIDE=1: after the mono branch on the second,
-# 0: on the main stream)
-_CNET_SIDE = int(os.environ.get("SA_CNET_SIDE", "2"))
-# launches of the update block on F(4x4)'s small blocks (two per CU), by name: "q16" (gru16's
-# r*h conv + the motion conv), "q08" (gru08's + gru32's r*h convs), "zr16", "zr08", "pro32"
-_SMALL_LAUNCHES = set(filter(None, os.environ.get("SA_SMALL_LAUNCHES", "").split(",")))
+@dataclass
+class ScheduleOptions:
+    """Launch-schedule choices of the MI355X forward.  Every combination computes the same
+    function (tests/test_gpu_model.py runs each non-default path against the reference
+    fixture); the defaults are the measured-fastest schedule.  Set per instance
+    (``model.opts``), e.g. by the A/B scripts under scripts/."""
+    # independent 3x3 convs of the update block share one launch (ops.conv2d_k3_multi)
+    group_convs: bool = True
+    # GRU z/r gates in the F(4x4) conv epilogue where its preconditions hold; False keeps the
+    # separate gate kernels
+    fuse_gates: bool = True
+    # ... and the state update in the r*h conv's epilogue (False: gru_out kernel, r*h conv split
+    # over its input channels)
+    fuse_out: bool = True
+    # mono branch on a second HIP stream beside the encoders (False: one stream)
+    mono_stream: bool = True
+    # the context encoder on a third stream (2), after the mono branch on the second (1), or on
+    # the main stream (0)
+    cnet_side: int = 2
+    # launches of the update block on F(4x4)'s small blocks (two per CU), by name: "q16" (gru16's
+    # r*h conv + the motion conv), "q08" (gru08's + gru32's r*h convs), "zr16", "zr08", "pro32"
+    small_launches: frozenset = field(default_factory=frozenset)
+    # the encoders' 7x7 stems and stride-2 convs on the direct fp32-MFMA kernel (False: MIOpen)
+    direct_conv: bool = True
+
 
 class StereoAnywhere(nn.Module):
     def __init__(self, args):
@@ -100,6 +107,7 @@ class StereoAnywhere(nn.Module):
         # side streams before the update loop (_forward); False runs everything on the
         # caller's stream (bench.py's per-launch event timing)
         self.stream_overlap = True
+        self.opts = ScheduleOptions()
 
     # ------------------------------------------------------------------ weights
     def _split_gru(self, gru, hidden: int):
@@ -120,6 +128,7 @@ class StereoAnywhere(nn.Module):
         """Derived tensors (split GRU kernels, permuted classifier kernels, folded BatchNorm),
         rebuilt when any parameter or buffer is modified or moved."""
         key = tuple((p.data_ptr(), p._version) for p in list(self.parameters()) + list(self.buffers()))
+        key += (self.opts.direct_conv,)
         if self._derived_key != key:
             ub = self.update_block
             hd = self.args.context_dims
@@ -152,9 +161,8 @@ class StereoAnywhere(nn.Module):
                 # eval-BatchNorm norm1 folded into the context encoder's conv1s
                 d["fold_cnet"] = encoders.fold_table(self.cnet)
                 # the stems and the stride-2 blocks on the direct fp32-MFMA conv (ops.conv_direct)
-                # (SA_DIRECT_CONV=0 leaves them on MIOpen, for A/B timing)
-                d["direct"] = (encoders.direct_table(self.cnet, self.fnet)
-                               if os.environ.get("SA_DIRECT_CONV", "1") != "0" else {})
+                # (opts.direct_conv = False leaves them on MIOpen)
+                d["direct"] = encoders.direct_table(self.cnet, self.fnet) if self.opts.direct_conv else {}
                 for gk in ("g08", "g16", "g32"):
                     g = d[gk]
                     half = g["wqh"].shape[1] // 2
@@ -227,11 +235,11 @@ class StereoAnywhere(nn.Module):
 
         # The mono branch (volume -> hourglass -> alignment) reads only the mono maps, so it can
         # run on a second HIP stream beside the encoders, filling their launch tails and
-        # HBM-bound passes with the hourglass's compute (SA_MONO_STREAM=0 turns it off).  The main stream
+        # HBM-bound passes with the hourglass's compute (opts.mono_stream = False turns it off).  The main stream
         # waits for it before the pyramids; tensors it hands over are recorded on the main
         # stream so the caching allocator does not reuse them early.
         main = torch.cuda.current_stream(dev)
-        side = self._side_stream(dev) if _MONO_STREAM and self.stream_overlap else None
+        side = self._side_stream(dev) if self.opts.mono_stream and self.stream_overlap else None
         if side is not None:
             side.wait_stream(main)
             with torch.cuda.stream(side):
@@ -243,12 +251,12 @@ class StereoAnywhere(nn.Module):
             ctx = [conv(torch.relu(x[1])) for x, conv in zip(cl, self.context_zqr_convs)]
             fm = self.fnet(torch.cat([image2, image3], 0))
         else:
-            if side is not None and _CNET_SIDE:
-                # the context encoder (it reads only mde2) on a third stream (SA_CNET_SIDE=2)
+            if side is not None and self.opts.cnet_side:
+                # the context encoder (it reads only mde2) on a third stream (cnet_side=2)
                 # or after the mono branch on the second (1), so the main stream runs the
                 # feature encoder alone
                 cs = side
-                if _CNET_SIDE == 2:
+                if self.opts.cnet_side == 2:
                     cs = self._side_stream(dev, 1)
                     cs.wait_stream(main)
                 with torch.cuda.stream(cs):
@@ -362,7 +370,8 @@ class StereoAnywhere(nn.Module):
         shapes = {"08": (H4, W4), "16": (H8, W8), "32": (H16, W16)}
         hd = h08.shape[1]
         # the F(4x4) kernel's preconditions at every level (W % 4; planes then stay 16-byte aligned)
-        fused = _FUSE_GATES and ops.gate_f4_ok() and all(s[1] % 4 == 0 for s in shapes.values())
+        o = self.opts
+        fused = o.fuse_gates and ops.gate_f4_ok() and all(s[1] % 4 == 0 for s in shapes.values())
         if fused:
             # one buffer per level, [h | x | r*h]: the z/r conv reads cat(h, x) and the r*h conv
             # reads r*h as channel views of it (no torch.cat)
@@ -380,7 +389,7 @@ class StereoAnywhere(nn.Module):
             x32 = torch.empty((B, xdims["32"], H16, W16), device=dev, dtype=f32)
             rh = {k: torch.empty_like(h) for k, h in (("08", h08), ("16", h16), ("32", h32))}
         hs = {"08": h08, "16": h16, "32": h32}
-        fuse_out = fused and _FUSE_OUT
+        fuse_out = fused and o.fuse_out
         z = {k: torch.empty(h.shape, device=dev, dtype=f32) for k, h in hs.items()}
         cz = [c[:, 0:128] for c in ctx]
         cr = [c[:, 128:256] for c in ctx]
@@ -388,9 +397,9 @@ class StereoAnywhere(nn.Module):
         lvl = {"08": 0, "16": 1, "32": 2}
 
         def conv_group(*probs, name=None):
-            """Independent 3x3 convs in one launch (SA_GROUP_CONVS=0: one launch each)."""
-            if _GROUP_CONVS:
-                return ops.conv2d_k3_multi(*probs, small_blocks=name in _SMALL_LAUNCHES)
+            """Independent 3x3 convs in one launch (opts.group_convs = False: one launch each)."""
+            if o.group_convs:
+                return ops.conv2d_k3_multi(*probs, small_blocks=name in o.small_launches)
             return [ops.conv2d_k3(**p) for p in probs]
 
         def gate_x_h(key, x, h):

@@ -516,8 +516,8 @@ class WinoFilters:
         self.u2, self.u4, self.cin, self.cout = u2, u4, cin, cout
 
 
-# SA_WINO4=0 keeps every 3x3 conv on the F(2x2,3x3) kernel (A/B runs)
-_WINO4 = os.environ.get("SA_WINO4", "1") != "0"
+# False keeps every 3x3 conv on the F(2x2,3x3) kernel (set by A/B scripts and tests)
+_WINO4 = True
 
 
 def wino_weights(weight: torch.Tensor) -> WinoFilters:

@@ -126,3 +126,31 @@ def test_side_streams_match_one_stream(model):
     for o in outs:
         assert np.isfinite(o).all()
         assert epe(o, ref) < 1e-5
+
+
+@pytest.mark.parametrize("change", [dict(group_convs=False), dict(fuse_gates=False), dict(fuse_out=False),
+                                    dict(mono_stream=False), dict(cnet_side=1), dict(cnet_side=0),
+                                    dict(small_launches=frozenset({"q16", "q08", "zr16", "zr08", "pro32"})),
+                                    dict(direct_conv=False), dict(wino4=False)])
+def test_schedule_options_vs_reference(change):
+    """Every non-default launch schedule (stereoanywhere_amd.model.ScheduleOptions; ops._WINO4)
+    computes the same forward: cfg1 against the reference's disparity."""
+    import dataclasses
+
+    from stereoanywhere_amd import ops
+    m = StereoAnywhere(dict(PUBLISHED)).eval()
+    synth.load_seeded_weights(m, 0)
+    m = m.cuda()
+    wino4 = change.pop("wino4", True)
+    m.opts = dataclasses.replace(m.opts, **change)
+    fix = load_fixture("cfg1_256x512_it8.npz")
+    pair = regenerate_inputs(fix, 1, 256, 512, 64.0)
+    old = ops._WINO4
+    ops._WINO4 = wino4
+    try:
+        disp = run(m, pair, 8)
+    finally:
+        ops._WINO4 = old
+    e = epe(disp, fix["disparity"])
+    print(change, "wino4" if wino4 else "no wino4", "EPE", e)
+    assert e < 1e-3

@@ -381,3 +381,25 @@ def test_fused_hourglass_matches_torch(shape):
         ref = torch.nn.functional.conv3d(hg(x, fl, fr), wcls, padding=1)
     torch.testing.assert_close(vd, ref[:, 0:1], atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(vc, ref[:, 1:2], atol=1e-4, rtol=1e-4)
+
+
+def test_corr_block_contract_five_levels_and_sampler_shim(micro):
+    """HipCorrBlock1D exposes the reference's num_levels + 1 pyramid levels (corr.py:85-91,
+    golden pyr.level0..4), and the CorrSampler replacement (corr.py:17-29 hook; the
+    CorrBlockFast1D call pattern, corr.py:47-58: level i at coords / 2**i) reproduces the
+    reference lookup level by level (golden lookup.out)."""
+    from stereoanywhere_amd.corr import CorrSampler, HipCorrBlock1D
+    vol = g(micro["corr.out"])                       # [2,3,37,1,45]
+    blk = HipCorrBlock1D(vol, num_levels=4, radius=4)
+    assert len(blk.corr_pyramid) == 5
+    for i, lv in enumerate(blk.corr_pyramid):
+        ref = micro[f"pyr.level{i}"]
+        assert tuple(lv.shape) == ref.shape
+        np.testing.assert_allclose(c(lv), ref, atol=1e-6)
+    coords = g(micro["lookup.coords"])
+    np.testing.assert_allclose(c(blk(coords)), micro["lookup.out"], atol=1e-5)
+    B, H, W1 = 2, 3, 37
+    for i in range(4):
+        lvl = blk.corr_pyramid[i].reshape(B, H, W1, -1)
+        taps = CorrSampler.apply(lvl, coords[:, :1] / 2 ** i, 4)
+        np.testing.assert_allclose(c(taps), micro["lookup.out"][:, 9 * i:9 * i + 9], atol=1e-5)

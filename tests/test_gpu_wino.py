@@ -188,32 +188,19 @@ def test_wino4_gru_gate_epilogues(monkeypatch):
                                            out2=torch.empty(1, 32, 8, 10, device=dev))))
 
 
-_SMALL_SHAPE_CHECK = r"""
-import torch, torch.nn.functional as F
-from stereoanywhere_amd import ops
-ops._WINO4_MIN_BLOCKS = 0
-g = torch.Generator(device="cpu").manual_seed(5)
-for N, Cin, Cout, H, W in ((2, 64, 96, 20, 52), (1, 128, 64, 136, 240), (2, 16, 32, 9, 36)):
-    x = torch.randn(N, Cin, H, W, generator=g).cuda()
-    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)).cuda()
-    ops.WORK = {}
-    out, (mean, rstd) = ops.conv2d_k3(x, ops.wino_weights(w), stats=True)
-    assert "conv2d_wino4" in ops.WORK
-    ref = F.conv2d(x, w, padding=1)
-    torch.testing.assert_close(out, ref, atol=1e-4, rtol=1e-4)
-    torch.testing.assert_close(mean, ref.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
-print("small shape ok")
-"""
-
-
-def test_wino4_small_block_shape():
-    """The 4-wave / 32-tile / 4-channel-chunk block shape (SA_W4_SHAPE=small, read once per
-    process: checked in a child process) against torch, with InstanceNorm statistics."""
-    import os
-    import subprocess
-    import sys
-    env = dict(os.environ, SA_W4_SHAPE="small")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", _SMALL_SHAPE_CHECK], env=env, cwd=root, capture_output=True,
-                       text=True, timeout=110)
-    assert r.returncode == 0 and "small shape ok" in r.stdout, r.stdout + r.stderr
+def test_wino4_small_block_shape(monkeypatch):
+    """The 4-wave / 32-tile / 4-channel-chunk block shape (block_shape 2 of
+    sa_conv2d_k3_wino4_multi_gate, ops.conv2d_k3_multi(small_blocks=True)) against torch,
+    with InstanceNorm statistics."""
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    for N, Cin, Cout, H, W in ((2, 64, 96, 20, 52), (1, 128, 64, 136, 240), (2, 16, 32, 9, 36)):
+        x = torch.randn(N, Cin, H, W, generator=g).cuda()
+        w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)).cuda()
+        ops.WORK = {}
+        out, (mean, rstd) = ops.conv2d_k3_multi(dict(x=x, U=ops.wino_weights(w), stats=True), small_blocks=True)[0]
+        assert "conv2d_wino4" in ops.WORK
+        ops.WORK = None
+        ref = F.conv2d(x, w, padding=1)
+        torch.testing.assert_close(out, ref, atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(mean, ref.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
