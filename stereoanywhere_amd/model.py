@@ -400,7 +400,7 @@ class StereoAnywhere(nn.Module):
             """Independent 3x3 convs in one launch (opts.group_convs = False: one launch each)."""
             if o.group_convs:
                 return ops.conv2d_k3_multi(*probs, small_blocks=name in o.small_launches)
-            return [ops.conv2d_k3(**p) for p in probs]
+            return [ops.conv2d_k3_multi(p, small_blocks=name in o.small_launches)[0] for p in probs]
 
         def gate_x_h(key, x, h):
             g = dw["g" + key]
