@@ -168,6 +168,168 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K1 v2 — the same volume + truncation + pyramid for the common case (C % 16 == 0, W1 and W2
+// multiples of 4, 16-byte aligned rows), built for W/4 of a few hundred pixels:
+//   block = one image row (b, h), 64 left pixels j (4 waves x one 16-row MFMA tile) x up to 256
+//           right pixels k; W1 = 240 takes 3.75 blocks per row with no padded j rows
+//   wave  = 16 j x 256 k as 16 v_mfma_f32_16x16x4_f32 tiles whose columns interleave by 4:
+//           tile (g, t) holds pixels k = 64 g + 4 n + t (n = the accumulator column), so a lane
+//           owns 4 consecutive k of every row it holds -> level 0 is one float4 store, levels 1
+//           and 2 are formed in registers and level 3 takes one lane shuffle
+//   chunk = 16 channels of both panels (A [16][64], B [16][256]) copied global -> LDS by
+//           LDS-DMA (no staging registers), double-buffered, one barrier per chunk; 40 KiB per
+//           block, so four blocks (16 waves) share a CU and cover each other's waits
+//   per K step (4 channels): one ds_read_b32 (A), four ds_read_b128 (B), 16 MFMAs
+// Arithmetic per element is the v1 kernel's: one k-ordered chain of exact fp32 MFMA products
+// and the same epilogue expressions.
+constexpr int V2_J = 64, V2_K = 256, V2_KC = 16;
+constexpr int V2_ABUF = V2_KC * V2_J, V2_BBUF = V2_KC * V2_K, V2_BUF = V2_ABUF + V2_BBUF;
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void v2_dma16(__amdgpu_buffer_rsrc_t r, float *lds, int voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)lds, 16, voff, 0, 0, 0);
+}
+
+template <bool TRUNC, bool POW2>
+__global__ __launch_bounds__(256, 4) void corr_pyramid_v2_kernel(const float *__restrict__ f2, const float *__restrict__ f3,
+                                                              Geo g, int jblocks, int kblocks, int kstep, float sqrt_c,
+                                                              float inv_c, const float *__restrict__ tdisp,
+                                                              const float *__restrict__ tconf, float atten,
+                                                              float *__restrict__ pyr, int f2_bytes, int f3_bytes) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * V2_BUF];
+  const unsigned nwg = gridDim.x;
+  const unsigned wid = sa::xcd_remap(blockIdx.x, nwg);
+  // consecutive ids: the j blocks of one (row, k block) -> they share the B panel in L2
+  const int jb = wid % jblocks, rest = wid / jblocks, kb = rest % kblocks, bh = rest / kblocks;
+  const int b = bh / g.H, h = bh % g.H;
+  // k range [k0, kend): kstep (a multiple of 64, <= 256) splits W2 into near-equal blocks
+  const int j0 = jb * V2_J, k0 = kb * kstep, kend = min(k0 + kstep, g.W2);
+  const int ngroups = (kend - k0 + 63) >> 6;   // 64-wide column groups with work (wave-uniform)
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(f2), (short)0, f2_bytes,
+                                                                      0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(f3), (short)0, f3_bytes,
+                                                                      0x00020000);
+  // DMA sources: wave w fills A rows 4w..4w+3 (lane: channel 4w + lane/16, j0 + 4 (lane%16)) and
+  // B rows 4w..4w+3 (one channel each, k0 + 4 lane); out-of-range groups read 0
+  const long plane1 = (long)g.H * g.W1, plane2 = (long)g.H * g.W2;
+  const int ja = j0 + 4 * (lane & 15);
+  int aoff = (ja < g.W1) ? (int)((((long)b * g.C + 4 * w + (lane >> 4)) * plane1 + (long)h * g.W1 + ja) * 4) : 0x7ffffff0;
+  const int kbq = k0 + 4 * lane;
+  int boff[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    boff[q] = (kbq < kend) ? (int)((((long)b * g.C + 4 * w + q) * plane2 + (long)h * g.W2 + kbq) * 4) : 0x7ffffff0;
+  const int astep = (int)(V2_KC * plane1 * 4), bstep = (int)(V2_KC * plane2 * 4);
+  auto issue = [&](int kc, int buf) __attribute__((always_inline)) {
+    float *pa = smem + buf * V2_BUF, *pb = pa + V2_ABUF;
+    v2_dma16(ra, pa + w * 256, aoff == 0x7ffffff0 ? aoff : aoff + kc * astep);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v2_dma16(rb, pb + (4 * w + q) * V2_K, boff[q] == 0x7ffffff0 ? boff[q] : boff[q] + kc * bstep);
+  };
+
+  f32x4v acc[4][4];
+#pragma unroll
+  for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[gg][t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  const int nchunks = g.C / V2_KC;
+  const int ar = (lane >> 4) * V2_J + 16 * w + (lane & 15);   // A[c = lane/16][16 w + lane%16]
+  const int br = (lane >> 4) * V2_K + 4 * (lane & 15);         // B[c = lane/16][4 n .. 4 n + 3]
+  const bool active = j0 + 16 * w < g.W1;                       // wave-uniform: rows left to compute
+  issue(0, 0);
+#pragma unroll 1
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const int cur = kc & 1;
+    __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
+    if (kc + 1 < nchunks) issue(kc + 1, cur ^ 1);
+    if (!active) continue;
+    const float *pa = smem + cur * V2_BUF + ar, *pb = smem + cur * V2_BUF + V2_ABUF + br;
+#pragma unroll
+    for (int s = 0; s < V2_KC / 4; ++s) {
+      const float a = pa[s * 4 * V2_J];
+      f32x4v bv[4];
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) bv[gg] = *reinterpret_cast<const f32x4v *>(pb + s * 4 * V2_K + 64 * gg);
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg)
+        if (gg < ngroups) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            acc[gg][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv[gg][t], acc[gg][t], 0, 0, 0);
+        }
+    }
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  const int n = lane & 15;
+  float dj[4], mj[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = j0 + 16 * w + 4 * (lane >> 4) + i;
+    dj[i] = mj[i] = 0.f;
+    if (TRUNC && j < g.W1) {
+      const long pix = ((long)b * g.H + h) * g.W1 + j;
+      dj[i] = tdisp[pix];
+      mj[i] = tconf[pix];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = j0 + 16 * w + 4 * (lane >> 4) + i;
+    const bool jok = j < g.W1;
+    float *row_ptr = pyr + (((long)b * g.H + h) * g.W1 + j) * g.rs;
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const int P = k0 + 64 * gg + 4 * n;
+      float v[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float x = POW2 ? acc[gg][t][i] * inv_c : acc[gg][t][i] / sqrt_c;
+        if (TRUNC) {
+          const float center = (float)j - dj[i];
+          const float tv = center - (float)(P + t);
+          const float s = sa::sigmoidf_fast(tv);
+          const float T = 1.0f * (1.0f - mj[i]) + mj[i] * (s * (1.0f - atten) + atten);
+          x = T * x;
+        }
+        v[t] = x;
+      }
+      if (P >= kend) continue;   // (kend - k0 is a multiple of 8 unless kend == W2)
+      if (jok) {
+        if (P + 3 < kend) {
+          *reinterpret_cast<f32x4v *>(row_ptr + P) = f32x4v{v[0], v[1], v[2], v[3]};
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (P + t < kend) row_ptr[P + t] = v[t];
+        }
+      }
+      if (g.nlev > 1) {
+        const float l1a = (v[0] + v[1]) * 0.5f, l1b = (v[2] + v[3]) * 0.5f;
+        const int k1 = P >> 1;
+        if (jok && k1 < g.wid[1]) row_ptr[g.off[1] + k1] = l1a;
+        if (jok && k1 + 1 < g.wid[1]) row_ptr[g.off[1] + k1 + 1] = l1b;
+        if (g.nlev > 2) {
+          const float l2 = (l1a + l1b) * 0.5f;
+          const int k2 = P >> 2;
+          if (jok && k2 < g.wid[2]) row_ptr[g.off[2] + k2] = l2;
+          if (g.nlev > 3) {
+            const float l3 = (l2 + __shfl_xor(l2, 1)) * 0.5f;
+            const int k3 = P >> 3;
+            if (jok && (n & 1) == 0 && k3 < g.wid[3]) row_ptr[g.off[3] + k3] = l3;
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);   // one (row, group) at a time: bounds the registers
+    }
+  }
+}
+
 // Pyramid from an existing volume (mono path, stereoanywhere.py:257-259): one wave per
 // row; each lane takes 8 consecutive level-0 values and emits the 4+2+1 coarser cells.
 __global__ __launch_bounds__(256) void pyramid_from_volume_kernel(const float *__restrict__ vol,
@@ -297,6 +459,35 @@ extern "C" int sa_corr_volume_pyramid(const float *fmap2, const float *fmap3, in
                    (reinterpret_cast<uintptr_t>(fmap2) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(fmap3) % 16 == 0);
   hipStream_t s = sa::as_stream(stream);
+  const long f2_bytes = (long)B * C * H * W1 * 4, f3_bytes = (long)B * C * H * W2 * 4;
+  if (vec && C % V2_KC == 0 && row_stride % 4 == 0 && reinterpret_cast<uintptr_t>(pyramid) % 16 == 0 &&
+      f2_bytes < (1L << 31) - 64 && f3_bytes < (1L << 31) - 64) {
+    const int jblocks = (W1 + V2_J - 1) / V2_J, kblocks = (W2 + V2_K - 1) / V2_K;
+    const int kstep = ((W2 + kblocks - 1) / kblocks + 63) / 64 * 64;   // <= V2_K
+    const long nb = (long)B * H * jblocks * kblocks;
+    SA_REQUIRE(nb < (1L << 31), "sa_corr_volume_pyramid: grid too large");
+    int ex = 0;
+    const float mant = frexpf(sqrt_c, &ex);
+    const bool pow2 = mant == 0.5f;
+    const float inv = pow2 ? 1.0f / sqrt_c : 0.0f;
+    sa::TimingScope ts(SA_K_CORR_PYRAMID, s);
+    const bool tr = trunc_disp != nullptr;
+    const unsigned nbu = (unsigned)nb;
+    const int a2 = (int)f2_bytes, a3 = (int)f3_bytes;
+    if (tr && pow2)
+      corr_pyramid_v2_kernel<true, true><<<nbu, 256, 0, s>>>(fmap2, fmap3, g, jblocks, kblocks, kstep, sqrt_c, inv, trunc_disp,
+                                                             trunc_conf, atten, pyramid, a2, a3);
+    else if (tr)
+      corr_pyramid_v2_kernel<true, false><<<nbu, 256, 0, s>>>(fmap2, fmap3, g, jblocks, kblocks, kstep, sqrt_c, inv,
+                                                              trunc_disp, trunc_conf, atten, pyramid, a2, a3);
+    else if (pow2)
+      corr_pyramid_v2_kernel<false, true><<<nbu, 256, 0, s>>>(fmap2, fmap3, g, jblocks, kblocks, kstep, sqrt_c, inv, nullptr,
+                                                              nullptr, atten, pyramid, a2, a3);
+    else
+      corr_pyramid_v2_kernel<false, false><<<nbu, 256, 0, s>>>(fmap2, fmap3, g, jblocks, kblocks, kstep, sqrt_c, inv, nullptr,
+                                                               nullptr, atten, pyramid, a2, a3);
+    return sa::check_launch("sa_corr_volume_pyramid");
+  }
   const unsigned nblk = (unsigned)((long)B * H * g.tilesJ * g.tilesK);
   sa::TimingScope ts(SA_K_CORR_PYRAMID, s);
   const bool tr = trunc_disp != nullptr;

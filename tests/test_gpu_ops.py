@@ -55,8 +55,11 @@ def test_corr_volume_matches_reference_vector(micro):
     np.testing.assert_allclose(vol, micro["corr.out"], atol=2e-5)
 
 
-def test_truncated_pyramid():
-    B, C, H, W = 2, 256, 4, 96
+@pytest.mark.parametrize("W", [96, 240, 280, 520])
+def test_truncated_pyramid(W):
+    """Volume x truncation -> pyramid (v2 kernel: 64-column groups, W2 > 256 split into
+    near-equal k blocks) against the oracle."""
+    B, C, H = 2, 256, 4
     rng = np.random.default_rng(3)
     f2 = rng.standard_normal((B, C, H, W)).astype(np.float32)
     f3 = rng.standard_normal((B, C, H, W)).astype(np.float32)
