@@ -373,50 +373,73 @@ __global__ __launch_bounds__(256) void pyramid_from_volume_kernel(const float *_
 // with loads coalesced along W1, then writes each pixel's pyramid row segment from LDS.  Any
 // W2 is handled chunk by chunk: a chunk starts at a multiple of 8, so every level-1/2/3 cell
 // (a pair / quad / octet of level-0 cells) lies inside one chunk.
-constexpr int PT_J = 64, PT_CHUNK = 256;
+constexpr int PT_J = 64, PT_CHUNK = 256, PT_PITCH = PT_CHUNK + 4;   // 16-byte aligned rows
 
 __global__ __launch_bounds__(256) void pyramid_from_strided_kernel(const float *__restrict__ vol, long sb, long sh,
                                                                    long sk, int H, int W1, int W2, Geo g,
                                                                    float *__restrict__ pyr) {
-  __shared__ float tile[PT_J][PT_CHUNK + 1];
+  __shared__ __attribute__((aligned(16))) float tile[PT_J * PT_PITCH];
   const int j0 = blockIdx.x * PT_J, h = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const float *src = vol + b * sb + h * sh + j0;
-  const bool jok = j0 + lane < W1;
+  // loads: thread t takes 4 consecutive pixels j = 4 (t % 16) .. + 3 of cell k = 16 i + t / 16
+  // (one float4; W1 % 4 == 0, so a group is wholly inside or outside), 16 cells per pass, all
+  // of a chunk's loads in flight before the transposing LDS writes.  LDS rows are XOR-swizzled
+  // by 4-cell groups (swz) so the writes of 16 pixels of one cell spread over the banks.
+  const int tq = threadIdx.x & 15, tk = threadIdx.x >> 4;
+  const int jq = 4 * tq;
+  const bool qok = j0 + jq < W1;
+  auto swz = [](int j) { return ((j >> 2) & 7) << 2; };
   for (int c0 = 0; c0 < W2; c0 += PT_CHUNK) {
     const int cw = min(PT_CHUNK, W2 - c0);
     if (c0 > 0) __syncthreads();  // the previous chunk's rows have been read
-    for (int k = wv; k < cw; k += 4) tile[lane][k] = jok ? src[(long)(c0 + k) * sk + lane] : 0.0f;
+    float4 q[PT_CHUNK / 16];
+#pragma unroll
+    for (int i = 0; i < PT_CHUNK / 16; ++i) {
+      const int k = 16 * i + tk;
+      q[i] = (qok && k < cw) ? *reinterpret_cast<const float4 *>(src + (long)(c0 + k) * sk + jq)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < PT_CHUNK / 16; ++i) {
+      const int k = 16 * i + tk;
+      tile[(jq + 0) * PT_PITCH + (k ^ swz(jq + 0))] = q[i].x;
+      tile[(jq + 1) * PT_PITCH + (k ^ swz(jq + 1))] = q[i].y;
+      tile[(jq + 2) * PT_PITCH + (k ^ swz(jq + 2))] = q[i].z;
+      tile[(jq + 3) * PT_PITCH + (k ^ swz(jq + 3))] = q[i].w;
+    }
     __syncthreads();
+    // a lane per 4 consecutive cells: level 0 as one float4, levels 1-2 in registers, level 3
+    // from the neighbour lane
+    const int lb = 4 * lane, base = c0 + lb;
     for (int jj = wv; jj < PT_J; jj += 4) {
       const int j = j0 + jj;
       if (j >= W1) break;
       float *dst = pyr + (((long)b * H + h) * W1 + j) * g.rs;
-      const float *row = tile[jj];
-      for (int lb = lane * 8; lb < cw; lb += 64 * 8) {
-        const int base = c0 + lb;
-        float v[8];
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (lb < cw) {
+        const float4 q = *reinterpret_cast<const float4 *>(tile + jj * PT_PITCH + (lb ^ swz(jj)));
+        v[0] = q.x;
+        v[1] = base + 1 < W2 ? q.y : 0.f;
+        v[2] = base + 2 < W2 ? q.z : 0.f;
+        v[3] = base + 3 < W2 ? q.w : 0.f;
+        if (base + 3 < W2) {
+          *reinterpret_cast<float4 *>(dst + base) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = (base + i < W2) ? row[lb + i] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (base + i < W2) dst[base + i] = v[i];
-        float l1[4], l2[2];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          l1[i] = (v[2 * i] + v[2 * i + 1]) * 0.5f;
-          const int k1 = base / 2 + i;
-          if (g.nlev > 1 && k1 < g.wid[1]) dst[g.off[1] + k1] = l1[i];
+          for (int i = 0; i < 4; ++i)
+            if (base + i < W2) dst[base + i] = v[i];
         }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          l2[i] = (l1[2 * i] + l1[2 * i + 1]) * 0.5f;
-          const int k2 = base / 4 + i;
-          if (g.nlev > 2 && k2 < g.wid[2]) dst[g.off[2] + k2] = l2[i];
-        }
-        const float l3 = (l2[0] + l2[1]) * 0.5f;
-        const int k3 = base / 8;
-        if (g.nlev > 3 && k3 < g.wid[3]) dst[g.off[3] + k3] = l3;
+      }
+      const float l1a = (v[0] + v[1]) * 0.5f, l1b = (v[2] + v[3]) * 0.5f;
+      const float l2 = (l1a + l1b) * 0.5f;
+      const float l3 = (l2 + __shfl_xor(l2, 1)) * 0.5f;
+      if (lb < cw) {
+        const int k1 = base / 2;
+        if (g.nlev > 1 && k1 < g.wid[1]) dst[g.off[1] + k1] = l1a;
+        if (g.nlev > 1 && k1 + 1 < g.wid[1]) dst[g.off[1] + k1 + 1] = l1b;
+        if (g.nlev > 2 && base / 4 < g.wid[2]) dst[g.off[2] + base / 4] = l2;
+        if (g.nlev > 3 && (lane & 1) == 0 && base / 8 < g.wid[3]) dst[g.off[3] + base / 8] = l3;
       }
     }
   }
@@ -526,6 +549,10 @@ extern "C" int sa_corr_pyramid_from_volume_strided(const float *volume, int B, i
   SA_REQUIRE(num_levels >= 1 && num_levels <= 4, "sa_corr_pyramid_from_volume_strided: num_levels must be 1..4");
   SA_REQUIRE(row_stride >= sa_pyramid_level_offset(W2, num_levels),
              "sa_corr_pyramid_from_volume_strided: row_stride too small");
+  SA_REQUIRE(row_stride % 4 == 0 && reinterpret_cast<uintptr_t>(pyramid) % 16 == 0,
+             "sa_corr_pyramid_from_volume_strided: pyramid rows must be 16-byte aligned");
+  SA_REQUIRE(W1 % 4 == 0 && sb % 4 == 0 && sh % 4 == 0 && sk % 4 == 0 && reinterpret_cast<uintptr_t>(volume) % 16 == 0,
+             "sa_corr_pyramid_from_volume_strided: needs W1 %% 4 == 0 and 16-byte aligned volume rows");
   Geo g = make_geo(1, 1, 1, W2, num_levels, row_stride);
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_MISC, s);

@@ -102,10 +102,13 @@ def corr_volume(fmap2: torch.Tensor, fmap3: torch.Tensor) -> torch.Tensor:
 
 def pyramid_from_volume(volume: torch.Tensor, num_levels: int = 4) -> torch.Tensor:
     """CorrBlock1D.__init__ on an existing volume [..., W2] (rows contiguous along W2), or on a
-    [B, 1, H, W1, W2] view whose W1 axis is the contiguous one (any W2)."""
+    [B, 1, H, W1, W2] view whose W1 axis is the contiguous one (any W2; needs W1 % 4 == 0 and
+    16-byte aligned rows, else the view is made contiguous first)."""
     _check(volume, "volume", contiguous=False)
     W2 = volume.shape[-1]
-    if volume.dim() == 5 and volume.shape[1] == 1 and volume.stride(-1) != 1 and volume.stride(3) == 1:
+    if (volume.dim() == 5 and volume.shape[1] == 1 and volume.stride(-1) != 1 and volume.stride(3) == 1
+            and volume.shape[3] % 4 == 0 and volume.data_ptr() % 16 == 0
+            and all(volume.stride(i) % 4 == 0 for i in (0, 2, 4))):
         # [B, 1, H, W1, W2] view of a [B, 1, W2, H, W1] volume: transposed while staging
         B, _, H, W1, _ = volume.shape
         rs = pyramid_geometry(W2, num_levels)[0]
@@ -114,6 +117,8 @@ def pyramid_from_volume(volume: torch.Tensor, num_levels: int = 4) -> torch.Tens
                volume.stride(2), volume.stride(4), num_levels, out.data_ptr(), rs, _stream(volume))
         return out
     rows2d = volume.reshape(-1, W2)
+    if rows2d.stride(1) != 1 and volume.dim() == 5:   # a strided view the kernel above cannot take
+        rows2d = volume.contiguous().reshape(-1, W2)
     if rows2d.stride(1) != 1:
         raise RuntimeError("volume rows must be contiguous along the last axis")
     rs = pyramid_geometry(W2, num_levels)[0]
