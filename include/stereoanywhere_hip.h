@@ -93,6 +93,15 @@ int sa_mono_masked_volume(const float *n2, const float *n3, const float *m2, con
                           int B, int H, int W1, int W2, int nbins, float gain, float *out,
                           void *stream);
 
+/* a2 + a3 without the volume — per-pixel records (n0, n1, n2, bin) of one view (normals of
+ * estimate_normals, utils.py:73-77; depth bin of generate_masks, utils.py:48-54, -1 = none):
+ *   normals [B,3,H,W], m [B,1,H,W] -> rec [B,H,W] float4 (16-byte aligned).  Masked-volume
+ *   cell (n, k, h, j) = gain * (nL[h,j] . nR[h,k]) / sqrt(3) iff binL[h,j] == binR[h,k] == n
+ *   (stereoanywhere.py:136, 161): what sa_conv3d_onehot / sa_conv3d_pointwise_upcat_onehot
+ *   evaluate in place of reading the [B, nbins, W2, H, W1] volume. */
+int sa_mono_bin_records(const float *normals, const float *m, int B, int H, int W, int nbins,
+                        float *rec, void *stream);
+
 /* a5 + a6 — estimate_left/right_disparity (utils.py:112-152) and
  * estimate_left/right_confidence (utils.py:154-170) on volumes given by strides
  * (element (b,h,j,k) at v[b*sb + h*sh + j*sj + k*sk]; sj == 1 or sk == 1).
@@ -216,6 +225,22 @@ int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_mean, const
                               int Dp, int Hp, int Wp, int B, int D, int H, int W, float slope,
                               const float *weight, int Cout, float *out, double *stats_partial,
                               void *stream);
+/* The hourglass's two readers of the masked mono volume (down_layers[0][0], hourglass.py:27-33;
+ * final_agg[0] over cat(orig, up(x)), hourglass.py:326-328) on the one-hot volume given by its
+ * records (sa_mono_bin_records; rec_l [B,H,W] of the left pixels = the volume's W axis, rec_r
+ * [B,H,D] of the right pixels = its D axis): each tap is one gather of W[bin][tap][:].
+ *   sa_conv3d_onehot: as sa_conv3d on the volume [B, nbins, D, H, W] with the identity
+ *     transform; built for nbins 8, stride 2, Cout 16; parts = sa_conv3d_onehot_stat_parts.
+ *   sa_conv3d_pointwise_upcat_onehot: as sa_conv3d_pointwise_upcat with a = that volume
+ *     (Ca = nbins = 8, Cout 8, identity transform); parts = sa_conv3d_upcat_stat_parts. */
+long sa_conv3d_onehot_stat_parts(int Do, int Ho, int Wo);
+int sa_conv3d_onehot(const float *rec_l, const float *rec_r, int B, int nbins, int D, int H, int W,
+                     int stride, float gain, const float *weight, int Cout, float *out,
+                     double *stats_partial, void *stream);
+int sa_conv3d_pointwise_upcat_onehot(const float *rec_l, const float *rec_r, int nbins, float gain,
+                                     const float *p, int Dp, int Hp, int Wp, int B, int D, int H,
+                                     int W, const float *weight, int Cout, float *out,
+                                     double *stats_partial, void *stream);
 /* out = T(in) elementwise on a [B,C,D,H,W] volume (T as for sa_conv3d). */
 int sa_vol_apply(const float *in, int B, int C, int D, int H, int W, const float *mean,
                  const float *rstd, int act, float slope, const float *gate_l, const float *gate_r,

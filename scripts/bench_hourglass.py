@@ -2,7 +2,7 @@
 """Per-layer timing of the fused mono hourglass at the bench shape (B=4, 544x960 ->
 volume [4, 8, 240, 136, 240]), random weights.  Each ops.* call of the fused path is
 bracketed by HIP events on the current stream.
-usage: python scripts/bench_hourglass.py [reps]   (SA_HIP_LIB=... selects a library build)"""
+usage: python scripts/bench_hourglass.py [reps] [--dense]   (SA_HIP_LIB=... selects a library build)"""
 import collections
 import os
 import sys
@@ -15,15 +15,22 @@ from stereoanywhere_amd.blocks import Hourglass  # noqa: E402
 
 
 def main():
-    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 5
     B, D, H, W = 4, 240, 136, 240
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     hg = Hourglass(8, 8).to(dev).eval()
     g = torch.Generator(device=dev).manual_seed(1)
-    ch = torch.randint(0, 9, (B, 1, D, H, W), device=dev, generator=g)
-    x = (torch.arange(8, device=dev)[None, :, None, None, None] == ch).float() * torch.randn(
-        (B, 1, D, H, W), device=dev, generator=g)
+    if "--dense" in sys.argv:   # the materialised one-hot-like volume (the round-1 input)
+        ch = torch.randint(0, 9, (B, 1, D, H, W), device=dev, generator=g)
+        x = (torch.arange(8, device=dev)[None, :, None, None, None] == ch).float() * torch.randn(
+            (B, 1, D, H, W), device=dev, generator=g)
+    else:   # the model's input: one-hot records of smooth mono maps
+        def mono(w):
+            m = torch.rand((B, 1, H // 8, w // 8), device=dev, generator=g)
+            return torch.nn.functional.interpolate(m, size=(H, w), mode="bilinear", align_corners=True).contiguous()
+        m2, m3 = mono(W), mono(D)
+        x = ops.OneHotVolume(ops.mono_normals(m2, W / 10), ops.mono_normals(m3, D / 10), m2, m3, 8, 1.73)
     fl = [torch.rand((B, 1, H >> i, W >> i), device=dev, generator=g) for i in range(4)]
     fr = [torch.rand((B, 1, H >> i, D >> i), device=dev, generator=g) for i in range(4)]
     wcls = torch.randn((2, 8, 3, 3, 3), device=dev, generator=g) * 0.2

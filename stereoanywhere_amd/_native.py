@@ -48,6 +48,7 @@ SIGNATURES = {
     "sa_corr_lookup_conv1x1": (I, [P, P, I, L, I, I, P, L, I, I, I, P, P, I, P, P]),
     "sa_mono_normals": (I, [P, I, I, I, F, P, P]),
     "sa_mono_masked_volume": (I, [P, P, P, P, I, I, I, I, I, F, P, P]),
+    "sa_mono_bin_records": (I, [P, P, I, I, I, I, P, P]),
     "sa_softargmin_conf": (I, [P, P, I, I, I, I, L, L, L, L, P, P, P, P, L, P]),
     "sa_softlrc": (I, [P, P, P, P, I, I, I, L, F, P, P, P]),
     "sa_weighted_lsq": (I, [P, P, P, I, I, F, F, P, P, P]),
@@ -84,6 +85,9 @@ SIGNATURES = {
     "sa_conv3d_pointwise": (I, [P, I, I, I, I, I, P, P, I, F, P, P, P, I, P, P]),
     "sa_conv3d_pointwise_upcat": (I, [P, I, P, P, I, P, P, P, I, I, I, I, I, I, I, F, P, I, P, P, P]),
     "sa_instnorm_finalize": (I, [P, I, L, L, F, P, P, P]),
+    "sa_conv3d_onehot_stat_parts": (L, [I, I, I]),
+    "sa_conv3d_onehot": (I, [P, P, I, I, I, I, I, I, F, P, I, P, P, P]),
+    "sa_conv3d_pointwise_upcat_onehot": (I, [P, P, I, F, P, I, I, I, I, I, I, I, P, I, P, P, P]),
     "sa_vol_apply": (I, [P, I, I, I, I, I, P, P, I, F, P, P, P, P]),
     "sa_conv2d_small": (I, [P, L, I, I, I, I, P, P, I, I, I, P, L, P]),
     "sa_timing_enable": (I, [I]),

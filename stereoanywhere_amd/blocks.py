@@ -234,7 +234,8 @@ class Hourglass(nn.Module):
             if g is None:
                 raise RuntimeError("fused hourglass: feature pyramid does not match the volume")
             return v.with_gate(g)
-        orig = ops.VolAct(masked)
+        # the masked volume by its one-hot records (ops.OneHotVolume) or materialised
+        orig = masked if isinstance(masked, ops.OneHotVolume) else ops.VolAct(masked)
         r = ops.conv3d(orig, fw["d00"], 16, stride=2, slope=slope)                  # down_layers[0][0]
         r = ops.conv3d(r, fw["d01"], 16, slope=slope)                               # down_layers[0][1]
         down0 = gated(r, self.feature_atts[0], 1)

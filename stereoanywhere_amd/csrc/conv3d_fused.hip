@@ -90,6 +90,119 @@ __device__ __forceinline__ void block_stats(const float (&s)[NC], const float (&
   }
 }
 
+// The masked mono volume (stereoanywhere.py:161, mono_volume.hip) is one-hot over its
+// nbins channels: cell (n, d, h, w) = 1.73 * (nL[h,w] . nR[h,d]) / sqrt(3) if the left pixel
+// (h, w) and the right pixel (h, d) are both in depth bin n, else 0.  Its two consumers
+// evaluate the cells from per-pixel records (n0, n1, n2, bin) (sa_mono_bin_records) instead of
+// reading 8 channels of which 7 are zero: a tap costs one weight-row gather W[bin][tap][:].
+struct OneHotVol {
+  const float4 *recL;   // [B, H, W]: left pixels (the volume's W axis = W1)
+  const float4 *recR;   // [B, H, D]: right pixels (its D axis = W2)
+  float gain;
+};
+
+// the masked_volume_kernel's value, same operation order, no contraction; bin -1 (none) or a
+// padding sentinel never matches
+__device__ __forceinline__ float onehot_cell(const float4 l, const float4 r, float gain, int &bin) {
+#pragma clang fp contract(off)
+  const float v = gain * ((l.x * r.x + l.y * r.y + l.z * r.z) / sqrtf(3.0f));
+  const bool m = l.w == r.w && l.w >= 0.0f;
+  bin = m ? (int)l.w : 0;
+  return m ? v : 0.0f;
+}
+
+// Stride-2 3x3x3 conv (pad 1, no bias) of the one-hot volume (down_layers[0][0],
+// hourglass.py:27-33 / submodule.py:25-53): out[co] = sum over taps of W[bin][tap][co] * cell.
+// Thread = one (w, h) output column x TDx output planes along D; block 64 (w) x 4 (h).  The
+// taps' records come from L1/L2 (the left record of (h, w) serves every d, the right records
+// of (h, d) every w); weight rows in LDS at a pitch that puts the 8 bins' 16-byte reads on
+// disjoint banks.
+template <int COUT, int TDx>
+__global__ __launch_bounds__(256) void conv3d_onehot_s2_kernel(OneHotVol v, int nbins, int D, int H, int W, int Do,
+                                                               int Ho, int Wo, const float *__restrict__ wt,
+                                                               float *__restrict__ out, double *__restrict__ partial,
+                                                               int tilesD) {
+  constexpr int WP = 27 * COUT + 4;   // weight row pitch: (WP / 4) odd -> 8 rows on disjoint 16-byte banks
+  static_assert(COUT % 4 == 0 && (WP / 4) % 2 == 1, "weight pitch");
+  __shared__ __attribute__((aligned(16))) float ws[8 * WP];
+  __shared__ double red[COUT * 4 * 2];
+  for (int i = threadIdx.x; i < nbins * 27 * COUT; i += 256) {
+    const int n = i / (27 * COUT), r = i - n * 27 * COUT;
+    ws[n * WP + r] = wt[i];
+  }
+  __syncthreads();
+  const int tx_ = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int wo = blockIdx.x * 64 + tx_, ho = blockIdx.y * 4 + ty;
+  const int b = blockIdx.z / tilesD, d0 = (blockIdx.z % tilesD) * TDx;
+  const bool ok = wo < Wo && ho < Ho;
+  const int woc = min(wo, Wo - 1), hoc = min(ho, Ho - 1);
+  const float4 *rl = v.recL + (long)b * H * W, *rr = v.recR + (long)b * H * D;
+  const float4 pad_l = make_float4(0.f, 0.f, 0.f, -3.f), pad_r = make_float4(0.f, 0.f, 0.f, -2.f);
+  float acc[TDx][COUT];
+#pragma unroll
+  for (int i = 0; i < TDx; ++i)
+#pragma unroll
+    for (int c = 0; c < COUT; ++c) acc[i][c] = 0.f;
+  constexpr int ND = 2 * TDx + 1;   // input planes of the thread's outputs
+#pragma unroll 1
+  for (int kh = 0; kh < 3; ++kh) {
+    const int h = 2 * hoc - 1 + kh;
+    const bool hok = h >= 0 && h < H;
+    float4 r[ND];
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      const int d = 2 * d0 - 1 + i;
+      r[i] = (hok && d >= 0 && d < D) ? rr[(long)h * D + d] : pad_r;
+    }
+#pragma unroll 1
+    for (int kw = 0; kw < 3; ++kw) {
+      const int w = 2 * woc - 1 + kw;
+      const float4 l = (hok && w >= 0 && w < W) ? rl[(long)h * W + w] : pad_l;
+      float cv[ND];
+      int cb[ND];
+#pragma unroll
+      for (int i = 0; i < ND; ++i) cv[i] = onehot_cell(l, r[i], v.gain, cb[i]);
+#pragma unroll
+      for (int od = 0; od < TDx; ++od)
+#pragma unroll
+        for (int kd = 0; kd < 3; ++kd) {
+          const int i = 2 * od + kd;
+          const float4 *wp = reinterpret_cast<const float4 *>(ws + cb[i] * WP + ((kd * 3 + kh) * 3 + kw) * COUT);
+#pragma unroll
+          for (int g = 0; g < COUT / 4; ++g) {
+            const float4 w4 = wp[g];
+            acc[od][4 * g + 0] += w4.x * cv[i];
+            acc[od][4 * g + 1] += w4.y * cv[i];
+            acc[od][4 * g + 2] += w4.z * cv[i];
+            acc[od][4 * g + 3] += w4.w * cv[i];
+          }
+        }
+    }
+  }
+  float s[COUT], q[COUT];
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) s[c] = q[c] = 0.0f;
+  if (ok) {
+#pragma unroll
+    for (int od = 0; od < TDx; ++od) {
+      const int d = d0 + od;
+      if (d < Do) {
+#pragma unroll
+        for (int co = 0; co < COUT; ++co) {
+          out[(((long)b * COUT + co) * Do + d) * (long)Ho * Wo + (long)ho * Wo + wo] = acc[od][co];
+          s[co] += acc[od][co];
+          q[co] += acc[od][co] * acc[od][co];
+        }
+      }
+    }
+  }
+  if (partial) {
+    const int nparts = gridDim.x * gridDim.y * tilesD;
+    const int blk = (blockIdx.z % tilesD) * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x;
+    block_stats<COUT>(s, q, red, partial, b, nparts, blk, COUT);
+  }
+}
+
 template <int S, int TWx>
 struct ConvTile {
   static constexpr int valid_w = TWx - (S == 1 ? 2 : 1);  // output columns per tile
@@ -270,8 +383,10 @@ __global__ __launch_bounds__(256) void pointwise_kernel(const float *__restrict_
 // (pointwise_kernel).  The block's low-resolution footprint of p (at most 4 x 4 x 34
 // voxels for an upsampling factor >= 2) is staged in LDS as [d][h][w][co], so each
 // voxel's 8 trilinear corners are COUT/4 float4 reads apiece.
-template <int CA, int COUT, bool AX>
-__global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__restrict__ a, InXform ta,
+// OH: a is the one-hot mono volume given by its records (OneHotVol): Wa . a = Wa[bin] * cell,
+// one weight-row gather per voxel instead of CA products.
+template <int CA, int COUT, bool AX, bool OH = false>
+__global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__restrict__ a, InXform ta, OneHotVol oh,
                                                               const float *__restrict__ pu, int D, int H, int W,
                                                               int Du, int Hu, int Wu, float sd, float sh, float sw,
                                                               const float *__restrict__ wt, float *__restrict__ out,
@@ -281,6 +396,9 @@ __global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__res
   static_assert(COUT % 4 == 0, "float4 corners");
   __shared__ float4 pt[ED * EH * EW * (COUT / 4)];
   __shared__ double red[COUT * 4 * 2];
+  __shared__ float4 wa[OH ? CA * COUT / 4 : 1];
+  if (OH)
+    for (int i = threadIdx.x; i < CA * COUT; i += 256) reinterpret_cast<float *>(wa)[i] = wt[i];
   const int tx_ = threadIdx.x & 63;
   const int ty = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // one H row per wave
   const int w0 = blockIdx.x * TWV, h0 = blockIdx.y * TH;
@@ -312,8 +430,27 @@ __global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__res
 #pragma unroll
     for (int co = 0; co < COUT; ++co) r[od][co] = 0.0f;
   const long pos0 = ((long)min(d0, D - 1) * H + hc) * W + wc;
+  if constexpr (OH) {
+    // the sum over the CA channels has one non-zero term: r = Wa[bin] * cell (as the dense sum
+    // gives it: zero products add nothing)
+    const float4 l = oh.recL[((long)b * H + hc) * W + wc];
+    const float4 *rr = oh.recR + ((long)b * H + hc) * D;
+#pragma unroll
+    for (int od = 0; od < TD; ++od) {
+      int bin;
+      const float cv = onehot_cell(l, rr[min(d0 + od, D - 1)], oh.gain, bin);
+#pragma unroll
+      for (int g = 0; g < COUT / 4; ++g) {
+        const float4 w4 = wa[bin * (COUT / 4) + g];
+        r[od][4 * g + 0] += w4.x * cv;
+        r[od][4 * g + 1] += w4.y * cv;
+        r[od][4 * g + 2] += w4.z * cv;
+        r[od][4 * g + 3] += w4.w * cv;
+      }
+    }
+  }
 #pragma unroll 2
-  for (int c = 0; c < CA; ++c) {
+  for (int c = 0; c < (OH ? 0 : CA); ++c) {
     const long bc = (long)b * CA + c;
     const float *ap = a + bc * vol + pos0;
     float av[TD];
@@ -545,8 +682,8 @@ extern "C" int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_
   sa::TimingScope ts(SA_K_CONV3D, s);
 #define SA_PW(CA, CO, AXV)                                                                                    \
   if (Ca == CA && Cout == CO && ax == AXV) {                                                                 \
-    pointwise_upcat_kernel<CA, CO, AXV><<<grid, 256, 0, s>>>(a, ta, p, D, H, W, Dp, Hp, Wp, sd, sh, sw, weight, \
-                                                             out, stats_partial, tilesD);                    \
+    pointwise_upcat_kernel<CA, CO, AXV><<<grid, 256, 0, s>>>(a, ta, OneHotVol{}, p, D, H, W, Dp, Hp, Wp, sd, sh, \
+                                                             sw, weight, out, stats_partial, tilesD);        \
     return sa::check_launch("sa_conv3d_pointwise_upcat");                                                    \
   }
   SA_PW(8, 8, false)
@@ -554,6 +691,55 @@ extern "C" int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_
 #undef SA_PW
   sa::set_error("sa_conv3d_pointwise_upcat: no kernel built for %d -> %d (a transform %d)", Ca, Cout, ax);
   return SA_E_ARG;
+}
+
+extern "C" long sa_conv3d_onehot_stat_parts(int Do, int Ho, int Wo) {
+  return (long)((Wo + 63) / 64) * ((Ho + 3) / 4) * ((Do + 1) / 2);
+}
+
+extern "C" int sa_conv3d_onehot(const float *rec_l, const float *rec_r, int B, int nbins, int D, int H, int W,
+                                int stride, float gain, const float *weight, int Cout, float *out,
+                                double *stats_partial, void *stream) {
+  SA_REQUIRE(rec_l && rec_r && weight && out, "sa_conv3d_onehot: null pointer");
+  SA_REQUIRE(B > 0 && D > 0 && H > 0 && W > 0, "sa_conv3d_onehot: empty shape");
+  SA_REQUIRE(((uintptr_t)rec_l & 15) == 0 && ((uintptr_t)rec_r & 15) == 0, "sa_conv3d_onehot: records need 16-byte alignment");
+  SA_REQUIRE(nbins == 8 && stride == 2 && Cout == 16,
+             "sa_conv3d_onehot: built for 8 bins, stride 2, 16 outputs (got %d, %d, %d)", nbins, stride, Cout);
+  SA_REQUIRE((long)D * H * W < (1L << 31), "sa_conv3d_onehot: a channel plane must hold < 2^31 voxels");
+  const int Do = out_size(D, 2), Ho = out_size(H, 2), Wo = out_size(W, 2);
+  const int tilesD = (Do + 1) / 2;
+  const dim3 grid((Wo + 63) / 64, (Ho + 3) / 4, tilesD * B);
+  SA_REQUIRE((long)grid.x * grid.y * tilesD == sa_conv3d_onehot_stat_parts(Do, Ho, Wo), "sa_conv3d_onehot: parts");
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_CONV3D, s);
+  OneHotVol v{reinterpret_cast<const float4 *>(rec_l), reinterpret_cast<const float4 *>(rec_r), gain};
+  conv3d_onehot_s2_kernel<16, 2><<<grid, 256, 0, s>>>(v, nbins, D, H, W, Do, Ho, Wo, weight, out, stats_partial,
+                                                      tilesD);
+  return sa::check_launch("sa_conv3d_onehot");
+}
+
+extern "C" int sa_conv3d_pointwise_upcat_onehot(const float *rec_l, const float *rec_r, int nbins, float gain,
+                                                const float *p, int Dp, int Hp, int Wp, int B, int D, int H, int W,
+                                                const float *weight, int Cout, float *out, double *stats_partial,
+                                                void *stream) {
+  SA_REQUIRE(rec_l && rec_r && p && weight && out && stats_partial, "sa_conv3d_pointwise_upcat_onehot: null pointer");
+  SA_REQUIRE(((uintptr_t)rec_l & 15) == 0 && ((uintptr_t)rec_r & 15) == 0,
+             "sa_conv3d_pointwise_upcat_onehot: records need 16-byte alignment");
+  SA_REQUIRE(B > 0 && D > 1 && H > 1 && W > 1 && Dp > 0 && Hp > 0 && Wp > 0,
+             "sa_conv3d_pointwise_upcat_onehot: bad shape");
+  SA_REQUIRE(2 * (Dp - 1) <= D - 1 && 2 * (Hp - 1) <= H - 1 && 2 * (Wp - 1) <= W - 1,
+             "sa_conv3d_pointwise_upcat_onehot: the low-resolution branch must be at most half size");
+  SA_REQUIRE(nbins == 8 && Cout == 8, "sa_conv3d_pointwise_upcat_onehot: built for 8 bins -> 8 outputs");
+  int tilesD;
+  dim3 grid = upcat_grid(B, D, H, W, tilesD);
+  const float sd = (float)(Dp - 1) / (float)(D - 1), sh = (float)(Hp - 1) / (float)(H - 1),
+              sw = (float)(Wp - 1) / (float)(W - 1);
+  OneHotVol v{reinterpret_cast<const float4 *>(rec_l), reinterpret_cast<const float4 *>(rec_r), gain};
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_CONV3D, s);
+  pointwise_upcat_kernel<8, 8, false, true><<<grid, 256, 0, s>>>(nullptr, InXform{}, v, p, D, H, W, Dp, Hp, Wp, sd,
+                                                                  sh, sw, weight, out, stats_partial, tilesD);
+  return sa::check_launch("sa_conv3d_pointwise_upcat_onehot");
 }
 
 extern "C" int sa_vol_apply(const float *in, int B, int C, int D, int H, int W, const float *mean, const float *rstd,

@@ -10,6 +10,9 @@
 // (hourglass.py:63).  The reference materialises [B,8,H,W1,W2] and then a permuted
 // copy; here each output cell is computed once and written once (7 of 8 channels are
 // zero because a pixel pair shares at most one bin).  Write-bound: 4·nbins bytes/cell.
+// The fused hourglass does not read this volume: its two consumers (the stride-2 conv and
+// the final up-cat conv, conv3d_fused.hip) evaluate the one-hot cells from per-pixel
+// records (sa_mono_bin_records); the volume remains for the unfused (torch) hourglass.
 #include "sa_common.h"
 
 namespace {
@@ -103,7 +106,32 @@ __global__ __launch_bounds__(256) void masked_volume_kernel(
   }
 }
 
+// per-pixel record (n0, n1, n2, bin) of one view: the mono volume's one-hot structure
+// without the volume (the hourglass's first convs evaluate cell (n, k, h, j) from the two
+// records: value at channel n = bin iff both pixels are in bin n, else 0)
+__global__ __launch_bounds__(256) void bin_records_kernel(const float *__restrict__ nrm, const float *__restrict__ m,
+                                                          int hw, int nbins, long npix, float4 *__restrict__ rec) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+  const long b = p / hw, q = p - b * hw;
+  const float *n = nrm + b * 3 * hw + q;
+  rec[p] = make_float4(n[0], n[hw], n[2 * hw], (float)depth_bin(m[p], nbins));
+}
+
 }  // namespace
+
+extern "C" int sa_mono_bin_records(const float *normals, const float *m, int B, int H, int W, int nbins,
+                                   float *rec, void *stream) {
+  SA_REQUIRE(normals && m && rec, "sa_mono_bin_records: null pointer");
+  SA_REQUIRE(B > 0 && H > 0 && W > 0 && nbins > 0 && nbins <= 64, "sa_mono_bin_records: bad shape");
+  SA_REQUIRE(((uintptr_t)rec & 15) == 0, "sa_mono_bin_records: records need 16-byte alignment");
+  const long npix = (long)B * H * W;
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_MISC, s);
+  bin_records_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, s>>>(normals, m, H * W, nbins, npix,
+                                                                     reinterpret_cast<float4 *>(rec));
+  return sa::check_launch("sa_mono_bin_records");
+}
 
 extern "C" int sa_mono_normals(const float *mde, int B, int H, int W, float gain, float *normals,
                                void *stream) {

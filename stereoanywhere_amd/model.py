@@ -9,7 +9,7 @@ Drop-in for models/stereoanywhere/stereoanywhere.py:
   * identical parameter names (state dicts of the reference load with strict=True).
 
 Hot path, one kernel family per row:
-  a2+a3  normals + masked mono volume, written in the hourglass layout   sa_mono_*
+  a2+a3  normals + one-hot mono volume records (read by the fused hourglass)  sa_mono_*
   a5+a6  soft-argmin and entropy confidence of the aggregated volumes    sa_softargmin_conf
   a7     softLRC, weighted LSQ (exact quantile band, no host sync)       sa_softlrc, sa_weighted_lsq
   a8+a11 scaled mono, mirror detector, initial coordinates               sa_mono_scale_mirror
@@ -326,14 +326,17 @@ class StereoAnywhere(nn.Module):
                    for i in range(a.n_downsample, len(self.feature_channels))]
 
         # ---- mono cost volume -> 3-D hourglass -> classifiers (native [B,C,W2,H,W1] layout)
-        masked = ops.mono_masked_volume(n2, n3, m2l, m3l, a.vol_n_masks, 1.73)
+        # the fused hourglass reads the one-hot masked volume through per-pixel records (its two
+        # readers evaluate the cells); the torch path materialises it
+        masked = ops.OneHotVolume(n2, n3, m2l, m3l, a.vol_n_masks, 1.73)
         # stack[i] for i < n_additional (stereoanywhere.py:163-164): stack[0] is the identity,
         # so only n_additional >= 2 puts a real hourglass after hourglass_mono
         extra = [self.hourglass_mono_stack[i] for i in range(a.n_additional_hourglass)
                  if not isinstance(self.hourglass_mono_stack[i], HourglassIdentity)]
-        if not extra and self.hourglass_mono.fusable(masked, feats_l):
+        if not extra and a.vol_n_masks == 8 and self.hourglass_mono.fusable(masked, feats_l):
             vol_d, vol_c = self.hourglass_mono(masked, feats_l, feats_r, fused=dw["hg"])
         else:
+            masked = ops.mono_masked_volume(n2, n3, m2l, m3l, a.vol_n_masks, 1.73)
             agg = self.hourglass_mono(masked, feats_l, feats_r)
             for hg in extra:
                 agg = hg(agg, feats_l, feats_r)

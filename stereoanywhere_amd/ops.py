@@ -203,6 +203,30 @@ def mono_masked_volume(n2, n3, m2, m3, nbins: int = 8, gain: float = 1.73) -> to
     return out
 
 
+def mono_bin_records(normals: torch.Tensor, m: torch.Tensor, nbins: int = 8) -> torch.Tensor:
+    """-> [B, H, W, 4] records (n0, n1, n2, depth bin or -1) of one view (sa_mono_bin_records)."""
+    _check(normals, "normals")
+    _check(m, "m")
+    B, _, H, W = normals.shape
+    rec = torch.empty((B, H, W, 4), device=normals.device, dtype=torch.float32)
+    N.call("sa_mono_bin_records", normals.data_ptr(), m.data_ptr(), B, H, W, nbins, rec.data_ptr(), _stream(rec))
+    return rec
+
+
+class OneHotVolume:
+    """The masked mono volume [B, nbins, W2, H, W1] (stereoanywhere.py:161) by its per-pixel
+    records: cell (n, k, h, j) = gain * nL[h,j] . nR[h,k] / sqrt(3) iff both pixels are in bin n.
+    The fused hourglass's readers of the volume (ops.conv3d at stride 2, ops.conv3d_pointwise_upcat)
+    evaluate the cells from the records; nothing of the volume is written."""
+
+    def __init__(self, n2, n3, m2, m3, nbins: int = 8, gain: float = 1.73):
+        self.rec_l, self.rec_r = mono_bin_records(n2, m2, nbins), mono_bin_records(n3, m3, nbins)
+        self.nbins, self.gain = nbins, gain
+        B, _, H, W1 = n2.shape
+        self.shape = torch.Size((B, nbins, n3.shape[3], H, W1))
+        self.device = n2.device
+
+
 # ----------------------------------------------------------------------- a5 + a6
 def softargmin_conf(vol_disp: Optional[torch.Tensor], vol_conf: Optional[torch.Tensor], strides, dims,
                     out_disp: Optional[torch.Tensor] = None, out_conf: Optional[torch.Tensor] = None):
@@ -398,6 +422,8 @@ def vol_apply(x: "VolAct", slope: float = 0.01) -> "VolAct":
 def conv3d(x: "VolAct", w_t: torch.Tensor, cout: int, stride: int = 1, slope: float = 0.01, stats: bool = True):
     """3x3x3 conv (pad 1, no bias) of T(x.raw); w_t pre-arranged [Cin][27][Cout].
     Returns VolAct(out, InstanceNorm stats of out if requested, act=True)."""
+    if isinstance(x, OneHotVolume):
+        return _conv3d_onehot(x, w_t, cout, stride, stats)
     _check(x.raw, "x")
     _check(w_t, "w_t")
     B, Cin, D, H, W = x.raw.shape
@@ -408,6 +434,19 @@ def conv3d(x: "VolAct", w_t: torch.Tensor, cout: int, stride: int = 1, slope: fl
     a = x.args()
     N.call("sa_conv3d", x.raw.data_ptr(), B, Cin, D, H, W, stride, w_t.data_ptr(), cout, a[0], a[1], a[2], slope,
            a[3], a[4], out.data_ptr(), _ptr(partial), _stream(out))
+    norm = instnorm_finalize(partial, B * cout, parts, Do * Ho * Wo) if stats else None
+    return VolAct(out, norm, act=stats)
+
+
+def _conv3d_onehot(x: OneHotVolume, w_t: torch.Tensor, cout: int, stride: int, stats: bool):
+    _check(w_t, "w_t")
+    B, nb, D, H, W = x.shape
+    Do, Ho, Wo = (D - 1) // stride + 1, (H - 1) // stride + 1, (W - 1) // stride + 1
+    out = torch.empty((B, cout, Do, Ho, Wo), device=x.device, dtype=torch.float32)
+    parts = int(N.lib().sa_conv3d_onehot_stat_parts(Do, Ho, Wo))
+    partial = torch.empty((B * cout * parts * 2,), device=out.device, dtype=torch.float64) if stats else None
+    N.call("sa_conv3d_onehot", x.rec_l.data_ptr(), x.rec_r.data_ptr(), B, nb, D, H, W, stride, x.gain,
+           w_t.data_ptr(), cout, out.data_ptr(), _ptr(partial), _stream(out))
     norm = instnorm_finalize(partial, B * cout, parts, Do * Ho * Wo) if stats else None
     return VolAct(out, norm, act=stats)
 
@@ -428,6 +467,17 @@ def conv3d_pointwise_upcat(a: "VolAct", u: "VolAct", w_a: torch.Tensor, w_u: tor
                            slope: float = 0.01) -> "VolAct":
     """1x1x1 conv over cat(T(a), trilinear_up(T(u))) -> VolAct(out, IN stats, act=True), as
     Wa.T(a) + up(Wu.T(u)) (two launches); w_a [Ca][Cout], w_u [Cu][Cout]."""
+    if isinstance(a, OneHotVolume):
+        p = conv3d_pointwise(u, w_u, cout, slope)
+        B, _, D, H, W = a.shape
+        _, _, Dp, Hp, Wp = p.shape
+        out = torch.empty((B, cout, D, H, W), device=p.device, dtype=torch.float32)
+        parts = int(N.lib().sa_conv3d_upcat_stat_parts(D, H, W))
+        partial = torch.empty((B * cout * parts * 2,), device=out.device, dtype=torch.float64)
+        N.call("sa_conv3d_pointwise_upcat_onehot", a.rec_l.data_ptr(), a.rec_r.data_ptr(), a.nbins, a.gain,
+               p.data_ptr(), Dp, Hp, Wp, B, D, H, W, w_a.data_ptr(), cout, out.data_ptr(), partial.data_ptr(),
+               _stream(out))
+        return VolAct(out, instnorm_finalize(partial, B * cout, parts, D * H * W), act=True)
     _check(a.raw, "a")
     p = conv3d_pointwise(u, w_u, cout, slope)
     B, Ca, D, H, W = a.raw.shape

@@ -406,3 +406,68 @@ def test_corr_block_contract_five_levels_and_sampler_shim(micro):
         lvl = blk.corr_pyramid[i].reshape(B, H, W1, -1)
         taps = CorrSampler.apply(lvl, coords[:, :1] / 2 ** i, 4)
         np.testing.assert_allclose(c(taps), micro["lookup.out"][:, 9 * i:9 * i + 9], atol=1e-5)
+
+
+def _onehot_case(B, H, W1, W2, seed):
+    """normals + depth maps with every edge case of the bins (mde == 1.0 in no bin, exact edges)."""
+    rng = np.random.default_rng(seed)
+    # three bins only, so that many pixel pairs match (m3 on the exact bin edges)
+    m2 = (np.floor(rng.random((B, 1, H, W1)) * 3) / 8 + 0.03).astype(np.float32)
+    m3 = (np.floor(rng.random((B, 1, H, W2)) * 3) / 8).astype(np.float32)
+    m2[0, 0, 0, :4] = [1.0, 0.0, 0.5, 0.375]
+    m3[0, 0, 1, :4] = [1.0, 0.125, 0.5, 0.999]
+    n2 = ops.mono_normals(g(m2), 2.0)
+    n3 = ops.mono_normals(g(m3), 2.0)
+    return n2, n3, g(m2), g(m3)
+
+
+@pytest.mark.parametrize("B,H,W1,W2", [(2, 16, 44, 36), (1, 12, 140, 132)])
+def test_onehot_hourglass_readers_match_dense(B, H, W1, W2):
+    """The hourglass's two readers of the masked mono volume on its one-hot records
+    (sa_conv3d_onehot, sa_conv3d_pointwise_upcat_onehot) against the same convs on the
+    materialised volume (sa_mono_masked_volume): outputs and InstanceNorm statistics."""
+    n2, n3, m2, m3 = _onehot_case(B, H, W1, W2, 5 + W1)
+    oh = ops.OneHotVolume(n2, n3, m2, m3, 8, 1.73)
+    dense = ops.mono_masked_volume(n2, n3, m2, m3, 8, 1.73)
+    assert tuple(oh.shape) == tuple(dense.shape)
+    assert int((dense != 0).sum()) > dense.numel() // 40   # the case exercises real matches
+    rng = np.random.default_rng(3)
+    w = g(rng.standard_normal((8, 27, 16)) * 0.2)
+    a = ops.conv3d(oh, w, 16, stride=2)
+    b = ops.conv3d(ops.VolAct(dense), w, 16, stride=2)
+    torch.testing.assert_close(a.raw, b.raw, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(a.norm[0], b.norm[0], atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(a.norm[1], b.norm[1], atol=1e-6, rtol=1e-5)
+    # final_agg[0]: 1x1x1 over cat(orig, up(x)) with x at half resolution
+    u = ops.VolAct(g(rng.standard_normal((B, 16, (W2 - 1) // 2 + 1, (H - 1) // 2 + 1, (W1 - 1) // 2 + 1))))
+    wa = g(rng.standard_normal((8, 8)) * 0.3)
+    wu = g(rng.standard_normal((16, 8)) * 0.3)
+    a = ops.conv3d_pointwise_upcat(oh, u, wa, wu, 8)
+    b = ops.conv3d_pointwise_upcat(ops.VolAct(dense), u, wa, wu, 8)
+    # one non-zero term per voxel: the same products (the trilinear term's FMA contraction may
+    # differ between the two kernels by an ulp)
+    torch.testing.assert_close(a.raw, b.raw, atol=1e-6, rtol=1e-6)
+    torch.testing.assert_close(a.norm[0], b.norm[0], atol=1e-6, rtol=1e-6)
+    torch.testing.assert_close(a.norm[1], b.norm[1], atol=1e-6, rtol=1e-6)
+
+
+def test_fused_hourglass_on_onehot_records_matches_torch():
+    """The fused hourglass fed the one-hot records (the model's path) against the torch
+    hourglass on the materialised masked volume."""
+    from stereoanywhere_amd.blocks import Hourglass
+    B, D, H, W = 2, 32, 16, 40
+    n2, n3, m2, m3 = _onehot_case(B, H, W, D, 9)
+    torch.manual_seed(0)
+    hg = Hourglass(8, 8).to(dev).eval()
+    rng = np.random.default_rng(4)
+    fl = [g(rng.random((B, 1, H >> i, W >> i))) for i in range(4)]
+    fr = [g(rng.random((B, 1, H >> i, D >> i))) for i in range(4)]
+    wcls = g(rng.standard_normal((2, 8, 3, 3, 3)) * 0.2)
+    oh = ops.OneHotVolume(n2, n3, m2, m3, 8, 1.73)
+    dense = ops.mono_masked_volume(n2, n3, m2, m3, 8, 1.73)
+    with torch.no_grad():
+        assert hg.fusable(oh, fl)
+        vd, vc = hg(oh, fl, fr, fused=hg.fused_weights(wcls))
+        ref = torch.nn.functional.conv3d(hg(dense, fl, fr), wcls, padding=1)
+    torch.testing.assert_close(vd, ref[:, 0:1], atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(vc, ref[:, 1:2], atol=1e-4, rtol=1e-4)
