@@ -225,6 +225,15 @@ int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_mean, const
                               int Dp, int Hp, int Wp, int B, int D, int H, int W, float slope,
                               const float *weight, int Cout, float *out, double *stats_partial,
                               void *stream);
+/* sa_conv3d at stride 1 for Cin 8 -> Cout 8 or 2 (final_agg[1], final_agg[2], the classifier
+ * pair) with the D-taps as Winograd F(4,3) along D: weight_wd [Cin][3 kh][3 kw][6][Cout] =
+ * G (points 0, +-1, +-2, inf) applied to the kernel's D-taps (ops.conv3d_wd_weights).  The
+ * input's transform must include the InstanceNorm + LeakyReLU (in_mean, act); statistics as for
+ * sa_conv3d with parts = sa_conv3d_stat_parts(Cout, 1, D, H, W). */
+int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W, const float *weight_wd,
+                 int Cout, const float *in_mean, const float *in_rstd, int act, float slope,
+                 const float *gate_l, const float *gate_r, float *out, double *stats_partial,
+                 void *stream);
 /* The hourglass's two readers of the masked mono volume (down_layers[0][0], hourglass.py:27-33;
  * final_agg[0] over cat(orig, up(x)), hourglass.py:326-328) on the one-hot volume given by its
  * records (sa_mono_bin_records; rec_l [B,H,W] of the left pixels = the volume's W axis, rec_r

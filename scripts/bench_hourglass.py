@@ -47,7 +47,7 @@ def main():
             rec.append((f"{name} {shape} -> {a[2] if name == 'conv3d' else ''}", e0, e1))
             return r
         return f
-    for n in ("conv3d", "conv3d_pointwise", "conv3d_pointwise_upcat"):
+    for n in ("conv3d", "conv3d_wd", "conv3d_pointwise", "conv3d_pointwise_upcat"):
         setattr(ops, n, wrap(n, getattr(ops, n)))
     with torch.no_grad():
         hg(x, fl, fr, fused=fw)

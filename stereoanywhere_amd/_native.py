@@ -85,6 +85,7 @@ SIGNATURES = {
     "sa_conv3d_pointwise": (I, [P, I, I, I, I, I, P, P, I, F, P, P, P, I, P, P]),
     "sa_conv3d_pointwise_upcat": (I, [P, I, P, P, I, P, P, P, I, I, I, I, I, I, I, F, P, I, P, P, P]),
     "sa_instnorm_finalize": (I, [P, I, L, L, F, P, P, P]),
+    "sa_conv3d_wd": (I, [P, I, I, I, I, I, P, I, P, P, I, F, P, P, P, P, P]),
     "sa_conv3d_onehot_stat_parts": (L, [I, I, I]),
     "sa_conv3d_onehot": (I, [P, P, I, I, I, I, I, I, F, P, I, P, P, P]),
     "sa_conv3d_pointwise_upcat_onehot": (I, [P, P, I, F, P, I, I, I, I, I, I, I, P, I, P, P, P]),

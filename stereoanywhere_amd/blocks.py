@@ -248,15 +248,17 @@ class Hourglass(nn.Module):
         r = ops.conv3d(r, fw["a12"], 16, slope=slope)                               # agg_layers[1][2]
         x = gated(r, self.feature_atts_up[1], 1)
         r = ops.conv3d_pointwise_upcat(orig, x, *fw["fa0"], 8, slope=slope)         # final_agg[0]
-        r = ops.conv3d(r, fw["fa1"], 8, slope=slope)                                # final_agg[1]
-        r = ops.conv3d(r, fw["fa2"], 8, slope=slope)                                # final_agg[2]
+        # full-resolution 8-channel convs: F(4,3) Winograd along D (6 products per 4 outputs)
+        r = ops.conv3d_wd(r, fw["fa1_wd"], 8, slope=slope)                          # final_agg[1]
+        r = ops.conv3d_wd(r, fw["fa2_wd"], 8, slope=slope)                          # final_agg[2]
         r = gated(r, self.final_feature_atts_up, 0)
-        vol = ops.conv3d(r, fw["cls"], 2, slope=slope, stats=False).raw             # both classifiers
+        vol = ops.conv3d_wd(r, fw["cls_wd"], 2, slope=slope, stats=False).raw       # both classifiers
         return vol[:, 0:1], vol[:, 1:2]
 
     def fused_weights(self, classifiers):
         """[ci][27][co] / [cin][co] arrangements of every conv used by _forward_fused;
         ``classifiers``: [2, 8, 3, 3, 3] kernels already in the (W2, H, W1) layout."""
+        from . import ops
         def k3(w):
             return w.reshape(w.shape[0], w.shape[1], 27).permute(1, 2, 0).contiguous()
 
@@ -265,13 +267,15 @@ class Hourglass(nn.Module):
             return w[:, a_cols].t().contiguous(), w[:, u_cols].t().contiguous()
         a10 = self.agg_layers[1][0].conv.weight  # input cat(up(down1) [32], down0 [16])
         fa0 = self.final_agg[0].conv.weight      # input cat(orig [8], up(x) [16])
+        fa1, fa2, cls = k3(self.final_agg[1].conv.weight), k3(self.final_agg[2].conv.weight), k3(classifiers)
         return dict(
+            fa1_wd=ops.conv3d_wd_weights(fa1), fa2_wd=ops.conv3d_wd_weights(fa2), cls_wd=ops.conv3d_wd_weights(cls),
             d00=k3(self.down_layers[0][0].conv.weight), d01=k3(self.down_layers[0][1].conv.weight),
             d10=k3(self.down_layers[1][0].conv.weight), d11=k3(self.down_layers[1][1].conv.weight),
             a10=pw(a10, slice(32, 48), slice(0, 32)),
             a11=k3(self.agg_layers[1][1].conv.weight), a12=k3(self.agg_layers[1][2].conv.weight),
             fa0=pw(fa0, slice(0, 8), slice(8, 24)),
-            fa1=k3(self.final_agg[1].conv.weight), fa2=k3(self.final_agg[2].conv.weight), cls=k3(classifiers))
+            fa1=fa1, fa2=fa2, cls=cls)
 
 
 class ConvGRU(nn.Module):

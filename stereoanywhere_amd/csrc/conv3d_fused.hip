@@ -203,6 +203,26 @@ __global__ __launch_bounds__(256) void conv3d_onehot_s2_kernel(OneHotVol v, int 
   }
 }
 
+// F(4,3) transforms (points 0, +-1, +-2, inf; the same B^T / A^T as conv2d_wino4.hip), for
+// correlation along one axis: out[i] = sum_k g[k] x[i + k] = A^T ((G g) . (B^T x))
+__device__ __forceinline__ void bt6(const float x0, const float x1, const float x2, const float x3, const float x4,
+                                    const float x5, float *o) {
+  const float a = x4 - 4.0f * x2, b = x3 - 4.0f * x1, c = x4 - x2, e = x3 - x1;
+  o[0] = 4.0f * x0 - 5.0f * x2 + x4;
+  o[1] = a + b;
+  o[2] = a - b;
+  o[3] = 2.0f * e + c;
+  o[4] = c - 2.0f * e;
+  o[5] = 4.0f * x1 - 5.0f * x3 + x5;
+}
+__device__ __forceinline__ void at6(const float *m, float *o) {
+  const float a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], e = m[3] - m[4];
+  o[0] = m[0] + a + c;
+  o[1] = b + 2.0f * e;
+  o[2] = a + 4.0f * c;
+  o[3] = b + 8.0f * e + m[5];
+}
+
 template <int S, int TWx>
 struct ConvTile {
   static constexpr int valid_w = TWx - (S == 1 ? 2 : 1);  // output columns per tile
@@ -345,6 +365,179 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const float *__restrict__ i
       }
     }
   }
+  if (partial) {
+    const int nparts = gridDim.x * gridDim.y * tilesD;
+    const int blk = (blockIdx.z % tilesD) * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x;
+    block_stats<COUT>(s, q, red, partial, b, nparts, blk, COUT);
+  }
+}
+
+// Stride-1 3x3x3 conv of 8 input channels (final_agg[1], final_agg[2] and the classifier pair:
+// hourglass.py:329, submodule.py:25-53, stereoanywhere.py:165-166) as Winograd F(4,3) along D:
+// for each (ci, kh, kw) the 3 D-taps of the kernel act on a column of the input along D, so the
+// column is transformed once when it is staged (6 points per 4 outputs, points 0, +-1, +-2, inf:
+// B^T / A^T of conv2d_wino4.hip) and every tap pair (kh, kw) multiplies it by the transformed
+// kernel G g: 6 products per 4 outputs instead of 12 (12 + 12 FMA per column and output channel
+// instead of 24 for the two D-tiles of a thread).  The products accumulate in the transform
+// domain over (ci, kh, kw); one A^T per output column at the end.
+//   block  = 64 (w) x 4 (h) threads, each 2 D-tiles (8 planes) x COUT channels; the staged slab
+//            of one input channel is [6 h rows][64 w columns][12 points] (16-byte reads of a
+//            column's points: a wave's 16-lane groups hit disjoint banks at the 48-byte stride)
+//   staging = the producer's InstanceNorm + LeakyReLU (+ gate), zero padding, then B^T along D,
+//            fetched one input channel ahead; one barrier per input channel
+//   weights = (G g)[ci][kh][kw][p][co] (sa_conv3d_wd weight layout), wave-uniform (SGPR) operands
+template <int COUT, bool GATED>
+__global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict__ in, int D, int H, int W,
+                                                        const float *__restrict__ wt, InXform tx,
+                                                        float *__restrict__ out, double *__restrict__ partial,
+                                                        int tilesD) {
+  constexpr int CIN = 8, NT = 2, TD = 4 * NT, LD = TD + 2, NP = 6 * NT, LH = 6, TWV = 62;
+  constexpr int ROWP = 64 * NP + 4;   // row pitch (floats); 16-byte aligned
+  static_assert(NP % 4 == 0 && ROWP % 4 == 0, "b128 column reads");
+  __shared__ __attribute__((aligned(16))) float slab[2][LH * ROWP];
+  __shared__ double red[COUT * 4 * 2];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int w0 = blockIdx.x * TWV, h0 = blockIdx.y * 4;
+  const int b = blockIdx.z / tilesD, d0 = (blockIdx.z % tilesD) * TD;
+  const int hw = H * W;
+  const int wl = w0 - 1 + lane;
+  const bool wok = wl >= 0 && wl < W;
+  const int wcl = min(max(wl, 0), W - 1);
+  // D-validity of the LD staged planes (block-uniform)
+  unsigned dmask = 0;
+#pragma unroll
+  for (int j = 0; j < LD; ++j) dmask |= (d0 - 1 + j >= 0 && d0 - 1 + j < D) ? (1u << j) : 0u;
+  // this lane's plane offset for the gate_r vector load (lane j < LD holds plane d0 - 1 + j)
+  const int dlane = min(max(d0 - 1 + min(lane, LD - 1), 0), D - 1);
+
+  // staging columns of this thread: (row wv, lane) and, for waves 0-1, (row wv + 4, lane)
+  constexpr int NCOL = 2;
+  float pv[NCOL][LD];
+  float pgl[NCOL], pgr[NCOL];
+  auto fetch = [&](int ci) __attribute__((always_inline)) {
+    const long bc = (long)b * CIN + ci;
+    const float *src = in + bc * (long)D * hw;
+#pragma unroll
+    for (int k = 0; k < NCOL; ++k) {
+      const int hh = wv + 4 * k;
+      if (hh < LH) {
+        const int hc = min(max(h0 - 1 + hh, 0), H - 1);
+        const float *colp = src + hc * W + wcl;
+#pragma unroll
+        for (int j = 0; j < LD; ++j) {
+          int off = min(max(d0 - 1 + j, 0), D - 1) * hw;
+          asm volatile("" : "+v"(off));   // plane offsets in VGPRs: SGPRs hold the weights
+          pv[k][j] = colp[off];
+        }
+        if (GATED) {
+          pgl[k] = tx.gl[(bc * H + hc) * W + wcl];
+          pgr[k] = tx.gr[(bc * H + hc) * D + dlane];   // one plane per lane, read back by readlane
+        }
+      }
+    }
+  };
+  auto commit = [&](int ci, int buf) __attribute__((always_inline)) {
+    const long bc = (long)b * CIN + ci;
+    const float mean = tx.mean[bc], rstd = tx.rstd[bc];
+#pragma unroll
+    for (int k = 0; k < NCOL; ++k) {
+      const int hh = wv + 4 * k;
+      if (hh < LH) {
+        const int h = h0 - 1 + hh;
+        const bool cok = wok && h >= 0 && h < H;
+        float x[LD];
+#pragma unroll
+        for (int j = 0; j < LD; ++j) {
+          float v = (pv[k][j] - mean) * rstd;
+          v = v > 0.0f ? v : v * tx.slope;
+          if (GATED) {   // gate_l[h, w] * gate_r[h, d] (xform's order)
+            const float gr = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pgr[k]), j));
+            v = (pgl[k] * gr) * v;
+          }
+          x[j] = (cok && ((dmask >> j) & 1u)) ? v : 0.0f;
+        }
+        float o[NP];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          bt6(x[4 * t], x[4 * t + 1], x[4 * t + 2], x[4 * t + 3], x[4 * t + 4], x[4 * t + 5], o + 6 * t);
+        float4 *dst = reinterpret_cast<float4 *>(slab[buf] + hh * ROWP + lane * NP);
+#pragma unroll
+        for (int q = 0; q < NP / 4; ++q) dst[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+      }
+    }
+  };
+
+  float M[NT][6][COUT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int p = 0; p < 6; ++p)
+#pragma unroll
+      for (int c = 0; c < COUT; ++c) M[t][p][c] = 0.0f;
+
+  fetch(0);
+  commit(0, 0);
+  __syncthreads();
+#pragma unroll 1
+  for (int ci = 0; ci < CIN; ++ci) {
+    const int buf = ci & 1;
+    if (ci + 1 < CIN) fetch(ci + 1);
+    const float *lb = slab[buf] + wv * ROWP + lane * NP;
+    const float *wc = wt + (long)ci * 9 * 6 * COUT;
+#pragma unroll 1
+    for (int kh = 0; kh < 3; ++kh) {
+#pragma unroll 1
+      for (int kw = 0; kw < 3; ++kw) {
+        const float4 *xp = reinterpret_cast<const float4 *>(lb + kh * ROWP + kw * NP);
+        float X[NP];
+#pragma unroll
+        for (int q = 0; q < NP / 4; ++q) {
+          const float4 v = xp[q];
+          X[4 * q] = v.x;
+          X[4 * q + 1] = v.y;
+          X[4 * q + 2] = v.z;
+          X[4 * q + 3] = v.w;
+        }
+        const float *wp = wc + (kh * 3 + kw) * 6 * COUT;
+#pragma unroll
+        for (int p = 0; p < 6; ++p)
+#pragma unroll
+          for (int c = 0; c < COUT; ++c) {
+            const float wv_ = wp[p * COUT + c];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) M[t][p][c] += X[6 * t + p] * wv_;
+          }
+      }
+    }
+    if (ci + 1 < CIN) commit(ci + 1, buf ^ 1);
+    __syncthreads();
+  }
+
+  // A^T along D, stores, InstanceNorm partials
+  const int w = w0 + lane, h = h0 + wv;
+  const bool ok = lane < TWV && w < W && h < H;
+  float s[COUT], q[COUT];
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) s[c] = q[c] = 0.0f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int c = 0; c < COUT; ++c) {
+      float m[6], o[4];
+#pragma unroll
+      for (int p = 0; p < 6; ++p) m[p] = M[t][p][c];
+      at6(m, o);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int d = d0 + 4 * t + i;
+        if (ok && d < D) {
+          out[(((long)b * COUT + c) * D + d) * (long)hw + (long)h * W + w] = o[i];
+          s[c] += o[i];
+          q[c] += o[i] * o[i];
+        }
+      }
+    }
   if (partial) {
     const int nparts = gridDim.x * gridDim.y * tilesD;
     const int blk = (blockIdx.z % tilesD) * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x;
@@ -637,6 +830,37 @@ extern "C" int sa_conv3d(const float *in, int B, int Cin, int Di, int Hi, int Wi
 #undef SA_CONV
   sa::set_error("sa_conv3d: no kernel built for Cin %d -> Cout %d, stride %d", Cin, Cout, stride);
   return SA_E_ARG;
+}
+
+extern "C" int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W, const float *weight_wd, int Cout,
+                            const float *in_mean, const float *in_rstd, int act, float slope, const float *gate_l,
+                            const float *gate_r, float *out, double *stats_partial, void *stream) {
+  SA_REQUIRE(in && weight_wd && out, "sa_conv3d_wd: null pointer");
+  SA_REQUIRE(B > 0 && D > 0 && H > 0 && W > 0, "sa_conv3d_wd: empty shape");
+  SA_REQUIRE((in_mean == nullptr) == (in_rstd == nullptr), "sa_conv3d_wd: mean and rstd go together");
+  SA_REQUIRE((gate_l == nullptr) == (gate_r == nullptr), "sa_conv3d_wd: both gate maps or none");
+  SA_REQUIRE((long)D * H * W < (1L << 31), "sa_conv3d_wd: a channel plane must hold < 2^31 voxels");
+  SA_REQUIRE(Cin == 8 && (Cout == 8 || Cout == 2), "sa_conv3d_wd: built for 8 -> 8 and 8 -> 2 (got %d -> %d)", Cin,
+             Cout);
+  // the same tiling as sa_conv3d's for these shapes (8 planes x 4 rows x 62 columns): the same
+  // statistic parts
+  const ConvGeo geo = conv_geo(Cout, 1);
+  SA_REQUIRE(geo.td == 8 && geo.tw == 64 && geo.th == 4, "sa_conv3d_wd: tiling");
+  int tilesD;
+  dim3 grid = conv_grid(B, D, H, W, geo, tilesD);
+  InXform tx{in_mean, in_rstd, gate_l, gate_r, slope, act};
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_CONV3D, s);
+  SA_REQUIRE(in_mean && act, "sa_conv3d_wd: built for an InstanceNorm + LeakyReLU producer");
+  if (Cout == 8 && !gate_l)
+    conv3d_wd_kernel<8, false><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, tilesD);
+  else if (Cout == 2 && gate_l)
+    conv3d_wd_kernel<2, true><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, tilesD);
+  else if (Cout == 8)
+    conv3d_wd_kernel<8, true><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, tilesD);
+  else
+    conv3d_wd_kernel<2, false><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, tilesD);
+  return sa::check_launch("sa_conv3d_wd");
 }
 
 extern "C" int sa_conv3d_pointwise(const float *in, int B, int Cin, int D, int H, int W, const float *mean,

@@ -438,6 +438,36 @@ def conv3d(x: "VolAct", w_t: torch.Tensor, cout: int, stride: int = 1, slope: fl
     return VolAct(out, norm, act=stats)
 
 
+# G of Winograd F(4,3) (points 0, +-1, +-2, inf; conv2d_wino4.hip's filter transform)
+_G43 = ((0.25, 0.0, 0.0), (-1.0 / 6, -1.0 / 6, -1.0 / 6), (-1.0 / 6, 1.0 / 6, -1.0 / 6),
+        (1.0 / 24, 1.0 / 12, 1.0 / 6), (1.0 / 24, -1.0 / 12, 1.0 / 6), (0.0, 0.0, 1.0))
+
+
+def conv3d_wd_weights(w_t: torch.Tensor) -> torch.Tensor:
+    """[Cin][27][Cout] 3x3x3 kernel (ops.conv3d layout) -> [Cin][3 kh][3 kw][6][Cout], the D-taps
+    transformed by G of F(4,3) in float64 and rounded once (sa_conv3d_wd)."""
+    cin, _, cout = w_t.shape
+    G = torch.tensor(_G43, dtype=torch.float64, device=w_t.device)
+    w = w_t.to(torch.float64).reshape(cin, 3, 3, 3, cout)   # [ci][kd][kh][kw][co]
+    return torch.einsum("pk,ikhwc->ihwpc", G, w).to(torch.float32).contiguous()
+
+
+def conv3d_wd(x: "VolAct", w_wd: torch.Tensor, cout: int, slope: float = 0.01, stats: bool = True) -> "VolAct":
+    """ops.conv3d at stride 1 for 8 input channels (-> 8 or 2) on the F(4,3)-along-D kernel;
+    w_wd from conv3d_wd_weights.  The input must carry an InstanceNorm + LeakyReLU (+ gate)."""
+    _check(x.raw, "x")
+    _check(w_wd, "w_wd")
+    B, Cin, D, H, W = x.raw.shape
+    out = torch.empty((B, cout, D, H, W), device=x.raw.device, dtype=torch.float32)
+    parts = conv3d_stat_parts(cout, 1, D, H, W)
+    partial = torch.empty((B * cout * parts * 2,), device=out.device, dtype=torch.float64) if stats else None
+    a = x.args()
+    N.call("sa_conv3d_wd", x.raw.data_ptr(), B, Cin, D, H, W, w_wd.data_ptr(), cout, a[0], a[1], a[2], slope,
+           a[3], a[4], out.data_ptr(), _ptr(partial), _stream(out))
+    norm = instnorm_finalize(partial, B * cout, parts, D * H * W) if stats else None
+    return VolAct(out, norm, act=stats)
+
+
 def _conv3d_onehot(x: OneHotVolume, w_t: torch.Tensor, cout: int, stride: int, stats: bool):
     _check(w_t, "w_t")
     B, nb, D, H, W = x.shape
