@@ -44,7 +44,7 @@ def main():
             r = fn(*a, **k)
             e1.record()
             shape = tuple(a[0].raw.shape) if hasattr(a[0], "raw") else tuple(a[0].shape)
-            rec.append((f"{name} {shape} -> {a[2] if name == 'conv3d' else ''}", e0, e1))
+            rec.append((f"{name} {shape} -> {a[2] if name in ('conv3d', 'conv3d_wd') else ''}", e0, e1))
             return r
         return f
     for n in ("conv3d", "conv3d_wd", "conv3d_pointwise", "conv3d_pointwise_upcat"):

@@ -386,14 +386,19 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const float *__restrict__ i
 //   staging = the producer's InstanceNorm + LeakyReLU (+ gate), zero padding, then B^T along D,
 //            fetched one input channel ahead; one barrier per input channel
 //   weights = (G g)[ci][kh][kw][p][co] (sa_conv3d_wd weight layout), wave-uniform (SGPR) operands
-template <int COUT, bool GATED>
+template <int CIN, int COUT, int NT, bool GATED>
 __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict__ in, int D, int H, int W,
                                                         const float *__restrict__ wt, InXform tx,
                                                         float *__restrict__ out, double *__restrict__ partial,
                                                         int tilesD) {
-  constexpr int CIN = 8, NT = 2, TD = 4 * NT, LD = TD + 2, NP = 6 * NT, LH = 6, TWV = 62;
+  constexpr int TD = 4 * NT, LD = TD + 2, NP = 6 * NT, LH = 6, TWV = 62;
   constexpr int ROWP = 64 * NP + 4;   // row pitch (floats); 16-byte aligned
-  static_assert(NP % 4 == 0 && ROWP % 4 == 0, "b128 column reads");
+  // a column's points: 16-byte accesses at a 48-byte lane stride (NT = 2) or 8-byte ones at 24
+  // (NT = 1); either way a wave's lane groups hit disjoint banks
+  using VT = typename std::conditional<NP % 4 == 0, float4, float2>::type;
+  constexpr int VW = sizeof(VT) / 4;
+  static_assert(ROWP % 4 == 0, "row alignment");
+  constexpr int CC = COUT < 8 ? COUT : 8;   // output channels per weight group (48 SGPRs)
   __shared__ __attribute__((aligned(16))) float slab[2][LH * ROWP];
   __shared__ double red[COUT * 4 * 2];
   const int lane = threadIdx.x & 63;
@@ -461,9 +466,14 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
 #pragma unroll
         for (int t = 0; t < NT; ++t)
           bt6(x[4 * t], x[4 * t + 1], x[4 * t + 2], x[4 * t + 3], x[4 * t + 4], x[4 * t + 5], o + 6 * t);
-        float4 *dst = reinterpret_cast<float4 *>(slab[buf] + hh * ROWP + lane * NP);
+        VT *dst = reinterpret_cast<VT *>(slab[buf] + hh * ROWP + lane * NP);
 #pragma unroll
-        for (int q = 0; q < NP / 4; ++q) dst[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+        for (int q = 0; q < NP / VW; ++q) {
+          VT v;
+#pragma unroll
+          for (int e = 0; e < VW; ++e) reinterpret_cast<float *>(&v)[e] = o[VW * q + e];
+          dst[q] = v;
+        }
       }
     }
   };
@@ -489,25 +499,27 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
     for (int kh = 0; kh < 3; ++kh) {
 #pragma unroll 1
       for (int kw = 0; kw < 3; ++kw) {
-        const float4 *xp = reinterpret_cast<const float4 *>(lb + kh * ROWP + kw * NP);
+        const VT *xp = reinterpret_cast<const VT *>(lb + kh * ROWP + kw * NP);
         float X[NP];
 #pragma unroll
-        for (int q = 0; q < NP / 4; ++q) {
-          const float4 v = xp[q];
-          X[4 * q] = v.x;
-          X[4 * q + 1] = v.y;
-          X[4 * q + 2] = v.z;
-          X[4 * q + 3] = v.w;
+        for (int q = 0; q < NP / VW; ++q) {
+          const VT v = xp[q];
+#pragma unroll
+          for (int e = 0; e < VW; ++e) X[VW * q + e] = reinterpret_cast<const float *>(&v)[e];
         }
         const float *wp = wc + (kh * 3 + kw) * 6 * COUT;
 #pragma unroll
-        for (int p = 0; p < 6; ++p)
+        for (int cg = 0; cg < COUT / CC; ++cg) {
+          if (cg) __builtin_amdgcn_sched_barrier(0);   // one channel group's weights live at a time
 #pragma unroll
-          for (int c = 0; c < COUT; ++c) {
-            const float wv_ = wp[p * COUT + c];
+          for (int p = 0; p < 6; ++p)
 #pragma unroll
-            for (int t = 0; t < NT; ++t) M[t][p][c] += X[6 * t + p] * wv_;
-          }
+            for (int c = cg * CC; c < cg * CC + CC; ++c) {
+              const float wv_ = wp[p * COUT + c];
+#pragma unroll
+              for (int t = 0; t < NT; ++t) M[t][p][c] += X[6 * t + p] * wv_;
+            }
+        }
       }
     }
     if (ci + 1 < CIN) commit(ci + 1, buf ^ 1);
@@ -840,27 +852,32 @@ extern "C" int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W
   SA_REQUIRE((in_mean == nullptr) == (in_rstd == nullptr), "sa_conv3d_wd: mean and rstd go together");
   SA_REQUIRE((gate_l == nullptr) == (gate_r == nullptr), "sa_conv3d_wd: both gate maps or none");
   SA_REQUIRE((long)D * H * W < (1L << 31), "sa_conv3d_wd: a channel plane must hold < 2^31 voxels");
-  SA_REQUIRE(Cin == 8 && (Cout == 8 || Cout == 2), "sa_conv3d_wd: built for 8 -> 8 and 8 -> 2 (got %d -> %d)", Cin,
-             Cout);
-  // the same tiling as sa_conv3d's for these shapes (8 planes x 4 rows x 62 columns): the same
-  // statistic parts
+  SA_REQUIRE((Cin == 8 && (Cout == 8 || Cout == 2)) || (Cin == 16 && Cout == 16),
+             "sa_conv3d_wd: built for 8 -> 8, 8 -> 2 and 16 -> 16 (got %d -> %d)", Cin, Cout);
+  // the same tiling as sa_conv3d's for these shapes (8 or 4 planes x 4 rows x 62 columns): the
+  // same statistic parts
   const ConvGeo geo = conv_geo(Cout, 1);
-  SA_REQUIRE(geo.td == 8 && geo.tw == 64 && geo.th == 4, "sa_conv3d_wd: tiling");
+  SA_REQUIRE(geo.td == (Cin == 8 ? 8 : 4) && geo.tw == 64 && geo.th == 4, "sa_conv3d_wd: tiling");
   int tilesD;
   dim3 grid = conv_grid(B, D, H, W, geo, tilesD);
   InXform tx{in_mean, in_rstd, gate_l, gate_r, slope, act};
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV3D, s);
   SA_REQUIRE(in_mean && act, "sa_conv3d_wd: built for an InstanceNorm + LeakyReLU producer");
-  if (Cout == 8 && !gate_l)
-    conv3d_wd_kernel<8, false><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, tilesD);
-  else if (Cout == 2 && gate_l)
-    conv3d_wd_kernel<2, true><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, tilesD);
-  else if (Cout == 8)
-    conv3d_wd_kernel<8, true><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, tilesD);
-  else
-    conv3d_wd_kernel<2, false><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, tilesD);
-  return sa::check_launch("sa_conv3d_wd");
+#define SA_WD(CI, CO, NTV, G)                                                                                   \
+  if (Cin == CI && Cout == CO && (gate_l != nullptr) == G) {                                                    \
+    conv3d_wd_kernel<CI, CO, NTV, G><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, tilesD); \
+    return sa::check_launch("sa_conv3d_wd");                                                                     \
+  }
+  SA_WD(8, 8, 2, false)
+  SA_WD(8, 2, 2, true)
+  SA_WD(8, 8, 2, true)
+  SA_WD(8, 2, 2, false)
+  SA_WD(16, 16, 1, false)
+  SA_WD(16, 16, 1, true)
+#undef SA_WD
+  sa::set_error("sa_conv3d_wd: no kernel for %d -> %d", Cin, Cout);
+  return SA_E_ARG;
 }
 
 extern "C" int sa_conv3d_pointwise(const float *in, int B, int Cin, int D, int H, int W, const float *mean,

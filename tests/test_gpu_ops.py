@@ -473,19 +473,20 @@ def test_fused_hourglass_on_onehot_records_matches_torch():
     torch.testing.assert_close(vc, ref[:, 1:2], atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize("cout,gated,shape", [(8, False, (2, 20, 12, 70)), (2, True, (1, 13, 9, 130)),
-                                              (8, True, (1, 8, 5, 64)), (2, False, (2, 17, 6, 30))])
-def test_conv3d_wd_matches_direct(cout, gated, shape):
+@pytest.mark.parametrize("cin,cout,gated,shape", [(8, 8, False, (2, 20, 12, 70)), (8, 2, True, (1, 13, 9, 130)),
+                                                  (8, 8, True, (1, 8, 5, 64)), (8, 2, False, (2, 17, 6, 30)),
+                                                  (16, 16, False, (2, 15, 10, 66)), (16, 16, True, (1, 6, 7, 20))])
+def test_conv3d_wd_matches_direct(cin, cout, gated, shape):
     """The F(4,3)-along-D conv (sa_conv3d_wd) against the direct fused conv (sa_conv3d) on the
     same transformed input: ragged D (not a multiple of the 8-plane tile), H, W edges."""
     B, D, H, W = shape
     rng = np.random.default_rng(D * W)
-    x = g(rng.standard_normal((B, 8, D, H, W)))
-    mean = g(rng.standard_normal(B * 8) * 0.1)
-    rstd = g(rng.random(B * 8) + 0.5)
-    gate = (g(rng.random((B, 8, H, W))), g(rng.random((B, 8, H, D)))) if gated else None
+    x = g(rng.standard_normal((B, cin, D, H, W)))
+    mean = g(rng.standard_normal(B * cin) * 0.1)
+    rstd = g(rng.random(B * cin) + 0.5)
+    gate = (g(rng.random((B, cin, H, W))), g(rng.random((B, cin, H, D)))) if gated else None
     v = ops.VolAct(x, (mean, rstd), act=True, gate=gate)
-    w = g(rng.standard_normal((8, 27, cout)) * 0.2)
+    w = g(rng.standard_normal((cin, 27, cout)) * 0.2)
     a = ops.conv3d_wd(v, ops.conv3d_wd_weights(w), cout, slope=0.01)
     b = ops.conv3d(v, w, cout, slope=0.01)
     torch.testing.assert_close(a.raw, b.raw, atol=2e-5, rtol=1e-5)
