@@ -318,6 +318,11 @@ int sa_conv2d_k3_wino_multi(int nprob, const SaWinoProblem *probs, void *stream)
  * (in_m / in_s / in_t NULL, in_act 0); bias, ReLU and the InstanceNorm partials
  * ([N*Cout][parts][2], parts = sa_conv2d_k3_wino4_stat_parts(H, W)) as sa_conv2d_k3_wino_ex. */
 int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, float *U4, void *stream);
+/* U4 for the wide block shape (block_shape 3 of sa_conv2d_k3_wino4_multi_gate: 64 output
+ * channels per block): co_block 64 lays the filters out [Cout/64][Cin/8][36][2][4][16][4]
+ * (Cout % 64 == 0); co_block 32 is sa_conv2d_wino4_weights. */
+int sa_conv2d_wino4_weights_cb(const float *weight, int Cout, int Cin, int co_block, float *U4,
+                               void *stream);
 long sa_conv2d_k3_wino4_stat_parts(int H, int W);
 int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, void *stream);
 /* ConvGRU gates in the epilogue (update.py:16-27), per problem (gates[i].mode 0 = plain; gates
@@ -341,7 +346,9 @@ typedef struct SaGateEpilogue {
   long out2_bs;
 } SaGateEpilogue;
 /* block_shape: 0 / 1 large blocks (8 waves, 64 Winograd tiles, one per CU), 2 small blocks (4
- * waves, 32 tiles, two per CU: shorter launches of few rounds fill the chip better). */
+ * waves, 32 tiles, two per CU: shorter launches of few rounds fill the chip better), 3 wide
+ * blocks (4 waves, 32 tiles x 64 output channels, one per CU; every problem's U from
+ * sa_conv2d_wino4_weights_cb(..., 64, ...), Cout % 64 == 0, and Cout % 128 == 0 with a z/r gate). */
 int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                                   int block_shape, void *stream);
 

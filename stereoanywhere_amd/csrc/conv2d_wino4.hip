@@ -42,7 +42,7 @@
 #ifndef SA_W4_DIAG
 #define SA_W4_DIAG 0   // timing diagnostics only (wrong results): 1 no DMA in the loop, 2 no
                        // transform / MFMA, 3 no DMA and no barrier in the loop, 4 as 3 and no
-                       // DMA at all
+                       // DMA at all, 5 no column pass, 6 no row pass, 7 no filter reads in the loop
 #endif
 #ifndef SA_W4_PRIO
 #define SA_W4_PRIO 0
@@ -54,16 +54,17 @@ using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f32x2 = __attribute__((ext_vector_type(2))) float;
 
 constexpr int NPT = 36;                   // transform points
-constexpr int CO = 32;                    // output channels per block
 
 // Two block shapes of the same algorithm.  Large (the default): 8 waves, 64 tiles, 8-channel
 // chunks, one block per CU (158 KiB of LDS).  Small (block_shape 2): 4 waves, 32 tiles,
 // 4-channel chunks, 66 KiB, two blocks per CU, so one block's first DMA wait and epilogue
 // overlap the other's MFMAs (per block ~6-8k cycles until the first chunk lands and ~9k of
 // epilogue around 6.8k per chunk, scripts/w4_clock.py); it is not faster in the forward.
-template <int NW_, int KC_>
+template <int NW_, int KC_, int CO_ = 32>
 struct W4Cfg {
   static constexpr int NW = NW_, NTHR = 64 * NW_, TG = NW_ / 2, NT = 16 * TG, KC = KC_, JPC = KC_ / 4;
+  static constexpr int CO = CO_, CG = CO_ / 16;                // output channels per block, 16-channel groups
+  static constexpr int SB = 4 * CO_;                        // filters per (point, 4-channel job): [k][n][g]
   static constexpr int PS_MAX = NT == 64 ? 340 : 204;       // (BH + 2)(BW / 4 + 2), largest geometry
   static constexpr int PBUF = (KC * PS_MAX + 32) * 4;       // + the last DMA's idle lanes
   static constexpr int UBUF = NPT * KC * CO;                // filters per chunk
@@ -74,12 +75,20 @@ struct W4Cfg {
   static constexpr int UDMA = UBUF / 256;                   // filter DMA pieces (1 KiB) per chunk
   static constexpr int UPW = (UDMA + NW - 1) / NW;          // per wave
   static_assert(SMEM * 4 <= 160 * 1024, "LDS budget");
-  static_assert(PDMA <= 6 && UPW <= 6, "three DMA parts of two pieces");
+  static constexpr int PPART = (PDMA > UPW ? PDMA : UPW) > 6 ? 3 : 2;   // DMA pieces per part
+  static_assert(PDMA <= 3 * PPART && UPW <= 3 * PPART, "three DMA parts");
   static_assert(OPP % 32 == 4, "conflict-free staging");
 };
 using W4Big = W4Cfg<8, 8>;
 using W4Small = W4Cfg<4, 4>;
+// Wide: one wave per SIMD, 32 tiles x 64 output channels, 4-channel chunks.  Each transformed
+// input value feeds four MFMAs (one per 16-channel group) instead of two, and one ds_read_b128
+// hands a lane its four filter operands: half the transform VALU and the filter-read
+// instructions per MFMA of the 8-wave shape (whose main loop measured VALU- and LDS-issue
+// bound: -DSA_W4_DIAG=5/7 builds ran 20% / 15% faster).  288 accumulators per lane.
+using W4Wide = W4Cfg<4, 4, 64>;
 static_assert(2 * W4Small::SMEM * 4 <= 160 * 1024, "two small blocks per CU");
+static_assert(W4Wide::SMEM * 4 <= 160 * 1024, "one wide block per CU");
 
 struct W4Prob {
   const float *in;
@@ -171,7 +180,9 @@ __device__ unsigned long long g_w4_clock[65536][10];   // + [8] chunk 0 issued, 
 template <class C, int HF, int LTW, bool GATED>
 __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, const unsigned wid, float *smem) {
   constexpr int NWAVE = C::NW, NTHR = C::NTHR, KC = C::KC, JPC = C::JPC, NT = C::NT, PDMA = C::PDMA,
-                UDMA = C::UDMA, UPW = C::UPW, UBUF = C::UBUF, BUF = C::BUF, PBUF = C::PBUF, OPP = C::OPP;
+                UDMA = C::UDMA, UPW = C::UPW, UBUF = C::UBUF, BUF = C::BUF, PBUF = C::PBUF, OPP = C::OPP,
+                CO = C::CO, CG = C::CG, SB = C::SB;
+  using f32xg = __attribute__((ext_vector_type(CG))) float;   // a lane's filter operands, one per group
   const int Cin = P.Cin, H = P.H, W = P.W, Cout = P.Cout;
   // block geometry as compile-time constants (the patch offsets divide by PS and PG)
   constexpr int ltw = LTW, tw = 1 << ltw, tr = NT >> ltw;
@@ -190,15 +201,15 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   const __amdgpu_buffer_rsrc_t xin = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float *>(P.in + (long)n * P.in_bs), (short)0, Cin * hw * 4, 0x00020000);
   // the filters' global layout has 8-channel chunks (sa_conv2d_wino4_weights); a 4-channel
-  // chunk is every other 512-byte piece of one (the DMA gathers it by its source addresses)
+  // chunk is every other SB-float piece of one (the DMA gathers it by its source addresses)
   const __amdgpu_buffer_rsrc_t uin = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float *>(P.U + (long)cb * Cin * NPT * CO), (short)0, Cin * NPT * CO * 4, 0x00020000);
   auto u_src = [&](int piece) {   // byte offset of this lane's 16 bytes of filter DMA piece `piece`
     const int f = piece * 256 + lane * 4;
-    return (JPC == 2 ? f : f + (f >> 7) * 128) * 4;
+    return (JPC == 2 ? f : f + (f / SB) * SB) * 4;
   };
   auto u_chunk = [&](int chunk) {   // byte offset of a chunk's filters
-    return JPC == 2 ? chunk * UBUF * 4 : (chunk >> 1) * 2 * UBUF * 4 + (chunk & 1) * 512;
+    return JPC == 2 ? chunk * UBUF * 4 : (chunk >> 1) * 2 * UBUF * 4 + (chunk & 1) * SB * 4;
   };
 
   // patch DMA: the chunk's image is [channel][PR rows][PG groups of 4 floats], dense, starting
@@ -227,12 +238,12 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
     const int xs = chunk * KC * hw * 4;
 #pragma unroll
     for (int j = 0; j < PDMA; ++j)
-      if ((part < 0 || j / 2 == part) && wv + NWAVE * j < npi) dma16(xin, pb + (wv + NWAVE * j) * 256, po[j], xs);
+      if ((part < 0 || j / C::PPART == part) && wv + NWAVE * j < npi) dma16(xin, pb + (wv + NWAVE * j) * 256, po[j], xs);
     float *ub = pb + PBUF;
     const int us = u_chunk(chunk);
 #pragma unroll
     for (int j = 0; j < UPW; ++j)
-      if ((part < 0 || j / 2 == part) && wv + NWAVE * j < UDMA)
+      if ((part < 0 || j / C::PPART == part) && wv + NWAVE * j < UDMA)
         dma16(uin, ub + (wv + NWAVE * j) * 256, u_src(wv + NWAVE * j), us);
   };
   auto issue = [&](int chunk, int buf) __attribute__((always_inline)) { issue_part(chunk, buf, -1); };
@@ -254,14 +265,16 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   int PSv = PS, PGv = PG;
   asm volatile("" : "+s"(PSv), "+s"(PGv));
   const int pread = k * PSv * 4 + 4 * trow * PGv * 4 + 4 * tcol + 2;
-  const int uread = k * 32 + 2 * m;
+  const int uread = (k * 16 + m) * CG;
 
-  // acc[i][jj][g]: point (row i, column 3 HF + jj) of output-channel half g
-  f32x4 acc[6][3][2];
+  // acc[i][jj][g]: point (row i, column 3 HF + jj) of output-channel group g
+  f32x4 acc[6][3][CG];
 #pragma unroll
   for (int i = 0; i < 6; ++i)
 #pragma unroll
-    for (int jj = 0; jj < 3; ++jj) acc[i][jj][0] = acc[i][jj][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int jj = 0; jj < 3; ++jj)
+#pragma unroll
+      for (int g = 0; g < CG; ++g) acc[i][jj][g] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (SA_W4_PRIO && HF == 1) __builtin_amdgcn_s_setprio(1);   // static priority for waves 4-7
   if (SA_W4_DIAG != 4) issue_p0();
@@ -297,10 +310,10 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
         rc[r] = *reinterpret_cast<const f32x2 *>(p + r * PGv * 4 + 6);
       }
     };
-    f32x2 bc[6], bn[6];
-    auto load_b = [&](int s, int jj, f32x2 *b) __attribute__((always_inline)) {
+    f32xg bc[6], bn[6];
+    auto load_b = [&](int s, int jj, f32xg *b) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < 6; ++i) b[i] = *reinterpret_cast<const f32x2 *>(ub + ((6 * i + 3 * HF + jj) * JPC + s) * 4 * 32);
+      for (int i = 0; i < 6; ++i) b[i] = *reinterpret_cast<const f32xg *>(ub + ((6 * i + 3 * HF + jj) * JPC + s) * SB);
     };
     load_rows(0, 0, 6);
     load_b(0, 0, bc);
@@ -309,18 +322,29 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
       if (s == 1) load_rows(1, 3, 6);
       float t[6][3];
 #pragma unroll
-      for (int r = 0; r < 6; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t[r]);
+      for (int r = 0; r < 6; ++r) {
+        if (SA_W4_DIAG == 6) {   // timing only: no row pass
+          t[r][0] = ra[r].y; t[r][1] = rb[r].x; t[r][2] = rc[r].x;
+        } else {
+          bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t[r]);
+        }
+      }
       if (s + 1 < JPC) load_rows(1, 0, 3);
 #pragma unroll
       for (int jj = 0; jj < 3; ++jj) {
-        if (s + 1 < JPC || jj < 2) load_b(jj < 2 ? s : s + 1, jj < 2 ? jj + 1 : 0, bn);
+        if (SA_W4_DIAG != 7 && (s + 1 < JPC || jj < 2)) load_b(jj < 2 ? s : s + 1, jj < 2 ? jj + 1 : 0, bn);
         float v[6];
-        bt6(t[0][jj], t[1][jj], t[2][jj], t[3][jj], t[4][jj], t[5][jj], v);
+        if (SA_W4_DIAG == 5) {   // timing only: no column pass
 #pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], bc[i].x, acc[i][jj][0], 0, 0, 0);
-          acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], bc[i].y, acc[i][jj][1], 0, 0, 0);
+          for (int i = 0; i < 6; ++i) v[i] = t[i][jj];
+        } else {
+          bt6(t[0][jj], t[1][jj], t[2][jj], t[3][jj], t[4][jj], t[5][jj], v);
         }
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+          for (int g = 0; g < CG; ++g)
+            acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], bc[i][g], acc[i][jj][g], 0, 0, 0);
 #if SA_W4_FENCE
         __builtin_amdgcn_sched_barrier(0);   // bound the scheduler's hoisting (register pressure)
 #endif
@@ -343,16 +367,18 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   // ---- output transform.  Lane holds tiles tg * 16 + 4 (lane >> 4) + i of output channels
   // g * 16 + (lane & 15), points of columns 3 HF .. 3 HF + 2.  Y = A^T M A: the column-wise
   // A^T runs per column, the row-wise A^T only over this half's columns (a partial sum).  The
-  // halves meet in LDS, O[co][row][x] (one float4 per output row of a tile), balanced: in
-  // phase 0 each half stages its partials of the OTHER half's channel group (g = 1 - HF); in
-  // phase 1 it adds its own partials of group g = HF, the bias and the ReLU.  Plane pitch OPP =
+  // halves meet in LDS, O[co][row][x] (one float4 per output row of a tile), balanced: half HF
+  // finishes the channel groups g with g % 2 == HF: in phase 0 each half stages its partials of
+  // the OTHER half's groups; in phase 1 it adds its own partials, the bias and the ReLU.  Plane pitch OPP =
   // 4 (mod 32) floats: the 8 lanes of a ds_write_b128 group (8 output channels) hit disjoint
   // banks.
   float *ot = smem;
   const int relu = P.relu;
 #pragma unroll
   for (int phase = 0; phase < 2; ++phase) {
-    const int g = phase == 0 ? 1 - HF : HF;
+#pragma unroll
+  for (int gi = 0; gi < CG / 2; ++gi) {
+    const int g = 2 * gi + (phase == 0 ? 1 - HF : HF);
     const int col = g * 16 + (lane & 15);
     const float bv = (phase == 1 && P.bias) ? P.bias[co0 + col] : 0.0f;
 #pragma unroll
@@ -363,7 +389,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
       for (int jj = 0; jj < 3; ++jj) {
         float mcol[6], o[4];
 #pragma unroll
-        for (int a = 0; a < 6; ++a) mcol[a] = phase == 0 ? acc[a][jj][1 - HF][i] : acc[a][jj][HF][i];
+        for (int a = 0; a < 6; ++a) mcol[a] = acc[a][jj][g][i];
         at6(mcol, o);
 #pragma unroll
         for (int a = 0; a < 4; ++a) u[a][jj] = o[a];
@@ -391,6 +417,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
         }
       }
     }
+  }
     if (phase == 0) __syncthreads();
   }
 #ifdef SA_W4_CLOCK
@@ -509,7 +536,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
 }
 
 template <class C, bool GATED>
-__global__ __launch_bounds__(C::NTHR, C::NW == 8 ? 1 : 2) void wino_f4k3_kernel(const W4Launch L) {
+__global__ __launch_bounds__(C::NTHR, C::NW == 8 || C::CO == 64 ? 1 : 2) void wino_f4k3_kernel(const W4Launch L) {
   // problem of the block from its raw id (ranges padded to multiples of 8: every XCD gets an
   // equal share of each problem), then the L2-locality remap within it (conv2d_wino.hip)
   const unsigned g = blockIdx.x;
@@ -550,7 +577,7 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 ? 1 : 2) void wino_f4k3_kernel(
 // [Cout/32][Cin/8][36][2][4][16][2]: per (output block, chunk) one contiguous 36 KiB image of
 // the LDS filter buffer; channel ci = 8 chunk + 4 s + k, output co = 32 cb + 16 h + n at
 // [n][h].
-__global__ __launch_bounds__(256) void wino4_weights_kernel(const float *__restrict__ w, int Cout, int Cin,
+__global__ __launch_bounds__(256) void wino4_weights_kernel(const float *__restrict__ w, int Cout, int Cin, int CB,
                                                             float *__restrict__ U) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)Cout * Cin) return;
@@ -565,12 +592,12 @@ __global__ __launch_bounds__(256) void wino4_weights_kernel(const float *__restr
   double t[6][3];
   for (int a = 0; a < 6; ++a)
     for (int c = 0; c < 3; ++c) t[a][c] = G[a][0] * g[c] + G[a][1] * g[3 + c] + G[a][2] * g[6 + c];
-  const int chunk = ci / 8, s = (ci % 8) / 4, k = ci % 4, cb = co / 32, c = co % 32;
+  const int chunk = ci / 8, s = (ci % 8) / 4, k = ci % 4, cb = co / CB, c = co % CB, ng = CB / 16;
   for (int a = 0; a < 6; ++a)
     for (int b = 0; b < 6; ++b) {
       const double u = t[a][0] * G[b][0] + t[a][1] * G[b][1] + t[a][2] * G[b][2];
       const int pt = 6 * a + b;
-      U[(((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 2 + s) * 4 + k) * CO + (c & 15) * 2 + (c >> 4)] = (float)u;
+      U[(((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 2 + s) * 4 + k) * CB + (c & 15) * ng + (c >> 4)] = (float)u;
     }
 }
 
@@ -583,13 +610,19 @@ int w4_ltw(int H, int W) {
 
 }  // namespace
 
-extern "C" int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, float *U, void *stream) {
-  SA_REQUIRE(weight && U && Cout > 0 && Cin > 0 && Cin % 8 == 0 && Cout % 32 == 0,
-             "sa_conv2d_wino4_weights: bad arguments (Cin %% 8, Cout %% 32)");
+extern "C" int sa_conv2d_wino4_weights_cb(const float *weight, int Cout, int Cin, int co_block, float *U,
+                                          void *stream) {
+  SA_REQUIRE(co_block == 32 || co_block == 64, "sa_conv2d_wino4_weights: co_block 32 or 64");
+  SA_REQUIRE(weight && U && Cout > 0 && Cin > 0 && Cin % 8 == 0 && Cout % co_block == 0,
+             "sa_conv2d_wino4_weights: bad arguments (Cin %% 8, Cout %% %d)", co_block);
   const long n = (long)Cout * Cin;
   hipStream_t s = sa::as_stream(stream);
-  wino4_weights_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(weight, Cout, Cin, U);
+  wino4_weights_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(weight, Cout, Cin, co_block, U);
   return sa::check_launch("sa_conv2d_wino4_weights");
+}
+
+extern "C" int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, float *U, void *stream) {
+  return sa_conv2d_wino4_weights_cb(weight, Cout, Cin, 32, U, stream);
 }
 
 #ifdef SA_W4_CLOCK
@@ -611,12 +644,14 @@ extern "C" int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, v
 extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                                              int block_shape, void *stream) {
   SA_REQUIRE(nprob >= 1 && nprob <= MAX_PROB && probs, "sa_conv2d_k3_wino4_multi: 1..%d problems", MAX_PROB);
-  SA_REQUIRE(block_shape >= 0 && block_shape <= 2, "sa_conv2d_k3_wino4_multi: block_shape 0..2");
-  // Large blocks unless the caller asks for small ones (block_shape 2).  The small shape
-  // measured 2-8% faster on standalone launches of Cin <= 128 with a few rounds of blocks
-  // (qh08, convc2) but not faster in the forward as a blanket choice.
-  const bool small = block_shape == 2;
-  const int nt = small ? W4Small::NT : W4Big::NT;
+  SA_REQUIRE(block_shape >= 0 && block_shape <= 3, "sa_conv2d_k3_wino4_multi: block_shape 0..3");
+  // Large blocks unless the caller asks for small ones (block_shape 2) or wide ones (3: 64
+  // output channels per block, filters from sa_conv2d_wino4_weights_cb(..., 64, ...)).  The
+  // small shape measured 2-8% faster on standalone launches of Cin <= 128 with a few rounds of
+  // blocks (qh08, convc2) but not faster in the forward as a blanket choice.
+  const bool small = block_shape == 2, wide = block_shape == 3;
+  const int nt = small || wide ? W4Small::NT : W4Big::NT;
+  const int CO = wide ? 64 : 32;
   W4Launch L{};
   long total = 0;
   bool gated = false;
@@ -644,9 +679,9 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
       SA_REQUIRE(!q.relu && !q.stats_partial, "sa_conv2d_k3_wino4: a gate epilogue takes no ReLU / statistics");
       SA_REQUIRE(e.ctx && e.h && a16(e.ctx) && a16(e.h) && e.ctx_bs % 4 == 0 && e.h_bs % 4 == 0,
                  "sa_conv2d_k3_wino4: gate needs 16-byte aligned ctx and h planes");
-      if (e.mode == 1)
-        SA_REQUIRE(q.Cout % 64 == 0 && e.out2 && a16(e.out2) && e.out2_bs % 4 == 0,
-                   "sa_conv2d_k3_wino4: z/r gate needs Cout %% 64 == 0 and an aligned r*h output");
+      if (e.mode == 1)   // a block's channels lie wholly in the z half or the r half
+        SA_REQUIRE(q.Cout % (2 * CO) == 0 && e.out2 && a16(e.out2) && e.out2_bs % 4 == 0,
+                   "sa_conv2d_k3_wino4: z/r gate needs Cout %% %d == 0 and an aligned r*h output", 2 * CO);
       else
         SA_REQUIRE(e.z && e.add && a16(e.z) && a16(e.add) && e.z_bs % 4 == 0 && e.add_bs % 4 == 0,
                    "sa_conv2d_k3_wino4: state gate needs aligned z and addend planes");
@@ -669,6 +704,9 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
   if (small)
     gated ? wino_f4k3_kernel<W4Small, true><<<(unsigned)total, W4Small::NTHR, 0, s>>>(L)
           : wino_f4k3_kernel<W4Small, false><<<(unsigned)total, W4Small::NTHR, 0, s>>>(L);
+  else if (wide)
+    gated ? wino_f4k3_kernel<W4Wide, true><<<(unsigned)total, W4Wide::NTHR, 0, s>>>(L)
+          : wino_f4k3_kernel<W4Wide, false><<<(unsigned)total, W4Wide::NTHR, 0, s>>>(L);
   else
     gated ? wino_f4k3_kernel<W4Big, true><<<(unsigned)total, W4Big::NTHR, 0, s>>>(L)
           : wino_f4k3_kernel<W4Big, false><<<(unsigned)total, W4Big::NTHR, 0, s>>>(L);

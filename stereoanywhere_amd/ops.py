@@ -594,15 +594,19 @@ def conv2d_k3_narrow(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch
 
 class WinoFilters:
     """Transformed filters of one 3x3 conv for both fused Winograd kernels: ``u2`` for
-    F(2x2,3x3) (conv2d_wino.hip) and ``u4`` for F(4x4,3x3) (conv2d_wino4.hip)."""
-    __slots__ = ("u2", "u4", "cin", "cout")
+    F(2x2,3x3) (conv2d_wino.hip), ``u4`` for F(4x4,3x3) (conv2d_wino4.hip) in 32-channel
+    blocks and ``u4w`` in the wide shape's 64-channel blocks (None unless Cout % 64 == 0)."""
+    __slots__ = ("u2", "u4", "u4w", "cin", "cout")
 
-    def __init__(self, u2: torch.Tensor, u4: torch.Tensor, cin: int, cout: int):
-        self.u2, self.u4, self.cin, self.cout = u2, u4, cin, cout
+    def __init__(self, u2: torch.Tensor, u4: torch.Tensor, cin: int, cout: int, u4w: Optional[torch.Tensor] = None):
+        self.u2, self.u4, self.u4w, self.cin, self.cout = u2, u4, u4w, cin, cout
 
 
 # False keeps every 3x3 conv on the F(2x2,3x3) kernel (set by A/B scripts and tests)
 _WINO4 = True
+# F(4x4) launches on the wide block shape (64 output channels per block, one wave per SIMD)
+# where every problem allows it (Cout % 64; Cout % 128 with a z/r gate)
+W4_WIDE = False
 
 
 def wino_weights(weight: torch.Tensor) -> WinoFilters:
@@ -614,7 +618,11 @@ def wino_weights(weight: torch.Tensor) -> WinoFilters:
     N.call("sa_conv2d_wino_weights", weight.data_ptr(), Cout, Cin, u2.data_ptr(), _stream(weight))
     u4 = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.float32)
     N.call("sa_conv2d_wino4_weights", weight.data_ptr(), Cout, Cin, u4.data_ptr(), _stream(weight))
-    return WinoFilters(u2, u4, Cin, Cout)
+    u4w = None
+    if Cout % 64 == 0 and Cin % 8 == 0:
+        u4w = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.float32)
+        N.call("sa_conv2d_wino4_weights_cb", weight.data_ptr(), Cout, Cin, 64, u4w.data_ptr(), _stream(weight))
+    return WinoFilters(u2, u4, Cin, Cout, u4w)
 
 
 def _wino4_ok(x: torch.Tensor, in_aff=None, in_act=None, out: Optional[torch.Tensor] = None, **_) -> bool:
@@ -640,7 +648,7 @@ _WINO4_MIN_BLOCKS = 384
 
 def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] = None, relu: bool = False,
                   out: Optional[torch.Tensor] = None, in_aff: Optional[Affine] = None, in_act=None,
-                  stats: bool = False, f4: bool = False, out_cout: Optional[int] = None):
+                  stats: bool = False, f4: bool = False, out_cout: Optional[int] = None, wide: bool = False):
     """out_cout: channels of ``out`` when the epilogue writes fewer than Cout there (gate mode 1)."""
     bs = _plane_bs(x, "x")
     if not isinstance(U, WinoFilters):
@@ -657,7 +665,8 @@ def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] 
     parts_fn = N.lib().sa_conv2d_k3_wino4_stat_parts if f4 else N.lib().sa_conv2d_k3_wino_stat_parts
     parts = int(parts_fn(H, W)) if stats else 0
     partial = torch.empty((B * Cout * parts * 2,), device=x.device, dtype=torch.float64) if stats else None
-    prob = N.SaWinoProblem(x.data_ptr(), bs, B, Cin, H, W, (U.u4 if f4 else U.u2).data_ptr(), Cout, _ptr(bias),
+    Uf = (U.u4w if wide else U.u4) if f4 else U.u2
+    prob = N.SaWinoProblem(x.data_ptr(), bs, B, Cin, H, W, Uf.data_ptr(), Cout, _ptr(bias),
                            1 if relu else 0, m, s, t, ps, ACT[in_act], out.data_ptr(), _plane_bs(out, "out"),
                            _ptr(partial))
     # Winograd-domain products actually executed: 36 per 4x4 tile (F4) or 16 per 2x2 tile (F2)
@@ -729,13 +738,15 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     if gated and not ok4:
         raise RuntimeError("conv2d_k3_multi: gate epilogues need the F(4x4,3x3) kernel (gate_f4_ok)")
     f4 = ok4 and (gated or sum(_wino4_blocks(**p) for p in plain) >= _WINO4_MIN_BLOCKS)
-    built = [_wino_problem(**p, f4=f4) for p in plain]
+    wide = (f4 and W4_WIDE and not small_blocks and all(p["U"].u4w is not None for p in plain)
+            and all(p["U"].cout % 128 == 0 for p in problems if p.get("gate") and p["gate"]["mode"] == 1))
+    built = [_wino_problem(**p, f4=f4, wide=wide) for p in plain]
     arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
-    if f4 and (gated or small_blocks):
+    if f4 and (gated or small_blocks or wide):
         gates = (N.SaGateEpilogue * len(built))(*[_gate_epilogue(p) if p.get("gate") else N.SaGateEpilogue()
                                                   for p in problems])
         N.call("sa_conv2d_k3_wino4_multi_gate", len(built), ctypes.addressof(arr), ctypes.addressof(gates),
-               2 if small_blocks else 0, _stream(problems[0]["x"]))
+               3 if wide else 2 if small_blocks else 0, _stream(problems[0]["x"]))
     else:
         N.call("sa_conv2d_k3_wino4_multi" if f4 else "sa_conv2d_k3_wino_multi", len(built), ctypes.addressof(arr),
                _stream(problems[0]["x"]))

@@ -143,11 +143,13 @@ def test_wino4_multi_stats_views(monkeypatch):
     torch.testing.assert_close(yd, F.conv2d(xb, wb, padding=1), atol=2e-5, rtol=1e-4)
 
 
-def test_wino4_gru_gate_epilogues(monkeypatch):
+@pytest.mark.parametrize("wide", [False, True])
+def test_wino4_gru_gate_epilogues(monkeypatch, wide):
     """ConvGRU gates in the F(4x4) epilogue (update.py:16-27) against the reference's expressions
     in torch fp32: mode 1 (convz | convr over cat(h, x) -> z, r*h) on channel views of one
     [h | x | r*h] buffer, beside a plain problem in the same launch; mode 2 (convq's r*h part ->
     the new state, in place on h).  Two levels' shapes (8 x 128 and 16 x 64 blocks)."""
+    monkeypatch.setattr(ops, "W4_WIDE", wide)   # also on the wide block shape (64 channels per block)
     g = torch.Generator(device="cpu").manual_seed(42)
 
     def r(*s):
@@ -204,3 +206,33 @@ def test_wino4_small_block_shape(monkeypatch):
         ref = F.conv2d(x, w, padding=1)
         torch.testing.assert_close(out, ref, atol=1e-4, rtol=1e-4)
         torch.testing.assert_close(mean, ref.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 64, 64, 20, 52), (1, 128, 256, 136, 240), (2, 16, 128, 9, 36),
+                                            (1, 384, 128, 34, 60), (4, 256, 384, 17, 120)])
+def test_wino4_wide_block_shape(monkeypatch, N, Cin, Cout, H, W):
+    """The wide block shape (block_shape 3: 32 tiles x 64 output channels, one wave per SIMD;
+    filters in 64-channel blocks) against torch: bias + ReLU, InstanceNorm statistics, both
+    tile geometries (8 x 64 and 4 x 128 px), a ragged last tile row and column."""
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    monkeypatch.setattr(ops, "W4_WIDE", True)
+    g = torch.Generator(device="cpu").manual_seed(Cin + Cout)
+    x = torch.randn(N, Cin, H, W, generator=g).cuda()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)).cuda()
+    b = torch.randn(Cout, generator=g).cuda()
+    U = ops.wino_weights(w)
+    assert U.u4w is not None
+    ops.WORK = {}
+    try:
+        (out, (mean, rstd)), = ops.conv2d_k3_multi(dict(x=x, U=U, stats=True))
+        (outr,) = ops.conv2d_k3_multi(dict(x=x, U=U, bias=b, relu=True))
+        assert "conv2d_wino4" in ops.WORK
+    finally:
+        ops.WORK = None
+    ref = F.conv2d(x, w, padding=1)
+    scale = max(float(ref.pow(2).mean().sqrt()), 1.0)
+    assert float((out - ref).abs().max()) < 1e-4 * scale and float((out - ref).pow(2).mean().sqrt()) < 1e-5 * scale
+    torch.testing.assert_close(outr, torch.relu(F.conv2d(x, w, b, padding=1)), atol=1e-4 * scale, rtol=1e-4)
+    torch.testing.assert_close(mean, ref.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(rstd, torch.rsqrt(ref.var(dim=(2, 3), unbiased=False) + 1e-5).flatten(),
+                               atol=1e-4, rtol=1e-4)
