@@ -619,7 +619,7 @@ def wino_weights(weight: torch.Tensor) -> WinoFilters:
     u4 = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.float32)
     N.call("sa_conv2d_wino4_weights", weight.data_ptr(), Cout, Cin, u4.data_ptr(), _stream(weight))
     u4w = None
-    if Cout % 64 == 0 and Cin % 8 == 0:
+    if W4_WIDE and Cout % 64 == 0 and Cin % 8 == 0:   # the wide shape's layout only when it may run
         u4w = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.float32)
         N.call("sa_conv2d_wino4_weights_cb", weight.data_ptr(), Cout, Cin, 64, u4w.data_ptr(), _stream(weight))
     return WinoFilters(u2, u4, Cin, Cout, u4w)
