@@ -237,6 +237,7 @@ def main():
     ap.add_argument("--width", type=int, default=960)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-epe", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of hipGraph replay")
     ap.add_argument("--miopen-find", type=int, default=0,
                     help="let MIOpen time its conv algorithms per shape (torch cudnn.benchmark)")
     args = ap.parse_args()
@@ -276,8 +277,18 @@ def main():
         runner = CPUOffloadWrapper(wrap) if tiled["offload"] else wrap
         units, shape = 1, (len(tiles), th // 4, tw // 4)
 
+    eager_runner = runner
+    if tiled is None and not args.no_graph:
+        # the timed steps replay the whole forward from a hipGraph (inputs copied into its static
+        # buffers each step): one host enqueue per forward instead of ~1.4k kernel launches
+        from stereoanywhere_amd.graph import ForwardGraph
+        runner = ForwardGraph(model)
+
     def step():
         return runner(*x, iters=iters, test_mode=True)
+
+    def eager_step():
+        return eager_runner(*x, iters=iters, test_mode=True)
 
     with torch.no_grad():
         for i in range(args.warmup):
@@ -288,7 +299,7 @@ def main():
         # untimed forward
         from stereoanywhere_amd import ops as O
         O.WORK = {}
-        step()
+        eager_step()
         work, O.WORK = O.WORK, None
         torch.cuda.synchronize()
         # timed region: K plain steps -> value.  The per-launch HIP events of the roofline
@@ -302,12 +313,22 @@ def main():
         D.barrier(r)
         elapsed = time.perf_counter() - t0
         log(f"timed {args.steps} steps in {elapsed:.3f} s")
+        # the same steps launched eagerly (no graph), for the record
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        for _ in range(args.steps):
+            out_e = eager_step()
+        torch.cuda.synchronize()
+        elapsed_eager = time.perf_counter() - t3
+        graph_dev = None
+        if runner is not eager_runner:   # the replayed forward is the eager one
+            graph_dev = float((out[0] - out_e[0]).abs().max())
         # one-stream plain steps: the schedule the per-launch times below are measured in
         model.stream_overlap = False
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         for _ in range(args.steps):
-            step()
+            eager_step()
         torch.cuda.synchronize()
         elapsed_1s = time.perf_counter() - t2
         # per-launch times of one kernel at a time: the side streams' overlap (model.py) would
@@ -316,7 +337,7 @@ def main():
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for _ in range(args.steps):
-            step()
+            eager_step()
         torch.cuda.synchronize()
         elapsed_ev = time.perf_counter() - t1
         kt = {k: N.timing_read(k) for k in N.KERNEL_IDS}
@@ -388,7 +409,12 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded value-noise pairs, "
         "seeded random weights; no dataset/checkpoint offline)",
         "config": config, "roofline": roof, "gathered_units": int(allm.shape[0]),
+        "execution": ("hipGraph replay of the whole forward (stereoanywhere_amd.graph.ForwardGraph; inputs "
+                      "copied into its static buffers each step)" if graph_dev is not None else "eager launches"),
+        "eager_ms_per_step": elapsed_eager / args.steps * 1e3,
     }
+    if graph_dev is not None:
+        res["graph_vs_eager_max_abs"] = graph_dev
     if tiled is not None:
         res["tiles_per_s"] = total_units * tiled["tiles"] / elapsed
     if not args.no_epe:

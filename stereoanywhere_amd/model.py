@@ -52,6 +52,15 @@ def _normalize_pair(a: torch.Tensor, b: torch.Tensor, eps: float = 1e-4):
 
 
 
+def _drive(gen):
+    """Run a generator to its end; its return value."""
+    while True:
+        try:
+            next(gen)
+        except StopIteration as e:
+            return e.value
+
+
 @dataclass
 class ScheduleOptions:
     """Launch-schedule choices of the MI355X forward.  Every combination computes the same
@@ -76,6 +85,14 @@ class ScheduleOptions:
     small_launches: frozenset = field(default_factory=frozenset)
     # the encoders' 7x7 stems and stride-2 convs on the direct fp32-MFMA kernel (False: MIOpen)
     direct_conv: bool = True
+    # the GRU loop's batch in this many parts, each on a HIP stream of its own: one part's launch
+    # tails and small kernels overlap the other's convs (1: one stream, the whole batch per
+    # launch).  B = 4 at 544x960: 82.2 ms/step with 1 part, 79.5 with 2, 86-91 with 3-4 (eager);
+    # replayed from a hipGraph (graph.ForwardGraph) 82.3 and 77.5-77.7 (scripts/ab_graph.py)
+    loop_parts: int = 2
+    # ... part i > 0 starting on the GPU after part i - 1's first half iteration (False: all at
+    # once; the same time from a graph, faster eager)
+    loop_offset: bool = False
 
 
 class StereoAnywhere(nn.Module):
@@ -292,7 +309,63 @@ class StereoAnywhere(nn.Module):
                                   _shape=(B, H4, W4, W4))
         del mono_rows, vol_d, vol_c
 
-        return self._iterate(dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4)
+        parts = min(self.opts.loop_parts, B) if self.stream_overlap else 1
+        if parts <= 1:
+            return _drive(self._iterate(dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4))
+        return self._iterate_parts(parts, dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4)
+
+    def _iterate_parts(self, parts, dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4):
+        """The GRU loop over batch parts (pairs are independent), each on its own stream; the
+        host enqueues them in turn, half an iteration at a time, and part i > 0 starts on the
+        GPU once part i - 1 has finished its first half iteration.  The main stream waits for
+        every part; the inputs stay referenced until then."""
+        dev = coords_x.device
+        main = torch.cuda.current_stream(dev)
+        bounds = [(B * i // parts, B * (i + 1) // parts) for i in range(parts)]
+        rows = H4 * W4
+
+        def blk(b, lo, hi):
+            return HipCorrBlock1D(None, b.num_levels, b.radius, _pyramid=b.pyramid[lo * rows:hi * rows],
+                                  _shape=(hi - lo, H4, W4, W4))
+        streams, gens = [], []
+        for i, (lo, hi) in enumerate(bounds):
+            st = self._loop_stream(dev, i)
+            st.wait_stream(main)
+            streams.append(st)
+            with torch.cuda.stream(st):
+                gens.append(self._iterate(dw, [h[lo:hi] for h in hid], [c[lo:hi] for c in ctx],
+                                          blk(stereo_blk, lo, hi), blk(mono_blk, lo, hi), coords_x[lo:hi], iters,
+                                          hi - lo, H4, W4))
+        results = [None] * parts
+        first = [None] * parts   # event after each part's first half iteration
+        done = [False] * parts
+        while not all(done):
+            for i in range(parts):
+                if done[i] or (i > 0 and first[i - 1] is None):
+                    continue
+                st = streams[i]
+                with torch.cuda.stream(st):
+                    if first[i] is None and i > 0 and self.opts.loop_offset:   # before part i's first launch
+                        st.wait_event(first[i - 1])
+                    try:
+                        next(gens[i])
+                    except StopIteration as e:
+                        results[i], done[i] = e.value, True
+                        continue
+                    if first[i] is None:
+                        first[i] = torch.cuda.Event()
+                        first[i].record(st)
+        for st in streams:
+            main.wait_stream(st)
+        return torch.cat([r[0] for r in results], 0), None
+
+    def _loop_stream(self, dev, i: int):
+        ls = getattr(self, "_loops", None)
+        if ls is None or ls[0].device != dev:
+            ls = self._loops = []
+        while len(ls) <= i:
+            ls.append(torch.cuda.Stream(dev))
+        return ls[i]
 
     def _context(self, dw, mde2):
         """Context encoder (eval BatchNorm folded) -> tanh hidden states and the context_zqr
@@ -358,6 +431,9 @@ class StereoAnywhere(nn.Module):
         return vol_d, vol_c, sm2, mirror, coords_x
 
     def _iterate(self, dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4):
+        """The GRU loop as a generator: it yields twice per iteration (after gru16 and at the
+        end) so that batch parts on separate streams can be enqueued in turn (_iterate_parts);
+        its return value is (flow_up, None)."""
         ub = self.update_block
         enc = ub.encoder
         dev = coords_x.device
@@ -479,6 +555,7 @@ class StereoAnywhere(nn.Module):
             res = conv_group(*qp, dict(x=motin, U=dw["U_mot"], bias=dw["mot_b"], relu=True, out=x08[:, :128]),
                              name="q16")
             q_finish(1, "16", xc16, res[:len(qp)])
+            yield   # half an iteration (the batch-parts schedule interleaves here)
             ops.flow_update(coords_x, None, None, x08[:, 126:128])
             ops.interp(h16, x08[:, 128:])
             # gru08's x/h convs (+ gru32's of the next iteration), then the r*h convs
@@ -508,4 +585,5 @@ class StereoAnywhere(nn.Module):
                 m1 = ops.conv2d_k3(h08, dw["U_mask"], ub.mask[0].bias, relu=True)
                 mask = F.conv2d(m1, ub.mask[2].weight, ub.mask[2].bias).mul_(0.25)
                 flow_up = ops.convex_upsample(flow[:, 0:1].contiguous(), mask, 2 ** self.args.n_downsample)
+            yield
         return flow_up, None

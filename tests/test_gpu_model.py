@@ -128,6 +128,29 @@ def test_side_streams_match_one_stream(model):
         assert epe(o, ref) < 1e-5
 
 
+@pytest.mark.parametrize("parts", [2, 3])
+def test_loop_parts_match_one_stream(model, parts):
+    """The GRU loop over batch parts on separate streams (ScheduleOptions.loop_parts; a ragged
+    split at B = 3 with 2 parts) gives the one-part result; back-to-back forwards without a
+    host sync."""
+    import dataclasses
+    pb = synth.synthetic_batch(3, 128, 256, 48.0, seed0=13)
+    x = [torch.from_numpy(pb[k]).cuda() for k in ("left", "right", "mono_left", "mono_right")]
+    old = model.opts
+    try:
+        with torch.no_grad():
+            model.opts = dataclasses.replace(old, loop_parts=1)
+            ref = -model(*x, iters=6, test_mode=True)[0][:, 0].cpu().numpy()
+            model.opts = dataclasses.replace(old, loop_parts=parts)
+            outs = [model(*x, iters=6, test_mode=True)[0] for _ in range(3)]
+            outs = [-o[:, 0].cpu().numpy() for o in outs]
+    finally:
+        model.opts = old
+    for o in outs:
+        assert o.shape == ref.shape and np.isfinite(o).all()
+        assert epe(o, ref) < 1e-5
+
+
 @pytest.mark.parametrize("change", [dict(group_convs=False), dict(fuse_gates=False), dict(fuse_out=False),
                                     dict(mono_stream=False), dict(cnet_side=1), dict(cnet_side=0),
                                     dict(small_launches=frozenset({"q16", "q08", "zr16", "zr08", "pro32"})),
@@ -154,3 +177,19 @@ def test_schedule_options_vs_reference(change):
     e = epe(disp, fix["disparity"])
     print(change, "wino4" if wino4 else "no wino4", "EPE", e)
     assert e < 1e-3
+
+
+def test_forward_graph_replays_the_forward(model):
+    """graph.ForwardGraph (hipGraph capture of the whole forward, side streams and batch parts
+    included) returns the eager forward's disparity for fresh inputs on every replay, and
+    re-captures when the iteration count changes."""
+    from stereoanywhere_amd.graph import ForwardGraph
+    fg = ForwardGraph(model)
+    for seed, iters in ((21, 4), (22, 4), (23, 3)):
+        pb = synth.synthetic_batch(2, 128, 256, 48.0, seed0=seed)
+        x = [torch.from_numpy(pb[k]).cuda() for k in ("left", "right", "mono_left", "mono_right")]
+        with torch.no_grad():
+            ref = model(*x, iters=iters, test_mode=True)[0]
+            got = fg(*x, iters=iters)[0]
+        assert got.shape == ref.shape
+        assert float((got - ref).abs().max()) < 1e-4
