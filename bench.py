@@ -238,6 +238,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-epe", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of hipGraph replay")
+    ap.add_argument("--one-stream", action="store_true",
+                    help="every step eager on one stream, the whole batch per launch (the schedule of the "
+                         "instrumented steps: rocprof per-launch times and PMC bytes comparable with the live ones)")
     ap.add_argument("--miopen-find", type=int, default=0,
                     help="let MIOpen time its conv algorithms per shape (torch cudnn.benchmark)")
     args = ap.parse_args()
@@ -278,7 +281,9 @@ def main():
         units, shape = 1, (len(tiles), th // 4, tw // 4)
 
     eager_runner = runner
-    if tiled is None and not args.no_graph:
+    if args.one_stream:
+        model.stream_overlap = False
+    if tiled is None and not args.no_graph and not args.one_stream:
         # the timed steps replay the whole forward from a hipGraph (inputs copied into its static
         # buffers each step): one host enqueue per forward instead of ~1.4k kernel launches
         from stereoanywhere_amd.graph import ForwardGraph
@@ -342,7 +347,7 @@ def main():
         elapsed_ev = time.perf_counter() - t1
         kt = {k: N.timing_read(k) for k in N.KERNEL_IDS}
         N.timing_enable(False)
-        model.stream_overlap = True
+        model.stream_overlap = not args.one_stream
         log(f"instrumented {args.steps} steps in {elapsed_ev:.3f} s")
         elapsed = D.max_over_ranks(elapsed, r, device)
         # per-unit metrics gathered once, after the timed region (the only collective)

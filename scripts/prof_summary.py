@@ -18,7 +18,7 @@ def dur(r):
 
 
 look = [i for i, r in enumerate(fw) if "lookup" in r["Kernel_Name"]][0]
-mv = [i for i, r in enumerate(fw) if "masked_volume" in r["Kernel_Name"]][0]
+mv = [i for i, r in enumerate(fw) if "bin_records" in r["Kernel_Name"] or "masked_volume" in r["Kernel_Name"]][0]
 span = (int(fw[-1]["End_Timestamp"]) - int(fw[0]["Start_Timestamp"])) / 1e6
 print(f"forward span {span:.2f} ms, busy {sum(map(dur, fw)) / 1e6:.2f} ms, {len(fw)} kernels")
 for name, seg in (("encoders", fw[:mv]), ("mono volume + hourglass + alignment", fw[mv:look]),

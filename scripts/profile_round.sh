@@ -1,10 +1,10 @@
 #!/bin/bash
 # Full measurement pass on the GPU box (outputs under gpurun_out/prof):
 #   bench      the default bench line (value, roofline, cpu baseline)
-#   trace      rocprofv3 --kernel-trace --stats over a short bench run
-#   trace1s    the same with every step on one stream (SA_MONO_STREAM=0): per-launch times
-#              without the side streams' overlap, as bench.py's instrumented steps
-#   fetch/write  rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs (HBM bytes)
+#   trace      rocprofv3 --kernel-trace --stats over a short bench run (hipGraph replays)
+#   trace1s    the same with every step eager on one stream, the whole batch per launch
+#              (bench.py --one-stream: the instrumented steps' schedule, per-launch times comparable)
+#   fetch/write  rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs (HBM bytes, --one-stream)
 # Each step under its own limit; a fault or time-out ends the script (gpu_steps.sh).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 R=$(pwd)
@@ -13,8 +13,8 @@ SHORT="python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-epe"
 exec_steps=(
   "bench:420:python3 $R/bench.py > $R/gpurun_out/prof/bench.log 2>&1; tail -n 1 $R/gpurun_out/prof/bench.log > $R/gpurun_out/prof/bench.json"
   "trace:300:cd /tmp && rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof/trace -o run --output-format csv -- $SHORT"
-  "trace1s:300:cd /tmp && SA_MONO_STREAM=0 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof/trace1s -o run --output-format csv -- $SHORT"
-  "fetch:300:cd /tmp && rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/prof/fetch -o run --output-format csv -- $SHORT"
-  "write:300:cd /tmp && rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/prof/write -o run --output-format csv -- $SHORT"
+  "trace1s:300:cd /tmp && rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof/trace1s -o run --output-format csv -- $SHORT --one-stream"
+  "fetch:300:cd /tmp && rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/prof/fetch -o run --output-format csv -- $SHORT --one-stream"
+  "write:300:cd /tmp && rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/prof/write -o run --output-format csv -- $SHORT --one-stream"
 )
 bash "$R/scripts/gpu_steps.sh" "${exec_steps[@]}"
