@@ -388,9 +388,12 @@ def main():
                  "note": "achieved = algorithmic amount per launch / mean live HIP-event launch time, "
                          "events recorded around every launch over K steps run right after the K "
                          "plain timed steps (the events cost ~6 % of a step), in the one-stream order "
-                         "(model.stream_overlap = False; its plain time is one_stream_ms_per_step; the "
-                         "headline steps overlap the mono branch and the context encoder with the "
-                         "feature encoder on side streams); "
+                         "(model.stream_overlap = False, the whole batch per launch; its plain time is "
+                         "one_stream_ms_per_step; the headline steps overlap the mono branch and the "
+                         "context encoder with the feature encoder on side streams and run the GRU loop "
+                         "as two batch parts on two streams, replayed from a hipGraph); "
+                         "conv3d_fused counts the direct 3x3x3 convolutions' flops (its stride-1 "
+                         "convs execute half of them: F(4,3) Winograd along D); "
                          "fp32 FMA peak 157.3 TF/s is the same for MFMA (v_mfma_f32_*_f32) and VALU; "
                          "conv2d_wino / conv2d_wino4 count the Winograd-domain products they execute "
                          "(16/36 resp. 36/144 of the direct convolution's), so their direct-equivalent "
