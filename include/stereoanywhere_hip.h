@@ -314,8 +314,10 @@ int sa_conv2d_k3_wino_multi(int nprob, const SaWinoProblem *probs, void *stream)
  * output instead of 4).  sa_conv2d_wino4_weights transforms [Cout][Cin][3][3] (Cin % 8 == 0,
  * Cout % 32 == 0) once into U4, 36*Cin*Cout floats laid out [Cout/32][Cin/8][36][2][4][32]
  * (16-byte aligned).  sa_conv2d_k3_wino4_multi takes SaWinoProblem with U = U4 and needs
- * W % 4 == 0, 16-byte aligned input planes (in, in_bs % 4 == 0) and no input transform
- * (in_m / in_s / in_t NULL, in_act 0); bias, ReLU and the InstanceNorm partials
+ * W % 4 == 0 and 16-byte aligned input planes (in, in_bs % 4 == 0); an input transform
+ * (in_m / in_s / in_t / in_pstride, in_act 0 or 1 = ReLU, as sa_conv2d_k3_wino_ex) needs
+ * Cin <= 256 (block_shape 0) or 512 (2), no gate epilogue in the launch and not the wide
+ * shape; bias, ReLU and the InstanceNorm partials
  * ([N*Cout][parts][2], parts = sa_conv2d_k3_wino4_stat_parts(H, W)) as sa_conv2d_k3_wino_ex. */
 int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, float *U4, void *stream);
 /* U4 for the wide block shape (block_shape 3 of sa_conv2d_k3_wino4_multi_gate: 64 output

@@ -495,6 +495,7 @@ int wino_prob(const SaWinoProblem &q, WinoProb &P, bool &aff) {
   aff = q.in_m || q.in_s || q.in_t || q.in_act;
   SA_REQUIRE(!aff || q.Cin <= MAX_CIN_AFFINE, "sa_conv2d_k3_wino: input transform needs Cin <= %d", MAX_CIN_AFFINE);
   SA_REQUIRE(q.in_pstride == 0 || q.in_pstride == q.Cin, "sa_conv2d_k3_wino: in_pstride must be 0 or Cin");
+  SA_REQUIRE(q.in_act == 0 || q.in_act == 1, "sa_conv2d_k3_wino: input activation none or ReLU (got %d)", q.in_act);
   const int cg = q.Cout % 64 == 0 ? 2 : 1;
   const int tiles_w = (q.W + OTW - 1) / OTW, tiles_h = (q.H + OTH - 1) / OTH;
   P = WinoProb{q.in, q.in_bs, q.Cin, q.H, q.W, q.U, q.Cout, q.bias, q.relu, q.out, q.out_bs, tiles_w,

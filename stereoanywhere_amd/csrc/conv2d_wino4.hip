@@ -78,6 +78,8 @@ struct W4Cfg {
   static constexpr int PPART = (PDMA > UPW ? PDMA : UPW) > 6 ? 3 : 2;   // DMA pieces per part
   static_assert(PDMA <= 3 * PPART && UPW <= 3 * PPART, "three DMA parts");
   static_assert(OPP % 32 == 4, "conflict-free staging");
+  // input (scale, shift) table of an input-transform launch in the LDS left over
+  static constexpr int AFF_MAX = (160 * 1024 - SMEM * 4) / 8 > 512 ? 512 : (160 * 1024 - SMEM * 4) / 8;
 };
 using W4Big = W4Cfg<8, 8>;
 using W4Small = W4Cfg<4, 4>;
@@ -103,6 +105,9 @@ struct W4Prob {
   int ltw;                 // log2 of Winograd tiles per block row: 4 (16 x 64 px) or 5 (8 x 128 px)
   int tiles_w, tiles_hw, co_blocks;
   double *partial;
+  // input transform (the producer's norm + ReLU, SaWinoProblem in_m / in_s / in_t / in_act)
+  const float *in_m, *in_s, *in_t;
+  int in_pstride, in_act;
 };
 constexpr int MAX_PROB = 8;
 // GRU gate epilogues (SaGateEpilogue in the header), read by the store loop only
@@ -177,8 +182,9 @@ __device__ __forceinline__ void bt6h(const float x0, const float x1, const float
 __device__ unsigned long long g_w4_clock[65536][10];   // + [8] chunk 0 issued, [9] last wave's start
 #endif
 
-template <class C, int HF, int LTW, bool GATED>
-__device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, const unsigned wid, float *smem) {
+template <class C, int HF, int LTW, bool GATED, bool AFF>
+__device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, const unsigned wid, float *smem,
+                                        float2 *atab) {
   constexpr int NWAVE = C::NW, NTHR = C::NTHR, KC = C::KC, JPC = C::JPC, NT = C::NT, PDMA = C::PDMA,
                 UDMA = C::UDMA, UPW = C::UPW, UBUF = C::UBUF, BUF = C::BUF, PBUF = C::PBUF, OPP = C::OPP,
                 CO = C::CO, CG = C::CG, SB = C::SB;
@@ -222,6 +228,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   }
   const int npi = (KC * PS + 63) >> 6;
   int po[PDMA];
+  int pc[PDMA];   // input transform: the group's channel in the chunk (-1: padding or idle lane)
 #pragma unroll
   for (int j = 0; j < PDMA; ++j) {
     const int s = (wv + NWAVE * j) * 64 + lane;
@@ -229,6 +236,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
     const int y = y0 - 1 + r, x = x0 - 4 + 4 * g;
     const bool ok = s < KC * PS && y >= 0 && y < H && x >= 0 && x < W;
     po[j] = ok ? (ci * hw + y * W + x) * 4 : 0x7ffffff0;   // out of range: the load returns 0
+    pc[j] = ok && wv + NWAVE * j < (KC * PS + 63) / 64 ? ci : -1;
   }
   // the chunk's DMAs in three parts (part -1: all at once), spread over the first job's three
   // column phases (each piece costs tens of issue cycles; clustered after the barrier they
@@ -278,13 +286,43 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
 
   if (SA_W4_PRIO && HF == 1) __builtin_amdgcn_s_setprio(1);   // static priority for waves 4-7
   if (SA_W4_DIAG != 4) issue_p0();
+  // Input transform: v -> act(v * scale + shift), scale = s, shift = t - m * s per channel
+  // (in_pstride 0) or per (image, channel) (in_pstride = Cin).  Each lane transforms the
+  // 4-float groups its own DMAs brought in (in the LDS, after its own vmcnt wait, before the
+  // chunk's barrier); padding groups stay zero, as in the reference (padding of the activated
+  // input).  One read-modify-write per staged float, against the standalone pass's HBM round
+  // trip of the whole input.
+  const float act_floor = P.in_act ? 0.0f : -INFINITY;
+  if constexpr (AFF) {
+    for (int c = tid; c < Cin; c += NTHR) {
+      const int pi = n * P.in_pstride + c;
+      const float m0 = P.in_m ? P.in_m[pi] : 0.0f, sc = P.in_s ? P.in_s[pi] : 1.0f, t0 = P.in_t ? P.in_t[pi] : 0.0f;
+      atab[c] = make_float2(sc, t0 - m0 * sc);
+    }
+    __syncthreads();
+  }
 #ifdef SA_W4_CLOCK
   if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][8] = __builtin_amdgcn_s_memtime();
 #endif
 #pragma unroll 1
   for (int kc = 0; kc < nchunks; ++kc) {
     const int cur = kc & 1;
-    if (SA_W4_DIAG < 3) __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
+    if constexpr (AFF) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this lane's DMAs of chunk kc landed
+      float *pbuf = smem + cur * BUF;
+#pragma unroll
+      for (int j = 0; j < PDMA; ++j) {
+        if (pc[j] >= 0) {
+          f32x4 *q = reinterpret_cast<f32x4 *>(pbuf + ((wv + NWAVE * j) * 64 + lane) * 4);
+          const float2 ab = atab[kc * KC + pc[j]];
+          f32x4 v = *q;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] * ab.x + ab.y, act_floor);
+          *q = v;
+        }
+      }
+    }
+    if (SA_W4_DIAG < 3 || AFF) __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
 #ifdef SA_W4_CLOCK
     if (kc == 0 && HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][4] = __builtin_amdgcn_s_memtime();
 #endif
@@ -535,7 +573,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   }
 }
 
-template <class C, bool GATED>
+template <class C, bool GATED, bool AFF = false>
 __global__ __launch_bounds__(C::NTHR, C::NW == 8 || C::CO == 64 ? 1 : 2) void wino_f4k3_kernel(const W4Launch L) {
   // problem of the block from its raw id (ranges padded to multiples of 8: every XCD gets an
   // equal share of each problem), then the L2-locality remap within it (conv2d_wino.hip)
@@ -550,6 +588,7 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 || C::CO == 64 ? 1 : 2) void wi
   const unsigned base = pi ? L.end[pi - 1] : 0u, nb = L.nblk[pi];
   if (g - base >= nb) return;
   __shared__ __attribute__((aligned(16))) float smem[C::SMEM];
+  __shared__ float2 atab[AFF ? C::AFF_MAX : 1];
 #ifdef SA_W4_CLOCK
   unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == C::NTHR - 64 && blockIdx.x < 65536) g_w4_clock[blockIdx.x][9] = t0;
@@ -557,11 +596,11 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 || C::CO == 64 ? 1 : 2) void wi
   // the first half of the waves takes point columns 0-2, the second half 3-5 (wave-uniform)
   const unsigned wid = sa::xcd_remap(g - base, nb);
   if (threadIdx.x < C::NTHR / 2) {
-    if (P.ltw == 4) w4_body<C, 0, 4, GATED>(P, GATED ? &L.gate[pi] : nullptr, wid, smem);
-    else w4_body<C, 0, 5, GATED>(P, GATED ? &L.gate[pi] : nullptr, wid, smem);
+    if (P.ltw == 4) w4_body<C, 0, 4, GATED, AFF>(P, GATED ? &L.gate[pi] : nullptr, wid, smem, atab);
+    else w4_body<C, 0, 5, GATED, AFF>(P, GATED ? &L.gate[pi] : nullptr, wid, smem, atab);
   } else {
-    if (P.ltw == 4) w4_body<C, 1, 4, GATED>(P, GATED ? &L.gate[pi] : nullptr, wid, smem);
-    else w4_body<C, 1, 5, GATED>(P, GATED ? &L.gate[pi] : nullptr, wid, smem);
+    if (P.ltw == 4) w4_body<C, 1, 4, GATED, AFF>(P, GATED ? &L.gate[pi] : nullptr, wid, smem, atab);
+    else w4_body<C, 1, 5, GATED, AFF>(P, GATED ? &L.gate[pi] : nullptr, wid, smem, atab);
   }
 #ifdef SA_W4_CLOCK
   if (threadIdx.x == 0 && g < 65536) {
@@ -654,7 +693,7 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
   const int CO = wide ? 64 : 32;
   W4Launch L{};
   long total = 0;
-  bool gated = false;
+  bool gated = false, aff = false;
   for (int i = 0; i < nprob; ++i) {
     const SaWinoProblem &q = probs[i];
     SA_REQUIRE(q.in && q.U && q.out && q.N > 0 && q.H > 0 && q.W > 0, "sa_conv2d_k3_wino4: bad arguments");
@@ -664,13 +703,20 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
                    (reinterpret_cast<uintptr_t>(q.out) & 15) == 0 && q.out_bs % 4 == 0 &&
                    (reinterpret_cast<uintptr_t>(q.U) & 15) == 0,
                "sa_conv2d_k3_wino4: needs W %% 4 == 0 and 16-byte aligned input / output planes and filters");
-    SA_REQUIRE(!q.in_m && !q.in_s && !q.in_t && !q.in_act, "sa_conv2d_k3_wino4: no input transform");
+    const bool qaff = q.in_m || q.in_s || q.in_t || q.in_act;
+    SA_REQUIRE(q.in_act == 0 || q.in_act == 1, "sa_conv2d_k3_wino4: input activation none or ReLU (got %d)", q.in_act);
+    SA_REQUIRE(q.in_pstride == 0 || q.in_pstride == q.Cin, "sa_conv2d_k3_wino4: in_pstride must be 0 or Cin");
+    SA_REQUIRE(!qaff || (!wide && q.Cin <= (small ? W4Small::AFF_MAX : W4Big::AFF_MAX)),
+               "sa_conv2d_k3_wino4: an input transform needs the 8- or 4-wave shape and Cin <= %d",
+               small ? W4Small::AFF_MAX : W4Big::AFF_MAX);
+    aff = aff || qaff;
     SA_REQUIRE((long)q.Cin * q.H * q.W * 4 < (1L << 31) - 64 && 36L * q.Cin * q.Cout * 4 < (1L << 31),
                "sa_conv2d_k3_wino4: an image or the filter bank exceeds the 2 GB buffer-descriptor range");
     const int ltw = w4_ltw(q.H, q.W), bw = 4 << ltw, bh = 4 * (nt >> ltw);
     const int tiles_w = (q.W + bw - 1) / bw, tiles_h = (q.H + bh - 1) / bh;
     L.p[i] = W4Prob{q.in, q.in_bs, q.Cin, q.H, q.W, q.U, q.Cout, q.bias, q.relu, q.out, q.out_bs,
-                    ltw, tiles_w, tiles_w * tiles_h, q.Cout / CO, q.stats_partial};
+                    ltw, tiles_w, tiles_w * tiles_h, q.Cout / CO, q.stats_partial,
+                    q.in_m, q.in_s, q.in_t, q.in_pstride, q.in_act};
     L.gate[i] = W4Gate{};
     if (gates && gates[i].mode != 0) {
       const SaGateEpilogue &e = gates[i];
@@ -699,9 +745,14 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
     L.nblk[i] = 0;
   }
   L.nprob = nprob;
+  SA_REQUIRE(!(aff && gated), "sa_conv2d_k3_wino4: an input transform and a gate epilogue in one launch");
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV2D_W4, s);
-  if (small)
+  if (aff && small)
+    wino_f4k3_kernel<W4Small, false, true><<<(unsigned)total, W4Small::NTHR, 0, s>>>(L);
+  else if (aff)
+    wino_f4k3_kernel<W4Big, false, true><<<(unsigned)total, W4Big::NTHR, 0, s>>>(L);
+  else if (small)
     gated ? wino_f4k3_kernel<W4Small, true><<<(unsigned)total, W4Small::NTHR, 0, s>>>(L)
           : wino_f4k3_kernel<W4Small, false><<<(unsigned)total, W4Small::NTHR, 0, s>>>(L);
   else if (wide)

@@ -136,13 +136,9 @@ class _Finisher:
 
 def _conv_k3(x: torch.Tensor, conv: nn.Conv2d, fin: _Finisher, in_aff=None):
     """Winograd conv of a qualifying 3x3 layer -> (raw out, IN stats or None); with in_aff the
-    producer's norm + ReLU is applied while x is loaded (F(2x2) kernel), or, where the faster
-    F(4x4) kernel takes the conv, by one norm_act pass over x (in place: x is the producer's
-    raw output, read by nothing else) before it."""
+    producer's norm + ReLU is applied while x is loaded (both Winograd kernels), so the
+    normalised activation is never written."""
     U = _WINO[conv.weight.data_ptr()]
-    if in_aff is not None and ops.wino4_applies(x, U):
-        x = ops.norm_act(x, in_aff, act_in="relu", out=x)
-        in_aff = None
     r = ops.conv2d_k3(x, U, in_aff=in_aff, in_act="relu" if in_aff is not None else None, stats=fin.instance)
     return r if fin.instance else (r, None)
 
@@ -194,9 +190,6 @@ def residual_blocks_grouped(blks, names, xs, fin: _Finisher) -> List[torch.Tenso
 
     def stage(convs, inputs, affs):
         Us = [_WINO[c.weight.data_ptr()] for c in convs]
-        if affs[0] is not None and ops.wino4_applies(inputs[0], Us[0], *zip(inputs[1:], Us[1:])):
-            inputs = [ops.norm_act(x, a, act_in="relu", out=x) for x, a in zip(inputs, affs)]
-            affs = [None] * len(affs)
         res = ops.conv2d_k3_multi(*[dict(x=x, U=U, in_aff=a, in_act="relu" if a is not None else None,
                                          stats=fin.instance) for x, U, a in zip(inputs, Us, affs)])
         return [r if fin.instance else (r, None) for r in res]

@@ -625,9 +625,17 @@ def wino_weights(weight: torch.Tensor) -> WinoFilters:
     return WinoFilters(u2, u4, Cin, Cout, u4w)
 
 
+# largest Cin of an F(4x4,3x3) launch with an input transform (its (scale, shift) table fills the
+# 8-wave block's spare LDS)
+_WINO4_AFF_CIN = 256
+
+
 def _wino4_ok(x: torch.Tensor, in_aff=None, in_act=None, out: Optional[torch.Tensor] = None, **_) -> bool:
-    """F(4x4,3x3) kernel preconditions: no input transform, W % 4 == 0, 16-byte aligned planes."""
-    return (in_aff is None and in_act is None and x.shape[3] % 4 == 0 and x.data_ptr() % 16 == 0
+    """F(4x4,3x3) kernel preconditions: W % 4 == 0, 16-byte aligned planes; an input transform
+    (the producer's norm, ReLU or none) for Cin <= _WINO4_AFF_CIN."""
+    if (in_aff is not None or in_act is not None) and (x.shape[1] > _WINO4_AFF_CIN or ACT[in_act] > 1):
+        return False
+    return (x.shape[3] % 4 == 0 and x.data_ptr() % 16 == 0
             and x.stride(0) % 4 == 0 and (out is None or (out.data_ptr() % 16 == 0 and out.stride(0) % 4 == 0)))
 
 
@@ -738,7 +746,10 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     if gated and not ok4:
         raise RuntimeError("conv2d_k3_multi: gate epilogues need the F(4x4,3x3) kernel (gate_f4_ok)")
     f4 = ok4 and (gated or sum(_wino4_blocks(**p) for p in plain) >= _WINO4_MIN_BLOCKS)
-    wide = (f4 and W4_WIDE and not small_blocks and all(p["U"].u4w is not None for p in plain)
+    aff = any(p.get("in_aff") is not None or p.get("in_act") is not None for p in plain)
+    if gated and aff:
+        raise RuntimeError("conv2d_k3_multi: an input transform and a gate epilogue in one launch")
+    wide = (f4 and W4_WIDE and not small_blocks and not aff and all(p["U"].u4w is not None for p in plain)
             and all(p["U"].cout % 128 == 0 for p in problems if p.get("gate") and p["gate"]["mode"] == 1))
     built = [_wino_problem(**p, f4=f4, wide=wide) for p in plain]
     arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])

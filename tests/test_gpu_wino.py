@@ -111,6 +111,61 @@ def test_wino4_matches_conv2d(monkeypatch, N, Cin, Cout, H, W):
         assert err_max < 1e-4 * scale and err_rms < 1e-5 * scale, (err_max, err_rms)
 
 
+@pytest.mark.parametrize("small", [False, True])
+def test_wino4_input_transform(monkeypatch, small):
+    """The producer's norm + activation applied on load by the F(4x4) kernel (the LDS pass over
+    each staged chunk): per-(image, channel) InstanceNorm + ReLU with output statistics on a
+    channel-slice input, per-channel BatchNorm + ReLU, affine without activation, a problem
+    without a transform sharing the launch; padding stays zero (padding of the activated
+    input, as in the reference), checked on the borders of 8 x 128 and 16 x 64 blocks."""
+    from stereoanywhere_amd import encoders
+    g = torch.Generator(device="cpu").manual_seed(51)
+
+    def r(*s):
+        return torch.randn(*s, generator=g).cuda()
+    xa = r(2, 96, 37, 132) * 2 + 0.7           # channel slice [16, 80) of it
+    xb, xc = r(3, 32, 20, 52) + 0.3, r(1, 64, 9, 36)
+    wa, wb, wc = r(64, 64, 3, 3) / 24, r(96, 32, 3, 3) / 17, r(32, 64, 3, 3) / 24
+    mean, rstd = ops.plane_stats(xa[:, 16:80])
+    bn = torch.nn.BatchNorm2d(32).cuda().eval()
+    with torch.no_grad():
+        bn.running_mean.copy_(r(32))
+        bn.running_var.copy_(r(32).abs() + 0.5)
+        bn.weight.copy_(r(32))
+        bn.bias.copy_(r(32))
+    aff_b = encoders.bn_affine(bn, None)
+    monkeypatch.setattr(ops, "_WINO4", True)
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    ops.WORK = {}
+    try:
+        (ya, (ma, ra)), yb, yc = ops.conv2d_k3_multi(
+            dict(x=xa[:, 16:80], U=ops.wino_weights(wa), in_aff=ops.Affine(mean, rstd, None, per_plane=True),
+                 in_act="relu", stats=True),
+            dict(x=xb, U=ops.wino_weights(wb), in_aff=aff_b, in_act="relu"),
+            dict(x=xc, U=ops.wino_weights(wc)), small_blocks=small)
+        work = dict(ops.WORK)
+    finally:
+        ops.WORK = None
+    assert "conv2d_wino4" in work and "conv2d_wino" not in work
+    with torch.no_grad():
+        ref_a = F.conv2d(torch.relu(F.instance_norm(xa[:, 16:80])), wa, padding=1)
+        ref_b = F.conv2d(torch.relu(bn(xb)), wb, padding=1)
+    torch.testing.assert_close(ya, ref_a, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(ma, ref_a.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(ra, torch.rsqrt(ref_a.var(dim=(2, 3), unbiased=False) + 1e-5).flatten(),
+                               atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(yb, ref_b, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(yc, F.conv2d(xc, wc, padding=1), atol=1e-4, rtol=1e-4)
+    # affine without activation: negative inputs pass through
+    s, t = r(64).abs() + 0.5, r(64)
+    (yd,), _ = _run(monkeypatch, True, dict(x=xc, U=ops.wino_weights(wc), in_aff=ops.Affine(None, s, t)))
+    torch.testing.assert_close(yd, F.conv2d(xc * s[:, None, None] + t[:, None, None], wc, padding=1),
+                               atol=1e-4, rtol=1e-4)
+    # tanh on load is not built: the launch falls back to F(2x2)'s check, which rejects it
+    with pytest.raises(RuntimeError):
+        ops.conv2d_k3(xc, ops.wino_weights(wc), in_aff=ops.Affine(None, s, t), in_act="tanh")
+
+
 def test_wino4_multi_stats_views(monkeypatch):
     """Three convolutions of different geometries in one F(4x4) launch (8 x 128 and 16 x 64
     blocks), a channel-slice input and output, InstanceNorm statistics; an ineligible problem
