@@ -375,7 +375,8 @@ int sa_conv_direct(const float *in, long in_bs, int N, int Cin, int H, int W, in
  * sa_plane_stats: InstanceNorm2d statistics (biased variance, eps) of each (b, c) plane of
  *   x [B,C,hw] (batch stride x_bs) -> mean, rstd [B*C].
  * sa_norm_act: out = act_out(act_in((x - m) * s + t) + skip_term), skip_term =
- *   (skip - skip_m) * skip_s + skip_t (any of the three NULL = 0 / 1 / 0) or 0 without skip;
+ *   act_skip((skip - skip_m) * skip_s + skip_t) (any of the three NULL = 0 / 1 / 0) or 0
+ *   without skip;
  *   parameters per channel (pstride 0) or per (b, c) plane (pstride C); act 0 none,
  *   1 ReLU, 2 tanh; x, skip and out may be channel-slice views (batch strides); out may
  *   alias x. */
@@ -384,7 +385,7 @@ int sa_plane_stats(const float *x, long x_bs, int B, int C, long hw, float eps, 
 int sa_norm_act(const float *x, long x_bs, int B, int C, long hw, const float *m, const float *s,
                 const float *t, int pstride, int act_in, const float *skip, long skip_bs,
                 const float *skip_m, const float *skip_s, const float *skip_t, int skip_pstride,
-                int act_out, float *out, long out_bs, void *stream);
+                int act_skip, int act_out, float *out, long out_bs, void *stream);
 
 /* Live per-kernel timing for bench.py: when enabled, every launch of kernel `id`
  * is bracketed by hipEvents on the launch stream; sa_timing_read synchronises the

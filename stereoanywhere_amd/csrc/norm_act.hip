@@ -9,7 +9,7 @@
 //   sa_plane_stats  InstanceNorm2d statistics (biased variance, fp64 sums) per (b, c)
 //                   plane — only for instance-norm layers;
 //   sa_norm_act     out = act_out( act_in((x - m) * s + t) + skip_term ),
-//                   skip_term = (skip - m') * s' + t'  or  skip,
+//                   skip_term = act_skip((skip - m') * s' + t')  or  act_skip(skip),
 //                   so bias (m = -b), eval BatchNorm (m = mean - b, s = gamma / sqrt(var +
 //                   eps), t = beta), InstanceNorm (m = mean, s = rstd), ReLU / tanh and the
 //                   residual block's projection norm + add + ReLU are one pass.
@@ -85,7 +85,7 @@ struct Affine {
 template <int VEC>
 __global__ __launch_bounds__(256) void norm_act_kernel(const float *__restrict__ x, long x_bs, int C, long hw,
                                                        Affine ax, int act_in, const float *__restrict__ skip,
-                                                       long skip_bs, Affine as, int act_out,
+                                                       long skip_bs, Affine as, int act_skip, int act_out,
                                                        float *__restrict__ out, long out_bs) {
   const int plane = blockIdx.y, b = plane / C, c = plane % C;
   float m, s, t, sm = 0.0f, ss = 1.0f, st = 0.0f;
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void norm_act_kernel(const float *__restrict__
 #pragma unroll
   for (int j = 0; j < VEC; ++j) {
     float y = act_fn((v[j] - m) * s + t, act_in);
-    if (skip) y = y + (skip_aff ? (k[j] - sm) * ss + st : k[j]);
+    if (skip) y = y + act_fn(skip_aff ? (k[j] - sm) * ss + st : k[j], act_skip);
     v[j] = act_fn(y, act_out);
   }
   if (VEC == 4) {
@@ -136,9 +136,10 @@ extern "C" int sa_plane_stats(const float *x, long x_bs, int B, int C, long hw, 
 extern "C" int sa_norm_act(const float *x, long x_bs, int B, int C, long hw, const float *m, const float *sc,
                            const float *t, int pstride, int act_in, const float *skip, long skip_bs,
                            const float *skip_m, const float *skip_s, const float *skip_t, int skip_pstride,
-                           int act_out, float *out, long out_bs, void *stream) {
+                           int act_skip, int act_out, float *out, long out_bs, void *stream) {
   SA_REQUIRE(x && out && B > 0 && C > 0 && hw > 0, "sa_norm_act: bad arguments");
-  SA_REQUIRE(act_in >= 0 && act_in <= 2 && act_out >= 0 && act_out <= 2, "sa_norm_act: unknown activation");
+  SA_REQUIRE(act_in >= 0 && act_in <= 2 && act_out >= 0 && act_out <= 2 && act_skip >= 0 && act_skip <= 2,
+             "sa_norm_act: unknown activation");
   SA_REQUIRE(pstride == 0 || pstride == C, "sa_norm_act: pstride must be 0 or C");
   SA_REQUIRE(skip_pstride == 0 || skip_pstride == C, "sa_norm_act: skip_pstride must be 0 or C");
   SA_REQUIRE((long)B * C <= 65535, "sa_norm_act: too many planes");
@@ -149,10 +150,12 @@ extern "C" int sa_norm_act(const float *x, long x_bs, int B, int C, long hw, con
                    aligned16(x) && aligned16(out) && (!skip || aligned16(skip));
   if (vec) {
     dim3 grid((unsigned)((hw / 4 + 255) / 256), (unsigned)(B * C));
-    norm_act_kernel<4><<<grid, 256, 0, s>>>(x, x_bs, C, hw, ax, act_in, skip, skip_bs, as, act_out, out, out_bs);
+    norm_act_kernel<4><<<grid, 256, 0, s>>>(x, x_bs, C, hw, ax, act_in, skip, skip_bs, as, act_skip, act_out, out,
+                                            out_bs);
   } else {
     dim3 grid((unsigned)((hw + 255) / 256), (unsigned)(B * C));
-    norm_act_kernel<1><<<grid, 256, 0, s>>>(x, x_bs, C, hw, ax, act_in, skip, skip_bs, as, act_out, out, out_bs);
+    norm_act_kernel<1><<<grid, 256, 0, s>>>(x, x_bs, C, hw, ax, act_in, skip, skip_bs, as, act_skip, act_out, out,
+                                            out_bs);
   }
   return sa::check_launch("sa_norm_act");
 }

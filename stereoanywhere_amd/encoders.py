@@ -143,8 +143,29 @@ def _conv_k3(x: torch.Tensor, conv: nn.Conv2d, fin: _Finisher, in_aff=None):
     return r if fin.instance else (r, None)
 
 
-def residual_block(blk: nn.Module, name: str, x: torch.Tensor, fin: _Finisher) -> torch.Tensor:
+# A block input may arrive as (raw, affine): the stem's conv output whose norm + ReLU has not
+# been applied (_stem).  A stride-1 block without downsample whose convs are Winograd takes it
+# as is: conv1 applies the norm + ReLU on load and the block's closing pass applies it to the
+# skip term, so relu(N(stem)) is never written.  Any other block gets it materialised first.
+Pending = Tuple[torch.Tensor, "ops.Affine"]
+
+
+def _materialize(x) -> torch.Tensor:
+    if isinstance(x, tuple):
+        raw, aff = x
+        return ops.norm_act(raw, aff, act_in="relu", out=raw)
+    return x
+
+
+def residual_block(blk: nn.Module, name: str, x, fin: _Finisher) -> torch.Tensor:
     w1, w2 = blk.conv1.weight.data_ptr(), blk.conv2.weight.data_ptr()
+    pending = None
+    if isinstance(x, tuple):
+        if blk.downsample is None and blk.conv1.stride == (1, 1) and w1 in _WINO and w2 in _WINO:
+            x, pending = x
+        else:
+            x = _materialize(x)
+    pact = "relu" if pending is not None else None
     direct = _DIRECT.get(w1)
     if direct is not None and w2 in _WINO and _direct_fills_chip(x, blk.conv1):
         # stride-2 conv1 and the 1x1 downsample in one direct-MFMA launch (raw outputs, IN
@@ -159,11 +180,11 @@ def residual_block(blk: nn.Module, name: str, x: torch.Tensor, fin: _Finisher) -
     if fold is not None and w2 in _WINO and blk.conv1.stride == (1, 1) and ops.wino4_applies(x, _WINO[w2]):
         # eval BatchNorm: norm1 + ReLU in conv1's epilogue (folded weights), so conv2 reads y1
         # on the F(4x4) kernel without a norm_act pass in between
-        y1 = ops.conv2d_k3(x, fold[0], fold[1], relu=True)
+        y1 = ops.conv2d_k3(x, fold[0], fold[1], relu=True, in_aff=pending, in_act=pact)
         c2, s2 = _conv_k3(y1, blk.conv2, fin)
     elif w1 in _WINO and w2 in _WINO:
         # y1 = relu(N1(c1)) is never written: conv2 applies it while loading c1
-        c1, s1 = _conv_k3(x, blk.conv1, fin)
+        c1, s1 = _conv_k3(x, blk.conv1, fin, in_aff=pending)
         c2, s2 = _conv_k3(c1, blk.conv2, fin, in_aff=fin.affine(name + ".norm1", c1, s1))
     else:
         c1 = _conv(x, blk.conv1)
@@ -174,7 +195,7 @@ def residual_block(blk: nn.Module, name: str, x: torch.Tensor, fin: _Finisher) -
             c2, s2 = _conv(y1, blk.conv2), None
     a2 = fin.affine(name + ".norm2", c2, s2)
     if blk.downsample is None:
-        return ops.norm_act(c2, a2, act_in="relu", skip=x, act_out="relu", out=c2)
+        return ops.norm_act(c2, a2, act_in="relu", skip=x, skip_aff=pending, skip_act=pact, act_out="relu", out=c2)
     d = _conv(x, blk.downsample[0])
     return ops.norm_act(c2, a2, act_in="relu", skip=d, skip_aff=fin.affine(name + ".norm3", d), act_out="relu",
                         out=c2)
@@ -215,7 +236,7 @@ def _convs_grouped(convs, xs) -> List[torch.Tensor]:
     return [_conv(x, c) for c, x in zip(convs, xs)]
 
 
-def _stem(enc: nn.Module, x: torch.Tensor, fin: _Finisher) -> torch.Tensor:
+def _stem(enc: nn.Module, x: torch.Tensor, fin: _Finisher) -> Pending:
     direct = _DIRECT.get(enc.conv1.weight.data_ptr())
     stats = None
     if direct is not None:
@@ -224,13 +245,14 @@ def _stem(enc: nn.Module, x: torch.Tensor, fin: _Finisher) -> torch.Tensor:
         stats = r[1][0] if fin.instance else None
     else:
         c = _conv(x, enc.conv1)
-    return ops.norm_act(c, fin.affine("norm1", c, stats), act_in="relu", out=c)
+    # relu(norm1(c)) is left to the first block (Pending)
+    return c, fin.affine("norm1", c, stats)
 
 
-def _stage(seq: nn.Sequential, name: str, x: torch.Tensor, fin: _Finisher) -> torch.Tensor:
+def _stage(seq: nn.Sequential, name: str, x, fin: _Finisher) -> torch.Tensor:
     for i, blk in enumerate(seq):
         x = residual_block(blk, f"{name}.{i}", x, fin)
-    return x
+    return _materialize(x)
 
 
 def _install(wino: Optional[WinoTable], direct: Optional[DirectTable], fold: Optional[FoldTable] = None) -> None:

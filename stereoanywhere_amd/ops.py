@@ -558,8 +558,10 @@ class Affine:
 
 
 def norm_act(x: torch.Tensor, aff: Optional[Affine] = None, act_in=None, skip: Optional[torch.Tensor] = None,
-             skip_aff: Optional[Affine] = None, act_out=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out = act_out(act_in(aff(x)) + skip_aff(skip)) in one pass (out may be x or a channel slice)."""
+             skip_aff: Optional[Affine] = None, act_out=None, out: Optional[torch.Tensor] = None,
+             skip_act=None) -> torch.Tensor:
+    """out = act_out(act_in(aff(x)) + skip_act(skip_aff(skip))) in one pass (out may be x or a
+    channel slice)."""
     xb = _plane_bs(x, "x")
     B, C, H, W = x.shape
     if out is None:
@@ -574,7 +576,8 @@ def norm_act(x: torch.Tensor, aff: Optional[Affine] = None, act_in=None, skip: O
         sb = _plane_bs(skip, "skip")
     a = (aff or Affine()).args(C)
     sa_ = (skip_aff or Affine()).args(C)
-    N.call("sa_norm_act", x.data_ptr(), xb, B, C, H * W, *a, ACT[act_in], _ptr(skip), sb, *sa_, ACT[act_out],
+    N.call("sa_norm_act", x.data_ptr(), xb, B, C, H * W, *a, ACT[act_in], _ptr(skip), sb, *sa_, ACT[skip_act],
+           ACT[act_out],
            out.data_ptr(), ob, _stream(x))
     _account("norm_act", 4.0 * B * C * H * W * (3 if skip is not None else 2))
     return out
