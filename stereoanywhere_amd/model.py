@@ -17,9 +17,14 @@ Hot path, one kernel family per row:
   a10    stereo + mono pyramid lookups, one launch per iteration         sa_corr_lookup
   a12    GRU gates in the conv epilogues over [h | x | r*h] buffers    sa_conv2d_k3_wino4_multi_gate
   a14    convex upsampling of the final flow                            sa_convex_upsample
-Training (test_mode=False), vol_downsample > 0 and use_aggregate_stereo_vol are outside
-this tier and raise NotImplementedError.  use_truncate_vol / use_aggregate_mono_vol may be
-off (the reference CLI's store_true defaults, test.py:94-98).
+Training (test_mode=False) is outside this tier and raises NotImplementedError.
+use_truncate_vol / use_aggregate_mono_vol may be off (the reference CLI's store_true
+defaults, test.py:94-98).  The non-published flags run on the same kernels with torch glue
+around them: vol_downsample > 0 (the masked volume at 1/2^vd as a dense volume, the
+classifier outputs trilinearly back to 1/4) and use_aggregate_stereo_vol (the masked stereo
+volume through hourglass_stereo + classifier_stereo, times the truncation volume, as the
+stereo pyramid); n_additional_hourglass > 1 takes the unfused hourglass.  Combinations the
+reference cannot run either raise (tests/golden/flags.npz).
 """
 from __future__ import annotations
 
@@ -115,6 +120,12 @@ class StereoAnywhere(nn.Module):
         self.hourglass_mono_stack = nn.ModuleList([HourglassIdentity()] + [
             Hourglass(a.volume_channels, a.volume_channels, self.feature_channels)
             for _ in range(a.n_additional_hourglass)])
+        if a.use_aggregate_stereo_vol:   # stereoanywhere.py:59-65
+            self.hourglass_stereo = Hourglass(a.vol_n_masks, a.volume_channels, self.feature_channels)
+            self.hourglass_stereo_stack = nn.ModuleList([HourglassIdentity()] + [
+                Hourglass(a.volume_channels, a.volume_channels, self.feature_channels)
+                for _ in range(a.n_additional_hourglass)])
+            self.classifier_stereo = nn.Conv3d(a.volume_channels, 1, 3, 1, 1, bias=False)
         self.classifier_mono = nn.Conv3d(a.volume_channels, 1, 3, 1, 1, bias=False)
         self.classifier_monoconf = nn.Conv3d(a.volume_channels, 1, 3, 1, 1, bias=False)
         self.update_block = BasicMultiUpdateBlock(a.corr_levels, a.corr_radius, a.encoder_output_dim,
@@ -199,6 +210,11 @@ class StereoAnywhere(nn.Module):
                          U_ctx=[ops.wino_weights(c.weight.detach().contiguous()) for c in self.context_zqr_convs])
                 cls = torch.cat([self._derived["cls_d"], self._derived["cls_c"]], 0)  # [2,8,3,3,3]
                 self._derived["hg"] = self.hourglass_mono.fused_weights(cls)
+                if self.args.use_aggregate_stereo_vol:
+                    cs = self.classifier_stereo.weight.permute(0, 1, 4, 2, 3).contiguous()
+                    self._derived["cls_s"] = cs
+                    # the fused classifier pair's second output is unused here
+                    self._derived["hg_stereo"] = self.hourglass_stereo.fused_weights(torch.cat([cs, cs], 0))
             self._derived_key = key
         return self._derived
 
@@ -212,9 +228,14 @@ class StereoAnywhere(nn.Module):
         a = self.args
         if not test_mode:
             raise NotImplementedError("training forward (test_mode=False) is outside the inference tier")
-        if a.vol_downsample > 0 or a.use_aggregate_stereo_vol or a.n_gru_layers != 3 or a.n_downsample != 2:
-            raise NotImplementedError("only the published configuration (vol_downsample=0, no stereo "
-                                      "aggregation, 3 GRU levels, n_downsample=2) is built")
+        if a.n_gru_layers != 3 or a.n_downsample != 2:
+            raise NotImplementedError("only 3 GRU levels at n_downsample=2 are built")
+        if a.vol_downsample > 0 and (a.use_aggregate_stereo_vol or not a.use_aggregate_mono_vol):
+            # the reference fails on these combinations too (tests/golden/flags.npz): its
+            # full-resolution stereo volume meets the downsampled masks, or its GRU samples the
+            # downsampled raw mono volume with full-resolution coordinates
+            raise RuntimeError("vol_downsample > 0 needs use_aggregate_mono_vol and no use_aggregate_stereo_vol "
+                               "(the reference's volumes stop matching otherwise)")
         get_corr_block(a.corr_implementation)
         if image2.device.type != "cuda":
             raise RuntimeError("StereoAnywhere (MI355X build) runs on the GPU only; move inputs to cuda")
@@ -296,8 +317,11 @@ class StereoAnywhere(nn.Module):
 
         # ---- pyramids
         trunc = (sm2, mirror) if a.use_truncate_vol else (None, None)
-        stereo_blk = HipCorrBlock1D.from_features(fmap2, fmap3, a.corr_levels, a.corr_radius, trunc[0], trunc[1],
-                                                  float(a.mirror_attenuation))
+        if a.use_aggregate_stereo_vol:
+            stereo_blk = self._stereo_aggregate(dw, fmap2, fmap3, mde2, mde3, m2l, m3l, trunc, B, H4, W4)
+        else:
+            stereo_blk = HipCorrBlock1D.from_features(fmap2, fmap3, a.corr_levels, a.corr_radius, trunc[0], trunc[1],
+                                                      float(a.mirror_attenuation))
         del fmap2, fmap3
         if a.use_aggregate_mono_vol:
             mono_rows = vol_d.permute(0, 1, 3, 4, 2)  # [B,1,H,W1,W2] view (transposed by the pyramid kernel)
@@ -393,15 +417,20 @@ class StereoAnywhere(nn.Module):
         mono left, mirror map, initial coords_x)."""
         a = self.args
         dev, f32 = mde2.device, torch.float32
-        feats_l = [F.interpolate(mde2, scale_factor=1 / 2 ** i, mode="bilinear", align_corners=True)
-                   for i in range(a.n_downsample, len(self.feature_channels))]
-        feats_r = [F.interpolate(mde3, scale_factor=1 / 2 ** i, mode="bilinear", align_corners=True)
-                   for i in range(a.n_downsample, len(self.feature_channels))]
+        feats_l, feats_r = self._volume_features(mde2, mde3)
+        vd = a.vol_downsample
 
         # ---- mono cost volume -> 3-D hourglass -> classifiers (native [B,C,W2,H,W1] layout)
         # the fused hourglass reads the one-hot masked volume through per-pixel records (its two
         # readers evaluate the cells); the torch path materialises it
-        masked = ops.OneHotVolume(n2, n3, m2l, m3l, a.vol_n_masks, 1.73)
+        if vd > 0:
+            # stereoanywhere.py:141-145: the raw volume (trilinear) and the masks (nearest) at
+            # 1/2^vd, masked as a dense volume (the downsampled cells are no longer a product of
+            # per-pixel terms)
+            vol = (1.73 * ops.corr_volume(n2, n3)).view(B, 1, H4, W4, W4)
+            masked = self._masked_dense(vol, m2l, m3l, vd)
+        else:
+            masked = ops.OneHotVolume(n2, n3, m2l, m3l, a.vol_n_masks, 1.73)
         # stack[i] for i < n_additional (stereoanywhere.py:163-164): stack[0] is the identity,
         # so only n_additional >= 2 puts a real hourglass after hourglass_mono
         extra = [self.hourglass_mono_stack[i] for i in range(a.n_additional_hourglass)
@@ -409,7 +438,8 @@ class StereoAnywhere(nn.Module):
         if not extra and a.vol_n_masks == 8 and self.hourglass_mono.fusable(masked, feats_l):
             vol_d, vol_c = self.hourglass_mono(masked, feats_l, feats_r, fused=dw["hg"])
         else:
-            masked = ops.mono_masked_volume(n2, n3, m2l, m3l, a.vol_n_masks, 1.73)
+            if isinstance(masked, ops.OneHotVolume):
+                masked = ops.mono_masked_volume(n2, n3, m2l, m3l, a.vol_n_masks, 1.73)
             agg = self.hourglass_mono(masked, feats_l, feats_r)
             for hg in extra:
                 agg = hg(agg, feats_l, feats_r)
@@ -417,6 +447,11 @@ class StereoAnywhere(nn.Module):
             vol_c = F.conv3d(agg, dw["cls_c"], padding=1)
             del agg
         del masked
+        if vd > 0:
+            # back to the 1/4 grid (stereoanywhere.py:170-172); the native axis order (W2, H, W1)
+            # of the same per-axis trilinear interpolation
+            up = dict(size=(W4, H4, W4), mode="trilinear", align_corners=True)
+            vol_d, vol_c = F.interpolate(vol_d, **up), F.interpolate(vol_c, **up)
         # (b, h, j, k) -> native [B, ., W2, H, W1] layout; vol_d/vol_c may be channel views
         strides = (vol_d.stride(0), W4, 1, H4 * W4)
         disp_lr, conf_lr = ops.softargmin_conf(vol_d, vol_c, strides, (B, H4, W4, W4))
@@ -429,6 +464,70 @@ class StereoAnywhere(nn.Module):
         if a.init_disparity_zero:
             coords_x = torch.arange(W4, device=dev, dtype=f32).expand(B, 1, H4, W4).contiguous()
         return vol_d, vol_c, sm2, mirror, coords_x
+
+    def _volume_features(self, mde2, mde3):
+        """The hourglasses' guidance pyramids fmde2 / fmde3 (stereoanywhere.py:111-112, 122-123):
+        the mono maps at the volume's resolution (1/2^vol_downsample), then at 1/2^i for
+        i = n_downsample .. 5."""
+        a = self.args
+        out = []
+        for m in (mde2, mde3):
+            if a.vol_downsample > 0:
+                m = F.interpolate(m, scale_factor=1 / 2 ** a.vol_downsample, mode="bilinear", align_corners=True)
+            out.append([F.interpolate(m, scale_factor=1 / 2 ** i, mode="bilinear", align_corners=True)
+                        for i in range(a.n_downsample, len(self.feature_channels))])
+        return out
+
+    def _masked_dense(self, vol, m2l, m3l, vd: int) -> torch.Tensor:
+        """vol [B,1,H,W1,W2] x the depth-bin masks of the 1/4-res mono maps (generate_masks,
+        utils.py:48-54: bin n holds n/N <= m < (n+1)/N), both at 1/2^vd when vd > 0
+        (stereoanywhere.py:141-145, 147, 161) -> the hourglass's [B, N, W2, H, W1] layout."""
+        N = self.args.vol_n_masks
+
+        def masks(m):
+            n = torch.arange(N, device=m.device, dtype=m.dtype).view(1, N, 1, 1)
+            return ((m < (n + 1) / N) & (m >= n / N)).to(torch.float16)
+        ml, mr = masks(m2l), masks(m3l)
+        if vd > 0:
+            vol = F.interpolate(vol, scale_factor=1 / 2 ** vd, mode="trilinear", align_corners=True)
+            ml = F.interpolate(ml, scale_factor=1 / 2 ** vd, mode="nearest")
+            mr = F.interpolate(mr, scale_factor=1 / 2 ** vd, mode="nearest")
+        masked = vol * ml.unsqueeze(4) * mr.unsqueeze(3)            # [B, N, H, W1, W2]
+        return masked.permute(0, 1, 4, 2, 3).contiguous()
+
+    def _stereo_aggregate(self, dw, fmap2, fmap3, mde2, mde3, m2l, m3l, trunc, B, H4, W4):
+        """use_aggregate_stereo_vol (stereoanywhere.py:147-157, 201-205, 253-255): the masked
+        stereo volume through hourglass_stereo and classifier_stereo, times the truncation
+        volume, as the GRU's stereo pyramid (the coarse stereo disparities the reference also
+        forms there are not used by the test-mode forward)."""
+        a = self.args
+        vol = ops.corr_volume(fmap2, fmap3).view(B, 1, H4, W4, W4)
+        masked = self._masked_dense(vol, m2l, m3l, 0)
+        del vol
+        feats_l, feats_r = self._volume_features(mde2, mde3)
+        extra = [self.hourglass_stereo_stack[i] for i in range(a.n_additional_hourglass)
+                 if not isinstance(self.hourglass_stereo_stack[i], HourglassIdentity)]
+        if not extra and a.vol_n_masks == 8 and self.hourglass_stereo.fusable(masked, feats_l):
+            vol_s = self.hourglass_stereo(masked, feats_l, feats_r, fused=dw["hg_stereo"])[0]
+        else:
+            agg = self.hourglass_stereo(masked, feats_l, feats_r)
+            for hg in extra:
+                agg = hg(agg, feats_l, feats_r)
+            vol_s = F.conv3d(agg, dw["cls_s"], padding=1)
+            del agg
+        del masked
+        rows = vol_s.permute(0, 1, 3, 4, 2)       # [B, 1, H, W1, W2] view
+        if trunc[0] is not None:
+            # truncate_corr_volume_v2 (utils.py:216-238), conf_th=None
+            d, m = trunc[0].view(B, 1, H4, W4, 1), trunc[1].view(B, 1, H4, W4, 1)
+            j = torch.arange(W4, device=d.device, dtype=d.dtype).view(1, 1, 1, W4, 1)
+            k = torch.arange(W4, device=d.device, dtype=d.dtype).view(1, 1, 1, 1, W4)
+            att = float(a.mirror_attenuation)
+            T = 1 * (1 - m) + m * (torch.sigmoid((j - d) - k) * (1 - att) + att)
+            rows = T * rows
+        return HipCorrBlock1D(None, a.corr_levels, a.corr_radius,
+                              _pyramid=ops.pyramid_from_volume(rows.contiguous(), a.corr_levels),
+                              _shape=(B, H4, W4, W4))
 
     def _iterate(self, dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4):
         """The GRU loop as a generator: it yields twice per iteration (after gru16 and at the

@@ -17,12 +17,12 @@ def load_fixture(name: str) -> dict:
     return out
 
 
-def regenerate_inputs(fix: dict, B: int, H: int, W: int, D: float) -> dict:
+def regenerate_inputs(fix: dict, B: int, H: int, W: int, D: float, seed0: int = 1, prefix: str = "") -> dict:
     from stereoanywhere_amd import synth
 
-    pair = synth.synthetic_batch(B, H, W, D, seed0=1)
+    pair = synth.synthetic_batch(B, H, W, D, seed0=seed0)
     got = synth.digest([pair[k] for k in ("left", "right", "mono_left", "mono_right")])
-    assert got == str(fix["inputs_sha256"]), "synthetic inputs differ from the ones the fixture was made with"
+    assert got == str(fix[prefix + "inputs_sha256"]), "synthetic inputs differ from the ones the fixture was made with"
     return pair
 
 

@@ -193,3 +193,31 @@ def test_forward_graph_replays_the_forward(model):
             got = fg(*x, iters=iters)[0]
         assert got.shape == ref.shape
         assert float((got - ref).abs().max()) < 1e-4
+
+
+@pytest.mark.parametrize("name,over", [("vd1", dict(vol_downsample=1)), ("aggstereo", dict(use_aggregate_stereo_vol=True)),
+                                       ("rawmono", dict(use_aggregate_mono_vol=False)),
+                                       ("addhg2", dict(n_additional_hourglass=2))])
+def test_non_published_flags_vs_reference(name, over):
+    """Non-published model flags (stereoanywhere.py:141-177) against the reference run with the
+    same seeded weights on one 128x256 pair, 4 iterations (tests/golden/flags.npz; addhg2 on an
+    input where the reference's own quantile-band LSQ is stable, see make_golden.FLAG_CASES)."""
+    fix = load_fixture("flags.npz")
+    m = StereoAnywhere(dict(PUBLISHED, **over)).eval()
+    synth.load_seeded_weights(m, 0)
+    pair = regenerate_inputs(fix, 1, 128, 256, 48.0, seed0=int(fix[f"{name}.seed"]), prefix=f"{name}.")
+    disp = run(m.cuda(), pair, 4)
+    e = epe(disp, fix[f"{name}.disparity"])
+    print(name, "EPE", e, "max", float(np.abs(disp - fix[f"{name}.disparity"]).max()))
+    assert e < 1e-3
+
+
+@pytest.mark.parametrize("name,over", [("vd1_rawmono", dict(vol_downsample=1, use_aggregate_mono_vol=False)),
+                                       ("vd1_aggstereo", dict(vol_downsample=1, use_aggregate_stereo_vol=True))])
+def test_flag_combinations_the_reference_cannot_run(name, over):
+    fix = load_fixture("flags.npz")
+    assert str(fix[f"{name}.error"]) == "RuntimeError"
+    m = StereoAnywhere(dict(PUBLISHED, **over)).eval().cuda()
+    t = [torch.zeros(1, c, 128, 256, device="cuda") for c in (3, 3, 1, 1)]
+    with pytest.raises(RuntimeError):
+        m(*t, iters=1, test_mode=True)

@@ -21,6 +21,18 @@ def test_state_dict_names_match_reference():
     assert ours == ref
 
 
+@pytest.mark.parametrize("name,over", [("aggstereo", dict(use_aggregate_stereo_vol=True)),
+                                       ("addhg2", dict(n_additional_hourglass=2)), ("vd1", dict(vol_downsample=1))])
+def test_state_dict_names_match_reference_under_flags(name, over):
+    """The non-published flags' extra modules (hourglass_stereo, its stack, classifier_stereo,
+    additional hourglasses) carry the reference's names and shapes (tests/golden/flags.npz)."""
+    import numpy as np
+    fix = np.load(os.path.join(GOLDEN, "flags.npz"))
+    ref = json.loads(str(fix[f"{name}.keys"]))
+    m = StereoAnywhere(dict(PUBLISHED, **over))
+    assert {k: list(v.shape) for k, v in m.state_dict().items()} == ref
+
+
 def test_reference_checkpoint_layout_loads_strict():
     m = StereoAnywhere(dict(PUBLISHED))
     sd = {k: torch.from_numpy(v) for k, v in synth.seeded_state_dict(
