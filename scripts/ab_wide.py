@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""F(4x4) conv launches on the 8-wave (32 channels per block) vs the wide (64 channels per
-block) shape at the model's shapes (B = 4 pairs at 544x960), HIP events per call."""
+"""F(4x4) conv launches on the 8-wave (32 channels per block) vs the wide and the quadrant (64
+channels per block) shapes at the model's shapes (B = 4 pairs at 544x960), HIP events per call.
+--no-wide skips the wide shape."""
 import os
 import sys
 
@@ -19,15 +20,22 @@ def main():
             continue
         x = torch.randn(N, Cin, H, W, device=dev)
         w = torch.randn(Cout, Cin, 3, 3, device=dev) / (3 * Cin ** 0.5)
-        U = ops.wino_weights(w)
         out = torch.empty(N, Cout, H, W, device=dev)
+        ref = torch.nn.functional.conv2d(x, w, padding=1)
         res = {}
-        for wide in (False, True):
-            ops.W4_WIDE = wide
-            res[wide] = timeit(lambda: ops.conv2d_k3(x, U, out=out))
+        for shape in ("8-wave", "wide", "quad"):
+            if shape == "wide" and "--no-wide" in sys.argv:
+                continue
+            ops.W4_WIDE, ops.W4_QUAD = shape == "wide", shape == "quad"
+            U = ops.wino_weights(w)
+            res[shape] = timeit(lambda: ops.conv2d_k3(x, U, out=out))
+            err = float((out - ref).abs().max())
+            res[shape + "_err"] = err
+        ops.W4_WIDE = ops.W4_QUAD = False
         fl = 2.0 * 36 * Cin * Cout * N * -(-H // 4) * -(-W // 4)
-        print(f"{name:12s} {N}x{Cin}->{Cout} {H}x{W}: 8-wave {res[False]:8.1f} us ({fl / res[False] / 1e6:5.1f} TF)"
-              f"  wide {res[True]:8.1f} us ({fl / res[True] / 1e6:5.1f} TF)", flush=True)
+        print(f"{name:12s} {N}x{Cin}->{Cout} {H}x{W}: " + "  ".join(
+            f"{k} {v:8.1f} us ({fl / v / 1e6:5.1f} TF, err {res[k + '_err']:.1e})"
+            for k, v in res.items() if not k.endswith("_err")), flush=True)
 
 
 if __name__ == "__main__":

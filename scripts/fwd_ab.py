@@ -11,6 +11,8 @@ import os, sys, time, torch
 sys.path.insert(0, os.environ["SA_ROOT"])
 from stereoanywhere_amd import synth
 from stereoanywhere_amd.model import StereoAnywhere
+from stereoanywhere_amd import ops
+ops.W4_QUAD = os.environ.get("SA_AB_W4_QUAD") == "1"
 P = dict(use_truncate_vol=True, use_aggregate_mono_vol=True, vol_n_masks=8, n_additional_hourglass=0,
          vol_downsample=0, mirror_conf_th=0.98, mirror_attenuation=0.9, lrc_th=1.0, normal_gain=10)
 m = StereoAnywhere(dict(P)).eval(); synth.load_seeded_weights(m, 0); m = m.cuda()

@@ -60,9 +60,13 @@ constexpr int NPT = 36;                   // transform points
 // 4-channel chunks, 66 KiB, two blocks per CU, so one block's first DMA wait and epilogue
 // overlap the other's MFMAs (per block ~6-8k cycles until the first chunk lands and ~9k of
 // epilogue around 6.8k per chunk, scripts/w4_clock.py); it is not faster in the forward.
-template <int NW_, int KC_, int CO_ = 32>
+template <int NW_, int KC_, int CO_ = 32, bool QUAD_ = false>
 struct W4Cfg {
-  static constexpr int NW = NW_, NTHR = 64 * NW_, TG = NW_ / 2, NT = 16 * TG, KC = KC_, JPC = KC_ / 4;
+  // QUAD: the waves of a tile group split the 6 x 6 points in quadrants (rows 0-2 / 3-5 x
+  // columns 0-2 / 3-5) instead of column halves
+  static constexpr bool QUAD = QUAD_;
+  static constexpr int NW = NW_, NTHR = 64 * NW_, TG = QUAD_ ? NW_ / 4 : NW_ / 2, NT = 16 * TG, KC = KC_, JPC = KC_ / 4;
+  static constexpr int NR = QUAD_ ? 3 : 6;                  // point rows per wave
   static constexpr int CO = CO_, CG = CO_ / 16;                // output channels per block, 16-channel groups
   static constexpr int SB = 4 * CO_;                        // filters per (point, 4-channel job): [k][n][g]
   static constexpr int PS_MAX = NT == 64 ? 340 : 204;       // (BH + 2)(BW / 4 + 2), largest geometry
@@ -89,6 +93,14 @@ using W4Small = W4Cfg<4, 4>;
 // instructions per MFMA of the 8-wave shape (whose main loop measured VALU- and LDS-issue
 // bound: -DSA_W4_DIAG=5/7 builds ran 20% / 15% faster).  288 accumulators per lane.
 using W4Wide = W4Cfg<4, 4, 64>;
+// Quad: 8 waves (two per SIMD), 32 tiles x 64 output channels, 4-channel chunks; a wave owns
+// 16 tiles x 64 channels x one quadrant of the points (9 points x 4 channel groups = 144
+// accumulators, as the 8-wave shape).  Per (tile, channel) job the row pass is the 8-wave
+// shape's (3 of 6 outputs per row) but the column pass yields 3 instead of 6 points, and each
+// transformed value feeds four MFMAs: ~1.5 instead of ~2 transform operations per MFMA, and one
+// ds_read_b128 instead of two ds_read_b64 per four MFMAs.  The price: a barrier per 4 input
+// channels and four partial output transforms meeting in LDS.
+using W4Quad = W4Cfg<8, 4, 64, true>;
 static_assert(2 * W4Small::SMEM * 4 <= 160 * 1024, "two small blocks per CU");
 static_assert(W4Wide::SMEM * 4 <= 160 * 1024, "one wide block per CU");
 
@@ -159,6 +171,19 @@ __device__ __forceinline__ void at6(const float *m, float *o) {
   o[3] = b + 8.0f * e + m[5];
 }
 
+// A^T restricted to its columns 0-2 (H = 0: rows [1,1,1] [0,1,-1] [0,1,1] [0,1,-1]) or 3-5
+// (H = 1: [1,1,0] [2,-2,0] [4,4,0] [8,-8,1]) applied to those 3 points: a partial of at6
+template <int H>
+__device__ __forceinline__ f32x4 at6h(const float u0, const float u1, const float u2) {
+  if (H == 0) {
+    const float p = u1 + u2, q = u1 - u2;
+    return f32x4{u0 + p, q, p, q};
+  } else {
+    const float p = u0 + u1, q = u0 - u1;
+    return f32x4{p, 2.0f * q, 4.0f * p, 8.0f * q + u2};
+  }
+}
+
 // half HF of B^T x: outputs 0-2 (HF = 0) or 3-5 (HF = 1)
 template <int HF>
 __device__ __forceinline__ void bt6h(const float x0, const float x1, const float x2, const float x3, const float x4,
@@ -182,12 +207,13 @@ __device__ __forceinline__ void bt6h(const float x0, const float x1, const float
 __device__ unsigned long long g_w4_clock[65536][10];   // + [8] chunk 0 issued, [9] last wave's start
 #endif
 
-template <class C, int HF, int LTW, bool GATED, bool AFF>
+template <class C, int HF, int LTW, bool GATED, bool AFF, int RH = 0>
 __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, const unsigned wid, float *smem,
                                         float2 *atab) {
   constexpr int NWAVE = C::NW, NTHR = C::NTHR, KC = C::KC, JPC = C::JPC, NT = C::NT, PDMA = C::PDMA,
                 UDMA = C::UDMA, UPW = C::UPW, UBUF = C::UBUF, BUF = C::BUF, PBUF = C::PBUF, OPP = C::OPP,
-                CO = C::CO, CG = C::CG, SB = C::SB;
+                CO = C::CO, CG = C::CG, SB = C::SB, NR = C::NR;
+  constexpr bool QUAD = C::QUAD;
   using f32xg = __attribute__((ext_vector_type(CG))) float;   // a lane's filter operands, one per group
   const int Cin = P.Cin, H = P.H, W = P.W, Cout = P.Cout;
   // block geometry as compile-time constants (the patch offsets divide by PS and PG)
@@ -275,10 +301,11 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   const int pread = k * PSv * 4 + 4 * trow * PGv * 4 + 4 * tcol + 2;
   const int uread = (k * 16 + m) * CG;
 
-  // acc[i][jj][g]: point (row i, column 3 HF + jj) of output-channel group g
-  f32x4 acc[6][3][CG];
+  // acc[i][jj][g]: point (row i, or 3 RH + i in a quadrant; column 3 HF + jj) of output-channel
+  // group g
+  f32x4 acc[NR][3][CG];
 #pragma unroll
-  for (int i = 0; i < 6; ++i)
+  for (int i = 0; i < NR; ++i)
 #pragma unroll
     for (int jj = 0; jj < 3; ++jj)
 #pragma unroll
@@ -337,6 +364,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
     // 6 x 2 MFMAs each.  Software pipeline (the scheduler is fenced per column to bound its
     // register use): the filter operands of the next column and rows 0-2 of the next job are
     // read under the current column's MFMAs.
+    // (ds_read_b32 + b128 + b32 of just the 6 inputs measured 4-7% slower)
     f32x2 ra[6], rc[6];
     f32x4 rb[6];
     auto load_rows = [&](int s, int r0, int r1) __attribute__((always_inline)) {
@@ -348,10 +376,11 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
         rc[r] = *reinterpret_cast<const f32x2 *>(p + r * PGv * 4 + 6);
       }
     };
-    f32xg bc[6], bn[6];
+    f32xg bc[NR], bn[NR];
     auto load_b = [&](int s, int jj, f32xg *b) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < 6; ++i) b[i] = *reinterpret_cast<const f32xg *>(ub + ((6 * i + 3 * HF + jj) * JPC + s) * SB);
+      for (int i = 0; i < NR; ++i)
+        b[i] = *reinterpret_cast<const f32xg *>(ub + ((6 * (QUAD ? 3 * RH + i : i) + 3 * HF + jj) * JPC + s) * SB);
     };
     load_rows(0, 0, 6);
     load_b(0, 0, bc);
@@ -374,12 +403,14 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
         float v[6];
         if (SA_W4_DIAG == 5) {   // timing only: no column pass
 #pragma unroll
-          for (int i = 0; i < 6; ++i) v[i] = t[i][jj];
+          for (int i = 0; i < NR; ++i) v[i] = t[i][jj];
+        } else if constexpr (QUAD) {
+          bt6h<RH>(t[0][jj], t[1][jj], t[2][jj], t[3][jj], t[4][jj], t[5][jj], v);
         } else {
           bt6(t[0][jj], t[1][jj], t[2][jj], t[3][jj], t[4][jj], t[5][jj], v);
         }
 #pragma unroll
-        for (int i = 0; i < 6; ++i)
+        for (int i = 0; i < NR; ++i)
 #pragma unroll
           for (int g = 0; g < CG; ++g)
             acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], bc[i][g], acc[i][jj][g], 0, 0, 0);
@@ -393,7 +424,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
 #endif
         }
 #pragma unroll
-        for (int i = 0; i < 6; ++i) bc[i] = bn[i];
+        for (int i = 0; i < NR; ++i) bc[i] = bn[i];
       }
     }
   }
@@ -412,6 +443,41 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   // banks.
   float *ot = smem;
   const int relu = P.relu;
+  if constexpr (QUAD) {
+    // Quadrant (RH, HF) contributes A_RH^T M_q A_HF (at6h along each, over its 3 x 3 points).
+    // The four partials of a channel group meet in LDS in a rotation: in phase p quadrant
+    // q = 2 RH + HF handles group (q + 1 + p) % 4 (store, add, add, then its own group: add,
+    // bias, ReLU), so each group plane has one writer per phase.
+    constexpr int QD = 2 * RH + HF;
+#pragma unroll
+    for (int phase = 0; phase < 4; ++phase) {
+      const int g = (QD + 1 + phase) & 3;
+      const int col = g * 16 + (lane & 15);
+      const float bv = (phase == 3 && P.bias) ? P.bias[co0 + col] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ti = tg * 16 + 4 * (lane >> 4) + i, orow = (ti >> ltw) * 4, ocol = (ti & (tw - 1)) * 4;
+        f32x4 u[3];
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) u[jj] = at6h<RH>(acc[0][jj][g][i], acc[1][jj][g][i], acc[2][jj][g][i]);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const f32x4 y = at6h<HF>(u[0][a], u[1][a], u[2][a]);
+          f32x4 *o = reinterpret_cast<f32x4 *>(ot + col * OPP + (orow + a) * BW + ocol);
+          if (phase == 0) {
+            *o = y;
+          } else if (phase < 3) {
+            *o = *o + y;
+          } else {
+            f32x4 v = (*o + y) + bv;
+            if (relu) v = f32x4{fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f)};
+            *o = v;
+          }
+        }
+      }
+      if (phase < 3) __syncthreads();
+    }
+  } else {
 #pragma unroll
   for (int phase = 0; phase < 2; ++phase) {
 #pragma unroll
@@ -457,6 +523,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
     }
   }
     if (phase == 0) __syncthreads();
+  }
   }
 #ifdef SA_W4_CLOCK
   if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][6] = __builtin_amdgcn_s_memtime();
@@ -595,7 +662,18 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 || C::CO == 64 ? 1 : 2) void wi
 #endif
   // the first half of the waves takes point columns 0-2, the second half 3-5 (wave-uniform)
   const unsigned wid = sa::xcd_remap(g - base, nb);
-  if (threadIdx.x < C::NTHR / 2) {
+  const W4Gate *gp = GATED ? &L.gate[pi] : nullptr;
+  if constexpr (C::QUAD) {   // quadrant 2 RH + HF = wave / TG
+    const int qd = threadIdx.x / (C::NTHR / 4);
+#define SA_W4_Q(HF_, RH_)                                                   \
+  (P.ltw == 4 ? w4_body<C, HF_, 4, GATED, AFF, RH_>(P, gp, wid, smem, atab) \
+              : w4_body<C, HF_, 5, GATED, AFF, RH_>(P, gp, wid, smem, atab))
+    if (qd == 0) SA_W4_Q(0, 0);
+    else if (qd == 1) SA_W4_Q(1, 0);
+    else if (qd == 2) SA_W4_Q(0, 1);
+    else SA_W4_Q(1, 1);
+#undef SA_W4_Q
+  } else if (threadIdx.x < C::NTHR / 2) {
     if (P.ltw == 4) w4_body<C, 0, 4, GATED, AFF>(P, GATED ? &L.gate[pi] : nullptr, wid, smem, atab);
     else w4_body<C, 0, 5, GATED, AFF>(P, GATED ? &L.gate[pi] : nullptr, wid, smem, atab);
   } else {
@@ -683,14 +761,16 @@ extern "C" int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, v
 extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                                              int block_shape, void *stream) {
   SA_REQUIRE(nprob >= 1 && nprob <= MAX_PROB && probs, "sa_conv2d_k3_wino4_multi: 1..%d problems", MAX_PROB);
-  SA_REQUIRE(block_shape >= 0 && block_shape <= 3, "sa_conv2d_k3_wino4_multi: block_shape 0..3");
+  SA_REQUIRE(block_shape >= 0 && block_shape <= 4, "sa_conv2d_k3_wino4_multi: block_shape 0..4");
   // Large blocks unless the caller asks for small ones (block_shape 2) or wide ones (3: 64
   // output channels per block, filters from sa_conv2d_wino4_weights_cb(..., 64, ...)).  The
   // small shape measured 2-8% faster on standalone launches of Cin <= 128 with a few rounds of
   // blocks (qh08, convc2) but not faster in the forward as a blanket choice.
-  const bool small = block_shape == 2, wide = block_shape == 3;
-  const int nt = small || wide ? W4Small::NT : W4Big::NT;
-  const int CO = wide ? 64 : 32;
+  // block_shape 4: the quadrant shape (W4Quad), also on the 64-channel filter layout
+  const bool small = block_shape == 2, wide = block_shape == 3, quad = block_shape == 4;
+  const int nt = small || wide || quad ? W4Small::NT : W4Big::NT;
+  const int CO = wide || quad ? 64 : 32;
+  const int aff_max = small ? W4Small::AFF_MAX : quad ? W4Quad::AFF_MAX : W4Big::AFF_MAX;
   W4Launch L{};
   long total = 0;
   bool gated = false, aff = false;
@@ -706,9 +786,9 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
     const bool qaff = q.in_m || q.in_s || q.in_t || q.in_act;
     SA_REQUIRE(q.in_act == 0 || q.in_act == 1, "sa_conv2d_k3_wino4: input activation none or ReLU (got %d)", q.in_act);
     SA_REQUIRE(q.in_pstride == 0 || q.in_pstride == q.Cin, "sa_conv2d_k3_wino4: in_pstride must be 0 or Cin");
-    SA_REQUIRE(!qaff || (!wide && q.Cin <= (small ? W4Small::AFF_MAX : W4Big::AFF_MAX)),
-               "sa_conv2d_k3_wino4: an input transform needs the 8- or 4-wave shape and Cin <= %d",
-               small ? W4Small::AFF_MAX : W4Big::AFF_MAX);
+    SA_REQUIRE(!qaff || (!wide && q.Cin <= aff_max),
+               "sa_conv2d_k3_wino4: an input transform needs the 8-wave, quadrant or 4-wave shape and Cin <= %d",
+               aff_max);
     aff = aff || qaff;
     SA_REQUIRE((long)q.Cin * q.H * q.W * 4 < (1L << 31) - 64 && 36L * q.Cin * q.Cout * 4 < (1L << 31),
                "sa_conv2d_k3_wino4: an image or the filter bank exceeds the 2 GB buffer-descriptor range");
@@ -748,7 +828,11 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
   SA_REQUIRE(!(aff && gated), "sa_conv2d_k3_wino4: an input transform and a gate epilogue in one launch");
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV2D_W4, s);
-  if (aff && small)
+  if (quad)
+    aff     ? wino_f4k3_kernel<W4Quad, false, true><<<(unsigned)total, W4Quad::NTHR, 0, s>>>(L)
+    : gated ? wino_f4k3_kernel<W4Quad, true><<<(unsigned)total, W4Quad::NTHR, 0, s>>>(L)
+            : wino_f4k3_kernel<W4Quad, false><<<(unsigned)total, W4Quad::NTHR, 0, s>>>(L);
+  else if (aff && small)
     wino_f4k3_kernel<W4Small, false, true><<<(unsigned)total, W4Small::NTHR, 0, s>>>(L);
   else if (aff)
     wino_f4k3_kernel<W4Big, false, true><<<(unsigned)total, W4Big::NTHR, 0, s>>>(L);

@@ -610,6 +610,9 @@ _WINO4 = True
 # F(4x4) launches on the wide block shape (64 output channels per block, one wave per SIMD)
 # where every problem allows it (Cout % 64; Cout % 128 with a z/r gate)
 W4_WIDE = False
+# F(4x4) launches on the quadrant block shape (block_shape 4: 32 tiles x 64 output channels,
+# two waves per SIMD, each wave one quadrant of the 6 x 6 points) where every problem allows it
+W4_QUAD = False
 
 
 def wino_weights(weight: torch.Tensor) -> WinoFilters:
@@ -622,7 +625,7 @@ def wino_weights(weight: torch.Tensor) -> WinoFilters:
     u4 = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.float32)
     N.call("sa_conv2d_wino4_weights", weight.data_ptr(), Cout, Cin, u4.data_ptr(), _stream(weight))
     u4w = None
-    if W4_WIDE and Cout % 64 == 0 and Cin % 8 == 0:   # the wide shape's layout only when it may run
+    if (W4_WIDE or W4_QUAD) and Cout % 64 == 0 and Cin % 8 == 0:   # the 64-channel layout only when it may run
         u4w = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.float32)
         N.call("sa_conv2d_wino4_weights_cb", weight.data_ptr(), Cout, Cin, 64, u4w.data_ptr(), _stream(weight))
     return WinoFilters(u2, u4, Cin, Cout, u4w)
@@ -752,7 +755,8 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     aff = any(p.get("in_aff") is not None or p.get("in_act") is not None for p in plain)
     if gated and aff:
         raise RuntimeError("conv2d_k3_multi: an input transform and a gate epilogue in one launch")
-    wide = (f4 and W4_WIDE and not small_blocks and not aff and all(p["U"].u4w is not None for p in plain)
+    wide = (f4 and (W4_QUAD or (W4_WIDE and not aff)) and not small_blocks
+            and all(p["U"].u4w is not None for p in plain)
             and all(p["U"].cout % 128 == 0 for p in problems if p.get("gate") and p["gate"]["mode"] == 1))
     built = [_wino_problem(**p, f4=f4, wide=wide) for p in plain]
     arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
@@ -760,7 +764,7 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
         gates = (N.SaGateEpilogue * len(built))(*[_gate_epilogue(p) if p.get("gate") else N.SaGateEpilogue()
                                                   for p in problems])
         N.call("sa_conv2d_k3_wino4_multi_gate", len(built), ctypes.addressof(arr), ctypes.addressof(gates),
-               3 if wide else 2 if small_blocks else 0, _stream(problems[0]["x"]))
+               (4 if W4_QUAD else 3) if wide else 2 if small_blocks else 0, _stream(problems[0]["x"]))
     else:
         N.call("sa_conv2d_k3_wino4_multi" if f4 else "sa_conv2d_k3_wino_multi", len(built), ctypes.addressof(arr),
                _stream(problems[0]["x"]))

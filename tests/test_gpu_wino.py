@@ -111,7 +111,7 @@ def test_wino4_matches_conv2d(monkeypatch, N, Cin, Cout, H, W):
         assert err_max < 1e-4 * scale and err_rms < 1e-5 * scale, (err_max, err_rms)
 
 
-@pytest.mark.parametrize("small", [False, True])
+@pytest.mark.parametrize("small", [False, True, "quad"])
 def test_wino4_input_transform(monkeypatch, small):
     """The producer's norm + activation applied on load by the F(4x4) kernel (the LDS pass over
     each staged chunk): per-(image, channel) InstanceNorm + ReLU with output statistics on a
@@ -125,7 +125,10 @@ def test_wino4_input_transform(monkeypatch, small):
         return torch.randn(*s, generator=g).cuda()
     xa = r(2, 96, 37, 132) * 2 + 0.7           # channel slice [16, 80) of it
     xb, xc = r(3, 32, 20, 52) + 0.3, r(1, 64, 9, 36)
-    wa, wb, wc = r(64, 64, 3, 3) / 24, r(96, 32, 3, 3) / 17, r(32, 64, 3, 3) / 24
+    quad = small == "quad"   # the quadrant shape (64 output channels per block)
+    monkeypatch.setattr(ops, "W4_QUAD", quad)
+    small = small is True
+    wa, wb, wc = r(64, 64, 3, 3) / 24, r(128 if quad else 96, 32, 3, 3) / 17, r(64 if quad else 32, 64, 3, 3) / 24
     mean, rstd = ops.plane_stats(xa[:, 16:80])
     bn = torch.nn.BatchNorm2d(32).cuda().eval()
     with torch.no_grad():
@@ -198,13 +201,15 @@ def test_wino4_multi_stats_views(monkeypatch):
     torch.testing.assert_close(yd, F.conv2d(xb, wb, padding=1), atol=2e-5, rtol=1e-4)
 
 
-@pytest.mark.parametrize("wide", [False, True])
+@pytest.mark.parametrize("wide", [False, True, "quad"])
 def test_wino4_gru_gate_epilogues(monkeypatch, wide):
     """ConvGRU gates in the F(4x4) epilogue (update.py:16-27) against the reference's expressions
     in torch fp32: mode 1 (convz | convr over cat(h, x) -> z, r*h) on channel views of one
     [h | x | r*h] buffer, beside a plain problem in the same launch; mode 2 (convq's r*h part ->
     the new state, in place on h).  Two levels' shapes (8 x 128 and 16 x 64 blocks)."""
-    monkeypatch.setattr(ops, "W4_WIDE", wide)   # also on the wide block shape (64 channels per block)
+    # also on the wide and the quadrant block shapes (64 channels per block)
+    monkeypatch.setattr(ops, "W4_WIDE", wide is True)
+    monkeypatch.setattr(ops, "W4_QUAD", wide == "quad")
     g = torch.Generator(device="cpu").manual_seed(42)
 
     def r(*s):
@@ -263,14 +268,17 @@ def test_wino4_small_block_shape(monkeypatch):
         torch.testing.assert_close(mean, ref.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("shape", ["wide", "quad"])
 @pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 64, 64, 20, 52), (1, 128, 256, 136, 240), (2, 16, 128, 9, 36),
                                             (1, 384, 128, 34, 60), (4, 256, 384, 17, 120)])
-def test_wino4_wide_block_shape(monkeypatch, N, Cin, Cout, H, W):
-    """The wide block shape (block_shape 3: 32 tiles x 64 output channels, one wave per SIMD;
-    filters in 64-channel blocks) against torch: bias + ReLU, InstanceNorm statistics, both
-    tile geometries (8 x 64 and 4 x 128 px), a ragged last tile row and column."""
+def test_wino4_wide_block_shape(monkeypatch, N, Cin, Cout, H, W, shape):
+    """The 64-channel block shapes (block_shape 3, wide: 32 tiles x 64 output channels, one wave
+    per SIMD; block_shape 4, quad: the same tile with two waves per SIMD, each on a quadrant of
+    the points; filters in 64-channel blocks) against torch: bias + ReLU, InstanceNorm
+    statistics, both tile geometries (8 x 64 and 4 x 128 px), a ragged last tile row and column."""
     monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
-    monkeypatch.setattr(ops, "W4_WIDE", True)
+    monkeypatch.setattr(ops, "W4_WIDE", shape == "wide")
+    monkeypatch.setattr(ops, "W4_QUAD", shape == "quad")
     g = torch.Generator(device="cpu").manual_seed(Cin + Cout)
     x = torch.randn(N, Cin, H, W, generator=g).cuda()
     w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)).cuda()
