@@ -44,6 +44,9 @@
                        // transform / MFMA, 3 no DMA and no barrier in the loop, 4 as 3 and no
                        // DMA at all, 5 no column pass, 6 no row pass, 7 no filter reads in the loop
 #endif
+#ifndef SA_W4_PERM
+#define SA_W4_PERM 1   // lane -> tile permutation that makes the patch rows' ds_read_b128 conflict-free
+#endif
 #ifndef SA_W4_PRIO
 #define SA_W4_PRIO 0
 #endif
@@ -184,6 +187,19 @@ __device__ __forceinline__ f32x4 at6h(const float u0, const float u1, const floa
   }
 }
 
+// Tile (within a wave's 16) of MFMA row m.  The patch rows' ds_read_b128 serves four 16-lane
+// groups, {0-3, 12-15, 20-27} and {4-11, 16-19, 28-31} (+ 32): channel k = lane / 16 of two
+// adjacent channels in one group, their planes 16 (mod 64) dwords apart (PS * 4 for either
+// geometry).  With tile = m the two channels' 4-bank slots overlap (2-way); mapping rows 4-11 to
+// tiles {0,1,4,5,8,9,12,13} and the others to {2,3,6,7,10,11,14,15} (sets invariant under a
+// shift of 4 slots) makes every group hit 16 distinct slots.
+__device__ __forceinline__ int w4_tile_of_row(int m) {
+  if (!SA_W4_PERM) return m;
+  const bool mid = m >= 4 && m < 12;
+  const int j = mid ? m - 4 : (m < 4 ? m : m - 8);
+  return (mid ? 0 : 2) + 4 * (j >> 1) + (j & 1);
+}
+
 // half HF of B^T x: outputs 0-2 (HF = 0) or 3-5 (HF = 1)
 template <int HF>
 __device__ __forceinline__ void bt6h(const float x0, const float x1, const float x2, const float x3, const float x4,
@@ -291,7 +307,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   // output channel n of each 16-channel half)
   const int tg = wv % C::TG;
   const int k = lane >> 4, m = lane & 15;
-  const int tidx = tg * 16 + m, trow = tidx >> ltw, tcol = tidx & (tw - 1);
+  const int tidx = tg * 16 + w4_tile_of_row(m), trow = tidx >> ltw, tcol = tidx & (tw - 1);
   // patch row 0 of the tile (input row y0 + 4 trow - 1), columns 4 tcol + 2 .. 4 tcol + 9
   // (input x0 + 4 tcol - 2 ...): the tile's 6 inputs are columns 3..8 of that span
   // the main loop addresses the patch with run-time PS / PG (as before the geometry became a
@@ -456,7 +472,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
       const float bv = (phase == 3 && P.bias) ? P.bias[co0 + col] : 0.0f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int ti = tg * 16 + 4 * (lane >> 4) + i, orow = (ti >> ltw) * 4, ocol = (ti & (tw - 1)) * 4;
+        const int ti = tg * 16 + w4_tile_of_row(4 * (lane >> 4) + i), orow = (ti >> ltw) * 4, ocol = (ti & (tw - 1)) * 4;
         f32x4 u[3];
 #pragma unroll
         for (int jj = 0; jj < 3; ++jj) u[jj] = at6h<RH>(acc[0][jj][g][i], acc[1][jj][g][i], acc[2][jj][g][i]);
@@ -487,7 +503,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
     const float bv = (phase == 1 && P.bias) ? P.bias[co0 + col] : 0.0f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int ti = tg * 16 + 4 * (lane >> 4) + i, orow = (ti >> ltw) * 4, ocol = (ti & (tw - 1)) * 4;
+      const int ti = tg * 16 + w4_tile_of_row(4 * (lane >> 4) + i), orow = (ti >> ltw) * 4, ocol = (ti & (tw - 1)) * 4;
       float u[4][3];
 #pragma unroll
       for (int jj = 0; jj < 3; ++jj) {
