@@ -47,6 +47,9 @@
 #ifndef SA_W4_PERM
 #define SA_W4_PERM 1   // lane -> tile permutation that makes the patch rows' ds_read_b128 conflict-free
 #endif
+#ifndef SA_W4_GJB
+#define SA_W4_GJB 8    // gate-epilogue store iterations whose plane loads go out together
+#endif
 #ifndef SA_W4_PRIO
 #define SA_W4_PRIO 0
 #endif
@@ -618,38 +621,61 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   const int half = Cout / 2;
   const bool rhalf = co0 >= half;
   const float *ctxb = GT.ctx + (long)n * GT.ctx_bs;
-#pragma unroll 2
-  for (int j = 0; j < (CO * NT * 16) / (4 * NTHR); ++j) {
-    const int i4 = tid + NTHR * j;
-    const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
-    const int y = y0 + r, x = x0 + cx;
-    if (y < H && x < W) {
+  // The gate planes are loaded for GJB store iterations at once (out-of-image positions read
+  // the block's first pixel, whose load is always in range, and are not stored), so GJB x 4
+  // planes of loads are in flight together instead of the previous iterations' branchy loop
+  // waiting for its own loads each time (the accumulators are dead here: registers are free).
+  constexpr int NJ = (CO * NT * 16) / (4 * NTHR), GJB = SA_W4_GJB < NJ ? SA_W4_GJB : NJ;
+  static_assert(NJ % GJB == 0, "gate batches");
+  const float *hb = GT.h + (long)n * GT.h_bs;
+  const float *ab = GT.add + (long)n * GT.add_bs;
+  const float *zb = GT.z + (long)n * GT.z_bs;
+#pragma unroll 1
+  for (int jb = 0; jb < NJ; jb += GJB) {
+    long pos[GJB];
+    bool ok[GJB];
+    f32x4 cv[GJB], hv[GJB], av[GJB], zv[GJB];
+#pragma unroll
+    for (int u = 0; u < GJB; ++u) {
+      const int i4 = tid + NTHR * (jb + u);
+      const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
+      const int y = y0 + r, x = x0 + cx;
+      ok[u] = y < H && x < W;
       const int co = co0 + c;
-      const long px = (long)y * W + x;
+      pos[u] = (long)co * hw + (ok[u] ? (long)y * W + x : (long)y0 * W + x0);
+      cv[u] = *reinterpret_cast<const f32x4 *>(ctxb + pos[u]);
+      if (GT.mode == 1) {
+        if (rhalf) hv[u] = *reinterpret_cast<const f32x4 *>(hb + pos[u] - (long)half * hw);
+      } else {
+        av[u] = *reinterpret_cast<const f32x4 *>(ab + pos[u]);
+        zv[u] = *reinterpret_cast<const f32x4 *>(zb + pos[u]);
+        hv[u] = *reinterpret_cast<const f32x4 *>(hb + pos[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < GJB; ++u) {
+      if (!ok[u]) continue;
+      const int i4 = tid + NTHR * (jb + u);
+      const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4;
       const f32x4 v = *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
-      const f32x4 cv = *reinterpret_cast<const f32x4 *>(ctxb + (long)co * hw + px);
       f32x4 o;
       if (GT.mode == 1) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = sa::sigmoidf_ref(v[e] + cv[e]);
+        for (int e = 0; e < 4; ++e) o[e] = sa::sigmoidf_ref(v[e] + cv[u][e]);
         if (!rhalf) {
-          *reinterpret_cast<f32x4 *>(dst + (long)co * hw + px) = o;
+          *reinterpret_cast<f32x4 *>(dst + pos[u]) = o;
         } else {
-          const f32x4 hv = *reinterpret_cast<const f32x4 *>(GT.h + (long)n * GT.h_bs + (long)(co - half) * hw + px);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = o[e] * hv[e];
-          *reinterpret_cast<f32x4 *>(GT.out2 + (long)n * GT.out2_bs + (long)(co - half) * hw + px) = o;
+          for (int e = 0; e < 4; ++e) o[e] = o[e] * hv[u][e];
+          *reinterpret_cast<f32x4 *>(GT.out2 + (long)n * GT.out2_bs + pos[u] - (long)half * hw) = o;
         }
       } else {
-        const f32x4 av = *reinterpret_cast<const f32x4 *>(GT.add + (long)n * GT.add_bs + (long)co * hw + px);
-        const f32x4 zv = *reinterpret_cast<const f32x4 *>(GT.z + (long)n * GT.z_bs + (long)co * hw + px);
-        const f32x4 hv = *reinterpret_cast<const f32x4 *>(GT.h + (long)n * GT.h_bs + (long)co * hw + px);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float q = tanhf((av[e] + v[e]) + cv[e]);
-          o[e] = (1.0f - zv[e]) * hv[e] + zv[e] * q;
+          const float q = tanhf((av[u][e] + v[e]) + cv[u][e]);
+          o[e] = (1.0f - zv[u][e]) * hv[u][e] + zv[u][e] * q;
         }
-        *reinterpret_cast<f32x4 *>(dst + (long)co * hw + px) = o;
+        *reinterpret_cast<f32x4 *>(dst + pos[u]) = o;
       }
     }
   }

@@ -495,9 +495,14 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
     if (ci + 1 < CIN) fetch(ci + 1);
     const float *lb = slab[buf] + wv * ROWP + lane * NP;
     const float *wc = wt + (long)ci * 9 * 6 * COUT;
+    // the kw loop unrolled for the 16-channel convs and the classifier pair (the scalar weight
+    // loads of the next kw then overlap this one's FMAs: 711 -> 567 and 568 -> 506 us), rolled
+    // for 8 -> 8 (unrolled it measured 1057 -> 1310 us: SGPR pressure of 48 weights per kw;
+    // with 4- or 2-channel weight groups 1460 / 1900 us, rolled with 4-channel groups 1130)
+    constexpr int KW_UNR = (NT == 1 || COUT <= 2) ? 3 : 1;
 #pragma unroll 1
     for (int kh = 0; kh < 3; ++kh) {
-#pragma unroll 1
+#pragma unroll KW_UNR
       for (int kw = 0; kw < 3; ++kw) {
         const VT *xp = reinterpret_cast<const VT *>(lb + kh * ROWP + kw * NP);
         float X[NP];
