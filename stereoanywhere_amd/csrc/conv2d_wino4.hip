@@ -29,6 +29,7 @@
 #include "sa_common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 #pragma clang fp contract(fast)
 
@@ -48,7 +49,10 @@
 #define SA_W4_PERM 1   // lane -> tile permutation that makes the patch rows' ds_read_b128 conflict-free
 #endif
 #ifndef SA_W4_GJB
-#define SA_W4_GJB 8    // gate-epilogue store iterations whose plane loads go out together
+#define SA_W4_GJB 8    // gate-epilogue store iterations whose plane loads go out together (mode 2)
+#endif
+#ifndef SA_W4_GJB1
+#define SA_W4_GJB1 16  // the same for mode 1
 #endif
 #ifndef SA_W4_PRIO
 #define SA_W4_PRIO 0
@@ -330,6 +334,12 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
 #pragma unroll
       for (int g = 0; g < CG; ++g) acc[i][jj][g] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // the bias of the channel groups this lane finishes in the epilogue, loaded now (a load
+  // there would wait a global round trip between the two LDS phases)
+  float bpre[QUAD ? 1 : CG / 2];
+#pragma unroll
+  for (int k = 0; k < (QUAD ? 1 : CG / 2); ++k)
+    bpre[k] = P.bias ? P.bias[co0 + (QUAD ? 2 * RH + HF : 2 * k + HF) * 16 + (lane & 15)] : 0.0f;
   if (SA_W4_PRIO && HF == 1) __builtin_amdgcn_s_setprio(1);   // static priority for waves 4-7
   if (SA_W4_DIAG != 4) issue_p0();
   // Input transform: v -> act(v * scale + shift), scale = s, shift = t - m * s per channel
@@ -472,7 +482,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
     for (int phase = 0; phase < 4; ++phase) {
       const int g = (QD + 1 + phase) & 3;
       const int col = g * 16 + (lane & 15);
-      const float bv = (phase == 3 && P.bias) ? P.bias[co0 + col] : 0.0f;
+      const float bv = phase == 3 ? bpre[0] : 0.0f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ti = tg * 16 + w4_tile_of_row(4 * (lane >> 4) + i), orow = (ti >> ltw) * 4, ocol = (ti & (tw - 1)) * 4;
@@ -503,7 +513,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   for (int gi = 0; gi < CG / 2; ++gi) {
     const int g = 2 * gi + (phase == 0 ? 1 - HF : HF);
     const int col = g * 16 + (lane & 15);
-    const float bv = (phase == 1 && P.bias) ? P.bias[co0 + col] : 0.0f;
+    const float bv = phase == 1 ? bpre[gi] : 0.0f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int ti = tg * 16 + w4_tile_of_row(4 * (lane >> 4) + i), orow = (ti >> ltw) * 4, ocol = (ti & (tw - 1)) * 4;
@@ -621,64 +631,72 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   const int half = Cout / 2;
   const bool rhalf = co0 >= half;
   const float *ctxb = GT.ctx + (long)n * GT.ctx_bs;
-  // The gate planes are loaded for GJB store iterations at once (out-of-image positions read
-  // the block's first pixel, whose load is always in range, and are not stored), so GJB x 4
-  // planes of loads are in flight together instead of the previous iterations' branchy loop
-  // waiting for its own loads each time (the accumulators are dead here: registers are free).
-  constexpr int NJ = (CO * NT * 16) / (4 * NTHR), GJB = SA_W4_GJB < NJ ? SA_W4_GJB : NJ;
-  static_assert(NJ % GJB == 0, "gate batches");
+  // The gate planes are loaded for a batch of store iterations at once (out-of-image
+  // positions read the block's first pixel, whose load is always in range, and are not
+  // stored), so all of a batch's loads are in flight together instead of a branchy loop
+  // waiting for its own loads every iteration (the accumulators are dead here: registers are
+  // free).  Batches: 16 iterations in mode 1 (ctx, and h for the r half), 8 in mode 2 (four
+  // planes): 128 registers either way.
+  constexpr int NJ = (CO * NT * 16) / (4 * NTHR);
   const float *hb = GT.h + (long)n * GT.h_bs;
   const float *ab = GT.add + (long)n * GT.add_bs;
   const float *zb = GT.z + (long)n * GT.z_bs;
+  auto gate_stores = [&](auto gjb_c, auto mode_c) __attribute__((always_inline)) {
+    constexpr int GJB = decltype(gjb_c)::value < NJ ? decltype(gjb_c)::value : NJ, MODE = decltype(mode_c)::value;
+    static_assert(NJ % GJB == 0, "gate batches");
 #pragma unroll 1
-  for (int jb = 0; jb < NJ; jb += GJB) {
-    long pos[GJB];
-    bool ok[GJB];
-    f32x4 cv[GJB], hv[GJB], av[GJB], zv[GJB];
+    for (int jb = 0; jb < NJ; jb += GJB) {
+      int pos[GJB];
+      bool ok[GJB];
+      f32x4 cv[GJB], hv[GJB], av[GJB], zv[GJB];
 #pragma unroll
-    for (int u = 0; u < GJB; ++u) {
-      const int i4 = tid + NTHR * (jb + u);
-      const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
-      const int y = y0 + r, x = x0 + cx;
-      ok[u] = y < H && x < W;
-      const int co = co0 + c;
-      pos[u] = (long)co * hw + (ok[u] ? (long)y * W + x : (long)y0 * W + x0);
-      cv[u] = *reinterpret_cast<const f32x4 *>(ctxb + pos[u]);
-      if (GT.mode == 1) {
-        if (rhalf) hv[u] = *reinterpret_cast<const f32x4 *>(hb + pos[u] - (long)half * hw);
-      } else {
-        av[u] = *reinterpret_cast<const f32x4 *>(ab + pos[u]);
-        zv[u] = *reinterpret_cast<const f32x4 *>(zb + pos[u]);
-        hv[u] = *reinterpret_cast<const f32x4 *>(hb + pos[u]);
+      for (int u = 0; u < GJB; ++u) {
+        const int i4 = tid + NTHR * (jb + u);
+        const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
+        const int y = y0 + r, x = x0 + cx;
+        ok[u] = y < H && x < W;
+        pos[u] = (co0 + c) * hw + (ok[u] ? y * W + x : y0 * W + x0);
+        cv[u] = *reinterpret_cast<const f32x4 *>(ctxb + pos[u]);
+        if (MODE == 1) {
+          if (rhalf) hv[u] = *reinterpret_cast<const f32x4 *>(hb + (pos[u] - half * hw));
+        } else {
+          av[u] = *reinterpret_cast<const f32x4 *>(ab + pos[u]);
+          zv[u] = *reinterpret_cast<const f32x4 *>(zb + pos[u]);
+          hv[u] = *reinterpret_cast<const f32x4 *>(hb + pos[u]);
+        }
       }
-    }
 #pragma unroll
-    for (int u = 0; u < GJB; ++u) {
-      if (!ok[u]) continue;
-      const int i4 = tid + NTHR * (jb + u);
-      const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4;
-      const f32x4 v = *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
-      f32x4 o;
-      if (GT.mode == 1) {
+      for (int u = 0; u < GJB; ++u) {
+        if (!ok[u]) continue;
+        const int i4 = tid + NTHR * (jb + u);
+        const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4;
+        const f32x4 v = *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
+        f32x4 o;
+        if (MODE == 1) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = sa::sigmoidf_ref(v[e] + cv[u][e]);
-        if (!rhalf) {
-          *reinterpret_cast<f32x4 *>(dst + pos[u]) = o;
+          for (int e = 0; e < 4; ++e) o[e] = sa::sigmoidf_ref(v[e] + cv[u][e]);
+          if (!rhalf) {
+            *reinterpret_cast<f32x4 *>(dst + pos[u]) = o;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = o[e] * hv[u][e];
+            *reinterpret_cast<f32x4 *>(GT.out2 + (long)n * GT.out2_bs + (pos[u] - half * hw)) = o;
+          }
         } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = o[e] * hv[u][e];
-          *reinterpret_cast<f32x4 *>(GT.out2 + (long)n * GT.out2_bs + pos[u] - (long)half * hw) = o;
+          for (int e = 0; e < 4; ++e) {
+            const float q = tanhf((av[u][e] + v[e]) + cv[u][e]);
+            o[e] = (1.0f - zv[u][e]) * hv[u][e] + zv[u][e] * q;
+          }
+          *reinterpret_cast<f32x4 *>(dst + pos[u]) = o;
         }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float q = tanhf((av[u][e] + v[e]) + cv[u][e]);
-          o[e] = (1.0f - zv[u][e]) * hv[u][e] + zv[u][e] * q;
-        }
-        *reinterpret_cast<f32x4 *>(dst + pos[u]) = o;
       }
     }
-  }
+  };
+  // (the 64-channel shapes spill with 16 in mode 1: 8 there)
+  if (GT.mode == 1)
+    gate_stores(std::integral_constant<int, CO == 64 ? SA_W4_GJB : SA_W4_GJB1>{}, std::integral_constant<int, 1>{});
+  else gate_stores(std::integral_constant<int, SA_W4_GJB>{}, std::integral_constant<int, 2>{});
   }
 }
 
