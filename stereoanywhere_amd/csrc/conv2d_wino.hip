@@ -255,6 +255,10 @@ __device__ __forceinline__ void wino_body(const WinoProb &P, const unsigned wid)
     for (int g = 0; g < CG; ++g) acc[k][g] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int tg = wv & 3, ch = wv >> 2;                 // tile row, output-channel half
   const int ak = lane >> 4, am = lane & 15;            // operand lane map (16x16x4)
+  // the epilogue's bias values, loaded now (there a load would wait a global round trip)
+  float bpre[CG];
+#pragma unroll
+  for (int g = 0; g < CG; ++g) bpre[g] = bias ? bias[co0 + (ch * CG + g) * 16 + (lane & 15)] : 0.0f;
   // operand slots (float2 units) of row xi * 4 + ak: the swizzle depends on ak's parity only
   const int a_slot = swz(ak, tg * TC + am, NT);
   int b_slot[CG];
@@ -352,7 +356,7 @@ __device__ __forceinline__ void wino_body(const WinoProb &P, const unsigned wid)
 #pragma unroll
   for (int g = 0; g < CG; ++g) {
     const int col = (ch * CG + g) * 16 + (lane & 15);
-    const float bv = bias ? bias[co0 + col] : 0.0f;
+    const float bv = bpre[g];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int tx = 4 * (lane >> 4) + r;
