@@ -72,8 +72,11 @@ def seeded_state_dict(template: Dict[str, "np.ndarray"], seed: int = 0) -> Dict[
             else:  # norm bias
                 out[name] = rng.uniform(-0.05, 0.05, shape).astype(np.float32)
             continue
-        if leaf == "weight":  # norm scale
+        if leaf in ("weight", "gamma"):  # norm scale, ViT LayerScale
             out[name] = rng.uniform(0.9, 1.1, shape).astype(np.float32)
+        elif leaf in ("cls_token", "pos_embed", "mask_token", "register_tokens"):
+            # ViT embeddings (depth_anything_v2/dinov2.py:109-114, init 230-235): N(0, 0.02)
+            out[name] = (rng.standard_normal(shape) * 0.02).astype(np.float32)
         elif leaf == "running_mean":
             out[name] = rng.uniform(-0.05, 0.05, shape).astype(np.float32)
         elif leaf == "running_var":

@@ -10,8 +10,9 @@ Same flags, same per-sample procedure:
   an all-zero prediction (182-187); --stereomodel skip_pred predicts zeros (219-228).
 Over --tries: per-try sample means, then mean / std over tries, printed as the reference's
 MEAN / STD tables and written with its write_csv_header / write_csv_row (251-274, 347-403).
-DAv2 is outside this tier: --monomodel DAv2 needs precomputed maps (--mono_tag) as written
-by mono_sceneflow-style preprocessing.  Datasets: `middlebury` (folder layout of
+--monomodel DAv2 runs the Depth Anything V2 producer (stereoanywhere_amd/mono.py) when
+--loadmonomodel names a checkpoint (or `seeded`), on both views stacked, min-max normalised
+jointly (test.py:189-199); without --loadmonomodel the precomputed maps (--mono_tag) are read.  Datasets: `middlebury` (folder layout of
 middlebury_dataset.py) and `synthetic` (seeded pairs with true disparity).
 The tiled harness (configs 3 and 5) is test_mapreduce_v2.py.
 Multi-GPU: run under torchrun; samples are split across ranks and the per-sample metric
@@ -30,7 +31,7 @@ import torch.nn.functional as F
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from stereoanywhere_amd import data, dist, harness, metrics, synth, tiler  # noqa: E402
+from stereoanywhere_amd import data, dist, harness, metrics, mono, synth, tiler  # noqa: E402
 from stereoanywhere_amd.checkpoint import load_reference_checkpoint  # noqa: E402
 from stereoanywhere_amd.model import StereoAnywhere  # noqa: E402
 
@@ -89,7 +90,7 @@ def build_dataset(args):
 
 
 @torch.no_grad()
-def run(net, sample, args, device):
+def run(net, sample, args, device, mono_model=None):
     """test.py:161-249 for one sample (batch 1)."""
     t = {k: torch.from_numpy(np.ascontiguousarray(v))[None] for k, v in sample.items() if isinstance(v, np.ndarray)}
     t.setdefault("maskocc", torch.zeros_like(t["gt"]))
@@ -107,7 +108,9 @@ def run(net, sample, args, device):
         res["disp"] = torch.ones_like(t["gt"]).squeeze(1)
         return res
     im2, im3 = t["im2"].to(device), t["im3"].to(device)
-    if "im2_mono" in t and args.monomodel != "none":
+    if mono_model is not None:
+        m2, m3 = mono.mono_pair_test(mono_model, im2, im3, args.dataset)
+    elif "im2_mono" in t and args.monomodel != "none":
         m2, m3 = t["im2_mono"].to(device), t["im3_mono"].to(device)
         if m2.shape[-2:] != im2.shape[-2:]:
             m2 = F.interpolate(m2, size=im2.shape[-2:], mode="bilinear", align_corners=False)
@@ -155,6 +158,7 @@ def main(argv=None):
         else:
             synth.load_seeded_weights(net, 0)
         net = net.to(device)
+    mono_model = mono.load_for_harness(args, device)
     ds = build_dataset(args)
     n = len(ds) if args.valsize <= 0 else min(args.valsize, len(ds))
 
@@ -164,7 +168,7 @@ def main(argv=None):
             data.write_pfm(os.path.join(args.outdir, f"{ds[i]['name']}_disp.pfm"), res["disp"][0].cpu().numpy())
         if args.verbose:
             print(f"{i}) " + ", ".join(f"{k}: {float(res[k])}" for k in harness.METRIC_ORDER))
-    out = harness.evaluate(lambda i: run(net, ds[i], args, device), n, args.tries, r, device, on_result)
+    out = harness.evaluate(lambda i: run(net, ds[i], args, device, mono_model), n, args.tries, r, device, on_result)
     if out is None:
         return None
     acc_mean, acc_std = out

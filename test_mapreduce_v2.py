@@ -6,7 +6,9 @@ compatible tiler (stereoanywhere_amd/tiler.py).  Configs 3 and 5 (Middlebury-H, 
 Per sample, as the reference does:
   bilinear ``iscale`` down-sampling of the images (194), nearest ``oscale`` of the ground
   truth -> mono maps min-max normalised jointly over the stacked pair with +1e-8 (159;
-  precomputed maps here: DAv2 is outside this tier; zeros for --monomodel none) ->
+  --monomodel DAv2 with --loadmonomodel <checkpoint | seeded> runs the Depth Anything V2
+  producer, stereoanywhere_amd/mono.py, at compute_mono_pair's input size, 113-160; without
+  --loadmonomodel the precomputed maps; zeros for --monomodel none) ->
   replicate pad to x32 (left/top get pad//2) -> uint8 truncation of the padded images
   (tensor_to_numpy_image, 163-175, 229-230) -> MapReduceInference.infer(iscale=1,
   oscale=1, iters, test_mode=True) -> unpad -> nearest resize to the ground truth
@@ -29,7 +31,7 @@ import torch.nn.functional as F
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from stereoanywhere_amd import data, dist, harness, metrics, synth, tiler  # noqa: E402
+from stereoanywhere_amd import data, dist, harness, metrics, mono, synth, tiler  # noqa: E402
 from stereoanywhere_amd.checkpoint import load_reference_checkpoint  # noqa: E402
 from stereoanywhere_amd.model import StereoAnywhere  # noqa: E402
 from stereoanywhere_amd.offload import CPUOffloadWrapper  # noqa: E402
@@ -136,7 +138,7 @@ def build_inferencer(net, args, rank: int = 0, world: int = 1) -> tiler.MapReduc
 
 
 @torch.no_grad()
-def run_mapreduce(sample, args, device, inferencer: tiler.MapReduceInference) -> dict:
+def run_mapreduce(sample, args, device, inferencer: tiler.MapReduceInference, mono_model=None) -> dict:
     """test_mapreduce_v2.py:178-301 for one sample (batch 1)."""
     t = {k: torch.from_numpy(np.ascontiguousarray(v))[None] for k, v in sample.items() if isinstance(v, np.ndarray)}
     t.setdefault("maskocc", torch.zeros_like(t["gt"]))
@@ -148,7 +150,10 @@ def run_mapreduce(sample, args, device, inferencer: tiler.MapReduceInference) ->
         t["validgt"] = F.interpolate(t["validgt"].float(), scale_factor=1.0 / args.oscale, mode="nearest")
         t["maskocc"] = F.interpolate(t["maskocc"].float(), scale_factor=1.0 / args.oscale, mode="nearest")
     im2, im3 = t["im2"].to(device), t["im3"].to(device)
-    if "im2_mono" in t and args.monomodel != "none":
+    if mono_model is not None:
+        m = mono.mono_pair_mapreduce(mono_model, im2, im3, args.dataset)
+        ml, mr = m[0:1], m[1:2]
+    elif "im2_mono" in t and args.monomodel != "none":
         m = torch.cat([t["im2_mono"], t["im3_mono"]]).to(device)
         if m.shape[-2:] != im2.shape[-2:]:
             m = F.interpolate(m, size=im2.shape[-2:], mode="bilinear", align_corners=False)
@@ -202,6 +207,7 @@ def main(argv=None):
     if args.cpu_offload:
         # config 5: the tiler runs under the offload wrapper (HBM-resident on MI355X, offload.py)
         inferencer.tile_wrapper = CPUOffloadWrapper(inferencer.tile_wrapper)
+    mono_model = mono.load_for_harness(args, device)
     ds = build_dataset(args)
     n = len(ds) if args.valsize <= 0 else min(args.valsize, len(ds))
 
@@ -211,7 +217,7 @@ def main(argv=None):
             data.write_pfm(os.path.join(args.outdir, f"{ds[i]['name']}_disp.pfm"), res["disp"][0].cpu().numpy())
         if args.verbose:
             print(ds[i]["name"], {k: round(float(res[k]), 4) for k in harness.METRIC_ORDER[:10]})
-    out = harness.evaluate(lambda i: run_mapreduce(ds[i], args, device, inferencer), n, args.tries, r, device,
+    out = harness.evaluate(lambda i: run_mapreduce(ds[i], args, device, inferencer, mono_model), n, args.tries, r, device,
                            on_result)
     if out is None:
         return None

@@ -648,8 +648,59 @@ def flag_cases(sa_mod, ut, corr_mod):
     return out
 
 
+DAV2_LAST_BIAS = 0.3
+
+
+def dav2_cases():
+    """Reference Depth Anything V2 (models/depth_anything_v2/dpt.py:168-238) on seeded weights:
+    vits ``infer_image`` outputs for a landscape, a portrait (the swapped input size) and a
+    square 518 x 518 case (the position grid used as stored), plus every encoder's state-dict
+    names and shapes.  cv2 is absent: on this path the reference
+    uses it only for the interpolation-method constants its Resize object stores (the resize
+    itself is torch's bicubic interpolate, dpt.py:227), so the stub carries those constants."""
+    cv2 = sys.modules["cv2"]
+    cv2.INTER_NEAREST, cv2.INTER_CUBIC, cv2.INTER_AREA = 0, 2, 3
+    tvt = sys.modules.setdefault("torchvision.transforms", types.ModuleType("torchvision.transforms"))
+    if not hasattr(tvt, "Compose"):
+        tvt.Compose = lambda ts: ts
+    from models.depth_anything_v2 import dpt  # noqa
+    cfgs = {
+        "vits": dict(encoder="vits", features=64, out_channels=[48, 96, 192, 384]),
+        "vitb": dict(encoder="vitb", features=128, out_channels=[96, 192, 384, 768]),
+        "vitl": dict(encoder="vitl", features=256, out_channels=[256, 512, 1024, 1024]),
+        "vitg": dict(encoder="vitg", features=384, out_channels=[1536, 1536, 1536, 1536]),
+    }
+    out = {}
+    init = dpt.DINOv2.__globals__["DinoVisionTransformer"].init_weights
+    dpt.DINOv2.__globals__["DinoVisionTransformer"].init_weights = lambda self: None   # names only
+    for enc, cfg in cfgs.items():
+        m = dpt.DepthAnythingV2(**cfg)
+        out[f"keys.{enc}"] = np.array(json.dumps({k: list(v.shape) for k, v in m.state_dict().items()}, sort_keys=True))
+        del m
+    dpt.DINOv2.__globals__["DinoVisionTransformer"].init_weights = init
+    model = dpt.DepthAnythingV2(**cfgs["vits"]).eval()
+    synth.load_seeded_weights(model, seed=0)
+    # seeded weights drive the head's last conv negative everywhere (its ReLU then outputs 0):
+    # its bias is raised so the depth map carries signal
+    with torch.no_grad():
+        model.depth_head.scratch.output_conv2[2].bias.fill_(DAV2_LAST_BIAS)
+    rng = np.random.default_rng(7)
+    cases = [("land", (2, 3, 60, 90), 126, 98), ("portrait", (1, 3, 80, 50), 98, 70), ("square", (1, 3, 100, 100), 518, 518)]
+    for name, shape, iw, ih in cases:
+        raw = rng.random(shape).astype(np.float32)
+        with torch.no_grad():
+            img, _, (fh, fw) = model.image2tensor(torch.from_numpy(raw.copy()), iw, ih)
+            d = model.infer_image(torch.from_numpy(raw.copy()), input_size_width=iw, input_size_height=ih)
+        out[f"{name}.raw"] = raw
+        out[f"{name}.size"] = np.array([iw, ih, fh, fw], dtype=np.int64)
+        out[f"{name}.depth"] = _np(d)
+        print("dav2", name, tuple(d.shape), (fh, fw), float(d.min()), float(d.max()), float(d.std()),
+              float((d > 0).float().mean()))
+    return out
+
+
 def main(only=None):
-    """``python tests/golden/make_golden.py [wide] [tiled] [csv] [offload] [flags]`` regenerates
+    """``python tests/golden/make_golden.py [wide] [tiled] [csv] [offload] [flags] [dav2]`` regenerates
     just the named round-2 fixtures; no argument regenerates everything."""
     torch.set_num_threads(8)
     sa_mod, ut, corr_mod = _load_reference()
@@ -666,6 +717,8 @@ def main(only=None):
             np.savez_compressed(os.path.join(HERE, "offload.npz"), **offload_cases())
         if "flags" in only:
             np.savez_compressed(os.path.join(HERE, "flags.npz"), **flag_cases(sa_mod, ut, corr_mod))
+        if "dav2" in only:
+            np.savez_compressed(os.path.join(HERE, "dav2.npz"), **dav2_cases())
         return
     np.savez_compressed(os.path.join(HERE, "wide_96x1152_it4.npz"), **wide_case(sa_mod, ut, corr_mod, model))
     np.savez_compressed(os.path.join(HERE, "tiled_model.npz"), **tiled_model_cases(sa_mod, model))
@@ -673,6 +726,7 @@ def main(only=None):
         json.dump(harness_csv_cases(), f, indent=1)
     np.savez_compressed(os.path.join(HERE, "offload.npz"), **offload_cases())
     np.savez_compressed(os.path.join(HERE, "flags.npz"), **flag_cases(sa_mod, ut, corr_mod))
+    np.savez_compressed(os.path.join(HERE, "dav2.npz"), **dav2_cases())
     keys = {k: list(v.shape) for k, v in model.state_dict().items()}
     with open(os.path.join(HERE, "state_dict_keys.json"), "w") as f:
         json.dump(keys, f, indent=0, sort_keys=True)
