@@ -41,7 +41,8 @@ def main():
             blocks += nb
             flops += 2.0 * 36 * Cin * U.cout * B * -(-H // 4) * -(-W // 4)
             g = p.get("gate")
-            desc.append(f"{Cin}->{U.cout}@{H}x{W}" + (f"g{g['mode']}" if g else ""))
+            # the batch is part of the key: fnet's launches carry both views (N = 2B)
+            desc.append(f"{B}x{Cin}->{U.cout}@{H}x{W}" + (f"g{g['mode']}" if g else ""))
         rec.append((" + ".join(desc), blocks, flops, e0, e1))
         return r
     ops.conv2d_k3_multi = wrap
