@@ -15,7 +15,7 @@ FAMILIES = {
     "conv3d_kernel": "conv3d_fused", "pointwise_upcat_kernel": "conv3d_fused", "pointwise_kernel": "conv3d_fused",
     "conv3d_wd_kernel": "conv3d_fused", "conv3d_onehot_s2_kernel": "conv3d_fused",
     "vol_apply_kernel": "conv3d_fused", "lookup_kernel": "corr_lookup", "lookup_c1_kernel": "corr_lookup", "lookup_c1_vec_kernel": "corr_lookup",
-    "corr_pyramid_kernel": "corr_volume_pyramid", "masked_volume_kernel": "mono_masked_volume",
+    "corr_pyramid_kernel": "corr_volume_pyramid", "corr_pyramid_v2_kernel": "corr_volume_pyramid", "masked_volume_kernel": "mono_masked_volume",
     "sam_contig_kernel": "softargmin_conf", "sam_strided_kernel": "softargmin_conf", "sam_row_kernel": "softargmin_conf",
     "sam_col_kernel": "softargmin_conf", "lsq_kernel": "weighted_lsq", "lsq_hist_kernel": "weighted_lsq",
     "lsq_solve_kernel": "weighted_lsq",
