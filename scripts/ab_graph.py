@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Forward at the bench config (B=4 pairs 544x960, 22 iterations) eager vs replayed from a
 hipGraph captured with torch.cuda.graph (static input buffers refilled each step), for
-ScheduleOptions.loop_parts = 1 and 2.  usage: python scripts/ab_graph.py [steps]"""
+ScheduleOptions.loop_parts / loop_offset combinations.
+usage: python scripts/ab_graph.py [steps] [parts{T|F} ...]  (default 1T 2T 2F 3T 4T 4F)"""
 import dataclasses
 import os
 import sys
@@ -37,7 +38,9 @@ def main():
     base = model.opts
     ref = None
     with torch.no_grad():
-        for parts, offset in ((1, True), (2, True), (2, False), (3, True), (4, True), (4, False)):
+        combos = [(int(a[:-1]), a[-1] == "T") for a in sys.argv[2:]] or \
+            [(1, True), (2, True), (2, False), (3, True), (4, True), (4, False)]
+        for parts, offset in combos:
             model.opts = dataclasses.replace(base, loop_parts=parts, loop_offset=offset)
             t_e, out_e = timed(lambda: model(*x, iters=22, test_mode=True)[0], 1 if parts > 1 else steps)
             if ref is None:

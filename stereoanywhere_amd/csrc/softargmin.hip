@@ -56,58 +56,73 @@ __device__ __forceinline__ float sam_final(int mode, int left, int o, float acc,
   return 1.0f - (-acc) / (left ? g.log2W2 : g.log2W1);
 }
 
-// one wave per contiguous line of n <= 256 elements; V4: element 4*lane+i (float4 loads),
-// else element lane+64*i
+// one wave per LPW contiguous lines of n <= 256 elements (all of its lines' loads issued
+// before any reduction, so a wave has LPW x 2 KB in flight instead of 2 KB); V4: element
+// 4*lane+i (float4 loads), else element lane+64*i
+constexpr int SAM_LPW = 4;
+
 template <bool V4>
 __global__ __launch_bounds__(256) void sam_row_kernel(LineJob jd, LineJob jc, SGeo g, int left, long nlines) {
-  const long line = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (line >= nlines) return;
+  const long line0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * SAM_LPW;
+  if (line0 >= nlines) return;
   const int lane = threadIdx.x & 63;
   const int nout = left ? g.W1 : g.W2;
   const int n = left ? g.W2 : g.W1;
-  const long bh = line / nout;
-  const int o = (int)(line % nout);
-  const long b = bh / g.H, h = bh % g.H;
-  const long base = b * g.sb + h * g.sh + (long)o * (left ? g.sj : g.sk);
   const LineJob jobs[2] = {jd, jc};
-  float v[2][4];
   int idx[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) idx[i] = V4 ? 4 * lane + i : lane + 64 * i;
+  float v[SAM_LPW][2][4];
+  long ob[SAM_LPW];
+  int oo[SAM_LPW];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    if (!jobs[q].vol) continue;
-    const float *src = jobs[q].vol + base;
-    if (V4) {
-      if (4 * lane < n) {
-        const float4 t = *reinterpret_cast<const float4 *>(src + 4 * lane);
-        v[q][0] = t.x, v[q][1] = t.y, v[q][2] = t.z, v[q][3] = t.w;
+  for (int t = 0; t < SAM_LPW; ++t) {
+    const long line = line0 + t < nlines ? line0 + t : nlines - 1;   // a ragged tail re-reads the last line
+    const long bh = line / nout;
+    const int o = (int)(line % nout);
+    const long b = bh / g.H, h = bh % g.H;
+    ob[t] = b * g.obs + h * nout;
+    oo[t] = o;
+    const long base = b * g.sb + h * g.sh + (long)o * (left ? g.sj : g.sk);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (!jobs[q].vol) continue;
+      const float *src = jobs[q].vol + base;
+      if (V4) {
+        if (4 * lane < n) {
+          const float4 x = *reinterpret_cast<const float4 *>(src + 4 * lane);
+          v[t][q][0] = x.x, v[t][q][1] = x.y, v[t][q][2] = x.z, v[t][q][3] = x.w;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[t][q][i] = -INFINITY;
+        }
       } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[q][i] = -INFINITY;
+        for (int i = 0; i < 4; ++i) v[t][q][i] = idx[i] < n ? src[idx[i]] : -INFINITY;
       }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[q][i] = idx[i] < n ? src[idx[i]] : -INFINITY;
     }
   }
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const LineJob &J = jobs[q];
-    if (!J.vol) continue;
-    const float m = wave_max(fmaxf(fmaxf(v[q][0], v[q][1]), fmaxf(v[q][2], v[q][3])));
-    float e[4];
+  for (int t = 0; t < SAM_LPW; ++t) {
+    if (line0 + t >= nlines) break;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) e[i] = idx[i] < n ? expf(v[q][i] - m) : 0.f;
-    const float inv = 1.0f / wave_sum((e[0] + e[1]) + (e[2] + e[3]));
-    float acc = 0.f;
+    for (int q = 0; q < 2; ++q) {
+      const LineJob &J = jobs[q];
+      if (!J.vol) continue;
+      const float m = wave_max(fmaxf(fmaxf(v[t][q][0], v[t][q][1]), fmaxf(v[t][q][2], v[t][q][3])));
+      float e[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float p = e[i] * inv;
-      if (idx[i] < n) acc += J.mode == 0 ? p * (float)idx[i] : p * log2f(p + 1e-6f);
+      for (int i = 0; i < 4; ++i) e[i] = idx[i] < n ? expf(v[t][q][i] - m) : 0.f;
+      const float inv = 1.0f / wave_sum((e[0] + e[1]) + (e[2] + e[3]));
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = e[i] * inv;
+        if (idx[i] < n) acc += J.mode == 0 ? p * (float)idx[i] : p * log2f(p + 1e-6f);
+      }
+      acc = wave_sum(acc);
+      if (lane == 0) J.out[ob[t] + oo[t]] = sam_final(J.mode, left, oo[t], acc, g);
     }
-    acc = wave_sum(acc);
-    if (lane == 0) J.out[b * g.obs + h * nout + o] = sam_final(J.mode, left, o, acc, g);
   }
 }
 
@@ -262,8 +277,9 @@ int launch_side(LineJob jd, LineJob jc, const SGeo &g, int B, int left, hipStrea
       auto al = [](const float *p) { return !p || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
       const long os = left ? g.sj : g.sk;
       const bool v4 = n % 4 == 0 && g.sb % 4 == 0 && g.sh % 4 == 0 && os % 4 == 0 && al(jd.vol) && al(jc.vol);
-      if (v4) sam_row_kernel<true><<<(unsigned)((nlines + 3) / 4), 256, 0, s>>>(jd, jc, g, left, nlines);
-      else sam_row_kernel<false><<<(unsigned)((nlines + 3) / 4), 256, 0, s>>>(jd, jc, g, left, nlines);
+      const unsigned nb = (unsigned)((nlines + 4 * SAM_LPW - 1) / (4 * SAM_LPW));
+      if (v4) sam_row_kernel<true><<<nb, 256, 0, s>>>(jd, jc, g, left, nlines);
+      else sam_row_kernel<false><<<nb, 256, 0, s>>>(jd, jc, g, left, nlines);
     } else {
       sam_col_kernel<<<(unsigned)((nlines + 63) / 64), 256, 0, s>>>(jd, jc, g, left, nlines);
     }

@@ -96,8 +96,9 @@ class ScheduleOptions:
     # replayed from a hipGraph (graph.ForwardGraph) 82.3 and 77.5-77.7 (scripts/ab_graph.py)
     loop_parts: int = 2
     # ... part i > 0 starting on the GPU after part i - 1's first half iteration (False: all at
-    # once; the same time from a graph, faster eager)
-    loop_offset: bool = False
+    # once).  Replayed from a hipGraph at the bench config: 74.05-74.22 ms/step against
+    # 74.38-74.47 without the offset (three alternating pairs, scripts/ab_graph.py 10 2T 2F ...)
+    loop_offset: bool = True
 
 
 class StereoAnywhere(nn.Module):

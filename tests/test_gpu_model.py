@@ -128,8 +128,9 @@ def test_side_streams_match_one_stream(model):
         assert epe(o, ref) < 1e-5
 
 
+@pytest.mark.parametrize("offset", [True, False])
 @pytest.mark.parametrize("parts", [2, 3])
-def test_loop_parts_match_one_stream(model, parts):
+def test_loop_parts_match_one_stream(model, parts, offset):
     """The GRU loop over batch parts on separate streams (ScheduleOptions.loop_parts; a ragged
     split at B = 3 with 2 parts) gives the one-part result; back-to-back forwards without a
     host sync."""
@@ -141,7 +142,7 @@ def test_loop_parts_match_one_stream(model, parts):
         with torch.no_grad():
             model.opts = dataclasses.replace(old, loop_parts=1)
             ref = -model(*x, iters=6, test_mode=True)[0][:, 0].cpu().numpy()
-            model.opts = dataclasses.replace(old, loop_parts=parts)
+            model.opts = dataclasses.replace(old, loop_parts=parts, loop_offset=offset)
             outs = [model(*x, iters=6, test_mode=True)[0] for _ in range(3)]
             outs = [-o[:, 0].cpu().numpy() for o in outs]
     finally:
