@@ -62,8 +62,6 @@ def step_costs(B: int, H4: int, W4: int, iters: int, C: int = 256):
     px = B * H4 * W4                      # 1/4-res pixels
     vol = px * W4                         # cost-volume cells
     lv = [W4 >> i for i in range(4)]
-    gru_px = B * (H4 * W4 + ((H4 + 1) // 2) * ((W4 + 1) // 2) + ((H4 + 3) // 4) * ((W4 + 3) // 4))
-    hid = 128
     return {
         # fp32 MFMA: 2*C flops per volume cell (a1); epilogue work (trunc, pyramid) is free
         "corr_volume_pyramid": ("TFLOP/s", 2.0 * vol * C),
@@ -75,10 +73,6 @@ def step_costs(B: int, H4: int, W4: int, iters: int, C: int = 256):
         "softargmin_conf": ("GB/s", 2 * vol * 4 + 4 * px * 4),
         # three joint L/R maps read once
         "weighted_lsq": ("GB/s", 3 * 2 * px * 4),
-        # per pixel and GRU level: xc(2C) + hzr(2C) + cz,cr(2C) + h(C) read, z, r*h (2C) written
-        "gru_zr": ("GB/s", iters * gru_px * 9 * hid * 4),
-        # xc_q, qh, cq, z, h read, h written
-        "gru_out": ("GB/s", iters * gru_px * 6 * hid * 4),
         "convex_upsample": ("GB/s", px * (144 + 1) * 4 + px * 16 * 4),
         # the whole mono hourglass + classifier (11 fused conv launches; fp32 FMA), flops
         # per full-res volume cell: full res 1x1x1 24->8, 3x3x3 8->8 (x2), 8->2;
@@ -111,13 +105,36 @@ def make_inputs(B, H, W, Hp, Wp, D, seed0, device):
     return out
 
 
-def host_threads() -> int:
-    """CPU share of this process: OMP_NUM_THREADS if set (16 on the GPU box), else the
-    affinity mask — os.cpu_count() reports the whole machine there."""
+def _cgroup_cpus():
+    """CPUs the cgroup's CFS quota grants (cpu.max 'quota period'), or None without a quota."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(p)))
+    except (OSError, ValueError):
+        return None
+
+
+def host_cpu_share() -> dict:
+    """The host CPUs this process may use: the affinity mask, capped by the cgroup's CPU quota
+    when there is one; OMP_NUM_THREADS (16 on the GPU box) is reported beside them and is
+    the fallback cap when neither the mask nor a quota bounds the share (os.cpu_count() reports
+    the whole machine there)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = _cgroup_cpus()
     env = os.environ.get("OMP_NUM_THREADS")
-    if env and env.isdigit() and int(env) > 0:
-        return int(env)
-    return len(os.sched_getaffinity(0))
+    omp = int(env) if env and env.isdigit() and int(env) > 0 else None
+    if quota is not None:
+        use = min(aff, quota)
+    elif omp is not None and aff >= (os.cpu_count() or aff):
+        use = omp    # the mask is the whole machine: stay within the box's stated share
+    else:
+        use = aff
+    return {"threads": use, "affinity_cpus": aff, "cgroup_quota_cpus": quota, "omp_num_threads": omp}
+
+
+def host_threads() -> int:
+    return host_cpu_share()["threads"]
 
 
 def log(msg: str) -> None:
@@ -156,13 +173,14 @@ def cpu_baseline(iters: int, H: int, W: int, runs: int = 3):
     at cfg1 (256x512, 8 iterations)."""
     from oracle import model_ref as M
 
-    torch.set_num_threads(host_threads())
+    share = host_cpu_share()
+    torch.set_num_threads(share["threads"])
     sd = M.load_state_dict_seeded(0)
     ts = _time_oracle(sd, H, W, iters, 192.0, runs)
     t1 = _time_oracle(sd, 256, 512, 8, 64.0, runs)
     med, med1 = ts[len(ts) // 2], t1[len(t1) // 2]
     return {"value": 1.0 / med, "unit": "pairs/s", "cores": torch.get_num_threads(), "kind": "port",
-            "cpu_model": cpu_model(),
+            "cpu_model": cpu_model(), "cpu_share": share,
             "sample": f"1 pair 1x{H}x{W}, {iters} iters, oracle (torch CPU convs + numpy hot path); "
                       f"1 warm-up + median of {runs}: {', '.join(f'{x:.2f}' for x in ts)} s",
             "cfg1": {"value": 1.0 / med1, "unit": "pairs/s",
@@ -170,22 +188,26 @@ def cpu_baseline(iters: int, H: int, W: int, runs: int = 3):
                                f"{', '.join(f'{x:.2f}' for x in t1)} s"}}
 
 
-def cpu_baseline_tile(cfg, iters: int):
-    """Tiled configs: the oracle on ONE tile of the config (bounded sample), one run."""
-    from oracle import model_ref as M
-
-    torch.set_num_threads(host_threads())
-    sd = M.load_state_dict_seeded(0)
+def cpu_baseline_tile(cfg, iters: int, runs: int = 3):
+    """Tiled configs: the oracle on ONE tile of the config (bounded sample): one warm-up
+    run, then the median of ``runs``."""
+    share = host_cpu_share()
+    torch.set_num_threads(share["threads"])
+    sd = M_load()
     th, tw = cfg["tile_hw"]
-    pair = synth.synthetic_batch(1, th, tw, cfg["D"], seed0=1)
-    t = [torch.from_numpy(pair[k]) for k in ("left", "right", "mono_left", "mono_right")]
-    t0 = time.perf_counter()
-    M.forward(sd, *t, iters=iters)
-    dt = time.perf_counter() - t0
+    ts = _time_oracle(sd, th, tw, iters, cfg["D"], runs)
+    dt = ts[len(ts) // 2]
+    n = cfg["unique_tiles"]
     return {"value": 1.0 / dt, "unit": "tiles/s", "cores": torch.get_num_threads(), "kind": "port",
-            "cpu_model": cpu_model(),
-            "sample": f"1 tile 1x{th}x{tw}, {iters} iters, oracle, one run: {dt:.1f} s "
-                      f"(one image = {cfg['tiles']} tiles -> {1.0 / (dt * cfg['tiles']):.4f} images/s)"}
+            "cpu_model": cpu_model(), "cpu_share": share,
+            "sample": f"1 tile 1x{th}x{tw}, {iters} iters, oracle; 1 warm-up + median of {runs}: "
+                      f"{', '.join(f'{x:.1f}' for x in ts)} s (one image = {n} unique tile forwards -> "
+                      f"{1.0 / (dt * n):.4f} images/s)"}
+
+
+def M_load():
+    from oracle import model_ref as M
+    return M.load_state_dict_seeded(0)
 
 
 def epe_vs_reference(model, device):
@@ -200,21 +222,31 @@ def epe_vs_reference(model, device):
     return float(np.abs(disp.astype(np.float64) - fix["disparity"]).mean())
 
 
-def epe_vs_reference_tiled(model, device, preset: str):
-    """The reference TileWrapper + reference model's two-tile stitch at the preset's tile size
-    (tests/golden/tiled_model.npz, 3 iterations) against this build's tiler + model."""
+def epe_vs_reference_tiled(model, device, config: str):
+    """Against the reference at the tiled configs' own 32 iterations (tests/golden/tiled32.npz):
+    cfg3 = config 3's whole padded 1024x1408 image through this build's tiler (6 tiles, 3 unique)
+    vs the reference TileWrapper + model; cfg5 = one 896x1120 booster tile through the model."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from fixtures_util import load_fixture  # golden data only
     from stereoanywhere_amd import tiler
 
-    fix = load_fixture("tiled_model.npz")
-    H, W, tw, th, ov, iters = (int(v) for v in fix[f"{preset}.geom"])
-    seed = 11 + [c for c in ("middlebury", "booster")].index(preset)
-    pair = synth.synthetic_batch(1, H, W, float(fix[f"{preset}.D"]), seed0=seed)
-    t = [torch.from_numpy(pair[k]).to(device) for k in ("left", "right", "mono_left", "mono_right")]
-    st = tiler.TileWrapper(model, tile_width=tw, tile_height=th, overlap=ov)(*t, iters=iters, test_mode=True)
-    got = st[0, 0, ::int(fix["row_step"])].cpu().numpy()
-    return float(np.abs(got.astype(np.float64) - fix[f"{preset}.out"]).mean())
+    fix = load_fixture("tiled32.npz")
+    step = int(fix["row_step"])
+    if config == "cfg3":
+        H, W, tw, th, ov, seed = (int(v) for v in fix["cfg3.geom"])
+        pair = synth.synthetic_batch(1, H, W, float(fix["cfg3.D"]), seed0=seed)
+        t = [torch.from_numpy(pair[k]).to(device) for k in ("left", "right", "mono_left", "mono_right")]
+        got = tiler.TileWrapper(model, tile_width=tw, tile_height=th, overlap=ov, batch_tiles=True)(
+            *t, iters=32, test_mode=True)
+        ref = fix["cfg3.out"]
+    else:
+        H, W, seed = (int(v) for v in fix["booster_tile.geom"])
+        pair = synth.synthetic_batch(1, H, W, float(fix["booster_tile.D"]), seed0=seed)
+        t = [torch.from_numpy(pair[k]).to(device) for k in ("left", "right", "mono_left", "mono_right")]
+        got = -model(*t, iters=32, test_mode=True)[0]
+        ref = fix["booster_tile.out"]
+    got = got[0, 0, ::step].cpu().numpy()
+    return float(np.abs(got.astype(np.float64) - ref).mean())
 
 
 # the tiled BASELINE configs (SURVEY §8(d)): padded image, preset, iterations
@@ -276,9 +308,11 @@ def main():
         wrap = tiler.from_preset(model, tiled["preset"], batch_tiles=True)
         tiles = wrap._enumerate_tiles(Hp, Wp)
         th, tw = min(wrap.tile_height, Hp), min(wrap.tile_width, Wp)
-        tiled["tiles"], tiled["tile_hw"] = len(tiles), (th, tw)
+        # the tiler runs each unique rectangle once (tiler.TileWrapper: duplicates are
+        # accumulated again, not recomputed)
+        tiled["tiles"], tiled["unique_tiles"], tiled["tile_hw"] = len(tiles), len(set(tiles)), (th, tw)
         runner = CPUOffloadWrapper(wrap) if tiled["offload"] else wrap
-        units, shape = 1, (len(tiles), th // 4, tw // 4)
+        units, shape = 1, (len(set(tiles)), th // 4, tw // 4)
 
     eager_runner = runner
     if args.one_stream:
@@ -328,8 +362,14 @@ def main():
         graph_dev = None
         if runner is not eager_runner:   # the replayed forward is the eager one
             graph_dev = float((out[0] - out_e[0]).abs().max())
-        # one-stream plain steps: the schedule the per-launch times below are measured in
+            if graph_dev != 0.0:
+                raise SystemExit(f"bench: the hipGraph replay differs from the eager forward by {graph_dev:g} "
+                                 "(it must compute the same function bit for bit); no throughput reported")
+        # one-stream plain steps: the schedule the per-launch times below are measured in.  One
+        # untimed step first: the whole batch per launch is a new set of shapes (allocator
+        # growth, MIOpen kernels built on first use: cfg5's first one-stream steps ran 2.7x slow)
         model.stream_overlap = False
+        eager_step()
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         for _ in range(args.steps):
@@ -365,6 +405,10 @@ def main():
     costs["conv2d_wino4"] = ("TFLOP/s", work.get("conv2d_wino4", 0.0))
     costs["conv2d_direct"] = ("TFLOP/s", work.get("conv2d_direct", 0.0))
     costs["norm_act"] = ("GB/s", work.get("norm_act", 0.0))
+    # the separate GRU gate kernels run only at levels whose width keeps the gates out of the
+    # F(4x4) epilogues (W % 4 != 0): priced per call (ops.gru_zr / gru_out, 9 resp. 6-7 planes)
+    costs["gru_zr"] = ("GB/s", work.get("gru_zr", 0.0))
+    costs["gru_out"] = ("GB/s", work.get("gru_out", 0.0))
     kernels = {}
     for k, (ms_tot, n_launch) in kt.items():
         if n_launch == 0 or k not in costs:
@@ -406,10 +450,12 @@ def main():
     else:
         metric, unit = f"stereo images/sec, tiled ({args.config}) + EPE vs reference", "images/s"
         config = {"workload": f"configs[{tiled['index']}]: 1 image/GPU {H}x{W} (padded {Hp}x{Wp}), preset "
-                              f"{tiled['preset']} -> {tiled['tiles']} tiles of {th}x{tw} (batch_tiles), "
+                              f"{tiled['preset']} -> {tiled['tiles']} tiles of {th}x{tw} ({tiled['unique_tiles']} unique rectangles, "
+                              f"each run once; batch_tiles), "
                               f"{iters} GRU iters, published flags"
                               + (", CPUOffloadWrapper (HBM-resident)" if tiled["offload"] else ""),
-                  "global_batch": r.world, "tiles_per_image": tiled["tiles"], "iters": iters,
+                  "global_batch": r.world, "tiles_per_image": tiled["tiles"],
+                  "unique_tile_forwards_per_image": tiled["unique_tiles"], "iters": iters,
                   "parallelism": f"dp{r.world} (independent images)"}
     res = {
         "metric": metric, "value": total_units / elapsed, "unit": unit, "n_gpus": r.world, "steps": args.steps,
@@ -425,9 +471,10 @@ def main():
         res["graph_vs_eager_max_abs"] = graph_dev
     if tiled is not None:
         res["tiles_per_s"] = total_units * tiled["tiles"] / elapsed
+        res["unique_tile_forwards_per_s"] = total_units * tiled["unique_tiles"] / elapsed
     if not args.no_epe:
         res["epe_vs_reference"] = (epe_vs_reference(model, device) if tiled is None
-                                   else epe_vs_reference_tiled(model, device, tiled["preset"]))
+                                   else epe_vs_reference_tiled(model, device, args.config))
         log(f"EPE vs reference {res['epe_vs_reference']:.3g}")
     if r.world == 1 and not args.no_cpu_baseline:
         log("cpu baseline (oracle, bounded sample) ...")

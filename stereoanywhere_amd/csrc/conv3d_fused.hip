@@ -493,7 +493,9 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
   for (int ci = 0; ci < CIN; ++ci) {
     const int buf = ci & 1;
     if (ci + 1 < CIN) fetch(ci + 1);
-    const float *lb = slab[buf] + wv * ROWP + lane * NP;
+    // lanes 62-63 (no output column) read lane 61's columns: lane + kw stays inside the 64
+    // staged columns of the row
+    const float *lb = slab[buf] + wv * ROWP + min(lane, TWV - 1) * NP;
     const float *wc = wt + (long)ci * 9 * 6 * COUT;
     // the kw loop unrolled for the 16-channel convs and the classifier pair (the scalar weight
     // loads of the next kw then overlap this one's FMAs: 711 -> 567 and 568 -> 506 us), rolled

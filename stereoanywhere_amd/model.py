@@ -380,8 +380,11 @@ class StereoAnywhere(nn.Module):
                     if first[i] is None:
                         first[i] = torch.cuda.Event()
                         first[i].record(st)
-        for st in streams:
+        for st, r in zip(streams, results):
             main.wait_stream(st)
+            # each part's output was allocated on its loop stream and is read by the cat on
+            # main: keep the caching allocator from handing it back to that stream early
+            r[0].record_stream(main)
         return torch.cat([r[0] for r in results], 0), None
 
     def _loop_stream(self, dev, i: int):
@@ -424,23 +427,27 @@ class StereoAnywhere(nn.Module):
         # ---- mono cost volume -> 3-D hourglass -> classifiers (native [B,C,W2,H,W1] layout)
         # the fused hourglass reads the one-hot masked volume through per-pixel records (its two
         # readers evaluate the cells); the torch path materialises it
+        # stack[i] for i < n_additional (stereoanywhere.py:163-164): stack[0] is the identity,
+        # so only n_additional >= 2 puts a real hourglass after hourglass_mono
+        extra = [self.hourglass_mono_stack[i] for i in range(a.n_additional_hourglass)
+                 if not isinstance(self.hourglass_mono_stack[i], HourglassIdentity)]
         if vd > 0:
             # stereoanywhere.py:141-145: the raw volume (trilinear) and the masks (nearest) at
             # 1/2^vd, masked as a dense volume (the downsampled cells are no longer a product of
             # per-pixel terms)
             vol = (1.73 * ops.corr_volume(n2, n3)).view(B, 1, H4, W4, W4)
             masked = self._masked_dense(vol, m2l, m3l, vd)
+            fuse = not extra and a.vol_n_masks == 8 and self.hourglass_mono.fusable(masked, feats_l)
         else:
-            masked = ops.OneHotVolume(n2, n3, m2l, m3l, a.vol_n_masks, 1.73)
-        # stack[i] for i < n_additional (stereoanywhere.py:163-164): stack[0] is the identity,
-        # so only n_additional >= 2 puts a real hourglass after hourglass_mono
-        extra = [self.hourglass_mono_stack[i] for i in range(a.n_additional_hourglass)
-                 if not isinstance(self.hourglass_mono_stack[i], HourglassIdentity)]
-        if not extra and a.vol_n_masks == 8 and self.hourglass_mono.fusable(masked, feats_l):
+            # the one-hot records only where the fused hourglass will read them; the torch path
+            # gets the materialised volume
+            shape = SimpleNamespace(shape=(B, a.vol_n_masks, W4, H4, W4))
+            fuse = not extra and a.vol_n_masks == 8 and self.hourglass_mono.fusable(shape, feats_l)
+            masked = (ops.OneHotVolume(n2, n3, m2l, m3l, a.vol_n_masks, 1.73) if fuse
+                      else ops.mono_masked_volume(n2, n3, m2l, m3l, a.vol_n_masks, 1.73))
+        if fuse:
             vol_d, vol_c = self.hourglass_mono(masked, feats_l, feats_r, fused=dw["hg"])
         else:
-            if isinstance(masked, ops.OneHotVolume):
-                masked = ops.mono_masked_volume(n2, n3, m2l, m3l, a.vol_n_masks, 1.73)
             agg = self.hourglass_mono(masked, feats_l, feats_r)
             for hg in extra:
                 agg = hg(agg, feats_l, feats_r)
@@ -548,27 +555,31 @@ class StereoAnywhere(nn.Module):
         xdims = {"08": 256, "16": 256, "32": 128}
         shapes = {"08": (H4, W4), "16": (H8, W8), "32": (H16, W16)}
         hd = h08.shape[1]
-        # the F(4x4) kernel's preconditions at every level (W % 4; planes then stay 16-byte aligned)
         o = self.opts
-        fused = o.fuse_gates and ops.gate_f4_ok() and all(s[1] % 4 == 0 for s in shapes.values())
-        if fused:
-            # one buffer per level, [h | x | r*h]: the z/r conv reads cat(h, x) and the r*h conv
-            # reads r*h as channel views of it (no torch.cat)
-            hxr = {k: torch.empty((B, 2 * hd + xdims[k], *shapes[k]), device=dev, dtype=f32) for k in shapes}
-            for k, h in zip(("08", "16", "32"), hid):
+        # GRU gates in the F(4x4) conv epilogues, per level: the kernel's preconditions (W % 4,
+        # planes then 16-byte aligned) hold or fail per level.  A level with W % 4 != 0 (e.g.
+        # W/16 = 42 or 70 at the middlebury / booster tile presets) keeps the separate gate
+        # kernels and its convs run on F(2x2) in launches of their own (ops.conv2d_k3_multi
+        # splits a mixed group), while the other levels stay on the fused path.
+        fused = {k: o.fuse_gates and ops.gate_f4_ok() and s[1] % 4 == 0 for k, s in shapes.items()}
+        fuse_out = {k: fused[k] and o.fuse_out for k in shapes}
+        hxr, xq, rh, xs = {}, {}, {}, {}
+        for k, h in zip(("08", "16", "32"), hid):
+            if fused[k]:
+                # one buffer per level, [h | x | r*h]: the z/r conv reads cat(h, x) and the r*h
+                # conv reads r*h as channel views of it (no torch.cat)
+                hxr[k] = torch.empty((B, 2 * hd + xdims[k], *shapes[k]), device=dev, dtype=f32)
                 hxr[k][:, :hd].copy_(h)
-            h08, h16, h32 = (hxr[k][:, :hd] for k in ("08", "16", "32"))
-            x08, x16, x32 = (hxr[k][:, hd:hd + xdims[k]] for k in ("08", "16", "32"))
-            rh = {k: hxr[k][:, hd + xdims[k]:] for k in shapes}
-            # convq's x part lands in channels 2*hd.. of a [B, 3*hd] buffer: gru_out reads it there
-            xq = {k: torch.empty((B, 3 * hd, *shapes[k]), device=dev, dtype=f32) for k in shapes}
-        else:
-            x08 = torch.empty((B, xdims["08"], H4, W4), device=dev, dtype=f32)
-            x16 = torch.empty((B, xdims["16"], H8, W8), device=dev, dtype=f32)
-            x32 = torch.empty((B, xdims["32"], H16, W16), device=dev, dtype=f32)
-            rh = {k: torch.empty_like(h) for k, h in (("08", h08), ("16", h16), ("32", h32))}
+                xs[k] = hxr[k][:, hd:hd + xdims[k]]
+                rh[k] = hxr[k][:, hd + xdims[k]:]
+                # convq's x part lands in channels 2*hd.. of a [B, 3*hd] buffer: gru_out reads it there
+                xq[k] = torch.empty((B, 3 * hd, *shapes[k]), device=dev, dtype=f32)
+            else:
+                xs[k] = torch.empty((B, xdims[k], *shapes[k]), device=dev, dtype=f32)
+                rh[k] = torch.empty_like(h)
+        h08, h16, h32 = (hxr[k][:, :hd] if fused[k] else h for k, h in zip(("08", "16", "32"), hid))
+        x08, x16, x32 = xs["08"], xs["16"], xs["32"]
         hs = {"08": h08, "16": h16, "32": h32}
-        fuse_out = fused and o.fuse_out
         z = {k: torch.empty(h.shape, device=dev, dtype=f32) for k, h in hs.items()}
         cz = [c[:, 0:128] for c in ctx]
         cr = [c[:, 128:256] for c in ctx]
@@ -583,7 +594,7 @@ class StereoAnywhere(nn.Module):
 
         def gate_x_h(key, x, h):
             g = dw["g" + key]
-            if fused:
+            if fused[key]:
                 # convz | convr over cat(h, x) (+ bias) with z = sigmoid(. + cz) and r*h = sigmoid(. + cr) * h
                 # in the epilogue (update.py:24-25); convq's x part (bias added in gru_out)
                 hx = hxr[key][:, :hd + xdims[key]]
@@ -594,11 +605,11 @@ class StereoAnywhere(nn.Module):
             return [dict(x=x, U=g["Ux"]), dict(x=h, U=g["Uhzr"])]
 
         def gru_zr(level, key, h, xc, hzr):
-            if not fused:   # else done in the conv epilogue
+            if not fused[key]:   # else done in the conv epilogue
                 ops.gru_zr(xc, hzr, cz[level], cr[level], h, z[key], rh[key], bx=dw["g" + key]["bx"])
 
         def gru_out(level, key, h, xc, qh, qh2=None):
-            ops.gru_out(xq[key] if fused else xc, qh, cq[level], z[key], h, bx=dw["g" + key]["bx"], qh2=qh2)
+            ops.gru_out(xq[key] if fused[key] else xc, qh, cq[level], z[key], h, bx=dw["g" + key]["bx"], qh2=qh2)
 
         def qh_split(key):
             """r*h conv of one GRU as two half-Cin problems (more, shorter blocks: the launch's
@@ -611,14 +622,14 @@ class StereoAnywhere(nn.Module):
             """convq's r*h part: with the state update h = (1 - z) h + z tanh(. + x part + cq) in
             its epilogue (one problem, in place on h), else plain problem(s) (split over Cin when
             ``split``) whose sums q_finish hands to gru_out."""
-            if fuse_out:
+            if fuse_out[key]:
                 g = dw["g" + key]
                 return [dict(x=rh[key], U=g["Uqh"], bias=g["bx"][2 * hd:], out=hs[key],
                              gate=dict(mode=2, ctx=cq[lvl[key]], h=hs[key], z=z[key], add=xq[key][:, 2 * hd:]))]
             return qh_split(key) if split else [dict(x=rh[key], U=dw["g" + key]["Uqh"])]
 
         def q_finish(level, key, xc, res):
-            if not fuse_out:
+            if not fuse_out[key]:
                 gru_out(level, key, hs[key], xc, *res)
 
         ops.flow_update(coords_x, None, flow, x08[:, 126:128])

@@ -312,6 +312,8 @@ def gru_zr(xc, hzr, cz, cr, h, z_out, rh_out, bx: Optional[torch.Tensor] = None)
     N.call("sa_gru_zr", xc.data_ptr(), _plane_bs(xc, "xc"), _ptr(bx), hzr.data_ptr(), _plane_bs(hzr, "hzr"),
            cz.data_ptr(), cr.data_ptr(), _plane_bs(cz, "cz"), h.data_ptr(), _plane_bs(h, "h"), B, C, H * W,
            z_out.data_ptr(), rh_out.data_ptr(), _stream(h))
+    # xc (z, r), hzr (z, r), cz, cr, h read; z, r*h written
+    _account("gru_zr", 4.0 * 9 * B * C * H * W)
 
 
 def gru_out(xc, qh, cq, z, h, bx: Optional[torch.Tensor] = None, qh2: Optional[torch.Tensor] = None):
@@ -323,6 +325,8 @@ def gru_out(xc, qh, cq, z, h, bx: Optional[torch.Tensor] = None, qh2: Optional[t
     N.call("sa_gru_out_split", xc.data_ptr(), _plane_bs(xc, "xc"), _ptr(bx), qh.data_ptr(), _ptr(qh2),
            _plane_bs(qh, "qh"), cq.data_ptr(), _plane_bs(cq, "cq"), z.data_ptr(), B, C, H * W, h.data_ptr(),
            _plane_bs(h, "h"), _stream(h))
+    # xc_q, qh (+ qh2), cq, z, h read; h written
+    _account("gru_out", 4.0 * (6 + (qh2 is not None)) * B * C * H * W)
 
 
 def pool2x(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
@@ -453,7 +457,7 @@ def conv3d_wd_weights(w_t: torch.Tensor) -> torch.Tensor:
 
 
 def conv3d_wd(x: "VolAct", w_wd: torch.Tensor, cout: int, slope: float = 0.01, stats: bool = True) -> "VolAct":
-    """ops.conv3d at stride 1 for 8 input channels (-> 8 or 2) on the F(4,3)-along-D kernel;
+    """ops.conv3d at stride 1 for 8 input channels (-> 8 or 2) or 16 -> 16 on the F(4,3)-along-D kernel;
     w_wd from conv3d_wd_weights.  The input must carry an InstanceNorm + LeakyReLU (+ gate)."""
     _check(x.raw, "x")
     _check(w_wd, "w_wd")
@@ -737,8 +741,9 @@ def _gate_epilogue(p: dict) -> "N.SaGateEpilogue":
 def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     """Independent conv2d_k3 calls (each a dict of conv2d_k3's keyword arguments) in ONE launch:
     their blocks share the grid, so each conv's partly filled last round of blocks is filled by
-    the others.  On the F(4x4,3x3) kernel when every problem meets its preconditions, else on
-    F(2x2,3x3), where all must agree on Cout % 64 == 0 and on having an input transform or not.
+    the others.  On the F(4x4,3x3) kernel when every problem meets its preconditions; a group
+    that mixes eligible and ineligible problems is split into an F(4x4) and an F(2x2) launch;
+    on F(2x2,3x3) all must agree on Cout % 64 == 0 and on having an input transform or not.
     A problem with a ``gate`` (_gate_epilogue) puts the launch on F(4x4,3x3) whatever its size.
     small_blocks: F(4x4)'s small block shape (two blocks per CU) for this launch."""
     if not 1 <= len(problems) <= 8:
@@ -748,7 +753,20 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     for p, q in zip(problems, plain):
         if p.get("gate") and p["gate"]["mode"] == 1:
             q["out_cout"] = p["U"].cout // 2   # z only: r*h goes to the gate's out2
-    ok4 = _WINO4 and all(_wino4_ok(**p) for p in plain)
+    oks = [_WINO4 and _wino4_ok(**p) for p in plain]
+    if any(oks) and not all(oks):
+        # a mixed group: the problems F(4x4) cannot take (W % 4 != 0, unaligned planes) go to a
+        # launch of their own instead of demoting the whole group to F(2x2) — unless the F(4x4)
+        # part is too small for F(4x4) anyway (then one F(2x2) launch of all of them)
+        four = [i for i, k in enumerate(oks) if k]
+        if gated or sum(_wino4_blocks(**plain[i]) for i in four) >= _WINO4_MIN_BLOCKS:
+            two = [i for i, k in enumerate(oks) if not k]
+            res = [None] * len(problems)
+            for idx in (four, two):
+                for i, r in zip(idx, conv2d_k3_multi(*[problems[i] for i in idx], small_blocks=small_blocks)):
+                    res[i] = r
+            return res
+    ok4 = all(oks)
     if gated and not ok4:
         raise RuntimeError("conv2d_k3_multi: gate epilogues need the F(4x4,3x3) kernel (gate_f4_ok)")
     f4 = ok4 and (gated or sum(_wino4_blocks(**p) for p in plain) >= _WINO4_MIN_BLOCKS)

@@ -17,7 +17,9 @@ Mirrors the reference's mapreduce_v2 package so results stitch identically:
     (56-99) and the VRAM heuristic of memory_utils.py:34-57.
   * ``to_uint8_image`` — the harness's clip / x255 / truncating cast
     (test_mapreduce_v2.py:163-175).
-Multi-GPU: with ``rank``/``world`` set, rank r processes tiles r, r+world, ...; the partial
+Duplicate rectangles of the enumeration run once and are accumulated once per occurrence,
+in the reference's order.
+Multi-GPU: with ``rank``/``world`` set, rank r processes unique tiles r, r+world, ...; the partial
 stitched and weight maps are summed with one all_reduce (RCCL over xGMI) — the tiled
 path's only exchange.
 
@@ -223,9 +225,16 @@ class TileWrapper(torch.nn.Module):
                 raise ValueError("global_guidance must match the input's spatial shape")
         device = self.device
         tiles = self._enumerate_tiles(H, W)
+        # The enumeration can emit one rectangle twice (the last row / column is pushed back
+        # inside the image: config 3's 1024-row image gives rows y = 0 and y = 992 both as
+        # 0..1024).  Each unique rectangle runs once; the accumulation below still visits the
+        # tiles in the reference's order, so a duplicate adds the same d * w again and the
+        # stitched sums equal the reference's (tile_wrapper.py:169-185) term for term.
+        unique = list(dict.fromkeys(tiles))
+        self.last_tile_counts = (len(tiles), len(unique))
         stitched = torch.zeros((1, 1, H, W), device=device, dtype=torch.float32)
         weight = torch.zeros_like(stitched)
-        mine = tiles[self.rank::self.world]
+        mine = unique[self.rank::self.world]
 
         def view(t, s):
             return None if t is None else t[:, :, s.y_start:s.y_end, s.x_start:s.x_end]
@@ -240,13 +249,22 @@ class TileWrapper(torch.nn.Module):
         else:
             outs = [self._run(view(left, s), view(right, s), view(mono_left, s), view(mono_right, s), args, kw)
                     for s in mine]
+        done = {}
         for s, d in zip(mine, outs):
             d = d.detach().to(device)
             if d.shape[-2:] != (s.height, s.width):
                 raise ValueError("Tile output spatial size mismatch")
-            wgt = blend_weight(s.height, s.width, d.device)[None, None]
             if guide is not None:
                 d = guidance_blend(d, view(guide, s).to(d.device, d.dtype), guidance_weight)
+            done[s] = d
+        wgts = {}
+        for s in tiles:
+            d = done.get(s)
+            if d is None:   # another rank's rectangle
+                continue
+            wgt = wgts.get((s.height, s.width))
+            if wgt is None:
+                wgt = wgts[(s.height, s.width)] = blend_weight(s.height, s.width, d.device)[None, None]
             stitched[:, :, s.y_start:s.y_end, s.x_start:s.x_end] += d * wgt
             weight[:, :, s.y_start:s.y_end, s.x_start:s.x_end] += wgt
         if self.world > 1:

@@ -511,6 +511,55 @@ def tiled_model_cases(sa_mod, model):
     return out
 
 
+# (name, H, W, D, seed): single tiles at the tiled configs' own shapes and iteration count
+# (test_mapreduce_v2.py:56 / run_test_contextaware_mapreduce.py:69 run --iters 32): the
+# middlebury preset's 1024x672 tile of a 1024-row image (W/16 = 42) and the booster preset's
+# 896x1120 tile (W/16 = 70) — GRU levels whose width is not a multiple of 4
+TILED32_CASES = [("mb_tile", 1024, 672, 256.0, 31), ("booster_tile", 896, 1120, 512.0, 32)]
+# config 3's whole padded image through the reference TileWrapper (middlebury preset): its
+# tile grid emits every rectangle twice (y = 0 and y = 992 both clamp to rows 0..1024)
+CFG3_IMAGE = (1024, 1408, 672, 1120, 128, 256.0, 33)
+TILED32_ROW_STEP = 8
+
+
+def tiled32_cases(sa_mod, model):
+    """The reference model at 32 GRU iterations on one tile of each tiled config, and the
+    reference TileWrapper over config 3's whole image (6 tiles, 3 unique rectangles).  Outputs
+    keep every TILED32_ROW_STEP-th row."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_tile_wrapper", os.path.join(REF, "mapreduce_v2", "tile_wrapper.py"))
+    tw = importlib.util.module_from_spec(spec)
+    sys.modules["ref_tile_wrapper"] = tw
+    spec.loader.exec_module(tw)
+    restore = _single_thread_lsq(sa_mod)
+    out = {"row_step": np.array(TILED32_ROW_STEP), "iters": np.array(32)}
+    for name, H, W, D, seed in TILED32_CASES:
+        pair = synth.synthetic_batch(1, H, W, D, seed0=seed)
+        t = [torch.from_numpy(pair[k]) for k in ("left", "right", "mono_left", "mono_right")]
+        with torch.no_grad():
+            d = -model(*t, iters=32, test_mode=True)[0]
+        out[f"{name}.geom"] = np.array([H, W, seed], np.int64)
+        out[f"{name}.D"] = np.array(D)
+        out[f"{name}.out"] = _np(d)[0, 0, ::TILED32_ROW_STEP].astype(np.float32)
+        out.update(_pair_record(pair, f"{name}."))
+        print(name, "range", float(d.min()), float(d.max()), flush=True)
+    H, W, tw_, th, ov, D, seed = CFG3_IMAGE
+    pair = synth.synthetic_batch(1, H, W, D, seed0=seed)
+    t = [torch.from_numpy(pair[k]) for k in ("left", "right", "mono_left", "mono_right")]
+    wrap = tw.TileWrapper(model, tile_width=tw_, tile_height=th, overlap=ov)
+    tiles = wrap._enumerate_tiles(H, W)
+    with torch.no_grad():
+        st = wrap(*t, iters=32, test_mode=True)
+    out["cfg3.geom"] = np.array([H, W, tw_, th, ov, seed], np.int64)
+    out["cfg3.D"] = np.array(D)
+    out["cfg3.tiles"] = np.array([[s.y_start, s.y_end, s.x_start, s.x_end] for s in tiles])
+    out["cfg3.out"] = _np(st)[0, 0, ::TILED32_ROW_STEP].astype(np.float32)
+    out.update(_pair_record(pair, "cfg3."))
+    print("cfg3 tiles", len(tiles), "range", float(st.min()), float(st.max()), flush=True)
+    restore()
+    return out
+
+
 def harness_csv_cases():
     """The reference test.py's write_csv_header / write_csv_row (test.py:251-274) on fixed
     metric dicts.  test.py parses argv and builds models at import, so only those two
@@ -700,7 +749,7 @@ def dav2_cases():
 
 
 def main(only=None):
-    """``python tests/golden/make_golden.py [wide] [tiled] [csv] [offload] [flags] [dav2]`` regenerates
+    """``python tests/golden/make_golden.py [wide] [tiled] [tiled32] [csv] [offload] [flags] [dav2]`` regenerates
     just the named round-2 fixtures; no argument regenerates everything."""
     torch.set_num_threads(8)
     sa_mod, ut, corr_mod = _load_reference()
@@ -710,6 +759,8 @@ def main(only=None):
             np.savez_compressed(os.path.join(HERE, "wide_96x1152_it4.npz"), **wide_case(sa_mod, ut, corr_mod, model))
         if "tiled" in only:
             np.savez_compressed(os.path.join(HERE, "tiled_model.npz"), **tiled_model_cases(sa_mod, model))
+        if "tiled32" in only:
+            np.savez_compressed(os.path.join(HERE, "tiled32.npz"), **tiled32_cases(sa_mod, model))
         if "csv" in only:
             with open(os.path.join(HERE, "harness_csv.json"), "w") as f:
                 json.dump(harness_csv_cases(), f, indent=1)
@@ -722,6 +773,7 @@ def main(only=None):
         return
     np.savez_compressed(os.path.join(HERE, "wide_96x1152_it4.npz"), **wide_case(sa_mod, ut, corr_mod, model))
     np.savez_compressed(os.path.join(HERE, "tiled_model.npz"), **tiled_model_cases(sa_mod, model))
+    np.savez_compressed(os.path.join(HERE, "tiled32.npz"), **tiled32_cases(sa_mod, model))
     with open(os.path.join(HERE, "harness_csv.json"), "w") as f:
         json.dump(harness_csv_cases(), f, indent=1)
     np.savez_compressed(os.path.join(HERE, "offload.npz"), **offload_cases())

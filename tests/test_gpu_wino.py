@@ -171,8 +171,9 @@ def test_wino4_input_transform(monkeypatch, small):
 
 def test_wino4_multi_stats_views(monkeypatch):
     """Three convolutions of different geometries in one F(4x4) launch (8 x 128 and 16 x 64
-    blocks), a channel-slice input and output, InstanceNorm statistics; an ineligible problem
-    (W % 4 != 0) sends the whole launch to the F(2x2) kernel."""
+    blocks), a channel-slice input and output, InstanceNorm statistics; a group with an
+    ineligible problem (W % 4 != 0) is split: the eligible ones stay on F(4x4), the other runs
+    on F(2x2) — unless the eligible part is below F(4x4)'s block threshold (then all on F(2x2))."""
     g = torch.Generator(device="cpu").manual_seed(41)
 
     def r(*s):
@@ -195,10 +196,23 @@ def test_wino4_multi_stats_views(monkeypatch):
     torch.testing.assert_close(mean, ref_c.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(rstd, torch.rsqrt(ref_c.var(dim=(2, 3), unbiased=False) + 1e-5).flatten(),
                                atol=1e-4, rtol=1e-4)
-    (yd, ye), work = _run(monkeypatch, True, dict(x=xb, U=ops.wino_weights(wb)),
-                          dict(x=r(1, 128, 9, 37), U=ops.wino_weights(wb)))
+    xe = r(1, 128, 9, 37)
+    (yd, ye), work = _run(monkeypatch, True, dict(x=xb, U=ops.wino_weights(wb)), dict(x=xe, U=ops.wino_weights(wb)))
+    assert work["conv2d_wino4"] == 2.0 * 36 * 128 * 128 * 3 * 9 * 15        # xb: 3 x 9 x 15 F(4x4) tiles
+    assert work["conv2d_wino"] == 2.0 * 16 * 128 * 128 * 1 * 5 * 19         # xe: 5 x 19 F(2x2) tiles
+    torch.testing.assert_close(yd, F.conv2d(xb, wb, padding=1), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(ye, F.conv2d(xe, wb, padding=1), atol=2e-5, rtol=1e-4)
+    # the eligible part below the threshold: one F(2x2) launch of both
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 10 ** 6)
+    ops.WORK = {}
+    try:
+        yd, ye = ops.conv2d_k3_multi(dict(x=xb, U=ops.wino_weights(wb)), dict(x=xe, U=ops.wino_weights(wb)))
+        work = dict(ops.WORK)
+    finally:
+        ops.WORK = None
     assert "conv2d_wino" in work and "conv2d_wino4" not in work
     torch.testing.assert_close(yd, F.conv2d(xb, wb, padding=1), atol=2e-5, rtol=1e-4)
+    torch.testing.assert_close(ye, F.conv2d(xe, wb, padding=1), atol=2e-5, rtol=1e-4)
 
 
 @pytest.mark.parametrize("wide", [False, True, "quad"])
