@@ -372,10 +372,14 @@ def main():
         eager_step()
         torch.cuda.synchronize()
         t2 = time.perf_counter()
+        one_stream_steps = []
         for _ in range(args.steps):
+            ts = time.perf_counter()
             eager_step()
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            one_stream_steps.append((time.perf_counter() - ts) * 1e3)
         elapsed_1s = time.perf_counter() - t2
+        log("one-stream steps (ms): " + ", ".join(f"{v:.1f}" for v in one_stream_steps))
         # per-launch times of one kernel at a time: the side streams' overlap (model.py) would
         # stretch each launch by the work running beside it
         N.timing_enable(True)
@@ -428,6 +432,7 @@ def main():
                  "kernels": kernels, "misc_ms_per_step": kt["misc"][0] / args.steps,
                  "schedule": "one-stream (model.stream_overlap = False)",
                  "one_stream_ms_per_step": elapsed_1s / args.steps * 1e3,
+                 "one_stream_step_ms": one_stream_steps,
                  "instrumented_ms_per_step": elapsed_ev / args.steps * 1e3,
                  "note": "achieved = algorithmic amount per launch / mean live HIP-event launch time, "
                          "events recorded around every launch over K steps run right after the K "

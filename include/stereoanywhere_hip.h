@@ -110,6 +110,10 @@ int sa_mono_bin_records(const float *normals, const float *m, int B, int H, int 
 int sa_softargmin_conf(const float *vol_disp, const float *vol_conf, int B, int H, int W1,
                        int W2, long sb, long sh, long sj, long sk, float *dL, float *dR,
                        float *cL, float *cR, long out_bs, void *stream);
+/* With sj == 1 and W1 == W2 <= 288 (the model's layout) sa_softargmin_conf reads each volume
+ * once: a workgroup per (b, h) slice forms both sides' reductions.  on = 0 selects the
+ * per-line kernels instead (two launches, each reading both volumes); for A/B runs and tests. */
+void sa_softargmin_set_one_pass(int on);
 
 /* a7 — softlrc (utils.py:189-198) with disp_warping (utils.py:172-187); optional
  * fuzzy_and with a confidence (utils.py:240-241, stereoanywhere.py:188-189):
@@ -173,6 +177,13 @@ int sa_pool2x(const float *in, long in_bs, int B, int C, int H, int W, float *ou
               void *stream);
 int sa_interp_bilinear_ac(const float *in, long in_bs, int B, int C, int H, int W, int Ho, int Wo,
                           float *out, long out_bs, void *stream);
+/* The same on pitched planes ([H][in_pitch] in, [Ho][out_pitch] out; pitch >= width; columns
+ * beyond the width are neither read nor written): the padded planes of a GRU level whose width
+ * is not a multiple of 4 (SaWinoProblem.pitch). */
+int sa_pool2x_p(const float *in, long in_bs, int in_pitch, int B, int C, int H, int W, float *out,
+                long out_bs, int out_pitch, void *stream);
+int sa_interp_bilinear_ac_p(const float *in, long in_bs, int in_pitch, int B, int C, int H, int W,
+                            int Ho, int Wo, float *out, long out_bs, int out_pitch, void *stream);
 int sa_relu_copy(const float *in, long in_bs, int B, int C, int HW, float *out, long out_bs,
                  void *stream);
 int sa_flow_update(float *coords_x, const float *delta, long delta_bs, int B, int H, int W,
@@ -186,6 +197,22 @@ int sa_corr_lookup_conv1x1(const float *pyramid_a, const float *pyramid_b, int W
                            int num_levels, int radius, const float *coords_x, long coords_bstride,
                            int B, int H, int W1, const float *weight_kc, const float *bias, int Cout,
                            float *out, void *stream);
+/* a10 on a disparity-sheared copy of the pyramid (csrc/corr_shear.hip): level l of image row
+ * (b, h) as S_l[e][j] = C_l[j][(j >> l) - e + W_l - 1], e in [0, W_l + ((W1 - 1) >> l)), cells
+ * outside [0, W_l) stored as 0, levels back to back in a slice of sa_shear_slice_size floats
+ * per image row: a wave's neighbouring pixels then read neighbouring addresses.
+ *   sa_corr_pyramid_shear: the row-layout pyramid [B*H*W1][row_stride] -> sheared [B*H][slice]
+ *   sa_corr_lookup_conv1x1_sheared: sa_corr_lookup_conv1x1 on sheared pyramids (same taps,
+ *     same arithmetic; 4 levels, radius 4, Cout 64). */
+long sa_shear_slice_size(int W1, int W2, int num_levels);
+long sa_shear_level_offset(int W1, int W2, int num_levels, int level);
+int sa_corr_pyramid_shear(const float *pyramid, long row_stride, int B, int H, int W1, int W2,
+                          int num_levels, float *sheared, void *stream);
+int sa_corr_lookup_conv1x1_sheared(const float *sheared_a, const float *sheared_b, int W2,
+                                   int num_levels, int radius, const float *coords_x,
+                                   long coords_bstride, int B, int H, int W1,
+                                   const float *weight_kc, const float *bias, int Cout,
+                                   float *out, void *stream);
 
 /* a14 — convex_upflow (utils.py:97-110), factor 4: flow [B,1,H,W] (low-res x flow),
  * mask [B, 9*f*f, H, W] -> out [B,1,f*H,f*W] (sign as given: the reference's
@@ -234,6 +261,10 @@ int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W, const flo
                  int Cout, const float *in_mean, const float *in_rstd, int act, float slope,
                  const float *gate_l, const float *gate_r, float *out, double *stats_partial,
                  void *stream);
+/* sa_conv3d_wd's weight staging: 0 (default) wave-uniform scalar loads; 1 the per-channel
+ * weights go through LDS with the input slab, a channel ahead (measured slower).  For A/B runs
+ * and tests. */
+void sa_conv3d_wd_set_variant(int lds_weights);
 /* The hourglass's two readers of the masked mono volume (down_layers[0][0], hourglass.py:27-33;
  * final_agg[0] over cat(orig, up(x)), hourglass.py:326-328) on the one-hot volume given by its
  * records (sa_mono_bin_records; rec_l [B,H,W] of the left pixels = the volume's W axis, rec_r
@@ -307,6 +338,11 @@ typedef struct SaWinoProblem {
   float *out;
   long out_bs;
   double *stats_partial;
+  /* row pitch (floats) of the input, output and gate planes when it differs from W (0 = W):
+   * planes are [H][pitch] with columns W .. pitch - 1 zero in the input (they act as the right
+   * zero padding) and kept zero in every output.  F(4x4) only (pitch % 4 == 0): a GRU level
+   * whose width is not a multiple of 4 runs on it with its planes padded to a multiple of 4. */
+  int pitch;
 } SaWinoProblem;
 int sa_conv2d_k3_wino_multi(int nprob, const SaWinoProblem *probs, void *stream);
 
@@ -350,7 +386,10 @@ typedef struct SaGateEpilogue {
 /* block_shape: 0 / 1 large blocks (8 waves, 64 Winograd tiles, one per CU), 2 small blocks (4
  * waves, 32 tiles, two per CU: shorter launches of few rounds fill the chip better), 3 wide
  * blocks (4 waves, 32 tiles x 64 output channels, one per CU; every problem's U from
- * sa_conv2d_wino4_weights_cb(..., 64, ...), Cout % 64 == 0, and Cout % 128 == 0 with a z/r gate). */
+ * sa_conv2d_wino4_weights_cb(..., 64, ...), Cout % 64 == 0, and Cout % 128 == 0 with a z/r gate),
+ * 4 quadrant blocks (8 waves, 32 tiles x 64 output channels, the 64-channel U), 5 persistent large
+ * blocks (the large shape, one block per CU walking the launch's work items; each item prefetches
+ * the next item's first input-channel chunk under its own epilogue). */
 int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                                   int block_shape, void *stream);
 

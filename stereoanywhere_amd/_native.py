@@ -26,7 +26,7 @@ class SaWinoProblem(ctypes.Structure):
     """include/stereoanywhere_hip.h: one convolution of sa_conv2d_k3_wino_multi."""
     _fields_ = [("in_", P), ("in_bs", L), ("N", I), ("Cin", I), ("H", I), ("W", I), ("U", P), ("Cout", I),
                 ("bias", P), ("relu", I), ("in_m", P), ("in_s", P), ("in_t", P), ("in_pstride", I),
-                ("in_act", I), ("out", P), ("out_bs", L), ("stats_partial", P)]
+                ("in_act", I), ("out", P), ("out_bs", L), ("stats_partial", P), ("pitch", I)]
 
 
 class SaGateEpilogue(ctypes.Structure):
@@ -46,10 +46,15 @@ SIGNATURES = {
     "sa_corr_pyramid_from_volume_strided": (I, [P, I, I, I, I, L, L, L, I, P, L, P]),
     "sa_corr_lookup": (I, [P, P, I, L, I, I, P, L, I, I, I, P, L, P]),
     "sa_corr_lookup_conv1x1": (I, [P, P, I, L, I, I, P, L, I, I, I, P, P, I, P, P]),
+    "sa_shear_slice_size": (L, [I, I, I]),
+    "sa_shear_level_offset": (L, [I, I, I, I]),
+    "sa_corr_pyramid_shear": (I, [P, L, I, I, I, I, I, P, P]),
+    "sa_corr_lookup_conv1x1_sheared": (I, [P, P, I, I, I, P, L, I, I, I, P, P, I, P, P]),
     "sa_mono_normals": (I, [P, I, I, I, F, P, P]),
     "sa_mono_masked_volume": (I, [P, P, P, P, I, I, I, I, I, F, P, P]),
     "sa_mono_bin_records": (I, [P, P, I, I, I, I, P, P]),
     "sa_softargmin_conf": (I, [P, P, I, I, I, I, L, L, L, L, P, P, P, P, L, P]),
+    "sa_softargmin_set_one_pass": (None, [I]),
     "sa_softlrc": (I, [P, P, P, P, I, I, I, L, F, P, P, P]),
     "sa_weighted_lsq": (I, [P, P, P, I, I, F, F, P, P, P]),
     "sa_weighted_lsq_ws_size": (L, [I, I]),
@@ -60,6 +65,8 @@ SIGNATURES = {
     "sa_gru_out_split": (I, [P, L, P, P, P, L, P, L, P, I, I, I, P, L, P]),
     "sa_pool2x": (I, [P, L, I, I, I, I, P, L, P]),
     "sa_interp_bilinear_ac": (I, [P, L, I, I, I, I, I, I, P, L, P]),
+    "sa_pool2x_p": (I, [P, L, I, I, I, I, I, P, L, I, P]),
+    "sa_interp_bilinear_ac_p": (I, [P, L, I, I, I, I, I, I, I, P, L, I, P]),
     "sa_relu_copy": (I, [P, L, I, I, I, P, L, P]),
     "sa_flow_update": (I, [P, P, L, I, I, I, P, L, P, L, P]),
     "sa_convex_upsample": (I, [P, P, L, I, I, I, I, P, P]),
@@ -87,6 +94,7 @@ SIGNATURES = {
     "sa_conv3d_pointwise_upcat": (I, [P, I, P, P, I, P, P, P, I, I, I, I, I, I, I, F, P, I, P, P, P]),
     "sa_instnorm_finalize": (I, [P, I, L, L, F, P, P, P]),
     "sa_conv3d_wd": (I, [P, I, I, I, I, I, P, I, P, P, I, F, P, P, P, P, P]),
+    "sa_conv3d_wd_set_variant": (None, [I]),
     "sa_conv3d_onehot_stat_parts": (L, [I, I, I]),
     "sa_conv3d_onehot": (I, [P, P, I, I, I, I, I, I, F, P, I, P, P, P]),
     "sa_conv3d_pointwise_upcat_onehot": (I, [P, P, I, F, P, I, I, I, I, I, I, I, P, I, P, P, P]),

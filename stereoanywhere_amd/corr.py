@@ -27,7 +27,10 @@ class HipCorrBlock1D:
         self.num_levels = num_levels
         self.radius = radius
         self.pad = list(pad)
-        if _pyramid is None:
+        if _pyramid is None and fullcorr is None:
+            if _shape is None:
+                raise RuntimeError("HipCorrBlock1D needs a volume, a pyramid or (sheared-only) a shape")
+        elif _pyramid is None:
             if fullcorr.dim() != 5 or fullcorr.shape[3] != 1:
                 raise RuntimeError(f"fullcorr must be [B,H,W1,1,W2], got {tuple(fullcorr.shape)}")
             B, H, W1, _, W2 = fullcorr.shape
@@ -35,6 +38,7 @@ class HipCorrBlock1D:
             _shape = (B, H, W1, W2)
         self.shape = _shape
         self.pyramid = _pyramid
+        self.sheared = None   # disparity-sheared copy for the fused lookup (shear())
         self._views = None
 
     @property
@@ -74,10 +78,24 @@ class HipCorrBlock1D:
                         self.radius, coords_x, out)
         return out
 
+    def shear(self, release: bool = False) -> "HipCorrBlock1D":
+        """Build the disparity-sheared copy the fused lookup reads (ops.corr_pyramid_shear);
+        release: drop the row-layout buffer afterwards (the per-level views need it)."""
+        B, H, W1, W2 = self.shape
+        self.sheared = ops.corr_pyramid_shear(self.pyramid, B, H, W1, W2, self.num_levels)
+        if release:
+            self.pyramid, self._views = None, None
+        return self
+
     def lookup_conv1x1_into(self, coords_x: torch.Tensor, weight_kc: torch.Tensor, bias: torch.Tensor,
                             out: torch.Tensor, other: Optional["HipCorrBlock1D"] = None):
         """Lookup of this pyramid (and ``other``'s) followed, in the same kernel, by a 1x1 conv
-        + bias + ReLU of the taps -> out [B*nvol, Cout, H, W1] (sample b*nvol + v)."""
+        + bias + ReLU of the taps -> out [B*nvol, Cout, H, W1] (sample b*nvol + v); on the
+        sheared copies when both blocks have one."""
+        if self.sheared is not None and (other is None or other.sheared is not None):
+            return ops.corr_lookup_conv1x1_sheared(self.sheared, None if other is None else other.sheared,
+                                                   self.shape[3], self.num_levels, self.radius, coords_x, weight_kc,
+                                                   bias, out)
         return ops.corr_lookup_conv1x1(self.pyramid, None if other is None else other.pyramid, self.shape[3],
                                        self.num_levels, self.radius, coords_x, weight_kc, bias, out)
 

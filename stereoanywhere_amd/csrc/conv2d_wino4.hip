@@ -28,6 +28,7 @@
 // lane that feeds it to its two MFMAs (about 2 VALU operations per MFMA).
 #include "sa_common.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -56,6 +57,9 @@
 #endif
 #ifndef SA_W4_PRIO
 #define SA_W4_PRIO 0
+#endif
+#ifndef SA_W4_PF
+#define SA_W4_PF 1     // persistent kernel: prefetch the next item's chunk 0 (0: each item issues its own)
 #endif
 
 namespace {
@@ -130,6 +134,7 @@ struct W4Prob {
   // input transform (the producer's norm + ReLU, SaWinoProblem in_m / in_s / in_t / in_act)
   const float *in_m, *in_s, *in_t;
   int in_pstride, in_act;
+  int pitch;               // row pitch of the input / output / gate planes (>= W, % 4 == 0; SaWinoProblem)
 };
 constexpr int MAX_PROB = 8;
 // GRU gate epilogues (SaGateEpilogue in the header), read by the store loop only
@@ -224,25 +229,232 @@ __device__ __forceinline__ void bt6h(const float x0, const float x1, const float
   }
 }
 
+// Chunk 0 (filters + patch) of work item `wid` of problem P into LDS buffer pb, with the patch
+// geometry at run time (P.ltw): the persistent kernel issues it for its NEXT work item during
+// the current item's last chunk, so the next item's first chunk lands under this item's
+// epilogue instead of after it.  Same DMA pieces and lanes as w4_body's own chunk-0 issue.
+template <class C>
+__device__ __forceinline__ void w4_issue_chunk0(const W4Prob &P, const unsigned wid, float *pb, const int wv,
+                                                const int lane) {
+  constexpr int NWAVE = C::NW, KC = C::KC, PDMA = C::PDMA, UDMA = C::UDMA, UPW = C::UPW, PBUF = C::PBUF,
+                NT = C::NT, CO = C::CO, SB = C::SB, JPC = C::JPC;
+  const int Cin = P.Cin, H = P.H;
+  const int ltw = P.ltw, tw = 1 << ltw, tr = NT >> ltw;
+  const int BH = 4 * tr, BW = 4 * tw, PG = tw + 2, PR = BH + 2, PS = PR * PG;
+  const int co_blocks = P.co_blocks, tiles_hw = P.tiles_hw, tiles_w = P.tiles_w;
+  const int cb = wid % co_blocks;
+  const int st = (wid / co_blocks) % tiles_hw;
+  const int n = wid / (co_blocks * tiles_hw);
+  const int y0 = (st / tiles_w) * BH, x0 = (st % tiles_w) * BW;
+  const int pitch = P.pitch, hw = H * pitch;
+  const __amdgpu_buffer_rsrc_t xin = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(P.in + (long)n * P.in_bs), (short)0, Cin * hw * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t uin = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(P.U + (long)cb * Cin * NPT * CO), (short)0, Cin * NPT * CO * 4, 0x00020000);
+#pragma unroll
+  for (int j = 0; j < UPW; ++j)
+    if (wv + NWAVE * j < UDMA) {
+      const int f = (wv + NWAVE * j) * 256 + lane * 4;
+      dma16(uin, pb + PBUF + (wv + NWAVE * j) * 256, (JPC == 2 ? f : f + (f / SB) * SB) * 4, 0);
+    }
+  const int npi = (KC * PS + 63) >> 6;
+  // rolled: this runs with the accumulators live (an unrolled loop's address math spilled)
+#pragma unroll 1
+  for (int j = 0; j < PDMA; ++j) {
+    if (wv + NWAVE * j < npi) {
+      const int s = (wv + NWAVE * j) * 64 + lane;
+      const int ci = s / PS, rem = s - ci * PS, r = rem / PG, g = rem - r * PG;
+      const int y = y0 - 1 + r, x = x0 - 4 + 4 * g;
+      const bool ok = s < KC * PS && y >= 0 && y < H && x >= 0 && x < pitch;
+      dma16(xin, pb + (wv + NWAVE * j) * 256, ok ? (ci * hw + y * pitch + x) * 4 : 0x7ffffff0, 0);
+    }
+  }
+}
+
+// The block's staged outputs, channels [cbase, cbase + NCH) of its CO at ot (plane c - cbase,
+// pitch OPP): InstanceNorm partials (if requested), then float4 stores or the GRU gate epilogue.
+template <class C, bool GATED, int NCH>
+__device__ __forceinline__ void w4_emit(const W4Prob &P, const W4Gate *gate, const float *ot, const int cbase,
+                                        const int n, const int co0, const int st, const int tiles_w, const int y0,
+                                        const int x0, const int BH, const int BW, const int lbw, const int tid) {
+  constexpr int NT = C::NT, NTHR = C::NTHR, OPP = C::OPP, CO = C::CO;
+  const int H = P.H, W = P.W, Cout = P.Cout, pitch = P.pitch, hw = H * pitch;
+  const int cb0 = co0 + cbase;   // first output channel of this pass
+  // a group of 4 that straddles the last column (pitch > W): its columns >= W stay zero
+  auto tail0 = [&](f32x4 v, const int x) __attribute__((always_inline)) {
+    if (x + 4 > W) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (x + e >= W) v[e] = 0.0f;
+    }
+    return v;
+  };
+  if (P.partial) {
+    // InstanceNorm partials, indexed by the small blocks' tiling (BH rows of a large block = 2
+    // small tiles), so both block shapes fill the same [N * Cout][parts][2] array: TPC threads
+    // per (channel, small tile), each over consecutive pixels of it, fixed-order reduction
+    constexpr int NSUB = NT / 32, TPC = NTHR / (NCH * NSUB), PPT = 32 * 16 / TPC;
+    const int c = tid / (TPC * NSUB), sub = (tid / TPC) % NSUB, part = tid % TPC;
+    const int sub_rows = BH / NSUB, fine_h = (H + sub_rows - 1) / sub_rows;
+    const int frow = (st / tiles_w) * NSUB + sub;
+    double ssum = 0.0, ssq = 0.0;
+#pragma unroll 2
+    for (int p = sub * 512 + part * PPT; p < sub * 512 + (part + 1) * PPT; p += 4) {
+      const int r = p >> lbw, cx = p & (BW - 1);
+      if (y0 + r < H && x0 + cx < W) {   // (the straddling group of a pitched plane: masked)
+        const f32x4 v = tail0(*reinterpret_cast<const f32x4 *>(ot + c * OPP + p), x0 + cx);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const double d = v[e];
+          ssum += d;
+          ssq += d * d;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = TPC / 2; o > 0; o >>= 1) {
+      ssum += __shfl_xor(ssum, o);
+      ssq += __shfl_xor(ssq, o);
+    }
+    if (part == 0 && frow < fine_h) {
+      const long fst = (long)frow * tiles_w + st % tiles_w;
+      double *pp = P.partial + (((long)n * Cout + cb0 + c) * ((long)fine_h * tiles_w) + fst) * 2;
+      pp[0] = ssum;
+      pp[1] = ssq;
+    }
+  }
+  // float4 stores: NT * 4 per channel plane of the block
+  float *dst = P.out + (long)n * P.out_bs;
+  constexpr int NJ = (NCH * NT * 16) / (4 * NTHR);
+  auto plain_stores = [&]() __attribute__((always_inline)) {
+#pragma unroll 4
+    for (int j = 0; j < NJ; ++j) {
+      const int i4 = tid + NTHR * j;
+      const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
+      const int y = y0 + r, x = x0 + cx;
+      if (y < H && x < W)
+        *reinterpret_cast<f32x4 *>(dst + (long)(cb0 + c) * hw + (long)y * pitch + x) =
+            tail0(*reinterpret_cast<const f32x4 *>(ot + c * OPP + p), x);
+    }
+  };
+  if constexpr (!GATED) {
+    plain_stores();
+    return;
+  } else {
+  // GRU gates (update.py:16-27): conv (+ bias, staged) + context, then
+  //   mode 1 (z | r over cat(h, x)): z = sigmoid(.) -> out, r * h -> out2 (block-uniform half)
+  //   mode 2 (q over r*h):           h' = (1 - z) h + z tanh(. + add) -> out (in place on h)
+  // the gate parameters are read here, not at the kernel's start (they would lengthen the
+  // prologue before chunk 0's DMA)
+  const W4Gate &GT = *gate;
+  if (GT.mode == 0) {
+    plain_stores();
+    return;
+  }
+  const int half = Cout / 2;
+  const bool rhalf = co0 >= half;
+  const float *ctxb = GT.ctx + (long)n * GT.ctx_bs;
+  // The gate planes are loaded for a batch of store iterations at once (out-of-image
+  // positions read the block's first pixel, whose load is always in range, and are not
+  // stored), so all of a batch's loads are in flight together instead of a branchy loop
+  // waiting for its own loads every iteration (the accumulators are dead here: registers are
+  // free).  Batches: 16 iterations in mode 1 (ctx, and h for the r half), 8 in mode 2 (four
+  // planes): 128 registers either way.
+  const float *hb = GT.h + (long)n * GT.h_bs;
+  const float *ab = GT.add + (long)n * GT.add_bs;
+  const float *zb = GT.z + (long)n * GT.z_bs;
+  auto gate_stores = [&](auto gjb_c, auto mode_c) __attribute__((always_inline)) {
+    constexpr int GJB = decltype(gjb_c)::value < NJ ? decltype(gjb_c)::value : NJ, MODE = decltype(mode_c)::value;
+    static_assert(NJ % GJB == 0, "gate batches");
+#pragma unroll 1
+    for (int jb = 0; jb < NJ; jb += GJB) {
+      int pos[GJB];
+      bool ok[GJB];
+      f32x4 cv[GJB], hv[GJB], av[GJB], zv[GJB];
+#pragma unroll
+      for (int u = 0; u < GJB; ++u) {
+        const int i4 = tid + NTHR * (jb + u);
+        const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
+        const int y = y0 + r, x = x0 + cx;
+        ok[u] = y < H && x < W;
+        pos[u] = (cb0 + c) * hw + (ok[u] ? y * pitch + x : y0 * pitch + x0);
+        cv[u] = *reinterpret_cast<const f32x4 *>(ctxb + pos[u]);
+        if (MODE == 1) {
+          if (rhalf) hv[u] = *reinterpret_cast<const f32x4 *>(hb + (pos[u] - half * hw));
+        } else {
+          av[u] = *reinterpret_cast<const f32x4 *>(ab + pos[u]);
+          zv[u] = *reinterpret_cast<const f32x4 *>(zb + pos[u]);
+          hv[u] = *reinterpret_cast<const f32x4 *>(hb + pos[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < GJB; ++u) {
+        if (!ok[u]) continue;
+        const int i4 = tid + NTHR * (jb + u);
+        const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4;
+        const int xg = x0 + (p & (BW - 1));
+        const f32x4 v = *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
+        f32x4 o;
+        if (MODE == 1) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = sa::sigmoidf_ref(v[e] + cv[u][e]);
+          if (!rhalf) {
+            *reinterpret_cast<f32x4 *>(dst + pos[u]) = tail0(o, xg);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = o[e] * hv[u][e];
+            *reinterpret_cast<f32x4 *>(GT.out2 + (long)n * GT.out2_bs + (pos[u] - half * hw)) = tail0(o, xg);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float q = tanhf((av[u][e] + v[e]) + cv[u][e]);
+            o[e] = (1.0f - zv[u][e]) * hv[u][e] + zv[u][e] * q;
+          }
+          *reinterpret_cast<f32x4 *>(dst + pos[u]) = tail0(o, xg);
+        }
+      }
+    }
+  };
+  // (the 64-channel shapes spill with 16 in mode 1: 8 there; a 16-channel pass of the persistent
+  // kernel runs with the other group's accumulators live: 4)
+  if (GT.mode == 1)
+    gate_stores(std::integral_constant<int, NCH == 16 ? 4 : CO == 64 ? SA_W4_GJB : SA_W4_GJB1>{},
+                std::integral_constant<int, 1>{});
+  else gate_stores(std::integral_constant<int, NCH == 16 ? 4 : SA_W4_GJB>{}, std::integral_constant<int, 2>{});
+  }
+}
+
 #ifdef SA_W4_CLOCK
 // diagnostic build only: per block (s_memtime, s_memrealtime) at the start and the end of wave 0,
 // then s_memtime after the first chunk's barrier and after the main loop
 __device__ unsigned long long g_w4_clock[65536][10];   // + [8] chunk 0 issued, [9] last wave's start
 #endif
 
-template <class C, int HF, int LTW, bool GATED, bool AFF, int RH = 0>
+// PERSIST: a work item of the persistent kernel.  Its chunk kc is staged in LDS buffer
+// (kc + par) & 1; `pre`: chunk 0 was issued by the previous item (w4_issue_chunk0); NP / nwid:
+// the next item (if has_next), whose chunk 0 this item issues as its main loop ends.  The epilogue then stages
+// one 16-channel group at a time in the last chunk's buffer (the other one receives the
+// prefetch).
+template <class C, int HF, int LTW, bool GATED, bool AFF, int RH = 0, bool PERSIST = false>
 __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, const unsigned wid, float *smem,
-                                        float2 *atab) {
+                                        float2 *atab, const int par = 0, const bool pre = false,
+                                        const bool has_next = false, const W4Prob &NP = W4Prob{},
+                                        const unsigned nwid = 0) {
   constexpr int NWAVE = C::NW, NTHR = C::NTHR, KC = C::KC, JPC = C::JPC, NT = C::NT, PDMA = C::PDMA,
                 UDMA = C::UDMA, UPW = C::UPW, UBUF = C::UBUF, BUF = C::BUF, PBUF = C::PBUF, OPP = C::OPP,
                 CO = C::CO, CG = C::CG, SB = C::SB, NR = C::NR;
   constexpr bool QUAD = C::QUAD;
   using f32xg = __attribute__((ext_vector_type(CG))) float;   // a lane's filter operands, one per group
-  const int Cin = P.Cin, H = P.H, W = P.W, Cout = P.Cout;
+  const int Cin = P.Cin, H = P.H;
   // block geometry as compile-time constants (the patch offsets divide by PS and PG)
   constexpr int ltw = LTW, tw = 1 << ltw, tr = NT >> ltw;
   constexpr int BH = 4 * tr, BW = 4 * tw, PG = tw + 2, PR = BH + 2, PS = PR * PG;
-  const int tid = threadIdx.x, lane = tid & 63;
+  int tid = threadIdx.x;
+  // persistent items: an opaque thread id per item keeps the compiler from hoisting the
+  // lane-dependent offsets out of the item loop (live across it they cost ~20 VGPRs and spilled)
+  if constexpr (PERSIST) asm volatile("" : "+v"(tid));
+  const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int co_blocks = P.co_blocks, tiles_hw = P.tiles_hw, tiles_w = P.tiles_w;
   const int cb = wid % co_blocks;
@@ -250,7 +462,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   const int n = wid / (co_blocks * tiles_hw);
   const int y0 = (st / tiles_w) * BH, x0 = (st % tiles_w) * BW;
   const int co0 = cb * CO;
-  const int hw = H * W;
+  const int pitch = P.pitch, hw = H * pitch;
   const int nchunks = Cin / KC;
 
   const __amdgpu_buffer_rsrc_t xin = __builtin_amdgcn_make_buffer_rsrc(
@@ -270,10 +482,11 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   // patch DMA: the chunk's image is [channel][PR rows][PG groups of 4 floats], dense, starting
   // at (y0 - 1, x0 - 4); wave-instruction gi fills groups 64 gi .. 64 gi + 63 (lane-linear)
   // chunk 0's filters first: their offsets need no patch geometry
-  if (SA_W4_DIAG != 4) {
+  if (SA_W4_DIAG != 4 && !pre) {
 #pragma unroll
     for (int j = 0; j < UPW; ++j)
-      if (wv + NWAVE * j < UDMA) dma16(uin, smem + PBUF + (wv + NWAVE * j) * 256, u_src(wv + NWAVE * j), u_chunk(0));
+      if (wv + NWAVE * j < UDMA)
+        dma16(uin, smem + par * BUF + PBUF + (wv + NWAVE * j) * 256, u_src(wv + NWAVE * j), u_chunk(0));
   }
   const int npi = (KC * PS + 63) >> 6;
   int po[PDMA];
@@ -283,8 +496,9 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
     const int s = (wv + NWAVE * j) * 64 + lane;
     const int ci = s / PS, rem = s - ci * PS, r = rem / PG, g = rem - r * PG;
     const int y = y0 - 1 + r, x = x0 - 4 + 4 * g;
-    const bool ok = s < KC * PS && y >= 0 && y < H && x >= 0 && x < W;
-    po[j] = ok ? (ci * hw + y * W + x) * 4 : 0x7ffffff0;   // out of range: the load returns 0
+    // (a pitched plane's columns W .. pitch - 1 are zero: they load as the right padding)
+    const bool ok = s < KC * PS && y >= 0 && y < H && x >= 0 && x < pitch;
+    po[j] = ok ? (ci * hw + y * pitch + x) * 4 : 0x7ffffff0;   // out of range: the load returns 0
     pc[j] = ok && wv + NWAVE * j < (KC * PS + 63) / 64 ? ci : -1;
   }
   // the chunk's DMAs in three parts (part -1: all at once), spread over the first job's three
@@ -307,7 +521,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   auto issue_p0 = [&]() __attribute__((always_inline)) {   // chunk 0's patch (its filters went first)
 #pragma unroll
     for (int j = 0; j < PDMA; ++j)
-      if (wv + NWAVE * j < npi) dma16(xin, smem + (wv + NWAVE * j) * 256, po[j], 0);
+      if (wv + NWAVE * j < npi) dma16(xin, smem + par * BUF + (wv + NWAVE * j) * 256, po[j], 0);
   };
 
   // lane roles: MFMA A operand A[m][k] = (tile m, channel k); B operands B[k][n] = (channel k,
@@ -341,7 +555,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   for (int k = 0; k < (QUAD ? 1 : CG / 2); ++k)
     bpre[k] = P.bias ? P.bias[co0 + (QUAD ? 2 * RH + HF : 2 * k + HF) * 16 + (lane & 15)] : 0.0f;
   if (SA_W4_PRIO && HF == 1) __builtin_amdgcn_s_setprio(1);   // static priority for waves 4-7
-  if (SA_W4_DIAG != 4) issue_p0();
+  if (SA_W4_DIAG != 4 && !pre) issue_p0();
   // Input transform: v -> act(v * scale + shift), scale = s, shift = t - m * s per channel
   // (in_pstride 0) or per (image, channel) (in_pstride = Cin).  Each lane transforms the
   // 4-float groups its own DMAs brought in (in the LDS, after its own vmcnt wait, before the
@@ -362,7 +576,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
 #endif
 #pragma unroll 1
   for (int kc = 0; kc < nchunks; ++kc) {
-    const int cur = kc & 1;
+    const int cur = (kc + par) & 1;
     if constexpr (AFF) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this lane's DMAs of chunk kc landed
       float *pbuf = smem + cur * BUF;
@@ -452,6 +666,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
           __builtin_amdgcn_sched_barrier(0);
 #endif
         }
+
 #pragma unroll
         for (int i = 0; i < NR; ++i) bc[i] = bn[i];
       }
@@ -461,6 +676,80 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
 #ifdef SA_W4_CLOCK
   if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][5] = __builtin_amdgcn_s_memtime();
 #endif
+
+  if constexpr (PERSIST) {
+    // Persistent item: the next item's chunk 0 is landing in the other buffer, so the outputs
+    // are staged one 16-channel group at a time in this item's last buffer (16 planes of OPP
+    // fit in BUF).  Group g is finished by half HF == g: both halves form their partial of g
+    // in registers, half 1 - g stages its own, half g adds it (same order as below: p1 + p0),
+    // then the group is emitted.
+    static_assert(!QUAD && CG == 2 && 16 * OPP <= BUF, "persistent shape: 8 waves x 32 channels");
+    // the next item's chunk 0 into the buffer after this item's last one (free since the last
+    // chunk's barrier); issued here, not inside the last chunk, where the MFMA loop's registers
+    // are live (the address math there spilled)
+    if (SA_W4_PF && has_next) w4_issue_chunk0<C>(NP, nwid, smem + ((nchunks + par) & 1) * BUF, wv, lane);
+    float *ot = smem + ((nchunks - 1 + par) & 1) * BUF;
+    const int relu = P.relu;
+    const int col = lane & 15;
+#pragma unroll
+    for (int g = 0; g < CG; ++g) {
+      // this half's partial of group g at tile i (of the lane's 4), output rows 0-3
+      auto partial = [&](int i, f32x4 *y) __attribute__((always_inline)) {
+        float u[4][3];
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) {
+          float mcol[6], o[4];
+#pragma unroll
+          for (int a = 0; a < 6; ++a) mcol[a] = acc[a][jj][g][i];
+          at6(mcol, o);
+#pragma unroll
+          for (int a = 0; a < 4; ++a) u[a][jj] = o[a];
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          if (HF == 0) {
+            const float p = u[a][1] + u[a][2], q = u[a][1] - u[a][2];
+            y[a] = f32x4{u[a][0] + p, q, p, q};
+          } else {
+            const float p = u[a][0] + u[a][1], q = u[a][0] - u[a][1];
+            y[a] = f32x4{p, 2.0f * q, 4.0f * p, 8.0f * q + u[a][2]};
+          }
+        }
+      };
+      auto slot = [&](int i, int a) __attribute__((always_inline)) {
+        const int ti = tg * 16 + w4_tile_of_row(4 * (lane >> 4) + i), orow = (ti >> ltw) * 4, ocol = (ti & (tw - 1)) * 4;
+        return reinterpret_cast<f32x4 *>(ot + col * OPP + (orow + a) * BW + ocol);
+      };
+      if (HF != g) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f32x4 y[4];
+          partial(i, y);
+#pragma unroll
+          for (int a = 0; a < 4; ++a) *slot(i, a) = y[a];
+        }
+      }
+      __syncthreads();
+      if (HF == g) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f32x4 y[4];
+          partial(i, y);
+#pragma unroll
+          for (int a = 0; a < 4; ++a) {
+            f32x4 *o = slot(i, a);
+            f32x4 v = (HF == 0 ? (*o + y[a]) : (y[a] + *o)) + bpre[0];
+            if (relu) v = f32x4{fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f)};
+            *o = v;
+          }
+        }
+      }
+      __syncthreads();
+      w4_emit<C, GATED, 16>(P, gate, ot, 16 * g, n, co0, st, tiles_w, y0, x0, BH, BW, ltw + 2, tid);
+      if (g + 1 < CG) __syncthreads();
+    }
+    return;
+  }
 
   // ---- output transform.  Lane holds tiles tg * 16 + 4 (lane >> 4) + i of output channels
   // g * 16 + (lane & 15), points of columns 3 HF .. 3 HF + 2.  Y = A^T M A: the column-wise
@@ -558,146 +847,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][6] = __builtin_amdgcn_s_memtime();
 #endif
   __syncthreads();
-  const int lbw = ltw + 2;   // log2 BW
-  if (P.partial) {
-    // InstanceNorm partials, indexed by the small blocks' tiling (BH rows of a large block = 2
-    // small tiles), so both block shapes fill the same [N * Cout][parts][2] array: TPC threads
-    // per (channel, small tile), each over consecutive pixels of it, fixed-order reduction
-    constexpr int NSUB = NT / 32, TPC = NTHR / (CO * NSUB), PPT = 32 * 16 / TPC;
-    const int c = tid / (TPC * NSUB), sub = (tid / TPC) % NSUB, part = tid % TPC;
-    const int sub_rows = BH / NSUB, fine_h = (H + sub_rows - 1) / sub_rows;
-    const int frow = (st / tiles_w) * NSUB + sub;
-    double ssum = 0.0, ssq = 0.0;
-#pragma unroll 2
-    for (int p = sub * 512 + part * PPT; p < sub * 512 + (part + 1) * PPT; p += 4) {
-      const int r = p >> lbw, cx = p & (BW - 1);
-      if (y0 + r < H && x0 + cx < W) {   // W % 4 == 0: a float4 is wholly inside or outside
-        const f32x4 v = *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const double d = v[e];
-          ssum += d;
-          ssq += d * d;
-        }
-      }
-    }
-#pragma unroll
-    for (int o = TPC / 2; o > 0; o >>= 1) {
-      ssum += __shfl_xor(ssum, o);
-      ssq += __shfl_xor(ssq, o);
-    }
-    if (part == 0 && frow < fine_h) {
-      const long fst = (long)frow * tiles_w + st % tiles_w;
-      double *pp = P.partial + (((long)n * Cout + co0 + c) * ((long)fine_h * tiles_w) + fst) * 2;
-      pp[0] = ssum;
-      pp[1] = ssq;
-    }
-  }
-#ifdef SA_W4_CLOCK
-  if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][7] = __builtin_amdgcn_s_memtime();
-#endif
-  // float4 stores: NT * 4 per channel plane of the block
-  float *dst = P.out + (long)n * P.out_bs;
-  if constexpr (!GATED) {
-#pragma unroll 4
-    for (int j = 0; j < (CO * NT * 16) / (4 * NTHR); ++j) {
-      const int i4 = tid + NTHR * j;
-      const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
-      const int y = y0 + r, x = x0 + cx;
-      if (y < H && x < W)
-        *reinterpret_cast<f32x4 *>(dst + (long)(co0 + c) * hw + (long)y * W + x) =
-            *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
-    }
-    return;
-  } else {
-  // GRU gates (update.py:16-27): conv (+ bias, staged) + context, then
-  //   mode 1 (z | r over cat(h, x)): z = sigmoid(.) -> out, r * h -> out2 (block-uniform half)
-  //   mode 2 (q over r*h):           h' = (1 - z) h + z tanh(. + add) -> out (in place on h)
-  // the gate parameters are read here, not at the kernel's start (they would lengthen the
-  // prologue before chunk 0's DMA)
-  const W4Gate &GT = *gate;
-  if (GT.mode == 0) {
-#pragma unroll 4
-    for (int j = 0; j < (CO * NT * 16) / (4 * NTHR); ++j) {
-      const int i4 = tid + NTHR * j;
-      const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
-      const int y = y0 + r, x = x0 + cx;
-      if (y < H && x < W)
-        *reinterpret_cast<f32x4 *>(dst + (long)(co0 + c) * hw + (long)y * W + x) =
-            *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
-    }
-    return;
-  }
-  const int half = Cout / 2;
-  const bool rhalf = co0 >= half;
-  const float *ctxb = GT.ctx + (long)n * GT.ctx_bs;
-  // The gate planes are loaded for a batch of store iterations at once (out-of-image
-  // positions read the block's first pixel, whose load is always in range, and are not
-  // stored), so all of a batch's loads are in flight together instead of a branchy loop
-  // waiting for its own loads every iteration (the accumulators are dead here: registers are
-  // free).  Batches: 16 iterations in mode 1 (ctx, and h for the r half), 8 in mode 2 (four
-  // planes): 128 registers either way.
-  constexpr int NJ = (CO * NT * 16) / (4 * NTHR);
-  const float *hb = GT.h + (long)n * GT.h_bs;
-  const float *ab = GT.add + (long)n * GT.add_bs;
-  const float *zb = GT.z + (long)n * GT.z_bs;
-  auto gate_stores = [&](auto gjb_c, auto mode_c) __attribute__((always_inline)) {
-    constexpr int GJB = decltype(gjb_c)::value < NJ ? decltype(gjb_c)::value : NJ, MODE = decltype(mode_c)::value;
-    static_assert(NJ % GJB == 0, "gate batches");
-#pragma unroll 1
-    for (int jb = 0; jb < NJ; jb += GJB) {
-      int pos[GJB];
-      bool ok[GJB];
-      f32x4 cv[GJB], hv[GJB], av[GJB], zv[GJB];
-#pragma unroll
-      for (int u = 0; u < GJB; ++u) {
-        const int i4 = tid + NTHR * (jb + u);
-        const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
-        const int y = y0 + r, x = x0 + cx;
-        ok[u] = y < H && x < W;
-        pos[u] = (co0 + c) * hw + (ok[u] ? y * W + x : y0 * W + x0);
-        cv[u] = *reinterpret_cast<const f32x4 *>(ctxb + pos[u]);
-        if (MODE == 1) {
-          if (rhalf) hv[u] = *reinterpret_cast<const f32x4 *>(hb + (pos[u] - half * hw));
-        } else {
-          av[u] = *reinterpret_cast<const f32x4 *>(ab + pos[u]);
-          zv[u] = *reinterpret_cast<const f32x4 *>(zb + pos[u]);
-          hv[u] = *reinterpret_cast<const f32x4 *>(hb + pos[u]);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < GJB; ++u) {
-        if (!ok[u]) continue;
-        const int i4 = tid + NTHR * (jb + u);
-        const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4;
-        const f32x4 v = *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
-        f32x4 o;
-        if (MODE == 1) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = sa::sigmoidf_ref(v[e] + cv[u][e]);
-          if (!rhalf) {
-            *reinterpret_cast<f32x4 *>(dst + pos[u]) = o;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = o[e] * hv[u][e];
-            *reinterpret_cast<f32x4 *>(GT.out2 + (long)n * GT.out2_bs + (pos[u] - half * hw)) = o;
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float q = tanhf((av[u][e] + v[e]) + cv[u][e]);
-            o[e] = (1.0f - zv[u][e]) * hv[u][e] + zv[u][e] * q;
-          }
-          *reinterpret_cast<f32x4 *>(dst + pos[u]) = o;
-        }
-      }
-    }
-  };
-  // (the 64-channel shapes spill with 16 in mode 1: 8 there)
-  if (GT.mode == 1)
-    gate_stores(std::integral_constant<int, CO == 64 ? SA_W4_GJB : SA_W4_GJB1>{}, std::integral_constant<int, 1>{});
-  else gate_stores(std::integral_constant<int, SA_W4_GJB>{}, std::integral_constant<int, 2>{});
-  }
+  w4_emit<C, GATED, C::CO>(P, gate, ot, 0, n, co0, st, tiles_w, y0, x0, BH, BW, ltw + 2, tid);
 }
 
 template <class C, bool GATED, bool AFF = false>
@@ -748,6 +898,72 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 || C::CO == 64 ? 1 : 2) void wi
     g_w4_clock[g][3] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
+}
+
+// Persistent variant of the 8-wave shape: one block per CU walks the launch's work items
+// g = blockIdx.x, blockIdx.x + gridDim.x, ... (gridDim.x a multiple of 8, so an item stays on the
+// XCD the one-shot grid would put it on, and the L2-locality remap is unchanged).  Each item
+// issues the next item's chunk 0 as its main loop ends (w4_issue_chunk0), so the first-chunk
+// wait of every item but the block's first is hidden under the previous item's epilogue.
+template <class C, bool GATED, bool AFF = false>
+__global__ __launch_bounds__(C::NTHR, 1) void wino_f4k3_persist_kernel(const W4Launch L) {
+  static_assert(C::NW == 8 && C::CO == 32 && !C::QUAD, "persistent: the 8-wave 32-channel shape");
+  __shared__ __attribute__((aligned(16))) float smem[C::SMEM];
+  __shared__ float2 atab[AFF ? C::AFF_MAX : 1];
+  const unsigned total = L.end[MAX_PROB - 1], G = gridDim.x;
+  auto locate = [&](const unsigned g, int &pi, unsigned &wid) __attribute__((always_inline)) {
+    pi = 0;
+#pragma unroll
+    for (int i = 1; i < MAX_PROB; ++i) pi += (i < L.nprob && g >= L.end[i - 1]) ? 1 : 0;
+    const unsigned base = pi ? L.end[pi - 1] : 0u, nb = L.nblk[pi];
+    if (g - base >= nb) return false;   // padding of a problem's range to a multiple of 8
+    wid = sa::xcd_remap(g - base, nb);
+    return true;
+  };
+  auto next_valid = [&](unsigned g, int &pi, unsigned &wid) __attribute__((always_inline)) {
+    while (g < total && !locate(g, pi, wid)) g += G;
+    return g;
+  };
+  int pi = 0, pi2 = 0;
+  unsigned wid = 0, wid2 = 0;
+  unsigned g = next_valid(blockIdx.x, pi, wid);
+  int par = 0;
+  bool pre = false;
+  while (g < total) {
+    const unsigned g2 = next_valid(g + G, pi2, wid2);
+    const W4Prob &P = L.p[pi];
+    // (a reference, not a pointer that may be null: a null-or-kernarg pointer made the compiler
+    // copy the whole launch struct to scratch)
+    const bool has_next = g2 < total;
+    const W4Prob &NP = L.p[pi2];
+    const W4Gate *gp = GATED ? &L.gate[pi] : nullptr;
+    // wave-uniform (readfirstlane): a branch on threadIdx.x would be divergent to the compiler,
+    // and the item loop's carried state would then live in VGPRs
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < C::NW / 2) {
+      if (P.ltw == 4) w4_body<C, 0, 4, GATED, AFF, 0, true>(P, gp, wid, smem, atab, par, pre, has_next, NP, wid2);
+      else w4_body<C, 0, 5, GATED, AFF, 0, true>(P, gp, wid, smem, atab, par, pre, has_next, NP, wid2);
+    } else {
+      if (P.ltw == 4) w4_body<C, 1, 4, GATED, AFF, 0, true>(P, gp, wid, smem, atab, par, pre, has_next, NP, wid2);
+      else w4_body<C, 1, 5, GATED, AFF, 0, true>(P, gp, wid, smem, atab, par, pre, has_next, NP, wid2);
+    }
+    par = (par + P.Cin / C::KC) & 1;
+    pre = SA_W4_PF && has_next;
+    g = g2;
+    pi = pi2;
+    wid = wid2;
+  }
+}
+
+int w4_num_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
 }
 
 // U = G g G^T for g = w[co][ci] (3x3), fp64, rounded once.  Layout
@@ -821,13 +1037,13 @@ extern "C" int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, v
 extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                                              int block_shape, void *stream) {
   SA_REQUIRE(nprob >= 1 && nprob <= MAX_PROB && probs, "sa_conv2d_k3_wino4_multi: 1..%d problems", MAX_PROB);
-  SA_REQUIRE(block_shape >= 0 && block_shape <= 4, "sa_conv2d_k3_wino4_multi: block_shape 0..4");
+  SA_REQUIRE(block_shape >= 0 && block_shape <= 5, "sa_conv2d_k3_wino4_multi: block_shape 0..5");
   // Large blocks unless the caller asks for small ones (block_shape 2) or wide ones (3: 64
   // output channels per block, filters from sa_conv2d_wino4_weights_cb(..., 64, ...)).  The
   // small shape measured 2-8% faster on standalone launches of Cin <= 128 with a few rounds of
   // blocks (qh08, convc2) but not faster in the forward as a blanket choice.
   // block_shape 4: the quadrant shape (W4Quad), also on the 64-channel filter layout
-  const bool small = block_shape == 2, wide = block_shape == 3, quad = block_shape == 4;
+  const bool small = block_shape == 2, wide = block_shape == 3, quad = block_shape == 4, persist = block_shape == 5;
   const int nt = small || wide || quad ? W4Small::NT : W4Big::NT;
   const int CO = wide || quad ? 64 : 32;
   const int aff_max = small ? W4Small::AFF_MAX : quad ? W4Quad::AFF_MAX : W4Big::AFF_MAX;
@@ -839,10 +1055,13 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
     SA_REQUIRE(q.in && q.U && q.out && q.N > 0 && q.H > 0 && q.W > 0, "sa_conv2d_k3_wino4: bad arguments");
     SA_REQUIRE(q.Cin % 8 == 0 && q.Cout % CO == 0,
                "sa_conv2d_k3_wino4: needs Cin %% 8 == 0 and Cout %% 32 == 0 (got %d, %d)", q.Cin, q.Cout);
-    SA_REQUIRE(q.W % 4 == 0 && (reinterpret_cast<uintptr_t>(q.in) & 15) == 0 && q.in_bs % 4 == 0 &&
+    const int pitch = q.pitch ? q.pitch : q.W;
+    SA_REQUIRE(pitch >= q.W, "sa_conv2d_k3_wino4: pitch %d < W %d", pitch, q.W);
+    SA_REQUIRE(pitch % 4 == 0 && (reinterpret_cast<uintptr_t>(q.in) & 15) == 0 && q.in_bs % 4 == 0 &&
                    (reinterpret_cast<uintptr_t>(q.out) & 15) == 0 && q.out_bs % 4 == 0 &&
                    (reinterpret_cast<uintptr_t>(q.U) & 15) == 0,
-               "sa_conv2d_k3_wino4: needs W %% 4 == 0 and 16-byte aligned input / output planes and filters");
+               "sa_conv2d_k3_wino4: needs W (or the row pitch) %% 4 == 0 and 16-byte aligned input / output planes "
+               "and filters");
     const bool qaff = q.in_m || q.in_s || q.in_t || q.in_act;
     SA_REQUIRE(q.in_act == 0 || q.in_act == 1, "sa_conv2d_k3_wino4: input activation none or ReLU (got %d)", q.in_act);
     SA_REQUIRE(q.in_pstride == 0 || q.in_pstride == q.Cin, "sa_conv2d_k3_wino4: in_pstride must be 0 or Cin");
@@ -850,13 +1069,13 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
                "sa_conv2d_k3_wino4: an input transform needs the 8-wave, quadrant or 4-wave shape and Cin <= %d",
                aff_max);
     aff = aff || qaff;
-    SA_REQUIRE((long)q.Cin * q.H * q.W * 4 < (1L << 31) - 64 && 36L * q.Cin * q.Cout * 4 < (1L << 31),
+    SA_REQUIRE((long)q.Cin * q.H * pitch * 4 < (1L << 31) - 64 && 36L * q.Cin * q.Cout * 4 < (1L << 31),
                "sa_conv2d_k3_wino4: an image or the filter bank exceeds the 2 GB buffer-descriptor range");
     const int ltw = w4_ltw(q.H, q.W), bw = 4 << ltw, bh = 4 * (nt >> ltw);
     const int tiles_w = (q.W + bw - 1) / bw, tiles_h = (q.H + bh - 1) / bh;
     L.p[i] = W4Prob{q.in, q.in_bs, q.Cin, q.H, q.W, q.U, q.Cout, q.bias, q.relu, q.out, q.out_bs,
                     ltw, tiles_w, tiles_w * tiles_h, q.Cout / CO, q.stats_partial,
-                    q.in_m, q.in_s, q.in_t, q.in_pstride, q.in_act};
+                    q.in_m, q.in_s, q.in_t, q.in_pstride, q.in_act, pitch};
     L.gate[i] = W4Gate{};
     if (gates && gates[i].mode != 0) {
       const SaGateEpilogue &e = gates[i];
@@ -888,7 +1107,13 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
   SA_REQUIRE(!(aff && gated), "sa_conv2d_k3_wino4: an input transform and a gate epilogue in one launch");
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV2D_W4, s);
-  if (quad)
+  if (persist) {
+    // one block per CU (rounded down to a multiple of 8: every block keeps its items on one XCD)
+    const unsigned grid = (unsigned)std::min<long>(total, std::max(8, w4_num_cus() / 8 * 8));
+    aff     ? wino_f4k3_persist_kernel<W4Big, false, true><<<grid, W4Big::NTHR, 0, s>>>(L)
+    : gated ? wino_f4k3_persist_kernel<W4Big, true><<<grid, W4Big::NTHR, 0, s>>>(L)
+            : wino_f4k3_persist_kernel<W4Big, false><<<grid, W4Big::NTHR, 0, s>>>(L);
+  } else if (quad)
     aff     ? wino_f4k3_kernel<W4Quad, false, true><<<(unsigned)total, W4Quad::NTHR, 0, s>>>(L)
     : gated ? wino_f4k3_kernel<W4Quad, true><<<(unsigned)total, W4Quad::NTHR, 0, s>>>(L)
             : wino_f4k3_kernel<W4Quad, false><<<(unsigned)total, W4Quad::NTHR, 0, s>>>(L);

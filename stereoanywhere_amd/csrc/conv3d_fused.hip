@@ -386,7 +386,11 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const float *__restrict__ i
 //   staging = the producer's InstanceNorm + LeakyReLU (+ gate), zero padding, then B^T along D,
 //            fetched one input channel ahead; one barrier per input channel
 //   weights = (G g)[ci][kh][kw][p][co] (sa_conv3d_wd weight layout), wave-uniform (SGPR) operands
-template <int CIN, int COUT, int NT, bool GATED>
+//   WL     = the weights staged in LDS a channel ahead with the input (per channel 54 x COUT
+//            floats, double-buffered), read as wave-uniform LDS vectors instead of SGPR loads
+//            (the scalar-load variant spends 42% of its wave cycles at waitcnt / barrier);
+//            measured slower, so off by default (sa_conv3d_wd_set_variant)
+template <int CIN, int COUT, int NT, bool GATED, bool WL = false>
 __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict__ in, int D, int H, int W,
                                                         const float *__restrict__ wt, InXform tx,
                                                         float *__restrict__ out, double *__restrict__ partial,
@@ -401,6 +405,27 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
   constexpr int CC = COUT < 8 ? COUT : 8;   // output channels per weight group (48 SGPRs)
   __shared__ __attribute__((aligned(16))) float slab[2][LH * ROWP];
   __shared__ double red[COUT * 4 * 2];
+  constexpr int WPC = 54 * COUT, NWL = (WPC + 255) / 256;   // weights per input channel, per thread
+  __shared__ __attribute__((aligned(16))) float wsl[WL ? 2 : 1][WL ? WPC : 4];
+  float pw[NWL];
+  auto wfetch = [&](int ci) __attribute__((always_inline)) {
+    if constexpr (WL) {
+#pragma unroll
+      for (int q = 0; q < NWL; ++q) {
+        const int idx = (int)threadIdx.x + 256 * q;
+        pw[q] = idx < WPC ? wt[(long)ci * WPC + idx] : 0.0f;
+      }
+    }
+  };
+  auto wcommit = [&](int buf) __attribute__((always_inline)) {
+    if constexpr (WL) {
+#pragma unroll
+      for (int q = 0; q < NWL; ++q) {
+        const int idx = (int)threadIdx.x + 256 * q;
+        if (idx < WPC) wsl[buf][idx] = pw[q];
+      }
+    }
+  };
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int w0 = blockIdx.x * TWV, h0 = blockIdx.y * 4;
@@ -487,16 +512,21 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
       for (int c = 0; c < COUT; ++c) M[t][p][c] = 0.0f;
 
   fetch(0);
+  wfetch(0);
   commit(0, 0);
+  wcommit(0);
   __syncthreads();
 #pragma unroll 1
   for (int ci = 0; ci < CIN; ++ci) {
     const int buf = ci & 1;
-    if (ci + 1 < CIN) fetch(ci + 1);
+    if (ci + 1 < CIN) {
+      fetch(ci + 1);
+      wfetch(ci + 1);
+    }
     // lanes 62-63 (no output column) read lane 61's columns: lane + kw stays inside the 64
     // staged columns of the row
     const float *lb = slab[buf] + wv * ROWP + min(lane, TWV - 1) * NP;
-    const float *wc = wt + (long)ci * 9 * 6 * COUT;
+    const float *wc = WL ? wsl[buf] : wt + (long)ci * 9 * 6 * COUT;
     // the kw loop unrolled for the 16-channel convs and the classifier pair (the scalar weight
     // loads of the next kw then overlap this one's FMAs: 711 -> 567 and 568 -> 506 us), rolled
     // for 8 -> 8 (unrolled it measured 1057 -> 1310 us: SGPR pressure of 48 weights per kw;
@@ -529,7 +559,10 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
         }
       }
     }
-    if (ci + 1 < CIN) commit(ci + 1, buf ^ 1);
+    if (ci + 1 < CIN) {
+      commit(ci + 1, buf ^ 1);
+      wcommit(buf ^ 1);
+    }
     __syncthreads();
   }
 
@@ -851,6 +884,12 @@ extern "C" int sa_conv3d(const float *in, int B, int Cin, int Di, int Hi, int Wi
   return SA_E_ARG;
 }
 
+// 0: wave-uniform scalar weight loads (default); 1: the weights staged in LDS (conv3d_wd_kernel
+// WL), measured slower: bench_hourglass whole hourglass 8.62 against 7.73 ms, the 8 -> 8 convs
+// 1.29-1.36 against 1.08-1.11 ms (LDS reads in the FMA loop cost more than the SGPR waits)
+static int sa_conv3d_wd_lds_weights = 0;
+extern "C" void sa_conv3d_wd_set_variant(int lds_weights) { sa_conv3d_wd_lds_weights = lds_weights ? 1 : 0; }
+
 extern "C" int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W, const float *weight_wd, int Cout,
                             const float *in_mean, const float *in_rstd, int act, float slope, const float *gate_l,
                             const float *gate_r, float *out, double *stats_partial, void *stream) {
@@ -873,7 +912,11 @@ extern "C" int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W
   SA_REQUIRE(in_mean && act, "sa_conv3d_wd: built for an InstanceNorm + LeakyReLU producer");
 #define SA_WD(CI, CO, NTV, G)                                                                                   \
   if (Cin == CI && Cout == CO && (gate_l != nullptr) == G) {                                                    \
-    conv3d_wd_kernel<CI, CO, NTV, G><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, tilesD); \
+    if (sa_conv3d_wd_lds_weights)                                                                               \
+      conv3d_wd_kernel<CI, CO, NTV, G, true><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, \
+                                                                  tilesD);                                      \
+    else                                                                                                        \
+      conv3d_wd_kernel<CI, CO, NTV, G><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, tilesD); \
     return sa::check_launch("sa_conv3d_wd");                                                                     \
   }
   SA_WD(8, 8, 2, false)

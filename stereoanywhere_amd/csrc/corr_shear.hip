@@ -1,0 +1,212 @@
+// K4 on a disparity-sheared pyramid: the correlation-pyramid lookup (CorrBlock1D.__call__,
+// corr.py:93-115, through bilinear_sampler, utils.py:19-35) fused with the motion encoder's
+// convc1 (update.py:75, 84), reading a copy of the pyramid laid out so that a wave's lanes
+// (consecutive pixels j of one image row) read consecutive addresses.
+//
+// The row layout (corr_volume.hip: pixel row j holds its levels back to back) puts each
+// pixel's 10-cell window in its own row, ~1.8 KB from its neighbour's: a wave touches 64
+// separate cache lines per level, and the lookup moved 2.3x the bytes it uses.  Level l of
+// image row (b, h) is sheared here into S_l[e][j] = C_l[j][(j >> l) - e + W_l - 1]:
+//   e in [0, E_l), E_l = W_l + ((W1 - 1) >> l)   (all (j, k) pairs of the level, k = (j >> l) -
+//   e + W_l - 1; cells with k outside [0, W_l) are stored as 0, the reference's zero padding)
+// so pixel j's cell k sits at row e = (j >> l) - k + W_l - 1, column j.  Neighbouring pixels
+// at the same disparity read the same row e at neighbouring columns: one load instruction of
+// the wave is one or two row segments.  Storage ~2x the row layout; written once per forward
+// by sa_corr_pyramid_shear from the row-layout pyramid, read at every GRU iteration.
+#include "sa_common.h"
+
+namespace {
+
+// the sheared slice of one image row (b, h): levels back to back, each E_l x W1 floats
+struct ShGeo {
+  int L, W1, W2;
+  int wid[4], rows[4];
+  long off[4];   // level offsets within a slice (floats)
+  long slice;    // floats per slice, a multiple of 4
+};
+
+ShGeo shear_geo(int W1, int W2, int L) {
+  ShGeo g{};
+  g.L = L;
+  g.W1 = W1;
+  g.W2 = W2;
+  long off = 0;
+  for (int l = 0; l < L; ++l) {
+    g.wid[l] = sa_pyramid_level_width(W2, l);
+    g.rows[l] = g.wid[l] + ((W1 - 1) >> l);
+    g.off[l] = off;
+    off += (long)g.rows[l] * W1;
+  }
+  g.slice = (off + 3) / 4 * 4;
+  return g;
+}
+
+// one level, one (64 j x 64 e) tile of one slice: the source band (64 rows of <= 128 cells)
+// through LDS, written along j (coalesced)
+__global__ __launch_bounds__(256) void shear_kernel(const float *__restrict__ pyr, long rs, int W1, int off_l,
+                                                    int Wl, int El, int lev, long slice_sz, long soff,
+                                                    float *__restrict__ out) {
+  __shared__ float tile[64][129];
+  const long slice = blockIdx.z;
+  const int j0 = blockIdx.x * 64, e0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+  // k = (j >> lev) - e + Wl - 1 over the tile spans [kmin, kmin + 126]
+  const int kmin = (j0 >> lev) - (e0 + 63) + Wl - 1;
+  for (int i = tid; i < 64 * 128; i += 256) {
+    const int r = i >> 7, c = i & 127, j = j0 + r, k = kmin + c;
+    tile[r][c] = (j < W1 && k >= 0 && k < Wl) ? pyr[(slice * W1 + j) * rs + off_l + k] : 0.0f;
+  }
+  __syncthreads();
+  for (int i = tid; i < 64 * 64; i += 256) {
+    const int el = i >> 6, jl = i & 63, j = j0 + jl, e = e0 + el;
+    if (j < W1 && e < El) {
+      const int k = (j >> lev) - e + Wl - 1;
+      out[slice * slice_sz + soff + (long)e * W1 + j] = tile[jl][k - kmin];
+    }
+  }
+}
+
+struct ShLGeo {
+  int H, W1;
+  long cbs;
+  long slice;
+  int wid[4], rows[4];
+  int off[4];
+};
+
+// lookup_c1_vec_kernel (corr_lookup.hip) on the sheared pyramid: the same per-tap grid
+// arithmetic, the window's cells gathered by one load each from the rows e of column j
+template <int L, int R, int COUT>
+__global__ __launch_bounds__(256) void lookup_c1_shear_kernel(const float *__restrict__ sa, const float *__restrict__ sb,
+                                                              const float *__restrict__ cx, ShLGeo g, int npix,
+                                                              const float *__restrict__ wt,
+                                                              const float *__restrict__ bias, int nvol,
+                                                              float *__restrict__ out) {
+  constexpr int K = 2 * R + 1, NT = L * K, WIN = 2 * R + 4;   // cells x_-R - 1 .. x_-R + 2R + 2
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= npix) return;
+  const int v = blockIdx.y;
+  const int hw = g.H * g.W1;
+  const int b = p / hw, rem = p - b * hw;
+  const int h = rem / g.W1, j = rem - h * g.W1;
+  const float x = cx[(long)b * g.cbs + rem];
+  const float *__restrict__ S = (v ? sb : sa) + ((long)b * g.H + h) * g.slice + j;
+  float f[NT];
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    const int Wl = g.wid[l], El = g.rows[l];
+    const float xl = x / (float)(1 << l);
+    const float denom = (float)(Wl - 1);
+    const float sf = (float)(Wl - 1) / 2.0f;
+    int xi[K];
+    float wgt[K];
+#pragma unroll
+    for (int t = -R; t <= R; ++t) {
+      const float x0 = (float)t + xl;
+      const float xg = 2.0f * x0 / denom - 1.0f;
+      const float ix = (xg + 1.0f) * sf;
+      float xw = floorf(ix);
+      wgt[t + R] = ix - xw;
+      // (the wide clamp of lookup_c1_vec_kernel: consecutive taps stay within 1 of x_-R + t)
+      xw = fminf(fmaxf(xw, -16777216.0f), 16777216.0f);
+      xi[t + R] = (int)xw;
+    }
+    // cell k = xi[0] - 1 + c sits at row e = (j >> l) - k + Wl - 1 of column j
+    const int e0 = (j >> l) - xi[0] + Wl;
+    const float *__restrict__ lv = S + g.off[l];
+    float cell[WIN];
+#pragma unroll
+    for (int c = 0; c < WIN; ++c) {
+      const int e = e0 - c;
+      cell[c] = (unsigned)e < (unsigned)El ? lv[(long)e * g.W1] : 0.0f;
+    }
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const int d = xi[t] - xi[0] - t;   // -1, 0 or +1 (fp32 rounding of the grid position)
+      const float c0 = d == 0 ? cell[t + 1] : d < 0 ? cell[t] : cell[t + 2];
+      const float c1 = d == 0 ? cell[t + 2] : d < 0 ? cell[t + 1] : cell[t + 3 < WIN ? t + 3 : WIN - 1];
+      const float v0 = (xi[t] >= 0 && xi[t] <= Wl - 1) ? c0 : 0.0f;
+      const float v1 = (xi[t] + 1 >= 0 && xi[t] + 1 <= Wl - 1) ? c1 : 0.0f;
+      const float w = wgt[t];
+      f[l * K + t] = v0 * (1.0f - w) + v1 * w;
+    }
+  }
+  float *__restrict__ o = out + ((long)b * nvol + v) * COUT * hw + rem;
+#pragma unroll 4
+  for (int c0 = 0; c0 < COUT; c0 += 8) {
+    float acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = bias[c0 + c];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[c] = fmaf(wt[k * COUT + c0 + c], f[k], acc[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) o[(long)(c0 + c) * hw] = fmaxf(acc[c], 0.0f);
+  }
+}
+
+}  // namespace
+
+extern "C" long sa_shear_slice_size(int W1, int W2, int num_levels) {
+  if (W1 <= 0 || W2 <= 0 || num_levels < 1 || num_levels > 4) return -1;
+  return shear_geo(W1, W2, num_levels).slice;
+}
+
+extern "C" long sa_shear_level_offset(int W1, int W2, int num_levels, int level) {
+  if (level < 0 || level >= num_levels || num_levels > 4) return -1;
+  return shear_geo(W1, W2, num_levels).off[level];
+}
+
+extern "C" int sa_corr_pyramid_shear(const float *pyramid, long row_stride, int B, int H, int W1, int W2,
+                                     int num_levels, float *sheared, void *stream) {
+  SA_REQUIRE(pyramid && sheared, "sa_corr_pyramid_shear: null pointer");
+  SA_REQUIRE(B > 0 && H > 0 && W1 > 0 && W2 > 0 && num_levels >= 1 && num_levels <= 4,
+             "sa_corr_pyramid_shear: bad shape");
+  SA_REQUIRE(row_stride >= sa_pyramid_level_offset(W2, num_levels), "sa_corr_pyramid_shear: row_stride too small");
+  SA_REQUIRE((long)B * H <= 65535, "sa_corr_pyramid_shear: more than 65535 image rows");
+  const ShGeo g = shear_geo(W1, W2, num_levels);
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_LOOKUP, s);
+  for (int l = 0; l < num_levels; ++l) {
+    const dim3 grid((unsigned)((W1 + 63) / 64), (unsigned)((g.rows[l] + 63) / 64), (unsigned)(B * H));
+    shear_kernel<<<grid, 256, 0, s>>>(pyramid, row_stride, W1, sa_pyramid_level_offset(W2, l), g.wid[l], g.rows[l],
+                                      l, g.slice, g.off[l], sheared);
+  }
+  return sa::check_launch("sa_corr_pyramid_shear");
+}
+
+extern "C" int sa_corr_lookup_conv1x1_sheared(const float *sheared_a, const float *sheared_b, int W2, int num_levels,
+                                              int radius, const float *coords_x, long coords_bstride, int B, int H,
+                                              int W1, const float *weight_kc, const float *bias, int Cout, float *out,
+                                              void *stream) {
+  SA_REQUIRE(sheared_a && coords_x && out && weight_kc && bias, "sa_corr_lookup_conv1x1_sheared: null pointer");
+  SA_REQUIRE(B > 0 && H > 0 && W1 > 0 && W2 > 0, "sa_corr_lookup_conv1x1_sheared: empty shape");
+  SA_REQUIRE(num_levels == 4 && radius == 4 && Cout == 64,
+             "sa_corr_lookup_conv1x1_sheared: built for 4 levels, radius 4, 64 outputs (got %d, %d, %d)", num_levels,
+             radius, Cout);
+  SA_REQUIRE(sa_pyramid_level_width(W2, num_levels - 1) >= 2,
+             "sa_corr_lookup_conv1x1_sheared: level %d of width %d is too narrow to sample", num_levels - 1,
+             sa_pyramid_level_width(W2, num_levels - 1));
+  const long npix = (long)B * H * W1;
+  SA_REQUIRE(npix < (1L << 31), "sa_corr_lookup_conv1x1_sheared: too many pixels");
+  const ShGeo sg = shear_geo(W1, W2, num_levels);
+  ShLGeo g{};
+  g.H = H;
+  g.W1 = W1;
+  g.cbs = coords_bstride;
+  g.slice = sg.slice;
+  for (int l = 0; l < 4; ++l) {
+    g.wid[l] = l < num_levels ? sg.wid[l] : 0;
+    g.rows[l] = l < num_levels ? sg.rows[l] : 0;
+    g.off[l] = l < num_levels ? (int)sg.off[l] : 0;
+  }
+  const int nvol = sheared_b ? 2 : 1;
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_LOOKUP, s);
+  dim3 grid((unsigned)((npix + 255) / 256), nvol);
+  lookup_c1_shear_kernel<4, 4, 64><<<grid, 256, 0, s>>>(sheared_a, sheared_b ? sheared_b : sheared_a, coords_x, g,
+                                                        (int)npix, weight_kc, bias, nvol, out);
+  return sa::check_launch("sa_corr_lookup_conv1x1_sheared");
+}

@@ -106,12 +106,15 @@ __global__ __launch_bounds__(256) void gru_out_kernel(const float *__restrict__ 
 
 // F.avg_pool2d(x, 3, stride=2, padding=1), count_include_pad=True -> always / 9.
 // grid: x over output columns (64 per block), y over output rows (4 per block), z = (b, c)
+// (in_p / out_p: row pitches of the planes, >= W / Wo: columns beyond the width are not read
+// or written)
 __global__ __launch_bounds__(256) void pool2x_kernel(const float *__restrict__ in, long in_bs, int C, int H,
-                                                     int W, int Ho, int Wo, float *__restrict__ out, long out_bs) {
+                                                     int W, int Ho, int Wo, float *__restrict__ out, long out_bs,
+                                                     int in_p, int out_p) {
   const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (x >= Wo || y >= Ho) return;
   const int b = blockIdx.z / C, c = blockIdx.z % C;
-  const float *p = in + b * in_bs + (long)c * H * W;
+  const float *p = in + b * in_bs + (long)c * H * in_p;
   float s = 0.f;
   for (int dy = -1; dy <= 1; ++dy) {
     const int yy = 2 * y + dy;
@@ -119,28 +122,28 @@ __global__ __launch_bounds__(256) void pool2x_kernel(const float *__restrict__ i
     for (int dx = -1; dx <= 1; ++dx) {
       const int xx = 2 * x + dx;
       if (xx < 0 || xx >= W) continue;
-      s += p[yy * W + xx];
+      s += p[yy * in_p + xx];
     }
   }
-  out[b * out_bs + (long)c * Ho * Wo + y * Wo + x] = s / 9.0f;
+  out[b * out_bs + (long)c * Ho * out_p + y * out_p + x] = s / 9.0f;
 }
 
 // F.interpolate(bilinear, align_corners=True) (upsample_bilinear2d arithmetic); grid as pool2x
 __global__ __launch_bounds__(256) void interp_kernel(const float *__restrict__ in, long in_bs, int C, int H,
                                                      int W, int Ho, int Wo, float sh, float sw,
-                                                     float *__restrict__ out, long out_bs) {
+                                                     float *__restrict__ out, long out_bs, int in_p, int out_p) {
   const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (x >= Wo || y >= Ho) return;
   const int b = blockIdx.z / C, c = blockIdx.z % C;
-  const float *p = in + b * in_bs + (long)c * H * W;
+  const float *p = in + b * in_bs + (long)c * H * in_p;
   const float ry = sh * (float)y, rx = sw * (float)x;
   const int y0 = (int)ry, x0 = (int)rx;
   const int yp = y0 < H - 1 ? 1 : 0, xp = x0 < W - 1 ? 1 : 0;
   const float ly1 = ry - (float)y0, ly0 = 1.0f - ly1;
   const float lx1 = rx - (float)x0, lx0 = 1.0f - lx1;
-  const float *r0 = p + y0 * W, *r1 = p + (y0 + yp) * W;
+  const float *r0 = p + y0 * in_p, *r1 = p + (y0 + yp) * in_p;
   const float v = ly0 * (lx0 * r0[x0] + lx1 * r0[x0 + xp]) + ly1 * (lx0 * r1[x0] + lx1 * r1[x0 + xp]);
-  out[b * out_bs + (long)c * Ho * Wo + y * Wo + x] = v;
+  out[b * out_bs + (long)c * Ho * out_p + y * out_p + x] = v;
 }
 
 // interp_kernel with 4 consecutive outputs per thread and one float4 store (Wo % 4 == 0,
@@ -148,16 +151,16 @@ __global__ __launch_bounds__(256) void interp_kernel(const float *__restrict__ i
 // to interp_kernel. grid: x over quads of output columns (64 per block), y over rows (4)
 __global__ __launch_bounds__(256) void interp_v4_kernel(const float *__restrict__ in, long in_bs, int C, int H,
                                                         int W, int Ho, int Wo, float sh, float sw,
-                                                        float *__restrict__ out, long out_bs) {
+                                                        float *__restrict__ out, long out_bs, int in_p) {
   const int xq = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (4 * xq >= Wo || y >= Ho) return;
   const int b = blockIdx.z / C, c = blockIdx.z % C;
-  const float *p = in + b * in_bs + (long)c * H * W;
+  const float *p = in + b * in_bs + (long)c * H * in_p;
   const float ry = sh * (float)y;
   const int y0 = (int)ry;
   const int yp = y0 < H - 1 ? 1 : 0;
   const float ly1 = ry - (float)y0, ly0 = 1.0f - ly1;
-  const float *r0 = p + y0 * W, *r1 = p + (y0 + yp) * W;
+  const float *r0 = p + y0 * in_p, *r1 = p + (y0 + yp) * in_p;
   float v[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -282,40 +285,55 @@ extern "C" int sa_gru_out(const float *xc, long xc_bs, const float *bx, const fl
   return sa_gru_out_split(xc, xc_bs, bx, qh, nullptr, qh_bs, cq, c_bs, z, B, C, HW, h, h_bs, stream);
 }
 
-extern "C" int sa_pool2x(const float *in, long in_bs, int B, int C, int H, int W, float *out, long out_bs,
-                         void *stream) {
+extern "C" int sa_pool2x_p(const float *in, long in_bs, int in_pitch, int B, int C, int H, int W, float *out,
+                           long out_bs, int out_pitch, void *stream) {
   SA_REQUIRE(in && out, "sa_pool2x: null pointer");
   SA_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0 && (long)B * C <= 65535, "sa_pool2x: bad shape");
-  SA_REQUIRE((long)H * W < (1L << 31), "sa_pool2x: plane too large");
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  SA_REQUIRE(in_pitch >= W && out_pitch >= Wo, "sa_pool2x: row pitch below the width");
+  SA_REQUIRE((long)H * in_pitch < (1L << 31), "sa_pool2x: plane too large");
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_MISC, s);
-  if (W % 8 == 0 && Wo % 4 == 0 && al16(in) && al16(out) && in_bs % 4 == 0 && out_bs % 4 == 0)
+  if (in_pitch == W && out_pitch == Wo && W % 8 == 0 && Wo % 4 == 0 && al16(in) && al16(out) && in_bs % 4 == 0 &&
+      out_bs % 4 == 0)
     pool2x_v4_kernel<<<dim3((Wo / 4 + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, out,
                                                                                    out_bs);
   else
-    pool2x_kernel<<<dim3((Wo + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, out, out_bs);
+    pool2x_kernel<<<dim3((Wo + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, out, out_bs,
+                                                                            in_pitch, out_pitch);
   return sa::check_launch("sa_pool2x");
 }
 
-extern "C" int sa_interp_bilinear_ac(const float *in, long in_bs, int B, int C, int H, int W, int Ho, int Wo,
-                                     float *out, long out_bs, void *stream) {
+extern "C" int sa_pool2x(const float *in, long in_bs, int B, int C, int H, int W, float *out, long out_bs,
+                         void *stream) {
+  return sa_pool2x_p(in, in_bs, W, B, C, H, W, out, out_bs, (W + 2 - 3) / 2 + 1, stream);
+}
+
+extern "C" int sa_interp_bilinear_ac_p(const float *in, long in_bs, int in_pitch, int B, int C, int H, int W, int Ho,
+                                       int Wo, float *out, long out_bs, int out_pitch, void *stream) {
   SA_REQUIRE(in && out, "sa_interp_bilinear_ac: null pointer");
   SA_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && (long)B * C <= 65535,
              "sa_interp_bilinear_ac: bad shape");
-  SA_REQUIRE((long)H * W < (1L << 31) && (long)Ho * Wo < (1L << 31), "sa_interp_bilinear_ac: plane too large");
+  SA_REQUIRE(in_pitch >= W && out_pitch >= Wo, "sa_interp_bilinear_ac: row pitch below the width");
+  SA_REQUIRE((long)H * in_pitch < (1L << 31) && (long)Ho * out_pitch < (1L << 31),
+             "sa_interp_bilinear_ac: plane too large");
   // area_pixel_compute_scale(align_corners=True): (in - 1) / (out - 1), 0 for out == 1
   const float sh = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.0f;
   const float sw = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.0f;
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_MISC, s);
-  if (Wo % 4 == 0 && al16(out) && out_bs % 4 == 0)
+  if (out_pitch == Wo && Wo % 4 == 0 && al16(out) && out_bs % 4 == 0)
     interp_v4_kernel<<<dim3((Wo / 4 + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, sh, sw,
-                                                                                   out, out_bs);
+                                                                                   out, out_bs, in_pitch);
   else
     interp_kernel<<<dim3((Wo + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, sh, sw, out,
-                                                                            out_bs);
+                                                                            out_bs, in_pitch, out_pitch);
   return sa::check_launch("sa_interp_bilinear_ac");
+}
+
+extern "C" int sa_interp_bilinear_ac(const float *in, long in_bs, int B, int C, int H, int W, int Ho, int Wo,
+                                     float *out, long out_bs, void *stream) {
+  return sa_interp_bilinear_ac_p(in, in_bs, W, B, C, H, W, Ho, Wo, out, out_bs, Wo, stream);
 }
 
 extern "C" int sa_relu_copy(const float *in, long in_bs, int B, int C, int HW, float *out, long out_bs,

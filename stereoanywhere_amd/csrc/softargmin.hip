@@ -267,6 +267,149 @@ __global__ __launch_bounds__(256) void sam_strided_kernel(LineJob jd, LineJob jc
   }
 }
 
+// exp(d) for d = x - max <= 0 and log2(y) for y = p + 1e-6 in [1e-6, 1 + 1e-6]: the hardware
+// v_exp_f32 / v_log_f32 (one quarter-rate op each; relative error ~1e-7 here, against ~10 VALU
+// operations of the library's range-reduced expf / log2f).  The slice kernel below is
+// VALU-bound, not HBM-bound, with the library versions.
+__device__ __forceinline__ float exp_le0(float d) { return __builtin_amdgcn_exp2f(d * 1.44269504088896341f); }
+__device__ __forceinline__ float log2_pos(float y) { return __builtin_amdgcn_logf(y); }
+
+// One pass over each (b, h) slice: both reductions of a volume from one read.  A block of 1024
+// threads holds the slice's n x n cells in registers, element (k, j) at wave k % 16, slot
+// r = k / 16, lane j % 64, slot c = j / 64 (j is the contiguous axis, sj == 1).  The right
+// side (softmax over j, per k) reduces within a wave as each row's loads land; the left side
+// (softmax over k, per j) combines the 16 waves' column partials through LDS.  blockIdx.y
+// picks the volume (0: disparity, 1: confidence).  The two launches of the line kernels above
+// each read both volumes; this reads each once.
+template <int NR, int NC>
+__global__ __launch_bounds__(1024) void sam_slice_kernel(const float *__restrict__ vd, const float *__restrict__ vc,
+                                                         SGeo g, int n, float *dL, float *dR, float *cL, float *cR,
+                                                         int y0) {
+  __shared__ float red[16][NC * 64];
+  __shared__ float colv[NC * 64];
+  const int conf = y0 + (int)blockIdx.y;
+  const float *vol = conf ? vc : vd;
+  float *outL = conf ? cL : dL, *outR = conf ? cR : dR;
+  const int bh = blockIdx.x, b = bh / g.H, h = bh % g.H;
+  const float *src = vol + (long)b * g.sb + (long)h * g.sh;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long ob = (long)b * g.obs + (long)h * n;
+  float x[NR][NC];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int k = w + 16 * r;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int j = lane + 64 * c;
+      x[r][c] = (k < n && j < n) ? src[(long)k * g.sk + j] : -INFINITY;
+    }
+  }
+  // ---- right: per row k, softmax over j (estimate_right_*, utils.py:132-152, 162-170)
+  const float lw_r = g.log2W1;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int k = w + 16 * r;
+    if (k >= n) continue;   // wave-uniform
+    float m = x[r][0];
+#pragma unroll
+    for (int c = 1; c < NC; ++c) m = fmaxf(m, x[r][c]);
+    m = wave_max(m);
+    float e[NC], se = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      e[c] = exp_le0(x[r][c] - m);   // -inf (j >= n) -> 0
+      se += e[c];
+    }
+    const float inv = 1.0f / wave_sum(se);
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int j = lane + 64 * c;
+      const float p = e[c] * inv;
+      if (j < n) acc += conf ? p * log2_pos(p + 1e-6f) : p * (float)j;
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) outR[ob + k] = conf ? 1.0f - (-acc) / lw_r : acc - (float)k;
+  }
+  // ---- left: per column j, softmax over k (estimate_left_*, utils.py:112-130, 154-161)
+  auto column_total = [&](float *part, bool is_max) __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) red[w][lane + 64 * c] = part[c];
+    __syncthreads();
+    if (tid < n) {
+      float t = red[0][tid];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) t = is_max ? fmaxf(t, red[i][tid]) : t + red[i][tid];
+      colv[tid] = t;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NC; ++c) part[c] = colv[lane + 64 * c < n ? lane + 64 * c : 0];
+    __syncthreads();   // red / colv are reused by the next total
+  };
+  float q[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    q[c] = x[0][c];
+#pragma unroll
+    for (int r = 1; r < NR; ++r) q[c] = fmaxf(q[c], x[r][c]);
+  }
+  column_total(q, true);   // q = column max
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    float se = 0.f;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      x[r][c] = exp_le0(x[r][c] - q[c]);   // rows k >= n: -inf -> 0
+      se += x[r][c];
+    }
+    q[c] = se;
+  }
+  column_total(q, false);   // q = column sum of exponentials
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const float inv = 1.0f / q[c];
+    float acc = 0.f;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int k = w + 16 * r;
+      const float p = x[r][c] * inv;
+      if (k < n) acc += conf ? p * log2_pos(p + 1e-6f) : p * (float)k;
+    }
+    q[c] = acc;
+  }
+  // the column totals of the accumulated terms, written by the threads that own column tid
+#pragma unroll
+  for (int c = 0; c < NC; ++c) red[w][lane + 64 * c] = q[c];
+  __syncthreads();
+  if (tid < n) {
+    float acc = red[0][tid];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) acc += red[i][tid];
+    outL[ob + tid] = conf ? 1.0f - (-acc) / g.log2W2 : (float)tid - acc;
+  }
+}
+
+// sam_slice_kernel for a slice of side n (sj == 1, W1 == W2); false if no instantiation fits
+bool launch_slices(const float *vd, const float *vc, const SGeo &g, int B, int n, float *dL, float *dR, float *cL,
+                   float *cR, hipStream_t s) {
+  // grid.y: the volumes present (a confidence-only call starts at y0 = 1)
+  const dim3 grid((unsigned)(B * g.H), vd && vc ? 2u : 1u);
+  const int y0 = vd ? 0 : 1;
+#define SA_SLICE(NR_, NC_)                                                                          \
+  if (n <= 16 * NR_ && n <= 64 * NC_) {                                                             \
+    sam_slice_kernel<NR_, NC_><<<grid, 1024, 0, s>>>(vd, vc, g, n, dL, dR, cL, cR, y0);           \
+    return true;                                                                                    \
+  }
+  SA_SLICE(8, 2)
+  SA_SLICE(12, 3)
+  SA_SLICE(16, 4)
+  SA_SLICE(18, 5)
+#undef SA_SLICE
+  return false;
+}
+
 int launch_side(LineJob jd, LineJob jc, const SGeo &g, int B, int left, hipStream_t s) {
   const long nlines = (long)B * g.H * (left ? g.W1 : g.W2);
   const long red_stride = left ? g.sk : g.sj;
@@ -293,6 +436,11 @@ int launch_side(LineJob jd, LineJob jc, const SGeo &g, int B, int left, hipStrea
 
 }  // namespace
 
+// 1: the one-pass slice kernel where it applies (default); 0: the two line-kernel launches
+// (sa_softargmin_set_one_pass, for A/B runs and tests)
+static int sa_softargmin_one_pass = 1;
+extern "C" void sa_softargmin_set_one_pass(int on) { sa_softargmin_one_pass = on ? 1 : 0; }
+
 extern "C" int sa_softargmin_conf(const float *vol_disp, const float *vol_conf, int B, int H, int W1,
                                   int W2, long sb, long sh, long sj, long sk, float *dL, float *dR,
                                   float *cL, float *cR, long out_bs, void *stream) {
@@ -305,6 +453,9 @@ extern "C" int sa_softargmin_conf(const float *vol_disp, const float *vol_conf, 
   SGeo g{H, W1, W2, sb, sh, sj, sk, out_bs, (float)std::log2((double)W1), (float)std::log2((double)W2)};
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_SOFTARGMIN, s);
+  // one read of each volume: a block per (b, h) slice (the model's layout: j contiguous, square)
+  if (sj == 1 && W1 == W2 && sa_softargmin_one_pass && launch_slices(vol_disp, vol_conf, g, B, W1, dL, dR, cL, cR, s))
+    return sa::check_launch("sa_softargmin_conf");
   LineJob ld{vol_disp, dL, 0}, lc{vol_conf, cL, 1};
   LineJob rd{vol_disp, dR, 0}, rc{vol_conf, cR, 1};
   int rc1 = launch_side(ld, lc, g, B, 1, s);

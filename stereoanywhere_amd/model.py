@@ -90,6 +90,14 @@ class ScheduleOptions:
     small_launches: frozenset = field(default_factory=frozenset)
     # the encoders' 7x7 stems and stride-2 convs on the direct fp32-MFMA kernel (False: MIOpen)
     direct_conv: bool = True
+    # the GRU loop's lookups on disparity-sheared copies of the two pyramids (corr_shear.hip:
+    # one load instruction of a wave reads one or two row segments; the row layout spreads
+    # it over 64 cache lines); False: the row-layout lookup
+    sheared_lookup: bool = True
+    # a GRU level whose width is not a multiple of 4 keeps its planes padded to one (zero
+    # columns) and runs on F(4x4) with the gates in the epilogue (False: separate gate kernels and
+    # F(2x2) launches for that level)
+    pad_ragged: bool = True
     # the GRU loop's batch in this many parts, each on a HIP stream of its own: one part's launch
     # tails and small kernels overlap the other's convs (1: one stream, the whole batch per
     # launch).  B = 4 at 544x960: 82.2 ms/step with 1 part, 79.5 with 2, 86-91 with 3-4 (eager);
@@ -334,6 +342,11 @@ class StereoAnywhere(nn.Module):
                                   _shape=(B, H4, W4, W4))
         del mono_rows, vol_d, vol_c
 
+        if self.opts.sheared_lookup:
+            # the lookups read disparity-sheared copies (coalesced across a wave's pixels); the
+            # row-layout buffers are not read again
+            stereo_blk.shear(release=True)
+            mono_blk.shear(release=True)
         parts = min(self.opts.loop_parts, B) if self.stream_overlap else 1
         if parts <= 1:
             return _drive(self._iterate(dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4))
@@ -350,8 +363,12 @@ class StereoAnywhere(nn.Module):
         rows = H4 * W4
 
         def blk(b, lo, hi):
-            return HipCorrBlock1D(None, b.num_levels, b.radius, _pyramid=b.pyramid[lo * rows:hi * rows],
-                                  _shape=(hi - lo, H4, W4, W4))
+            nb = HipCorrBlock1D(None, b.num_levels, b.radius,
+                                _pyramid=None if b.pyramid is None else b.pyramid[lo * rows:hi * rows],
+                                _shape=(hi - lo, H4, W4, W4))
+            if b.sheared is not None:
+                nb.sheared = b.sheared[lo * H4:hi * H4]
+            return nb
         streams, gens = [], []
         for i, (lo, hi) in enumerate(bounds):
             st = self._loop_stream(dev, i)
@@ -554,37 +571,58 @@ class StereoAnywhere(nn.Module):
         # x08 = [motion(126) | flow(2) | interp(h16)], x16 = [pool(h08) | interp(h32)], x32 = [pool(h16)]
         xdims = {"08": 256, "16": 256, "32": 128}
         shapes = {"08": (H4, W4), "16": (H8, W8), "32": (H16, W16)}
+        lvl_of = {"08": 0, "16": 1, "32": 2}
         hd = h08.shape[1]
         o = self.opts
-        # GRU gates in the F(4x4) conv epilogues, per level: the kernel's preconditions (W % 4,
-        # planes then 16-byte aligned) hold or fail per level.  A level with W % 4 != 0 (e.g.
-        # W/16 = 42 or 70 at the middlebury / booster tile presets) keeps the separate gate
-        # kernels and its convs run on F(2x2) in launches of their own (ops.conv2d_k3_multi
-        # splits a mixed group), while the other levels stay on the fused path.
-        fused = {k: o.fuse_gates and ops.gate_f4_ok() and s[1] % 4 == 0 for k, s in shapes.items()}
-        fuse_out = {k: fused[k] and o.fuse_out for k in shapes}
+        # GRU gates in the F(4x4) conv epilogues, per level.  A level whose width is not a
+        # multiple of 4 (e.g. W/16 = 42 or 70 at the middlebury / booster tile presets) keeps
+        # its state in PITCHED planes, rows padded to a multiple of 4 with zero columns
+        # (opts.pad_ragged), which F(4x4) reads as the right zero padding and keeps zero in its
+        # outputs; without it that level keeps the separate gate kernels and F(2x2) launches of
+        # its own (ops.conv2d_k3_multi splits a mixed group).
+        f4 = o.fuse_gates and ops.gate_f4_ok()
+        # (not the 1/4 level: its planes are also read and written by the lookup, motion and
+        # flow kernels, which take dense planes only)
+        fused = {k: f4 and (s[1] % 4 == 0 or (o.pad_ragged and k != "08")) for k, s in shapes.items()}
+        # row pitch of each level's GRU planes (its width unless padded) and the conv width
+        pitch = {k: (s[1] + 3) // 4 * 4 if fused[k] else s[1] for k, s in shapes.items()}
+        wid = {k: s[1] if pitch[k] != s[1] else None for k, s in shapes.items()}
+        # (a padded level always updates its state in the r*h conv's epilogue: the gate kernels
+        # take dense planes)
+        fuse_out = {k: fused[k] and (o.fuse_out or wid[k] is not None) for k in shapes}
         hxr, xq, rh, xs = {}, {}, {}, {}
+        ctxp = list(ctx)
         for k, h in zip(("08", "16", "32"), hid):
             if fused[k]:
+                padded = wid[k] is not None
+                alloc = torch.zeros if padded else torch.empty
+                Hk, Wk = shapes[k]
                 # one buffer per level, [h | x | r*h]: the z/r conv reads cat(h, x) and the r*h
                 # conv reads r*h as channel views of it (no torch.cat)
-                hxr[k] = torch.empty((B, 2 * hd + xdims[k], *shapes[k]), device=dev, dtype=f32)
-                hxr[k][:, :hd].copy_(h)
+                hxr[k] = alloc((B, 2 * hd + xdims[k], Hk, pitch[k]), device=dev, dtype=f32)
+                hxr[k][:, :hd, :, :Wk].copy_(h)
                 xs[k] = hxr[k][:, hd:hd + xdims[k]]
                 rh[k] = hxr[k][:, hd + xdims[k]:]
                 # convq's x part lands in channels 2*hd.. of a [B, 3*hd] buffer: gru_out reads it there
-                xq[k] = torch.empty((B, 3 * hd, *shapes[k]), device=dev, dtype=f32)
+                xq[k] = alloc((B, 3 * hd, Hk, pitch[k]), device=dev, dtype=f32)
+                if padded:   # the context planes cz | cr | cq of the level, pitched once per forward
+                    c = ctx[lvl_of[k]]
+                    cp = torch.zeros((B, c.shape[1], Hk, pitch[k]), device=dev, dtype=f32)
+                    cp[..., :Wk].copy_(c)
+                    ctxp[lvl_of[k]] = cp
             else:
                 xs[k] = torch.empty((B, xdims[k], *shapes[k]), device=dev, dtype=f32)
                 rh[k] = torch.empty_like(h)
+        ctx = ctxp
         h08, h16, h32 = (hxr[k][:, :hd] if fused[k] else h for k, h in zip(("08", "16", "32"), hid))
         x08, x16, x32 = xs["08"], xs["16"], xs["32"]
         hs = {"08": h08, "16": h16, "32": h32}
-        z = {k: torch.empty(h.shape, device=dev, dtype=f32) for k, h in hs.items()}
+        z = {k: (torch.zeros if wid[k] is not None else torch.empty)(h.shape, device=dev, dtype=f32)
+             for k, h in hs.items()}
         cz = [c[:, 0:128] for c in ctx]
         cr = [c[:, 128:256] for c in ctx]
         cq = [c[:, 256:384] for c in ctx]
-        lvl = {"08": 0, "16": 1, "32": 2}
+        lvl = lvl_of
 
         def conv_group(*probs, name=None):
             """Independent 3x3 convs in one launch (opts.group_convs = False: one launch each)."""
@@ -598,9 +636,9 @@ class StereoAnywhere(nn.Module):
                 # convz | convr over cat(h, x) (+ bias) with z = sigmoid(. + cz) and r*h = sigmoid(. + cr) * h
                 # in the epilogue (update.py:24-25); convq's x part (bias added in gru_out)
                 hx = hxr[key][:, :hd + xdims[key]]
-                return [dict(x=hx, U=g["Uzr"], bias=g["bzr"], out=z[key],
+                return [dict(x=hx, U=g["Uzr"], bias=g["bzr"], out=z[key], width=wid[key],
                              gate=dict(mode=1, ctx=ctx[lvl[key]], h=h, out2=rh[key])),
-                        dict(x=x, U=g["Uqx"], out=xq[key][:, 2 * hd:])]
+                        dict(x=x, U=g["Uqx"], out=xq[key][:, 2 * hd:], width=wid[key])]
             # x and h halves of convz/convr/convq; bias added in the gate kernels
             return [dict(x=x, U=g["Ux"]), dict(x=h, U=g["Uhzr"])]
 
@@ -624,7 +662,7 @@ class StereoAnywhere(nn.Module):
             ``split``) whose sums q_finish hands to gru_out."""
             if fuse_out[key]:
                 g = dw["g" + key]
-                return [dict(x=rh[key], U=g["Uqh"], bias=g["bx"][2 * hd:], out=hs[key],
+                return [dict(x=rh[key], U=g["Uqh"], bias=g["bx"][2 * hd:], out=hs[key], width=wid[key],
                              gate=dict(mode=2, ctx=cq[lvl[key]], h=hs[key], z=z[key], add=xq[key][:, 2 * hd:]))]
             return qh_split(key) if split else [dict(x=rh[key], U=dw["g" + key]["Uqh"])]
 
@@ -641,7 +679,12 @@ class StereoAnywhere(nn.Module):
         # motion encoder reads neither GRU state, so its convs share gru16's launches.  Every op
         # is deterministic and reads the same inputs as in the reference order: the result is
         # identical, with fewer and fuller conv launches.
-        ops.pool2x(h16, x32)
+        def pool(src, ks, dst, kd):
+            ops.pool2x(src, dst, width=wid[ks], out_width=wid[kd])
+
+        def up(src, ks, dst, kd):
+            ops.interp(src, dst, width=wid[ks], out_width=wid[kd])
+        pool(h16, "16", x32, "32")
         xc32, hzr32 = conv_group(*gate_x_h("32", x32, h32), name="pro32")
         gru_zr(2, "32", h32, xc32, hzr32)
         q_finish(2, "32", xc32, conv_group(*q_probs("32", False), name="pro32"))
@@ -650,8 +693,8 @@ class StereoAnywhere(nn.Module):
             # lookup of both pyramids + convc1 + ReLU in one kernel (sample 2b: stereo, 2b+1: mono)
             stereo_blk.lookup_conv1x1_into(coords_x, dw["c1_kc"], enc.convc1.bias, c1, other=mono_blk)
             fl = ops.conv2d_small(flow, dw["f1"], enc.convf1.bias, 64, 7, relu=True)
-            ops.pool2x(h08, x16[:, :128])
-            ops.interp(h32, x16[:, 128:])
+            pool(h08, "08", x16[:, :128], "16")
+            up(h32, "32", x16[:, 128:], "16")
             # gru16's x/h convs + the motion encoder's 3x3 convs (bias + ReLU in the epilogue,
             # written straight into the motion conv's input cat(convc2(stereo), convc2(mono),
             # convf2(convf1(flow))))
@@ -668,11 +711,11 @@ class StereoAnywhere(nn.Module):
             q_finish(1, "16", xc16, res[:len(qp)])
             yield   # half an iteration (the batch-parts schedule interleaves here)
             ops.flow_update(coords_x, None, None, x08[:, 126:128])
-            ops.interp(h16, x08[:, 128:])
+            up(h16, "16", x08[:, 128:], "08")
             # gru08's x/h convs (+ gru32's of the next iteration), then the r*h convs
             probs = gate_x_h("08", x08, h08)
             if not last:
-                ops.pool2x(h16, x32)
+                pool(h16, "16", x32, "32")
                 probs += gate_x_h("32", x32, h32)
             res = conv_group(*probs, name="zr08")
             xc08, hzr08 = res[:2]

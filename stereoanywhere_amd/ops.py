@@ -182,6 +182,45 @@ def corr_lookup_conv1x1(pyr_a: torch.Tensor, pyr_b: Optional[torch.Tensor], W2: 
     return out
 
 
+def corr_pyramid_shear(pyr: torch.Tensor, B: int, H: int, W1: int, W2: int, num_levels: int = 4) -> torch.Tensor:
+    """Row-layout pyramid [B*H*W1, row_stride] -> its disparity-sheared copy [B*H, slice]
+    (sa_corr_pyramid_shear; read by corr_lookup_conv1x1_sheared)."""
+    _check(pyr, "pyramid")
+    if pyr.shape[0] != B * H * W1:
+        raise RuntimeError(f"pyramid rows {pyr.shape[0]} != B*H*W1 {B * H * W1}")
+    slice_sz = int(N.lib().sa_shear_slice_size(W1, W2, num_levels))
+    out = torch.empty((B * H, slice_sz), device=pyr.device, dtype=torch.float32)
+    N.call("sa_corr_pyramid_shear", pyr.data_ptr(), pyr.shape[1], B, H, W1, W2, num_levels, out.data_ptr(),
+           _stream(pyr))
+    return out
+
+
+def corr_lookup_conv1x1_sheared(sh_a: torch.Tensor, sh_b: Optional[torch.Tensor], W2: int, num_levels: int,
+                                radius: int, coords_x: torch.Tensor, weight_kc: torch.Tensor, bias: torch.Tensor,
+                                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """corr_lookup_conv1x1 on sheared pyramids [B*H, slice] (corr_pyramid_shear)."""
+    _check(sh_a, "sheared_a")
+    if sh_b is not None:
+        _check(sh_b, "sheared_b")
+        if sh_b.shape != sh_a.shape:
+            raise RuntimeError("both sheared pyramids must share a geometry")
+    _check(weight_kc, "weight_kc")
+    _check(bias, "bias")
+    cbs = _plane_bs(coords_x, "coords_x")
+    B, _, H, W1 = coords_x.shape
+    if sh_a.shape != (B * H, int(N.lib().sa_shear_slice_size(W1, W2, num_levels))):
+        raise RuntimeError(f"sheared pyramid {tuple(sh_a.shape)} does not match coords {tuple(coords_x.shape)}")
+    nvol = 2 if sh_b is not None else 1
+    Cout = weight_kc.shape[1]
+    if out is None:
+        out = torch.empty((B * nvol, Cout, H, W1), device=sh_a.device, dtype=torch.float32)
+    _check(out, "out")
+    N.call("sa_corr_lookup_conv1x1_sheared", sh_a.data_ptr(), _ptr(sh_b), W2, num_levels, radius,
+           coords_x.data_ptr(), cbs, B, H, W1, weight_kc.data_ptr(), bias.data_ptr(), Cout, out.data_ptr(),
+           _stream(sh_a))
+    return out
+
+
 # ----------------------------------------------------------------------- a2 + a3
 def mono_normals(mde_lowres: torch.Tensor, gain: float) -> torch.Tensor:
     _check(mde_lowres, "mde_lowres")
@@ -329,23 +368,39 @@ def gru_out(xc, qh, cq, z, h, bx: Optional[torch.Tensor] = None, qh2: Optional[t
     _account("gru_out", 4.0 * (6 + (qh2 is not None)) * B * C * H * W)
 
 
-def pool2x(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-    B, C, H, W = x.shape
+def _pitched_bs(t: torch.Tensor, name: str) -> int:
+    """Batch stride of a [B, C, H, P] (possibly channel-sliced) view of dense [H, P] planes."""
+    _check(t, name, contiguous=False)
+    B, C, H, P = t.shape
+    if t.stride(3) != 1 or t.stride(2) != P or (C > 1 and t.stride(1) != H * P):
+        raise RuntimeError(f"{name}: inner [C,H,P] block must be dense (strides {t.stride()})")
+    return t.stride(0)
+
+
+def pool2x(x: torch.Tensor, out: torch.Tensor, width: Optional[int] = None,
+           out_width: Optional[int] = None) -> torch.Tensor:
+    """avg_pool2d(3, 2, 1) of x [B,C,H,W] into out [B,C,Ho,Wo]; width / out_width: the image
+    widths of pitched planes (the last dimension is then the row pitch; pad columns untouched)."""
+    B, C, H, Px = x.shape
+    W = width or Px
     Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
-    if tuple(out.shape) != (B, C, Ho, Wo):
-        raise RuntimeError(f"pool2x: out {tuple(out.shape)} != {(B, C, Ho, Wo)}")
-    N.call("sa_pool2x", x.data_ptr(), _plane_bs(x, "x"), B, C, H, W, out.data_ptr(), _plane_bs(out, "out"),
-           _stream(x))
+    Po = out.shape[3]
+    if (out_width or Po) != Wo or tuple(out.shape[:3]) != (B, C, Ho):
+        raise RuntimeError(f"pool2x: out {tuple(out.shape)} (width {out_width}) != {(B, C, Ho, Wo)}")
+    N.call("sa_pool2x_p", x.data_ptr(), _pitched_bs(x, "x"), Px, B, C, H, W, out.data_ptr(),
+           _pitched_bs(out, "out"), Po, _stream(x))
     return out
 
 
-def interp(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-    B, C, H, W = x.shape
-    Bo, Co, Ho, Wo = out.shape
+def interp(x: torch.Tensor, out: torch.Tensor, width: Optional[int] = None,
+           out_width: Optional[int] = None) -> torch.Tensor:
+    """Bilinear align_corners resize of x into out's size; width / out_width as in pool2x."""
+    B, C, H, Px = x.shape
+    Bo, Co, Ho, Po = out.shape
     if (Bo, Co) != (B, C):
         raise RuntimeError("interp: batch/channels mismatch")
-    N.call("sa_interp_bilinear_ac", x.data_ptr(), _plane_bs(x, "x"), B, C, H, W, Ho, Wo, out.data_ptr(),
-           _plane_bs(out, "out"), _stream(x))
+    N.call("sa_interp_bilinear_ac_p", x.data_ptr(), _pitched_bs(x, "x"), Px, B, C, H, width or Px, Ho,
+           out_width or Po, out.data_ptr(), _pitched_bs(out, "out"), Po, _stream(x))
     return out
 
 
@@ -614,6 +669,10 @@ _WINO4 = True
 # F(4x4) launches on the wide block shape (64 output channels per block, one wave per SIMD)
 # where every problem allows it (Cout % 64; Cout % 128 with a z/r gate)
 W4_WIDE = False
+# F(4x4) launches of the default (8-wave) shape on its persistent kernel (block_shape 5): one block
+# per CU walking the launch's work items, each prefetching the next item's first chunk under its
+# own epilogue
+W4_PERSIST = False
 # F(4x4) launches on the quadrant block shape (block_shape 4: 32 tiles x 64 output channels,
 # two waves per SIMD, each wave one quadrant of the 6 x 6 points) where every problem allows it
 W4_QUAD = False
@@ -640,10 +699,13 @@ def wino_weights(weight: torch.Tensor) -> WinoFilters:
 _WINO4_AFF_CIN = 256
 
 
-def _wino4_ok(x: torch.Tensor, in_aff=None, in_act=None, out: Optional[torch.Tensor] = None, **_) -> bool:
-    """F(4x4,3x3) kernel preconditions: W % 4 == 0, 16-byte aligned planes; an input transform
-    (the producer's norm, ReLU or none) for Cin <= _WINO4_AFF_CIN."""
-    if (in_aff is not None or in_act is not None) and (x.shape[1] > _WINO4_AFF_CIN or ACT[in_act] > 1):
+def _wino4_ok(x: torch.Tensor, in_aff=None, in_act=None, out: Optional[torch.Tensor] = None,
+              width: Optional[int] = None, **_) -> bool:
+    """F(4x4,3x3) kernel preconditions: W % 4 == 0 (the pitch of pitched planes), 16-byte aligned
+    planes; an input transform (the producer's norm, ReLU or none) for Cin <= _WINO4_AFF_CIN and
+    not on pitched planes (it would turn their zero pad columns into t)."""
+    if (in_aff is not None or in_act is not None) and (x.shape[1] > _WINO4_AFF_CIN or ACT[in_act] > 1
+                                                      or (width is not None and width != x.shape[3])):
         return False
     return (x.shape[3] % 4 == 0 and x.data_ptr() % 16 == 0
             and x.stride(0) % 4 == 0 and (out is None or (out.data_ptr() % 16 == 0 and out.stride(0) % 4 == 0)))
@@ -666,18 +728,27 @@ _WINO4_MIN_BLOCKS = 384
 
 def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] = None, relu: bool = False,
                   out: Optional[torch.Tensor] = None, in_aff: Optional[Affine] = None, in_act=None,
-                  stats: bool = False, f4: bool = False, out_cout: Optional[int] = None, wide: bool = False):
-    """out_cout: channels of ``out`` when the epilogue writes fewer than Cout there (gate mode 1)."""
+                  stats: bool = False, f4: bool = False, out_cout: Optional[int] = None, wide: bool = False,
+                  width: Optional[int] = None):
+    """out_cout: channels of ``out`` when the epilogue writes fewer than Cout there (gate mode 1).
+    width: the image width when x (and out, and the gate planes) are PITCHED planes [.., H, P]
+    whose columns width .. P - 1 are zero (F(4x4) only; the outputs' pad columns stay zero)."""
     bs = _plane_bs(x, "x")
     if not isinstance(U, WinoFilters):
         raise RuntimeError("conv2d_k3: U must come from ops.wino_weights")
-    B, Cin, H, W = x.shape
+    B, Cin, H, P = x.shape
+    W = P if width is None else width
+    if not 0 < W <= P:
+        raise RuntimeError(f"conv2d_k3: width {W} outside the plane pitch {P}")
+    if W != P and not f4:
+        raise RuntimeError("conv2d_k3: pitched planes need the F(4x4,3x3) kernel")
     Cout = U.cout
     if U.cin != Cin:
         raise RuntimeError(f"conv2d_k3: U has {U.cin} input channels, x has {Cin}")
     if out is None:
-        out = torch.empty((B, out_cout or Cout, H, W), device=x.device, dtype=torch.float32)
-    if tuple(out.shape) != (B, out_cout or Cout, H, W):
+        alloc = torch.zeros if W != P else torch.empty
+        out = alloc((B, out_cout or Cout, H, P), device=x.device, dtype=torch.float32)
+    if tuple(out.shape) != (B, out_cout or Cout, H, P):
         raise RuntimeError("conv2d_k3: out shape mismatch")
     m, s, t, ps = (in_aff or Affine()).args(Cin)
     parts_fn = N.lib().sa_conv2d_k3_wino4_stat_parts if f4 else N.lib().sa_conv2d_k3_wino_stat_parts
@@ -686,11 +757,11 @@ def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] 
     Uf = (U.u4w if wide else U.u4) if f4 else U.u2
     prob = N.SaWinoProblem(x.data_ptr(), bs, B, Cin, H, W, Uf.data_ptr(), Cout, _ptr(bias),
                            1 if relu else 0, m, s, t, ps, ACT[in_act], out.data_ptr(), _plane_bs(out, "out"),
-                           _ptr(partial))
+                           _ptr(partial), P if P != W else 0)
     # Winograd-domain products actually executed: 36 per 4x4 tile (F4) or 16 per 2x2 tile (F2)
     # per (Cin, Cout) pair
     if f4:
-        _account("conv2d_wino4", 2.0 * 36 * Cin * Cout * B * ((H + 3) // 4) * ((W + 3) // 4))
+        _account("conv2d_wino4", 2.0 * 36 * Cin * Cout * B * ((H + 3) // 4) * ((W + 3) // 4))   # logical W
     else:
         _account("conv2d_wino", 2.0 * 16 * Cin * Cout * B * ((H + 1) // 2) * ((W + 1) // 2))
     fin = (lambda: (out, instnorm_finalize(partial, B * Cout, parts, H * W))) if stats else (lambda: out)
@@ -712,7 +783,7 @@ def _gate_epilogue(p: dict) -> "N.SaGateEpilogue":
     (1 - z) h + z tanh(add + conv + ctx) for convq's r*h part (out may be h itself)."""
     g = p["gate"]
     mode = g["mode"]
-    B, _, H, W = p["x"].shape
+    B, _, H, W = p["x"].shape   # (the plane pitch for pitched problems: every gate plane shares it)
     Cout = p["U"].cout
     Ch = Cout // 2 if mode == 1 else Cout
     ctx, h = g["ctx"], g["h"]
@@ -778,11 +849,13 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
             and all(p["U"].cout % 128 == 0 for p in problems if p.get("gate") and p["gate"]["mode"] == 1))
     built = [_wino_problem(**p, f4=f4, wide=wide) for p in plain]
     arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
-    if f4 and (gated or small_blocks or wide):
+    persist = f4 and W4_PERSIST and not (small_blocks or wide)
+    if f4 and (gated or small_blocks or wide or persist):
         gates = (N.SaGateEpilogue * len(built))(*[_gate_epilogue(p) if p.get("gate") else N.SaGateEpilogue()
                                                   for p in problems])
+        shape = (4 if W4_QUAD else 3) if wide else 2 if small_blocks else 5 if persist else 0
         N.call("sa_conv2d_k3_wino4_multi_gate", len(built), ctypes.addressof(arr), ctypes.addressof(gates),
-               (4 if W4_QUAD else 3) if wide else 2 if small_blocks else 0, _stream(problems[0]["x"]))
+               shape, _stream(problems[0]["x"]))
     else:
         N.call("sa_conv2d_k3_wino4_multi" if f4 else "sa_conv2d_k3_wino_multi", len(built), ctypes.addressof(arr),
                _stream(problems[0]["x"]))

@@ -7,7 +7,7 @@ import torch
 
 from fixtures_util import load_fixture
 from oracle import ops_ref as R
-from stereoanywhere_amd import ops
+from stereoanywhere_amd import _native as N, ops
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
@@ -157,6 +157,45 @@ def test_lookup_fused_taps_bit_exact():
         assert np.all(fused[v::2, 36:] == 0)
 
 
+@pytest.mark.parametrize("W1,W2", [(96, 96), (70, 70), (240, 240), (37, 45)])
+def test_lookup_sheared_bit_exact(W1, W2):
+    """The lookup + convc1 on the disparity-sheared pyramid copies (corr_shear.hip) equals the
+    row-layout kernel bit for bit (the same taps and arithmetic; only the layout differs):
+    general convc1 weights, coordinates on and a rounding step off integers, negative and past
+    the width, odd level widths, W1 != W2."""
+    rng = np.random.default_rng(W1 * 7 + W2)
+    B, H = 2, 5
+    va = rng.standard_normal((B, H, W1, W2)).astype(np.float32)
+    vb = rng.standard_normal((B, H, W1, W2)).astype(np.float32)
+    n = B * H * W1
+    base = np.concatenate([np.arange(-6, W2 + 6, dtype=np.float32),
+                           np.nextafter(np.arange(0, 40, dtype=np.float32), np.float32(-1)),
+                           np.nextafter(np.arange(0, 40, dtype=np.float32), np.float32(100)),
+                           (rng.random(n) * (W2 + 30) - 15).astype(np.float32)])
+    cx = base[:n].reshape(B, 1, H, W1).copy()
+    rng.shuffle(cx.reshape(-1))
+    wt = (rng.standard_normal((36, 64)) / 6).astype(np.float32)
+    bias = rng.standard_normal(64).astype(np.float32)
+    pa, pb = ops.pyramid_from_volume(g(va)), ops.pyramid_from_volume(g(vb))
+    row = c(ops.corr_lookup_conv1x1(pa, pb, W2, 4, 4, g(cx), g(wt), g(bias)))
+    sa, sb = ops.corr_pyramid_shear(pa, B, H, W1, W2), ops.corr_pyramid_shear(pb, B, H, W1, W2)
+    sh = c(ops.corr_lookup_conv1x1_sheared(sa, sb, W2, 4, 4, g(cx), g(wt), g(bias)))
+    np.testing.assert_array_equal(sh, row)
+    # the sheared copy holds every level cell once, zeros elsewhere
+    _, offs, wids = ops.pyramid_geometry(W2, 4)
+    sa_h = c(sa)
+    for l in range(4):
+        o = int(N.lib().sa_shear_level_offset(W1, W2, 4, l))
+        E = wids[l] + ((W1 - 1) >> l)
+        lvl = sa_h[:, o:o + E * W1].reshape(B * H, E, W1)
+        ref = c(pa)[:, offs[l]:offs[l] + wids[l]].reshape(B * H, W1, wids[l])
+        j = np.arange(W1)
+        for k in (0, wids[l] - 1, wids[l] // 2):
+            e = (j >> l) - k + wids[l] - 1
+            np.testing.assert_array_equal(lvl[:, e, j], ref[:, j, k])
+        assert np.count_nonzero(lvl) <= np.count_nonzero(ref)
+
+
 def test_hip_corr_block_contract(micro):
     from stereoanywhere_amd.corr import HipCorrBlock1D
     blk = HipCorrBlock1D(g(micro["corr.out"]), num_levels=4, radius=4)
@@ -200,12 +239,45 @@ def test_softargmin_confidence(micro, layout):
     np.testing.assert_allclose(cf[:, 1:2], micro["conf.right"], atol=2e-6)
 
 
-@pytest.mark.parametrize("n", [64, 240, 250, 300])
-@pytest.mark.parametrize("layout", ["reference", "native"])
+@pytest.mark.parametrize("n", [64, 168, 240, 250, 280, 300])
+@pytest.mark.parametrize("layout", ["reference", "native", "native-lines"])
 def test_softargmin_confidence_lines(n, layout):
-    """Register-resident kernels (line length <= 256: float4 rows, ragged rows, strided
-    columns split over 4 waves) and the generic ones (n = 300), on two different volumes
-    that are channel views of one tensor, as the model passes them."""
+    """The native layout (j contiguous, square) takes the one-pass slice kernel up to n = 288
+    (the booster tile's 280 included); "native-lines" forces the per-line kernels on it.  The
+    reference layout runs the register-resident line kernels (line length <= 256: float4 rows,
+    ragged rows, strided columns split over 4 waves) and the generic ones (n = 300).  Two
+    different volumes that are channel views of one tensor, as the model passes them."""
+    N.lib().sa_softargmin_set_one_pass(0 if layout == "native-lines" else 1)
+    try:
+        _softargmin_lines(n, layout.split("-")[0])
+    finally:
+        N.lib().sa_softargmin_set_one_pass(1)
+
+
+def test_softargmin_one_pass_single_volume():
+    """A call with only the disparity or only the confidence volume on the one-pass kernel
+    equals the same call on the per-line kernels (and the two-volume call)."""
+    rng = np.random.default_rng(5)
+    B, H, n = 2, 5, 240
+    vols = (rng.standard_normal((B, 2, n, H, n)) * 4).astype(np.float32)   # [B,2,W2,H,W1]
+    t = g(vols)
+    strides = (2 * n * H * n, n, 1, H * n)
+    res = {}
+    for on in (1, 0):
+        N.lib().sa_softargmin_set_one_pass(on)
+        try:
+            d, _ = ops.softargmin_conf(t[:, 0], None, strides, (B, H, n, n))
+            _, cf = ops.softargmin_conf(None, t[:, 1], strides, (B, H, n, n))
+            d2, cf2 = ops.softargmin_conf(t[:, 0], t[:, 1], strides, (B, H, n, n))
+        finally:
+            N.lib().sa_softargmin_set_one_pass(1)
+        assert torch.equal(d, d2) and torch.equal(cf, cf2)
+        res[on] = (c(d), c(cf))
+    np.testing.assert_allclose(res[1][0], res[0][0], atol=5e-4)
+    np.testing.assert_allclose(res[1][1], res[0][1], atol=2e-6)
+
+
+def _softargmin_lines(n, layout):
     rng = np.random.default_rng(n)
     B, H = 2, 3
     vols = (rng.standard_normal((B, 2, H, n, n)) * 4).astype(np.float32)  # [B,2,H,W1,W2]
@@ -490,5 +562,12 @@ def test_conv3d_wd_matches_direct(cin, cout, gated, shape):
     a = ops.conv3d_wd(v, ops.conv3d_wd_weights(w), cout, slope=0.01)
     b = ops.conv3d(v, w, cout, slope=0.01)
     torch.testing.assert_close(a.raw, b.raw, atol=2e-5, rtol=1e-5)
+    # the LDS-weight variant computes the same products in the same order
+    N.lib().sa_conv3d_wd_set_variant(1)
+    try:
+        a1 = ops.conv3d_wd(v, ops.conv3d_wd_weights(w), cout, slope=0.01)
+    finally:
+        N.lib().sa_conv3d_wd_set_variant(0)
+    assert torch.equal(a1.raw, a.raw)
     torch.testing.assert_close(a.norm[0], b.norm[0], atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(a.norm[1], b.norm[1], atol=1e-5, rtol=1e-5)

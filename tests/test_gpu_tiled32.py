@@ -3,8 +3,8 @@ run_test_contextaware_mapreduce.py:69) against the REFERENCE model / TileWrapper
 (tests/golden/make_golden.py tiled32_cases, seeded weights):
 
 * one middlebury-preset tile, 1024x672 (GRU widths 168 / 84 / 42: the 1/16 level has
-  W % 4 != 0, so its gates run in the separate kernels while the other levels keep the
-  fused F(4x4) epilogues);
+  W % 4 != 0, so its planes are padded to 44 columns and it runs on F(4x4) with the gates in
+  the epilogue, ScheduleOptions.pad_ragged);
 * one booster-preset tile, 896x1120 (280 / 140 / 70);
 * config 3's whole padded image (1024x1408) through the tiler: 6 tiles, 3 unique rectangles,
   each run once and accumulated twice;
@@ -48,8 +48,7 @@ def _inputs(fix, prefix, H, W, D, seed):
 def test_tile_32_iterations_vs_reference(model, fix, name):
     H, W, seed = (int(v) for v in fix[f"{name}.geom"])
     x = _inputs(fix, name, H, W, float(fix[f"{name}.D"]), seed)
-    # the 1/16 GRU level is ragged (W/16 = 42 or 70): the per-level schedule must keep the
-    # other two levels on the fused path
+    # the 1/16 GRU level is ragged (W/16 = 42 or 70): padded planes on F(4x4)
     assert (W // 16) % 4 != 0 and (W // 4) % 4 == 0 and (W // 8) % 4 == 0
     with torch.no_grad():
         d = -model(*x, iters=32, test_mode=True)[0]
@@ -60,18 +59,20 @@ def test_tile_32_iterations_vs_reference(model, fix, name):
     assert e < 1e-3
 
 
-def test_tile_32_iterations_fallback_schedule(model, fix):
+@pytest.mark.parametrize("option", ["fuse_gates", "pad_ragged"])
+def test_tile_32_iterations_fallback_schedule(model, fix, option):
     """The same booster tile with the gates kept out of the conv epilogues at every level
-    (ScheduleOptions.fuse_gates = False): the separate gate kernels agree."""
+    (ScheduleOptions.fuse_gates = False), or only at the ragged 1/16 level (pad_ragged = False:
+    F(2x2) and the separate gate kernels there, split out of the shared launches)."""
     H, W, seed = (int(v) for v in fix["booster_tile.geom"])
     x = _inputs(fix, "booster_tile", H, W, 512.0, seed)
-    saved = model.opts.fuse_gates
-    model.opts.fuse_gates = False
+    saved = getattr(model.opts, option)
+    setattr(model.opts, option, False)
     try:
         with torch.no_grad():
             d = -model(*x, iters=32, test_mode=True)[0]
     finally:
-        model.opts.fuse_gates = saved
+        setattr(model.opts, option, saved)
     got = d[0, 0, ::int(fix["row_step"])].cpu().numpy()
     e = epe(got, fix["booster_tile.out"])
     print("booster tile (unfused gates) EPE", e)

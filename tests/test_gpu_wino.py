@@ -215,15 +215,17 @@ def test_wino4_multi_stats_views(monkeypatch):
     torch.testing.assert_close(ye, F.conv2d(xe, wb, padding=1), atol=2e-5, rtol=1e-4)
 
 
-@pytest.mark.parametrize("wide", [False, True, "quad"])
+@pytest.mark.parametrize("wide", [False, True, "quad", "persist"])
 def test_wino4_gru_gate_epilogues(monkeypatch, wide):
     """ConvGRU gates in the F(4x4) epilogue (update.py:16-27) against the reference's expressions
     in torch fp32: mode 1 (convz | convr over cat(h, x) -> z, r*h) on channel views of one
     [h | x | r*h] buffer, beside a plain problem in the same launch; mode 2 (convq's r*h part ->
     the new state, in place on h).  Two levels' shapes (8 x 128 and 16 x 64 blocks)."""
-    # also on the wide and the quadrant block shapes (64 channels per block)
+    # also on the wide and the quadrant block shapes (64 channels per block) and on the
+    # persistent kernel (two 16-channel epilogue passes)
     monkeypatch.setattr(ops, "W4_WIDE", wide is True)
     monkeypatch.setattr(ops, "W4_QUAD", wide == "quad")
+    monkeypatch.setattr(ops, "W4_PERSIST", wide == "persist")
     g = torch.Generator(device="cpu").manual_seed(42)
 
     def r(*s):
@@ -313,3 +315,143 @@ def test_wino4_wide_block_shape(monkeypatch, N, Cin, Cout, H, W, shape):
     torch.testing.assert_close(mean, ref.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(rstd, torch.rsqrt(ref.var(dim=(2, 3), unbiased=False) + 1e-5).flatten(),
                                atol=1e-4, rtol=1e-4)
+
+
+def test_wino4_persistent_equals_one_shot(monkeypatch):
+    """The persistent F(4x4) kernel (block_shape 5: one block per CU walking the work items, the
+    next item's first chunk prefetched under the epilogue, outputs staged in two 16-channel
+    passes) computes the one-shot kernel's outputs bit for bit: a multi-problem launch mixing
+    both tile geometries and input-channel counts (so consecutive items of a block change
+    problem, geometry and buffer parity), bias + ReLU, channel-slice views, InstanceNorm
+    statistics, and an input-transform launch; more items than blocks."""
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    g = torch.Generator(device="cpu").manual_seed(77)
+
+    def r(*s):
+        return torch.randn(*s, generator=g).cuda()
+    xa, xb, xc = r(4, 136, 136, 240), r(4, 64, 68, 120), r(3, 200, 34, 60)
+    wa, wb, wc = r(64, 128, 3, 3) / 34, r(96, 64, 3, 3) / 24, r(128, 200, 3, 3) / 42
+    ba = r(64)
+    probs = lambda: [dict(x=xa[:, 8:], U=ops.wino_weights(wa), bias=ba, relu=True),   # noqa: E731
+                     dict(x=xb, U=ops.wino_weights(wb), stats=True),
+                     dict(x=xc, U=ops.wino_weights(wc), bias=r(128) * 0)]
+    outs = {}
+    for persist in (False, True):
+        monkeypatch.setattr(ops, "W4_PERSIST", persist)
+        outs[persist] = ops.conv2d_k3_multi(*probs())
+    (a0, b0, c0), (a1, b1, c1) = outs[False], outs[True]
+    assert torch.equal(a0, a1) and torch.equal(c0, c1) and torch.equal(b0[0], b1[0])
+    torch.testing.assert_close(b0[1][0], b1[1][0], atol=1e-6, rtol=1e-6)   # IN mean / rstd
+    torch.testing.assert_close(b0[1][1], b1[1][1], atol=1e-6, rtol=1e-6)
+    torch.testing.assert_close(a1, torch.relu(F.conv2d(xa[:, 8:], wa, ba, padding=1)), atol=1e-4, rtol=1e-4)
+    # input transform (producer InstanceNorm + ReLU applied on load), per-plane parameters
+    x = r(8, 64, 136, 240)
+    w = r(64, 64, 3, 3) / 24
+    m, s_ = r(8 * 64) * 0.1, r(8 * 64).abs() + 0.5
+    res = {}
+    for persist in (False, True):
+        monkeypatch.setattr(ops, "W4_PERSIST", persist)
+        res[persist] = ops.conv2d_k3(x, ops.wino_weights(w), in_aff=ops.Affine(m, s_, None, per_plane=True),
+                                     in_act="relu")
+    assert torch.equal(res[False], res[True])
+    xn = torch.relu((x - m.view(8, 64, 1, 1)) * s_.view(8, 64, 1, 1))
+    torch.testing.assert_close(res[True], F.conv2d(xn, w, padding=1), atol=1e-4, rtol=1e-4)
+
+
+def _pitched(x, P):
+    """x [B, C, H, W] -> [B, C, H, P] with zero columns W .. P - 1."""
+    out = torch.zeros(*x.shape[:3], P, device=x.device)
+    out[..., :x.shape[3]] = x
+    return out
+
+
+@pytest.mark.parametrize("persist", [False, True])
+def test_wino4_pitched_planes(monkeypatch, persist):
+    """F(4x4) on pitched planes (SaWinoProblem.pitch: widths 70 and 42 padded to 72 and 44, the
+    booster / middlebury tiles' 1/16 GRU level): the convolution of the first W columns, the pad
+    columns of the outputs left zero, InstanceNorm statistics over the W columns only, beside a
+    dense problem in the same launch."""
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    monkeypatch.setattr(ops, "W4_PERSIST", persist)
+    g = torch.Generator(device="cpu").manual_seed(91)
+
+    def r(*s):
+        return torch.randn(*s, generator=g).cuda()
+    for B, Cin, Cout, H, W in ((3, 256, 256, 56, 70), (2, 128, 128, 64, 42)):
+        P = (W + 3) // 4 * 4
+        x = r(B, Cin, H, W)
+        w = r(Cout, Cin, 3, 3) / (3 * Cin ** 0.5)
+        b = r(Cout)
+        xd, wd = r(2, 64, 40, 96), r(64, 64, 3, 3) / 24
+        (ya, (yb, (mean, rstd))), work = _run(monkeypatch, True,
+                                              dict(x=_pitched(x, P), U=ops.wino_weights(w), bias=b, relu=True,
+                                                   width=W),
+                                              dict(x=xd, U=ops.wino_weights(wd), stats=True))
+        assert "conv2d_wino" not in work
+        assert ya.shape == (B, Cout, H, P)
+        assert float(ya[..., W:].abs().max()) == 0.0
+        torch.testing.assert_close(ya[..., :W], torch.relu(F.conv2d(x, w, b, padding=1)), atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(yb, F.conv2d(xd, wd, padding=1), atol=1e-4, rtol=1e-4)
+        # statistics of a pitched problem: only the W real columns
+        ((yc, (mc, rc)),), _ = _run(monkeypatch, True, dict(x=_pitched(x, P), U=ops.wino_weights(w), stats=True,
+                                                            width=W))
+        ref = F.conv2d(x, w, padding=1)
+        torch.testing.assert_close(mc, ref.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(rc, torch.rsqrt(ref.var(dim=(2, 3), unbiased=False) + 1e-5).flatten(),
+                                   atol=1e-4, rtol=1e-4)
+
+
+def test_wino4_pitched_gate_epilogues(monkeypatch):
+    """The ConvGRU gate epilogues (modes 1 and 2) on a pitched level (W = 70 in rows of 72): the
+    gate values of the W columns as in test_wino4_gru_gate_epilogues, the pad columns of z, r*h
+    and the new state kept zero."""
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    g = torch.Generator(device="cpu").manual_seed(93)
+
+    def r(*s):
+        return torch.randn(*s, generator=g).cuda()
+    B, hd, xd, H, W = 2, 128, 128, 56, 70
+    P = 72
+    hxr = torch.zeros(B, 2 * hd + xd, H, P, device=dev)
+    hxr[..., :W] = r(B, 2 * hd + xd, H, W)
+    hxr[:, hd + xd:] = 0.0
+    h, x, rh_out = hxr[:, :hd], hxr[:, hd:hd + xd], hxr[:, hd + xd:]
+    ctx = _pitched(r(B, 3 * hd, H, W), P)
+    wz, wr, wq = (r(hd, hd + xd, 3, 3) / (3 * (hd + xd) ** 0.5) for _ in range(3))
+    bz, br, bq = r(hd), r(hd), r(hd)
+    z = torch.zeros(B, hd, H, P, device=dev)
+    qx = torch.zeros(B, hd, H, P, device=dev)
+    _run(monkeypatch, True,
+         dict(x=hxr[:, :hd + xd], U=ops.wino_weights(torch.cat([wz, wr]).contiguous()), bias=torch.cat([bz, br]),
+              out=z, width=W, gate=dict(mode=1, ctx=ctx, h=h, out2=rh_out)),
+         dict(x=x, U=ops.wino_weights(wq[:, hd:].contiguous()), out=qx, width=W))
+    hx = torch.cat([h, x], 1)[..., :W]
+    z_ref = torch.sigmoid(F.conv2d(hx, wz, bz, padding=1) + ctx[:, :hd, :, :W])
+    r_ref = torch.sigmoid(F.conv2d(hx, wr, br, padding=1) + ctx[:, hd:2 * hd, :, :W])
+    torch.testing.assert_close(z[..., :W], z_ref, atol=3e-5, rtol=1e-4)
+    torch.testing.assert_close(rh_out[..., :W], r_ref * h[..., :W], atol=3e-5, rtol=1e-4)
+    assert float(z[..., W:].abs().max()) == 0 and float(rh_out[..., W:].abs().max()) == 0
+    assert float(qx[..., W:].abs().max()) == 0
+    h0 = h[..., :W].clone()
+    q_ref = torch.tanh(F.conv2d(torch.cat([rh_out, x], 1)[..., :W], wq, bq, padding=1) + ctx[:, 2 * hd:, :, :W])
+    h_ref = (1 - z[..., :W]) * h0 + z[..., :W] * q_ref
+    _run(monkeypatch, True, dict(x=rh_out, U=ops.wino_weights(wq[:, :hd].contiguous()), bias=bq, out=h, width=W,
+                                 gate=dict(mode=2, ctx=ctx[:, 2 * hd:], h=h, z=z, add=qx)))
+    torch.testing.assert_close(h[..., :W], h_ref, atol=1e-4, rtol=1e-4)
+    assert float(h[..., W:].abs().max()) == 0
+
+
+def test_pool_interp_pitched():
+    """pool2x / interp between pitched and dense planes equal the dense computation."""
+    g = torch.Generator(device="cpu").manual_seed(94)
+    a = torch.randn(2, 16, 112, 140, generator=g).cuda()
+    Wo = (140 - 1) // 2 + 1   # 70
+    dense = ops.pool2x(a, torch.empty(2, 16, 56, Wo, device=dev))
+    pitched = torch.zeros(2, 16, 56, 72, device=dev)
+    ops.pool2x(a, pitched, out_width=Wo)
+    assert torch.equal(pitched[..., :Wo], dense) and float(pitched[..., Wo:].abs().max()) == 0
+    up_d = ops.interp(dense, torch.empty(2, 16, 112, 140, device=dev))
+    up_p = ops.interp(pitched, torch.empty(2, 16, 112, 140, device=dev), width=Wo)
+    assert torch.equal(up_d, up_p)
+    torch.testing.assert_close(up_d, F.interpolate(dense, size=(112, 140), mode="bilinear", align_corners=True),
+                               atol=1e-5, rtol=1e-5)
