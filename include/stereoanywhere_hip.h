@@ -204,6 +204,10 @@ int sa_corr_lookup_conv1x1(const float *pyramid_a, const float *pyramid_b, int W
  *   sa_corr_pyramid_shear: the row-layout pyramid [B*H*W1][row_stride] -> sheared [B*H][slice]
  *   sa_corr_lookup_conv1x1_sheared: sa_corr_lookup_conv1x1 on sheared pyramids (same taps,
  *     same arithmetic; 4 levels, radius 4, Cout 64). */
+/* convc1 of the fused lookups (both layouts) on the VALU (0, default) or fp32 MFMA (1, measured
+ * slower): the same k-ordered fmaf chain either way.  For A/B runs and tests. */
+void sa_lookup_set_mfma(int on);
+int sa_lookup_get_mfma(void);
 long sa_shear_slice_size(int W1, int W2, int num_levels);
 long sa_shear_level_offset(int W1, int W2, int num_levels, int level);
 int sa_corr_pyramid_shear(const float *pyramid, long row_stride, int B, int H, int W1, int W2,

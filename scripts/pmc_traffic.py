@@ -17,7 +17,8 @@ FAMILIES = {
     "vol_apply_kernel": "conv3d_fused", "lookup_kernel": "corr_lookup", "lookup_c1_kernel": "corr_lookup", "lookup_c1_vec_kernel": "corr_lookup",
     "corr_pyramid_kernel": "corr_volume_pyramid", "corr_pyramid_v2_kernel": "corr_volume_pyramid", "masked_volume_kernel": "mono_masked_volume",
     "sam_contig_kernel": "softargmin_conf", "sam_strided_kernel": "softargmin_conf", "sam_row_kernel": "softargmin_conf",
-    "sam_col_kernel": "softargmin_conf", "lsq_kernel": "weighted_lsq", "lsq_hist_kernel": "weighted_lsq",
+    "sam_col_kernel": "softargmin_conf", "sam_slice_kernel": "softargmin_conf",
+    "lookup_c1_shear_kernel": "corr_lookup", "shear_kernel": "corr_lookup", "wino_f4k3_persist_kernel": "conv2d_wino4", "lsq_kernel": "weighted_lsq", "lsq_hist_kernel": "weighted_lsq",
     "lsq_solve_kernel": "weighted_lsq",
     "gru_zr_kernel": "gru_zr", "gru_out_kernel": "gru_out", "convex_up_kernel": "convex_upsample",
     "wino_f2k3_kernel": "conv2d_wino", "wino_f4k3_kernel": "conv2d_wino4", "conv_direct_kernel": "conv2d_direct", "norm_act_kernel": "norm_act", "plane_stats_kernel": "norm_act",

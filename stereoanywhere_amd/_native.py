@@ -46,6 +46,8 @@ SIGNATURES = {
     "sa_corr_pyramid_from_volume_strided": (I, [P, I, I, I, I, L, L, L, I, P, L, P]),
     "sa_corr_lookup": (I, [P, P, I, L, I, I, P, L, I, I, I, P, L, P]),
     "sa_corr_lookup_conv1x1": (I, [P, P, I, L, I, I, P, L, I, I, I, P, P, I, P, P]),
+    "sa_lookup_set_mfma": (None, [I]),
+    "sa_lookup_get_mfma": (I, []),
     "sa_shear_slice_size": (L, [I, I, I]),
     "sa_shear_level_offset": (L, [I, I, I, I]),
     "sa_corr_pyramid_shear": (I, [P, L, I, I, I, I, I, P, P]),

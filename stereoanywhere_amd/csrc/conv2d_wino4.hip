@@ -1109,7 +1109,11 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
   sa::TimingScope ts(SA_K_CONV2D_W4, s);
   if (persist) {
     // one block per CU (rounded down to a multiple of 8: every block keeps its items on one XCD)
-    const unsigned grid = (unsigned)std::min<long>(total, std::max(8, w4_num_cus() / 8 * 8));
+#ifndef SA_W4_PGRID
+#define SA_W4_PGRID 1   // 0: one block per work item (timing diagnostic of the persistent code path)
+#endif
+    const unsigned grid = SA_W4_PGRID ? (unsigned)std::min<long>(total, std::max(8, w4_num_cus() / 8 * 8))
+                                      : (unsigned)total;
     aff     ? wino_f4k3_persist_kernel<W4Big, false, true><<<grid, W4Big::NTHR, 0, s>>>(L)
     : gated ? wino_f4k3_persist_kernel<W4Big, true><<<grid, W4Big::NTHR, 0, s>>>(L)
             : wino_f4k3_persist_kernel<W4Big, false><<<grid, W4Big::NTHR, 0, s>>>(L);

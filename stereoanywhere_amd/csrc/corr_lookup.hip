@@ -11,6 +11,7 @@
 //   ix = (xg + 1) * ((W_l - 1) / 2)          (ATen CPU grid_sample, align_corners=True)
 //   out = v[floor] * (1 - w) + v[floor + 1] * w, zero outside [0, W_l - 1].
 #include "sa_common.h"
+#include "convc1_mfma.h"
 
 namespace {
 
@@ -122,7 +123,8 @@ __global__ __launch_bounds__(256) void lookup_c1_kernel(const float *__restrict_
 // position lies within 1 of x_-R + t; its fp32 rounding is reproduced exactly per tap), the
 // alignment shift is undone with selects, and every tap picks its two cells with 3-way
 // selects.  Loads past the buffer return 0 (cells outside [0, W_l - 1] are zeroed anyway).
-template <int L, int R, int COUT>
+// MF: convc1 on fp32 MFMA (convc1_mfma.h; the same k-ordered fmaf chain as the VALU loop)
+template <int L, int R, int COUT, bool MF = false>
 __global__ __launch_bounds__(256) void lookup_c1_vec_kernel(const float *__restrict__ pa, const float *__restrict__ pb,
                                                             const float *__restrict__ cx, LGeo g, int npix,
                                                             int pyr_bytes, const float *__restrict__ wt,
@@ -130,8 +132,13 @@ __global__ __launch_bounds__(256) void lookup_c1_vec_kernel(const float *__restr
                                                             float *__restrict__ out) {
   constexpr int K = 2 * R + 1, NT = L * K, WIN = 2 * R + 4;   // cells x_-R - 1 .. x_-R + 2R + 2
   static_assert(WIN + 3 <= 16, "four float4s cover the window at any alignment");
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= npix) return;
+  static_assert(!MF || COUT == 64, "MFMA convc1: 64 outputs");
+  __shared__ float c1lds[MF ? 4 : 1][MF ? NT * sa::C1_PITCH : 1];
+  const int p0 = blockIdx.x * 256 + threadIdx.x;
+  if (!MF && p0 >= npix) return;
+  // (MFMA: every lane of the wave takes part; lanes past the end sample the last pixel and
+  // store nothing)
+  const int p = p0 < npix ? p0 : npix - 1;
   const int v = blockIdx.y;
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(v ? pb : pa), (short)0, pyr_bytes, 0x00020000);
@@ -194,6 +201,16 @@ __global__ __launch_bounds__(256) void lookup_c1_vec_kernel(const float *__restr
       f[l * K + t] = v0 * (1.0f - w) + v1 * w;
     }
   }
+  if constexpr (MF) {
+    const int lane = threadIdx.x & 63;
+    sa::C1Weights<NT> w;
+    sa::c1_load_weights<NT>(wt, bias, lane, w);
+    const int wp0 = p0 - lane;   // the wave's first pixel
+    sa::c1_mfma<NT>(f, w, c1lds[threadIdx.x >> 6], lane, [&](int q, int gq, const auto &r) {
+      sa::c1_store4(out, wp0 + 16 * q + 4 * (lane >> 4), 16 * gq + (lane & 15), hw, nvol, v, npix, r);
+    });
+    return;
+  }
   float *__restrict__ o = out + ((long)b * nvol + v) * COUT * hw + rem;
 #pragma unroll 4
   for (int c0 = 0; c0 < COUT; c0 += 8) {
@@ -211,6 +228,14 @@ __global__ __launch_bounds__(256) void lookup_c1_vec_kernel(const float *__restr
 }
 
 }  // namespace
+
+// convc1 of the fused lookups on the VALU (0, default) or on fp32 MFMA (1): the MFMA form measured
+// slower (scripts/bench_lookup.py: 64.9 vs 55.6 us at B = 4 x 136 x 240, 816 vs 707 us on the
+// sheared booster batch): the lookup is bound by its gathers, and the taps' LDS round trip and
+// the lower occupancy (3 instead of 4 waves per SIMD) cost more than the FMAs it removes
+static int sa_lookup_mfma = 0;
+extern "C" void sa_lookup_set_mfma(int on) { sa_lookup_mfma = on ? 1 : 0; }
+extern "C" int sa_lookup_get_mfma() { return sa_lookup_mfma; }
 
 extern "C" int sa_corr_lookup_conv1x1(const float *pyramid_a, const float *pyramid_b, int W2, long row_stride,
                                       int num_levels, int radius, const float *coords_x, long coords_bstride,
@@ -243,8 +268,12 @@ extern "C" int sa_corr_lookup_conv1x1(const float *pyramid_a, const float *pyram
   dim3 grid((unsigned)((npix + 255) / 256), nvol);
   const long pyr_bytes = npix * row_stride * 4;
   if (pyr_bytes < (1L << 31) - 64 && row_stride % 4 == 0 && (long)H * W1 < (1L << 30)) {
-    lookup_c1_vec_kernel<4, 4, 64><<<grid, 256, 0, s>>>(pyramid_a, pyramid_b ? pyramid_b : pyramid_a, coords_x, g,
-                                                        (int)npix, (int)pyr_bytes, weight_kc, bias, nvol, out);
+    if (sa_lookup_mfma)
+      lookup_c1_vec_kernel<4, 4, 64, true><<<grid, 256, 0, s>>>(pyramid_a, pyramid_b ? pyramid_b : pyramid_a, coords_x,
+                                                                g, (int)npix, (int)pyr_bytes, weight_kc, bias, nvol, out);
+    else
+      lookup_c1_vec_kernel<4, 4, 64><<<grid, 256, 0, s>>>(pyramid_a, pyramid_b ? pyramid_b : pyramid_a, coords_x, g,
+                                                          (int)npix, (int)pyr_bytes, weight_kc, bias, nvol, out);
     return sa::check_launch("sa_corr_lookup_conv1x1");
   }
   lookup_c1_kernel<4, 4, 64><<<grid, 256, 0, s>>>(pyramid_a, pyramid_b ? pyramid_b : pyramid_a, coords_x, g, npix,

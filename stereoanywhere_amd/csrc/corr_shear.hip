@@ -8,12 +8,14 @@
 // separate cache lines per level, and the lookup moved 2.3x the bytes it uses.  Level l of
 // image row (b, h) is sheared here into S_l[e][j] = C_l[j][(j >> l) - e + W_l - 1]:
 //   e in [0, E_l), E_l = W_l + ((W1 - 1) >> l)   (all (j, k) pairs of the level, k = (j >> l) -
-//   e + W_l - 1; cells with k outside [0, W_l) are stored as 0, the reference's zero padding)
+//   e + W_l - 1; the entries with k outside [0, W_l) are left unwritten: the lookup's tap test
+//   selects the reference's zero padding there without reading them into the result)
 // so pixel j's cell k sits at row e = (j >> l) - k + W_l - 1, column j.  Neighbouring pixels
 // at the same disparity read the same row e at neighbouring columns: one load instruction of
 // the wave is one or two row segments.  Storage ~2x the row layout; written once per forward
 // by sa_corr_pyramid_shear from the row-layout pyramid, read at every GRU iteration.
 #include "sa_common.h"
+#include "convc1_mfma.h"
 
 namespace {
 
@@ -41,28 +43,31 @@ ShGeo shear_geo(int W1, int W2, int L) {
   return g;
 }
 
-// one level, one (64 j x 64 e) tile of one slice: the source band (64 rows of <= 128 cells)
-// through LDS, written along j (coalesced)
+// one level of 32 consecutive pixel rows j of one slice: their W_l cells read once into LDS
+// (row-contiguous loads), then every row e of the level written along j (128-byte segments)
+constexpr int SH_J = 32;
 __global__ __launch_bounds__(256) void shear_kernel(const float *__restrict__ pyr, long rs, int W1, int off_l,
                                                     int Wl, int El, int lev, long slice_sz, long soff,
                                                     float *__restrict__ out) {
-  __shared__ float tile[64][129];
+  extern __shared__ float tile[];   // [SH_J][Wl + 1]
   const long slice = blockIdx.z;
-  const int j0 = blockIdx.x * 64, e0 = blockIdx.y * 64;
-  const int tid = threadIdx.x;
-  // k = (j >> lev) - e + Wl - 1 over the tile spans [kmin, kmin + 126]
-  const int kmin = (j0 >> lev) - (e0 + 63) + Wl - 1;
-  for (int i = tid; i < 64 * 128; i += 256) {
-    const int r = i >> 7, c = i & 127, j = j0 + r, k = kmin + c;
-    tile[r][c] = (j < W1 && k >= 0 && k < Wl) ? pyr[(slice * W1 + j) * rs + off_l + k] : 0.0f;
+  const int j0 = blockIdx.x * SH_J;
+  const int tid = threadIdx.x, pitch = Wl + 1;
+  const int nj = min(SH_J, W1 - j0);
+  for (int r = tid >> 6; r < nj; r += 4) {
+    const float *src = pyr + (slice * W1 + j0 + r) * rs + off_l;
+    for (int k = tid & 63; k < Wl; k += 64) tile[r * pitch + k] = src[k];
   }
   __syncthreads();
-  for (int i = tid; i < 64 * 64; i += 256) {
-    const int el = i >> 6, jl = i & 63, j = j0 + jl, e = e0 + el;
-    if (j < W1 && e < El) {
-      const int k = (j >> lev) - e + Wl - 1;
-      out[slice * slice_sz + soff + (long)e * W1 + j] = tile[jl][k - kmin];
-    }
+  // row e of column j holds cell k = (j >> lev) - e + Wl - 1 of row j; the cells with k outside
+  // [0, Wl) are not written: the lookup's tap test on the grid index selects 0 for them
+  // without using the loaded value (that halves this pass's writes)
+  const int jl = tid % SH_J, j = j0 + jl;
+  if (jl >= nj) return;
+  float *dst = out + slice * slice_sz + soff + j;
+  for (int e = tid / SH_J; e < El; e += 256 / SH_J) {
+    const int k = (j >> lev) - e + Wl - 1;
+    if (k >= 0 && k < Wl) dst[(long)e * W1] = tile[jl * pitch + k];
   }
 }
 
@@ -76,15 +81,18 @@ struct ShLGeo {
 
 // lookup_c1_vec_kernel (corr_lookup.hip) on the sheared pyramid: the same per-tap grid
 // arithmetic, the window's cells gathered by one load each from the rows e of column j
-template <int L, int R, int COUT>
+template <int L, int R, int COUT, bool MF = false>
 __global__ __launch_bounds__(256) void lookup_c1_shear_kernel(const float *__restrict__ sa, const float *__restrict__ sb,
                                                               const float *__restrict__ cx, ShLGeo g, int npix,
                                                               const float *__restrict__ wt,
                                                               const float *__restrict__ bias, int nvol,
                                                               float *__restrict__ out) {
   constexpr int K = 2 * R + 1, NT = L * K, WIN = 2 * R + 4;   // cells x_-R - 1 .. x_-R + 2R + 2
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= npix) return;
+  static_assert(!MF || COUT == 64, "MFMA convc1: 64 outputs");
+  __shared__ float c1lds[MF ? 4 : 1][MF ? NT * sa::C1_PITCH : 1];
+  const int p0 = blockIdx.x * 256 + threadIdx.x;
+  if (!MF && p0 >= npix) return;
+  const int p = p0 < npix ? p0 : npix - 1;   // (MFMA: the whole wave takes part)
   const int v = blockIdx.y;
   const int hw = g.H * g.W1;
   const int b = p / hw, rem = p - b * hw;
@@ -131,6 +139,16 @@ __global__ __launch_bounds__(256) void lookup_c1_shear_kernel(const float *__res
       f[l * K + t] = v0 * (1.0f - w) + v1 * w;
     }
   }
+  if constexpr (MF) {
+    const int lane = threadIdx.x & 63;
+    sa::C1Weights<NT> w;
+    sa::c1_load_weights<NT>(wt, bias, lane, w);
+    const int wp0 = p0 - lane;
+    sa::c1_mfma<NT>(f, w, c1lds[threadIdx.x >> 6], lane, [&](int q, int gq, const auto &r) {
+      sa::c1_store4(out, wp0 + 16 * q + 4 * (lane >> 4), 16 * gq + (lane & 15), hw, nvol, v, npix, r);
+    });
+    return;
+  }
   float *__restrict__ o = out + ((long)b * nvol + v) * COUT * hw + rem;
 #pragma unroll 4
   for (int c0 = 0; c0 < COUT; c0 += 8) {
@@ -148,6 +166,8 @@ __global__ __launch_bounds__(256) void lookup_c1_shear_kernel(const float *__res
 }
 
 }  // namespace
+
+extern "C" int sa_lookup_get_mfma();
 
 extern "C" long sa_shear_slice_size(int W1, int W2, int num_levels) {
   if (W1 <= 0 || W2 <= 0 || num_levels < 1 || num_levels > 4) return -1;
@@ -169,10 +189,12 @@ extern "C" int sa_corr_pyramid_shear(const float *pyramid, long row_stride, int 
   const ShGeo g = shear_geo(W1, W2, num_levels);
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_LOOKUP, s);
+  SA_REQUIRE((long)SH_J * (W2 + 1) * 4 <= 64 * 1024, "sa_corr_pyramid_shear: W2 %d too wide for the LDS tile", W2);
   for (int l = 0; l < num_levels; ++l) {
-    const dim3 grid((unsigned)((W1 + 63) / 64), (unsigned)((g.rows[l] + 63) / 64), (unsigned)(B * H));
-    shear_kernel<<<grid, 256, 0, s>>>(pyramid, row_stride, W1, sa_pyramid_level_offset(W2, l), g.wid[l], g.rows[l],
-                                      l, g.slice, g.off[l], sheared);
+    const dim3 grid((unsigned)((W1 + SH_J - 1) / SH_J), 1u, (unsigned)(B * H));
+    const size_t lds = (size_t)SH_J * (g.wid[l] + 1) * sizeof(float);
+    shear_kernel<<<grid, 256, lds, s>>>(pyramid, row_stride, W1, sa_pyramid_level_offset(W2, l), g.wid[l], g.rows[l],
+                                        l, g.slice, g.off[l], sheared);
   }
   return sa::check_launch("sa_corr_pyramid_shear");
 }
@@ -206,7 +228,11 @@ extern "C" int sa_corr_lookup_conv1x1_sheared(const float *sheared_a, const floa
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_LOOKUP, s);
   dim3 grid((unsigned)((npix + 255) / 256), nvol);
-  lookup_c1_shear_kernel<4, 4, 64><<<grid, 256, 0, s>>>(sheared_a, sheared_b ? sheared_b : sheared_a, coords_x, g,
-                                                        (int)npix, weight_kc, bias, nvol, out);
+  if (sa_lookup_get_mfma())
+    lookup_c1_shear_kernel<4, 4, 64, true><<<grid, 256, 0, s>>>(sheared_a, sheared_b ? sheared_b : sheared_a, coords_x,
+                                                                g, (int)npix, weight_kc, bias, nvol, out);
+  else
+    lookup_c1_shear_kernel<4, 4, 64><<<grid, 256, 0, s>>>(sheared_a, sheared_b ? sheared_b : sheared_a, coords_x, g,
+                                                          (int)npix, weight_kc, bias, nvol, out);
   return sa::check_launch("sa_corr_lookup_conv1x1_sheared");
 }

@@ -94,6 +94,8 @@ class ScheduleOptions:
     # one load instruction of a wave reads one or two row segments; the row layout spreads
     # it over 64 cache lines); False: the row-layout lookup
     sheared_lookup: bool = True
+    # ... when the stereo volume (B x H4 x W4 x W4 floats) is at least this large
+    shear_min_bytes: int = 1 << 30
     # a GRU level whose width is not a multiple of 4 keeps its planes padded to one (zero
     # columns) and runs on F(4x4) with the gates in the epilogue (False: separate gate kernels and
     # F(2x2) launches for that level)
@@ -342,9 +344,12 @@ class StereoAnywhere(nn.Module):
                                   _shape=(B, H4, W4, W4))
         del mono_rows, vol_d, vol_c
 
-        if self.opts.sheared_lookup:
+        if self.opts.sheared_lookup and B * H4 * W4 * W4 * 4 >= self.opts.shear_min_bytes:
             # the lookups read disparity-sheared copies (coalesced across a wave's pixels); the
-            # row-layout buffers are not read again
+            # row-layout buffers are not read again.  Only for large volumes: the copy costs
+            # ~2.9 TB/s of its bytes once, and the sheared lookup is no faster at B = 4 x 240
+            # (53.6 vs 52.9 us) but 0.69x at the booster tile batch (717 vs 1036 us;
+            # scripts/bench_lookup.py)
             stereo_blk.shear(release=True)
             mono_blk.shear(release=True)
         parts = min(self.opts.loop_parts, B) if self.stream_overlap else 1

@@ -155,7 +155,8 @@ def test_loop_parts_match_one_stream(model, parts, offset):
 @pytest.mark.parametrize("change", [dict(group_convs=False), dict(fuse_gates=False), dict(fuse_out=False),
                                     dict(mono_stream=False), dict(cnet_side=1), dict(cnet_side=0),
                                     dict(small_launches=frozenset({"q16", "q08", "zr16", "zr08", "pro32"})),
-                                    dict(direct_conv=False), dict(wino4=False)])
+                                    dict(direct_conv=False), dict(wino4=False),
+                                    dict(sheared_lookup=True, shear_min_bytes=0), dict(persist=True)])
 def test_schedule_options_vs_reference(change):
     """Every non-default launch schedule (stereoanywhere_amd.model.ScheduleOptions; ops._WINO4)
     computes the same forward: cfg1 against the reference's disparity."""
@@ -165,16 +166,18 @@ def test_schedule_options_vs_reference(change):
     m = StereoAnywhere(dict(PUBLISHED)).eval()
     synth.load_seeded_weights(m, 0)
     m = m.cuda()
+    change = dict(change)
     wino4 = change.pop("wino4", True)
+    persist = change.pop("persist", False)
     m.opts = dataclasses.replace(m.opts, **change)
     fix = load_fixture("cfg1_256x512_it8.npz")
     pair = regenerate_inputs(fix, 1, 256, 512, 64.0)
-    old = ops._WINO4
-    ops._WINO4 = wino4
+    old = ops._WINO4, ops.W4_PERSIST
+    ops._WINO4, ops.W4_PERSIST = wino4, persist
     try:
         disp = run(m, pair, 8)
     finally:
-        ops._WINO4 = old
+        ops._WINO4, ops.W4_PERSIST = old
     e = epe(disp, fix["disparity"])
     print(change, "wino4" if wino4 else "no wino4", "EPE", e)
     assert e < 1e-3

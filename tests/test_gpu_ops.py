@@ -157,7 +157,7 @@ def test_lookup_fused_taps_bit_exact():
         assert np.all(fused[v::2, 36:] == 0)
 
 
-@pytest.mark.parametrize("W1,W2", [(96, 96), (70, 70), (240, 240), (37, 45)])
+@pytest.mark.parametrize("W1,W2", [(96, 96), (70, 70), (240, 240), (37, 45), (30, 30)])
 def test_lookup_sheared_bit_exact(W1, W2):
     """The lookup + convc1 on the disparity-sheared pyramid copies (corr_shear.hip) equals the
     row-layout kernel bit for bit (the same taps and arithmetic; only the layout differs):
@@ -177,11 +177,20 @@ def test_lookup_sheared_bit_exact(W1, W2):
     wt = (rng.standard_normal((36, 64)) / 6).astype(np.float32)
     bias = rng.standard_normal(64).astype(np.float32)
     pa, pb = ops.pyramid_from_volume(g(va)), ops.pyramid_from_volume(g(vb))
-    row = c(ops.corr_lookup_conv1x1(pa, pb, W2, 4, 4, g(cx), g(wt), g(bias)))
     sa, sb = ops.corr_pyramid_shear(pa, B, H, W1, W2), ops.corr_pyramid_shear(pb, B, H, W1, W2)
-    sh = c(ops.corr_lookup_conv1x1_sheared(sa, sb, W2, 4, 4, g(cx), g(wt), g(bias)))
+    res = {}
+    for mf in (1, 0):   # convc1 on MFMA / on the VALU: the same fmaf chains
+        N.lib().sa_lookup_set_mfma(mf)
+        try:
+            res[mf] = (c(ops.corr_lookup_conv1x1(pa, pb, W2, 4, 4, g(cx), g(wt), g(bias))),
+                       c(ops.corr_lookup_conv1x1_sheared(sa, sb, W2, 4, 4, g(cx), g(wt), g(bias))))
+        finally:
+            N.lib().sa_lookup_set_mfma(1)
+    row, sh = res[1]
     np.testing.assert_array_equal(sh, row)
-    # the sheared copy holds every level cell once, zeros elsewhere
+    np.testing.assert_array_equal(res[0][0], row)
+    np.testing.assert_array_equal(res[0][1], row)
+    # the sheared copy holds every level cell once (other entries are never read)
     _, offs, wids = ops.pyramid_geometry(W2, 4)
     sa_h = c(sa)
     for l in range(4):
@@ -193,7 +202,6 @@ def test_lookup_sheared_bit_exact(W1, W2):
         for k in (0, wids[l] - 1, wids[l] // 2):
             e = (j >> l) - k + wids[l] - 1
             np.testing.assert_array_equal(lvl[:, e, j], ref[:, j, k])
-        assert np.count_nonzero(lvl) <= np.count_nonzero(ref)
 
 
 def test_hip_corr_block_contract(micro):
