@@ -453,7 +453,10 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   int tid = threadIdx.x;
   // persistent items: an opaque thread id per item keeps the compiler from hoisting the
   // lane-dependent offsets out of the item loop (live across it they cost ~20 VGPRs and spilled)
-  if constexpr (PERSIST) asm volatile("" : "+v"(tid));
+#ifndef SA_W4_OPAQUE
+#define SA_W4_OPAQUE 1
+#endif
+  if constexpr (PERSIST && SA_W4_OPAQUE) asm volatile("" : "+v"(tid));
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int co_blocks = P.co_blocks, tiles_hw = P.tiles_hw, tiles_w = P.tiles_w;
@@ -677,7 +680,10 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][5] = __builtin_amdgcn_s_memtime();
 #endif
 
-  if constexpr (PERSIST) {
+#ifndef SA_W4_P2PASS
+#define SA_W4_P2PASS 1   // 0 (diagnostic, with SA_W4_PF=0 only): the one-shot epilogue in persistent items
+#endif
+  if constexpr (PERSIST && SA_W4_P2PASS) {
     // Persistent item: the next item's chunk 0 is landing in the other buffer, so the outputs
     // are staged one 16-channel group at a time in this item's last buffer (16 planes of OPP
     // fit in BUF).  Group g is finished by half HF == g: both halves form their partial of g
