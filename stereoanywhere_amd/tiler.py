@@ -215,6 +215,7 @@ class TileWrapper(torch.nn.Module):
         if B != 1:
             raise ValueError("TileWrapper currently supports batch size == 1")
         if H <= self.tile_height and W <= self.tile_width:
+            self.last_tile_counts = (1, 1)
             return canonicalize(self.model(left, right, mono_left, mono_right, *args, **kw))
         guide = None
         if global_guidance is not None and guidance_weight > 0:

@@ -35,6 +35,9 @@ def test_tiles_weights_and_stitch_match_reference(fix, i):
     for batch in (False, True):
         wrap = tiler.TileWrapper(Mock(), tile_width=tw, tile_height=th, overlap=ov, batch_tiles=batch)
         out = wrap(t["l"], t["r"], t["ml"], t["mr"], iters=1, test_mode=True)
+        # cases 0-2 enumerate duplicate rectangles (10/8, 8/3, 20/9 tiles/unique): each unique one
+        # runs once and is added with its multiplicity, and the stitch still equals the reference's
+        assert wrap.last_tile_counts == (len(tiles), len(set(tiles)))
         np.testing.assert_allclose(out.numpy(), fix[f"case{i}.out"], atol=1e-6)
 
 
