@@ -265,10 +265,12 @@ int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W, const flo
                  int Cout, const float *in_mean, const float *in_rstd, int act, float slope,
                  const float *gate_l, const float *gate_r, float *out, double *stats_partial,
                  void *stream);
-/* sa_conv3d_wd's weight staging: 0 (default) wave-uniform scalar loads; 1 the per-channel
- * weights go through LDS with the input slab, a channel ahead (measured slower).  For A/B runs
- * and tests. */
-void sa_conv3d_wd_set_variant(int lds_weights);
+/* sa_conv3d_wd's kernel variant (same products in the same order, bit-identical results):
+ * 0 (default) wave-uniform scalar weights; 1 the per-channel weights staged in LDS with the input
+ * slab, a channel ahead; 2 (8-input-channel convs) the two D-tiles' transform points paired in the
+ * slab for packed FMAs; 3 variant 2 with the next channel's columns fetched by LDS-DMA.  For A/B
+ * runs and tests. */
+void sa_conv3d_wd_set_variant(int variant);
 /* The hourglass's two readers of the masked mono volume (down_layers[0][0], hourglass.py:27-33;
  * final_agg[0] over cat(orig, up(x)), hourglass.py:326-328) on the one-hot volume given by its
  * records (sa_mono_bin_records; rec_l [B,H,W] of the left pixels = the volume's W axis, rec_r

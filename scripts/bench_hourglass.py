@@ -2,8 +2,9 @@
 """Per-layer timing of the fused mono hourglass at the bench shape (B=4, 544x960 ->
 volume [4, 8, 240, 136, 240]), random weights.  Each ops.* call of the fused path is
 bracketed by HIP events on the current stream.
-usage: python scripts/bench_hourglass.py [reps] [--dense] [--lds-weights]
-(SA_HIP_LIB=... selects a library build; --lds-weights: sa_conv3d_wd's LDS-weight variant)"""
+usage: python scripts/bench_hourglass.py [reps] [--dense] [--lds-weights | --variant N]
+(SA_HIP_LIB=... selects a library build; --lds-weights: sa_conv3d_wd's LDS-weight variant,
+--variant N: sa_conv3d_wd_set_variant(N))"""
 import collections
 import os
 import sys
@@ -17,9 +18,11 @@ from stereoanywhere_amd.blocks import Hourglass  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 5
+    from stereoanywhere_amd import _native as N
     if "--lds-weights" in sys.argv:
-        from stereoanywhere_amd import _native as N
         N.lib().sa_conv3d_wd_set_variant(1)
+    if "--variant" in sys.argv:
+        N.lib().sa_conv3d_wd_set_variant(int(sys.argv[sys.argv.index("--variant") + 1]))
     B, D, H, W = 4, 240, 136, 240
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)

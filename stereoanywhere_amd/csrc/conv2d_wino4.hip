@@ -44,7 +44,8 @@
 #ifndef SA_W4_DIAG
 #define SA_W4_DIAG 0   // timing diagnostics only (wrong results): 1 no DMA in the loop, 2 no
                        // transform / MFMA, 3 no DMA and no barrier in the loop, 4 as 3 and no
-                       // DMA at all, 5 no column pass, 6 no row pass, 7 no filter reads in the loop
+                       // DMA at all, 5 no column pass, 6 no row pass, 7 no filter reads in the loop,
+                       // 8 neither row nor column pass (no input transform)
 #endif
 #ifndef SA_W4_PERM
 #define SA_W4_PERM 1   // lane -> tile permutation that makes the patch rows' ds_read_b128 conflict-free
@@ -636,7 +637,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
       float t[6][3];
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
-        if (SA_W4_DIAG == 6) {   // timing only: no row pass
+        if (SA_W4_DIAG == 6 || SA_W4_DIAG == 8) {   // timing only: no row pass
           t[r][0] = ra[r].y; t[r][1] = rb[r].x; t[r][2] = rc[r].x;
         } else {
           bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t[r]);
@@ -647,7 +648,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
       for (int jj = 0; jj < 3; ++jj) {
         if (SA_W4_DIAG != 7 && (s + 1 < JPC || jj < 2)) load_b(jj < 2 ? s : s + 1, jj < 2 ? jj + 1 : 0, bn);
         float v[6];
-        if (SA_W4_DIAG == 5) {   // timing only: no column pass
+        if (SA_W4_DIAG == 5 || SA_W4_DIAG == 8) {   // timing only: no column pass
 #pragma unroll
           for (int i = 0; i < NR; ++i) v[i] = t[i][jj];
         } else if constexpr (QUAD) {

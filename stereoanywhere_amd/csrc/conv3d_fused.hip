@@ -390,7 +390,20 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const float *__restrict__ i
 //            floats, double-buffered), read as wave-uniform LDS vectors instead of SGPR loads
 //            (the scalar-load variant spends 42% of its wave cycles at waitcnt / barrier);
 //            measured slower, so off by default (sa_conv3d_wd_set_variant)
-template <int CIN, int COUT, int NT, bool GATED, bool WL = false>
+//   PK     = (NT = 2) the two D-tiles' points interleaved in the slab, (t0 p, t1 p) pairs, so a
+//            16-byte read is two aligned register pairs and each (p, co) product pair is one
+//            v_pk_fma_f32 with the weight broadcast from its SGPR.  Without it the compiler packs
+//            over output-channel pairs and copies the X values that sit in odd registers into
+//            pairs whose other half can be a pending global load of the next channel's prefetch:
+//            the copy then waits for that load (s_waitcnt vmcnt) inside the first tap pair of
+//            every channel, and the prefetch stops overlapping the FMAs.
+//   DMA    = the next channel's raw columns fetched by LDS-DMA (buffer_load_dword ... lds) into
+//            a [6 rows][LD planes][64 lanes] staging area instead of 2 x LD VGPRs per thread; each
+//            wave reads back only its own lanes' words, after its own vmcnt(0) in commit
+#ifndef SA_WD_BUF
+#define SA_WD_BUF 0   // 1: the staging loads as buffer loads (diagnostic: 8 -> 8 then needs 175 VGPRs)
+#endif
+template <int CIN, int COUT, int NT, bool GATED, bool WL = false, bool PK = false, bool DMA = false>
 __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict__ in, int D, int H, int W,
                                                         const float *__restrict__ wt, InXform tx,
                                                         float *__restrict__ out, double *__restrict__ partial,
@@ -405,6 +418,7 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
   constexpr int CC = COUT < 8 ? COUT : 8;   // output channels per weight group (48 SGPRs)
   __shared__ __attribute__((aligned(16))) float slab[2][LH * ROWP];
   __shared__ double red[COUT * 4 * 2];
+  __shared__ float raw[DMA ? LH : 1][DMA ? LD : 1][64];
   constexpr int WPC = 54 * COUT, NWL = (WPC + 255) / 256;   // weights per input channel, per thread
   __shared__ __attribute__((aligned(16))) float wsl[WL ? 2 : 1][WL ? WPC : 4];
   float pw[NWL];
@@ -443,22 +457,47 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
 
   // staging columns of this thread: (row wv, lane) and, for waves 0-1, (row wv + 4, lane)
   constexpr int NCOL = 2;
-  float pv[NCOL][LD];
+  float pv[NCOL][DMA ? 1 : LD];
   float pgl[NCOL], pgr[NCOL];
+  float pmean, prstd;   // the channel's InstanceNorm, fetched with its columns
   auto fetch = [&](int ci) __attribute__((always_inline)) {
     const long bc = (long)b * CIN + ci;
     const float *src = in + bc * (long)D * hw;
+    if constexpr (NT == 2) {   // (the 16-channel convs measured ~8% slower with this)
+      pmean = tx.mean[bc];
+      prstd = tx.rstd[bc];
+    }
 #pragma unroll
     for (int k = 0; k < NCOL; ++k) {
       const int hh = wv + 4 * k;
-      if (hh < LH) {
+      if ((NT == 2 && k == 0) || hh < LH) {   // (row wv < 4 always exists)
         const int hc = min(max(h0 - 1 + hh, 0), H - 1);
         const float *colp = src + hc * W + wcl;
 #pragma unroll
         for (int j = 0; j < LD; ++j) {
           int off = min(max(d0 - 1 + j, 0), D - 1) * hw;
-          asm volatile("" : "+v"(off));   // plane offsets in VGPRs: SGPRs hold the weights
-          pv[k][j] = colp[off];
+          if constexpr (DMA) {
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(src), (short)0, D * hw * 4, 0x00020000);
+            // the LDS address laundered through an SGPR: the DMA then carries no alias scope, and
+            // the compiler does not make the slab reads of the tap loop wait for it (vmcnt(0));
+            // commit waits for this wave's DMAs itself
+            unsigned la = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void *)&raw[hh][j][0];
+            asm volatile("" : "+s"(la));
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(uintptr_t)la, 4,
+                                                     (off + hc * W + wcl) * 4, 0, 0, 0);
+          } else if constexpr (SA_WD_BUF) {
+            // a buffer load at a 32-bit lane offset from the channel's base (no 64-bit address
+            // per load); the plane offset in a VGPR (SGPRs hold the weights)
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(src), (short)0, D * hw * 4, 0x00020000);
+            int vo = (off + hc * W + wcl) * 4;
+            asm volatile("" : "+v"(vo));
+            pv[k][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 0, 0));
+          } else {
+            asm volatile("" : "+v"(off));   // plane offsets in VGPRs: SGPRs hold the weights
+            pv[k][j] = colp[off];
+          }
         }
         if (GATED) {
           pgl[k] = tx.gl[(bc * H + hc) * W + wcl];
@@ -468,18 +507,23 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
     }
   };
   auto commit = [&](int ci, int buf) __attribute__((always_inline)) {
+    // NT = 2: mean / rstd were fetched with the columns.  Loading them here, the loads' target
+    // registers were reused by the tap loop, and at its head the compiler waited for every
+    // outstanding load (s_waitcnt vmcnt(0)), i.e. for the next channel's prefetch: 8 -> 8
+    // 1100 -> 970 us without that wait
     const long bc = (long)b * CIN + ci;
-    const float mean = tx.mean[bc], rstd = tx.rstd[bc];
+    const float mean = NT == 2 ? pmean : tx.mean[bc], rstd = NT == 2 ? prstd : tx.rstd[bc];
+    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs landed
 #pragma unroll
     for (int k = 0; k < NCOL; ++k) {
       const int hh = wv + 4 * k;
-      if (hh < LH) {
+      if ((NT == 2 && k == 0) || hh < LH) {
         const int h = h0 - 1 + hh;
         const bool cok = wok && h >= 0 && h < H;
         float x[LD];
 #pragma unroll
         for (int j = 0; j < LD; ++j) {
-          float v = (pv[k][j] - mean) * rstd;
+          float v = ((DMA ? raw[hh][j][lane] : pv[k][j]) - mean) * rstd;
           v = v > 0.0f ? v : v * tx.slope;
           if (GATED) {   // gate_l[h, w] * gate_r[h, d] (xform's order)
             const float gr = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pgr[k]), j));
@@ -496,20 +540,32 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
         for (int q = 0; q < NP / VW; ++q) {
           VT v;
 #pragma unroll
-          for (int e = 0; e < VW; ++e) reinterpret_cast<float *>(&v)[e] = o[VW * q + e];
+          for (int e = 0; e < VW; ++e) {
+            const int i = VW * q + e;   // slab position; PK: (t0 p, t1 p) pairs
+            reinterpret_cast<float *>(&v)[e] = PK ? o[6 * (i & 1) + (i >> 1)] : o[i];
+          }
           dst[q] = v;
         }
       }
     }
   };
 
-  float M[NT][6][COUT];
+  static_assert(!PK || NT == 2, "PK pairs the two D-tiles");
+  using f2 = __attribute__((ext_vector_type(2))) float;
+  float M[PK ? 1 : NT][6][COUT];
+  f2 M2[PK ? 6 : 1][PK ? COUT : 1];
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
+  for (int t = 0; t < (PK ? 1 : NT); ++t)
 #pragma unroll
     for (int p = 0; p < 6; ++p)
 #pragma unroll
       for (int c = 0; c < COUT; ++c) M[t][p][c] = 0.0f;
+  if constexpr (PK) {
+#pragma unroll
+    for (int p = 0; p < 6; ++p)
+#pragma unroll
+      for (int c = 0; c < COUT; ++c) M2[p][c] = f2{0.0f, 0.0f};
+  }
 
   fetch(0);
   wfetch(0);
@@ -553,8 +609,13 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
 #pragma unroll
             for (int c = cg * CC; c < cg * CC + CC; ++c) {
               const float wv_ = wp[p * COUT + c];
+              if constexpr (PK) {
+                const f2 xp2 = f2{X[2 * p], X[2 * p + 1]};
+                M2[p][c] = __builtin_elementwise_fma(xp2, f2{wv_, wv_}, M2[p][c]);
+              } else {
 #pragma unroll
-              for (int t = 0; t < NT; ++t) M[t][p][c] += X[6 * t + p] * wv_;
+                for (int t = 0; t < NT; ++t) M[t][p][c] += X[6 * t + p] * wv_;
+              }
             }
         }
       }
@@ -578,7 +639,7 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
     for (int c = 0; c < COUT; ++c) {
       float m[6], o[4];
 #pragma unroll
-      for (int p = 0; p < 6; ++p) m[p] = M[t][p][c];
+      for (int p = 0; p < 6; ++p) m[p] = PK ? M2[p][c][t] : M[t][p][c];
       at6(m, o);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -887,8 +948,13 @@ extern "C" int sa_conv3d(const float *in, int B, int Cin, int Di, int Hi, int Wi
 // 0: wave-uniform scalar weight loads (default); 1: the weights staged in LDS (conv3d_wd_kernel
 // WL), measured slower: bench_hourglass whole hourglass 8.62 against 7.73 ms, the 8 -> 8 convs
 // 1.29-1.36 against 1.08-1.11 ms (LDS reads in the FMA loop cost more than the SGPR waits)
-static int sa_conv3d_wd_lds_weights = 0;
-extern "C" void sa_conv3d_wd_set_variant(int lds_weights) { sa_conv3d_wd_lds_weights = lds_weights ? 1 : 0; }
+// 0 (default): scalar weights; points in D-tile order, or paired for the 8 -> 2 classifier pair
+// (507 vs 547 us; 8 -> 8 is faster unpaired, 970 vs 1050 us); 1: LDS-staged weights (slower);
+// 2: paired points for every 8-input-channel conv (the 16-channel ones have one D-tile);
+// 3: variant 2 with the channel prefetch by LDS-DMA (slower: the compiler makes the tap loop's
+// slab reads wait for the DMA)
+static int sa_conv3d_wd_variant = 0;
+extern "C" void sa_conv3d_wd_set_variant(int variant) { sa_conv3d_wd_variant = variant; }
 
 extern "C" int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W, const float *weight_wd, int Cout,
                             const float *in_mean, const float *in_rstd, int act, float slope, const float *gate_l,
@@ -897,7 +963,7 @@ extern "C" int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W
   SA_REQUIRE(B > 0 && D > 0 && H > 0 && W > 0, "sa_conv3d_wd: empty shape");
   SA_REQUIRE((in_mean == nullptr) == (in_rstd == nullptr), "sa_conv3d_wd: mean and rstd go together");
   SA_REQUIRE((gate_l == nullptr) == (gate_r == nullptr), "sa_conv3d_wd: both gate maps or none");
-  SA_REQUIRE((long)D * H * W < (1L << 31), "sa_conv3d_wd: a channel plane must hold < 2^31 voxels");
+  SA_REQUIRE((long)D * H * W * 4 < (1L << 31), "sa_conv3d_wd: a channel volume must hold < 2^31 bytes");
   SA_REQUIRE((Cin == 8 && (Cout == 8 || Cout == 2)) || (Cin == 16 && Cout == 16),
              "sa_conv3d_wd: built for 8 -> 8, 8 -> 2 and 16 -> 16 (got %d -> %d)", Cin, Cout);
   // the same tiling as sa_conv3d's for these shapes (8 or 4 planes x 4 rows x 62 columns): the
@@ -912,9 +978,15 @@ extern "C" int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W
   SA_REQUIRE(in_mean && act, "sa_conv3d_wd: built for an InstanceNorm + LeakyReLU producer");
 #define SA_WD(CI, CO, NTV, G)                                                                                   \
   if (Cin == CI && Cout == CO && (gate_l != nullptr) == G) {                                                    \
-    if (sa_conv3d_wd_lds_weights)                                                                               \
+    if (sa_conv3d_wd_variant == 1)                                                                              \
       conv3d_wd_kernel<CI, CO, NTV, G, true><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, \
                                                                   tilesD);                                      \
+    else if ((sa_conv3d_wd_variant == 2 || (sa_conv3d_wd_variant == 0 && CO == 2)) && NTV == 2)                 \
+      conv3d_wd_kernel<CI, CO, NTV, G, false, NTV == 2><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out,    \
+                                                                             stats_partial, tilesD);            \
+    else if (sa_conv3d_wd_variant == 3)                                                                         \
+      conv3d_wd_kernel<CI, CO, NTV, G, false, NTV == 2, true><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx,   \
+                                                                                   out, stats_partial, tilesD); \
     else                                                                                                        \
       conv3d_wd_kernel<CI, CO, NTV, G><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out, stats_partial, tilesD); \
     return sa::check_launch("sa_conv3d_wd");                                                                     \
