@@ -400,6 +400,10 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const float *__restrict__ i
 //   DMA    = the next channel's raw columns fetched by LDS-DMA (buffer_load_dword ... lds) into
 //            a [6 rows][LD planes][64 lanes] staging area instead of 2 x LD VGPRs per thread; each
 //            wave reads back only its own lanes' words, after its own vmcnt(0) in commit
+#ifndef SA_WD_UNIF
+#define SA_WD_UNIF 0   // 1: uniform staging for the 16-channel convs (no wait on the prefetch in
+                       // their tap loop, but 570 -> 650 us: the duplicate loads and commits cost more)
+#endif
 #ifndef SA_WD_BUF
 #define SA_WD_BUF 0   // 1: the staging loads as buffer loads (diagnostic: 8 -> 8 then needs 175 VGPRs)
 #endif
@@ -416,7 +420,12 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
   constexpr int VW = sizeof(VT) / 4;
   static_assert(ROWP % 4 == 0, "row alignment");
   constexpr int CC = COUT < 8 ? COUT : 8;   // output channels per weight group (48 SGPRs)
-  __shared__ __attribute__((aligned(16))) float slab[2][LH * ROWP];
+  // SA_WD_UNIF: every wave stages two columns (waves 2-3 a clamped duplicate of row 5, committed
+  // to a spare slab row), so fetch and commit have no wave-dependent branch
+  // (the 16-channel convs; with 8 channels it needs 170 VGPRs: 2 waves per SIMD instead of 3)
+  constexpr bool UNIF = SA_WD_UNIF && NT == 1;
+  constexpr int SLR = UNIF ? LH + 1 : LH;
+  __shared__ __attribute__((aligned(16))) float slab[2][SLR * ROWP];
   __shared__ double red[COUT * 4 * 2];
   __shared__ float raw[DMA ? LH : 1][DMA ? LD : 1][64];
   constexpr int WPC = 54 * COUT, NWL = (WPC + 255) / 256;   // weights per input channel, per thread
@@ -470,8 +479,8 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
 #pragma unroll
     for (int k = 0; k < NCOL; ++k) {
       const int hh = wv + 4 * k;
-      if ((NT == 2 && k == 0) || hh < LH) {   // (row wv < 4 always exists)
-        const int hc = min(max(h0 - 1 + hh, 0), H - 1);
+      if (UNIF || (NT == 2 && k == 0) || hh < LH) {   // (row wv < 4 always exists)
+        const int hc = min(max(h0 - 1 + min(hh, LH - 1), 0), H - 1);
         const float *colp = src + hc * W + wcl;
 #pragma unroll
         for (int j = 0; j < LD; ++j) {
@@ -517,7 +526,7 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
 #pragma unroll
     for (int k = 0; k < NCOL; ++k) {
       const int hh = wv + 4 * k;
-      if ((NT == 2 && k == 0) || hh < LH) {
+      if (UNIF || (NT == 2 && k == 0) || hh < LH) {
         const int h = h0 - 1 + hh;
         const bool cok = wok && h >= 0 && h < H;
         float x[LD];
@@ -535,7 +544,7 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
 #pragma unroll
         for (int t = 0; t < NT; ++t)
           bt6(x[4 * t], x[4 * t + 1], x[4 * t + 2], x[4 * t + 3], x[4 * t + 4], x[4 * t + 5], o + 6 * t);
-        VT *dst = reinterpret_cast<VT *>(slab[buf] + hh * ROWP + lane * NP);
+        VT *dst = reinterpret_cast<VT *>(slab[buf] + min(hh, SLR - 1) * ROWP + lane * NP);
 #pragma unroll
         for (int q = 0; q < NP / VW; ++q) {
           VT v;
