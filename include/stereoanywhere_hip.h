@@ -111,8 +111,9 @@ int sa_softargmin_conf(const float *vol_disp, const float *vol_conf, int B, int 
                        int W2, long sb, long sh, long sj, long sk, float *dL, float *dR,
                        float *cL, float *cR, long out_bs, void *stream);
 /* With sj == 1 and W1 == W2 <= 288 (the model's layout) sa_softargmin_conf reads each volume
- * once: a workgroup per (b, h) slice forms both sides' reductions.  on = 0 selects the
- * per-line kernels instead (two launches, each reading both volumes); for A/B runs and tests. */
+ * once: a workgroup per (b, h) slice forms both sides' reductions.  on = 0 selects the per-line
+ * kernels instead (two launches, each reading both volumes), on = 2 the one-pass kernel's
+ * 16-byte-row variant (n % 4 == 0, n <= 256, aligned rows; slower); for A/B runs and tests. */
 void sa_softargmin_set_one_pass(int on);
 
 /* a7 — softlrc (utils.py:189-198) with disp_warping (utils.py:172-187); optional

@@ -18,9 +18,10 @@ vd, vc = t[:, 0:1], t[:, 1:2]
 strides = (t.stride(0), W, 1, H * W)
 alg = 2 * 4 * B * H * W * W
 from stereoanywhere_amd import _native as N  # noqa: E402
-for one_pass in (1, 0):
+NAMES = {1: "one-pass", 2: "one-pass (16-byte rows where they apply)", 0: "per-line"}
+for one_pass in (1, 2, 0):
     N.lib().sa_softargmin_set_one_pass(one_pass)
     us = timeit(lambda: ops.softargmin_conf(vd, vc, strides, (B, H, W, W)), reps=20)
-    print(f"softargmin_conf {B}x{H}x{W}x{W} {'one-pass' if one_pass else 'per-line'}: {us:.1f} us, "
+    print(f"softargmin_conf {B}x{H}x{W}x{W} {NAMES[one_pass]}: {us:.1f} us, "
           f"{alg / us / 1e6:.2f} TB/s of algorithmic bytes ({alg / 1e6:.0f} MB)", flush=True)
 N.lib().sa_softargmin_set_one_pass(1)

@@ -29,15 +29,33 @@ struct SGeo {
   float log2W1, log2W2;  // math.log2(W) of the reference (double), rounded once to fp32
 };
 
+// Wave reductions on DPP (VALU lane moves: quad_perm [1,0,3,2] and [2,3,0,1], row_half_mirror,
+// row_mirror, then row_bcast:15 / row_bcast:31 carry the row totals up to lane 63, read back as
+// a wave-uniform value).  __shfl_xor compiled to ds_bpermute, an LDS round trip per step: 18
+// dependent ones per row of the slice kernels, which made them latency-bound (the loads alone
+// take a quarter of their time).  Identity-filled lanes (masked rows) keep their value.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dppf(float identity, float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, identity),
+                                                               __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, false));
+}
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
+  v = fmaxf(v, dppf<0xB1>(-INFINITY, v));
+  v = fmaxf(v, dppf<0x4E>(-INFINITY, v));
+  v = fmaxf(v, dppf<0x141>(-INFINITY, v));
+  v = fmaxf(v, dppf<0x140>(-INFINITY, v));
+  v = fmaxf(v, dppf<0x142, 0xA>(-INFINITY, v));
+  v = fmaxf(v, dppf<0x143, 0xC>(-INFINITY, v));
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v += dppf<0xB1>(0.0f, v);
+  v += dppf<0x4E>(0.0f, v);
+  v += dppf<0x141>(0.0f, v);
+  v += dppf<0x140>(0.0f, v);
+  v += dppf<0x142, 0xA>(0.0f, v);
+  v += dppf<0x143, 0xC>(0.0f, v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
 // Reduce along an axis of length n with element stride es, output index o of `nout`
@@ -391,12 +409,135 @@ __global__ __launch_bounds__(1024) void sam_slice_kernel(const float *__restrict
   }
 }
 
+#ifndef SA_SAM_DIAG
+#define SA_SAM_DIAG 0   // timing diagnostics (wrong results): 1 loads only, 2 no loads (synthetic cells)
+#endif
+
+// sam_slice_kernel with 16-byte rows (n % 4 == 0, n <= 256, rows 16-byte aligned): lane L holds
+// columns 4L .. 4L + 3 of each of its wave's rows (one dwordx4 load per row instead of four
+// dword loads), wave w rows k = w + 16 r.  The row sums add a lane's four terms first, then
+// across the wave; the column partials go through LDS as in sam_slice_kernel.
+template <int NR>
+__global__ __launch_bounds__(1024) void sam_slice4_kernel(const float *__restrict__ vd, const float *__restrict__ vc,
+                                                          SGeo g, int n, float *dL, float *dR, float *cL, float *cR,
+                                                          int y0) {
+  using f4 = __attribute__((ext_vector_type(4))) float;
+  __shared__ __attribute__((aligned(16))) float red[16][256];
+  __shared__ float colv[256];
+  const int conf = y0 + (int)blockIdx.y;
+  const float *vol = conf ? vc : vd;
+  float *outL = conf ? cL : dL, *outR = conf ? cR : dR;
+  const int bh = blockIdx.x, b = bh / g.H, h = bh % g.H;
+  const float *src = vol + (long)b * g.sb + (long)h * g.sh;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long ob = (long)b * g.obs + (long)h * n;
+  const bool lv = 4 * lane < n;
+  f4 x[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int k = w + 16 * r;
+    if (SA_SAM_DIAG == 2)
+      x[r] = (k < n && lv) ? f4{(float)(k ^ lane), (float)(k + lane), (float)(k - lane), (float)(k * 3 % 7)} : f4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    else
+      x[r] = (k < n && lv) ? *reinterpret_cast<const f4 *>(src + (long)k * g.sk + 4 * lane)
+                           : f4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  }
+  if (SA_SAM_DIAG == 1) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) t += x[r].x + x[r].y + x[r].z + x[r].w;
+    if (t == 1.2345f) outL[ob + lane] = t;
+    return;
+  }
+  // ---- right: per row k, softmax over j
+  const float lw_r = g.log2W1;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int k = w + 16 * r;
+    if (k >= n) continue;   // wave-uniform
+    float m = fmaxf(fmaxf(x[r].x, x[r].y), fmaxf(x[r].z, x[r].w));
+    m = wave_max(m);
+    f4 e;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) e[i] = exp_le0(x[r][i] - m);   // -inf (j >= n) -> 0
+    const float inv = 1.0f / wave_sum((e.x + e.y) + (e.z + e.w));
+    float acc = 0.f;
+    if (lv) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = e[i] * inv;
+        acc += conf ? p * log2_pos(p + 1e-6f) : p * (float)(4 * lane + i);
+      }
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) outR[ob + k] = conf ? 1.0f - (-acc) / lw_r : acc - (float)k;
+  }
+  // ---- left: per column j, softmax over k
+  auto column_total = [&](f4 &part, bool is_max) __attribute__((always_inline)) {
+    *reinterpret_cast<f4 *>(&red[w][4 * lane]) = part;
+    __syncthreads();
+    if (tid < n) {
+      float t = red[0][tid];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) t = is_max ? fmaxf(t, red[i][tid]) : t + red[i][tid];
+      colv[tid] = t;
+    }
+    __syncthreads();
+    if (lv) part = *reinterpret_cast<const f4 *>(&colv[4 * lane]);
+    __syncthreads();   // red / colv are reused by the next total
+  };
+  f4 q = x[0];
+#pragma unroll
+  for (int r = 1; r < NR; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = fmaxf(q[i], x[r][i]);
+  column_total(q, true);   // q = column max
+  f4 se = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x[r][i] = exp_le0(x[r][i] - q[i]);   // rows k >= n: -inf -> 0
+      se[i] += x[r][i];
+    }
+  column_total(se, false);   // column sum of exponentials
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float inv = 1.0f / se[i];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int k = w + 16 * r;
+      const float p = x[r][i] * inv;
+      if (k < n) acc[i] += conf ? p * log2_pos(p + 1e-6f) : p * (float)k;
+    }
+  }
+  *reinterpret_cast<f4 *>(&red[w][4 * lane]) = acc;
+  __syncthreads();
+  if (tid < n) {
+    float t = red[0][tid];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) t += red[i][tid];
+    outL[ob + tid] = conf ? 1.0f - (-t) / g.log2W2 : (float)tid - t;
+  }
+}
+
 // sam_slice_kernel for a slice of side n (sj == 1, W1 == W2); false if no instantiation fits
+int sa_softargmin_v4 = 0;
 bool launch_slices(const float *vd, const float *vc, const SGeo &g, int B, int n, float *dL, float *dR, float *cL,
                    float *cR, hipStream_t s) {
   // grid.y: the volumes present (a confidence-only call starts at y0 = 1)
   const dim3 grid((unsigned)(B * g.H), vd && vc ? 2u : 1u);
   const int y0 = vd ? 0 : 1;
+  auto al = [](const float *p) { return !p || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (sa_softargmin_v4 && n % 4 == 0 && n <= 256 && g.sb % 4 == 0 && g.sh % 4 == 0 && g.sk % 4 == 0 && al(vd) && al(vc)) {
+    if (n <= 240)
+      sam_slice4_kernel<15><<<grid, 1024, 0, s>>>(vd, vc, g, n, dL, dR, cL, cR, y0);
+    else
+      sam_slice4_kernel<16><<<grid, 1024, 0, s>>>(vd, vc, g, n, dL, dR, cL, cR, y0);
+    return true;
+  }
 #define SA_SLICE(NR_, NC_)                                                                          \
   if (n <= 16 * NR_ && n <= 64 * NC_) {                                                             \
     sam_slice_kernel<NR_, NC_><<<grid, 1024, 0, s>>>(vd, vc, g, n, dL, dR, cL, cR, y0);           \
@@ -439,7 +580,12 @@ int launch_side(LineJob jd, LineJob jc, const SGeo &g, int B, int left, hipStrea
 // 1: the one-pass slice kernel where it applies (default); 0: the two line-kernel launches
 // (sa_softargmin_set_one_pass, for A/B runs and tests)
 static int sa_softargmin_one_pass = 1;
-extern "C" void sa_softargmin_set_one_pass(int on) { sa_softargmin_one_pass = on ? 1 : 0; }
+extern "C" void sa_softargmin_set_one_pass(int on) {
+  // 0: the two line-kernel launches; 1 (default): the one-pass slice kernel; 2: the one-pass
+  // slice kernel with 16-byte rows where they apply (cfg2: 132 against 124 us, so not default)
+  sa_softargmin_one_pass = on ? 1 : 0;
+  sa_softargmin_v4 = on == 2 ? 1 : 0;
+}
 
 extern "C" int sa_softargmin_conf(const float *vol_disp, const float *vol_conf, int B, int H, int W1,
                                   int W2, long sb, long sh, long sj, long sk, float *dL, float *dR,

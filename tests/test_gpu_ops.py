@@ -248,14 +248,15 @@ def test_softargmin_confidence(micro, layout):
 
 
 @pytest.mark.parametrize("n", [64, 168, 240, 250, 280, 300])
-@pytest.mark.parametrize("layout", ["reference", "native", "native-lines"])
+@pytest.mark.parametrize("layout", ["reference", "native", "native-v4", "native-lines"])
 def test_softargmin_confidence_lines(n, layout):
     """The native layout (j contiguous, square) takes the one-pass slice kernel up to n = 288
-    (the booster tile's 280 included); "native-lines" forces the per-line kernels on it.  The
-    reference layout runs the register-resident line kernels (line length <= 256: float4 rows,
-    ragged rows, strided columns split over 4 waves) and the generic ones (n = 300).  Two
-    different volumes that are channel views of one tensor, as the model passes them."""
-    N.lib().sa_softargmin_set_one_pass(0 if layout == "native-lines" else 1)
+    (the booster tile's 280 included; "native-v4" takes its 16-byte-row variant where n % 4 == 0
+    and n <= 256); "native-lines" forces the per-line kernels on it.  The reference layout
+    runs the register-resident line kernels (line length <= 256: float4 rows, ragged rows,
+    strided columns split over 4 waves) and the generic ones (n = 300).  Two different volumes
+    that are channel views of one tensor, as the model passes them."""
+    N.lib().sa_softargmin_set_one_pass({"native-lines": 0, "native-v4": 2}.get(layout, 1))
     try:
         _softargmin_lines(n, layout.split("-")[0])
     finally:
@@ -271,7 +272,7 @@ def test_softargmin_one_pass_single_volume():
     t = g(vols)
     strides = (2 * n * H * n, n, 1, H * n)
     res = {}
-    for on in (1, 0):
+    for on in (1, 2, 0):
         N.lib().sa_softargmin_set_one_pass(on)
         try:
             d, _ = ops.softargmin_conf(t[:, 0], None, strides, (B, H, n, n))
@@ -281,8 +282,9 @@ def test_softargmin_one_pass_single_volume():
             N.lib().sa_softargmin_set_one_pass(1)
         assert torch.equal(d, d2) and torch.equal(cf, cf2)
         res[on] = (c(d), c(cf))
-    np.testing.assert_allclose(res[1][0], res[0][0], atol=5e-4)
-    np.testing.assert_allclose(res[1][1], res[0][1], atol=2e-6)
+    for on in (1, 2):
+        np.testing.assert_allclose(res[on][0], res[0][0], atol=5e-4)
+        np.testing.assert_allclose(res[on][1], res[0][1], atol=2e-6)
 
 
 def _softargmin_lines(n, layout):
