@@ -258,10 +258,13 @@ int sa_conv3d_pointwise_upcat(const float *a, int Ca, const float *a_mean, const
                               const float *weight, int Cout, float *out, double *stats_partial,
                               void *stream);
 /* sa_conv3d at stride 1 for Cin 8 -> Cout 8 or 2 (final_agg[1], final_agg[2], the classifier
- * pair) with the D-taps as Winograd F(4,3) along D: weight_wd [Cin][3 kh][3 kw][6][Cout] =
- * G (points 0, +-1, +-2, inf) applied to the kernel's D-taps (ops.conv3d_wd_weights).  The
- * input's transform must include the InstanceNorm + LeakyReLU (in_mean, act); statistics as for
- * sa_conv3d with parts = sa_conv3d_stat_parts(Cout, 1, D, H, W). */
+ * pair), 16 -> 16 (down_layers[0][1], agg_layers[1][1..2]) and 32 -> 32 without gate
+ * (down_layers[1][1], as two 16-channel halves per tile) with the D-taps as Winograd F(4,3) along
+ * D: weight_wd [Cin][3 kh][3 kw][6][Cout] = G (points 0, +-1, +-2, inf) applied to the kernel's
+ * D-taps (ops.conv3d_wd_weights).  The input's transform must include the InstanceNorm +
+ * LeakyReLU (in_mean, act); statistics as for sa_conv3d with parts =
+ * sa_conv3d_wd_stat_parts(Cout, D, H, W) (the 32-channel conv tiles like the 16-channel ones). */
+long sa_conv3d_wd_stat_parts(int Cout, int D, int H, int W);
 int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W, const float *weight_wd,
                  int Cout, const float *in_mean, const float *in_rstd, int act, float slope,
                  const float *gate_l, const float *gate_r, float *out, double *stats_partial,

@@ -92,6 +92,7 @@ SIGNATURES = {
     "sa_plane_stats": (I, [P, L, I, I, L, F, P, P, P]),
     "sa_norm_act": (I, [P, L, I, I, L, P, P, P, I, I, P, L, P, P, P, I, I, I, P, L, P]),
     "sa_conv3d_upcat_stat_parts": (L, [I, I, I]),
+    "sa_conv3d_wd_stat_parts": (L, [I, I, I, I]),
     "sa_conv3d_pointwise": (I, [P, I, I, I, I, I, P, P, I, F, P, P, P, I, P, P]),
     "sa_conv3d_pointwise_upcat": (I, [P, I, P, P, I, P, P, P, I, I, I, I, I, I, I, F, P, I, P, P, P]),
     "sa_instnorm_finalize": (I, [P, I, L, L, F, P, P, P]),

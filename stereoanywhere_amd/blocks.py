@@ -240,7 +240,7 @@ class Hourglass(nn.Module):
         r = ops.conv3d_wd(r, fw["d01_wd"], 16, slope=slope)                         # down_layers[0][1]
         down0 = gated(r, self.feature_atts[0], 1)
         r = ops.conv3d(down0, fw["d10"], 32, stride=2, slope=slope)                 # down_layers[1][0]
-        r = ops.conv3d(r, fw["d11"], 32, slope=slope)                               # down_layers[1][1]
+        r = ops.conv3d_wd(r, fw["d11_wd"], 32, slope=slope)                         # down_layers[1][1]
         down1 = gated(r, self.feature_atts[1], 2)
         # up-cat convs: the low-res branch is projected to the output channels, then upsampled
         r = ops.conv3d_pointwise_upcat(down0, down1, *fw["a10"], 16, slope=slope)  # agg_layers[1][0]
@@ -248,7 +248,8 @@ class Hourglass(nn.Module):
         r = ops.conv3d_wd(r, fw["a12_wd"], 16, slope=slope)                         # agg_layers[1][2]
         x = gated(r, self.feature_atts_up[1], 1)
         r = ops.conv3d_pointwise_upcat(orig, x, *fw["fa0"], 8, slope=slope)         # final_agg[0]
-        # 8-channel full-res and 16-channel half-res stride-1 convs: F(4,3) Winograd along D
+        # the stride-1 convs (8 channels at full, 16 at half, 32 at quarter resolution): F(4,3)
+        # Winograd along D
         r = ops.conv3d_wd(r, fw["fa1_wd"], 8, slope=slope)                          # final_agg[1]
         r = ops.conv3d_wd(r, fw["fa2_wd"], 8, slope=slope)                          # final_agg[2]
         r = gated(r, self.final_feature_atts_up, 0)
@@ -273,6 +274,7 @@ class Hourglass(nn.Module):
         wd = ops.conv3d_wd_weights
         return dict(
             fa1_wd=wd(fa1), fa2_wd=wd(fa2), cls_wd=wd(cls), d01_wd=wd(d01), a11_wd=wd(a11), a12_wd=wd(a12),
+            d11_wd=wd(k3(self.down_layers[1][1].conv.weight)),
             d00=k3(self.down_layers[0][0].conv.weight), d01=k3(self.down_layers[0][1].conv.weight),
             d10=k3(self.down_layers[1][0].conv.weight), d11=k3(self.down_layers[1][1].conv.weight),
             a10=pw(a10, slice(32, 48), slice(0, 32)),

@@ -57,14 +57,22 @@ __device__ __forceinline__ float xform(float v, const InXform &t, long bc, int d
   return v;
 }
 
+#ifndef SA_STATS_DPP
+#define SA_STATS_DPP 1   // the wave sums of block_stats on DPP (0: __shfl_xor butterfly)
+#endif
 // block partial sums of (x, x^2) over the tile for each of NC channels -> partial[bc][blk].
 // A thread's own values (at most TD of them) are summed in fp32, everything above in fp64.
 template <int NC>
 __device__ __forceinline__ void block_stats(const float (&s)[NC], const float (&q)[NC], double *red,
-                                            double *partial, long b, int nparts, int blk, int Cout) {
+                                            double *partial, long b, int nparts, int blk, int Cout, int c0 = 0) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
+#if SA_STATS_DPP
+    // (DPP: the ds_bpermute butterfly is 12 dependent LDS round trips per channel)
+    const double a = sa::wave_sum_dpp_lane63((double)s[c]), e = sa::wave_sum_dpp_lane63((double)q[c]);
+    if (lane == 63) {
+#else
     double a = (double)s[c], e = (double)q[c];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -72,6 +80,7 @@ __device__ __forceinline__ void block_stats(const float (&s)[NC], const float (&
       e += __shfl_xor(e, o);
     }
     if (lane == 0) {
+#endif
       red[(c * 4 + wv) * 2] = a;
       red[(c * 4 + wv) * 2 + 1] = e;
     }
@@ -84,7 +93,7 @@ __device__ __forceinline__ void block_stats(const float (&s)[NC], const float (&
       a += red[(c * 4 + w) * 2];
       e += red[(c * 4 + w) * 2 + 1];
     }
-    double *p = partial + ((b * Cout + c) * (long)nparts + blk) * 2;
+    double *p = partial + ((b * Cout + c0 + c) * (long)nparts + blk) * 2;
     p[0] = a;
     p[1] = e;
   }
@@ -400,14 +409,12 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const float *__restrict__ i
 //   DMA    = the next channel's raw columns fetched by LDS-DMA (buffer_load_dword ... lds) into
 //            a [6 rows][LD planes][64 lanes] staging area instead of 2 x LD VGPRs per thread; each
 //            wave reads back only its own lanes' words, after its own vmcnt(0) in commit
-#ifndef SA_WD_UNIF
-#define SA_WD_UNIF 0   // 1: uniform staging for the 16-channel convs (no wait on the prefetch in
-                       // their tap loop, but 570 -> 650 us: the duplicate loads and commits cost more)
-#endif
 #ifndef SA_WD_BUF
 #define SA_WD_BUF 0   // 1: the staging loads as buffer loads (diagnostic: 8 -> 8 then needs 175 VGPRs)
 #endif
-template <int CIN, int COUT, int NT, bool GATED, bool WL = false, bool PK = false, bool DMA = false>
+//   COTT   = the conv's total output channels when a block computes COUT of them (COUT = 16 of
+//            32: the 32-channel stride-1 conv as two channel halves, blockIdx.z = (b, D tile, half))
+template <int CIN, int COUT, int NT, bool GATED, bool WL = false, bool PK = false, bool DMA = false, int COTT = 0>
 __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict__ in, int D, int H, int W,
                                                         const float *__restrict__ wt, InXform tx,
                                                         float *__restrict__ out, double *__restrict__ partial,
@@ -420,12 +427,9 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
   constexpr int VW = sizeof(VT) / 4;
   static_assert(ROWP % 4 == 0, "row alignment");
   constexpr int CC = COUT < 8 ? COUT : 8;   // output channels per weight group (48 SGPRs)
-  // SA_WD_UNIF: every wave stages two columns (waves 2-3 a clamped duplicate of row 5, committed
-  // to a spare slab row), so fetch and commit have no wave-dependent branch
-  // (the 16-channel convs; with 8 channels it needs 170 VGPRs: 2 waves per SIMD instead of 3)
-  constexpr bool UNIF = SA_WD_UNIF && NT == 1;
-  constexpr int SLR = UNIF ? LH + 1 : LH;
-  __shared__ __attribute__((aligned(16))) float slab[2][SLR * ROWP];
+  constexpr int COT = COTT ? COTT : COUT, NS = COT / COUT;
+  static_assert(COT % COUT == 0 && (NS == 1 || !WL), "channel split");
+  __shared__ __attribute__((aligned(16))) float slab[2][LH * ROWP];
   __shared__ double red[COUT * 4 * 2];
   __shared__ float raw[DMA ? LH : 1][DMA ? LD : 1][64];
   constexpr int WPC = 54 * COUT, NWL = (WPC + 255) / 256;   // weights per input channel, per thread
@@ -452,7 +456,11 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int w0 = blockIdx.x * TWV, h0 = blockIdx.y * 4;
-  const int b = blockIdx.z / tilesD, d0 = (blockIdx.z % tilesD) * TD;
+  // (NS == 1: the unsigned blockIdx.z arithmetic of the unsplit kernel, whose tap-loop schedule
+  // the 16-channel conv is sensitive to: 575 against 640 us with the signed form)
+  const unsigned zc = blockIdx.z / NS;
+  const int co0 = NS == 1 ? 0 : (int)(blockIdx.z % NS) * COUT;
+  const int b = zc / tilesD, d0 = (zc % tilesD) * TD;
   const int hw = H * W;
   const int wl = w0 - 1 + lane;
   const bool wok = wl >= 0 && wl < W;
@@ -479,8 +487,8 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
 #pragma unroll
     for (int k = 0; k < NCOL; ++k) {
       const int hh = wv + 4 * k;
-      if (UNIF || (NT == 2 && k == 0) || hh < LH) {   // (row wv < 4 always exists)
-        const int hc = min(max(h0 - 1 + min(hh, LH - 1), 0), H - 1);
+      if ((NT == 2 && k == 0) || hh < LH) {   // (row wv < 4 always exists)
+        const int hc = min(max(h0 - 1 + hh, 0), H - 1);
         const float *colp = src + hc * W + wcl;
 #pragma unroll
         for (int j = 0; j < LD; ++j) {
@@ -526,7 +534,7 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
 #pragma unroll
     for (int k = 0; k < NCOL; ++k) {
       const int hh = wv + 4 * k;
-      if (UNIF || (NT == 2 && k == 0) || hh < LH) {
+      if ((NT == 2 && k == 0) || hh < LH) {
         const int h = h0 - 1 + hh;
         const bool cok = wok && h >= 0 && h < H;
         float x[LD];
@@ -544,7 +552,7 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
 #pragma unroll
         for (int t = 0; t < NT; ++t)
           bt6(x[4 * t], x[4 * t + 1], x[4 * t + 2], x[4 * t + 3], x[4 * t + 4], x[4 * t + 5], o + 6 * t);
-        VT *dst = reinterpret_cast<VT *>(slab[buf] + min(hh, SLR - 1) * ROWP + lane * NP);
+        VT *dst = reinterpret_cast<VT *>(slab[buf] + hh * ROWP + lane * NP);
 #pragma unroll
         for (int q = 0; q < NP / VW; ++q) {
           VT v;
@@ -591,7 +599,7 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
     // lanes 62-63 (no output column) read lane 61's columns: lane + kw stays inside the 64
     // staged columns of the row
     const float *lb = slab[buf] + wv * ROWP + min(lane, TWV - 1) * NP;
-    const float *wc = WL ? wsl[buf] : wt + (long)ci * 9 * 6 * COUT;
+    const float *wc = WL ? wsl[buf] : wt + (long)ci * 9 * 6 * COT + (NS == 1 ? 0 : co0);
     // the kw loop unrolled for the 16-channel convs and the classifier pair (the scalar weight
     // loads of the next kw then overlap this one's FMAs: 711 -> 567 and 568 -> 506 us), rolled
     // for 8 -> 8 (unrolled it measured 1057 -> 1310 us: SGPR pressure of 48 weights per kw;
@@ -609,7 +617,7 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
 #pragma unroll
           for (int e = 0; e < VW; ++e) X[VW * q + e] = reinterpret_cast<const float *>(&v)[e];
         }
-        const float *wp = wc + (kh * 3 + kw) * 6 * COUT;
+        const float *wp = wc + (kh * 3 + kw) * 6 * COT;
 #pragma unroll
         for (int cg = 0; cg < COUT / CC; ++cg) {
           if (cg) __builtin_amdgcn_sched_barrier(0);   // one channel group's weights live at a time
@@ -617,7 +625,7 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
           for (int p = 0; p < 6; ++p)
 #pragma unroll
             for (int c = cg * CC; c < cg * CC + CC; ++c) {
-              const float wv_ = wp[p * COUT + c];
+              const float wv_ = wp[p * COT + c];
               if constexpr (PK) {
                 const f2 xp2 = f2{X[2 * p], X[2 * p + 1]};
                 M2[p][c] = __builtin_elementwise_fma(xp2, f2{wv_, wv_}, M2[p][c]);
@@ -654,7 +662,7 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
       for (int i = 0; i < 4; ++i) {
         const int d = d0 + 4 * t + i;
         if (ok && d < D) {
-          out[(((long)b * COUT + c) * D + d) * (long)hw + (long)h * W + w] = o[i];
+          out[(((long)b * COT + co0 + c) * D + d) * (long)hw + (long)h * W + w] = o[i];
           s[c] += o[i];
           q[c] += o[i] * o[i];
         }
@@ -662,8 +670,8 @@ __global__ __launch_bounds__(256) void conv3d_wd_kernel(const float *__restrict_
     }
   if (partial) {
     const int nparts = gridDim.x * gridDim.y * tilesD;
-    const int blk = (blockIdx.z % tilesD) * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x;
-    block_stats<COUT>(s, q, red, partial, b, nparts, blk, COUT);
+    const int blk = (zc % tilesD) * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x;
+    block_stats<COUT>(s, q, red, partial, b, nparts, blk, COT, co0);
   }
 }
 
@@ -916,6 +924,10 @@ extern "C" long sa_conv3d_stat_parts(int Cout, int stride, int Do, int Ho, int W
   return (long)g.x * g.y * g.z;
 }
 
+extern "C" long sa_conv3d_wd_stat_parts(int Cout, int D, int H, int W) {
+  return sa_conv3d_stat_parts(Cout < 16 ? Cout : 16, 1, D, H, W);
+}
+
 extern "C" long sa_conv3d_upcat_stat_parts(int D, int H, int W) {
   int tilesD;
   dim3 g = upcat_grid(1, D, H, W, tilesD);
@@ -973,11 +985,11 @@ extern "C" int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W
   SA_REQUIRE((in_mean == nullptr) == (in_rstd == nullptr), "sa_conv3d_wd: mean and rstd go together");
   SA_REQUIRE((gate_l == nullptr) == (gate_r == nullptr), "sa_conv3d_wd: both gate maps or none");
   SA_REQUIRE((long)D * H * W * 4 < (1L << 31), "sa_conv3d_wd: a channel volume must hold < 2^31 bytes");
-  SA_REQUIRE((Cin == 8 && (Cout == 8 || Cout == 2)) || (Cin == 16 && Cout == 16),
-             "sa_conv3d_wd: built for 8 -> 8, 8 -> 2 and 16 -> 16 (got %d -> %d)", Cin, Cout);
-  // the same tiling as sa_conv3d's for these shapes (8 or 4 planes x 4 rows x 62 columns): the
-  // same statistic parts
-  const ConvGeo geo = conv_geo(Cout, 1);
+  SA_REQUIRE((Cin == 8 && (Cout == 8 || Cout == 2)) || (Cin == 16 && Cout == 16) || (Cin == 32 && Cout == 32),
+             "sa_conv3d_wd: built for 8 -> 8, 8 -> 2, 16 -> 16 and 32 -> 32 (got %d -> %d)", Cin, Cout);
+  // the tiling of sa_conv3d's for 8 and 16 outputs (8 or 4 planes x 4 rows x 62 columns): the
+  // statistic parts of sa_conv3d_wd_stat_parts (= sa_conv3d_stat_parts for those shapes)
+  const ConvGeo geo = conv_geo(Cout < 16 ? Cout : 16, 1);
   SA_REQUIRE(geo.td == (Cin == 8 ? 8 : 4) && geo.tw == 64 && geo.th == 4, "sa_conv3d_wd: tiling");
   int tilesD;
   dim3 grid = conv_grid(B, D, H, W, geo, tilesD);
@@ -1007,6 +1019,12 @@ extern "C" int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W
   SA_WD(16, 16, 1, false)
   SA_WD(16, 16, 1, true)
 #undef SA_WD
+  if (Cin == 32 && Cout == 32 && gate_l == nullptr) {   // two 16-channel halves per tile
+    grid.z *= 2;
+    conv3d_wd_kernel<32, 16, 1, false, false, false, false, 32><<<grid, 256, 0, s>>>(in, D, H, W, weight_wd, tx, out,
+                                                                                  stats_partial, tilesD);
+    return sa::check_launch("sa_conv3d_wd");
+  }
   sa::set_error("sa_conv3d_wd: no kernel for %d -> %d", Cin, Cout);
   return SA_E_ARG;
 }

@@ -60,4 +60,49 @@ __device__ __forceinline__ float sigmoidf_fast(float x) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-x * 1.44269504088896341f));
 }
 
+// Wave-wide reductions on DPP lane moves (quad_perm [1,0,3,2] and [2,3,0,1], row_half_mirror,
+// row_mirror, then row_bcast:15 / row_bcast:31 carry the 16-lane row totals up to lane 63).
+// __shfl_xor compiles to ds_bpermute: an LDS round trip per butterfly step.  Lanes of masked
+// rows receive the identity.  The total is valid in lane 63 (wave_*_dpp return it wave-uniform).
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_f32(float identity, float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, identity),
+                                                               __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, false));
+}
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp_f64(double v) {   // identity 0.0 (both halves 0)
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, ROW_MASK, 0xF, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, ROW_MASK, 0xF, false);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_f32<0xB1>(-INFINITY, v));
+  v = fmaxf(v, dpp_f32<0x4E>(-INFINITY, v));
+  v = fmaxf(v, dpp_f32<0x141>(-INFINITY, v));
+  v = fmaxf(v, dpp_f32<0x140>(-INFINITY, v));
+  v = fmaxf(v, dpp_f32<0x142, 0xA>(-INFINITY, v));
+  v = fmaxf(v, dpp_f32<0x143, 0xC>(-INFINITY, v));
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f32<0xB1>(0.0f, v);
+  v += dpp_f32<0x4E>(0.0f, v);
+  v += dpp_f32<0x141>(0.0f, v);
+  v += dpp_f32<0x140>(0.0f, v);
+  v += dpp_f32<0x142, 0xA>(0.0f, v);
+  v += dpp_f32<0x143, 0xC>(0.0f, v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+// fp64 sum; the total is in lane 63 only
+__device__ __forceinline__ double wave_sum_dpp_lane63(double v) {
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0x141>(v);
+  v += dpp_f64<0x140>(v);
+  v += dpp_f64<0x142, 0xA>(v);
+  v += dpp_f64<0x143, 0xC>(v);
+  return v;
+}
+
 }  // namespace sa

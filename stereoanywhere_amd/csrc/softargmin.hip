@@ -29,34 +29,10 @@ struct SGeo {
   float log2W1, log2W2;  // math.log2(W) of the reference (double), rounded once to fp32
 };
 
-// Wave reductions on DPP (VALU lane moves: quad_perm [1,0,3,2] and [2,3,0,1], row_half_mirror,
-// row_mirror, then row_bcast:15 / row_bcast:31 carry the row totals up to lane 63, read back as
-// a wave-uniform value).  __shfl_xor compiled to ds_bpermute, an LDS round trip per step: 18
-// dependent ones per row of the slice kernels, which made them latency-bound (the loads alone
-// take a quarter of their time).  Identity-filled lanes (masked rows) keep their value.
-template <int CTRL, int ROW_MASK = 0xF>
-__device__ __forceinline__ float dppf(float identity, float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, identity),
-                                                               __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, false));
-}
-__device__ __forceinline__ float wave_max(float v) {
-  v = fmaxf(v, dppf<0xB1>(-INFINITY, v));
-  v = fmaxf(v, dppf<0x4E>(-INFINITY, v));
-  v = fmaxf(v, dppf<0x141>(-INFINITY, v));
-  v = fmaxf(v, dppf<0x140>(-INFINITY, v));
-  v = fmaxf(v, dppf<0x142, 0xA>(-INFINITY, v));
-  v = fmaxf(v, dppf<0x143, 0xC>(-INFINITY, v));
-  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
-}
-__device__ __forceinline__ float wave_sum(float v) {
-  v += dppf<0xB1>(0.0f, v);
-  v += dppf<0x4E>(0.0f, v);
-  v += dppf<0x141>(0.0f, v);
-  v += dppf<0x140>(0.0f, v);
-  v += dppf<0x142, 0xA>(0.0f, v);
-  v += dppf<0x143, 0xC>(0.0f, v);
-  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
-}
+// wave reductions on DPP (sa_common.h): __shfl_xor compiled to ds_bpermute, an LDS round trip
+// per step, 18 dependent ones per row of the slice kernels (latency-bound: 156 -> 124 us at cfg2)
+__device__ __forceinline__ float wave_max(float v) { return sa::wave_max_dpp(v); }
+__device__ __forceinline__ float wave_sum(float v) { return sa::wave_sum_dpp(v); }
 
 // Reduce along an axis of length n with element stride es, output index o of `nout`
 // outputs along the other axis with element stride os.  LEFT: output is j, reduce k.

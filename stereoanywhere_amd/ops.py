@@ -512,13 +512,14 @@ def conv3d_wd_weights(w_t: torch.Tensor) -> torch.Tensor:
 
 
 def conv3d_wd(x: "VolAct", w_wd: torch.Tensor, cout: int, slope: float = 0.01, stats: bool = True) -> "VolAct":
-    """ops.conv3d at stride 1 for 8 input channels (-> 8 or 2) or 16 -> 16 on the F(4,3)-along-D kernel;
-    w_wd from conv3d_wd_weights.  The input must carry an InstanceNorm + LeakyReLU (+ gate)."""
+    """ops.conv3d at stride 1 for 8 input channels (-> 8 or 2), 16 -> 16 or 32 -> 32 (no gate) on the
+    F(4,3)-along-D kernel; w_wd from conv3d_wd_weights.  The input must carry an InstanceNorm +
+    LeakyReLU (+ gate)."""
     _check(x.raw, "x")
     _check(w_wd, "w_wd")
     B, Cin, D, H, W = x.raw.shape
     out = torch.empty((B, cout, D, H, W), device=x.raw.device, dtype=torch.float32)
-    parts = conv3d_stat_parts(cout, 1, D, H, W)
+    parts = int(N.lib().sa_conv3d_wd_stat_parts(cout, D, H, W))
     partial = torch.empty((B * cout * parts * 2,), device=out.device, dtype=torch.float64) if stats else None
     a = x.args()
     N.call("sa_conv3d_wd", x.raw.data_ptr(), B, Cin, D, H, W, w_wd.data_ptr(), cout, a[0], a[1], a[2], slope,

@@ -557,7 +557,8 @@ def test_fused_hourglass_on_onehot_records_matches_torch():
 
 @pytest.mark.parametrize("cin,cout,gated,shape", [(8, 8, False, (2, 20, 12, 70)), (8, 2, True, (1, 13, 9, 130)),
                                                   (8, 8, True, (1, 8, 5, 64)), (8, 2, False, (2, 17, 6, 30)),
-                                                  (16, 16, False, (2, 15, 10, 66)), (16, 16, True, (1, 6, 7, 20))])
+                                                  (16, 16, False, (2, 15, 10, 66)), (16, 16, True, (1, 6, 7, 20)),
+                                                  (32, 32, False, (2, 9, 6, 40))])
 def test_conv3d_wd_matches_direct(cin, cout, gated, shape):
     """The F(4,3)-along-D conv (sa_conv3d_wd) against the direct fused conv (sa_conv3d) on the
     same transformed input: ragged D (not a multiple of the 8-plane tile), H, W edges."""
@@ -571,7 +572,8 @@ def test_conv3d_wd_matches_direct(cin, cout, gated, shape):
     w = g(rng.standard_normal((cin, 27, cout)) * 0.2)
     a = ops.conv3d_wd(v, ops.conv3d_wd_weights(w), cout, slope=0.01)
     b = ops.conv3d(v, w, cout, slope=0.01)
-    torch.testing.assert_close(a.raw, b.raw, atol=2e-5, rtol=1e-5)
+    # (Winograd along D rounds differently from the direct sum: the error grows with Cin)
+    torch.testing.assert_close(a.raw, b.raw, atol=2e-5 * max(1, cin // 16), rtol=1e-5)
     # the other variants (1: LDS weights, 2: paired D-tiles, 3: + LDS-DMA prefetch) compute the
     # same products in the same order (the paired ones may group an FMA differently: last bit)
     for variant in (1, 2, 3):
