@@ -68,6 +68,9 @@ def step_costs(B: int, H4: int, W4: int, iters: int, C: int = 256):
         # per pixel: 2 volumes x 4 levels x (2r+2) cells read, coords read, and (convc1 fused)
         # 2 x 64 channels of relu(convc1(taps)) written
         "corr_lookup": ("GB/s", iters * px * (2 * 4 * 10 * 4 + 4 + 2 * 64 * 4)),
+        # the sheared copies of the two pyramids (large volumes only): every level cell read
+        # from the row layout and written once
+        "corr_shear": ("GB/s", 2 * 2 * px * sum(lv) * 4),
         "mono_masked_volume": ("GB/s", 8 * vol * 4 + px * 2 * 4 * 4),
         # two aggregated volumes read once, four maps written
         "softargmin_conf": ("GB/s", 2 * vol * 4 + 4 * px * 4),

@@ -198,11 +198,16 @@ int sa_corr_lookup_conv1x1(const float *pyramid_a, const float *pyramid_b, int W
                            int num_levels, int radius, const float *coords_x, long coords_bstride,
                            int B, int H, int W1, const float *weight_kc, const float *bias, int Cout,
                            float *out, void *stream);
-/* a10 on a disparity-sheared copy of the pyramid (csrc/corr_shear.hip): level l of image row
- * (b, h) as S_l[e][j] = C_l[j][(j >> l) - e + W_l - 1], e in [0, W_l + ((W1 - 1) >> l)), cells
- * outside [0, W_l) stored as 0, levels back to back in a slice of sa_shear_slice_size floats
- * per image row: a wave's neighbouring pixels then read neighbouring addresses.
+/* a10 on a disparity-sheared pyramid (csrc/corr_shear.hip): level l of image row (b, h) as
+ * S_l[e][j] = C_l[j][(j >> l) - e + W_l - 1], e in [0, W_l + ((W1 - 1) >> l)), levels back to back
+ * in a slice of sa_shear_slice_size floats per image row: a wave's neighbouring pixels then read
+ * neighbouring addresses.  Cells whose k = (j >> l) - e + W_l - 1 falls outside [0, W_l) are not
+ * written (the lookup's tap test gives the reference's zero padding there without using them).
  *   sa_corr_pyramid_shear: the row-layout pyramid [B*H*W1][row_stride] -> sheared [B*H][slice]
+ *   sa_corr_volume_pyramid_sheared: sa_corr_volume_pyramid written sheared (C % 16 == 0, W1 and
+ *     W2 % 4 == 0, 16-byte aligned feature maps under 2 GiB; the same cell values)
+ *   sa_corr_pyramid_from_volume_strided_sheared: sa_corr_pyramid_from_volume_strided written
+ *     sheared
  *   sa_corr_lookup_conv1x1_sheared: sa_corr_lookup_conv1x1 on sheared pyramids (same taps,
  *     same arithmetic; 4 levels, radius 4, Cout 64). */
 /* convc1 of the fused lookups (both layouts) on the VALU (0, default) or fp32 MFMA (1, measured
@@ -213,6 +218,13 @@ long sa_shear_slice_size(int W1, int W2, int num_levels);
 long sa_shear_level_offset(int W1, int W2, int num_levels, int level);
 int sa_corr_pyramid_shear(const float *pyramid, long row_stride, int B, int H, int W1, int W2,
                           int num_levels, float *sheared, void *stream);
+int sa_corr_volume_pyramid_sheared(const float *fmap2, const float *fmap3, int B, int C, int H, int W1,
+                                   int W2, float sqrt_c, const float *trunc_disp,
+                                   const float *trunc_conf, float atten, int num_levels,
+                                   float *sheared, void *stream);
+int sa_corr_pyramid_from_volume_strided_sheared(const float *volume, int B, int H, int W1, int W2,
+                                                long sb, long sh, long sk, int num_levels,
+                                                float *sheared, void *stream);
 int sa_corr_lookup_conv1x1_sheared(const float *sheared_a, const float *sheared_b, int W2,
                                    int num_levels, int radius, const float *coords_x,
                                    long coords_bstride, int B, int H, int W1,
@@ -442,7 +454,7 @@ int sa_norm_act(const float *x, long x_bs, int B, int C, long hw, const float *m
 enum {
   SA_K_CORR_PYRAMID = 0, SA_K_LOOKUP, SA_K_MONO_VOLUME, SA_K_SOFTARGMIN, SA_K_LSQ,
   SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_NORM, SA_K_CONV2D, SA_K_CONV_DIRECT,
-  SA_K_CONV2D_W4, SA_K_COUNT
+  SA_K_CONV2D_W4, SA_K_SHEAR, SA_K_COUNT
 };
 int sa_timing_enable(int on);
 int sa_timing_read(int kernel_id, double *total_ms, long *count);

@@ -3,7 +3,8 @@
 the bench shape (B=4, 544x960, 22 iterations, one stream): for each launch position (in order
 within the forward) the mean time over the GRU iterations, the problems it carries (Cin->Cout
 @HxW, gate mode), its workgroups (rounds of 256 CUs) and executed Winograd TFLOP/s.
-usage: python scripts/wino4_launches.py [reps]"""
+usage: python scripts/wino4_launches.py [reps] [--shape B H W ITERS]   (e.g. --shape 3 1024 672 32: the
+cfg3 tiles, --shape 25 896 1120 32: the cfg5 booster batch)"""
 import collections
 import os
 import sys
@@ -17,13 +18,18 @@ from stereoanywhere_amd.model import StereoAnywhere  # noqa: E402
 
 
 def main():
-    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 2
+    B, H, W, iters = 4, 544, 960, 22
+    if "--shape" in sys.argv:
+        i = sys.argv.index("--shape")
+        B, H, W, iters = (int(v) for v in sys.argv[i + 1:i + 5])
     dev = torch.device("cuda", 0)
     model = StereoAnywhere(dict(bench.PUBLISHED)).eval()
     synth.load_seeded_weights(model, 0)
     model = model.to(dev)
     model.stream_overlap = False
-    inp = bench.make_inputs(4, 540, 960, 544, 960, 192.0, seed0=1, device=dev)
+    Hr, Wr = (540, 960) if (H, W) == (544, 960) else (H, W)
+    inp = bench.make_inputs(B, Hr, Wr, H, W, W / 5.0, seed0=1, device=dev)
     x = (inp["left"], inp["right"], inp["mono_left"], inp["mono_right"])
     rec = []
     orig = ops.conv2d_k3_multi
@@ -47,11 +53,11 @@ def main():
         return r
     ops.conv2d_k3_multi = wrap
     with torch.no_grad():
-        model(*x, iters=22, test_mode=True)
+        model(*x, iters=iters, test_mode=True)
         torch.cuda.synchronize()
         rec.clear()
         for _ in range(reps):
-            model(*x, iters=22, test_mode=True)
+            model(*x, iters=iters, test_mode=True)
         torch.cuda.synchronize()
     per = len(rec) // reps
     agg = collections.OrderedDict()

@@ -51,6 +51,8 @@ SIGNATURES = {
     "sa_shear_slice_size": (L, [I, I, I]),
     "sa_shear_level_offset": (L, [I, I, I, I]),
     "sa_corr_pyramid_shear": (I, [P, L, I, I, I, I, I, P, P]),
+    "sa_corr_volume_pyramid_sheared": (I, [P, P, I, I, I, I, I, F, P, P, F, I, P, P]),
+    "sa_corr_pyramid_from_volume_strided_sheared": (I, [P, I, I, I, I, L, L, L, I, P, P]),
     "sa_corr_lookup_conv1x1_sheared": (I, [P, P, I, I, I, P, L, I, I, I, P, P, I, P, P]),
     "sa_mono_normals": (I, [P, I, I, I, F, P, P]),
     "sa_mono_masked_volume": (I, [P, P, P, P, I, I, I, I, I, F, P, P]),
@@ -111,7 +113,7 @@ SIGNATURES = {
 KERNEL_IDS = {
     "corr_volume_pyramid": 0, "corr_lookup": 1, "mono_masked_volume": 2, "softargmin_conf": 3,
     "weighted_lsq": 4, "gru_zr": 5, "gru_out": 6, "convex_upsample": 7, "misc": 8, "conv3d_fused": 9,
-    "norm_act": 10, "conv2d_wino": 11, "conv2d_direct": 12, "conv2d_wino4": 13,
+    "norm_act": 10, "conv2d_wino": 11, "conv2d_direct": 12, "conv2d_wino4": 13, "corr_shear": 14,
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -64,10 +64,19 @@ class HipCorrBlock1D:
     @classmethod
     def from_features(cls, fmap2: torch.Tensor, fmap3: torch.Tensor, num_levels: int = 4, radius: int = 4,
                       trunc_disp: Optional[torch.Tensor] = None, trunc_conf: Optional[torch.Tensor] = None,
-                      attenuation: float = 0.9, pad: Sequence[int] = (0, 0)) -> "HipCorrBlock1D":
-        """corr -> x truncation volume -> pyramid fused (stereoanywhere.py:135, 201-205, 253-255)."""
+                      attenuation: float = 0.9, pad: Sequence[int] = (0, 0),
+                      sheared: bool = False) -> "HipCorrBlock1D":
+        """corr -> x truncation volume -> pyramid fused (stereoanywhere.py:135, 201-205, 253-255).
+        sheared: write the disparity-sheared layout only (ops.corr_volume_pyramid_sheared; the
+        row layout where that kernel does not apply)."""
         B, _, H, W1 = fmap2.shape
         W2 = fmap3.shape[3]
+        if sheared:
+            sh = ops.corr_volume_pyramid_sheared(fmap2, fmap3, num_levels, trunc_disp, trunc_conf, attenuation)
+            if sh is not None:
+                blk = cls(None, num_levels, radius, pad, _shape=(B, H, W1, W2))
+                blk.sheared = sh
+                return blk
         pyr = ops.corr_volume_pyramid(fmap2, fmap3, num_levels, trunc_disp, trunc_conf, attenuation)
         return cls(None, num_levels, radius, pad, _pyramid=pyr, _shape=(B, H, W1, W2))
 

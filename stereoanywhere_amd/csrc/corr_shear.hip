@@ -188,7 +188,7 @@ extern "C" int sa_corr_pyramid_shear(const float *pyramid, long row_stride, int 
   SA_REQUIRE((long)B * H <= 65535, "sa_corr_pyramid_shear: more than 65535 image rows");
   const ShGeo g = shear_geo(W1, W2, num_levels);
   hipStream_t s = sa::as_stream(stream);
-  sa::TimingScope ts(SA_K_LOOKUP, s);
+  sa::TimingScope ts(SA_K_SHEAR, s);
   SA_REQUIRE((long)SH_J * (W2 + 1) * 4 <= 64 * 1024, "sa_corr_pyramid_shear: W2 %d too wide for the LDS tile", W2);
   for (int l = 0; l < num_levels; ++l) {
     const dim3 grid((unsigned)((W1 + SH_J - 1) / SH_J), 1u, (unsigned)(B * H));

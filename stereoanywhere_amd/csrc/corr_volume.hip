@@ -192,12 +192,51 @@ __device__ __forceinline__ void v2_dma16(__amdgpu_buffer_rsrc_t r, float *lds, i
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)lds, 16, voff, 0, 0, 0);
 }
 
-template <bool TRUNC, bool POW2>
+// The disparity-sheared output (corr_shear.hip): per image row (b, h) a slice of `slice` floats,
+// level l at off[l] as rows[l] x W1 floats, S_l[e][j] = C_l[j][(j >> l) - e + W_l - 1]
+struct ShOut {
+  float *base;
+  long slice;
+  long off[4];
+  int rows[4];
+};
+
+// Level l of a 64-pixel (j) x (64 >> l)-cell (k) tile staged in LDS as T_l[jl][kl] (pitch 64 >> l,
+// the levels back to back: T_l at 64 * (128 - (128 >> l))... see tile_off), written as its
+// sheared rows: row e of the level takes, at column j, the cell kk = (j >> l) - e + W_l - 1 when
+// it lies in this tile and in the level; the wave's 64 lanes are the tile's 64 pixels, so each row
+// segment is one coalesced store.  The LDS reads T_l[jl][(jl >> l) - e'] are conflict-free (the
+// lane's address is jl (64 >> l) + (jl >> l), distinct mod 64 banks).  Cells of the level outside
+// [0, W_l) are not written (the sheared lookup's tap test never uses them).
+__device__ __forceinline__ int sh_tile_off(int l) { return 64 * (128 - (128 >> l)); }   // 0, 4096, 6144, 7168
+
+__device__ __forceinline__ void sh_write_tile(const ShOut &so, long slice_idx, const float *T, int nlev, const int *wid,
+                                              int W1, int j0, int k0l0, int wv, int nw, int lane) {
+  const int j = j0 + lane;
+  float *sl = so.base + slice_idx * so.slice;
+  for (int l = 0; l < nlev; ++l) {
+    const int Wl = wid[l], NK = 64 >> l, K = k0l0 >> l;
+    const int El = so.rows[l];
+    int emin = (j0 >> l) - (K + NK - 1) + Wl - 1, emax = ((j0 + 63) >> l) - K + Wl - 1;
+    emin = max(emin, 0);
+    emax = min(emax, El - 1);
+    const float *Tl = T + sh_tile_off(l) + lane * NK;
+    float *dst = sl + so.off[l] + j;
+    const int jsh = j >> l;
+    for (int e = emin + wv; e <= emax; e += nw) {
+      const int kk = jsh - e + Wl - 1;
+      if (j < W1 && kk >= K && kk < K + NK && kk < Wl) dst[(long)e * W1] = Tl[kk - K];
+    }
+  }
+}
+
+template <bool TRUNC, bool POW2, bool SHEAR = false>
 __global__ __launch_bounds__(256, 4) void corr_pyramid_v2_kernel(const float *__restrict__ f2, const float *__restrict__ f3,
                                                               Geo g, int jblocks, int kblocks, int kstep, float sqrt_c,
                                                               float inv_c, const float *__restrict__ tdisp,
                                                               const float *__restrict__ tconf, float atten,
-                                                              float *__restrict__ pyr, int f2_bytes, int f3_bytes) {
+                                                              float *__restrict__ pyr, int f2_bytes, int f3_bytes,
+                                                              ShOut so) {
   __shared__ __attribute__((aligned(16))) float smem[2 * V2_BUF];
   const unsigned nwg = gridDim.x;
   const unsigned wid = sa::xcd_remap(blockIdx.x, nwg);
@@ -267,6 +306,17 @@ __global__ __launch_bounds__(256, 4) void corr_pyramid_v2_kernel(const float *__
 
   // ---------------------------------------------------------------- epilogue
   const int n = lane & 15;
+  auto cell = [&](int gg, int i, int t, int j, int P, float dji, float mji) __attribute__((always_inline)) {
+    float x = POW2 ? acc[gg][t][i] * inv_c : acc[gg][t][i] / sqrt_c;
+    if (TRUNC) {
+      const float center = (float)j - dji;
+      const float tv = center - (float)(P + t);
+      const float s = sa::sigmoidf_fast(tv);
+      const float T = 1.0f * (1.0f - mji) + mji * (s * (1.0f - atten) + atten);
+      x = T * x;
+    }
+    return x;
+  };
   float dj[4], mj[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -278,6 +328,35 @@ __global__ __launch_bounds__(256, 4) void corr_pyramid_v2_kernel(const float *__
       mj[i] = tconf[pix];
     }
   }
+  if constexpr (SHEAR) {
+    // the (row, 64-cell group) tiles through LDS (the panels are free after this barrier), then
+    // written as sheared rows
+    float *T = smem;
+    static_assert(64 * 120 <= 2 * V2_BUF, "sheared tiles fit the panel buffers");
+#pragma unroll 1
+    for (int gg = 0; gg < ngroups; ++gg) {
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int jl = 16 * w + 4 * (lane >> 4) + i, j = j0 + jl;
+        const int P = k0 + 64 * gg + 4 * n;
+        float v[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = cell(gg, i, t, j, P, dj[i], mj[i]);
+        *reinterpret_cast<f32x4v *>(T + jl * 64 + 4 * n) = f32x4v{v[0], v[1], v[2], v[3]};
+        const float l1a = (v[0] + v[1]) * 0.5f, l1b = (v[2] + v[3]) * 0.5f;
+        T[sh_tile_off(1) + jl * 32 + 2 * n] = l1a;
+        T[sh_tile_off(1) + jl * 32 + 2 * n + 1] = l1b;
+        const float l2 = (l1a + l1b) * 0.5f;
+        T[sh_tile_off(2) + jl * 16 + n] = l2;
+        const float l3 = (l2 + __shfl_xor(l2, 1)) * 0.5f;
+        if ((n & 1) == 0) T[sh_tile_off(3) + jl * 8 + n / 2] = l3;
+      }
+      __syncthreads();
+      sh_write_tile(so, (long)b * g.H + h, T, g.nlev, g.wid, g.W1, j0, k0 + 64 * gg, w, 4, lane);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int j = j0 + 16 * w + 4 * (lane >> 4) + i;
@@ -288,17 +367,7 @@ __global__ __launch_bounds__(256, 4) void corr_pyramid_v2_kernel(const float *__
       const int P = k0 + 64 * gg + 4 * n;
       float v[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        float x = POW2 ? acc[gg][t][i] * inv_c : acc[gg][t][i] / sqrt_c;
-        if (TRUNC) {
-          const float center = (float)j - dj[i];
-          const float tv = center - (float)(P + t);
-          const float s = sa::sigmoidf_fast(tv);
-          const float T = 1.0f * (1.0f - mj[i]) + mj[i] * (s * (1.0f - atten) + atten);
-          x = T * x;
-        }
-        v[t] = x;
-      }
+      for (int t = 0; t < 4; ++t) v[t] = cell(gg, i, t, j, P, dj[i], mj[i]);
       if (P >= kend) continue;   // (kend - k0 is a multiple of 8 unless kend == W2)
       if (jok) {
         if (P + 3 < kend) {
@@ -375,9 +444,13 @@ __global__ __launch_bounds__(256) void pyramid_from_volume_kernel(const float *_
 // (a pair / quad / octet of level-0 cells) lies inside one chunk.
 constexpr int PT_J = 64, PT_CHUNK = 256, PT_PITCH = PT_CHUNK + 4;   // 16-byte aligned rows
 
+// SHEAR: the chunk's cells go out as sheared rows (ShOut) instead: row e of level l takes at
+// pixel j (a lane per pixel of the block) the cell kk = (j >> l) - e + W_l - 1 when it lies in
+// this chunk, formed from the staged level-0 cells with the row path's averaging order.
+template <bool SHEAR = false>
 __global__ __launch_bounds__(256) void pyramid_from_strided_kernel(const float *__restrict__ vol, long sb, long sh,
                                                                    long sk, int H, int W1, int W2, Geo g,
-                                                                   float *__restrict__ pyr) {
+                                                                   float *__restrict__ pyr, ShOut so) {
   __shared__ __attribute__((aligned(16))) float tile[PT_J * PT_PITCH];
   const int j0 = blockIdx.x * PT_J, h = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -409,6 +482,47 @@ __global__ __launch_bounds__(256) void pyramid_from_strided_kernel(const float *
       tile[(jq + 3) * PT_PITCH + (k ^ swz(jq + 3))] = q[i].w;
     }
     __syncthreads();
+    if constexpr (SHEAR) {
+      const int jj = lane, j = j0 + jj;
+      const float *trow = tile + jj * PT_PITCH;
+      const int sw = swz(jj);
+      auto c0v = [&](int k) __attribute__((always_inline)) { return trow[(k - c0) ^ sw]; };
+      float *sl = so.base + ((long)b * H + h) * so.slice;
+      for (int l = 0; l < g.nlev; ++l) {
+        const int Wl = g.wid[l], K = c0 >> l, KE = min((c0 + cw) >> l, Wl);
+        int emin = (j0 >> l) - (KE - 1) + Wl - 1, emax = ((j0 + PT_J - 1) >> l) - K + Wl - 1;
+        emin = max(emin, 0);
+        emax = min(emax, so.rows[l] - 1);
+        float *dst = sl + so.off[l] + j;
+        const int jsh = j >> l;
+        for (int e = emin + wv; e <= emax; e += 4) {
+          const int kk = jsh - e + Wl - 1;
+          if (j < W1 && kk >= K && kk < KE) {
+            const int k = kk << l;
+            float x;
+            if (l == 0) {
+              x = c0v(k);
+            } else {
+              // (v0 + v1) / 2, then pairs of those, as the row path's l1 / l2 / l3
+              float a[8];
+#pragma unroll
+              for (int q = 0; q < 8; ++q) a[q] = q < (1 << l) ? c0v(k + q) : 0.0f;
+              float b1[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) b1[q] = (a[2 * q] + a[2 * q + 1]) * 0.5f;
+              if (l == 1) {
+                x = b1[0];
+              } else {
+                const float c2a = (b1[0] + b1[1]) * 0.5f, c2b = (b1[2] + b1[3]) * 0.5f;
+                x = l == 2 ? c2a : (c2a + c2b) * 0.5f;
+              }
+            }
+            dst[(long)e * W1] = x;
+          }
+        }
+      }
+      continue;
+    }
     // a lane per 4 consecutive cells: level 0 as one float4, levels 1-2 in registers, level 3
     // from the neighbour lane
     const int lb = 4 * lane, base = c0 + lb;
@@ -464,10 +578,19 @@ Geo make_geo(int C, int H, int W1, int W2, int nlev, long rs) {
 
 }  // namespace
 
-extern "C" int sa_corr_volume_pyramid(const float *fmap2, const float *fmap3, int B, int C, int H,
-                                      int W1, int W2, float sqrt_c, const float *trunc_disp,
-                                      const float *trunc_conf, float atten, int num_levels,
-                                      float *pyramid, long row_stride, void *stream) {
+namespace {
+ShOut make_shout(float *sheared, int W1, int W2, int nlev);
+
+// sheared == nullptr: the row layout into pyramid / row_stride; else the sheared layout into
+// sheared (the v2 kernel's preconditions required)
+int corr_volume_pyramid_impl(const float *fmap2, const float *fmap3, int B, int C, int H, int W1, int W2,
+                             float sqrt_c, const float *trunc_disp, const float *trunc_conf, float atten,
+                             int num_levels, float *pyramid, long row_stride, float *sheared, void *stream) {
+  if (sheared) {
+    pyramid = sheared;   // (only for the checks below; the kernel writes through ShOut)
+    row_stride = sa_pyramid_level_offset(W2, num_levels);
+    row_stride = (row_stride + 3) / 4 * 4;
+  }
   SA_REQUIRE(fmap2 && fmap3 && pyramid, "sa_corr_volume_pyramid: null pointer");
   SA_REQUIRE(B > 0 && C > 0 && H > 0 && W1 > 0 && W2 > 0, "sa_corr_volume_pyramid: empty shape");
   SA_REQUIRE(num_levels >= 1 && num_levels <= 4, "sa_corr_volume_pyramid: num_levels must be 1..4");
@@ -497,20 +620,27 @@ extern "C" int sa_corr_volume_pyramid(const float *fmap2, const float *fmap3, in
     const bool tr = trunc_disp != nullptr;
     const unsigned nbu = (unsigned)nb;
     const int a2 = (int)f2_bytes, a3 = (int)f3_bytes;
-    if (tr && pow2)
-      corr_pyramid_v2_kernel<true, true><<<nbu, 256, 0, s>>>(fmap2, fmap3, g, jblocks, kblocks, kstep, sqrt_c, inv, trunc_disp,
-                                                             trunc_conf, atten, pyramid, a2, a3);
-    else if (tr)
-      corr_pyramid_v2_kernel<true, false><<<nbu, 256, 0, s>>>(fmap2, fmap3, g, jblocks, kblocks, kstep, sqrt_c, inv,
-                                                              trunc_disp, trunc_conf, atten, pyramid, a2, a3);
-    else if (pow2)
-      corr_pyramid_v2_kernel<false, true><<<nbu, 256, 0, s>>>(fmap2, fmap3, g, jblocks, kblocks, kstep, sqrt_c, inv, nullptr,
-                                                              nullptr, atten, pyramid, a2, a3);
-    else
-      corr_pyramid_v2_kernel<false, false><<<nbu, 256, 0, s>>>(fmap2, fmap3, g, jblocks, kblocks, kstep, sqrt_c, inv, nullptr,
-                                                               nullptr, atten, pyramid, a2, a3);
+    const ShOut so = sheared ? make_shout(sheared, W1, W2, num_levels) : ShOut{};
+#define SA_V2(TR_, P2_, SH_)                                                                                        \
+  corr_pyramid_v2_kernel<TR_, P2_, SH_><<<nbu, 256, 0, s>>>(fmap2, fmap3, g, jblocks, kblocks, kstep, sqrt_c, inv, \
+                                                            TR_ ? trunc_disp : nullptr, TR_ ? trunc_conf : nullptr, \
+                                                            atten, pyramid, a2, a3, so)
+    if (sheared) {
+      if (tr && pow2) SA_V2(true, true, true);
+      else if (tr) SA_V2(true, false, true);
+      else if (pow2) SA_V2(false, true, true);
+      else SA_V2(false, false, true);
+    } else {
+      if (tr && pow2) SA_V2(true, true, false);
+      else if (tr) SA_V2(true, false, false);
+      else if (pow2) SA_V2(false, true, false);
+      else SA_V2(false, false, false);
+    }
+#undef SA_V2
     return sa::check_launch("sa_corr_volume_pyramid");
   }
+  SA_REQUIRE(!sheared, "sa_corr_volume_pyramid_sheared: needs C %% 16 == 0, W1 and W2 %% 4 == 0, 16-byte aligned "
+                       "feature maps under 2 GiB");
   const unsigned nblk = (unsigned)((long)B * H * g.tilesJ * g.tilesK);
   sa::TimingScope ts(SA_K_CORR_PYRAMID, s);
   const bool tr = trunc_disp != nullptr;
@@ -523,6 +653,23 @@ extern "C" int sa_corr_volume_pyramid(const float *fmap2, const float *fmap3, in
   else
     corr_pyramid_kernel<false, false><<<nblk, 256, 0, s>>>(fmap2, fmap3, g, sqrt_c, nullptr, nullptr, atten, pyramid);
   return sa::check_launch("sa_corr_volume_pyramid");
+}
+}  // namespace
+
+extern "C" int sa_corr_volume_pyramid(const float *fmap2, const float *fmap3, int B, int C, int H,
+                                      int W1, int W2, float sqrt_c, const float *trunc_disp,
+                                      const float *trunc_conf, float atten, int num_levels,
+                                      float *pyramid, long row_stride, void *stream) {
+  return corr_volume_pyramid_impl(fmap2, fmap3, B, C, H, W1, W2, sqrt_c, trunc_disp, trunc_conf, atten, num_levels,
+                                  pyramid, row_stride, nullptr, stream);
+}
+
+extern "C" int sa_corr_volume_pyramid_sheared(const float *fmap2, const float *fmap3, int B, int C, int H, int W1,
+                                              int W2, float sqrt_c, const float *trunc_disp, const float *trunc_conf,
+                                              float atten, int num_levels, float *sheared, void *stream) {
+  SA_REQUIRE(sheared, "sa_corr_volume_pyramid_sheared: null pointer");
+  return corr_volume_pyramid_impl(fmap2, fmap3, B, C, H, W1, W2, sqrt_c, trunc_disp, trunc_conf, atten, num_levels,
+                                  nullptr, 0, sheared, stream);
 }
 
 extern "C" int sa_corr_pyramid_from_volume(const float *volume, long rows, int W2, long in_row_stride,
@@ -557,6 +704,37 @@ extern "C" int sa_corr_pyramid_from_volume_strided(const float *volume, int B, i
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_MISC, s);
   pyramid_from_strided_kernel<<<dim3((unsigned)((W1 + PT_J - 1) / PT_J), (unsigned)H, (unsigned)B), 256, 0, s>>>(
-      volume, sb, sh, sk, H, W1, W2, g, pyramid);
+      volume, sb, sh, sk, H, W1, W2, g, pyramid, ShOut{});
   return sa::check_launch("sa_corr_pyramid_from_volume_strided");
+}
+
+namespace {
+ShOut make_shout(float *sheared, int W1, int W2, int nlev) {
+  ShOut so{};
+  so.base = sheared;
+  so.slice = sa_shear_slice_size(W1, W2, nlev);
+  for (int l = 0; l < 4; ++l) {
+    so.off[l] = l < nlev ? sa_shear_level_offset(W1, W2, nlev, l) : 0;
+    so.rows[l] = l < nlev ? sa_pyramid_level_width(W2, l) + ((W1 - 1) >> l) : 0;
+  }
+  return so;
+}
+}  // namespace
+
+extern "C" int sa_corr_pyramid_from_volume_strided_sheared(const float *volume, int B, int H, int W1, int W2, long sb,
+                                                           long sh, long sk, int num_levels, float *sheared,
+                                                           void *stream) {
+  SA_REQUIRE(volume && sheared, "sa_corr_pyramid_from_volume_strided_sheared: null pointer");
+  SA_REQUIRE(B > 0 && B <= 65535 && H > 0 && H <= 65535 && W1 > 0 && W2 > 0,
+             "sa_corr_pyramid_from_volume_strided_sheared: bad shape");
+  SA_REQUIRE(num_levels >= 1 && num_levels <= 4,
+             "sa_corr_pyramid_from_volume_strided_sheared: num_levels must be 1..4");
+  SA_REQUIRE(W1 % 4 == 0 && sb % 4 == 0 && sh % 4 == 0 && sk % 4 == 0 && reinterpret_cast<uintptr_t>(volume) % 16 == 0,
+             "sa_corr_pyramid_from_volume_strided_sheared: needs W1 %% 4 == 0 and 16-byte aligned volume rows");
+  Geo g = make_geo(1, 1, 1, W2, num_levels, 0);
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_MISC, s);
+  pyramid_from_strided_kernel<true><<<dim3((unsigned)((W1 + PT_J - 1) / PT_J), (unsigned)H, (unsigned)B), 256, 0, s>>>(
+      volume, sb, sh, sk, H, W1, W2, g, nullptr, make_shout(sheared, W1, W2, num_levels));
+  return sa::check_launch("sa_corr_pyramid_from_volume_strided_sheared");
 }

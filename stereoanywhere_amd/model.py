@@ -94,7 +94,14 @@ class ScheduleOptions:
     # one load instruction of a wave reads one or two row segments; the row layout spreads
     # it over 64 cache lines); False: the row-layout lookup
     sheared_lookup: bool = True
-    # ... when the stereo volume (B x H4 x W4 x W4 floats) is at least this large
+    # ... when the stereo volume (B x H4 x W4 x W4 floats) is at least shear_min_bytes (the
+    # sheared lookup is 0.69x the row one at the booster tile batch, 1.03x at B = 4 x 240), as a
+    # copy pass from the row layout (sa_corr_pyramid_shear); True: the two pyramid producers write
+    # the sheared layout themselves (stereo: the volume + truncation + pyramid kernel; mono: the
+    # pyramid from the classifier output) -- measured slower: the diagonal row segments of a
+    # 64 x 64 tile end mid-sector, and the partial 4-byte writes cost the stereo producer 16.1
+    # instead of 3.0 ms at the booster batch, against 2.4 ms for the copy pass
+    sheared_producers: bool = False
     shear_min_bytes: int = 1 << 30
     # a GRU level whose width is not a multiple of 4 keeps its planes padded to one (zero
     # columns) and runs on F(4x4) with the gates in the epilogue (False: separate gate kernels and
@@ -328,30 +335,33 @@ class StereoAnywhere(nn.Module):
 
         # ---- pyramids
         trunc = (sm2, mirror) if a.use_truncate_vol else (None, None)
+        big = B * H4 * W4 * W4 * 4 >= self.opts.shear_min_bytes
+        direct = self.opts.sheared_lookup and self.opts.sheared_producers and big
         if a.use_aggregate_stereo_vol:
             stereo_blk = self._stereo_aggregate(dw, fmap2, fmap3, mde2, mde3, m2l, m3l, trunc, B, H4, W4)
         else:
             stereo_blk = HipCorrBlock1D.from_features(fmap2, fmap3, a.corr_levels, a.corr_radius, trunc[0], trunc[1],
-                                                      float(a.mirror_attenuation))
+                                                      float(a.mirror_attenuation), sheared=direct)
         del fmap2, fmap3
         if a.use_aggregate_mono_vol:
             mono_rows = vol_d.permute(0, 1, 3, 4, 2)  # [B,1,H,W1,W2] view (transposed by the pyramid kernel)
         else:
             # raw mono volume 1.73 * corr(normals) (stereoanywhere.py:136, 210)
             mono_rows = 1.73 * ops.corr_volume(n2, n3)
-        mono_blk = HipCorrBlock1D(None, a.corr_levels, a.corr_radius,
-                                  _pyramid=ops.pyramid_from_volume(mono_rows, a.corr_levels),
-                                  _shape=(B, H4, W4, W4))
+        mono_blk = HipCorrBlock1D(None, a.corr_levels, a.corr_radius, _shape=(B, H4, W4, W4))
+        if direct:
+            mono_blk.sheared = ops.pyramid_from_volume_sheared(mono_rows, a.corr_levels)
+        if mono_blk.sheared is None:
+            mono_blk.pyramid = ops.pyramid_from_volume(mono_rows, a.corr_levels)
         del mono_rows, vol_d, vol_c
 
-        if self.opts.sheared_lookup and B * H4 * W4 * W4 * 4 >= self.opts.shear_min_bytes:
-            # the lookups read disparity-sheared copies (coalesced across a wave's pixels); the
-            # row-layout buffers are not read again.  Only for large volumes: the copy costs
-            # ~2.9 TB/s of its bytes once, and the sheared lookup is no faster at B = 4 x 240
-            # (53.6 vs 52.9 us) but 0.69x at the booster tile batch (717 vs 1036 us;
-            # scripts/bench_lookup.py)
-            stereo_blk.shear(release=True)
-            mono_blk.shear(release=True)
+        if self.opts.sheared_lookup and big:
+            # the lookups read disparity-sheared pyramids (coalesced across a wave's pixels); a
+            # block whose producer wrote the row layout gets a sheared copy (the row-layout
+            # buffers are not read again)
+            for blk in (stereo_blk, mono_blk):
+                if blk.sheared is None:
+                    blk.shear(release=True)
         parts = min(self.opts.loop_parts, B) if self.stream_overlap else 1
         if parts <= 1:
             return _drive(self._iterate(dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4))

@@ -92,6 +92,53 @@ def corr_volume_pyramid(fmap2: torch.Tensor, fmap3: torch.Tensor, num_levels: in
     return out
 
 
+def corr_volume_pyramid_sheared(fmap2: torch.Tensor, fmap3: torch.Tensor, num_levels: int = 4,
+                                trunc_disp: Optional[torch.Tensor] = None, trunc_conf: Optional[torch.Tensor] = None,
+                                attenuation: float = 0.9) -> Optional[torch.Tensor]:
+    """corr_volume_pyramid written straight in the disparity-sheared layout [B*H, slice] that
+    corr_lookup_conv1x1_sheared reads (sa_corr_volume_pyramid_sheared: the same cells as
+    corr_pyramid_shear(corr_volume_pyramid(...))); None where the kernel's preconditions fail
+    (C % 16, W1 % 4, W2 % 4, 16-byte aligned feature maps under 2 GiB)."""
+    _check(fmap2, "fmap2")
+    _check(fmap3, "fmap3")
+    B, C, H, W1 = fmap2.shape
+    W2 = fmap3.shape[3]
+    if tuple(fmap3.shape[:3]) != (B, C, H):
+        raise RuntimeError(f"fmap shapes disagree: {tuple(fmap2.shape)} vs {tuple(fmap3.shape)}")
+    lim = (1 << 31) - 64
+    if (C % 16 or W1 % 4 or W2 % 4 or fmap2.data_ptr() % 16 or fmap3.data_ptr() % 16
+            or fmap2.numel() * 4 >= lim or fmap3.numel() * 4 >= lim):
+        return None
+    if trunc_disp is not None:
+        _check(trunc_disp, "trunc_disp")
+        _check(trunc_conf, "trunc_conf")
+        if trunc_disp.numel() != B * H * W1 or trunc_conf.numel() != B * H * W1:
+            raise RuntimeError("truncation maps must be [B,1,H,W1]")
+    slice_sz = int(N.lib().sa_shear_slice_size(W1, W2, num_levels))
+    out = torch.empty((B * H, slice_sz), device=fmap2.device, dtype=torch.float32)
+    sqrt_c = float(torch.sqrt(torch.tensor(float(C), dtype=torch.float32)))
+    N.call("sa_corr_volume_pyramid_sheared", fmap2.data_ptr(), fmap3.data_ptr(), B, C, H, W1, W2, sqrt_c,
+           _ptr(trunc_disp), _ptr(trunc_conf), attenuation, num_levels, out.data_ptr(), _stream(fmap2))
+    return out
+
+
+def pyramid_from_volume_sheared(volume: torch.Tensor, num_levels: int = 4) -> Optional[torch.Tensor]:
+    """pyramid_from_volume of a [B, 1, H, W1, W2] view of a [B, 1, W2, H, W1] volume (the
+    hourglass classifier's layout) written in the disparity-sheared layout [B*H, slice]
+    (sa_corr_pyramid_from_volume_strided_sheared); None for any other layout."""
+    _check(volume, "volume", contiguous=False)
+    if not (volume.dim() == 5 and volume.shape[1] == 1 and volume.stride(-1) != 1 and volume.stride(3) == 1
+            and volume.shape[3] % 4 == 0 and volume.data_ptr() % 16 == 0
+            and all(volume.stride(i) % 4 == 0 for i in (0, 2, 4))):
+        return None
+    B, _, H, W1, W2 = volume.shape
+    slice_sz = int(N.lib().sa_shear_slice_size(W1, W2, num_levels))
+    out = torch.empty((B * H, slice_sz), device=volume.device, dtype=torch.float32)
+    N.call("sa_corr_pyramid_from_volume_strided_sheared", volume.data_ptr(), B, H, W1, W2, volume.stride(0),
+           volume.stride(2), volume.stride(4), num_levels, out.data_ptr(), _stream(volume))
+    return out
+
+
 def corr_volume(fmap2: torch.Tensor, fmap3: torch.Tensor) -> torch.Tensor:
     """CorrBlock1D.corr contract: [B,C,H,W1] x [B,C,H,W2] -> [B,H,W1,1,W2]."""
     B, C, H, W1 = fmap2.shape

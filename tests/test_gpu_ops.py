@@ -157,6 +157,47 @@ def test_lookup_fused_taps_bit_exact():
         assert np.all(fused[v::2, 36:] == 0)
 
 
+def _sheared_valid_cells(sh, W1, W2, L=4):
+    """the level cells of a sheared pyramid [B*H, slice] as [B*H, n] (fixed order), the entries
+    with k outside the level dropped"""
+    _, _, wids = ops.pyramid_geometry(W2, L)
+    cols = []
+    for l in range(L):
+        o = int(N.lib().sa_shear_level_offset(W1, W2, L, l))
+        E = wids[l] + ((W1 - 1) >> l)
+        e = torch.arange(E, device=sh.device).view(E, 1)
+        j = torch.arange(W1, device=sh.device).view(1, W1)
+        k = (j >> l) - e + wids[l] - 1
+        idx = (o + e * W1 + j)[(k >= 0) & (k < wids[l])]
+        cols.append(sh[:, idx])
+    return torch.cat(cols, 1)
+
+
+@pytest.mark.parametrize("W1,W2,trunc", [(240, 240, True), (280, 280, True), (300, 300, False), (128, 200, True),
+                                         (64, 64, False)])
+def test_sheared_producers_equal_shear_copy(W1, W2, trunc):
+    """The producers writing the sheared layout directly (stereo volume + truncation + pyramid;
+    the mono pyramid from the classifier's [B, 1, W2, H, W1] output) hold exactly the cells of the
+    shear pass over their row-layout output: W > 256 (two k blocks / LDS chunks), W1 != W2."""
+    rng = np.random.default_rng(W1 + 3 * W2)
+    B, C, H = 2, 32, 3
+    f2, f3 = g(rng.standard_normal((B, C, H, W1))), g(rng.standard_normal((B, C, H, W2)))
+    td = g(rng.random((B, 1, H, W1)) * W1 / 3) if trunc else None
+    tc = g(rng.random((B, 1, H, W1))) if trunc else None
+    row = ops.corr_volume_pyramid(f2, f3, 4, td, tc, 0.9)
+    direct = ops.corr_volume_pyramid_sheared(f2, f3, 4, td, tc, 0.9)
+    assert direct is not None
+    copy = ops.corr_pyramid_shear(row, B, H, W1, W2)
+    assert torch.equal(_sheared_valid_cells(direct, W1, W2), _sheared_valid_cells(copy, W1, W2))
+    if W1 == W2:
+        vol = g(rng.standard_normal((B, 1, W2, H, W1)))      # the classifier output's layout
+        view = vol.permute(0, 1, 3, 4, 2)
+        sm = ops.pyramid_from_volume_sheared(view)
+        assert sm is not None
+        cm = ops.corr_pyramid_shear(ops.pyramid_from_volume(view), B, H, W1, W2)
+        assert torch.equal(_sheared_valid_cells(sm, W1, W2), _sheared_valid_cells(cm, W1, W2))
+
+
 @pytest.mark.parametrize("W1,W2", [(96, 96), (70, 70), (240, 240), (37, 45), (30, 30)])
 def test_lookup_sheared_bit_exact(W1, W2):
     """The lookup + convc1 on the disparity-sheared pyramid copies (corr_shear.hip) equals the
@@ -185,7 +226,7 @@ def test_lookup_sheared_bit_exact(W1, W2):
             res[mf] = (c(ops.corr_lookup_conv1x1(pa, pb, W2, 4, 4, g(cx), g(wt), g(bias))),
                        c(ops.corr_lookup_conv1x1_sheared(sa, sb, W2, 4, 4, g(cx), g(wt), g(bias))))
         finally:
-            N.lib().sa_lookup_set_mfma(1)
+            N.lib().sa_lookup_set_mfma(0)   # (the default: convc1 on the VALU)
     row, sh = res[1]
     np.testing.assert_array_equal(sh, row)
     np.testing.assert_array_equal(res[0][0], row)
