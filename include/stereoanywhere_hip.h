@@ -383,6 +383,11 @@ int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, float *U4, v
  * (Cout % 64 == 0); co_block 32 is sa_conv2d_wino4_weights. */
 int sa_conv2d_wino4_weights_cb(const float *weight, int Cout, int Cin, int co_block, float *U4,
                                void *stream);
+/* U4 for the split block shape (block_shape 6 of sa_conv2d_k3_wino4_multi_gate: the Winograd-domain
+ * products on f16 MFMA with hi/lo operand pairs): 72*Cin*Cout dwords laid out
+ * [Cout/32][Cin/4][36][4][16][2][2], each dword the f16 pair (hi, lo) of U * 2^12 (hi in the low
+ * half), stored twice.  Needs |weight| < 16 (U * 2^12 within the f16 range). */
+int sa_conv2d_wino4_weights_split(const float *weight, int Cout, int Cin, void *U4s, void *stream);
 long sa_conv2d_k3_wino4_stat_parts(int H, int W);
 int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, void *stream);
 /* ConvGRU gates in the epilogue (update.py:16-27), per problem (gates[i].mode 0 = plain; gates
@@ -411,7 +416,9 @@ typedef struct SaGateEpilogue {
  * sa_conv2d_wino4_weights_cb(..., 64, ...), Cout % 64 == 0, and Cout % 128 == 0 with a z/r gate),
  * 4 quadrant blocks (8 waves, 32 tiles x 64 output channels, the 64-channel U), 5 persistent large
  * blocks (the large shape, one block per CU walking the launch's work items; each item prefetches
- * the next item's first input-channel chunk under its own epilogue). */
+ * the next item's first input-channel chunk under its own epilogue), 6 split large blocks (8 waves,
+ * 64 tiles x 32 output channels, 4-channel chunks; every problem's U from
+ * sa_conv2d_wino4_weights_split; the transformed inputs must stay below 65504 in magnitude). */
 int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                                   int block_shape, void *stream);
 

@@ -46,6 +46,16 @@ def main():
         ops._WINO4 = True
         t_4 = timeit(lambda: ops.conv2d_k3(x, U, out=out))
         f4 = float((ops.conv2d_k3(x, U) - F.conv2d(x, w, None, padding=1)).abs().max())
+        if "--split" in sys.argv:   # F(4x4) fp32 MFMA vs the split kernel (block_shape 6)
+            ops.W4_SPLIT = True
+            Us = ops.wino_weights(w)
+            t_s = timeit(lambda: ops.conv2d_k3(x, Us, out=out))
+            fs = float((ops.conv2d_k3(x, Us) - F.conv2d(x, w, None, padding=1)).abs().max())
+            ops.W4_SPLIT = False
+            ex = 2.0 * 36 * N * Cout * Cin * ((H + 3) // 4) * ((W + 3) // 4)
+            print(f"{name:12s} wino4 {t_4:8.1f} us ({ex / t_4 / 1e6:6.1f} TF exec) max|d| {f4:.2e}   "
+                  f"split {t_s:8.1f} us ({ex / t_s / 1e6:6.1f} TF exec) max|d| {fs:.2e}  x{t_4 / t_s:.2f}", flush=True)
+            continue
         if "--only-wino" in sys.argv:
             fl = 2.0 * N * Cout * Cin * 9 * H * W
             print(f"{name:12s} wino {t_w:8.1f} us ({fl / t_w / 1e6:6.1f} TF-eq)  wino4 {t_4:8.1f} us "

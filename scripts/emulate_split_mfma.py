@@ -8,6 +8,8 @@ in which U and V are split into bf16 pieces before the products:
   fp32    no split (checks the restatement itself against the HIP kernel's EPE)
   bf16x3  V = V0 + V1, U = U0 + U1; products V0U0 + V0U1 + V1U0
   bf16x6  three pieces each; products with piece-order sum <= 2
+  f16x4   V = V0 + V1, U = (U0 + U1) / 2^12 as f16 pieces; all four products
+  f16x3   the same without V1U1
 bf16 x bf16 products are exact in fp32, so fp32 einsums over the pieces reproduce the MFMA
 arithmetic up to accumulation order.  Reports EPE against the reference's own cfg2 output
 (tests/golden/cfg2_544x960_it22.npz), the gate is 1e-3.
@@ -76,6 +78,7 @@ TILES = {"2": (AT, G, BT)}
 _WEIGHTS = {}
 _real_wino_weights = ops.wino_weights
 MODE = "fp32"
+STATS = {"vmax": 0.0, "umax": 0.0}
 MOUT = "2"   # tile config name: "2" F(2x2,3x3), "3" F(3x3), "4" F(4x4) points +-2, "4h" points +-1/2
 
 
@@ -86,6 +89,12 @@ def split(t: torch.Tensor, n: int):
         parts.append(p)
         r = r - p
     return parts
+
+
+def split16(t: torch.Tensor, scale: float):
+    t = t * scale
+    hi = t.half().float()
+    return [hi, (t - hi).half().float()]
 
 
 def wino_weights(weight):
@@ -126,8 +135,21 @@ def conv2d_k3(x, U, bias=None, relu=False, out=None, in_aff=None, in_act=None, s
     d = xp.unfold(2, n_, m_).unfold(3, n_, m_)                            # [B,Cin,Ht,Wt,n,n]
     btf = bt.to(x.device).float()
     V = torch.einsum("ik,bchwkl,jl->bchwij", btf, d, btf).reshape(B, Cin, Ht, Wt, n_ * n_)
+    STATS["vmax"] = max(STATS["vmax"], float(V.abs().max()))
+    STATS["umax"] = max(STATS["umax"], float(Uw.abs().max()))
     if MODE == "fp32":
         M = torch.einsum("bchwp,pco->bohwp", V, Uw)
+    elif MODE in ("f16x4", "f16x3"):
+        # f16 hi/lo pairs (conv2d_wino4.hip's split kernel): U scaled by 2^12 before the split,
+        # V unscaled; f16 x f16 products are exact in fp32
+        vs, us = split16(V, 1.0), split16(Uw, 4096.0)
+        M = 0
+        for i in range(2):
+            for j in range(2):
+                if MODE == "f16x3" and i + j == 2:
+                    continue
+                M = M + torch.einsum("bchwp,pco->bohwp", vs[i], us[j])
+        M = M / 4096.0
     else:
         n = 2 if MODE == "bf16x3" else 3
         vs, us = split(V, n), split(Uw, n)
@@ -179,7 +201,9 @@ def main():
         with torch.no_grad():
             disp = -net(*t, iters=22, test_mode=True)[0][:, 0].cpu().numpy()
         ref = fix["disparity"]
-        print(f"{mode:7s} EPE {epe(disp, ref):.3e}  max {float(np.abs(disp - ref).max()):.3e}", flush=True)
+        print(f"{mode:7s} EPE {epe(disp, ref):.3e}  max {float(np.abs(disp - ref).max()):.3e}  "
+              f"max|V| {STATS['vmax']:.3g} max|U| {STATS['umax']:.3g}", flush=True)
+        STATS.update(vmax=0.0, umax=0.0)
 
 
 if __name__ == "__main__":

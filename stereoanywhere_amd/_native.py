@@ -84,6 +84,7 @@ SIGNATURES = {
     "sa_conv2d_k3_wino_multi": (I, [I, P, P]),
     "sa_conv2d_wino4_weights": (I, [P, I, I, P, P]),
     "sa_conv2d_wino4_weights_cb": (I, [P, I, I, I, P, P]),
+    "sa_conv2d_wino4_weights_split": (I, [P, I, I, P, P]),
     "sa_conv2d_k3_wino4_stat_parts": (L, [I, I]),
     "sa_conv2d_k3_wino4_multi": (I, [I, P, P]),
     "sa_conv2d_k3_wino4_multi_gate": (I, [I, P, P, I, P]),

@@ -67,6 +67,9 @@ namespace {
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f32x2 = __attribute__((ext_vector_type(2))) float;
+using f16x2 = __attribute__((ext_vector_type(2))) _Float16;
+using f16x4 = __attribute__((ext_vector_type(4))) _Float16;
+using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
 
 constexpr int NPT = 36;                   // transform points
 
@@ -75,18 +78,20 @@ constexpr int NPT = 36;                   // transform points
 // 4-channel chunks, 66 KiB, two blocks per CU, so one block's first DMA wait and epilogue
 // overlap the other's MFMAs (per block ~6-8k cycles until the first chunk lands and ~9k of
 // epilogue around 6.8k per chunk, scripts/w4_clock.py); it is not faster in the forward.
-template <int NW_, int KC_, int CO_ = 32, bool QUAD_ = false>
+template <int NW_, int KC_, int CO_ = 32, bool QUAD_ = false, bool SPLIT_ = false>
 struct W4Cfg {
   // QUAD: the waves of a tile group split the 6 x 6 points in quadrants (rows 0-2 / 3-5 x
   // columns 0-2 / 3-5) instead of column halves
   static constexpr bool QUAD = QUAD_;
+  // SPLIT: the products on f16 MFMA with hi/lo operand pairs (W4Split below)
+  static constexpr bool SPLIT = SPLIT_;
   static constexpr int NW = NW_, NTHR = 64 * NW_, TG = QUAD_ ? NW_ / 4 : NW_ / 2, NT = 16 * TG, KC = KC_, JPC = KC_ / 4;
   static constexpr int NR = QUAD_ ? 3 : 6;                  // point rows per wave
   static constexpr int CO = CO_, CG = CO_ / 16;                // output channels per block, 16-channel groups
   static constexpr int SB = 4 * CO_;                        // filters per (point, 4-channel job): [k][n][g]
   static constexpr int PS_MAX = NT == 64 ? 340 : 204;       // (BH + 2)(BW / 4 + 2), largest geometry
   static constexpr int PBUF = (KC * PS_MAX + 32) * 4;       // + the last DMA's idle lanes
-  static constexpr int UBUF = NPT * KC * CO;                // filters per chunk
+  static constexpr int UBUF = NPT * KC * CO * (SPLIT_ ? 2 : 1);   // filters per chunk (dwords)
   static constexpr int BUF = PBUF + UBUF;                   // one buffer: patch, then filters
   static constexpr int OPP = NT * 16 + 4;                   // output staging plane pitch (4 mod 32)
   static constexpr int SMEM = 2 * BUF > CO * OPP ? 2 * BUF : CO * OPP;
@@ -116,6 +121,20 @@ using W4Wide = W4Cfg<4, 4, 64>;
 // ds_read_b128 instead of two ds_read_b64 per four MFMAs.  The price: a barrier per 4 input
 // channels and four partial output transforms meeting in LDS.
 using W4Quad = W4Cfg<8, 4, 64, true>;
+// Split: the 8-wave shape with 4-channel chunks whose Winograd-domain products run on
+// v_mfma_f32_16x16x16_f16 instead of v_mfma_f32_16x16x4_f32.  Each operand is an f16 hi/lo
+// pair (x = hi + lo, 22 significant bits; filters scaled by 2^W4S_LOG2 before the split and
+// the accumulators by 2^-W4S_LOG2 after the main loop, both exact), and one MFMA's K = 16
+// slots hold a lane's channel as the four products hi*bhi + hi*blo + lo*bhi + lo*blo: the A
+// operand (hi, hi, lo, lo) is the lane's transformed value (3 VALU to split), the B operand
+// (bhi, blo, bhi, blo) is staged that way in LDS (sa_conv2d_wino4_weights_split), so one
+// ds_read_b128 gives a lane both output-channel groups' operands.  Products of f16 pairs are
+// exact in fp32, so the result differs from the fp32 kernel only by the operands' rounding
+// (<= 2^-22 relative; below 2^-14 the lo halves are subnormal, an absolute 2^-25) and the
+// accumulation order.  |V| must stay below 65504 (the f16 range): V = B^T d B grows at most
+// 100-fold over the input patch.
+using W4Split = W4Cfg<8, 4, 32, false, true>;
+constexpr int W4S_LOG2 = 12;
 static_assert(2 * W4Small::SMEM * 4 <= 160 * 1024, "two small blocks per CU");
 static_assert(W4Wide::SMEM * 4 <= 160 * 1024, "one wide block per CU");
 
@@ -159,6 +178,16 @@ struct W4Launch {
   unsigned nblk[MAX_PROB];
   int nprob;
 };
+
+// x as the f16 A operand (hi, hi, lo, lo): hi = f16(x), lo = f16(x - hi) (x - hi is exact in
+// fp32; one v_fma_mix_f32 reads hi as f16), both round-to-nearest-even
+__device__ __forceinline__ f16x4 w4_split(const float x) {
+  const f16x2 hh = __builtin_convertvector(f32x2{x, x}, f16x2);
+  float l;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(__builtin_bit_cast(unsigned, hh)), "v"(x));
+  const f16x2 ll = __builtin_convertvector(f32x2{l, l}, f16x2);
+  return __builtin_shufflevector(hh, ll, 0, 1, 2, 3);
+}
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, float *lds, int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)lds, 16, voff, soff, 0, 0);
@@ -445,8 +474,10 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   constexpr int NWAVE = C::NW, NTHR = C::NTHR, KC = C::KC, JPC = C::JPC, NT = C::NT, PDMA = C::PDMA,
                 UDMA = C::UDMA, UPW = C::UPW, UBUF = C::UBUF, BUF = C::BUF, PBUF = C::PBUF, OPP = C::OPP,
                 CO = C::CO, CG = C::CG, SB = C::SB, NR = C::NR;
-  constexpr bool QUAD = C::QUAD;
-  using f32xg = __attribute__((ext_vector_type(CG))) float;   // a lane's filter operands, one per group
+  constexpr bool QUAD = C::QUAD, SPLIT = C::SPLIT;
+  static_assert(!SPLIT || (!QUAD && !PERSIST && KC == 4 && CG == 2), "split: the 8-wave 4-channel 32-channel shape");
+  // a lane's filter operands of a point: one float per group, or (split) two f16 pairs per group
+  using f32xg = std::conditional_t<SPLIT, f32x4, float __attribute__((ext_vector_type(CG)))>;
   const int Cin = P.Cin, H = P.H;
   // block geometry as compile-time constants (the patch offsets divide by PS and PG)
   constexpr int ltw = LTW, tw = 1 << ltw, tr = NT >> ltw;
@@ -473,14 +504,16 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
       const_cast<float *>(P.in + (long)n * P.in_bs), (short)0, Cin * hw * 4, 0x00020000);
   // the filters' global layout has 8-channel chunks (sa_conv2d_wino4_weights); a 4-channel
   // chunk is every other SB-float piece of one (the DMA gathers it by its source addresses)
+  constexpr int UW = SPLIT ? 2 : 1;   // dwords per filter value
   const __amdgpu_buffer_rsrc_t uin = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float *>(P.U + (long)cb * Cin * NPT * CO), (short)0, Cin * NPT * CO * 4, 0x00020000);
+      const_cast<float *>(P.U + (long)cb * Cin * NPT * CO * UW), (short)0, Cin * NPT * CO * 4 * UW, 0x00020000);
+  // (the split layout is one contiguous LDS image per 4-channel chunk)
   auto u_src = [&](int piece) {   // byte offset of this lane's 16 bytes of filter DMA piece `piece`
     const int f = piece * 256 + lane * 4;
-    return (JPC == 2 ? f : f + (f / SB) * SB) * 4;
+    return (JPC == 2 || SPLIT ? f : f + (f / SB) * SB) * 4;
   };
   auto u_chunk = [&](int chunk) {   // byte offset of a chunk's filters
-    return JPC == 2 ? chunk * UBUF * 4 : (chunk >> 1) * 2 * UBUF * 4 + (chunk & 1) * SB * 4;
+    return JPC == 2 || SPLIT ? chunk * UBUF * 4 : (chunk >> 1) * 2 * UBUF * 4 + (chunk & 1) * SB * 4;
   };
 
   // patch DMA: the chunk's image is [channel][PR rows][PG groups of 4 floats], dense, starting
@@ -540,7 +573,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   int PSv = PS, PGv = PG;
   asm volatile("" : "+s"(PSv), "+s"(PGv));
   const int pread = k * PSv * 4 + 4 * trow * PGv * 4 + 4 * tcol + 2;
-  const int uread = (k * 16 + m) * CG;
+  const int uread = (k * 16 + m) * (SPLIT ? 4 : CG);
 
   // acc[i][jj][g]: point (row i, or 3 RH + i in a quadrant; column 3 HF + jj) of output-channel
   // group g
@@ -627,7 +660,8 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
     auto load_b = [&](int s, int jj, f32xg *b) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < NR; ++i)
-        b[i] = *reinterpret_cast<const f32xg *>(ub + ((6 * (QUAD ? 3 * RH + i : i) + 3 * HF + jj) * JPC + s) * SB);
+        b[i] = *reinterpret_cast<const f32xg *>(
+            ub + (SPLIT ? (6 * i + 3 * HF + jj) * 256 : ((6 * (QUAD ? 3 * RH + i : i) + 3 * HF + jj) * JPC + s) * SB));
     };
     load_rows(0, 0, 6);
     load_b(0, 0, bc);
@@ -656,11 +690,23 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
         } else {
           bt6(t[0][jj], t[1][jj], t[2][jj], t[3][jj], t[4][jj], t[5][jj], v);
         }
+        if constexpr (SPLIT) {
 #pragma unroll
-        for (int i = 0; i < NR; ++i)
+          for (int i = 0; i < NR; ++i) {
+            const f16x4 a = w4_split(v[i]);
+            const f16x8 bb = __builtin_bit_cast(f16x8, bc[i]);
+            acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x16f16(a, __builtin_shufflevector(bb, bb, 0, 1, 2, 3),
+                                                                  acc[i][jj][0], 0, 0, 0);
+            acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x16f16(a, __builtin_shufflevector(bb, bb, 4, 5, 6, 7),
+                                                                  acc[i][jj][1], 0, 0, 0);
+          }
+        } else {
 #pragma unroll
-          for (int g = 0; g < CG; ++g)
-            acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], bc[i][g], acc[i][jj][g], 0, 0, 0);
+          for (int i = 0; i < NR; ++i)
+#pragma unroll
+            for (int g = 0; g < CG; ++g)
+              acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], bc[i][g], acc[i][jj][g], 0, 0, 0);
+        }
 #if SA_W4_FENCE
         __builtin_amdgcn_sched_barrier(0);   // bound the scheduler's hoisting (register pressure)
 #endif
@@ -680,6 +726,14 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
 #ifdef SA_W4_CLOCK
   if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][5] = __builtin_amdgcn_s_memtime();
 #endif
+  if constexpr (SPLIT) {   // the filters' 2^W4S_LOG2 (exact)
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj)
+#pragma unroll
+        for (int g = 0; g < CG; ++g) acc[i][jj][g] *= 1.0f / (1 << W4S_LOG2);
+  }
 
 #ifndef SA_W4_P2PASS
 #define SA_W4_P2PASS 1   // 0 (diagnostic, with SA_W4_PF=0 only): the one-shot epilogue in persistent items
@@ -1001,6 +1055,42 @@ __global__ __launch_bounds__(256) void wino4_weights_kernel(const float *__restr
     }
 }
 
+// Filters of the split kernel (W4Split): U = G g G^T in fp64, times 2^W4S_LOG2, as the f16
+// pair hi = f16(u), lo = f16(u - hi) in one dword (hi in the low half), stored twice (the B
+// operand (bhi, blo, bhi, blo) of v_mfma_f32_16x16x16_f16).  Layout
+// [Cout/32][Cin/4][36][4][16][2][2] dwords: per (output block, 4-channel chunk) one contiguous
+// 36 KiB image of the LDS filter buffer; channel ci = 4 chunk + k, output co = 32 cb + 16 g + n
+// at [k][n][g].
+__global__ __launch_bounds__(256) void wino4s_weights_kernel(const float *__restrict__ w, int Cout, int Cin,
+                                                             unsigned *__restrict__ U) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)Cout * Cin) return;
+  const int co = (int)(i / Cin), ci = (int)(i % Cin);
+  const float *g = w + i * 9;
+  const double G[6][3] = {{0.25, 0.0, 0.0},
+                          {-1.0 / 6, -1.0 / 6, -1.0 / 6},
+                          {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                          {1.0 / 24, 1.0 / 12, 1.0 / 6},
+                          {1.0 / 24, -1.0 / 12, 1.0 / 6},
+                          {0.0, 0.0, 1.0}};
+  double t[6][3];
+  for (int a = 0; a < 6; ++a)
+    for (int c = 0; c < 3; ++c) t[a][c] = G[a][0] * g[c] + G[a][1] * g[3 + c] + G[a][2] * g[6 + c];
+  const int chunk = ci / 4, k = ci % 4, cb = co / 32, gg = (co % 32) / 16, n = co % 16;
+  for (int a = 0; a < 6; ++a)
+    for (int b = 0; b < 6; ++b) {
+      const double u = (t[a][0] * G[b][0] + t[a][1] * G[b][1] + t[a][2] * G[b][2]) * (double)(1 << W4S_LOG2);
+      const _Float16 hi = (_Float16)(float)u;
+      const _Float16 lo = (_Float16)(float)(u - (double)hi);
+      const unsigned pr = (unsigned)__builtin_bit_cast(unsigned short, hi) |
+                          ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
+      const int pt = 6 * a + b;
+      unsigned *d = U + ((((((long)cb * (Cin / 4) + chunk) * NPT + pt) * 4 + k) * 16 + n) * 2 + gg) * 2;
+      d[0] = pr;
+      d[1] = pr;
+    }
+}
+
 // geometry with the fewest padded output pixels (ties: 16 x 64, the smaller halo)
 int w4_ltw(int H, int W) {
   const long a16 = (long)((W + 63) / 64) * 64 * ((H + 15) / 16) * 16;
@@ -1025,6 +1115,15 @@ extern "C" int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, f
   return sa_conv2d_wino4_weights_cb(weight, Cout, Cin, 32, U, stream);
 }
 
+extern "C" int sa_conv2d_wino4_weights_split(const float *weight, int Cout, int Cin, void *U, void *stream) {
+  SA_REQUIRE(weight && U && Cout > 0 && Cin > 0 && Cin % 8 == 0 && Cout % 32 == 0,
+             "sa_conv2d_wino4_weights_split: bad arguments (Cin %% 8, Cout %% 32)");
+  const long n = (long)Cout * Cin;
+  hipStream_t s = sa::as_stream(stream);
+  wino4s_weights_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(weight, Cout, Cin, static_cast<unsigned *>(U));
+  return sa::check_launch("sa_conv2d_wino4_weights_split");
+}
+
 #ifdef SA_W4_CLOCK
 extern "C" int sa_w4_clock_read(unsigned long long *out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4_clock), sizeof(unsigned long long) * 10 * n) == hipSuccess ? 0 : -1;
@@ -1044,16 +1143,18 @@ extern "C" int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, v
 extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                                              int block_shape, void *stream) {
   SA_REQUIRE(nprob >= 1 && nprob <= MAX_PROB && probs, "sa_conv2d_k3_wino4_multi: 1..%d problems", MAX_PROB);
-  SA_REQUIRE(block_shape >= 0 && block_shape <= 5, "sa_conv2d_k3_wino4_multi: block_shape 0..5");
+  SA_REQUIRE(block_shape >= 0 && block_shape <= 6, "sa_conv2d_k3_wino4_multi: block_shape 0..6");
   // Large blocks unless the caller asks for small ones (block_shape 2) or wide ones (3: 64
   // output channels per block, filters from sa_conv2d_wino4_weights_cb(..., 64, ...)).  The
   // small shape measured 2-8% faster on standalone launches of Cin <= 128 with a few rounds of
   // blocks (qh08, convc2) but not faster in the forward as a blanket choice.
   // block_shape 4: the quadrant shape (W4Quad), also on the 64-channel filter layout
-  const bool small = block_shape == 2, wide = block_shape == 3, quad = block_shape == 4, persist = block_shape == 5;
+  // block_shape 6: the split kernel (W4Split; filters from sa_conv2d_wino4_weights_split)
+  const bool small = block_shape == 2, wide = block_shape == 3, quad = block_shape == 4, persist = block_shape == 5,
+             split = block_shape == 6;
   const int nt = small || wide || quad ? W4Small::NT : W4Big::NT;
   const int CO = wide || quad ? 64 : 32;
-  const int aff_max = small ? W4Small::AFF_MAX : quad ? W4Quad::AFF_MAX : W4Big::AFF_MAX;
+  const int aff_max = small ? W4Small::AFF_MAX : quad ? W4Quad::AFF_MAX : split ? W4Split::AFF_MAX : W4Big::AFF_MAX;
   W4Launch L{};
   long total = 0;
   bool gated = false, aff = false;
@@ -1076,7 +1177,7 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
                "sa_conv2d_k3_wino4: an input transform needs the 8-wave, quadrant or 4-wave shape and Cin <= %d",
                aff_max);
     aff = aff || qaff;
-    SA_REQUIRE((long)q.Cin * q.H * pitch * 4 < (1L << 31) - 64 && 36L * q.Cin * q.Cout * 4 < (1L << 31),
+    SA_REQUIRE((long)q.Cin * q.H * pitch * 4 < (1L << 31) - 64 && 36L * q.Cin * q.Cout * (split ? 8 : 4) < (1L << 31),
                "sa_conv2d_k3_wino4: an image or the filter bank exceeds the 2 GB buffer-descriptor range");
     const int ltw = w4_ltw(q.H, q.W), bw = 4 << ltw, bh = 4 * (nt >> ltw);
     const int tiles_w = (q.W + bw - 1) / bw, tiles_h = (q.H + bh - 1) / bh;
@@ -1124,7 +1225,11 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
     aff     ? wino_f4k3_persist_kernel<W4Big, false, true><<<grid, W4Big::NTHR, 0, s>>>(L)
     : gated ? wino_f4k3_persist_kernel<W4Big, true><<<grid, W4Big::NTHR, 0, s>>>(L)
             : wino_f4k3_persist_kernel<W4Big, false><<<grid, W4Big::NTHR, 0, s>>>(L);
-  } else if (quad)
+  } else if (split)
+    aff     ? wino_f4k3_kernel<W4Split, false, true><<<(unsigned)total, W4Split::NTHR, 0, s>>>(L)
+    : gated ? wino_f4k3_kernel<W4Split, true><<<(unsigned)total, W4Split::NTHR, 0, s>>>(L)
+            : wino_f4k3_kernel<W4Split, false><<<(unsigned)total, W4Split::NTHR, 0, s>>>(L);
+  else if (quad)
     aff     ? wino_f4k3_kernel<W4Quad, false, true><<<(unsigned)total, W4Quad::NTHR, 0, s>>>(L)
     : gated ? wino_f4k3_kernel<W4Quad, true><<<(unsigned)total, W4Quad::NTHR, 0, s>>>(L)
             : wino_f4k3_kernel<W4Quad, false><<<(unsigned)total, W4Quad::NTHR, 0, s>>>(L);

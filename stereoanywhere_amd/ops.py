@@ -705,11 +705,13 @@ def conv2d_k3_narrow(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch
 class WinoFilters:
     """Transformed filters of one 3x3 conv for both fused Winograd kernels: ``u2`` for
     F(2x2,3x3) (conv2d_wino.hip), ``u4`` for F(4x4,3x3) (conv2d_wino4.hip) in 32-channel
-    blocks and ``u4w`` in the wide shape's 64-channel blocks (None unless Cout % 64 == 0)."""
-    __slots__ = ("u2", "u4", "u4w", "cin", "cout")
+    blocks, ``u4w`` in the wide shape's 64-channel blocks (None unless Cout % 64 == 0) and
+    ``u4s`` as the split kernel's f16 hi/lo pairs (None unless W4_SPLIT when derived)."""
+    __slots__ = ("u2", "u4", "u4w", "u4s", "cin", "cout")
 
-    def __init__(self, u2: torch.Tensor, u4: torch.Tensor, cin: int, cout: int, u4w: Optional[torch.Tensor] = None):
-        self.u2, self.u4, self.u4w, self.cin, self.cout = u2, u4, u4w, cin, cout
+    def __init__(self, u2: torch.Tensor, u4: torch.Tensor, cin: int, cout: int, u4w: Optional[torch.Tensor] = None,
+                 u4s: Optional[torch.Tensor] = None):
+        self.u2, self.u4, self.u4w, self.u4s, self.cin, self.cout = u2, u4, u4w, u4s, cin, cout
 
 
 # False keeps every 3x3 conv on the F(2x2,3x3) kernel (set by A/B scripts and tests)
@@ -724,6 +726,12 @@ W4_PERSIST = False
 # F(4x4) launches on the quadrant block shape (block_shape 4: 32 tiles x 64 output channels,
 # two waves per SIMD, each wave one quadrant of the 6 x 6 points) where every problem allows it
 W4_QUAD = False
+# F(4x4) launches of the default shape on the split kernel (block_shape 6): 4-channel chunks whose
+# Winograd-domain products run on v_mfma_f32_16x16x16_f16 with f16 hi/lo operand pairs (22
+# significant bits, exact f16 x f16 products, fp32 accumulation) instead of fp32 MFMA
+W4_SPLIT = False
+# the split filters need |U * 2^12| < 65504; |U| <= max |weight| for F(4x4,3x3)'s G
+_W4_SPLIT_WMAX = 15.99
 
 
 def wino_weights(weight: torch.Tensor) -> WinoFilters:
@@ -739,7 +747,13 @@ def wino_weights(weight: torch.Tensor) -> WinoFilters:
     if (W4_WIDE or W4_QUAD) and Cout % 64 == 0 and Cin % 8 == 0:   # the 64-channel layout only when it may run
         u4w = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.float32)
         N.call("sa_conv2d_wino4_weights_cb", weight.data_ptr(), Cout, Cin, 64, u4w.data_ptr(), _stream(weight))
-    return WinoFilters(u2, u4, Cin, Cout, u4w)
+    u4s = None
+    if W4_SPLIT and Cout % 32 == 0 and Cin % 8 == 0:
+        if float(weight.abs().max()) >= _W4_SPLIT_WMAX:
+            raise RuntimeError("wino_weights: |weight| >= 16 exceeds the split kernel's f16 filter range")
+        u4s = torch.empty((72 * Cin * Cout,), device=weight.device, dtype=torch.int32)
+        N.call("sa_conv2d_wino4_weights_split", weight.data_ptr(), Cout, Cin, u4s.data_ptr(), _stream(weight))
+    return WinoFilters(u2, u4, Cin, Cout, u4w, u4s)
 
 
 # largest Cin of an F(4x4,3x3) launch with an input transform (its (scale, shift) table fills the
@@ -777,7 +791,7 @@ _WINO4_MIN_BLOCKS = 384
 def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] = None, relu: bool = False,
                   out: Optional[torch.Tensor] = None, in_aff: Optional[Affine] = None, in_act=None,
                   stats: bool = False, f4: bool = False, out_cout: Optional[int] = None, wide: bool = False,
-                  width: Optional[int] = None):
+                  width: Optional[int] = None, split: bool = False):
     """out_cout: channels of ``out`` when the epilogue writes fewer than Cout there (gate mode 1).
     width: the image width when x (and out, and the gate planes) are PITCHED planes [.., H, P]
     whose columns width .. P - 1 are zero (F(4x4) only; the outputs' pad columns stay zero)."""
@@ -802,7 +816,7 @@ def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] 
     parts_fn = N.lib().sa_conv2d_k3_wino4_stat_parts if f4 else N.lib().sa_conv2d_k3_wino_stat_parts
     parts = int(parts_fn(H, W)) if stats else 0
     partial = torch.empty((B * Cout * parts * 2,), device=x.device, dtype=torch.float64) if stats else None
-    Uf = (U.u4w if wide else U.u4) if f4 else U.u2
+    Uf = (U.u4w if wide else U.u4s if split else U.u4) if f4 else U.u2
     prob = N.SaWinoProblem(x.data_ptr(), bs, B, Cin, H, W, Uf.data_ptr(), Cout, _ptr(bias),
                            1 if relu else 0, m, s, t, ps, ACT[in_act], out.data_ptr(), _plane_bs(out, "out"),
                            _ptr(partial), P if P != W else 0)
@@ -895,13 +909,15 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     wide = (f4 and (W4_QUAD or (W4_WIDE and not aff)) and not small_blocks
             and all(p["U"].u4w is not None for p in plain)
             and all(p["U"].cout % 128 == 0 for p in problems if p.get("gate") and p["gate"]["mode"] == 1))
-    built = [_wino_problem(**p, f4=f4, wide=wide) for p in plain]
-    arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
     persist = f4 and W4_PERSIST and not (small_blocks or wide)
-    if f4 and (gated or small_blocks or wide or persist):
+    split = (f4 and W4_SPLIT and not (small_blocks or wide or persist)
+             and all(p["U"].u4s is not None for p in plain))
+    built = [_wino_problem(**p, f4=f4, wide=wide, split=split) for p in plain]
+    arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
+    if f4 and (gated or small_blocks or wide or persist or split):
         gates = (N.SaGateEpilogue * len(built))(*[_gate_epilogue(p) if p.get("gate") else N.SaGateEpilogue()
                                                   for p in problems])
-        shape = (4 if W4_QUAD else 3) if wide else 2 if small_blocks else 5 if persist else 0
+        shape = (4 if W4_QUAD else 3) if wide else 2 if small_blocks else 5 if persist else 6 if split else 0
         N.call("sa_conv2d_k3_wino4_multi_gate", len(built), ctypes.addressof(arr), ctypes.addressof(gates),
                shape, _stream(problems[0]["x"]))
     else:

@@ -38,14 +38,18 @@ def test_tiny_case_and_intermediates(model):
     assert e < 1e-3
 
 
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("name,H,W,D,iters", [("cfg1_256x512_it8.npz", 256, 512, 64.0, 8),
                                                ("cfg2_544x960_it22.npz", 544, 960, 192.0, 22)])
-def test_end_to_end_vs_reference(model, name, H, W, D, iters):
+def test_end_to_end_vs_reference(model, monkeypatch, name, H, W, D, iters, split):
+    """split: every F(4x4) conv on the f16 hi/lo split kernel (ops.W4_SPLIT) or on fp32 MFMA."""
+    from stereoanywhere_amd import ops
+    monkeypatch.setattr(ops, "W4_SPLIT", split)
     fix = load_fixture(name)
     pair = regenerate_inputs(fix, 1, H, W, D)
     disp = run(model, pair, iters)
     e = epe(disp, fix["disparity"])
-    print(name, "EPE", e, "max", float(np.abs(disp - fix["disparity"]).max()))
+    print(name, "split" if split else "fp32", "EPE", e, "max", float(np.abs(disp - fix["disparity"]).max()))
     assert e < 1e-3
 
 

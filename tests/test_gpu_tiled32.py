@@ -44,8 +44,12 @@ def _inputs(fix, prefix, H, W, D, seed):
     return [torch.from_numpy(pair[k]).cuda() for k in ("left", "right", "mono_left", "mono_right")]
 
 
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("name", ["mb_tile", "booster_tile"])
-def test_tile_32_iterations_vs_reference(model, fix, name):
+def test_tile_32_iterations_vs_reference(model, fix, monkeypatch, name, split):
+    """split: the F(4x4) convs on the f16 hi/lo split kernel (ops.W4_SPLIT) or on fp32 MFMA."""
+    from stereoanywhere_amd import ops
+    monkeypatch.setattr(ops, "W4_SPLIT", split)
     H, W, seed = (int(v) for v in fix[f"{name}.geom"])
     x = _inputs(fix, name, H, W, float(fix[f"{name}.D"]), seed)
     # the 1/16 GRU level is ragged (W/16 = 42 or 70): padded planes on F(4x4)
@@ -54,7 +58,7 @@ def test_tile_32_iterations_vs_reference(model, fix, name):
         d = -model(*x, iters=32, test_mode=True)[0]
     got = d[0, 0, ::int(fix["row_step"])].cpu().numpy()
     e = epe(got, fix[f"{name}.out"])
-    print(name, "EPE", e, "max", float(np.abs(got - fix[f"{name}.out"]).max()))
+    print(name, "split" if split else "fp32", "EPE", e, "max", float(np.abs(got - fix[f"{name}.out"]).max()))
     assert np.isfinite(got).all()
     assert e < 1e-3
 

@@ -91,14 +91,18 @@ def _run(monkeypatch, on, *probs):
     return res, work
 
 
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("N,Cin,Cout,H,W", [(1, 8, 32, 8, 32), (2, 16, 64, 9, 36), (1, 64, 96, 17, 52),
                                             (2, 128, 256, 34, 60), (1, 256, 384, 20, 240), (3, 192, 128, 6, 8),
                                             (4, 128, 128, 68, 120), (2, 256, 128, 136, 240)])
-def test_wino4_matches_conv2d(monkeypatch, N, Cin, Cout, H, W):
+def test_wino4_matches_conv2d(monkeypatch, N, Cin, Cout, H, W, split):
+    """split: the f16 hi/lo split kernel (block_shape 6), under the same tolerance."""
+    monkeypatch.setattr(ops, "W4_SPLIT", split)
     x = rnd(N, Cin, H, W, seed=Cin + 1)
     w = rnd(Cout, Cin, 3, 3, seed=Cout + 1) / (3 * Cin ** 0.5)
     b = rnd(Cout, seed=8)
     U = ops.wino_weights(w)
+    assert (U.u4s is not None) == split
     for bias, relu in ((None, False), (b, True)):
         (got,), work = _run(monkeypatch, True, dict(x=x, U=U, bias=bias, relu=relu))
         assert "conv2d_wino4" in work and "conv2d_wino" not in work
@@ -111,7 +115,7 @@ def test_wino4_matches_conv2d(monkeypatch, N, Cin, Cout, H, W):
         assert err_max < 1e-4 * scale and err_rms < 1e-5 * scale, (err_max, err_rms)
 
 
-@pytest.mark.parametrize("small", [False, True, "quad"])
+@pytest.mark.parametrize("small", [False, True, "quad", "split"])
 def test_wino4_input_transform(monkeypatch, small):
     """The producer's norm + activation applied on load by the F(4x4) kernel (the LDS pass over
     each staged chunk): per-(image, channel) InstanceNorm + ReLU with output statistics on a
@@ -127,6 +131,7 @@ def test_wino4_input_transform(monkeypatch, small):
     xb, xc = r(3, 32, 20, 52) + 0.3, r(1, 64, 9, 36)
     quad = small == "quad"   # the quadrant shape (64 output channels per block)
     monkeypatch.setattr(ops, "W4_QUAD", quad)
+    monkeypatch.setattr(ops, "W4_SPLIT", small == "split")
     small = small is True
     wa, wb, wc = r(64, 64, 3, 3) / 24, r(128 if quad else 96, 32, 3, 3) / 17, r(64 if quad else 32, 64, 3, 3) / 24
     mean, rstd = ops.plane_stats(xa[:, 16:80])
@@ -215,7 +220,7 @@ def test_wino4_multi_stats_views(monkeypatch):
     torch.testing.assert_close(ye, F.conv2d(xe, wb, padding=1), atol=2e-5, rtol=1e-4)
 
 
-@pytest.mark.parametrize("wide", [False, True, "quad", "persist"])
+@pytest.mark.parametrize("wide", [False, True, "quad", "persist", "split"])
 def test_wino4_gru_gate_epilogues(monkeypatch, wide):
     """ConvGRU gates in the F(4x4) epilogue (update.py:16-27) against the reference's expressions
     in torch fp32: mode 1 (convz | convr over cat(h, x) -> z, r*h) on channel views of one
@@ -226,6 +231,7 @@ def test_wino4_gru_gate_epilogues(monkeypatch, wide):
     monkeypatch.setattr(ops, "W4_WIDE", wide is True)
     monkeypatch.setattr(ops, "W4_QUAD", wide == "quad")
     monkeypatch.setattr(ops, "W4_PERSIST", wide == "persist")
+    monkeypatch.setattr(ops, "W4_SPLIT", wide == "split")
     g = torch.Generator(device="cpu").manual_seed(42)
 
     def r(*s):
@@ -365,14 +371,15 @@ def _pitched(x, P):
     return out
 
 
-@pytest.mark.parametrize("persist", [False, True])
+@pytest.mark.parametrize("persist", [False, True, "split"])
 def test_wino4_pitched_planes(monkeypatch, persist):
     """F(4x4) on pitched planes (SaWinoProblem.pitch: widths 70 and 42 padded to 72 and 44, the
     booster / middlebury tiles' 1/16 GRU level): the convolution of the first W columns, the pad
     columns of the outputs left zero, InstanceNorm statistics over the W columns only, beside a
     dense problem in the same launch."""
     monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
-    monkeypatch.setattr(ops, "W4_PERSIST", persist)
+    monkeypatch.setattr(ops, "W4_PERSIST", persist is True)
+    monkeypatch.setattr(ops, "W4_SPLIT", persist == "split")
     g = torch.Generator(device="cpu").manual_seed(91)
 
     def r(*s):
@@ -401,11 +408,13 @@ def test_wino4_pitched_planes(monkeypatch, persist):
                                    atol=1e-4, rtol=1e-4)
 
 
-def test_wino4_pitched_gate_epilogues(monkeypatch):
+@pytest.mark.parametrize("split", [False, True])
+def test_wino4_pitched_gate_epilogues(monkeypatch, split):
     """The ConvGRU gate epilogues (modes 1 and 2) on a pitched level (W = 70 in rows of 72): the
     gate values of the W columns as in test_wino4_gru_gate_epilogues, the pad columns of z, r*h
     and the new state kept zero."""
     monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    monkeypatch.setattr(ops, "W4_SPLIT", split)
     g = torch.Generator(device="cpu").manual_seed(93)
 
     def r(*s):
@@ -455,3 +464,37 @@ def test_pool_interp_pitched():
     assert torch.equal(up_d, up_p)
     torch.testing.assert_close(up_d, F.interpolate(dense, size=(112, 140), mode="bilinear", align_corners=True),
                                atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("mag", [1e-4, 1e-2, 1.0, 30.0])
+def test_wino4_split_operand_range(monkeypatch, mag):
+    """The split kernel over the magnitudes its f16 hi/lo operands must carry: inputs scaled by
+    1e-4 (transformed values far below 2^-14, subnormal lo halves) up to 30 (|V| up to ~3000),
+    weights of 1e-3..1: error against the fp32 F(4x4) kernel and torch relative to the output's
+    scale as in test_wino4_matches_conv2d."""
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    for wmag in (1e-3, 1.0):
+        x = rnd(2, 64, 36, 120, seed=3) * mag
+        w = rnd(96, 64, 3, 3, seed=4) * wmag
+        monkeypatch.setattr(ops, "W4_SPLIT", True)
+        (ys,), _ = _run(monkeypatch, True, dict(x=x, U=ops.wino_weights(w)))
+        monkeypatch.setattr(ops, "W4_SPLIT", False)
+        (yf,), _ = _run(monkeypatch, True, dict(x=x, U=ops.wino_weights(w)))
+        ref = F.conv2d(x.double(), w.double(), padding=1).float()
+        scale = float(ref.pow(2).mean().sqrt())
+        es, ef = float((ys - ref).abs().max()) / scale, float((yf - ref).abs().max()) / scale
+        rs, rf = (float((y - ref).pow(2).mean().sqrt()) / scale for y in (ys, yf))
+        print(f"split operand range x~{mag} w~{wmag}: split max {es:.2e} rms {rs:.2e}, fp32 max {ef:.2e} rms {rf:.2e}")
+        assert es < 1e-4 and rs < 1e-5, (es, rs)
+
+
+def test_wino4_split_weights_range():
+    """Filters beyond the split kernel's f16 range are refused when derived, not overflowed."""
+    import stereoanywhere_amd.ops as o
+    old = o.W4_SPLIT
+    o.W4_SPLIT = True
+    try:
+        with pytest.raises(RuntimeError):
+            o.wino_weights(rnd(32, 8, 3, 3, seed=1) * 40)
+    finally:
+        o.W4_SPLIT = old
