@@ -46,6 +46,7 @@ sys.path.insert(0, ROOT)
 
 from stereoanywhere_amd import _native as N  # noqa: E402
 from stereoanywhere_amd import dist as D  # noqa: E402
+from stereoanywhere_amd import ops  # noqa: E402
 from stereoanywhere_amd import synth  # noqa: E402
 from stereoanywhere_amd.model import StereoAnywhere  # noqa: E402
 
@@ -278,7 +279,11 @@ def main():
                          "instrumented steps: rocprof per-launch times and PMC bytes comparable with the live ones)")
     ap.add_argument("--miopen-find", type=int, default=0,
                     help="let MIOpen time its conv algorithms per shape (torch cudnn.benchmark)")
+    ap.add_argument("--w4-split", type=int, default=None, choices=[0, 1],
+                    help="F(4x4) convs on the split kernel (1) or fp32 MFMA (0); default: ops.W4_SPLIT")
     args = ap.parse_args()
+    if args.w4_split is not None:
+        ops.W4_SPLIT = bool(args.w4_split)
 
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
     r = D.init_from_env("nccl")

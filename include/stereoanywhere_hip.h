@@ -384,9 +384,9 @@ int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, float *U4, v
 int sa_conv2d_wino4_weights_cb(const float *weight, int Cout, int Cin, int co_block, float *U4,
                                void *stream);
 /* U4 for the split block shape (block_shape 6 of sa_conv2d_k3_wino4_multi_gate: the Winograd-domain
- * products on f16 MFMA with hi/lo operand pairs): 72*Cin*Cout dwords laid out
- * [Cout/32][Cin/4][36][4][16][2][2], each dword the f16 pair (hi, lo) of U * 2^12 (hi in the low
- * half), stored twice.  Needs |weight| < 16 (U * 2^12 within the f16 range). */
+ * products on f16 MFMA with hi/lo operand pairs): 36*Cin*Cout dwords in U4's layout, each dword
+ * the f16 pair (hi, lo) of U * 2^12 (hi in the low half).  Needs |weight| < 16 (U * 2^12
+ * within the f16 range). */
 int sa_conv2d_wino4_weights_split(const float *weight, int Cout, int Cin, void *U4s, void *stream);
 long sa_conv2d_k3_wino4_stat_parts(int H, int W);
 int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, void *stream);

@@ -90,8 +90,8 @@ struct W4Cfg {
   static constexpr int CO = CO_, CG = CO_ / 16;                // output channels per block, 16-channel groups
   static constexpr int SB = 4 * CO_;                        // filters per (point, 4-channel job): [k][n][g]
   static constexpr int PS_MAX = NT == 64 ? 340 : 204;       // (BH + 2)(BW / 4 + 2), largest geometry
-  static constexpr int PBUF = (KC * PS_MAX + 32) * 4;       // + the last DMA's idle lanes
-  static constexpr int UBUF = NPT * KC * CO * (SPLIT_ ? 2 : 1);   // filters per chunk (dwords)
+  static constexpr int PBUF = (KC * PS_MAX + 63) / 64 * 64 * 4;   // whole DMA pieces (the last one's idle lanes write zeros)
+  static constexpr int UBUF = NPT * KC * CO;                // filters per chunk (dwords)
   static constexpr int BUF = PBUF + UBUF;                   // one buffer: patch, then filters
   static constexpr int OPP = NT * 16 + 4;                   // output staging plane pitch (4 mod 32)
   static constexpr int SMEM = 2 * BUF > CO * OPP ? 2 * BUF : CO * OPP;
@@ -121,19 +121,24 @@ using W4Wide = W4Cfg<4, 4, 64>;
 // ds_read_b128 instead of two ds_read_b64 per four MFMAs.  The price: a barrier per 4 input
 // channels and four partial output transforms meeting in LDS.
 using W4Quad = W4Cfg<8, 4, 64, true>;
-// Split: the 8-wave shape with 4-channel chunks whose Winograd-domain products run on
+#ifndef W4S_KC
+#define W4S_KC 8   // the split kernel's input-channel chunk (4: twice the barriers, measured slower)
+#endif
+// Split: the 8-wave shape (8- or 4-channel chunks) whose Winograd-domain products run on
 // v_mfma_f32_16x16x16_f16 instead of v_mfma_f32_16x16x4_f32.  Each operand is an f16 hi/lo
 // pair (x = hi + lo, 22 significant bits; filters scaled by 2^W4S_LOG2 before the split and
 // the accumulators by 2^-W4S_LOG2 after the main loop, both exact), and one MFMA's K = 16
 // slots hold a lane's channel as the four products hi*bhi + hi*blo + lo*bhi + lo*blo: the A
 // operand (hi, hi, lo, lo) is the lane's transformed value (3 VALU to split), the B operand
-// (bhi, blo, bhi, blo) is staged that way in LDS (sa_conv2d_wino4_weights_split), so one
-// ds_read_b128 gives a lane both output-channel groups' operands.  Products of f16 pairs are
+// (bhi, blo, bhi, blo) is the filter's (bhi, blo) dword twice: the LDS image holds each pair
+// once (sa_conv2d_wino4_weights_split; the same bytes per chunk as the fp32 filters, so the
+// same L2 -> LDS intake per channel, which bounds this kernel family), one ds_read_b64 gives a
+// lane both output-channel groups' pairs, and the copy is a register move.  Products of f16 pairs are
 // exact in fp32, so the result differs from the fp32 kernel only by the operands' rounding
 // (<= 2^-22 relative; below 2^-14 the lo halves are subnormal, an absolute 2^-25) and the
 // accumulation order.  |V| must stay below 65504 (the f16 range): V = B^T d B grows at most
 // 100-fold over the input patch.
-using W4Split = W4Cfg<8, 4, 32, false, true>;
+using W4Split = W4Cfg<8, W4S_KC, 32, false, true>;
 constexpr int W4S_LOG2 = 12;
 static_assert(2 * W4Small::SMEM * 4 <= 160 * 1024, "two small blocks per CU");
 static_assert(W4Wide::SMEM * 4 <= 160 * 1024, "one wide block per CU");
@@ -475,9 +480,9 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
                 UDMA = C::UDMA, UPW = C::UPW, UBUF = C::UBUF, BUF = C::BUF, PBUF = C::PBUF, OPP = C::OPP,
                 CO = C::CO, CG = C::CG, SB = C::SB, NR = C::NR;
   constexpr bool QUAD = C::QUAD, SPLIT = C::SPLIT;
-  static_assert(!SPLIT || (!QUAD && !PERSIST && KC == 4 && CG == 2), "split: the 8-wave 4-channel 32-channel shape");
-  // a lane's filter operands of a point: one float per group, or (split) two f16 pairs per group
-  using f32xg = std::conditional_t<SPLIT, f32x4, float __attribute__((ext_vector_type(CG)))>;
+  static_assert(!SPLIT || (!QUAD && !PERSIST && CG == 2), "split: the 8-wave 32-channel shape");
+  // a lane's filter operands of a point: one float, or (split) one f16 (hi, lo) pair, per group
+  using f32xg = float __attribute__((ext_vector_type(CG)));
   const int Cin = P.Cin, H = P.H;
   // block geometry as compile-time constants (the patch offsets divide by PS and PG)
   constexpr int ltw = LTW, tw = 1 << ltw, tr = NT >> ltw;
@@ -504,16 +509,14 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
       const_cast<float *>(P.in + (long)n * P.in_bs), (short)0, Cin * hw * 4, 0x00020000);
   // the filters' global layout has 8-channel chunks (sa_conv2d_wino4_weights); a 4-channel
   // chunk is every other SB-float piece of one (the DMA gathers it by its source addresses)
-  constexpr int UW = SPLIT ? 2 : 1;   // dwords per filter value
   const __amdgpu_buffer_rsrc_t uin = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float *>(P.U + (long)cb * Cin * NPT * CO * UW), (short)0, Cin * NPT * CO * 4 * UW, 0x00020000);
-  // (the split layout is one contiguous LDS image per 4-channel chunk)
+      const_cast<float *>(P.U + (long)cb * Cin * NPT * CO), (short)0, Cin * NPT * CO * 4, 0x00020000);
   auto u_src = [&](int piece) {   // byte offset of this lane's 16 bytes of filter DMA piece `piece`
     const int f = piece * 256 + lane * 4;
-    return (JPC == 2 || SPLIT ? f : f + (f / SB) * SB) * 4;
+    return (JPC == 2 ? f : f + (f / SB) * SB) * 4;
   };
   auto u_chunk = [&](int chunk) {   // byte offset of a chunk's filters
-    return JPC == 2 || SPLIT ? chunk * UBUF * 4 : (chunk >> 1) * 2 * UBUF * 4 + (chunk & 1) * SB * 4;
+    return JPC == 2 ? chunk * UBUF * 4 : (chunk >> 1) * 2 * UBUF * 4 + (chunk & 1) * SB * 4;
   };
 
   // patch DMA: the chunk's image is [channel][PR rows][PG groups of 4 floats], dense, starting
@@ -573,7 +576,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   int PSv = PS, PGv = PG;
   asm volatile("" : "+s"(PSv), "+s"(PGv));
   const int pread = k * PSv * 4 + 4 * trow * PGv * 4 + 4 * tcol + 2;
-  const int uread = (k * 16 + m) * (SPLIT ? 4 : CG);
+  const int uread = (k * 16 + m) * CG;
 
   // acc[i][jj][g]: point (row i, or 3 RH + i in a quadrant; column 3 HF + jj) of output-channel
   // group g
@@ -660,8 +663,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
     auto load_b = [&](int s, int jj, f32xg *b) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < NR; ++i)
-        b[i] = *reinterpret_cast<const f32xg *>(
-            ub + (SPLIT ? (6 * i + 3 * HF + jj) * 256 : ((6 * (QUAD ? 3 * RH + i : i) + 3 * HF + jj) * JPC + s) * SB));
+        b[i] = *reinterpret_cast<const f32xg *>(ub + ((6 * (QUAD ? 3 * RH + i : i) + 3 * HF + jj) * JPC + s) * SB);
     };
     load_rows(0, 0, 6);
     load_b(0, 0, bc);
@@ -694,11 +696,10 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
 #pragma unroll
           for (int i = 0; i < NR; ++i) {
             const f16x4 a = w4_split(v[i]);
-            const f16x8 bb = __builtin_bit_cast(f16x8, bc[i]);
-            acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x16f16(a, __builtin_shufflevector(bb, bb, 0, 1, 2, 3),
-                                                                  acc[i][jj][0], 0, 0, 0);
-            acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x16f16(a, __builtin_shufflevector(bb, bb, 4, 5, 6, 7),
-                                                                  acc[i][jj][1], 0, 0, 0);
+            const f16x4 b0 = __builtin_bit_cast(f16x4, f32x2{bc[i][0], bc[i][0]});
+            const f16x4 b1 = __builtin_bit_cast(f16x4, f32x2{bc[i][1], bc[i][1]});
+            acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x16f16(a, b0, acc[i][jj][0], 0, 0, 0);
+            acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x16f16(a, b1, acc[i][jj][1], 0, 0, 0);
           }
         } else {
 #pragma unroll
@@ -1056,11 +1057,9 @@ __global__ __launch_bounds__(256) void wino4_weights_kernel(const float *__restr
 }
 
 // Filters of the split kernel (W4Split): U = G g G^T in fp64, times 2^W4S_LOG2, as the f16
-// pair hi = f16(u), lo = f16(u - hi) in one dword (hi in the low half), stored twice (the B
-// operand (bhi, blo, bhi, blo) of v_mfma_f32_16x16x16_f16).  Layout
-// [Cout/32][Cin/4][36][4][16][2][2] dwords: per (output block, 4-channel chunk) one contiguous
-// 36 KiB image of the LDS filter buffer; channel ci = 4 chunk + k, output co = 32 cb + 16 g + n
-// at [k][n][g].
+// pair hi = f16(u), lo = f16(u - hi) in one dword (hi in the low half), in the fp32 filters'
+// layout (wino4_weights_kernel: [Cout/32][Cin/8][36][2][4][16][2], 4-channel chunks gathered
+// from it as there).
 __global__ __launch_bounds__(256) void wino4s_weights_kernel(const float *__restrict__ w, int Cout, int Cin,
                                                              unsigned *__restrict__ U) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1076,7 +1075,7 @@ __global__ __launch_bounds__(256) void wino4s_weights_kernel(const float *__rest
   double t[6][3];
   for (int a = 0; a < 6; ++a)
     for (int c = 0; c < 3; ++c) t[a][c] = G[a][0] * g[c] + G[a][1] * g[3 + c] + G[a][2] * g[6 + c];
-  const int chunk = ci / 4, k = ci % 4, cb = co / 32, gg = (co % 32) / 16, n = co % 16;
+  const int chunk = ci / 8, s = (ci % 8) / 4, k = ci % 4, cb = co / 32, gg = (co % 32) / 16, n = co % 16;
   for (int a = 0; a < 6; ++a)
     for (int b = 0; b < 6; ++b) {
       const double u = (t[a][0] * G[b][0] + t[a][1] * G[b][1] + t[a][2] * G[b][2]) * (double)(1 << W4S_LOG2);
@@ -1085,9 +1084,7 @@ __global__ __launch_bounds__(256) void wino4s_weights_kernel(const float *__rest
       const unsigned pr = (unsigned)__builtin_bit_cast(unsigned short, hi) |
                           ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
       const int pt = 6 * a + b;
-      unsigned *d = U + ((((((long)cb * (Cin / 4) + chunk) * NPT + pt) * 4 + k) * 16 + n) * 2 + gg) * 2;
-      d[0] = pr;
-      d[1] = pr;
+      U[(((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 2 + s) * 4 + k) * 32 + n * 2 + gg] = pr;
     }
 }
 
@@ -1177,7 +1174,7 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
                "sa_conv2d_k3_wino4: an input transform needs the 8-wave, quadrant or 4-wave shape and Cin <= %d",
                aff_max);
     aff = aff || qaff;
-    SA_REQUIRE((long)q.Cin * q.H * pitch * 4 < (1L << 31) - 64 && 36L * q.Cin * q.Cout * (split ? 8 : 4) < (1L << 31),
+    SA_REQUIRE((long)q.Cin * q.H * pitch * 4 < (1L << 31) - 64 && 36L * q.Cin * q.Cout * 4 < (1L << 31),
                "sa_conv2d_k3_wino4: an image or the filter bank exceeds the 2 GB buffer-descriptor range");
     const int ltw = w4_ltw(q.H, q.W), bw = 4 << ltw, bh = 4 * (nt >> ltw);
     const int tiles_w = (q.W + bw - 1) / bw, tiles_h = (q.H + bh - 1) / bh;

@@ -726,10 +726,11 @@ W4_PERSIST = False
 # F(4x4) launches on the quadrant block shape (block_shape 4: 32 tiles x 64 output channels,
 # two waves per SIMD, each wave one quadrant of the 6 x 6 points) where every problem allows it
 W4_QUAD = False
-# F(4x4) launches of the default shape on the split kernel (block_shape 6): 4-channel chunks whose
-# Winograd-domain products run on v_mfma_f32_16x16x16_f16 with f16 hi/lo operand pairs (22
-# significant bits, exact f16 x f16 products, fp32 accumulation) instead of fp32 MFMA
-W4_SPLIT = False
+# F(4x4) launches of the default shape on the split kernel (block_shape 6): the Winograd-domain
+# products on v_mfma_f32_16x16x16_f16 with f16 hi/lo operand pairs (22 significant bits, exact
+# f16 x f16 products, fp32 accumulation) instead of fp32 MFMA: 1.06-1.22x per conv, 54.3 -> 60.4
+# pairs/s at configs[1] with EPE vs the reference 1.78e-5 (fp32 MFMA: 1.84e-5)
+W4_SPLIT = True
 # the split filters need |U * 2^12| < 65504; |U| <= max |weight| for F(4x4,3x3)'s G
 _W4_SPLIT_WMAX = 15.99
 
@@ -751,7 +752,7 @@ def wino_weights(weight: torch.Tensor) -> WinoFilters:
     if W4_SPLIT and Cout % 32 == 0 and Cin % 8 == 0:
         if float(weight.abs().max()) >= _W4_SPLIT_WMAX:
             raise RuntimeError("wino_weights: |weight| >= 16 exceeds the split kernel's f16 filter range")
-        u4s = torch.empty((72 * Cin * Cout,), device=weight.device, dtype=torch.int32)
+        u4s = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.int32)
         N.call("sa_conv2d_wino4_weights_split", weight.data_ptr(), Cout, Cin, u4s.data_ptr(), _stream(weight))
     return WinoFilters(u2, u4, Cin, Cout, u4w, u4s)
 
