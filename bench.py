@@ -54,6 +54,9 @@ PUBLISHED = dict(use_truncate_vol=True, use_aggregate_mono_vol=True, vol_n_masks
                  vol_downsample=0, mirror_conf_th=0.98, mirror_attenuation=0.9, lrc_th=1.0, normal_gain=10)
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8 TB/s spec
 FP32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_*_f32 dense peak
+# fp32 products as f16 hi/lo pairs on v_mfma_f32_16x16x16_f16: 4 f16 products per fp32 product at
+# half the f16 MFMA peak (the 16x16x16 form issues at 16 cycles per SIMD, scripts/micro/mfma_rate.hip)
+SPLIT_MFMA_PEAK_TFS = 2 * FP32_MFMA_PEAK_TFS
 
 
 def step_costs(B: int, H4: int, W4: int, iters: int, C: int = 256):
@@ -429,6 +432,10 @@ def main():
         secs = ms_tot / 1e3 / args.steps                      # per step
         if unit == "TFLOP/s":
             ach, peak, bound = amount / secs / 1e12, FP32_MFMA_PEAK_TFS, "mfma"
+            if k == "conv2d_wino4" and ops.W4_SPLIT:
+                # the split kernel's products: v_mfma_f32_16x16x16_f16 (16 cycles per SIMD) carries
+                # one 16x16x4 fp32 MFMA's products as hi/lo pairs (32 cycles): twice the fp32 rate
+                peak = SPLIT_MFMA_PEAK_TFS
         else:
             ach, peak, bound = amount / secs / 1e9, HBM_PEAK_GBS, "hbm"
         kernels[k] = {"bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
@@ -454,7 +461,10 @@ def main():
                          "fp32 FMA peak 157.3 TF/s is the same for MFMA (v_mfma_f32_*_f32) and VALU; "
                          "conv2d_wino / conv2d_wino4 count the Winograd-domain products they execute "
                          "(16/36 resp. 36/144 of the direct convolution's), so their direct-equivalent "
-                         "rates are 2.25x resp. 4x achieved"})
+                         "rates are 2.25x resp. 4x achieved"
+                         + ("; conv2d_wino4 runs the split kernel (ops.W4_SPLIT): its peak is the "
+                            "fp32-product rate of v_mfma_f32_16x16x16_f16 on hi/lo pairs, 2x the fp32 "
+                            "MFMA peak" if ops.W4_SPLIT else "")})
     if tiled is None:
         metric, unit = "stereo pairs/sec @540x960 D=192 (1/2/4/8 GPU) + EPE vs reference", "pairs/s"
         config = {"workload": f"configs[1]: batch {args.batch}/GPU x {H}x{W} (padded {Hp}x{Wp}), "
@@ -473,7 +483,9 @@ def main():
     res = {
         "metric": metric, "value": total_units / elapsed, "unit": unit, "n_gpus": r.world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded value-noise pairs, "
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": ("f32 (F(4x4) Winograd-domain products as exact f16 hi/lo pair products on MFMA, fp32 "
+                  "accumulation; everything else fp32)" if ops.W4_SPLIT else "f32"), "data": "synthetic (seeded value-noise pairs, "
         "seeded random weights; no dataset/checkpoint offline)",
         "config": config, "roofline": roof, "gathered_units": int(allm.shape[0]),
         "execution": ("hipGraph replay of the whole forward (stereoanywhere_amd.graph.ForwardGraph; inputs "

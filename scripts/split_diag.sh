@@ -6,7 +6,7 @@ R=$GRAFT_REPO_ROOT
 cd $R
 mkdir -p gpurun_out/diag
 timeout -k 10 60 ./scripts/micro/mfma_rate > gpurun_out/diag/mfma_rate.log 2>&1 || exit 1
-for v in in-tree variants/d2.so variants/d3.so variants/d5.so variants/d7.so variants/d8.so; do
+for v in in-tree variants/d2.so variants/d3.so variants/d5.so variants/d8.so; do
   echo "== $v" >> gpurun_out/diag/variants.log
   if [ "$v" = in-tree ]; then
     timeout -k 10 120 python scripts/bench_conv2d.py --split --shape=xc08 --shape=hzr08 --shape=fnet.layer1 >> gpurun_out/diag/variants.log 2>&1 || exit 1

@@ -124,6 +124,10 @@ using W4Quad = W4Cfg<8, 4, 64, true>;
 #ifndef W4S_KC
 #define W4S_KC 8   // the split kernel's input-channel chunk (4: twice the barriers, measured slower)
 #endif
+#ifndef W4S_K32
+#define W4S_K32 0  // 1: plain launches take the products of both of a lane's channels on one v_mfma_f32_16x16x32_f16 (1.02-1.03x on the plain convs, but the gated / input-transform kernels then spill or read the filters as 2 x b32: forward 66.2 -> 72.4 ms)
+#endif
+static_assert(!W4S_K32 || W4S_KC == 8, "the K = 32 split form takes a lane's two channels of an 8-channel chunk");
 // Split: the 8-wave shape (8- or 4-channel chunks) whose Winograd-domain products run on
 // v_mfma_f32_16x16x16_f16 instead of v_mfma_f32_16x16x4_f32.  Each operand is an f16 hi/lo
 // pair (x = hi + lo, 22 significant bits; filters scaled by 2^W4S_LOG2 before the split and
@@ -192,6 +196,20 @@ __device__ __forceinline__ f16x4 w4_split(const float x) {
   asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(__builtin_bit_cast(unsigned, hh)), "v"(x));
   const f16x2 ll = __builtin_convertvector(f32x2{l, l}, f16x2);
   return __builtin_shufflevector(hh, ll, 0, 1, 2, 3);
+}
+
+// x0, x1 as the A operand (hi0, hi0, hi1, hi1, lo0, lo0, lo1, lo1) of v_mfma_f32_16x16x32_f16
+// (the B operand (p0, p1, p0, p1) with p = (bhi, blo): the four products of each channel)
+[[maybe_unused]] __device__ __forceinline__ f16x8 w4_split2(const float x0, const float x1) {
+  const f16x2 h0 = __builtin_convertvector(f32x2{x0, x0}, f16x2);
+  const f16x2 h1 = __builtin_convertvector(f32x2{x1, x1}, f16x2);
+  float l0, l1;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l0) : "v"(__builtin_bit_cast(unsigned, h0)), "v"(x0));
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l1) : "v"(__builtin_bit_cast(unsigned, h1)), "v"(x1));
+  const f16x2 g0 = __builtin_convertvector(f32x2{l0, l0}, f16x2);
+  const f16x2 g1 = __builtin_convertvector(f32x2{l1, l1}, f16x2);
+  return __builtin_shufflevector(__builtin_shufflevector(h0, h1, 0, 1, 2, 3), __builtin_shufflevector(g0, g1, 0, 1, 2, 3),
+                                 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, float *lds, int voff, int soff) {
@@ -663,8 +681,54 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
     auto load_b = [&](int s, int jj, f32xg *b) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < NR; ++i)
-        b[i] = *reinterpret_cast<const f32xg *>(ub + ((6 * (QUAD ? 3 * RH + i : i) + 3 * HF + jj) * JPC + s) * SB);
+        if constexpr (SPLIT && W4S_K32) {   // the K = 32 filter image [point][k][n][g][s], per channel
+          const float *q = smem + cur * BUF + PBUF + (k * 16 + m) * 4 + (6 * i + 3 * HF + jj) * 256 + s;
+          b[i] = f32xg{q[0], q[2]};
+        } else {
+          b[i] = *reinterpret_cast<const f32xg *>(ub + ((6 * (QUAD ? 3 * RH + i : i) + 3 * HF + jj) * JPC + s) * SB);
+        }
     };
+    if constexpr (SPLIT && W4S_K32 && !GATED && !AFF) {   // (the gated and input-transform kernels keep the per-channel form: with it they do not spill)
+      // Both jobs' row passes, then per point column one v_mfma_f32_16x16x32_f16 per output
+      // group over the lane's two channels (k, k + 4): half the MFMAs of the per-channel form
+      // and one 64-bit register copy per group for the B operand's repeat.  The filter image is
+      // [point][k][n][g][s] (sa_conv2d_wino4_weights_split): a lane's (p_s0, p_s1) pair of a
+      // group is one ds_read_b64.
+      const float *us = smem + cur * BUF + PBUF + (k * 16 + m) * 4;
+      float t0[6][3], t1[6][3];
+      load_rows(0, 0, 6);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t0[r]);
+      load_rows(1, 0, 6);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t1[r]);
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) {
+        float v0[6], v1[6];
+        bt6(t0[0][jj], t0[1][jj], t0[2][jj], t0[3][jj], t0[4][jj], t0[5][jj], v0);
+        bt6(t1[0][jj], t1[1][jj], t1[2][jj], t1[3][jj], t1[4][jj], t1[5][jj], v1);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const float *pp = us + (6 * i + 3 * HF + jj) * 256;
+          const f32x2 q0 = *reinterpret_cast<const f32x2 *>(pp), q1 = *reinterpret_cast<const f32x2 *>(pp + 2);
+          const f16x8 a = w4_split2(v0[i], v1[i]);
+          const f16x8 b0 = __builtin_bit_cast(f16x8, f32x4{q0.x, q0.y, q0.x, q0.y});
+          const f16x8 b1 = __builtin_bit_cast(f16x8, f32x4{q1.x, q1.y, q1.x, q1.y});
+          acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b0, acc[i][jj][0], 0, 0, 0);
+          acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b1, acc[i][jj][1], 0, 0, 0);
+        }
+#if SA_W4_FENCE
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+        if (SA_W4_DIAG == 0 && SA_W4_SPREAD && kc + 1 < nchunks) {
+          issue_part(kc + 1, cur ^ 1, jj);
+#if SA_W4_FENCE
+          __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+      }
+      continue;
+    }
     load_rows(0, 0, 6);
     load_b(0, 0, bc);
 #pragma unroll
@@ -1057,9 +1121,9 @@ __global__ __launch_bounds__(256) void wino4_weights_kernel(const float *__restr
 }
 
 // Filters of the split kernel (W4Split): U = G g G^T in fp64, times 2^W4S_LOG2, as the f16
-// pair hi = f16(u), lo = f16(u - hi) in one dword (hi in the low half), in the fp32 filters'
-// layout (wino4_weights_kernel: [Cout/32][Cin/8][36][2][4][16][2], 4-channel chunks gathered
-// from it as there).
+// pair hi = f16(u), lo = f16(u - hi) in one dword (hi in the low half): for the K = 32 form
+// [Cout/32][Cin/8][36][4][16][2][2] (channel 8 chunk + 4 s + k, output co = 32 cb + 16 g + n at
+// [k][n][g][s]), otherwise in the fp32 filters' layout (wino4_weights_kernel).
 __global__ __launch_bounds__(256) void wino4s_weights_kernel(const float *__restrict__ w, int Cout, int Cin,
                                                              unsigned *__restrict__ U) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1084,7 +1148,10 @@ __global__ __launch_bounds__(256) void wino4s_weights_kernel(const float *__rest
       const unsigned pr = (unsigned)__builtin_bit_cast(unsigned short, hi) |
                           ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
       const int pt = 6 * a + b;
-      U[(((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 2 + s) * 4 + k) * 32 + n * 2 + gg] = pr;
+      if (W4S_K32)   // [Cout/32][Cin/8][36][4][16][2][2]: channel 8 chunk + 4 s + k at [k][n][g][s]
+        U[(((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 4 + k) * 16 + n) * 4 + gg * 2 + s] = pr;
+      else
+        U[(((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 2 + s) * 4 + k) * 32 + n * 2 + gg] = pr;
     }
 }
 
