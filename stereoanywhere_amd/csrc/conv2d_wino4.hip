@@ -125,7 +125,7 @@ using W4Quad = W4Cfg<8, 4, 64, true>;
 #define W4S_KC 8   // the split kernel's input-channel chunk (4: twice the barriers, measured slower)
 #endif
 #ifndef W4S_K32
-#define W4S_K32 0  // 1: plain launches take the products of both of a lane's channels on one v_mfma_f32_16x16x32_f16 (1.02-1.03x on the plain convs, but the gated / input-transform kernels then spill or read the filters as 2 x b32: forward 66.2 -> 72.4 ms)
+#define W4S_K32 0  // 2: the paired form (both of a lane's channels per MFMA pair, hi then lo halves: no operand copies; 268 instead of ~375 VALU per chunk and wave, 1.0-1.06x on plain convs, but the forward 66.7 -> 68.3 ms);  1: plain launches take the products of both of a lane's channels on one v_mfma_f32_16x16x32_f16 (1.02-1.03x on the plain convs, but the gated / input-transform kernels then spill or read the filters as 2 x b32: forward 66.2 -> 72.4 ms)
 #endif
 static_assert(!W4S_K32 || W4S_KC == 8, "the K = 32 split form takes a lane's two channels of an 8-channel chunk");
 // Split: the 8-wave shape (8- or 4-channel chunks) whose Winograd-domain products run on
@@ -688,7 +688,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
           b[i] = *reinterpret_cast<const f32xg *>(ub + ((6 * (QUAD ? 3 * RH + i : i) + 3 * HF + jj) * JPC + s) * SB);
         }
     };
-    if constexpr (SPLIT && W4S_K32 && !GATED && !AFF) {   // (the gated and input-transform kernels keep the per-channel form: with it they do not spill)
+    if constexpr (SPLIT && W4S_K32 && ((!GATED && !AFF) || W4S_K32 == 2)) {   // (the gated and input-transform kernels keep the per-channel form: with it they do not spill)
       // Both jobs' row passes, then per point column one v_mfma_f32_16x16x32_f16 per output
       // group over the lane's two channels (k, k + 4): half the MFMAs of the per-channel form
       // and one 64-bit register copy per group for the B operand's repeat.  The filter image is
@@ -712,10 +712,21 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
           const float *pp = us + (6 * i + 3 * HF + jj) * 256;
           const f32x2 q0 = *reinterpret_cast<const f32x2 *>(pp), q1 = *reinterpret_cast<const f32x2 *>(pp + 2);
           const f16x8 a = w4_split2(v0[i], v1[i]);
-          const f16x8 b0 = __builtin_bit_cast(f16x8, f32x4{q0.x, q0.y, q0.x, q0.y});
-          const f16x8 b1 = __builtin_bit_cast(f16x8, f32x4{q1.x, q1.y, q1.x, q1.y});
-          acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b0, acc[i][jj][0], 0, 0, 0);
-          acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b1, acc[i][jj][1], 0, 0, 0);
+          if (W4S_K32 == 2) {
+            // paired: the B operand (p_s0, p_s1) of a group as loaded (no copies), once with the
+            // hi halves (hi0, hi0, hi1, hi1) and once with the lo halves of both channels
+            const f16x4 ah = __builtin_shufflevector(a, a, 0, 1, 2, 3), al = __builtin_shufflevector(a, a, 4, 5, 6, 7);
+            const f16x4 b0 = __builtin_bit_cast(f16x4, q0), b1 = __builtin_bit_cast(f16x4, q1);
+            acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, b0, acc[i][jj][0], 0, 0, 0);
+            acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, b1, acc[i][jj][1], 0, 0, 0);
+            acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x16f16(al, b0, acc[i][jj][0], 0, 0, 0);
+            acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x16f16(al, b1, acc[i][jj][1], 0, 0, 0);
+          } else {
+            const f16x8 b0 = __builtin_bit_cast(f16x8, f32x4{q0.x, q0.y, q0.x, q0.y});
+            const f16x8 b1 = __builtin_bit_cast(f16x8, f32x4{q1.x, q1.y, q1.x, q1.y});
+            acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b0, acc[i][jj][0], 0, 0, 0);
+            acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b1, acc[i][jj][1], 0, 0, 0);
+          }
         }
 #if SA_W4_FENCE
         __builtin_amdgcn_sched_barrier(0);
