@@ -688,7 +688,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
           b[i] = *reinterpret_cast<const f32xg *>(ub + ((6 * (QUAD ? 3 * RH + i : i) + 3 * HF + jj) * JPC + s) * SB);
         }
     };
-    if constexpr (SPLIT && W4S_K32 && ((!GATED && !AFF) || W4S_K32 == 2)) {   // (the gated and input-transform kernels keep the per-channel form: with it they do not spill)
+    if constexpr (SPLIT && W4S_K32 && ((!GATED && !AFF) || W4S_K32 >= 2)) {   // (the gated and input-transform kernels keep the per-channel form: with it they do not spill)
       // Both jobs' row passes, then per point column one v_mfma_f32_16x16x32_f16 per output
       // group over the lane's two channels (k, k + 4): half the MFMAs of the per-channel form
       // and one 64-bit register copy per group for the B operand's repeat.  The filter image is
@@ -697,9 +697,20 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
       const float *us = smem + cur * BUF + PBUF + (k * 16 + m) * 4;
       float t0[6][3], t1[6][3];
       load_rows(0, 0, 6);
+      if (W4S_K32 == 3) {
+        // channel k + 4's rows go out into the slots channel k's row pass has consumed, in
+        // two halves, so their reads overlap that row pass instead of following it
 #pragma unroll
-      for (int r = 0; r < 6; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t0[r]);
-      load_rows(1, 0, 6);
+        for (int r = 0; r < 3; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t0[r]);
+        load_rows(1, 0, 3);
+#pragma unroll
+        for (int r = 3; r < 6; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t0[r]);
+        load_rows(1, 3, 6);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t0[r]);
+        load_rows(1, 0, 6);
+      }
 #pragma unroll
       for (int r = 0; r < 6; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t1[r]);
 #pragma unroll
@@ -712,7 +723,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
           const float *pp = us + (6 * i + 3 * HF + jj) * 256;
           const f32x2 q0 = *reinterpret_cast<const f32x2 *>(pp), q1 = *reinterpret_cast<const f32x2 *>(pp + 2);
           const f16x8 a = w4_split2(v0[i], v1[i]);
-          if (W4S_K32 == 2) {
+          if (W4S_K32 >= 2) {
             // paired: the B operand (p_s0, p_s1) of a group as loaded (no copies), once with the
             // hi halves (hi0, hi0, hi1, hi1) and once with the lo halves of both channels
             const f16x4 ah = __builtin_shufflevector(a, a, 0, 1, 2, 3), al = __builtin_shufflevector(a, a, 4, 5, 6, 7);
