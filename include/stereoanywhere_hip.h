@@ -438,6 +438,13 @@ long sa_conv_direct_stat_parts(int Ho, int Wo);
 int sa_conv_direct(const float *in, long in_bs, int N, int Cin, int H, int W, int K, int S, const float *wg,
                    const float *wd, int Cout, float *out, long out_bs, float *out_ds, long out_ds_bs,
                    double *part, double *part_ds, void *stream);
+/* The same convolutions with the products as exact f16 hi/lo pair products on MFMA (fp32
+ * accumulation): wg / wd from sa_conv_direct_weights_split, which turns n arranged weights into
+ * n dwords, the f16 pair (hi, lo) of w * 2^12 (needs |w| < 16). */
+int sa_conv_direct_weights_split(const float *arranged, long n, void *out, void *stream);
+int sa_conv_direct_split(const float *in, long in_bs, int N, int Cin, int H, int W, int K, int S, const void *wg,
+                         const void *wd, int Cout, float *out, long out_bs, float *out_ds, long out_ds_bs,
+                         double *part, double *part_ds, void *stream);
 
 /* Epilogues of the MIOpen 2-D convs (encoders extractor.py:6-300, update block update.py:64-110).
  * sa_plane_stats: InstanceNorm2d statistics (biased variance, eps) of each (b, c) plane of

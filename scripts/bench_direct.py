@@ -40,6 +40,16 @@ def main():
             wdr = torch.randn(Cout, Cin, 1, 1, device=dev) / Cin ** 0.5
             wd = ops.conv_direct_weights(wdr, S, with_ds=True)
         t = timeit(lambda: ops.conv_direct(x, wg, K, S, Cout, wd=wd))
+        if "--split" in sys.argv:   # fp32 products vs the split kernel (ops.DIRECT_SPLIT)
+            res = {}
+            for sp in (False, True):
+                ops.DIRECT_SPLIT = sp
+                g_ = ops.conv_direct_weights(w, S)
+                d_ = ops.conv_direct_weights(wdr, S, with_ds=True) if S == 2 else None
+                res[sp] = timeit(lambda: ops.conv_direct(x, g_, K, S, Cout, wd=d_))
+            print(f"{name:10s} fp32 {res[False]:8.1f} us   split {res[True]:8.1f} us  x{res[False] / res[True]:.2f}",
+                  flush=True)
+            continue
         Ho, Wo = (H + 2 * (K // 2) - K) // S + 1, (W + 2 * (K // 2) - K) // S + 1
         fl = 2.0 * N * Cout * Cin * K * K * Ho * Wo + (2.0 * N * Cout * Cin * Ho * Wo if wd is not None else 0)
         tm = timeit(lambda: F.conv2d(x, w, None, S, K // 2))

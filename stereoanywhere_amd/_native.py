@@ -90,8 +90,10 @@ SIGNATURES = {
     "sa_conv2d_k3_wino4_multi_gate": (I, [I, P, P, I, P]),
     "sa_conv_direct_weights": (I, [P, I, I, I, I, I, P, P]),
     "sa_conv_direct_weights_size": (L, [I, I, I, I, I]),
+    "sa_conv_direct_weights_split": (I, [P, L, P, P]),
     "sa_conv_direct_stat_parts": (L, [I, I]),
     "sa_conv_direct": (I, [P, L, I, I, I, I, I, I, P, P, I, P, L, P, L, P, P, P]),
+    "sa_conv_direct_split": (I, [P, L, I, I, I, I, I, I, P, P, I, P, L, P, L, P, P, P]),
     "sa_plane_stats": (I, [P, L, I, I, L, F, P, P, P]),
     "sa_norm_act": (I, [P, L, I, I, L, P, P, P, I, I, P, L, P, P, P, I, I, I, P, L, P]),
     "sa_conv3d_upcat_stat_parts": (L, [I, I, I]),

@@ -23,6 +23,23 @@
 namespace {
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+using f16x2 = __attribute__((ext_vector_type(2))) _Float16;
+using f16x4 = __attribute__((ext_vector_type(4))) _Float16;
+
+// Split products (SP, sa_conv_direct_split): the weights are f16 (hi, lo) pairs of w * 2^12 in
+// one dword each (sa_conv_direct_weights_split), the patch values are split in registers, and
+// each v_mfma_f32_16x16x4_f32 becomes one v_mfma_f32_16x16x16_f16 over the four products
+// hi*bhi + hi*blo + lo*bhi + lo*blo (A = (hi, hi, lo, lo), B = (bhi, blo, bhi, blo)): exact
+// products, fp32 accumulation, half the MFMA cycles (as conv2d_wino4.hip's W4Split).
+constexpr float DSP_SCALE = 4096.0f;
+__device__ __forceinline__ f16x4 dsplit(const float x) {
+  const f16x2 hh = __builtin_convertvector(f32x2{x, x}, f16x2);
+  float l;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(__builtin_bit_cast(unsigned, hh)), "v"(x));
+  const f16x2 ll = __builtin_convertvector(f32x2{l, l}, f16x2);
+  return __builtin_shufflevector(hh, ll, 0, 1, 2, 3);
+}
 
 constexpr int DOTH = 8, DOTW = 32, MT = 2;   // output tile; row segments of 16 pixels per wave
 
@@ -62,7 +79,7 @@ struct DirArgs {
   double *part, *part_ds;
 };
 
-template <int K, int S, int KC, int NTL, bool DS>
+template <int K, int S, int KC, int NTL, bool DS, bool SP = false>
 __global__ __launch_bounds__(512, DS ? 2 : 4) void conv_direct_kernel(const DirArgs a) {
   using C = DCfg<K, S, KC, NTL, DS>;
   constexpr int NC = C::NC, NCP = C::NCP, PLANE = C::PLANE, PWP = C::PWP;
@@ -161,20 +178,21 @@ __global__ __launch_bounds__(512, DS ? 2 : 4) void conv_direct_kernel(const DirA
       float av[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) av[m] = sx[abase[m] + koff];
+      auto prod = [&](const float bv, f32x4 *ac) __attribute__((always_inline)) {
+        if constexpr (SP) {
+          const f16x4 b = __builtin_bit_cast(f16x4, f32x2{bv, bv});
 #pragma unroll
-      for (int t = 0; t < NTL; ++t) {
-        const float bv = sw[bbase + 4 * s * NCP + t * 16];
+          for (int m = 0; m < MT; ++m) ac[m * C::NACC] = __builtin_amdgcn_mfma_f32_16x16x16f16(dsplit(av[m]), b, ac[m * C::NACC], 0, 0, 0);
+        } else {
 #pragma unroll
-        for (int m = 0; m < MT; ++m) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv, acc[m][t], 0, 0, 0);
-      }
+          for (int m = 0; m < MT; ++m) ac[m * C::NACC] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv, ac[m * C::NACC], 0, 0, 0);
+        }
+      };
+#pragma unroll
+      for (int t = 0; t < NTL; ++t) prod(sw[bbase + 4 * s * NCP + t * 16], &acc[0][t]);
       if (DS && tap == (K / 2) * K + K / 2) {
 #pragma unroll
-        for (int t = 0; t < NTL; ++t) {
-          const float bv = sd[bbase + ci0 * NCP + t * 16];
-#pragma unroll
-          for (int m = 0; m < MT; ++m)
-            acc[m][NTL + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv, acc[m][NTL + t], 0, 0, 0);
-        }
+        for (int t = 0; t < NTL; ++t) prod(sd[bbase + ci0 * NCP + t * 16], &acc[0][NTL + t]);
       }
     }
     __syncthreads();
@@ -184,6 +202,12 @@ __global__ __launch_bounds__(512, DS ? 2 : 4) void conv_direct_kernel(const DirA
     }
   }
 
+  if constexpr (SP) {   // the weights' 2^12 (exact)
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int t = 0; t < C::NACC; ++t) acc[m][t] *= 1.0f / DSP_SCALE;
+  }
   // ---- epilogue: lane holds channel t*16 + (lane & 15), pixels 4*(lane>>4) + r of segment m.
   // The stats reduction reuses the staging LDS (free after the loop's last barrier).
   double *red = reinterpret_cast<double *>(sm);   // [8 waves][2][NACC * 16]
@@ -304,6 +328,27 @@ extern "C" int sa_conv_direct_weights(const float *weight, int Cout, int Cin, in
   return sa::check_launch("sa_conv_direct_weights");
 }
 
+namespace {
+// arranged fp32 weights (sa_conv_direct_weights) -> the split kernel's f16 (hi, lo) pairs of
+// w * 2^12, one dword per weight in the same layout
+__global__ void direct_split_kernel(const float *__restrict__ w, long n, unsigned *__restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double u = (double)w[i] * DSP_SCALE;
+  const _Float16 hi = (_Float16)(float)u;
+  const _Float16 lo = (_Float16)(float)(u - (double)hi);
+  out[i] = (unsigned)__builtin_bit_cast(unsigned short, hi) | ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
+}
+
+}  // namespace
+
+extern "C" int sa_conv_direct_weights_split(const float *arranged, long n, void *out, void *stream) {
+  SA_REQUIRE(arranged && out && n > 0, "sa_conv_direct_weights_split: bad arguments");
+  hipStream_t s = sa::as_stream(stream);
+  direct_split_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(arranged, n, static_cast<unsigned *>(out));
+  return sa::check_launch("sa_conv_direct_weights_split");
+}
+
 extern "C" long sa_conv_direct_weights_size(int Cout, int Cin, int K, int S, int with_ds) {
   int KC = 0, NTL = 0;
   if (!pick(K, S, Cout, KC, NTL) || (K == 1 && !with_ds)) return -1;
@@ -314,7 +359,8 @@ extern "C" long sa_conv_direct_stat_parts(int Ho, int Wo) {
   return (long)((Wo + DOTW - 1) / DOTW) * ((Ho + DOTH - 1) / DOTH);
 }
 
-extern "C" int sa_conv_direct(const float *in, long in_bs, int N, int Cin, int H, int W, int K, int S,
+template <bool SP>
+static int conv_direct_launch(const float *in, long in_bs, int N, int Cin, int H, int W, int K, int S,
                               const float *wg, const float *wd, int Cout, float *out, long out_bs, float *out_ds,
                               long out_ds_bs, double *part, double *part_ds, void *stream) {
   int KC = 0, NTL = 0;
@@ -336,11 +382,27 @@ extern "C" int sa_conv_direct(const float *in, long in_bs, int N, int Cin, int H
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV_DIRECT, s);
   if (K == 7) {
-    conv_direct_kernel<7, 1, 4, 4, false><<<(unsigned)nblk, 512, 0, s>>>(a);
+    conv_direct_kernel<7, 1, 4, 4, false, SP><<<(unsigned)nblk, 512, 0, s>>>(a);
   } else if (NTL == 6) {
-    conv_direct_kernel<3, 2, 8, 6, true><<<(unsigned)nblk, 512, 0, s>>>(a);
+    conv_direct_kernel<3, 2, 8, 6, true, SP><<<(unsigned)nblk, 512, 0, s>>>(a);
   } else {
-    conv_direct_kernel<3, 2, 8, 8, true><<<(unsigned)nblk, 512, 0, s>>>(a);
+    conv_direct_kernel<3, 2, 8, 8, true, SP><<<(unsigned)nblk, 512, 0, s>>>(a);
   }
   return sa::check_launch("sa_conv_direct");
+}
+
+extern "C" int sa_conv_direct(const float *in, long in_bs, int N, int Cin, int H, int W, int K, int S,
+                              const float *wg, const float *wd, int Cout, float *out, long out_bs, float *out_ds,
+                              long out_ds_bs, double *part, double *part_ds, void *stream) {
+  return conv_direct_launch<false>(in, in_bs, N, Cin, H, W, K, S, wg, wd, Cout, out, out_bs, out_ds, out_ds_bs, part,
+                                   part_ds, stream);
+}
+
+// the same with split weights (sa_conv_direct_weights_split for wg and wd)
+extern "C" int sa_conv_direct_split(const float *in, long in_bs, int N, int Cin, int H, int W, int K, int S,
+                                    const void *wg, const void *wd, int Cout, float *out, long out_bs, float *out_ds,
+                                    long out_ds_bs, double *part, double *part_ds, void *stream) {
+  return conv_direct_launch<true>(in, in_bs, N, Cin, H, W, K, S, static_cast<const float *>(wg),
+                                  static_cast<const float *>(wd), Cout, out, out_bs, out_ds, out_ds_bs, part, part_ds,
+                                  stream);
 }

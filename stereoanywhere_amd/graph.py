@@ -34,7 +34,7 @@ class ForwardGraph:
         # switches (set by A/B scripts and tests) and the model's flags
         args = tuple(sorted((k, repr(v)) for k, v in vars(m.args).items()))
         return (tuple((tuple(x.shape), x.dtype, x.device) for x in xs), iters, dataclasses.astuple(m.opts),
-                m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_WIDE, ops.W4_QUAD, ops.W4_PERSIST, ops.W4_SPLIT), args)
+                m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_WIDE, ops.W4_QUAD, ops.W4_PERSIST, ops.W4_SPLIT, ops.DIRECT_SPLIT), args)
 
     def __call__(self, image2, image3, mde2, mde3, iters: int = 12, test_mode: bool = True):
         if not test_mode:

@@ -733,6 +733,9 @@ W4_QUAD = False
 W4_SPLIT = True
 # the split filters need |U * 2^12| < 65504; |U| <= max |weight| for F(4x4,3x3)'s G
 _W4_SPLIT_WMAX = 15.99
+# the direct convs (stems, stride-2 + 1x1) with split products (sa_conv_direct_split), derived
+# by conv_direct_weights as int32-held (hi, lo) pairs
+DIRECT_SPLIT = False
 
 
 def wino_weights(weight: torch.Tensor) -> WinoFilters:
@@ -953,6 +956,12 @@ def conv_direct_weights(weight: torch.Tensor, stride: int, with_ds: bool = False
     out = torch.empty((n,), device=weight.device, dtype=torch.float32)
     N.call("sa_conv_direct_weights", weight.data_ptr(), Cout, Cin, K, stride, 1 if with_ds else 0, out.data_ptr(),
            _stream(weight))
+    if DIRECT_SPLIT:   # the split kernel's (hi, lo) pairs: an int32 container marks them
+        if float(weight.abs().max()) >= _W4_SPLIT_WMAX:
+            raise RuntimeError("conv_direct_weights: |weight| >= 16 exceeds the split kernel's f16 range")
+        sp = torch.empty((n,), device=weight.device, dtype=torch.int32)
+        N.call("sa_conv_direct_weights_split", out.data_ptr(), n, sp.data_ptr(), _stream(weight))
+        return sp
     return out
 
 
@@ -962,7 +971,11 @@ def conv_direct(x: torch.Tensor, wg: torch.Tensor, K: int, stride: int, Cout: in
     with its fused 1x1 stride-2 downsample (wd).  Returns [out, (out_ds)] and, with stats,
     the InstanceNorm (mean, rstd) of each output after it."""
     bs = _plane_bs(x, "x")
-    _check(wg, "wg")
+    if wg.dtype == torch.int32:   # split (hi, lo) pairs (conv_direct_weights under DIRECT_SPLIT)
+        if wg.device.type != "cuda" or not wg.is_contiguous():
+            raise RuntimeError("conv_direct: wg must be a contiguous GPU tensor")
+    else:
+        _check(wg, "wg")
     B, Cin, H, W = x.shape
     p = K // 2
     Ho, Wo = (H + 2 * p - K) // stride + 1, (W + 2 * p - K) // stride + 1
@@ -973,8 +986,12 @@ def conv_direct(x: torch.Tensor, wg: torch.Tensor, K: int, stride: int, Cout: in
     def part():
         return torch.empty((B * Cout * parts * 2,), device=x.device, dtype=torch.float64) if stats else None
     pa, pd = part(), (part() if wd is not None else None)
-    N.call("sa_conv_direct", x.data_ptr(), bs, B, Cin, H, W, K, stride, wg.data_ptr(), _ptr(wd), Cout,
-           out.data_ptr(), Cout * Ho * Wo, _ptr(out_ds), Cout * Ho * Wo, _ptr(pa), _ptr(pd), _stream(x))
+    split = wg.dtype == torch.int32
+    if wd is not None and (wd.dtype == torch.int32) != split:
+        raise RuntimeError("conv_direct: wg and wd must both be split or both fp32 (conv_direct_weights)")
+    N.call("sa_conv_direct_split" if split else "sa_conv_direct", x.data_ptr(), bs, B, Cin, H, W, K, stride,
+           wg.data_ptr(), _ptr(wd), Cout, out.data_ptr(), Cout * Ho * Wo, _ptr(out_ds), Cout * Ho * Wo, _ptr(pa),
+           _ptr(pd), _stream(x))
     # products executed: the stem's channels padded to the kernel's chunk of 4
     cin_x = -(-Cin // 4) * 4 if K == 7 else Cin
     _account("conv2d_direct", 2.0 * B * Cout * cin_x * K * K * Ho * Wo

@@ -16,8 +16,11 @@ def rnd(*shape, seed=0):
     return torch.randn(*shape, generator=g).to(dev)
 
 
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("B,Cin,H,W", [(2, 3, 40, 70), (1, 3, 33, 29), (2, 1, 16, 64)])
-def test_stem_7x7(B, Cin, H, W):
+def test_stem_7x7(monkeypatch, B, Cin, H, W, split):
+    """split: the products as exact f16 hi/lo pair products (ops.DIRECT_SPLIT), same tolerance."""
+    monkeypatch.setattr(ops, "DIRECT_SPLIT", split)
     x = rnd(B, Cin, H, W, seed=1)
     w = rnd(64, Cin, 7, 7, seed=2) / 10
     out, (stats,) = ops.conv_direct(x, ops.conv_direct_weights(w, 1), 7, 1, 64, stats=True)
@@ -29,13 +32,17 @@ def test_stem_7x7(B, Cin, H, W):
                                atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("B,Cin,Cout,H,W", [(2, 64, 96, 34, 70), (1, 96, 128, 27, 45), (2, 128, 128, 16, 30),
                                             (1, 32, 256, 20, 66)])
-def test_stride2_with_downsample(B, Cin, Cout, H, W):
+def test_stride2_with_downsample(monkeypatch, B, Cin, Cout, H, W, split):
+    monkeypatch.setattr(ops, "DIRECT_SPLIT", split)
     x = rnd(B, Cin, H, W, seed=3)
     w = rnd(Cout, Cin, 3, 3, seed=4) / (3 * Cin ** 0.5)
     wd = rnd(Cout, Cin, 1, 1, seed=5) / Cin ** 0.5
-    out, ds, (s1, sd) = ops.conv_direct(x, ops.conv_direct_weights(w, 2), 3, 2, Cout,
+    wg_ = ops.conv_direct_weights(w, 2)
+    assert (wg_.dtype == torch.int32) == split
+    out, ds, (s1, sd) = ops.conv_direct(x, wg_, 3, 2, Cout,
                                         wd=ops.conv_direct_weights(wd, 2, with_ds=True), stats=True)
     ref = F.conv2d(x, w, stride=2, padding=1)
     ref_d = F.conv2d(x, wd, stride=2)
