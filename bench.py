@@ -284,9 +284,13 @@ def main():
                     help="let MIOpen time its conv algorithms per shape (torch cudnn.benchmark)")
     ap.add_argument("--w4-split", type=int, default=None, choices=[0, 1],
                     help="F(4x4) convs on the split kernel (1) or fp32 MFMA (0); default: ops.W4_SPLIT")
+    ap.add_argument("--direct-split", type=int, default=None, choices=[0, 1],
+                    help="direct convs on split products (1) or fp32 MFMA (0); default: ops.DIRECT_SPLIT")
     args = ap.parse_args()
     if args.w4_split is not None:
         ops.W4_SPLIT = bool(args.w4_split)
+    if args.direct_split is not None:
+        ops.DIRECT_SPLIT = bool(args.direct_split)
 
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
     r = D.init_from_env("nccl")
@@ -484,8 +488,10 @@ def main():
         "metric": metric, "value": total_units / elapsed, "unit": unit, "n_gpus": r.world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
-        "dtype": ("f32 (F(4x4) Winograd-domain products as exact f16 hi/lo pair products on MFMA, fp32 "
-                  "accumulation; everything else fp32)" if ops.W4_SPLIT else "f32"), "data": "synthetic (seeded value-noise pairs, "
+        "dtype": ("f32 (" + " and ".join(n for n, on in (("F(4x4) Winograd-domain", ops.W4_SPLIT),
+                                                         ("direct-conv", ops.DIRECT_SPLIT)) if on)
+                  + " products as exact f16 hi/lo pair products on MFMA, fp32 accumulation; everything else "
+                  "fp32)" if ops.W4_SPLIT or ops.DIRECT_SPLIT else "f32"), "data": "synthetic (seeded value-noise pairs, "
         "seeded random weights; no dataset/checkpoint offline)",
         "config": config, "roofline": roof, "gathered_units": int(allm.shape[0]),
         "execution": ("hipGraph replay of the whole forward (stereoanywhere_amd.graph.ForwardGraph; inputs "

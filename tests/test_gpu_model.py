@@ -42,9 +42,11 @@ def test_tiny_case_and_intermediates(model):
 @pytest.mark.parametrize("name,H,W,D,iters", [("cfg1_256x512_it8.npz", 256, 512, 64.0, 8),
                                                ("cfg2_544x960_it22.npz", 544, 960, 192.0, 22)])
 def test_end_to_end_vs_reference(model, monkeypatch, name, H, W, D, iters, split):
-    """split: every F(4x4) conv on the f16 hi/lo split kernel (ops.W4_SPLIT) or on fp32 MFMA."""
+    """split: every F(4x4) and direct conv on the f16 hi/lo split kernels (ops.W4_SPLIT,
+    ops.DIRECT_SPLIT) or all on fp32 MFMA products."""
     from stereoanywhere_amd import ops
     monkeypatch.setattr(ops, "W4_SPLIT", split)
+    monkeypatch.setattr(ops, "DIRECT_SPLIT", split)
     fix = load_fixture(name)
     pair = regenerate_inputs(fix, 1, H, W, D)
     disp = run(model, pair, iters)

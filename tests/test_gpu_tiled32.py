@@ -47,9 +47,11 @@ def _inputs(fix, prefix, H, W, D, seed):
 @pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("name", ["mb_tile", "booster_tile"])
 def test_tile_32_iterations_vs_reference(model, fix, monkeypatch, name, split):
-    """split: the F(4x4) convs on the f16 hi/lo split kernel (ops.W4_SPLIT) or on fp32 MFMA."""
+    """split: the F(4x4) and direct convs on the f16 hi/lo split kernels (ops.W4_SPLIT,
+    ops.DIRECT_SPLIT) or all on fp32 MFMA products."""
     from stereoanywhere_amd import ops
     monkeypatch.setattr(ops, "W4_SPLIT", split)
+    monkeypatch.setattr(ops, "DIRECT_SPLIT", split)
     H, W, seed = (int(v) for v in fix[f"{name}.geom"])
     x = _inputs(fix, name, H, W, float(fix[f"{name}.D"]), seed)
     # the 1/16 GRU level is ragged (W/16 = 42 or 70): padded planes on F(4x4)
