@@ -436,7 +436,7 @@ def main():
         secs = ms_tot / 1e3 / args.steps                      # per step
         if unit == "TFLOP/s":
             ach, peak, bound = amount / secs / 1e12, FP32_MFMA_PEAK_TFS, "mfma"
-            if k == "conv2d_wino4" and ops.W4_SPLIT:
+            if (k == "conv2d_wino4" and ops.W4_SPLIT) or (k == "conv2d_direct" and ops.DIRECT_SPLIT):
                 # the split kernel's products: v_mfma_f32_16x16x16_f16 (16 cycles per SIMD) carries
                 # one 16x16x4 fp32 MFMA's products as hi/lo pairs (32 cycles): twice the fp32 rate
                 peak = SPLIT_MFMA_PEAK_TFS
@@ -466,9 +466,10 @@ def main():
                          "conv2d_wino / conv2d_wino4 count the Winograd-domain products they execute "
                          "(16/36 resp. 36/144 of the direct convolution's), so their direct-equivalent "
                          "rates are 2.25x resp. 4x achieved"
-                         + ("; conv2d_wino4 runs the split kernel (ops.W4_SPLIT): its peak is the "
-                            "fp32-product rate of v_mfma_f32_16x16x16_f16 on hi/lo pairs, 2x the fp32 "
-                            "MFMA peak" if ops.W4_SPLIT else "")})
+                         + ("; conv2d_wino4 / conv2d_direct run the split kernels (ops.W4_SPLIT, "
+                            "ops.DIRECT_SPLIT): their peak is the fp32-product rate of "
+                            "v_mfma_f32_16x16x16_f16 on hi/lo pairs, 2x the fp32 MFMA peak"
+                            if ops.W4_SPLIT or ops.DIRECT_SPLIT else "")})
     if tiled is None:
         metric, unit = "stereo pairs/sec @540x960 D=192 (1/2/4/8 GPU) + EPE vs reference", "pairs/s"
         config = {"workload": f"configs[1]: batch {args.batch}/GPU x {H}x{W} (padded {Hp}x{Wp}), "
