@@ -57,7 +57,7 @@
 #define SA_W4_GJB1 16  // the same for mode 1
 #endif
 #ifndef SA_W4_PRIO
-#define SA_W4_PRIO 0
+#define SA_W4_PRIO 1   // s_setprio 1 for the point-half-1 waves (split kernel forward: 66.8 -> 66.5 ms/step, wino4 49.8 -> 49.0 ms, two interleaved passes)
 #endif
 #ifndef SA_W4_PF
 #define SA_W4_PF 1     // persistent kernel: prefetch the next item's chunk 0 (0: each item issues its own)
