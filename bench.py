@@ -286,7 +286,11 @@ def main():
                     help="F(4x4) convs on the split kernel (1) or fp32 MFMA (0); default: ops.W4_SPLIT")
     ap.add_argument("--direct-split", type=int, default=None, choices=[0, 1],
                     help="direct convs on split products (1) or fp32 MFMA (0); default: ops.DIRECT_SPLIT")
+    ap.add_argument("--wino4-min-blocks", type=int, default=None,
+                    help="F(4x4) for launches of at least this many blocks (default: ops._WINO4_MIN_BLOCKS)")
     args = ap.parse_args()
+    if args.wino4_min_blocks is not None:
+        ops._WINO4_MIN_BLOCKS = args.wino4_min_blocks
     if args.w4_split is not None:
         ops.W4_SPLIT = bool(args.w4_split)
     if args.direct_split is not None:

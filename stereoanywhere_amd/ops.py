@@ -788,9 +788,11 @@ def _wino4_blocks(x: torch.Tensor, U: "WinoFilters", **_) -> int:
     return B * -(-H // bh) * -(-W // bw) * (U.cout // 32)
 
 
-# below this many workgroups per launch (1.5 per CU) the F(2x2) kernel's four times as many,
-# smaller blocks fill the chip better than F(4x4)'s (measured on the update block's convs)
-_WINO4_MIN_BLOCKS = 384
+# below this many workgroups per launch the F(2x2) kernel's four times as many, smaller blocks
+# fill the chip better than F(4x4)'s (measured on the update block's convs: 384 with the fp32
+# F(4x4) kernel; with the split kernel 128 is 0.4 ms/step faster in the forward than 384 or
+# 256, bench.py --wino4-min-blocks, two interleaved passes)
+_WINO4_MIN_BLOCKS = 128
 
 
 def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] = None, relu: bool = False,
