@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Throughput of the MI355X StereoAnywhere forward on synthetic 540x960 pairs.
 
-    python bench.py [--gpus N --steps K --warmup W] [--config cfg2|cfg3|cfg5]
+    python bench.py [--gpus N --steps K --warmup W] [--config cfg2|cfg4|cfg3|cfg5]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -19,6 +19,14 @@ Also reported (rank 0):
                 reference) on one 544x960 pair, all host threads, N=1 only: one warm-up
                 run, then the median of 3; cfg1 (256x512, 8 iters) the same
                 way beside it; the CPU model string and the thread count are reported
+
+  --config cfg4  configs[3]: batch 64 sharded 8-way = 8 pairs per GPU (seeds 1 + 8 * rank ..), the
+                 same step otherwise; at world size 8 the global batch is configs[3]'s 64, below it
+                 the line is configs[3]'s per-rank workload (the scaling curve needs an 8-GPU node)
+
+Box state: the GPU's sysfs clock levels, power and temperatures before and after the timed
+region, and sclk / power sampled every 100 ms during it (box_state; the run-to-run spread of
+the headline is attributed against these).
 
 Tiled configs (separate lines, not the headline):
   --config cfg3  Middlebury-H-sized synthetic pair 1000x1400 (padded 1024x1408), middlebury
@@ -100,6 +108,108 @@ def pmc_traffic(kernel: str, batch: int):
     with open(path) as f:
         rec = json.load(f).get(kernel)
     return None if rec is None else rec["hbm_bytes_per_launch"]
+
+
+F16_DENSE_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 MFMA ~2.5 PF dense (spec)
+
+
+def _gpu_sysfs(device):
+    """The sysfs directory of this process's GPU (by PCI address), or None."""
+    import glob
+    try:
+        pr = torch.cuda.get_device_properties(device)
+        addr = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}."
+    except Exception:
+        return None
+    for d in sorted(glob.glob("/sys/bus/pci/devices/*")):
+        if os.path.basename(d).startswith(addr) and os.path.exists(os.path.join(d, "pp_dpm_sclk")):
+            return d
+    return None
+
+
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _dpm_current(text):
+    """The starred line of a pp_dpm_* table ('1: 2400Mhz *') -> MHz."""
+    if not text:
+        return None
+    for line in text.splitlines():
+        if line.rstrip().endswith("*"):
+            try:
+                return float(line.split(":", 1)[1].strip().rstrip("*").strip().lower().replace("mhz", ""))
+            except ValueError:
+                return None
+    return None
+
+
+def box_state(d):
+    """One snapshot of the GPU's DPM levels, power and temperatures (sysfs; None where unreadable)."""
+    import glob
+    if d is None:
+        return None
+    out = {"sysfs": d, "sclk_mhz": _dpm_current(_read(os.path.join(d, "pp_dpm_sclk"))),
+           "mclk_mhz": _dpm_current(_read(os.path.join(d, "pp_dpm_mclk"))),
+           "fclk_mhz": _dpm_current(_read(os.path.join(d, "pp_dpm_fclk")))}
+    for hw in sorted(glob.glob(os.path.join(d, "hwmon", "hwmon*"))):
+        for name in ("power1_average", "power1_input"):
+            v = _read(os.path.join(hw, name))
+            if v and v.lstrip("-").isdigit():
+                out["power_w"] = int(v) / 1e6
+                break
+        cap = _read(os.path.join(hw, "power1_cap"))
+        if cap and cap.isdigit():
+            out["power_cap_w"] = int(cap) / 1e6
+        for t in sorted(glob.glob(os.path.join(hw, "temp*_input"))):
+            lab = _read(t.replace("_input", "_label")) or os.path.basename(t)
+            v = _read(t)
+            if v and v.lstrip("-").isdigit():
+                out[f"temp_{lab}_c"] = int(v) / 1e3
+        for fq in sorted(glob.glob(os.path.join(hw, "freq*_input"))):
+            lab = _read(fq.replace("_input", "_label")) or os.path.basename(fq)
+            v = _read(fq)
+            if v and v.isdigit():
+                out[f"{lab}_hwmon_mhz"] = int(v) / 1e6
+    return out
+
+
+class BoxSampler:
+    """sclk / power sampled from sysfs every ``period`` s on a thread while the timed steps run."""
+
+    def __init__(self, d, period: float = 0.1):
+        import threading
+        self.d, self.period, self.samples = d, period, []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True) if d else None
+
+    def _run(self):
+        while not self._stop.is_set():
+            st = box_state(self.d)
+            self.samples.append({k: st.get(k) for k in ("sclk_mhz", "power_w")})
+            self._stop.wait(self.period)
+
+    def __enter__(self):
+        if self._t:
+            self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self._t:
+            self._t.join()
+
+    def summary(self):
+        res = {"samples": len(self.samples)}
+        for k in ("sclk_mhz", "power_w"):
+            v = [x[k] for x in self.samples if x.get(k) is not None]
+            if v:
+                res[k] = {"min": min(v), "mean": sum(v) / len(v), "max": max(v)}
+        return res
 
 
 def make_inputs(B, H, W, Hp, Wp, D, seed0, device):
@@ -268,9 +378,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg5"],
-                    help="cfg2 = the headline (configs[1]); cfg3 / cfg5 = the tiled configs")
-    ap.add_argument("--batch", type=int, default=4, help="pairs per GPU (configs[1]: 4)")
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg4", "cfg3", "cfg5"],
+                    help="cfg2 = the headline (configs[1]); cfg4 = configs[3]'s 8 pairs per GPU; "
+                         "cfg3 / cfg5 = the tiled configs")
+    ap.add_argument("--batch", type=int, default=None, help="pairs per GPU (configs[1]: 4, configs[3]: 8)")
     ap.add_argument("--iters", type=int, default=None, help="GRU iterations (default: the config's)")
     ap.add_argument("--height", type=int, default=540)
     ap.add_argument("--width", type=int, default=960)
@@ -289,6 +400,8 @@ def main():
     ap.add_argument("--wino4-min-blocks", type=int, default=None,
                     help="F(4x4) for launches of at least this many blocks (default: ops._WINO4_MIN_BLOCKS)")
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 8 if args.config == "cfg4" else 4
     if args.wino4_min_blocks is not None:
         ops._WINO4_MIN_BLOCKS = args.wino4_min_blocks
     if args.w4_split is not None:
@@ -380,14 +493,20 @@ def main():
         torch.cuda.synchronize()
         # timed region: K plain steps -> value.  The per-launch HIP events of the roofline
         # serialise every launch (~6 % of a step), so they run over K more steps right after.
+        sysd = _gpu_sysfs(device)
+        state_before = box_state(sysd)
+        N.lib().sa_split_redo_blocks(1)   # (synchronises; outside the timed region)
         D.barrier(r)
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = step()
-        torch.cuda.synchronize()
-        D.barrier(r)
-        elapsed = time.perf_counter() - t0
+        with BoxSampler(sysd) as sampler:
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                out = step()
+            torch.cuda.synchronize()
+            D.barrier(r)
+            elapsed = time.perf_counter() - t0
+        redo_blocks = int(N.lib().sa_split_redo_blocks(1))
+        state_after = box_state(sysd)
         log(f"timed {args.steps} steps in {elapsed:.3f} s")
         # the same steps launched eagerly (no graph), for the record (or, when the probe chose
         # eager steps, replayed from the graph)
@@ -470,6 +589,12 @@ def main():
         kernels[k] = {"bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
                       "ms_per_step": ms_tot / args.steps, "launches_per_step": n_launch / args.steps,
                       "avg_launch_us": ms_tot * 1e3 / n_launch}
+        if peak == SPLIT_MFMA_PEAK_TFS:
+            # the same rate against the guide's peaks: the path's arithmetic type (fp32 products,
+            # 157.3 TF/s) and the f16 MFMA flops the kernel issues (4 f16 products per fp32 one)
+            # against the F16 dense peak (~2.5 PF)
+            kernels[k].update(frac_fp32_peak=ach / FP32_MFMA_PEAK_TFS, f16_issued_tflops=4 * ach,
+                              frac_f16_dense_peak=4 * ach / F16_DENSE_PEAK_TFS)
     dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
     roof = dict(kernels[dom])
     roof.update({"kernel": dom, "traffic": pmc_traffic(dom, args.batch) if tiled is None else None,
@@ -497,8 +622,14 @@ def main():
                             if ops.W4_SPLIT or ops.DIRECT_SPLIT else "")})
     if tiled is None:
         metric, unit = "stereo pairs/sec @540x960 D=192 (1/2/4/8 GPU) + EPE vs reference", "pairs/s"
-        config = {"workload": f"configs[1]: batch {args.batch}/GPU x {H}x{W} (padded {Hp}x{Wp}), "
-                              f"{iters} GRU iters, published flags", "global_batch": args.batch * r.world,
+        if args.config == "cfg4":
+            wl = (f"configs[3]: batch {args.batch * r.world} = {args.batch} pairs/GPU x {r.world} GPU"
+                  + ("" if r.world == 8 else f" (configs[3]'s per-rank workload; its batch 64 needs 8 GPUs)")
+                  + f", {H}x{W} (padded {Hp}x{Wp}), {iters} GRU iters, published flags")
+        else:
+            wl = (f"configs[1]: batch {args.batch}/GPU x {H}x{W} (padded {Hp}x{Wp}), "
+                  f"{iters} GRU iters, published flags")
+        config = {"workload": wl, "global_batch": args.batch * r.world,
                   "iters": iters, "parallelism": f"dp{r.world} (independent pairs, metrics all_gather)"}
     else:
         metric, unit = f"stereo images/sec, tiled ({args.config}) + EPE vs reference", "images/s"
@@ -526,6 +657,9 @@ def main():
                       "copied into its static buffers each step)" if graph_dev is not None else "eager launches"),
         "eager_ms_per_step": elapsed_eager / args.steps * 1e3,
         "execution_probe": probe,
+        # split-kernel blocks the f16 range guard recomputed on fp32 MFMA during the timed steps
+        "split_redo_blocks": redo_blocks,
+        "box_state": {"before": state_before, "during": sampler.summary(), "after": state_after},
     }
     if graph_dev is not None:
         res["graph_vs_eager_max_abs"] = graph_dev

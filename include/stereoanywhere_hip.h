@@ -115,6 +115,7 @@ int sa_softargmin_conf(const float *vol_disp, const float *vol_conf, int B, int 
  * kernels instead (two launches, each reading both volumes), on = 2 the one-pass kernel's
  * 16-byte-row variant (n % 4 == 0, n <= 256, aligned rows; slower); for A/B runs and tests. */
 void sa_softargmin_set_one_pass(int on);
+int sa_softargmin_get_one_pass(void);
 
 /* a7 — softlrc (utils.py:189-198) with disp_warping (utils.py:172-187); optional
  * fuzzy_and with a confidence (utils.py:240-241, stereoanywhere.py:188-189):
@@ -215,6 +216,9 @@ int sa_corr_lookup_conv1x1(const float *pyramid_a, const float *pyramid_b, int W
 void sa_lookup_set_mfma(int on);
 int sa_lookup_get_mfma(void);
 long sa_shear_slice_size(int W1, int W2, int num_levels);
+/* 1 when sa_corr_pyramid_shear + sa_corr_lookup_conv1x1_sheared take this geometry (B*H <= 65535,
+ * W2 <= 511, 4 levels with the coarsest >= 2 wide), else 0: the caller keeps the row layout */
+int sa_corr_shear_supported(int B, int H, int W1, int W2, int num_levels);
 long sa_shear_level_offset(int W1, int W2, int num_levels, int level);
 int sa_corr_pyramid_shear(const float *pyramid, long row_stride, int B, int H, int W1, int W2,
                           int num_levels, float *sheared, void *stream);
@@ -287,6 +291,7 @@ int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W, const flo
  * slab for packed FMAs; 3 variant 2 with the next channel's columns fetched by LDS-DMA.  For A/B
  * runs and tests. */
 void sa_conv3d_wd_set_variant(int variant);
+int sa_conv3d_wd_get_variant(void);
 /* The hourglass's two readers of the masked mono volume (down_layers[0][0], hourglass.py:27-33;
  * final_agg[0] over cat(orig, up(x)), hourglass.py:326-328) on the one-hot volume given by its
  * records (sa_mono_bin_records; rec_l [B,H,W] of the left pixels = the volume's W axis, rec_r
@@ -421,6 +426,12 @@ typedef struct SaGateEpilogue {
  * sa_conv2d_wino4_weights_split; the transformed inputs must stay below 65504 in magnitude). */
 int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                                   int block_shape, void *stream);
+/* Range guard of the split kernels (the F(4x4) kernel's f16 hi/lo products, block_shape 6, and
+ * sa_conv_direct_split): a block whose f16 operands overflowed (|transformed input| >= 65520)
+ * recomputes its outputs on fp32 MFMA products inside the same launch, so results never carry the
+ * overflow.  Returns the number of such blocks since the last reset (reset != 0 clears it), -1 on
+ * error; synchronises the device. */
+long sa_split_redo_blocks(int reset);
 
 /* Direct KxK convolution (padding K/2, no bias) on fp32 MFMA for the encoder convs the
  * Winograd kernel does not cover (extractor.py:22-40, 91, 208):

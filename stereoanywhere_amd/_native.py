@@ -49,6 +49,7 @@ SIGNATURES = {
     "sa_lookup_set_mfma": (None, [I]),
     "sa_lookup_get_mfma": (I, []),
     "sa_shear_slice_size": (L, [I, I, I]),
+    "sa_corr_shear_supported": (I, [I, I, I, I, I]),
     "sa_shear_level_offset": (L, [I, I, I, I]),
     "sa_corr_pyramid_shear": (I, [P, L, I, I, I, I, I, P, P]),
     "sa_corr_volume_pyramid_sheared": (I, [P, P, I, I, I, I, I, F, P, P, F, I, P, P]),
@@ -59,6 +60,8 @@ SIGNATURES = {
     "sa_mono_bin_records": (I, [P, P, I, I, I, I, P, P]),
     "sa_softargmin_conf": (I, [P, P, I, I, I, I, L, L, L, L, P, P, P, P, L, P]),
     "sa_softargmin_set_one_pass": (None, [I]),
+    "sa_softargmin_get_one_pass": (I, []),
+    "sa_split_redo_blocks": (L, [I]),
     "sa_softlrc": (I, [P, P, P, P, I, I, I, L, F, P, P, P]),
     "sa_weighted_lsq": (I, [P, P, P, I, I, F, F, P, P, P]),
     "sa_weighted_lsq_ws_size": (L, [I, I]),
@@ -103,6 +106,7 @@ SIGNATURES = {
     "sa_instnorm_finalize": (I, [P, I, L, L, F, P, P, P]),
     "sa_conv3d_wd": (I, [P, I, I, I, I, I, P, I, P, P, I, F, P, P, P, P, P]),
     "sa_conv3d_wd_set_variant": (None, [I]),
+    "sa_conv3d_wd_get_variant": (I, []),
     "sa_conv3d_onehot_stat_parts": (L, [I, I, I]),
     "sa_conv3d_onehot": (I, [P, P, I, I, I, I, I, I, F, P, I, P, P, P]),
     "sa_conv3d_pointwise_upcat_onehot": (I, [P, P, I, F, P, I, I, I, I, I, I, I, P, I, P, P, P]),

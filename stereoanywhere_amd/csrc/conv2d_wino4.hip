@@ -212,6 +212,17 @@ __device__ __forceinline__ f16x4 w4_split(const float x) {
                                  0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// the fp32 value w * 2^12 of a split filter dword (hi, lo): hi + lo is exact in fp32 (22 bits)
+__device__ __forceinline__ float w4_unsplit(const float packed) {
+  const f16x2 p = __builtin_bit_cast(f16x2, packed);
+  return (float)p[0] + (float)p[1];
+}
+
+// Range guard of the split kernel: blocks whose f16 operands overflowed (|V| >= 65520 turns hi
+// into inf, so every product of that value, and the accumulators it feeds, are NaN) recompute
+// their outputs on fp32 MFMA; this counts them (sa_split_redo_blocks)
+__device__ unsigned g_w4_redo_blocks;
+
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, float *lds, int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)lds, 16, voff, soff, 0, 0);
 }
@@ -810,6 +821,86 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
     }
   }
   __syncthreads();
+  if constexpr (SPLIT) {
+    // Range guard: an f16 operand overflow leaves NaN in every accumulator it fed (hi = inf and
+    // lo = -inf, or inf * 0), so a non-finite sum of the lane's first-group accumulators (both
+    // groups see the same A operands) marks the block, and the whole block (block-uniform: the
+    // DMA buffers are shared) recomputes on fp32 MFMA products before its epilogue, so in-place
+    // gate epilogues stay correct.  Genuine NaN inputs take the same path and give the fp32
+    // kernel's NaN.  The flags live at the top of the LDS, which neither the epilogue's output
+    // staging (the first CO * OPP floats) nor the redo's single buffer (buffer 0) touches.
+    static_assert(C::SMEM >= C::CO * C::OPP + NWAVE && C::SMEM >= BUF + NWAVE, "range guard flags");
+    f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) sum += acc[i][jj][0];
+    const float tot = (sum.x + sum.y) + (sum.z + sum.w);
+    int *flags = reinterpret_cast<int *>(smem + C::SMEM - NWAVE);
+    const bool wbad = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(tot)) != 0;
+    if (lane == 0) flags[wv] = wbad ? 1 : 0;
+    __syncthreads();
+    int any = 0;
+#pragma unroll
+    for (int w = 0; w < NWAVE; ++w) any |= flags[w];
+    if (any) {
+      if (tid == 0) atomicAdd(&g_w4_redo_blocks, 1u);
+#pragma unroll
+      for (int i = 0; i < NR; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj)
+#pragma unroll
+          for (int g = 0; g < CG; ++g) acc[i][jj][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // a plain loop (one buffer, no prefetch, rolled): the path is rare, and a second copy of
+      // the pipelined main loop raised its register pressure
+#pragma unroll 1
+      for (int kc = 0; kc < nchunks; ++kc) {
+        issue(kc, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (AFF) {
+#pragma unroll
+          for (int j = 0; j < PDMA; ++j) {
+            if (pc[j] >= 0) {
+              f32x4 *q = reinterpret_cast<f32x4 *>(smem + ((wv + NWAVE * j) * 64 + lane) * 4);
+              const float2 ab = atab[kc * KC + pc[j]];
+              f32x4 v = *q;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] * ab.x + ab.y, act_floor);
+              *q = v;
+            }
+          }
+        }
+        __syncthreads();
+        const float *pb = smem + pread;
+        const float *ub = smem + PBUF + uread;
+#pragma unroll 1
+        for (int s = 0; s < JPC; ++s) {
+          const float *p = pb + s * 4 * PSv * 4;
+          float t[6][3];
+#pragma unroll
+          for (int r = 0; r < 6; ++r) {
+            const f32x2 ra = *reinterpret_cast<const f32x2 *>(p + r * PGv * 4);
+            const f32x4 rb = *reinterpret_cast<const f32x4 *>(p + r * PGv * 4 + 2);
+            const f32x2 rc = *reinterpret_cast<const f32x2 *>(p + r * PGv * 4 + 6);
+            bt6h<HF>(ra.y, rb.x, rb.y, rb.z, rb.w, rc.x, t[r]);
+          }
+#pragma unroll
+          for (int jj = 0; jj < 3; ++jj) {
+            float v[6];
+            bt6(t[0][jj], t[1][jj], t[2][jj], t[3][jj], t[4][jj], t[5][jj], v);
+#pragma unroll
+            for (int i = 0; i < NR; ++i) {
+              const f32xg b = *reinterpret_cast<const f32xg *>(ub + ((6 * i + 3 * HF + jj) * JPC + s) * SB);
+#pragma unroll
+              for (int g = 0; g < CG; ++g)
+                acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], w4_unsplit(b[g]), acc[i][jj][g], 0, 0, 0);
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
 #ifdef SA_W4_CLOCK
   if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][5] = __builtin_amdgcn_s_memtime();
 #endif
@@ -1215,6 +1306,22 @@ extern "C" int sa_w4_clock_read(unsigned long long *out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4_clock), sizeof(unsigned long long) * 10 * n) == hipSuccess ? 0 : -1;
 }
 #endif
+
+long sa_direct_redo_blocks_internal(int reset);   // conv_direct.hip
+
+// blocks of the split kernels (F(4x4) and direct) that the range guard recomputed on fp32 MFMA
+// since the last reset; synchronises the device (tests and bench.py, outside timed regions)
+extern "C" long sa_split_redo_blocks(int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  unsigned v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_w4_redo_blocks), sizeof v) != hipSuccess) return -1;
+  if (reset) {
+    const unsigned z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_w4_redo_blocks), &z, sizeof z) != hipSuccess) return -1;
+  }
+  const long d = sa_direct_redo_blocks_internal(reset);
+  return d < 0 ? -1 : (long)v + d;
+}
 
 // InstanceNorm partial count: the small blocks' tiling (a large block writes its two halves)
 extern "C" long sa_conv2d_k3_wino4_stat_parts(int H, int W) {

@@ -976,6 +976,7 @@ extern "C" int sa_conv3d(const float *in, int B, int Cin, int Di, int Hi, int Wi
 // slab reads wait for the DMA)
 static int sa_conv3d_wd_variant = 0;
 extern "C" void sa_conv3d_wd_set_variant(int variant) { sa_conv3d_wd_variant = variant; }
+extern "C" int sa_conv3d_wd_get_variant() { return sa_conv3d_wd_variant; }
 
 extern "C" int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W, const float *weight_wd, int Cout,
                             const float *in_mean, const float *in_rstd, int act, float slope, const float *gate_l,

@@ -41,6 +41,15 @@ __device__ __forceinline__ f16x4 dsplit(const float x) {
   return __builtin_shufflevector(hh, ll, 0, 1, 2, 3);
 }
 
+// the fp32 value w * 2^12 of a split weight dword (hi, lo): exact in fp32
+__device__ __forceinline__ float dunsplit(const float packed) {
+  const f16x2 p = __builtin_bit_cast(f16x2, packed);
+  return (float)p[0] + (float)p[1];
+}
+
+// blocks the split kernel's range guard recomputed on fp32 MFMA (sa_split_redo_blocks)
+__device__ unsigned g_direct_redo_blocks;
+
 constexpr int DOTH = 8, DOTW = 32, MT = 2;   // output tile; row segments of 16 pixels per wave
 
 template <int K, int S, int KC, int NTL, bool DS>
@@ -201,6 +210,54 @@ __global__ __launch_bounds__(512, DS ? 2 : 4) void conv_direct_kernel(const DirA
       __syncthreads();
     }
   }
+  if constexpr (SP) {
+    // Range guard (as conv2d_wino4.hip's split kernel): a patch value >= 65520 in magnitude
+    // overflows its f16 hi half and leaves NaN in the accumulators it fed; the block then
+    // recomputes on fp32 MFMA products
+    f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int t = 0; t < C::NACC; ++t) sum += acc[m][t];
+    const float tot = (sum.x + sum.y) + (sum.z + sum.w);
+    if (__syncthreads_or(!__builtin_isfinite(tot))) {
+      if (tid == 0) atomicAdd(&g_direct_redo_blocks, 1u);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int t = 0; t < C::NACC; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // a plain (unpipelined, rolled) loop: this path is rare, and a second copy of the
+      // pipelined one would raise the main loop's register pressure
+#pragma unroll 1
+      for (int chunk = 0; chunk < a.nchunks; ++chunk) {
+        fetch(chunk);
+        commit();
+        __syncthreads();
+#pragma unroll 1
+        for (int s = 0; s < C::KSTEPS; ++s) {
+          const int tap = (4 * s) / KC, ci0 = (4 * s) % KC;
+          const int koff = ci0 * PLANE + (tap / K) * PWP + (tap % K);
+#pragma unroll
+          for (int t = 0; t < NTL; ++t) {
+            const float w = dunsplit(sw[bbase + 4 * s * NCP + t * 16]);
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+              acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sx[abase[m] + koff], w, acc[m][t], 0, 0, 0);
+          }
+          if (DS && tap == (K / 2) * K + K / 2) {
+#pragma unroll
+            for (int t = 0; t < NTL; ++t) {
+              const float w = dunsplit(sd[bbase + ci0 * NCP + t * 16]);
+#pragma unroll
+              for (int m = 0; m < MT; ++m)
+                acc[m][NTL + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sx[abase[m] + koff], w, acc[m][NTL + t], 0, 0, 0);
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
 
   if constexpr (SP) {   // the weights' 2^12 (exact)
 #pragma unroll
@@ -347,6 +404,16 @@ extern "C" int sa_conv_direct_weights_split(const float *arranged, long n, void 
   hipStream_t s = sa::as_stream(stream);
   direct_split_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(arranged, n, static_cast<unsigned *>(out));
   return sa::check_launch("sa_conv_direct_weights_split");
+}
+
+long sa_direct_redo_blocks_internal(int reset) {
+  unsigned v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_direct_redo_blocks), sizeof v) != hipSuccess) return -1;
+  if (reset) {
+    const unsigned z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_direct_redo_blocks), &z, sizeof z) != hipSuccess) return -1;
+  }
+  return v;
 }
 
 extern "C" long sa_conv_direct_weights_size(int Cout, int Cin, int K, int S, int with_ds) {

@@ -179,6 +179,18 @@ extern "C" long sa_shear_level_offset(int W1, int W2, int num_levels, int level)
   return shear_geo(W1, W2, num_levels).off[level];
 }
 
+// 1 when the sheared pipeline (sa_corr_pyramid_shear + sa_corr_lookup_conv1x1_sheared) takes this
+// geometry: one grid z-slice per image row (B * H <= 65535), a 32-row LDS tile of the widest
+// level (W2 <= 511), a coarsest level of width >= 2 and a pixel count in int range
+extern "C" int sa_corr_shear_supported(int B, int H, int W1, int W2, int num_levels) {
+  if (B <= 0 || H <= 0 || W1 <= 0 || W2 <= 0 || num_levels != 4) return 0;
+  if ((long)B * H > 65535) return 0;
+  if ((long)SH_J * (W2 + 1) * 4 > 64 * 1024) return 0;
+  if (sa_pyramid_level_width(W2, num_levels - 1) < 2) return 0;
+  if ((long)B * H * W1 >= (1L << 31)) return 0;
+  return 1;
+}
+
 extern "C" int sa_corr_pyramid_shear(const float *pyramid, long row_stride, int B, int H, int W1, int W2,
                                      int num_levels, float *sheared, void *stream) {
   SA_REQUIRE(pyramid && sheared, "sa_corr_pyramid_shear: null pointer");

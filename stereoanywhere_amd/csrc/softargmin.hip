@@ -562,6 +562,7 @@ extern "C" void sa_softargmin_set_one_pass(int on) {
   sa_softargmin_one_pass = on ? 1 : 0;
   sa_softargmin_v4 = on == 2 ? 1 : 0;
 }
+extern "C" int sa_softargmin_get_one_pass() { return sa_softargmin_one_pass ? (sa_softargmin_v4 ? 2 : 1) : 0; }
 
 extern "C" int sa_softargmin_conf(const float *vol_disp, const float *vol_conf, int B, int H, int W1,
                                   int W2, long sb, long sh, long sj, long sk, float *dL, float *dR,

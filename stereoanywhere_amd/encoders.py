@@ -94,9 +94,11 @@ def direct_table(*modules: nn.Module) -> DirectTable:
             t[mod.conv1.weight.data_ptr()] = (ops.conv_direct_weights(mod.conv1.weight.detach().contiguous(), 1), None)
         for blk in mod.modules():
             if block_direct(blk):
-                t[blk.conv1.weight.data_ptr()] = (
-                    ops.conv_direct_weights(blk.conv1.weight.detach().contiguous(), 2),
-                    ops.conv_direct_weights(blk.downsample[0].weight.detach().contiguous(), 2, with_ds=True))
+                w3, w1 = blk.conv1.weight.detach().contiguous(), blk.downsample[0].weight.detach().contiguous()
+                # one launch: the 3x3 and its fused 1x1 both split or both fp32
+                sp = ops.DIRECT_SPLIT and ops.split_range_ok(w3, w1)
+                t[blk.conv1.weight.data_ptr()] = (ops.conv_direct_weights(w3, 2, split=sp),
+                                                  ops.conv_direct_weights(w1, 2, with_ds=True, split=sp))
     return t
 
 

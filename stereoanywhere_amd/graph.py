@@ -30,11 +30,16 @@ class ForwardGraph:
         m = self.model
         m._weights()   # the derived weights of the current parameter version
         from . import ops
+        from . import _native as N
         # everything that picks the captured kernels: the schedule, the module-level kernel
-        # switches (set by A/B scripts and tests) and the model's flags
+        # switches and the library's own A/B switches (set by A/B scripts and tests) and the
+        # model's flags
         args = tuple(sorted((k, repr(v)) for k, v in vars(m.args).items()))
+        lib = N.lib()
+        c_switches = (lib.sa_lookup_get_mfma(), lib.sa_softargmin_get_one_pass(), lib.sa_conv3d_wd_get_variant())
         return (tuple((tuple(x.shape), x.dtype, x.device) for x in xs), iters, dataclasses.astuple(m.opts),
-                m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_WIDE, ops.W4_QUAD, ops.W4_PERSIST, ops.W4_SPLIT, ops.DIRECT_SPLIT), args)
+                m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_WIDE, ops.W4_QUAD, ops.W4_PERSIST, ops.W4_SPLIT,
+                                                   ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS), c_switches, args)
 
     def __call__(self, image2, image3, mde2, mde3, iters: int = 12, test_mode: bool = True):
         if not test_mode:

@@ -101,6 +101,11 @@ class ScheduleOptions:
     # pyramid from the classifier output) -- measured slower: the diagonal row segments of a
     # 64 x 64 tile end mid-sector, and the partial 4-byte writes cost the stereo producer 16.1
     # instead of 3.0 ms at the booster batch, against 2.4 ms for the copy pass
+    # Memory: a sheared copy is ~2x its row-layout pyramid (~3.75x the volume), so the GRU loop
+    # holds ~7.5x the volume instead of ~3.75x; each row pyramid is released right after its copy
+    # (the stereo one before the mono pyramid is built), which bounds the build at ~9.4x (e.g.
+    # 16.5 GB for cfg5's 25-tile booster batch).  Geometries the sheared kernels do not take
+    # (ops.shear_supported: W4 > 511, B * H4 > 65535) keep the row layout.
     sheared_producers: bool = False
     shear_min_bytes: int = 1 << 30
     # a GRU level whose width is not a multiple of 4 keeps its planes padded to one (zero
@@ -335,14 +340,22 @@ class StereoAnywhere(nn.Module):
 
         # ---- pyramids
         trunc = (sm2, mirror) if a.use_truncate_vol else (None, None)
-        big = B * H4 * W4 * W4 * 4 >= self.opts.shear_min_bytes
-        direct = self.opts.sheared_lookup and self.opts.sheared_producers and big
+        # the sheared lookup for large volumes, where its kernels take the geometry (W4 <= 511,
+        # B * H4 <= 65535 image rows, 4 levels of radius 4); the row layout otherwise
+        big = (self.opts.sheared_lookup and B * H4 * W4 * W4 * 4 >= self.opts.shear_min_bytes
+               and a.corr_levels == 4 and a.corr_radius == 4 and ops.shear_supported(B, H4, W4, W4, a.corr_levels))
+        direct = self.opts.sheared_producers and big
         if a.use_aggregate_stereo_vol:
             stereo_blk = self._stereo_aggregate(dw, fmap2, fmap3, mde2, mde3, m2l, m3l, trunc, B, H4, W4)
         else:
             stereo_blk = HipCorrBlock1D.from_features(fmap2, fmap3, a.corr_levels, a.corr_radius, trunc[0], trunc[1],
                                                       float(a.mirror_attenuation), sheared=direct)
         del fmap2, fmap3
+        if big and stereo_blk.sheared is None:
+            # the sheared copy of the stereo pyramid before the mono pyramid exists, and the row
+            # layout released right after it: at most one row pyramid and one sheared copy are
+            # live at a time besides the finished copies
+            stereo_blk.shear(release=True)
         if a.use_aggregate_mono_vol:
             mono_rows = vol_d.permute(0, 1, 3, 4, 2)  # [B,1,H,W1,W2] view (transposed by the pyramid kernel)
         else:
@@ -354,14 +367,11 @@ class StereoAnywhere(nn.Module):
         if mono_blk.sheared is None:
             mono_blk.pyramid = ops.pyramid_from_volume(mono_rows, a.corr_levels)
         del mono_rows, vol_d, vol_c
-
-        if self.opts.sheared_lookup and big:
+        if big and mono_blk.sheared is None:
             # the lookups read disparity-sheared pyramids (coalesced across a wave's pixels); a
             # block whose producer wrote the row layout gets a sheared copy (the row-layout
-            # buffers are not read again)
-            for blk in (stereo_blk, mono_blk):
-                if blk.sheared is None:
-                    blk.shear(release=True)
+            # buffer is not read again)
+            mono_blk.shear(release=True)
         parts = min(self.opts.loop_parts, B) if self.stream_overlap else 1
         if parts <= 1:
             return _drive(self._iterate(dw, hid, ctx, stereo_blk, mono_blk, coords_x, iters, B, H4, W4))

@@ -229,6 +229,12 @@ def corr_lookup_conv1x1(pyr_a: torch.Tensor, pyr_b: Optional[torch.Tensor], W2: 
     return out
 
 
+def shear_supported(B: int, H: int, W1: int, W2: int, num_levels: int = 4) -> bool:
+    """Whether the sheared lookup pipeline takes this geometry (sa_corr_shear_supported: B*H <=
+    65535 image rows, W2 <= 511 for the shear pass's LDS tile, 4 levels); else the row layout."""
+    return bool(N.lib().sa_corr_shear_supported(B, H, W1, W2, num_levels))
+
+
 def corr_pyramid_shear(pyr: torch.Tensor, B: int, H: int, W1: int, W2: int, num_levels: int = 4) -> torch.Tensor:
     """Row-layout pyramid [B*H*W1, row_stride] -> its disparity-sheared copy [B*H, slice]
     (sa_corr_pyramid_shear; read by corr_lookup_conv1x1_sheared)."""
@@ -739,6 +745,14 @@ _W4_SPLIT_WMAX = 15.99
 DIRECT_SPLIT = True
 
 
+def split_range_ok(*weights: Optional[torch.Tensor]) -> bool:
+    """Whether the split kernels' f16 filter pairs hold these weights: |w * 2^12| < 65504 (and the
+    F(4x4,3x3) transform keeps |U| <= max |w|), i.e. |w| < 16.  Otherwise the conv keeps its fp32
+    filters and runs on the fp32-product kernels (e.g. an eval-BatchNorm-folded conv of a trained
+    checkpoint with a large gamma / sqrt(var))."""
+    return all(w is None or float(w.abs().max()) < _W4_SPLIT_WMAX for w in weights)
+
+
 def wino_weights(weight: torch.Tensor) -> WinoFilters:
     """[Cout, Cin, 3, 3] -> Winograd filters (fp64 transforms, rounded once): U2 [16][Cin/8][4][Cout][2]
     and U4 [Cout/32][Cin/8][36][2][4][32], each in a flat container."""
@@ -753,9 +767,9 @@ def wino_weights(weight: torch.Tensor) -> WinoFilters:
         u4w = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.float32)
         N.call("sa_conv2d_wino4_weights_cb", weight.data_ptr(), Cout, Cin, 64, u4w.data_ptr(), _stream(weight))
     u4s = None
-    if W4_SPLIT and Cout % 32 == 0 and Cin % 8 == 0:
-        if float(weight.abs().max()) >= _W4_SPLIT_WMAX:
-            raise RuntimeError("wino_weights: |weight| >= 16 exceeds the split kernel's f16 filter range")
+    # (a conv whose filters exceed the split kernel's f16 range keeps u4s = None: its launches run
+    # the fp32-product kernel, conv2d_k3_multi)
+    if W4_SPLIT and Cout % 32 == 0 and Cin % 8 == 0 and split_range_ok(weight):
         u4s = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.int32)
         N.call("sa_conv2d_wino4_weights_split", weight.data_ptr(), Cout, Cin, u4s.data_ptr(), _stream(weight))
     return WinoFilters(u2, u4, Cin, Cout, u4w, u4s)
@@ -948,9 +962,12 @@ def conv2d_k3(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = N
                                 stats=stats))[0]
 
 
-def conv_direct_weights(weight: torch.Tensor, stride: int, with_ds: bool = False) -> torch.Tensor:
+def conv_direct_weights(weight: torch.Tensor, stride: int, with_ds: bool = False,
+                        split: Optional[bool] = None) -> torch.Tensor:
     """[Cout, Cin, K, K] -> the direct-conv kernel's chunked layout (sa_conv_direct_weights).
-    with_ds: the weight is the 1x1 downsample fused into a stride-``stride`` 3x3 launch."""
+    with_ds: the weight is the 1x1 downsample fused into a stride-``stride`` 3x3 launch.
+    split: the split kernel's (hi, lo) pairs (default: DIRECT_SPLIT where split_range_ok; a 3x3
+    and its fused downsample must agree, encoders.direct_table decides for both)."""
     _check(weight, "weight")
     Cout, Cin, K, _ = weight.shape
     n = int(N.lib().sa_conv_direct_weights_size(Cout, Cin, K, stride, 1 if with_ds else 0))
@@ -959,9 +976,11 @@ def conv_direct_weights(weight: torch.Tensor, stride: int, with_ds: bool = False
     out = torch.empty((n,), device=weight.device, dtype=torch.float32)
     N.call("sa_conv_direct_weights", weight.data_ptr(), Cout, Cin, K, stride, 1 if with_ds else 0, out.data_ptr(),
            _stream(weight))
-    if DIRECT_SPLIT:   # the split kernel's (hi, lo) pairs: an int32 container marks them
-        if float(weight.abs().max()) >= _W4_SPLIT_WMAX:
-            raise RuntimeError("conv_direct_weights: |weight| >= 16 exceeds the split kernel's f16 range")
+    if split is None:
+        split = DIRECT_SPLIT and split_range_ok(weight)
+    elif split and not split_range_ok(weight):
+        raise RuntimeError("conv_direct_weights: |weight| >= 16 exceeds the split kernel's f16 range")
+    if split:   # the split kernel's (hi, lo) pairs: an int32 container marks them
         sp = torch.empty((n,), device=weight.device, dtype=torch.int32)
         N.call("sa_conv_direct_weights_split", out.data_ptr(), n, sp.data_ptr(), _stream(weight))
         return sp

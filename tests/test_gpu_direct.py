@@ -56,3 +56,44 @@ def test_unsupported_shapes_raise():
     x = rnd(1, 12, 16, 16)
     with pytest.raises(RuntimeError):
         ops.conv_direct_weights(rnd(80, 12, 3, 3), 2, with_ds=False)
+
+
+def test_split_weights_beyond_range_keep_fp32(monkeypatch):
+    """Weights beyond the split kernel's f16 range (|w| >= 16) keep the fp32 layout (and a 3x3 and
+    its fused downsample agree, encoders.direct_table) instead of failing the forward."""
+    monkeypatch.setattr(ops, "DIRECT_SPLIT", True)
+    w = rnd(96, 64, 3, 3, seed=4) / 24
+    w[3, 2, 1, 1] = 20.0
+    wg_ = ops.conv_direct_weights(w, 2)
+    assert wg_.dtype == torch.float32
+    assert ops.conv_direct_weights(rnd(96, 64, 1, 1, seed=5) / 8, 2, with_ds=True, split=False).dtype == torch.float32
+    with pytest.raises(RuntimeError):
+        ops.conv_direct_weights(w, 2, split=True)
+    x = rnd(2, 64, 34, 70, seed=3)
+    (out,) = ops.conv_direct(x, wg_, 3, 2, 96)
+    torch.testing.assert_close(out, F.conv2d(x, w, stride=2, padding=1), atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("K,S", [(7, 1), (3, 2)])
+def test_split_range_guard(monkeypatch, K, S):
+    """Input values past the f16 range (|x| >= 65520) in part of the image: the split kernel's
+    range guard recomputes those blocks on fp32 MFMA products in the same launch; the output is
+    finite and equals the fp32-product kernel."""
+    from stereoanywhere_amd import _native as N
+    Cin, Cout = (3, 64) if K == 7 else (64, 96)
+    x = rnd(2, Cin, 40, 96, seed=6)
+    x[1, :, 3:9, 20:50] *= 1e5
+    w = rnd(Cout, Cin, K, K, seed=7) / (K * Cin ** 0.5)
+    outs = {}
+    for split in (False, True):
+        monkeypatch.setattr(ops, "DIRECT_SPLIT", split)
+        N.lib().sa_split_redo_blocks(1)
+        (o,) = ops.conv_direct(x, ops.conv_direct_weights(w, S), K, S, Cout)
+        outs[split] = (o, int(N.lib().sa_split_redo_blocks(1)))
+    ref = F.conv2d(x.double(), w.double(), stride=S, padding=K // 2).float()
+    scale = float(ref.abs().max())
+    ys, redo = outs[True]
+    print(f"direct range guard K{K}: {redo} blocks redone")
+    assert torch.isfinite(ys).all() and redo > 0 and outs[False][1] == 0
+    assert float((ys - ref).abs().max()) / scale < 1e-5
+    assert float((ys - outs[False][0]).abs().max()) / scale < 1e-5

@@ -81,6 +81,69 @@ def test_unpadded_sizes_vs_reference(model, i, H, W):
     assert e < 1e-3
 
 
+def test_configs3_rank_shard_b8(model):
+    """BASELINE configs[3] (batch 64 sharded 8-way) as one rank runs it: B = 8 pairs
+    at 544x960, 22 iterations, seeds 1..8 as bench.py --config cfg4 feeds rank 0.  Every pair is
+    finite, equals its own B = 1 forward, and pair 0 (seed 1) matches the reference fixture."""
+    from stereoanywhere_amd.graph import ForwardGraph
+    fix = load_fixture("cfg2_544x960_it22.npz")
+    pb = synth.synthetic_batch(8, 544, 960, 192.0, seed0=1)
+    batch = run(model, pb, 22)
+    assert np.isfinite(batch).all()
+    e0 = epe(batch[0:1], fix["disparity"])
+    print("cfg4 shard pair 0 EPE vs reference", e0)
+    assert e0 < 1e-3
+    for i in range(8):
+        single = run(model, {k: v[i:i + 1] for k, v in pb.items()}, 22)
+        e = epe(batch[i:i + 1], single)
+        assert e < 1e-4, (i, e)
+    # the bench's execution mode (graph replay of the batch-8 forward) gives the same result
+    x = [torch.from_numpy(pb[k]).cuda() for k in ("left", "right", "mono_left", "mono_right")]
+    with torch.no_grad():
+        g = -ForwardGraph(model)(*x, iters=22)[0][:, 0].cpu().numpy()
+    assert epe(g, batch) < 1e-6
+
+
+def test_large_disparity_split_vs_fp32(model, monkeypatch):
+    """cfg5's D = 512 extreme on the split kernels: a 128x1024 pair with disparities up to 0.9 x 512
+    px (flow up to ~115 px at 1/4 resolution in the GRU's input planes): finite, and the split
+    kernels (with their range guard) agree with the fp32-product kernels end to end."""
+    from stereoanywhere_amd import ops
+    pb = synth.synthetic_batch(1, 128, 1024, 512.0, seed0=3)
+    out = {}
+    for split in (False, True):
+        monkeypatch.setattr(ops, "W4_SPLIT", split)
+        monkeypatch.setattr(ops, "DIRECT_SPLIT", split)
+        out[split] = run(model, pb, 8)
+    assert np.isfinite(out[True]).all() and np.isfinite(out[False]).all()
+    assert float(np.abs(out[True]).max()) > 50.0   # the large-disparity regime is exercised
+    e = epe(out[True], out[False])
+    print("D=512 split vs fp32 EPE", e)
+    assert e < 1e-3
+
+
+def test_sheared_lookup_outside_kernel_range_keeps_row_layout(model):
+    """A width whose pyramid the shear kernels do not take (W/4 = 520 > 511) with the sheared
+    lookup forced on (shear_min_bytes = 0) falls back to the row layout: same result as the
+    sheared lookup off; a width inside the range takes the sheared path, bit-exact."""
+    import dataclasses
+
+    from stereoanywhere_amd import ops
+    assert not ops.shear_supported(1, 8, 520, 520) and ops.shear_supported(1, 16, 256, 256)
+    old = model.opts
+    try:
+        for H, W in ((32, 2080), (64, 1024)):
+            pb = synth.synthetic_batch(1, H, W, 96.0, seed0=4)
+            model.opts = dataclasses.replace(old, shear_min_bytes=0)
+            a = run(model, pb, 3)
+            model.opts = dataclasses.replace(old, sheared_lookup=False)
+            b = run(model, pb, 3)
+            assert np.isfinite(a).all()
+            assert float(np.abs(a - b).max()) < 1e-5, (H, W)
+    finally:
+        model.opts = old
+
+
 def test_size_not_multiple_of_4_is_rejected(model):
     t = [torch.zeros(1, c, 66, 98, device="cuda") for c in (3, 3, 1, 1)]
     with pytest.raises(RuntimeError):

@@ -495,13 +495,99 @@ def test_wino4_split_operand_range(monkeypatch, mag):
             assert es < 5e-3 and rs < 5e-4, (es, rs)
 
 
-def test_wino4_split_weights_range():
-    """Filters beyond the split kernel's f16 range are refused when derived, not overflowed."""
-    import stereoanywhere_amd.ops as o
-    old = o.W4_SPLIT
-    o.W4_SPLIT = True
-    try:
-        with pytest.raises(RuntimeError):
-            o.wino_weights(rnd(32, 8, 3, 3, seed=1) * 40)
-    finally:
-        o.W4_SPLIT = old
+def test_wino4_split_weights_range(monkeypatch):
+    """Filters beyond the split kernel's f16 range (|w| >= 16, e.g. an eval-BatchNorm-folded conv
+    of a trained checkpoint) keep fp32 filters: the conv runs on the fp32-product kernel."""
+    monkeypatch.setattr(ops, "W4_SPLIT", True)
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    w = rnd(32, 64, 3, 3, seed=1) / 24
+    w[0, 0, 1, 1] = 20.0
+    U = ops.wino_weights(w)
+    assert U.u4s is None and U.u4 is not None
+    x = rnd(2, 64, 20, 64, seed=2)
+    (got,), work = _run(monkeypatch, True, dict(x=x, U=U))
+    assert "conv2d_wino4" in work
+    ref = F.conv2d(x.double(), w.double(), padding=1).float()
+    scale = float(ref.pow(2).mean().sqrt())
+    assert float((got - ref).abs().max()) < 1e-4 * scale
+
+
+def _redo_blocks(reset=True):
+    from stereoanywhere_amd import _native as N
+    n = int(N.lib().sa_split_redo_blocks(1 if reset else 0))
+    assert n >= 0
+    return n
+
+
+@pytest.mark.parametrize("mag", [300.0, 3000.0, 1e5])
+def test_wino4_split_range_guard(monkeypatch, mag):
+    """Inputs whose transformed values pass the f16 range (|V| up to ~100 x the input): the split
+    kernel's range guard recomputes those blocks on fp32 MFMA products inside the launch, so the
+    output is finite and equals the fp32-product kernel; in-range blocks stay on the split path.
+    Only part of the image is scaled, so guarded and unguarded blocks share one launch."""
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    x = rnd(2, 64, 36, 256, seed=3)
+    x[0, :, 4:12, 70:90] *= mag   # one region of image 0
+    w = rnd(96, 64, 3, 3, seed=4) / 24
+    ref = F.conv2d(x.double(), w.double(), padding=1).float()
+    monkeypatch.setattr(ops, "W4_SPLIT", False)
+    (yf,), _ = _run(monkeypatch, True, dict(x=x, U=ops.wino_weights(w)))
+    monkeypatch.setattr(ops, "W4_SPLIT", True)
+    U = ops.wino_weights(w)
+    assert U.u4s is not None
+    _redo_blocks()
+    (ys,), _ = _run(monkeypatch, True, dict(x=x, U=U))
+    redo = _redo_blocks()
+    assert torch.isfinite(ys).all()
+    scale = float(ref.abs().max())
+    es, ef = float((ys - ref).abs().max()) / scale, float((yf - ref).abs().max()) / scale
+    print(f"range guard x{mag:g}: {redo} blocks redone; split max {es:.2e}, fp32 kernel {ef:.2e} (of max |y|)")
+    assert es < 1e-5 and float((ys - yf).abs().max()) / scale < 1e-5
+    # 2 x 36 x 256 at 16 x 64 px per block and 96 / 32 channel blocks: 2 x 3 x 4 x 3 = 72 blocks;
+    # the scaled region overflows (|V| >= 65520) from mag ~ 300 on: a few blocks, never all
+    if mag >= 3000:
+        assert 0 < redo < 72, redo
+
+
+def test_wino4_split_range_guard_gate_and_input_transform(monkeypatch):
+    """The guard ahead of the epilogues: a mode-2 gate epilogue updating h IN PLACE, and an
+    input-transform launch (the producer's norm on load scaled so the staged values overflow),
+    both equal the fp32-product kernel."""
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    B, hd, H, W = 2, 32, 16, 64
+    g = torch.Generator(device="cpu").manual_seed(7)
+
+    def r(*s):
+        return torch.randn(*s, generator=g).to(dev)
+    rh = r(B, hd, H, W)
+    rh[1, :, 2:6, 10:30] *= 5000.0
+    wq = r(hd, hd, 3, 3) / 17
+    bq = r(hd)
+    ctx, z0, h0, add = r(B, hd, H, W), torch.sigmoid(r(B, hd, H, W)), torch.tanh(r(B, hd, H, W)), r(B, hd, H, W)
+    outs = {}
+    for split in (False, True):
+        monkeypatch.setattr(ops, "W4_SPLIT", split)
+        h = h0.clone()
+        _redo_blocks()
+        _run(monkeypatch, True, dict(x=rh, U=ops.wino_weights(wq), bias=bq, out=h,
+                                     gate=dict(mode=2, ctx=ctx, h=h, z=z0, add=add)))
+        outs[split] = (h, _redo_blocks())
+    assert torch.isfinite(outs[True][0]).all() and outs[True][1] > 0 and outs[False][1] == 0
+    torch.testing.assert_close(outs[True][0], outs[False][0], atol=2e-5, rtol=1e-5)
+    # input transform: per-channel affine with a large scale on a few channels (norm on load)
+    x = r(B, 64, H, W)
+    w = r(64, 64, 3, 3) / 24
+    s_ = torch.ones(64, device=dev)
+    s_[5] = 4000.0
+    aff = ops.Affine(s=s_, t=torch.zeros(64, device=dev))
+    res = {}
+    for split in (False, True):
+        monkeypatch.setattr(ops, "W4_SPLIT", split)
+        _redo_blocks()
+        (y,), _ = _run(monkeypatch, True, dict(x=x, U=ops.wino_weights(w), in_aff=aff, in_act="relu"))
+        res[split] = (y, _redo_blocks())
+    ref = F.conv2d(torch.relu(x * s_.view(1, -1, 1, 1)).double(), w.double(), padding=1).float()
+    scale = float(ref.abs().max())
+    assert torch.isfinite(res[True][0]).all() and res[True][1] > 0
+    assert float((res[True][0] - ref).abs().max()) / scale < 1e-5
+    assert float((res[True][0] - res[False][0]).abs().max()) / scale < 1e-5
