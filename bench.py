@@ -397,6 +397,9 @@ def main():
                     help="F(4x4) convs on the split kernel (1) or fp32 MFMA (0); default: ops.W4_SPLIT")
     ap.add_argument("--direct-split", type=int, default=None, choices=[0, 1],
                     help="direct convs on split products (1) or fp32 MFMA (0); default: ops.DIRECT_SPLIT")
+    ap.add_argument("--offload-release", type=int, default=1, choices=[0, 1],
+                    help="cfg5: CPUOffloadWrapper empties the allocator cache after each call (1, the "
+                         "reference's behaviour) or keeps its pools (0)")
     ap.add_argument("--wino4-min-blocks", type=int, default=None,
                     help="F(4x4) for launches of at least this many blocks (default: ops._WINO4_MIN_BLOCKS)")
     args = ap.parse_args()
@@ -443,7 +446,9 @@ def main():
         # the tiler runs each unique rectangle once (tiler.TileWrapper: duplicates are
         # accumulated again, not recomputed)
         tiled["tiles"], tiled["unique_tiles"], tiled["tile_hw"] = len(tiles), len(set(tiles)), (th, tw)
-        runner = CPUOffloadWrapper(wrap) if tiled["offload"] else wrap
+        # the reference empties the caching allocator after every call (cpu_offload_wrapper.py:82):
+        # release_cache=True times that behaviour (--offload-release 0: HBM-resident pools)
+        runner = CPUOffloadWrapper(wrap, release_cache=bool(args.offload_release)) if tiled["offload"] else wrap
         units, shape = 1, (len(set(tiles)), th // 4, tw // 4)
 
     eager_runner = runner
@@ -572,6 +577,12 @@ def main():
     # F(4x4) epilogues (W % 4 != 0): priced per call (ops.gru_zr / gru_out, 9 resp. 6-7 planes)
     costs["gru_zr"] = ("GB/s", work.get("gru_zr", 0.0))
     costs["gru_out"] = ("GB/s", work.get("gru_out", 0.0))
+    # the update loop's plumbing (pool2x / interp / flow_update: planes read and written once),
+    # flow_head.conv2 (256 -> 2 planes), the mono pyramid (volume read, levels written) and convf1
+    # (7x7, 2 -> 64 channels on fp32 MFMA), each priced per call (ops._account)
+    for k_, u_ in (("gru_plumbing", "GB/s"), ("conv2d_narrow", "GB/s"), ("mono_pyramid", "GB/s"),
+                   ("conv2d_small", "TFLOP/s")):
+        costs[k_] = (u_, work.get(k_, 0.0))
     kernels = {}
     for k, (ms_tot, n_launch) in kt.items():
         if n_launch == 0 or k not in costs:
@@ -637,9 +648,11 @@ def main():
                               f"{tiled['preset']} -> {tiled['tiles']} tiles of {th}x{tw} ({tiled['unique_tiles']} unique rectangles, "
                               f"each run once; batch_tiles), "
                               f"{iters} GRU iters, published flags"
-                              + (", CPUOffloadWrapper (HBM-resident)" if tiled["offload"] else ""),
+                              + (f", CPUOffloadWrapper (HBM-resident weights and mono maps, release_cache="
+                                 f"{bool(args.offload_release)})" if tiled["offload"] else ""),
                   "global_batch": r.world, "tiles_per_image": tiled["tiles"],
                   "unique_tile_forwards_per_image": tiled["unique_tiles"], "iters": iters,
+                  "release_cache": bool(args.offload_release) if tiled["offload"] else None,
                   "parallelism": f"dp{r.world} (independent images)"}
     res = {
         "metric": metric, "value": total_units / elapsed, "unit": unit, "n_gpus": r.world, "steps": args.steps,

@@ -479,7 +479,7 @@ int sa_norm_act(const float *x, long x_bs, int B, int C, long hw, const float *m
 enum {
   SA_K_CORR_PYRAMID = 0, SA_K_LOOKUP, SA_K_MONO_VOLUME, SA_K_SOFTARGMIN, SA_K_LSQ,
   SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_NORM, SA_K_CONV2D, SA_K_CONV_DIRECT,
-  SA_K_CONV2D_W4, SA_K_SHEAR, SA_K_COUNT
+  SA_K_CONV2D_W4, SA_K_SHEAR, SA_K_MONO_PYRAMID, SA_K_PLUMBING, SA_K_CONV_SMALL, SA_K_NARROW, SA_K_COUNT
 };
 int sa_timing_enable(int on);
 int sa_timing_read(int kernel_id, double *total_ms, long *count);

@@ -121,6 +121,7 @@ KERNEL_IDS = {
     "corr_volume_pyramid": 0, "corr_lookup": 1, "mono_masked_volume": 2, "softargmin_conf": 3,
     "weighted_lsq": 4, "gru_zr": 5, "gru_out": 6, "convex_upsample": 7, "misc": 8, "conv3d_fused": 9,
     "norm_act": 10, "conv2d_wino": 11, "conv2d_direct": 12, "conv2d_wino4": 13, "corr_shear": 14,
+    "mono_pyramid": 15, "gru_plumbing": 16, "conv2d_small": 17, "conv2d_narrow": 18,
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -255,7 +255,7 @@ extern "C" int sa_conv2d_k3_narrow(const float *in, long in_bs, int B, int Cin, 
   SA_REQUIRE((long)H * W < (1L << 31), "sa_conv2d_k3_narrow: plane too large");
   dim3 grid((unsigned)((W + NCOL - 1) / NCOL), (unsigned)((H + NR - 1) / NR), (unsigned)B);
   hipStream_t s = sa::as_stream(stream);
-  sa::TimingScope ts(SA_K_MISC, s);
+  sa::TimingScope ts(SA_K_NARROW, s);
   if (Cout == 2) {
     conv2d_k3_narrow_kernel<2><<<grid, 512, 0, s>>>(in, in_bs, Cin, H, W, weight, bias, out, out_bs);
     return sa::check_launch("sa_conv2d_k3_narrow");
@@ -273,7 +273,7 @@ extern "C" int sa_conv2d_small(const float *in, long in_bs, int B, int Cin, int 
              ksize, Cout);
   dim3 grid((W + T - 1) / T, (H + T - 1) / T, B);
   hipStream_t s = sa::as_stream(stream);
-  sa::TimingScope ts(SA_K_MISC, s);
+  sa::TimingScope ts(SA_K_CONV_SMALL, s);
   const bool aligned = (reinterpret_cast<uintptr_t>(out) & 15) == 0 && out_bs % 4 == 0;
   if (Cin == F1_CIN && aligned)
     conv2d_f1_mfma_kernel<<<grid, 256, 0, s>>>(in, in_bs, H, W, weight, bias, relu, out, out_bs);

@@ -682,7 +682,7 @@ extern "C" int sa_corr_pyramid_from_volume(const float *volume, long rows, int W
              "sa_corr_pyramid_from_volume: row_stride too small");
   Geo g = make_geo(1, 1, 1, W2, num_levels, row_stride);
   hipStream_t s = sa::as_stream(stream);
-  sa::TimingScope ts(SA_K_MISC, s);
+  sa::TimingScope ts(SA_K_MONO_PYRAMID, s);
   pyramid_from_volume_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(volume, rows, W2, in_row_stride, g, pyramid);
   return sa::check_launch("sa_corr_pyramid_from_volume");
 }
@@ -702,7 +702,7 @@ extern "C" int sa_corr_pyramid_from_volume_strided(const float *volume, int B, i
              "sa_corr_pyramid_from_volume_strided: needs W1 %% 4 == 0 and 16-byte aligned volume rows");
   Geo g = make_geo(1, 1, 1, W2, num_levels, row_stride);
   hipStream_t s = sa::as_stream(stream);
-  sa::TimingScope ts(SA_K_MISC, s);
+  sa::TimingScope ts(SA_K_MONO_PYRAMID, s);
   pyramid_from_strided_kernel<<<dim3((unsigned)((W1 + PT_J - 1) / PT_J), (unsigned)H, (unsigned)B), 256, 0, s>>>(
       volume, sb, sh, sk, H, W1, W2, g, pyramid, ShOut{});
   return sa::check_launch("sa_corr_pyramid_from_volume_strided");
@@ -733,7 +733,7 @@ extern "C" int sa_corr_pyramid_from_volume_strided_sheared(const float *volume, 
              "sa_corr_pyramid_from_volume_strided_sheared: needs W1 %% 4 == 0 and 16-byte aligned volume rows");
   Geo g = make_geo(1, 1, 1, W2, num_levels, 0);
   hipStream_t s = sa::as_stream(stream);
-  sa::TimingScope ts(SA_K_MISC, s);
+  sa::TimingScope ts(SA_K_MONO_PYRAMID, s);
   pyramid_from_strided_kernel<true><<<dim3((unsigned)((W1 + PT_J - 1) / PT_J), (unsigned)H, (unsigned)B), 256, 0, s>>>(
       volume, sb, sh, sk, H, W1, W2, g, nullptr, make_shout(sheared, W1, W2, num_levels));
   return sa::check_launch("sa_corr_pyramid_from_volume_strided_sheared");

@@ -293,7 +293,7 @@ extern "C" int sa_pool2x_p(const float *in, long in_bs, int in_pitch, int B, int
   SA_REQUIRE(in_pitch >= W && out_pitch >= Wo, "sa_pool2x: row pitch below the width");
   SA_REQUIRE((long)H * in_pitch < (1L << 31), "sa_pool2x: plane too large");
   hipStream_t s = sa::as_stream(stream);
-  sa::TimingScope ts(SA_K_MISC, s);
+  sa::TimingScope ts(SA_K_PLUMBING, s);
   if (in_pitch == W && out_pitch == Wo && W % 8 == 0 && Wo % 4 == 0 && al16(in) && al16(out) && in_bs % 4 == 0 &&
       out_bs % 4 == 0)
     pool2x_v4_kernel<<<dim3((Wo / 4 + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, out,
@@ -321,7 +321,7 @@ extern "C" int sa_interp_bilinear_ac_p(const float *in, long in_bs, int in_pitch
   const float sh = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.0f;
   const float sw = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.0f;
   hipStream_t s = sa::as_stream(stream);
-  sa::TimingScope ts(SA_K_MISC, s);
+  sa::TimingScope ts(SA_K_PLUMBING, s);
   if (out_pitch == Wo && Wo % 4 == 0 && al16(out) && out_bs % 4 == 0)
     interp_v4_kernel<<<dim3((Wo / 4 + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, sh, sw,
                                                                                    out, out_bs, in_pitch);
@@ -342,7 +342,7 @@ extern "C" int sa_relu_copy(const float *in, long in_bs, int B, int C, int HW, f
   SA_REQUIRE(B > 0 && B <= 65535 && C > 0 && HW > 0 && (long)C * HW < (1L << 31), "sa_relu_copy: bad shape");
   const unsigned per = (unsigned)((long)C * HW);
   hipStream_t s = sa::as_stream(stream);
-  sa::TimingScope ts(SA_K_MISC, s);
+  sa::TimingScope ts(SA_K_PLUMBING, s);
   relu_copy_kernel<<<dim3((per + 255) / 256, B), 256, 0, s>>>(in, in_bs, per, out, out_bs);
   return sa::check_launch("sa_relu_copy");
 }
@@ -353,7 +353,7 @@ extern "C" int sa_flow_update(float *coords_x, const float *delta, long delta_bs
   SA_REQUIRE(B > 0 && B <= 65535 && H > 0 && W > 0 && (long)H * W < (1L << 31), "sa_flow_update: bad shape");
   const unsigned hw = (unsigned)((long)H * W);
   hipStream_t s = sa::as_stream(stream);
-  sa::TimingScope ts(SA_K_MISC, s);
+  sa::TimingScope ts(SA_K_PLUMBING, s);
   flow_update_kernel<<<dim3((hw + 255) / 256, B), 256, 0, s>>>(coords_x, delta, delta_bs, W, hw, flow_a, flow_a_bs,
                                                                 flow_b, flow_b_bs);
   return sa::check_launch("sa_flow_update");

@@ -136,6 +136,7 @@ def pyramid_from_volume_sheared(volume: torch.Tensor, num_levels: int = 4) -> Op
     out = torch.empty((B * H, slice_sz), device=volume.device, dtype=torch.float32)
     N.call("sa_corr_pyramid_from_volume_strided_sheared", volume.data_ptr(), B, H, W1, W2, volume.stride(0),
            volume.stride(2), volume.stride(4), num_levels, out.data_ptr(), _stream(volume))
+    _account("mono_pyramid", 4.0 * B * H * W1 * (W2 + sum(pyramid_geometry(W2, num_levels)[2])))
     return out
 
 
@@ -162,6 +163,8 @@ def pyramid_from_volume(volume: torch.Tensor, num_levels: int = 4) -> torch.Tens
         out = torch.empty((B * H * W1, rs), device=volume.device, dtype=torch.float32)
         N.call("sa_corr_pyramid_from_volume_strided", volume.data_ptr(), B, H, W1, W2, volume.stride(0),
                volume.stride(2), volume.stride(4), num_levels, out.data_ptr(), rs, _stream(volume))
+        # the volume read once, every level cell written once
+        _account("mono_pyramid", 4.0 * B * H * W1 * (W2 + sum(pyramid_geometry(W2, num_levels)[2])))
         return out
     rows2d = volume.reshape(-1, W2)
     if rows2d.stride(1) != 1 and volume.dim() == 5:   # a strided view the kernel above cannot take
@@ -172,6 +175,7 @@ def pyramid_from_volume(volume: torch.Tensor, num_levels: int = 4) -> torch.Tens
     out = torch.empty((rows2d.shape[0], rs), device=volume.device, dtype=torch.float32)
     N.call("sa_corr_pyramid_from_volume", rows2d.data_ptr(), rows2d.shape[0], W2, rows2d.stride(0),
            num_levels, out.data_ptr(), rs, _stream(volume))
+    _account("mono_pyramid", 4.0 * rows2d.shape[0] * (W2 + sum(pyramid_geometry(W2, num_levels)[2])))
     return out
 
 
@@ -442,6 +446,7 @@ def pool2x(x: torch.Tensor, out: torch.Tensor, width: Optional[int] = None,
         raise RuntimeError(f"pool2x: out {tuple(out.shape)} (width {out_width}) != {(B, C, Ho, Wo)}")
     N.call("sa_pool2x_p", x.data_ptr(), _pitched_bs(x, "x"), Px, B, C, H, W, out.data_ptr(),
            _pitched_bs(out, "out"), Po, _stream(x))
+    _account("gru_plumbing", 4.0 * B * C * (H * W + Ho * Wo))   # input read once, output written
     return out
 
 
@@ -454,6 +459,7 @@ def interp(x: torch.Tensor, out: torch.Tensor, width: Optional[int] = None,
         raise RuntimeError("interp: batch/channels mismatch")
     N.call("sa_interp_bilinear_ac_p", x.data_ptr(), _pitched_bs(x, "x"), Px, B, C, H, width or Px, Ho,
            out_width or Po, out.data_ptr(), _pitched_bs(out, "out"), Po, _stream(x))
+    _account("gru_plumbing", 4.0 * B * C * (H * (width or Px) + Ho * (out_width or Po)))
     return out
 
 
@@ -463,6 +469,7 @@ def relu_copy(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         raise RuntimeError("relu_copy: shape mismatch")
     N.call("sa_relu_copy", x.data_ptr(), _plane_bs(x, "x"), B, C, H * W, out.data_ptr(), _plane_bs(out, "out"),
            _stream(x))
+    _account("gru_plumbing", 8.0 * B * C * H * W)
     return out
 
 
@@ -473,6 +480,9 @@ def flow_update(coords_x: torch.Tensor, delta: Optional[torch.Tensor], flow_a: O
     N.call("sa_flow_update", coords_x.data_ptr(), _ptr(delta), 0 if delta is None else _plane_bs(delta, "delta"),
            B, H, W, _ptr(flow_a), 0 if flow_a is None else _plane_bs(flow_a, "flow_a"), _ptr(flow_b),
            0 if flow_b is None else _plane_bs(flow_b, "flow_b"), _stream(coords_x))
+    # coords read (+ written with a delta read), each flow plane written
+    _account("gru_plumbing", 4.0 * B * H * W * (1 + (2 if delta is not None else 0)
+                                                + (flow_a is not None) + (flow_b is not None)))
 
 
 def convex_upsample(flow_x: torch.Tensor, mask: torch.Tensor, factor: int = 4) -> torch.Tensor:
@@ -641,6 +651,7 @@ def conv2d_small(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor
     out = torch.empty((B, cout, H, W), device=x.device, dtype=torch.float32)
     N.call("sa_conv2d_small", x.data_ptr(), bs, B, Cin, H, W, w_t.data_ptr(), _ptr(bias), cout, ksize,
            1 if relu else 0, out.data_ptr(), cout * H * W, _stream(x))
+    _account("conv2d_small", 2.0 * B * cout * Cin * ksize * ksize * H * W)
     return out
 
 
@@ -705,6 +716,7 @@ def conv2d_k3_narrow(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch
     out = torch.empty((B, cout, H, W), device=x.device, dtype=torch.float32)
     N.call("sa_conv2d_k3_narrow", x.data_ptr(), bs, B, Cin, H, W, weight.data_ptr(), _ptr(bias), cout,
            out.data_ptr(), cout * H * W, _stream(x))
+    _account("conv2d_narrow", 4.0 * B * (Cin + cout) * H * W)   # the input read once, the output written
     return out
 
 
