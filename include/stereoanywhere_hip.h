@@ -414,6 +414,15 @@ typedef struct SaGateEpilogue {
   long add_bs;
   float *out2;
   long out2_bs;
+  /* mode 3 (the flow head's two convs, update.py:98-110, of which the model reads output
+   * channel 0 only, stereoanywhere.py:283): the conv (+ bias + ReLU) is conv1 over h08; head_w
+   * = conv2's channel-0 filter [Cout][3][3] (Cout = the conv's output channels); each block
+   * writes its channel block's partial conv2 sums over its tile plus a one-pixel border to
+   * head_part (floats per image head_part_bs = sa_flow_head_part_size / N), and nothing to out;
+   * sa_flow_head_reduce adds them up. */
+  const float *head_w;
+  float *head_part;
+  long head_part_bs;
 } SaGateEpilogue;
 /* block_shape: 0 / 1 large blocks (8 waves, 64 Winograd tiles, one per CU), 2 small blocks (4
  * waves, 32 tiles, two per CU: shorter launches of few rounds fill the chip better), 3 wide
@@ -432,6 +441,13 @@ int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const S
  * overflow.  Returns the number of such blocks since the last reset (reset != 0 clears it), -1 on
  * error; synchronises the device. */
 long sa_split_redo_blocks(int reset);
+/* The flow head fused (gate mode 3 above): floats of the partial-sum buffer of a conv over
+ * [N, Cout, H, W] (-1 on bad shapes), and the reduction that finishes it: delta = bias0 + the
+ * sum of the partials at each pixel (conv2's channel 0), then as sa_flow_update: coords_x +=
+ * delta, flow_a / flow_b (optional, [N, 2, H, W]) = (coords_x - x, 0). */
+long sa_flow_head_part_size(int N, int Cout, int H, int W);
+int sa_flow_head_reduce(const float *part, int N, int Cout, int H, int W, const float *bias0, float *coords_x,
+                        float *flow_a, long flow_a_bs, float *flow_b, long flow_b_bs, void *stream);
 
 /* Direct KxK convolution (padding K/2, no bias) on fp32 MFMA for the encoder convs the
  * Winograd kernel does not cover (extractor.py:22-40, 91, 208):

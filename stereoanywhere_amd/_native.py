@@ -32,7 +32,8 @@ class SaWinoProblem(ctypes.Structure):
 class SaGateEpilogue(ctypes.Structure):
     """include/stereoanywhere_hip.h: ConvGRU gate epilogue of sa_conv2d_k3_wino4_multi_gate."""
     _fields_ = [("mode", I), ("ctx", P), ("ctx_bs", L), ("h", P), ("h_bs", L), ("z", P), ("z_bs", L),
-                ("add", P), ("add_bs", L), ("out2", P), ("out2_bs", L)]
+                ("add", P), ("add_bs", L), ("out2", P), ("out2_bs", L), ("head_w", P), ("head_part", P),
+                ("head_part_bs", L)]
 
 
 SIGNATURES = {
@@ -62,6 +63,8 @@ SIGNATURES = {
     "sa_softargmin_set_one_pass": (None, [I]),
     "sa_softargmin_get_one_pass": (I, []),
     "sa_split_redo_blocks": (L, [I]),
+    "sa_flow_head_part_size": (L, [I, I, I, I]),
+    "sa_flow_head_reduce": (I, [P, I, I, I, I, P, P, P, L, P, L, P]),
     "sa_softlrc": (I, [P, P, P, P, I, I, I, L, F, P, P, P]),
     "sa_weighted_lsq": (I, [P, P, P, I, I, F, F, P, P, P]),
     "sa_weighted_lsq_ws_size": (L, [I, I]),

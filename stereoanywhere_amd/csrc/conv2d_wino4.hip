@@ -179,6 +179,9 @@ struct W4Gate {
   long add_bs;
   float *out2;
   long out2_bs;
+  const float *head_w;   // mode 3 (w4_flowhead)
+  float *head_part;
+  long head_part_bs;
 };
 struct W4Launch {
   W4Prob p[MAX_PROB];
@@ -486,6 +489,75 @@ __device__ __forceinline__ void w4_emit(const W4Prob &P, const W4Gate *gate, con
     gate_stores(std::integral_constant<int, NCH == 16 ? 4 : CO == 64 ? SA_W4_GJB : SA_W4_GJB1>{},
                 std::integral_constant<int, 1>{});
   else gate_stores(std::integral_constant<int, NCH == 16 ? 4 : SA_W4_GJB>{}, std::integral_constant<int, 2>{});
+  }
+}
+
+
+// Mode 3, the flow head (update.py:98-110): the block's staged outputs are relu(conv1(h08) + b1)
+// of its 32 channels over its BH x BW pixels (ot, [channel][row][col], pitch OPP); conv2's
+// output channel 0 (the only one the model reads, stereoanywhere.py:283) gets from them a partial
+// 3x3 sum over the tile plus its one-pixel border, written to head_part as [N][channel block]
+// [tile][BH + 2][BW + 2]; sa_flow_head_reduce adds the channel blocks and the overlapping borders.
+// f1 (the 256-channel conv1 output) is never written.  Thread item: one interior border-region
+// column c (1..BW) of one channel group (NQ groups: NQ * BW = 512 items), all BH + 2 region rows;
+// the two outer columns (c = 0, BW + 1, one tap column each) are a second, short pass.
+template <class C, int LTW>
+__device__ __forceinline__ void w4_flowhead(const W4Prob &P, const W4Gate &GT, float *smem, const int n, const int co0,
+                                            const int st, const int y0, const int x0, const int tid,
+                                            const float wpre) {
+  constexpr int BW = 4 << LTW, BH = 4 * (C::NT >> LTW), RH = BH + 2, RW = BW + 2, CO = C::CO, OPP = C::OPP;
+  constexpr int NQ = C::NTHR / BW, CPQ = CO / NQ;
+  static_assert(NQ * BW == C::NTHR && CPQ * NQ == CO, "flow head item mapping");
+  static_assert(NQ * RH * RW <= CO * OPP, "partial staging in the output planes");
+  static_assert(CO * OPP + CO * 9 <= C::SMEM, "head weights after the output planes");
+  const float *ot = smem;
+  float *wl = smem + CO * OPP;   // conv2's taps of this block's channels [ch][9]
+  if (tid < CO * 9) wl[tid] = wpre;
+  __syncthreads();
+  const int H = P.H, W = P.W;
+  auto item = [&](const int q, const int c, const int dx0, const int dx1, float *acc) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < RH; ++r) acc[r] = 0.0f;
+    for (int ch = q * CPQ; ch < (q + 1) * CPQ; ++ch) {
+      const float *plane = ot + ch * OPP;
+#pragma unroll
+      for (int dx = dx0; dx <= dx1; ++dx) {
+        const int fc = c + dx - 2;   // f1 column of tap dx for region column c (tile-relative)
+        if (fc < 0 || fc >= BW || x0 + fc >= W) continue;
+        float col[BH];
+#pragma unroll
+        for (int r = 0; r < BH; ++r) col[r] = y0 + r < H ? plane[r * BW + fc] : 0.0f;
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+          const float w = wl[ch * 9 + dy * 3 + dx];
+#pragma unroll
+          for (int r = 0; r < BH; ++r) acc[r - dy + 2] = fmaf(w, col[r], acc[r - dy + 2]);
+        }
+      }
+    }
+  };
+  float acc[RH];
+  const int q = tid / BW, c = 1 + tid % BW;
+  item(q, c, 0, 2, acc);
+  float acc2[RH];
+  const bool edge = tid < 2 * NQ;   // outer columns: c = 0 (tap dx = 2) or BW + 1 (dx = 0)
+  const int eq = tid >> 1, ec = (tid & 1) ? RW - 1 : 0;
+  if (edge) item(eq, ec, (tid & 1) ? 0 : 2, (tid & 1) ? 0 : 2, acc2);
+  __syncthreads();   // every item's reads of the output planes are done: reuse them
+  float *red = smem;   // [NQ][RH][RW]
+#pragma unroll
+  for (int r = 0; r < RH; ++r) red[(q * RH + r) * RW + c] = acc[r];
+  if (edge) {
+#pragma unroll
+    for (int r = 0; r < RH; ++r) red[(eq * RH + r) * RW + ec] = acc2[r];
+  }
+  __syncthreads();
+  float *dst = GT.head_part + (long)n * GT.head_part_bs + ((long)(co0 / CO) * P.tiles_hw + st) * (RH * RW);
+  for (int i = tid; i < RH * RW; i += C::NTHR) {
+    float v = red[i];
+#pragma unroll
+    for (int g = 1; g < NQ; ++g) v += red[g * RH * RW + i];
+    dst[i] = v;
   }
 }
 
@@ -1000,6 +1072,10 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   // banks.
   float *ot = smem;
   const int relu = P.relu;
+  // the flow head's conv2 taps (mode 3), loaded under the output transform
+  float whead = 0.0f;
+  if constexpr (GATED && !QUAD && C::CO == 32 && C::NTHR == 512)
+    if (gate->mode == 3 && tid < C::CO * 9) whead = gate->head_w[co0 * 9 + tid];
   if constexpr (QUAD) {
     // Quadrant (RH, HF) contributes A_RH^T M_q A_HF (at6h along each, over its 3 x 3 points).
     // The four partials of a channel group meet in LDS in a rotation: in phase p quadrant
@@ -1086,6 +1162,12 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][6] = __builtin_amdgcn_s_memtime();
 #endif
   __syncthreads();
+  if constexpr (GATED && !QUAD && C::CO == 32 && C::NTHR == 512) {
+    if (gate->mode == 3) {
+      w4_flowhead<C, LTW>(P, *gate, smem, n, co0, st, y0, x0, tid, whead);
+      return;
+    }
+  }
   w4_emit<C, GATED, C::CO>(P, gate, ot, 0, n, co0, st, tiles_w, y0, x0, BH, BW, ltw + 2, tid);
 }
 
@@ -1269,6 +1351,50 @@ __global__ __launch_bounds__(256) void wino4s_weights_kernel(const float *__rest
 }
 
 // geometry with the fewest padded output pixels (ties: 16 x 64, the smaller halo)
+
+// sa_flow_head_reduce: per pixel, conv2's channel 0 = bias0 + the partial sums of every channel block
+// from the (up to four) tiles whose bordered region holds the pixel, in a fixed order (channel
+// block, then tile row, then tile column); then the coordinates / flow update of sa_flow_update.
+__global__ __launch_bounds__(256) void flow_head_reduce_kernel(const float *__restrict__ part, long part_bs, int ncb,
+                                                               int H, int W, int BH, int BW, int tiles_w,
+                                                               int tiles_hw, const float *__restrict__ bias0,
+                                                               float *__restrict__ cx, float *__restrict__ fa,
+                                                               long fa_bs, float *__restrict__ fb, long fb_bs) {
+  const unsigned r = blockIdx.x * 256u + threadIdx.x;
+  const unsigned hw = (unsigned)(H * W);
+  if (r >= hw) return;
+  const long b = blockIdx.y;
+  const int y = (int)(r / (unsigned)W), x = (int)(r % (unsigned)W);
+  const int RH = BH + 2, RW = BW + 2, tiles_h = tiles_hw / tiles_w;
+  const int ty0 = y / BH, tx0 = x / BW;
+  float d = bias0[0];
+  const float *pb = part + b * part_bs;
+  for (int cb = 0; cb < ncb; ++cb) {
+    const float *pc = pb + (long)cb * tiles_hw * RH * RW;
+    for (int ty = ty0 - 1; ty <= ty0 + 1; ++ty) {
+      const int ry = y - (ty * BH - 1);
+      if (ty < 0 || ty >= tiles_h || ry < 0 || ry >= RH) continue;
+      for (int tx = tx0 - 1; tx <= tx0 + 1; ++tx) {
+        const int rx = x - (tx * BW - 1);
+        if (tx < 0 || tx >= tiles_w || rx < 0 || rx >= RW) continue;
+        d += pc[((long)(ty * tiles_w + tx) * RH + ry) * RW + rx];
+      }
+    }
+  }
+  const long i = b * hw + r;
+  const float c = cx[i] + d;
+  cx[i] = c;
+  const float fx = c - (float)x;
+  if (fa) {
+    fa[b * fa_bs + r] = fx;
+    fa[b * fa_bs + hw + r] = 0.0f;
+  }
+  if (fb) {
+    fb[b * fb_bs + r] = fx;
+    fb[b * fb_bs + hw + r] = 0.0f;
+  }
+}
+
 int w4_ltw(int H, int W) {
   const long a16 = (long)((W + 63) / 64) * 64 * ((H + 15) / 16) * 16;
   const long a32 = (long)((W + 127) / 128) * 128 * ((H + 7) / 8) * 8;
@@ -1306,6 +1432,30 @@ extern "C" int sa_w4_clock_read(unsigned long long *out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4_clock), sizeof(unsigned long long) * 10 * n) == hipSuccess ? 0 : -1;
 }
 #endif
+
+extern "C" long sa_flow_head_part_size(int N, int Cout, int H, int W) {
+  if (N <= 0 || Cout <= 0 || Cout % 32 || H <= 0 || W <= 0) return -1;
+  const int ltw = w4_ltw(H, W), bw = 4 << ltw, bh = 4 * (W4Big::NT >> ltw);
+  const long tiles = (long)((W + bw - 1) / bw) * ((H + bh - 1) / bh);
+  return (long)N * (Cout / 32) * tiles * (bh + 2) * (bw + 2);
+}
+
+extern "C" int sa_flow_head_reduce(const float *part, int N, int Cout, int H, int W, const float *bias0,
+                                   float *coords_x, float *flow_a, long flow_a_bs, float *flow_b, long flow_b_bs,
+                                   void *stream) {
+  SA_REQUIRE(part && bias0 && coords_x, "sa_flow_head_reduce: null pointer");
+  const long per = sa_flow_head_part_size(1, Cout, H, W);
+  SA_REQUIRE(per > 0 && N > 0 && N <= 65535 && (long)H * W < (1L << 31), "sa_flow_head_reduce: bad shape");
+  const int ltw = w4_ltw(H, W), bw = 4 << ltw, bh = 4 * (W4Big::NT >> ltw);
+  const int tiles_w = (W + bw - 1) / bw, tiles_hw = tiles_w * ((H + bh - 1) / bh);
+  const unsigned hw = (unsigned)((long)H * W);
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_PLUMBING, s);
+  flow_head_reduce_kernel<<<dim3((hw + 255) / 256, N), 256, 0, s>>>(part, per, Cout / 32, H, W, bh, bw, tiles_w,
+                                                                     tiles_hw, bias0, coords_x, flow_a, flow_a_bs,
+                                                                     flow_b, flow_b_bs);
+  return sa::check_launch("sa_flow_head_reduce");
+}
 
 long sa_direct_redo_blocks_internal(int reset);   // conv_direct.hip
 
@@ -1381,7 +1531,26 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
     if (gates && gates[i].mode != 0) {
       const SaGateEpilogue &e = gates[i];
       auto a16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-      SA_REQUIRE(e.mode == 1 || e.mode == 2, "sa_conv2d_k3_wino4: gate mode %d", e.mode);
+      SA_REQUIRE(e.mode >= 1 && e.mode <= 3, "sa_conv2d_k3_wino4: gate mode %d", e.mode);
+      if (e.mode == 3) {
+        SA_REQUIRE(e.head_w && e.head_part && !q.stats_partial && !q.pitch && (block_shape == 0 || block_shape == 6),
+                   "sa_conv2d_k3_wino4: the flow-head epilogue needs head_w / head_part, no statistics, dense "
+                   "planes and the 8-wave 32-channel shape (block_shape 0 or 6)");
+        SA_REQUIRE(e.head_part_bs >= sa_flow_head_part_size(1, q.Cout, q.H, q.W),
+                   "sa_conv2d_k3_wino4: head_part_bs too small");
+        L.gate[i] = W4Gate{};
+        L.gate[i].mode = 3;
+        L.gate[i].head_w = e.head_w;
+        L.gate[i].head_part = e.head_part;
+        L.gate[i].head_part_bs = e.head_part_bs;
+        gated = true;
+        const long nb3 = (long)q.N * L.p[i].tiles_hw * L.p[i].co_blocks;
+        total = (i + 1 < nprob ? (total + nb3 + 7) / 8 * 8 : total + nb3);
+        SA_REQUIRE(total < (1L << 31), "sa_conv2d_k3_wino4: grid too large");
+        L.end[i] = (unsigned)total;
+        L.nblk[i] = (unsigned)nb3;
+        continue;
+      }
       SA_REQUIRE(!q.relu && !q.stats_partial, "sa_conv2d_k3_wino4: a gate epilogue takes no ReLU / statistics");
       SA_REQUIRE(e.ctx && e.h && a16(e.ctx) && a16(e.h) && e.ctx_bs % 4 == 0 && e.h_bs % 4 == 0,
                  "sa_conv2d_k3_wino4: gate needs 16-byte aligned ctx and h planes");
@@ -1391,7 +1560,8 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
       else
         SA_REQUIRE(e.z && e.add && a16(e.z) && a16(e.add) && e.z_bs % 4 == 0 && e.add_bs % 4 == 0,
                    "sa_conv2d_k3_wino4: state gate needs aligned z and addend planes");
-      L.gate[i] = W4Gate{e.mode, e.ctx, e.ctx_bs, e.h, e.h_bs, e.z, e.z_bs, e.add, e.add_bs, e.out2, e.out2_bs};
+      L.gate[i] = W4Gate{e.mode, e.ctx, e.ctx_bs, e.h, e.h_bs, e.z, e.z_bs, e.add, e.add_bs, e.out2, e.out2_bs,
+                         nullptr, nullptr, 0};
       gated = true;
     }
     const long nb = (long)q.N * L.p[i].tiles_hw * L.p[i].co_blocks;

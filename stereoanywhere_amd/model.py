@@ -121,6 +121,10 @@ class ScheduleOptions:
     # once).  Replayed from a hipGraph at the bench config: 74.05-74.22 ms/step against
     # 74.38-74.47 without the offset (three alternating pairs, scripts/ab_graph.py 10 2T 2F ...)
     loop_offset: bool = True
+    # the flow head's conv2 (channel 0, the one the model reads) summed in conv1's F(4x4) epilogue
+    # and finished with the coordinate update in one small reduction (ops.flow_head_update); False:
+    # conv1 written out, then conv2d_k3_narrow and flow_update
+    fuse_flow_head: bool = True
 
 
 class StereoAnywhere(nn.Module):
@@ -755,9 +759,14 @@ class StereoAnywhere(nn.Module):
             q_finish(0, "08", xc08, qh[:len(qp)])
             if not last:
                 q_finish(2, "32", xc32, qh[len(qp):])
-            f1 = ops.conv2d_k3(h08, dw["U_fh1"], ub.flow_head.conv1.bias, relu=True)
-            delta = ops.conv2d_k3_narrow(f1, ub.flow_head.conv2.weight, ub.flow_head.conv2.bias)
-            ops.flow_update(coords_x, delta[:, 0:1], flow, None)
+            # flow head + coordinate update (update.py:98-110, stereoanywhere.py:283-285); fused: conv1's
+            # epilogue sums conv2's channel-0 taps, so conv1's 256-channel output is never written
+            if not (o.fuse_flow_head and ops.flow_head_update(h08, dw["U_fh1"], ub.flow_head.conv1.bias,
+                                                              ub.flow_head.conv2.weight, ub.flow_head.conv2.bias,
+                                                              coords_x, flow)):
+                f1 = ops.conv2d_k3(h08, dw["U_fh1"], ub.flow_head.conv1.bias, relu=True)
+                delta = ops.conv2d_k3_narrow(f1, ub.flow_head.conv2.weight, ub.flow_head.conv2.bias)
+                ops.flow_update(coords_x, delta[:, 0:1], flow, None)
             if it == iters - 1:
                 # mask head (update.py:185-191): 3x3 conv + bias + ReLU on the Winograd kernel,
                 # then the 1x1 conv; x 0.25 as the reference scales it

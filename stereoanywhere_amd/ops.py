@@ -959,6 +959,39 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     return [b[1]() for b in built]
 
 
+def flow_head_update(h: torch.Tensor, U1: "WinoFilters", b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
+                     coords_x: torch.Tensor, flow: Optional[torch.Tensor] = None) -> bool:
+    """The flow head (update.py:98-110: conv2(relu(conv1(h)))) fused with the coordinate update
+    (stereoanywhere.py:283-285: coords_x += delta_flow[:, 0]; the model reads conv2's channel 0
+    only): conv1 on the F(4x4,3x3) kernel with its epilogue summing conv2's channel-0 taps over each
+    block's channels (gate mode 3), then sa_flow_head_reduce; conv1's [B, Cout, H, W] output is
+    never written.  flow: the [B, 2, H, W] flow planes to refresh (as flow_update).  Returns False
+    (nothing launched) where the F(4x4) kernel does not take h: the caller then runs
+    conv2d_k3 + conv2d_k3_narrow + flow_update."""
+    B, Cin, H, W = h.shape
+    if not (_WINO4 and _wino4_ok(h) and U1.cout % 32 == 0 and U1.cin == Cin):
+        return False
+    split = W4_SPLIT and U1.u4s is not None
+    per = int(N.lib().sa_flow_head_part_size(1, U1.cout, H, W))
+    part = torch.empty((B * per,), device=h.device, dtype=torch.float32)
+    w2c = w2[0].contiguous()    # conv2's channel-0 filter [Cout][3][3]
+    _check(w2c, "w2")
+    _check(b2, "b2")
+    Uf = U1.u4s if split else U1.u4
+    prob = N.SaWinoProblem(h.data_ptr(), _plane_bs(h, "h"), B, Cin, H, W, Uf.data_ptr(), U1.cout, _ptr(b1), 1,
+                           None, None, None, 0, 0, part.data_ptr(), 0, None, 0)
+    gate = N.SaGateEpilogue(3)
+    gate.head_w, gate.head_part, gate.head_part_bs = w2c.data_ptr(), part.data_ptr(), per
+    _account("conv2d_wino4", 2.0 * 36 * Cin * U1.cout * B * ((H + 3) // 4) * ((W + 3) // 4))
+    N.call("sa_conv2d_k3_wino4_multi_gate", 1, ctypes.addressof(prob), ctypes.addressof(gate), 6 if split else 0,
+           _stream(h))
+    _check(coords_x, "coords_x")
+    N.call("sa_flow_head_reduce", part.data_ptr(), B, U1.cout, H, W, b2.data_ptr(), coords_x.data_ptr(),
+           _ptr(flow), 0 if flow is None else _plane_bs(flow, "flow"), None, 0, _stream(h))
+    _account("gru_plumbing", 4.0 * B * (per + H * W * (2 + (2 if flow is not None else 0))))
+    return True
+
+
 def gate_f4_ok(*xs: torch.Tensor) -> bool:
     """Whether GRU gate epilogues can run on convs of these inputs (F(4x4,3x3) preconditions)."""
     return _WINO4 and all(_wino4_ok(x) for x in xs)

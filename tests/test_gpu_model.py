@@ -226,7 +226,7 @@ def test_loop_parts_match_one_stream(model, parts, offset):
                                     dict(small_launches=frozenset({"q16", "q08", "zr16", "zr08", "pro32"})),
                                     dict(direct_conv=False), dict(wino4=False),
                                     dict(shear_min_bytes=0), dict(sheared_producers=True, shear_min_bytes=0),
-                                    dict(persist=True)])
+                                    dict(persist=True), dict(fuse_flow_head=False)])
 def test_schedule_options_vs_reference(change):
     """Every non-default launch schedule (stereoanywhere_amd.model.ScheduleOptions; ops._WINO4)
     computes the same forward: cfg1 against the reference's disparity."""

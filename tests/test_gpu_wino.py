@@ -591,3 +591,37 @@ def test_wino4_split_range_guard_gate_and_input_transform(monkeypatch):
     assert torch.isfinite(res[True][0]).all() and res[True][1] > 0
     assert float((res[True][0] - ref).abs().max()) / scale < 1e-5
     assert float((res[True][0] - res[False][0]).abs().max()) / scale < 1e-5
+
+
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("B,H,W", [(2, 136, 240), (1, 40, 64), (3, 52, 100), (1, 24, 136)])
+def test_flow_head_fused_matches_separate(monkeypatch, split, B, H, W):
+    """ops.flow_head_update (conv1's F(4x4) epilogue sums conv2's channel-0 taps, gate mode 3, then
+    the reduction + coordinate update) equals conv1 -> conv2d_k3_narrow -> flow_update, on both
+    block geometries (8 x 128 and 16 x 64 pixels) and ragged image edges."""
+    monkeypatch.setattr(ops, "W4_SPLIT", split)
+    g = torch.Generator(device="cpu").manual_seed(B * 1000 + H + W)
+
+    def r(*s):
+        return torch.randn(*s, generator=g).to(dev)
+    h = torch.tanh(r(B, 128, H, W))
+    w1, b1 = r(256, 128, 3, 3) / 34, r(256) * 0.1
+    w2, b2 = r(2, 256, 3, 3) / 48, r(2) * 0.1
+    U1 = ops.wino_weights(w1)
+    cx0 = torch.arange(W, device=dev, dtype=torch.float32).expand(B, 1, H, W).contiguous() - 3.0 * torch.rand(
+        B, 1, H, W, generator=g).to(dev)
+    cx_a, flow_a = cx0.clone(), torch.full((B, 2, H, W), 7.0, device=dev)
+    f1 = ops.conv2d_k3(h, U1, b1, relu=True)
+    delta = ops.conv2d_k3_narrow(f1, w2, b2)
+    ops.flow_update(cx_a, delta[:, 0:1], flow_a, None)
+    cx_b, flow_b = cx0.clone(), torch.full((B, 2, H, W), 7.0, device=dev)
+    assert ops.flow_head_update(h, U1, b1, w2, b2, cx_b, flow_b)
+    ref = F.conv2d(torch.relu(F.conv2d(h.double(), w1.double(), b1.double(), padding=1)), w2.double(),
+                   b2.double(), padding=1)[:, 0:1].float()
+    d_b = cx_b - cx0
+    print(f"flow head fused {B}x{H}x{W} split={split}: max |delta - ref| {float((d_b - ref).abs().max()):.2e}, "
+          f"separate {float((delta[:, 0:1] - ref).abs().max()):.2e}")
+    torch.testing.assert_close(d_b, ref, atol=2e-5, rtol=1e-4)
+    torch.testing.assert_close(cx_b, cx_a, atol=2e-5, rtol=1e-6)
+    torch.testing.assert_close(flow_b, flow_a, atol=2e-5, rtol=1e-5)
+    assert float(flow_b[:, 1].abs().max()) == 0.0
