@@ -397,9 +397,10 @@ def main():
                     help="F(4x4) convs on the split kernel (1) or fp32 MFMA (0); default: ops.W4_SPLIT")
     ap.add_argument("--direct-split", type=int, default=None, choices=[0, 1],
                     help="direct convs on split products (1) or fp32 MFMA (0); default: ops.DIRECT_SPLIT")
-    ap.add_argument("--offload-release", type=int, default=1, choices=[0, 1],
+    ap.add_argument("--offload-release", type=int, default=0, choices=[0, 1],
                     help="cfg5: CPUOffloadWrapper empties the allocator cache after each call (1, the "
-                         "reference's behaviour) or keeps its pools (0)")
+                         "reference's behaviour) or keeps its pools (0, HBM-resident; the other setting is "
+                         "timed beside it)")
     ap.add_argument("--wino4-min-blocks", type=int, default=None,
                     help="F(4x4) for launches of at least this many blocks (default: ops._WINO4_MIN_BLOCKS)")
     args = ap.parse_args()
@@ -513,6 +514,20 @@ def main():
         redo_blocks = int(N.lib().sa_split_redo_blocks(1))
         state_after = box_state(sysd)
         log(f"timed {args.steps} steps in {elapsed:.3f} s")
+        # cfg5: the other CPUOffloadWrapper cache policy over the same steps (the reference empties the
+        # allocator cache after every call, cpu_offload_wrapper.py:82)
+        other_release = None
+        if tiled is not None and tiled["offload"]:
+            runner.release_cache = not runner.release_cache
+            torch.cuda.synchronize()
+            t4 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            other_release = {"release_cache": runner.release_cache,
+                             "ms_per_step": (time.perf_counter() - t4) / args.steps * 1e3}
+            runner.release_cache = not runner.release_cache
+            log(f"release_cache={other_release['release_cache']}: {other_release['ms_per_step']:.1f} ms/step")
         # the same steps launched eagerly (no graph), for the record (or, when the probe chose
         # eager steps, replayed from the graph)
         other = graph_runner if graph_runner is not None else eager_runner
@@ -677,6 +692,8 @@ def main():
     if graph_dev is not None:
         res["graph_vs_eager_max_abs"] = graph_dev
     if tiled is not None:
+        if other_release is not None:
+            res["offload_other_release_cache"] = other_release
         res["tiles_per_s"] = total_units * tiled["tiles"] / elapsed
         res["unique_tile_forwards_per_s"] = total_units * tiled["unique_tiles"] / elapsed
     if not args.no_epe:

@@ -22,6 +22,12 @@ FAMILIES = {
     "lsq_solve_kernel": "weighted_lsq",
     "gru_zr_kernel": "gru_zr", "gru_out_kernel": "gru_out", "convex_up_kernel": "convex_upsample",
     "wino_f2k3_kernel": "conv2d_wino", "wino_f4k3_kernel": "conv2d_wino4", "conv_direct_kernel": "conv2d_direct", "norm_act_kernel": "norm_act", "plane_stats_kernel": "norm_act",
+    # round 4: the families bench.py times separately (were "misc")
+    "pyramid_from_volume_kernel": "mono_pyramid", "pyramid_from_strided_kernel": "mono_pyramid",
+    "pool2x_kernel": "gru_plumbing", "pool2x_v4_kernel": "gru_plumbing", "interp_kernel": "gru_plumbing",
+    "interp_v4_kernel": "gru_plumbing", "flow_update_kernel": "gru_plumbing", "relu_copy_kernel": "gru_plumbing",
+    "flow_head_reduce_kernel": "gru_plumbing",
+    "conv2d_k3_narrow_kernel": "conv2d_narrow", "conv2d_f1_mfma_kernel": "conv2d_small", "conv2d_small_kernel": "conv2d_small",
 }
 
 
