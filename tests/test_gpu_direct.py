@@ -70,8 +70,10 @@ def test_split_weights_beyond_range_keep_fp32(monkeypatch):
     with pytest.raises(RuntimeError):
         ops.conv_direct_weights(w, 2, split=True)
     x = rnd(2, 64, 34, 70, seed=3)
-    (out,) = ops.conv_direct(x, wg_, 3, 2, 96)
+    wd = rnd(96, 64, 1, 1, seed=5) / 8
+    out, ds = ops.conv_direct(x, wg_, 3, 2, 96, wd=ops.conv_direct_weights(wd, 2, with_ds=True, split=False))
     torch.testing.assert_close(out, F.conv2d(x, w, stride=2, padding=1), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(ds, F.conv2d(x, wd, stride=2), atol=1e-4, rtol=1e-4)
 
 
 @pytest.mark.parametrize("K,S", [(7, 1), (3, 2)])
@@ -84,12 +86,14 @@ def test_split_range_guard(monkeypatch, K, S):
     x = rnd(2, Cin, 40, 96, seed=6)
     x[1, :, 3:9, 20:50] *= 1e5
     w = rnd(Cout, Cin, K, K, seed=7) / (K * Cin ** 0.5)
+    wd = rnd(Cout, Cin, 1, 1, seed=8) / Cin ** 0.5 if S == 2 else None   # (the stride-2 kernel fuses a 1x1)
     outs = {}
     for split in (False, True):
         monkeypatch.setattr(ops, "DIRECT_SPLIT", split)
         N.lib().sa_split_redo_blocks(1)
-        (o,) = ops.conv_direct(x, ops.conv_direct_weights(w, S), K, S, Cout)
-        outs[split] = (o, int(N.lib().sa_split_redo_blocks(1)))
+        res = ops.conv_direct(x, ops.conv_direct_weights(w, S), K, S, Cout,
+                              wd=None if wd is None else ops.conv_direct_weights(wd, S, with_ds=True))
+        outs[split] = (res[0], int(N.lib().sa_split_redo_blocks(1)))
     ref = F.conv2d(x.double(), w.double(), stride=S, padding=K // 2).float()
     scale = float(ref.abs().max())
     ys, redo = outs[True]

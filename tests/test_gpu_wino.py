@@ -551,8 +551,11 @@ def test_wino4_split_range_guard(monkeypatch, mag):
 
 def test_wino4_split_range_guard_gate_and_input_transform(monkeypatch):
     """The guard ahead of the epilogues: a mode-2 gate epilogue updating h IN PLACE, and an
-    input-transform launch (the producer's norm on load scaled so the staged values overflow),
-    both equal the fp32-product kernel."""
+    input-transform launch (the producer's norm on load scaled so the staged values overflow):
+    finite, blocks redone, and as close to the float64 result as the fp32-product kernel.  (Winograd
+    rounding scales with the largest value of a tile, so outputs of tiles that mix the scaled values
+    with unit ones err by ~1e-7 of that value in either kernel: the two are compared through their
+    error against float64, not against each other.)"""
     monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
     B, hd, H, W = 2, 32, 16, 64
     g = torch.Generator(device="cpu").manual_seed(7)
@@ -564,6 +567,8 @@ def test_wino4_split_range_guard_gate_and_input_transform(monkeypatch):
     wq = r(hd, hd, 3, 3) / 17
     bq = r(hd)
     ctx, z0, h0, add = r(B, hd, H, W), torch.sigmoid(r(B, hd, H, W)), torch.tanh(r(B, hd, H, W)), r(B, hd, H, W)
+    q = torch.tanh((add.double() + F.conv2d(rh.double(), wq.double(), bq.double(), padding=1)) + ctx.double())
+    h_ref = ((1 - z0.double()) * h0.double() + z0.double() * q).float()
     outs = {}
     for split in (False, True):
         monkeypatch.setattr(ops, "W4_SPLIT", split)
@@ -571,26 +576,28 @@ def test_wino4_split_range_guard_gate_and_input_transform(monkeypatch):
         _redo_blocks()
         _run(monkeypatch, True, dict(x=rh, U=ops.wino_weights(wq), bias=bq, out=h,
                                      gate=dict(mode=2, ctx=ctx, h=h, z=z0, add=add)))
-        outs[split] = (h, _redo_blocks())
+        outs[split] = (h, _redo_blocks(), float((h - h_ref).abs().max()))
+    print("gate mode 2: split err", outs[True][2], "fp32 err", outs[False][2], "redone", outs[True][1])
     assert torch.isfinite(outs[True][0]).all() and outs[True][1] > 0 and outs[False][1] == 0
-    torch.testing.assert_close(outs[True][0], outs[False][0], atol=2e-5, rtol=1e-5)
+    assert outs[True][2] <= 1.5 * outs[False][2] + 1e-5
+    # image 0 has no scaled values: equal to the fp32 kernel at the usual tolerance
+    torch.testing.assert_close(outs[True][0][0], outs[False][0][0], atol=2e-5, rtol=1e-5)
     # input transform: per-channel affine with a large scale on a few channels (norm on load)
     x = r(B, 64, H, W)
     w = r(64, 64, 3, 3) / 24
     s_ = torch.ones(64, device=dev)
     s_[5] = 4000.0
     aff = ops.Affine(s=s_, t=torch.zeros(64, device=dev))
+    ref = F.conv2d(torch.relu(x * s_.view(1, -1, 1, 1)).double(), w.double(), padding=1).float()
     res = {}
     for split in (False, True):
         monkeypatch.setattr(ops, "W4_SPLIT", split)
         _redo_blocks()
         (y,), _ = _run(monkeypatch, True, dict(x=x, U=ops.wino_weights(w), in_aff=aff, in_act="relu"))
-        res[split] = (y, _redo_blocks())
-    ref = F.conv2d(torch.relu(x * s_.view(1, -1, 1, 1)).double(), w.double(), padding=1).float()
-    scale = float(ref.abs().max())
+        res[split] = (y, _redo_blocks(), float((y - ref).abs().max()))
+    print("input transform: split err", res[True][2], "fp32 err", res[False][2], "redone", res[True][1])
     assert torch.isfinite(res[True][0]).all() and res[True][1] > 0
-    assert float((res[True][0] - ref).abs().max()) / scale < 1e-5
-    assert float((res[True][0] - res[False][0]).abs().max()) / scale < 1e-5
+    assert res[True][2] <= 1.5 * res[False][2] + 1e-6 * float(ref.abs().max())
 
 
 @pytest.mark.parametrize("split", [False, True])
