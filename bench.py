@@ -397,6 +397,8 @@ def main():
                     help="F(4x4) convs on the split kernel (1) or fp32 MFMA (0); default: ops.W4_SPLIT")
     ap.add_argument("--direct-split", type=int, default=None, choices=[0, 1],
                     help="direct convs on split products (1) or fp32 MFMA (0); default: ops.DIRECT_SPLIT")
+    ap.add_argument("--opts", default="",
+                    help="ScheduleOptions overrides for A/B runs, e.g. fuse_flow_head=0,loop_parts=1")
     ap.add_argument("--offload-release", type=int, default=0, choices=[0, 1],
                     help="cfg5: CPUOffloadWrapper empties the allocator cache after each call (1, the "
                          "reference's behaviour) or keeps its pools (0, HBM-resident; the other setting is "
@@ -423,6 +425,14 @@ def main():
     model = StereoAnywhere(dict(PUBLISHED)).eval()
     synth.load_seeded_weights(model, 0)
     model = model.to(device)
+    if args.opts:
+        import dataclasses
+        over = {}
+        for kv in args.opts.split(","):
+            k_, v_ = kv.split("=")
+            cur = getattr(model.opts, k_)
+            over[k_] = (v_ not in ("0", "false", "False")) if isinstance(cur, bool) else type(cur)(v_)
+        model.opts = dataclasses.replace(model.opts, **over)
     tiled = TILED.get(args.config)
     if tiled is None:
         iters = args.iters or 22
@@ -687,6 +697,7 @@ def main():
         "execution_probe": probe,
         # split-kernel blocks the f16 range guard recomputed on fp32 MFMA during the timed steps
         "split_redo_blocks": redo_blocks,
+        "schedule_overrides": args.opts or None,
         "box_state": {"before": state_before, "during": sampler.summary(), "after": state_after},
     }
     if graph_dev is not None:

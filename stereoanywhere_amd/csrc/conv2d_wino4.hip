@@ -1367,19 +1367,24 @@ __global__ __launch_bounds__(256) void flow_head_reduce_kernel(const float *__re
   const int y = (int)(r / (unsigned)W), x = (int)(r % (unsigned)W);
   const int RH = BH + 2, RW = BW + 2, tiles_h = tiles_hw / tiles_w;
   const int ty0 = y / BH, tx0 = x / BW;
+  // the tiles whose bordered region holds (y, x): its own, the one above / below when the pixel is
+  // on its tile's first / last row, the one left / right on its first / last column, and the
+  // diagonal one when both; summed in that fixed order per channel block
+  const bool up = y % BH == 0 && ty0 > 0, dn = y % BH == BH - 1 && ty0 + 1 < tiles_h;
+  const bool lf = x % BW == 0 && tx0 > 0, rt = x % BW == BW - 1 && tx0 + 1 < tiles_w;
+  const int ty1 = up ? ty0 - 1 : ty0 + 1, tx1 = lf ? tx0 - 1 : tx0 + 1;
+  auto off = [&](int ty, int tx) { return ((long)(ty * tiles_w + tx) * RH + (y - (ty * BH - 1))) * RW + (x - (tx * BW - 1)); };
+  const bool hy = up || dn, hx = lf || rt;
+  const long o0 = off(ty0, tx0), o1 = hx ? off(ty0, tx1) : 0, o2 = hy ? off(ty1, tx0) : 0,
+             o3 = hx && hy ? off(ty1, tx1) : 0;
   float d = bias0[0];
-  const float *pb = part + b * part_bs;
-  for (int cb = 0; cb < ncb; ++cb) {
-    const float *pc = pb + (long)cb * tiles_hw * RH * RW;
-    for (int ty = ty0 - 1; ty <= ty0 + 1; ++ty) {
-      const int ry = y - (ty * BH - 1);
-      if (ty < 0 || ty >= tiles_h || ry < 0 || ry >= RH) continue;
-      for (int tx = tx0 - 1; tx <= tx0 + 1; ++tx) {
-        const int rx = x - (tx * BW - 1);
-        if (tx < 0 || tx >= tiles_w || rx < 0 || rx >= RW) continue;
-        d += pc[((long)(ty * tiles_w + tx) * RH + ry) * RW + rx];
-      }
-    }
+  const float *pc = part + b * part_bs;
+  const long cbs = (long)tiles_hw * RH * RW;
+  for (int cb = 0; cb < ncb; ++cb, pc += cbs) {
+    d += pc[o0];
+    if (hx) d += pc[o1];
+    if (hy) d += pc[o2];
+    if (hx && hy) d += pc[o3];
   }
   const long i = b * hw + r;
   const float c = cx[i] + d;
