@@ -154,7 +154,11 @@ def lib() -> ctypes.CDLL:
                 "or stereoanywhere_amd._native.build().")
         h = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(h, name)
+            fn = getattr(h, name, None)
+            if fn is None:
+                if os.environ.get("SA_HIP_LIB"):   # an older library of an A/B run: bind what it has
+                    continue
+                raise NativeError(f"{LIB_PATH} does not export {name}")
             fn.restype = res
             fn.argtypes = args
         _lib = h

@@ -221,6 +221,19 @@ __device__ __forceinline__ float w4_unsplit(const float packed) {
   return (float)p[0] + (float)p[1];
 }
 
+// LDS slots for the range guard's per-wave flags (kernels without an input-transform table: the 8-wave
+// shape leaves 2 KiB of LDS spare; with one there is none, and the flags go to the top of the DMA
+// buffers instead, see w4_body)
+template <bool AFF, int NW>
+__device__ __forceinline__ int *w4_flag_slots() {
+  if constexpr (AFF) {
+    return nullptr;
+  } else {
+    __shared__ int slots[NW];
+    return slots;
+  }
+}
+
 // Range guard of the split kernel: blocks whose f16 operands overflowed (|V| >= 65520 turns hi
 // into inf, so every product of that value, and the accumulators it feeds, are NaN) recompute
 // their outputs on fp32 MFMA; this counts them (sa_split_redo_blocks)
@@ -892,26 +905,35 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
       }
     }
   }
-  __syncthreads();
+  if constexpr (!SPLIT) __syncthreads();
   if constexpr (SPLIT) {
     // Range guard: an f16 operand overflow leaves NaN in every accumulator it fed (hi = inf and
     // lo = -inf, or inf * 0), so a non-finite sum of the lane's first-group accumulators (both
     // groups see the same A operands) marks the block, and the whole block (block-uniform: the
     // DMA buffers are shared) recomputes on fp32 MFMA products before its epilogue, so in-place
     // gate epilogues stay correct.  Genuine NaN inputs take the same path and give the fp32
-    // kernel's NaN.  The flags live at the top of the LDS, which neither the epilogue's output
-    // staging (the first CO * OPP floats) nor the redo's single buffer (buffer 0) touches.
-    static_assert(C::SMEM >= C::CO * C::OPP + NWAVE && C::SMEM >= BUF + NWAVE, "range guard flags");
+    // kernel's NaN.  One int per wave, written before the loop-end barrier: a dedicated LDS array,
+    // or with an input transform (no LDS to spare) the (scale, shift) table, which the main loop
+    // reads before each chunk's barrier only and the redo re-reads after this one.
     f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < NR; ++i)
 #pragma unroll
       for (int jj = 0; jj < 3; ++jj) sum += acc[i][jj][0];
     const float tot = (sum.x + sum.y) + (sum.z + sum.w);
-    int *flags = reinterpret_cast<int *>(smem + C::SMEM - NWAVE);
     const bool wbad = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(tot)) != 0;
+    int *flags;
+    if constexpr (AFF) {
+      // the top of the LDS: neither the epilogue's output staging (the first CO * OPP floats) nor the
+      // redo's buffer 0 touches it, but the other waves' last-chunk reads may, so after a barrier
+      static_assert(C::SMEM >= C::CO * C::OPP + NWAVE && C::SMEM >= BUF + NWAVE, "range guard flags");
+      flags = reinterpret_cast<int *>(smem + C::SMEM - NWAVE);
+      __syncthreads();
+    } else {
+      flags = w4_flag_slots<AFF, NWAVE>();
+    }
     if (lane == 0) flags[wv] = wbad ? 1 : 0;
-    __syncthreads();
+    __syncthreads();   // (the main loop's end: every wave's LDS reads and flag are in)
     int any = 0;
 #pragma unroll
     for (int w = 0; w < NWAVE; ++w) any |= flags[w];

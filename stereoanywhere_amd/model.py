@@ -266,7 +266,12 @@ class StereoAnywhere(nn.Module):
         get_corr_block(a.corr_implementation)
         if image2.device.type != "cuda":
             raise RuntimeError("StereoAnywhere (MI355X build) runs on the GPU only; move inputs to cuda")
-        with torch.no_grad():
+        # the few convs left on MIOpen (1x1 output convs, the mask head's 1x1) on deterministic solvers:
+        # at 16 images per launch (configs[3]'s 8 pairs per GPU) the default choice sums in an order
+        # that varies from run to run (5e-5 px), which would break bit-stable reruns and graph replays
+        cd = torch.backends.cudnn
+        with torch.no_grad(), cd.flags(enabled=cd.enabled, benchmark=cd.benchmark, deterministic=True,
+                                       allow_tf32=cd.allow_tf32):
             return self._forward(image2, image3, mde2, mde3, iters)
 
     def _forward(self, image2, image3, mde2, mde3, iters):
