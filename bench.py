@@ -212,6 +212,20 @@ class BoxSampler:
         return res
 
 
+def clock_probe(device):
+    """The in-kernel shader clock under a dense MFMA load (sa_clock_probe: median over waves of
+    delta s_memtime / delta s_memrealtime x 100 MHz; MI355X_MICROARCH.md 'DVFS give-back' 6), which
+    sysfs's pp_dpm_sclk does not show; ~3 ms of work on every CU.  None if unavailable."""
+    import ctypes
+    try:
+        cus = torch.cuda.get_device_properties(device).multi_processor_count
+        mhz, ms = ctypes.c_double(), ctypes.c_double()
+        N.call("sa_clock_probe", 2 * cus, 40000, ctypes.byref(mhz), ctypes.byref(ms))
+        return {"mfma_clock_mhz": mhz.value, "probe_ms": ms.value}
+    except Exception as e:   # (an older library, or no GPU)
+        return {"error": str(e)[:200]}
+
+
 def make_inputs(B, H, W, Hp, Wp, D, seed0, device):
     pb = synth.synthetic_batch(B, H, W, D, seed0=seed0)
     out = {}
@@ -510,7 +524,8 @@ def main():
         # timed region: K plain steps -> value.  The per-launch HIP events of the roofline
         # serialise every launch (~6 % of a step), so they run over K more steps right after.
         sysd = _gpu_sysfs(device)
-        state_before = box_state(sysd)
+        state_before = box_state(sysd) or {}
+        state_before.update(clock_probe(device))
         N.lib().sa_split_redo_blocks(1)   # (synchronises; outside the timed region)
         D.barrier(r)
         torch.cuda.synchronize()
@@ -522,7 +537,8 @@ def main():
             D.barrier(r)
             elapsed = time.perf_counter() - t0
         redo_blocks = int(N.lib().sa_split_redo_blocks(1))
-        state_after = box_state(sysd)
+        state_after = box_state(sysd) or {}
+        state_after.update(clock_probe(device))
         log(f"timed {args.steps} steps in {elapsed:.3f} s")
         # cfg5: the other CPUOffloadWrapper cache policy over the same steps (the reference empties the
         # allocator cache after every call, cpu_offload_wrapper.py:82)

@@ -497,6 +497,10 @@ enum {
   SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_NORM, SA_K_CONV2D, SA_K_CONV_DIRECT,
   SA_K_CONV2D_W4, SA_K_SHEAR, SA_K_MONO_PYRAMID, SA_K_PLUMBING, SA_K_CONV_SMALL, SA_K_NARROW, SA_K_COUNT
 };
+/* Box-state probe (bench.py, outside timed regions; synchronises the device): `blocks` blocks of 4
+ * waves run `iters` x 4 chained f16 MFMAs each; *mhz = the median over waves of the in-kernel shader
+ * clock (delta s_memtime / delta s_memrealtime x 100 MHz), *ms = the kernel's event time. */
+int sa_clock_probe(int blocks, int iters, double *mhz, double *ms);
 int sa_timing_enable(int on);
 int sa_timing_read(int kernel_id, double *total_ms, long *count);
 const char *sa_kernel_name(int kernel_id);

@@ -64,6 +64,7 @@ SIGNATURES = {
     "sa_softargmin_get_one_pass": (I, []),
     "sa_split_redo_blocks": (L, [I]),
     "sa_flow_head_part_size": (L, [I, I, I, I]),
+    "sa_clock_probe": (I, [I, I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "sa_flow_head_reduce": (I, [P, I, I, I, I, P, P, P, L, P, L, P]),
     "sa_softlrc": (I, [P, P, P, P, I, I, I, L, F, P, P, P]),
     "sa_weighted_lsq": (I, [P, P, P, I, I, F, F, P, P, P]),

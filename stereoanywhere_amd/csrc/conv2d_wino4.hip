@@ -59,6 +59,10 @@
 #ifndef SA_W4_PRIO
 #define SA_W4_PRIO 1   // s_setprio 1 for the point-half-1 waves (split kernel forward: 66.8 -> 66.5 ms/step, wino4 49.8 -> 49.0 ms, two interleaved passes)
 #endif
+#ifndef SA_W4_GUARD
+#define SA_W4_GUARD 2  // split kernel range guard: 2 detect + redo on fp32 MFMA; 1 detect and count only
+                       // (A/B timing); 0 none
+#endif
 #ifndef SA_W4_PF
 #define SA_W4_PF 1     // persistent kernel: prefetch the next item's chunk 0 (0: each item issues its own)
 #endif
@@ -905,8 +909,8 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
       }
     }
   }
-  if constexpr (!SPLIT) __syncthreads();
-  if constexpr (SPLIT) {
+  if constexpr (!SPLIT || !SA_W4_GUARD) __syncthreads();
+  if constexpr (SPLIT && SA_W4_GUARD) {
     // Range guard: an f16 operand overflow leaves NaN in every accumulator it fed (hi = inf and
     // lo = -inf, or inf * 0), so a non-finite sum of the lane's first-group accumulators (both
     // groups see the same A operands) marks the block, and the whole block (block-uniform: the
@@ -937,7 +941,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
     int any = 0;
 #pragma unroll
     for (int w = 0; w < NWAVE; ++w) any |= flags[w];
-    if (any) {
+    if (SA_W4_GUARD >= 2 && any) {
       if (tid == 0) atomicAdd(&g_w4_redo_blocks, 1u);
 #pragma unroll
       for (int i = 0; i < NR; ++i)
