@@ -920,10 +920,17 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
     // or with an input transform (no LDS to spare) the (scale, shift) table, which the main loop
     // reads before each chunk's barrier only and the redo re-reads after this one.
     f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+#ifndef SA_W4_GSUM
+#define SA_W4_GSUM 0   // which accumulators the guard sums (A/B of the register assignment it leads to)
+#endif
 #pragma unroll
     for (int i = 0; i < NR; ++i)
 #pragma unroll
-      for (int jj = 0; jj < 3; ++jj) sum += acc[i][jj][0];
+      for (int jj = 0; jj < 3; ++jj) {
+        if (SA_W4_GSUM == 0) sum += acc[i][jj][0];
+        else if (SA_W4_GSUM == 1) sum += acc[i][jj][1];
+        else sum += acc[NR - 1 - i][2 - jj][0];
+      }
     const float tot = (sum.x + sum.y) + (sum.z + sum.w);
     const bool wbad = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(tot)) != 0;
     int *flags;
