@@ -435,11 +435,17 @@ typedef struct SaGateEpilogue {
  * sa_conv2d_wino4_weights_split; the transformed inputs must stay below 65504 in magnitude). */
 int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                                   int block_shape, void *stream);
-/* Range guard of the split kernels (the F(4x4) kernel's f16 hi/lo products, block_shape 6, and
- * sa_conv_direct_split): a block whose f16 operands overflowed (|transformed input| >= 65520)
- * recomputes its outputs on fp32 MFMA products inside the same launch, so results never carry the
- * overflow.  Returns the number of such blocks since the last reset (reset != 0 clears it), -1 on
- * error; synchronises the device. */
+/* sa_conv2d_k3_wino4_multi_gate with the split kernel's range guard (block_shape 6): a block whose
+ * f16 operands overflowed (|transformed input| >= 65520) writes nothing and queues itself in
+ * redo_ws ([0] = count, then one entry per queued block; zero-initialised, redo_cap >= the launch's
+ * blocks, left zeroed again), and a one-workgroup kernel launched right after on the same stream
+ * recomputes those blocks on fp32 MFMA products (the split filters read as hi + lo), so results
+ * never carry the overflow.  redo_ws NULL: no guard.  Other block shapes ignore redo_ws. */
+int sa_conv2d_k3_wino4_launch(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
+                              int block_shape, unsigned *redo_ws, long redo_cap, void *stream);
+/* Blocks of the split kernels (F(4x4) and sa_conv_direct_split) that the range guards recomputed on
+ * fp32 MFMA since the last reset (reset != 0 clears the count), -1 on error; synchronises the
+ * device. */
 long sa_split_redo_blocks(int reset);
 /* The flow head fused (gate mode 3 above): floats of the partial-sum buffer of a conv over
  * [N, Cout, H, W] (-1 on bad shapes), and the reduction that finishes it: delta = bias0 + the

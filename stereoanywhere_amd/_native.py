@@ -63,6 +63,7 @@ SIGNATURES = {
     "sa_softargmin_set_one_pass": (None, [I]),
     "sa_softargmin_get_one_pass": (I, []),
     "sa_split_redo_blocks": (L, [I]),
+    "sa_conv2d_k3_wino4_launch": (I, [I, P, P, I, P, L, P]),
     "sa_flow_head_part_size": (L, [I, I, I, I]),
     "sa_clock_probe": (I, [I, I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "sa_flow_head_reduce": (I, [P, I, I, I, I, P, P, P, L, P, L, P]),

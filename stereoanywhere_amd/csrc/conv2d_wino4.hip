@@ -59,10 +59,6 @@
 #ifndef SA_W4_PRIO
 #define SA_W4_PRIO 1   // s_setprio 1 for the point-half-1 waves (split kernel forward: 66.8 -> 66.5 ms/step, wino4 49.8 -> 49.0 ms, two interleaved passes)
 #endif
-#ifndef SA_W4_GUARD
-#define SA_W4_GUARD 2  // split kernel range guard: 2 detect + redo on fp32 MFMA; 1 detect and count only
-                       // (A/B timing); 0 none
-#endif
 #ifndef SA_W4_PF
 #define SA_W4_PF 1     // persistent kernel: prefetch the next item's chunk 0 (0: each item issues its own)
 #endif
@@ -82,8 +78,11 @@ constexpr int NPT = 36;                   // transform points
 // 4-channel chunks, 66 KiB, two blocks per CU, so one block's first DMA wait and epilogue
 // overlap the other's MFMAs (per block ~6-8k cycles until the first chunk lands and ~9k of
 // epilogue around 6.8k per chunk, scripts/w4_clock.py); it is not faster in the forward.
-template <int NW_, int KC_, int CO_ = 32, bool QUAD_ = false, bool SPLIT_ = false>
+template <int NW_, int KC_, int CO_ = 32, bool QUAD_ = false, bool SPLIT_ = false, bool UNSPLIT_ = false>
 struct W4Cfg {
+  // UNSPLIT: fp32 MFMA products with the split kernel's (hi, lo) filter dwords read as hi + lo (the
+  // range guard's redo kernel, wino_f4k3_redo_kernel)
+  static constexpr bool UNSPLIT = UNSPLIT_;
   // QUAD: the waves of a tile group split the 6 x 6 points in quadrants (rows 0-2 / 3-5 x
   // columns 0-2 / 3-5) instead of column halves
   static constexpr bool QUAD = QUAD_;
@@ -147,6 +146,7 @@ static_assert(!W4S_K32 || W4S_KC == 8, "the K = 32 split form takes a lane's two
 // accumulation order.  |V| must stay below 65504 (the f16 range): V = B^T d B grows at most
 // 100-fold over the input patch.
 using W4Split = W4Cfg<8, W4S_KC, 32, false, true>;
+using W4SplitRedo = W4Cfg<8, W4S_KC, 32, false, false, true>;
 constexpr int W4S_LOG2 = 12;
 static_assert(2 * W4Small::SMEM * 4 <= 160 * 1024, "two small blocks per CU");
 static_assert(W4Wide::SMEM * 4 <= 160 * 1024, "one wide block per CU");
@@ -193,6 +193,10 @@ struct W4Launch {
   unsigned end[MAX_PROB];
   unsigned nblk[MAX_PROB];
   int nprob;
+  // the split kernel's range guard: [0] = count, [1 ..] = (problem << 27 | work item) of the blocks
+  // that skipped their epilogue; redo_cap entries (wino_f4k3_redo_kernel)
+  unsigned *redo;
+  unsigned redo_cap;
 };
 
 // x as the f16 A operand (hi, hi, lo, lo): hi = f16(x), lo = f16(x - hi) (x - hi is exact in
@@ -225,22 +229,9 @@ __device__ __forceinline__ float w4_unsplit(const float packed) {
   return (float)p[0] + (float)p[1];
 }
 
-// LDS slots for the range guard's per-wave flags (kernels without an input-transform table: the 8-wave
-// shape leaves 2 KiB of LDS spare; with one there is none, and the flags go to the top of the DMA
-// buffers instead, see w4_body)
-template <bool AFF, int NW>
-__device__ __forceinline__ int *w4_flag_slots() {
-  if constexpr (AFF) {
-    return nullptr;
-  } else {
-    __shared__ int slots[NW];
-    return slots;
-  }
-}
-
 // Range guard of the split kernel: blocks whose f16 operands overflowed (|V| >= 65520 turns hi
-// into inf, so every product of that value, and the accumulators it feeds, are NaN) recompute
-// their outputs on fp32 MFMA; this counts them (sa_split_redo_blocks)
+// into inf, so every product of that value, and the outputs it feeds, are NaN) skip their epilogue
+// and are recomputed on fp32 MFMA by wino_f4k3_redo_kernel; this counts them (sa_split_redo_blocks)
 __device__ unsigned g_w4_redo_blocks;
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, float *lds, int voff, int soff) {
@@ -593,7 +584,8 @@ template <class C, int HF, int LTW, bool GATED, bool AFF, int RH = 0, bool PERSI
 __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, const unsigned wid, float *smem,
                                         float2 *atab, const int par = 0, const bool pre = false,
                                         const bool has_next = false, const W4Prob &NP = W4Prob{},
-                                        const unsigned nwid = 0) {
+                                        const unsigned nwid = 0, unsigned *redo = nullptr,
+                                        const unsigned redo_cap = 0, const unsigned redo_tag = 0) {
   constexpr int NWAVE = C::NW, NTHR = C::NTHR, KC = C::KC, JPC = C::JPC, NT = C::NT, PDMA = C::PDMA,
                 UDMA = C::UDMA, UPW = C::UPW, UBUF = C::UBUF, BUF = C::BUF, PBUF = C::PBUF, OPP = C::OPP,
                 CO = C::CO, CG = C::CG, SB = C::SB, NR = C::NR;
@@ -892,7 +884,8 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
           for (int i = 0; i < NR; ++i)
 #pragma unroll
             for (int g = 0; g < CG; ++g)
-              acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], bc[i][g], acc[i][jj][g], 0, 0, 0);
+              acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], C::UNSPLIT ? w4_unsplit(bc[i][g]) : bc[i][g],
+                                                                    acc[i][jj][g], 0, 0, 0);
         }
 #if SA_W4_FENCE
         __builtin_amdgcn_sched_barrier(0);   // bound the scheduler's hoisting (register pressure)
@@ -909,107 +902,11 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
       }
     }
   }
-  if constexpr (!SPLIT || !SA_W4_GUARD) __syncthreads();
-  if constexpr (SPLIT && SA_W4_GUARD) {
-    // Range guard: an f16 operand overflow leaves NaN in every accumulator it fed (hi = inf and
-    // lo = -inf, or inf * 0), so a non-finite sum of the lane's first-group accumulators (both
-    // groups see the same A operands) marks the block, and the whole block (block-uniform: the
-    // DMA buffers are shared) recomputes on fp32 MFMA products before its epilogue, so in-place
-    // gate epilogues stay correct.  Genuine NaN inputs take the same path and give the fp32
-    // kernel's NaN.  One int per wave, written before the loop-end barrier: a dedicated LDS array,
-    // or with an input transform (no LDS to spare) the (scale, shift) table, which the main loop
-    // reads before each chunk's barrier only and the redo re-reads after this one.
-    f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-#ifndef SA_W4_GSUM
-#define SA_W4_GSUM 0   // which accumulators the guard sums (A/B of the register assignment it leads to)
-#endif
-#pragma unroll
-    for (int i = 0; i < NR; ++i)
-#pragma unroll
-      for (int jj = 0; jj < 3; ++jj) {
-        if (SA_W4_GSUM == 0) sum += acc[i][jj][0];
-        else if (SA_W4_GSUM == 1) sum += acc[i][jj][1];
-        else sum += acc[NR - 1 - i][2 - jj][0];
-      }
-    const float tot = (sum.x + sum.y) + (sum.z + sum.w);
-    const bool wbad = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(tot)) != 0;
-    int *flags;
-    if constexpr (AFF) {
-      // the top of the LDS: neither the epilogue's output staging (the first CO * OPP floats) nor the
-      // redo's buffer 0 touches it, but the other waves' last-chunk reads may, so after a barrier
-      static_assert(C::SMEM >= C::CO * C::OPP + NWAVE && C::SMEM >= BUF + NWAVE, "range guard flags");
-      flags = reinterpret_cast<int *>(smem + C::SMEM - NWAVE);
-      __syncthreads();
-    } else {
-      flags = w4_flag_slots<AFF, NWAVE>();
-    }
-    if (lane == 0) flags[wv] = wbad ? 1 : 0;
-    __syncthreads();   // (the main loop's end: every wave's LDS reads and flag are in)
-    int any = 0;
-#pragma unroll
-    for (int w = 0; w < NWAVE; ++w) any |= flags[w];
-    if (SA_W4_GUARD >= 2 && any) {
-      if (tid == 0) atomicAdd(&g_w4_redo_blocks, 1u);
-#pragma unroll
-      for (int i = 0; i < NR; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 3; ++jj)
-#pragma unroll
-          for (int g = 0; g < CG; ++g) acc[i][jj][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // a plain loop (one buffer, no prefetch, rolled): the path is rare, and a second copy of
-      // the pipelined main loop raised its register pressure
-#pragma unroll 1
-      for (int kc = 0; kc < nchunks; ++kc) {
-        issue(kc, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if constexpr (AFF) {
-#pragma unroll
-          for (int j = 0; j < PDMA; ++j) {
-            if (pc[j] >= 0) {
-              f32x4 *q = reinterpret_cast<f32x4 *>(smem + ((wv + NWAVE * j) * 64 + lane) * 4);
-              const float2 ab = atab[kc * KC + pc[j]];
-              f32x4 v = *q;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] * ab.x + ab.y, act_floor);
-              *q = v;
-            }
-          }
-        }
-        __syncthreads();
-        const float *pb = smem + pread;
-        const float *ub = smem + PBUF + uread;
-#pragma unroll 1
-        for (int s = 0; s < JPC; ++s) {
-          const float *p = pb + s * 4 * PSv * 4;
-          float t[6][3];
-#pragma unroll
-          for (int r = 0; r < 6; ++r) {
-            const f32x2 ra = *reinterpret_cast<const f32x2 *>(p + r * PGv * 4);
-            const f32x4 rb = *reinterpret_cast<const f32x4 *>(p + r * PGv * 4 + 2);
-            const f32x2 rc = *reinterpret_cast<const f32x2 *>(p + r * PGv * 4 + 6);
-            bt6h<HF>(ra.y, rb.x, rb.y, rb.z, rb.w, rc.x, t[r]);
-          }
-#pragma unroll
-          for (int jj = 0; jj < 3; ++jj) {
-            float v[6];
-            bt6(t[0][jj], t[1][jj], t[2][jj], t[3][jj], t[4][jj], t[5][jj], v);
-#pragma unroll
-            for (int i = 0; i < NR; ++i) {
-              const f32xg b = *reinterpret_cast<const f32xg *>(ub + ((6 * i + 3 * HF + jj) * JPC + s) * SB);
-#pragma unroll
-              for (int g = 0; g < CG; ++g)
-                acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], w4_unsplit(b[g]), acc[i][jj][g], 0, 0, 0);
-            }
-          }
-        }
-        __syncthreads();
-      }
-    }
-  }
+  __syncthreads();
 #ifdef SA_W4_CLOCK
   if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][5] = __builtin_amdgcn_s_memtime();
 #endif
-  if constexpr (SPLIT) {   // the filters' 2^W4S_LOG2 (exact)
+  if constexpr (SPLIT || C::UNSPLIT) {   // the filters' 2^W4S_LOG2 (exact)
 #pragma unroll
     for (int i = 0; i < NR; ++i)
 #pragma unroll
@@ -1105,6 +1002,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   // banks.
   float *ot = smem;
   const int relu = P.relu;
+  f32x4 chk = f32x4{0.f, 0.f, 0.f, 0.f};   // the split kernel's range guard (below)
   // the flow head's conv2 taps (mode 3), loaded under the output transform
   float whead = 0.0f;
   if constexpr (GATED && !QUAD && C::CO == 32 && C::NTHR == 512)
@@ -1182,6 +1080,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
         } else {
           // half 1's partial + half 0's: (p1 + p0) + bias for either finishing half
           f32x4 v = (HF == 0 ? (*o + y) : (y + *o)) + bv;
+          if constexpr (SPLIT) chk += v;   // (the range guard, before the ReLU that would mask a NaN)
           if (relu) v = f32x4{fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f)};
           *o = v;
         }
@@ -1194,7 +1093,32 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
 #ifdef SA_W4_CLOCK
   if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][6] = __builtin_amdgcn_s_memtime();
 #endif
-  __syncthreads();
+  if constexpr (SPLIT) {
+    // Range guard: an f16 operand overflow (|V| >= 65520: hi = inf, lo = -inf) makes every product
+    // of that value NaN, and so the staged outputs it feeds (checked before the ReLU).  Such a
+    // block writes nothing (its epilogue may update h in place) and queues itself for
+    // wino_f4k3_redo_kernel, which recomputes it on fp32 MFMA products right after this launch.
+    // Genuine NaN inputs take the same path and give the fp32 kernel's NaN.  One int per wave past
+    // the output planes and the flow head's taps (nothing else uses that LDS after the main loop).
+    static_assert(C::CO * C::OPP + C::CO * 9 + NWAVE <= C::SMEM, "range guard flags");
+    int *flags = reinterpret_cast<int *>(smem + C::CO * C::OPP + C::CO * 9);
+    const float t = (chk.x + chk.y) + (chk.z + chk.w);
+    const bool wbad = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(t)) != 0;
+    if (lane == 0) flags[wv] = wbad ? 1 : 0;
+    __syncthreads();
+    int any = 0;
+#pragma unroll
+    for (int w = 0; w < NWAVE; ++w) any |= flags[w];
+    if (any) {
+      if (tid == 0 && redo) {
+        const unsigned slot = atomicAdd(redo, 1u);
+        if (slot < redo_cap) redo[1 + slot] = redo_tag;
+      }
+      return;
+    }
+  } else {
+    __syncthreads();
+  }
   if constexpr (GATED && !QUAD && C::CO == 32 && C::NTHR == 512) {
     if (gate->mode == 3) {
       w4_flowhead<C, LTW>(P, *gate, smem, n, co0, st, y0, x0, tid, whead);
@@ -1237,12 +1161,18 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 || C::CO == 64 ? 1 : 2) void wi
     else if (qd == 2) SA_W4_Q(0, 1);
     else SA_W4_Q(1, 1);
 #undef SA_W4_Q
-  } else if (threadIdx.x < C::NTHR / 2) {
-    if (P.ltw == 4) w4_body<C, 0, 4, GATED, AFF>(P, GATED ? &L.gate[pi] : nullptr, wid, smem, atab);
-    else w4_body<C, 0, 5, GATED, AFF>(P, GATED ? &L.gate[pi] : nullptr, wid, smem, atab);
   } else {
-    if (P.ltw == 4) w4_body<C, 1, 4, GATED, AFF>(P, GATED ? &L.gate[pi] : nullptr, wid, smem, atab);
-    else w4_body<C, 1, 5, GATED, AFF>(P, GATED ? &L.gate[pi] : nullptr, wid, smem, atab);
+    const unsigned tag = ((unsigned)pi << 27) | wid;
+#define SA_W4_B(HF_, LTW_) \
+  w4_body<C, HF_, LTW_, GATED, AFF>(P, gp, wid, smem, atab, 0, false, false, W4Prob{}, 0, L.redo, L.redo_cap, tag)
+    if (threadIdx.x < C::NTHR / 2) {
+      if (P.ltw == 4) SA_W4_B(0, 4);
+      else SA_W4_B(0, 5);
+    } else {
+      if (P.ltw == 4) SA_W4_B(1, 4);
+      else SA_W4_B(1, 5);
+    }
+#undef SA_W4_B
   }
 #ifdef SA_W4_CLOCK
   if (threadIdx.x == 0 && g < 65536) {
@@ -1259,6 +1189,42 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 || C::CO == 64 ? 1 : 2) void wi
 // XCD the one-shot grid would put it on, and the L2-locality remap is unchanged).  Each item
 // issues the next item's chunk 0 as its main loop ends (w4_issue_chunk0), so the first-chunk
 // wait of every item but the block's first is hidden under the previous item's epilogue.
+// The split kernel's range guard, finished: one workgroup recomputes, on fp32 MFMA products (the
+// split filters read as hi + lo), every block the preceding split launch queued in L.redo (the list
+// holds every block of the launch), then clears the count.  Launched after every guarded split
+// launch on its stream; with nothing queued it reads one word and exits.
+template <bool GATED, bool AFF>
+__global__ __launch_bounds__(W4SplitRedo::NTHR, 1) void wino_f4k3_redo_kernel(const W4Launch L) {
+  using C = W4SplitRedo;
+  __shared__ __attribute__((aligned(16))) float smem[C::SMEM];
+  __shared__ float2 atab[AFF ? C::AFF_MAX : 1];
+  const unsigned n = __atomic_load_n(L.redo, __ATOMIC_RELAXED);
+  if (n == 0) return;
+  const unsigned total = n < L.redo_cap ? n : L.redo_cap;
+  unsigned done = 0;
+  for (unsigned i = 0; i < total; ++i) {
+    const unsigned tag = L.redo[1 + i];
+    const int pi = (int)(tag >> 27);
+    const unsigned wid = tag & ((1u << 27) - 1u);
+    const W4Prob &P = L.p[pi];
+    const W4Gate *gp = GATED ? &L.gate[pi] : nullptr;
+    __syncthreads();   // the previous block's LDS use is over
+    if (threadIdx.x < C::NTHR / 2) {
+      if (P.ltw == 4) w4_body<C, 0, 4, GATED, AFF>(P, gp, wid, smem, atab);
+      else w4_body<C, 0, 5, GATED, AFF>(P, gp, wid, smem, atab);
+    } else {
+      if (P.ltw == 4) w4_body<C, 1, 4, GATED, AFF>(P, gp, wid, smem, atab);
+      else w4_body<C, 1, 5, GATED, AFF>(P, gp, wid, smem, atab);
+    }
+    ++done;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(&g_w4_redo_blocks, done);
+    __atomic_store_n(L.redo, 0u, __ATOMIC_RELAXED);
+  }
+}
+
 template <class C, bool GATED, bool AFF = false>
 __global__ __launch_bounds__(C::NTHR, 1) void wino_f4k3_persist_kernel(const W4Launch L) {
   static_assert(C::NW == 8 && C::CO == 32 && !C::QUAD, "persistent: the 8-wave 32-channel shape");
@@ -1523,6 +1489,11 @@ extern "C" int sa_conv2d_k3_wino4_multi(int nprob, const SaWinoProblem *probs, v
 
 extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                                              int block_shape, void *stream) {
+  return sa_conv2d_k3_wino4_launch(nprob, probs, gates, block_shape, nullptr, 0, stream);
+}
+
+extern "C" int sa_conv2d_k3_wino4_launch(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
+                                         int block_shape, unsigned *redo_ws, long redo_cap, void *stream) {
   SA_REQUIRE(nprob >= 1 && nprob <= MAX_PROB && probs, "sa_conv2d_k3_wino4_multi: 1..%d problems", MAX_PROB);
   SA_REQUIRE(block_shape >= 0 && block_shape <= 6, "sa_conv2d_k3_wino4_multi: block_shape 0..6");
   // Large blocks unless the caller asks for small ones (block_shape 2) or wide ones (3: 64
@@ -1614,6 +1585,15 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
   }
   L.nprob = nprob;
   SA_REQUIRE(!(aff && gated), "sa_conv2d_k3_wino4: an input transform and a gate epilogue in one launch");
+  // the split kernel's range guard: blocks whose operands overflowed queue themselves in redo_ws and
+  // the redo kernel recomputes them on fp32 products (the list holds every block of the launch)
+  const bool guard = split && redo_ws;
+  if (guard) {
+    SA_REQUIRE(redo_cap >= total && (reinterpret_cast<uintptr_t>(redo_ws) & 3) == 0,
+               "sa_conv2d_k3_wino4: the redo workspace holds %ld entries, the launch has %ld blocks", redo_cap, total);
+    L.redo = redo_ws;
+    L.redo_cap = (unsigned)redo_cap;
+  }
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV2D_W4, s);
   if (persist) {
@@ -1626,10 +1606,15 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
     aff     ? wino_f4k3_persist_kernel<W4Big, false, true><<<grid, W4Big::NTHR, 0, s>>>(L)
     : gated ? wino_f4k3_persist_kernel<W4Big, true><<<grid, W4Big::NTHR, 0, s>>>(L)
             : wino_f4k3_persist_kernel<W4Big, false><<<grid, W4Big::NTHR, 0, s>>>(L);
-  } else if (split)
+  } else if (split) {
     aff     ? wino_f4k3_kernel<W4Split, false, true><<<(unsigned)total, W4Split::NTHR, 0, s>>>(L)
     : gated ? wino_f4k3_kernel<W4Split, true><<<(unsigned)total, W4Split::NTHR, 0, s>>>(L)
             : wino_f4k3_kernel<W4Split, false><<<(unsigned)total, W4Split::NTHR, 0, s>>>(L);
+    if (guard)
+      aff     ? wino_f4k3_redo_kernel<false, true><<<1, W4SplitRedo::NTHR, 0, s>>>(L)
+      : gated ? wino_f4k3_redo_kernel<true, false><<<1, W4SplitRedo::NTHR, 0, s>>>(L)
+              : wino_f4k3_redo_kernel<false, false><<<1, W4SplitRedo::NTHR, 0, s>>>(L);
+  }
   else if (quad)
     aff     ? wino_f4k3_kernel<W4Quad, false, true><<<(unsigned)total, W4Quad::NTHR, 0, s>>>(L)
     : gated ? wino_f4k3_kernel<W4Quad, true><<<(unsigned)total, W4Quad::NTHR, 0, s>>>(L)

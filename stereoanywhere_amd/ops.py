@@ -904,6 +904,36 @@ def _gate_epilogue(p: dict) -> "N.SaGateEpilogue":
     return e
 
 
+# the split kernel's range-guard workspaces ([0] = count, then one entry per block of a launch), one per
+# HIP stream (launches on one stream run in order, and the guard's redo kernel leaves the count
+# zeroed), grown by replacement; superseded buffers stay referenced, since a captured hipGraph may
+# still name them
+_REDO_WS: dict = {}
+_REDO_OLD: list = []
+
+
+def _redo_workspace(x: torch.Tensor, blocks: int) -> torch.Tensor:
+    st = torch.cuda.current_stream(x.device)
+    key = (x.device.index, st.cuda_stream)
+    ws = _REDO_WS.get(key)
+    if ws is None or ws.numel() < 1 + blocks:
+        if ws is not None:
+            _REDO_OLD.append(ws)
+        ws = torch.zeros((1 + max(blocks, 1 << 15),), device=x.device, dtype=torch.int32)
+        _REDO_WS[key] = ws
+    return ws
+
+
+def _wino4_launch(n: int, arr, gates, shape: int, x: torch.Tensor, blocks: int) -> None:
+    """sa_conv2d_k3_wino4_launch; the split shape (6) with its range-guard workspace."""
+    if shape == 6:
+        ws = _redo_workspace(x, blocks)
+        N.call("sa_conv2d_k3_wino4_launch", n, ctypes.addressof(arr), ctypes.addressof(gates), shape, ws.data_ptr(),
+               ws.numel() - 1, _stream(x))
+    else:
+        N.call("sa_conv2d_k3_wino4_multi_gate", n, ctypes.addressof(arr), ctypes.addressof(gates), shape, _stream(x))
+
+
 def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     """Independent conv2d_k3 calls (each a dict of conv2d_k3's keyword arguments) in ONE launch:
     their blocks share the grid, so each conv's partly filled last round of blocks is filled by
@@ -951,8 +981,8 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
         gates = (N.SaGateEpilogue * len(built))(*[_gate_epilogue(p) if p.get("gate") else N.SaGateEpilogue()
                                                   for p in problems])
         shape = (4 if W4_QUAD else 3) if wide else 2 if small_blocks else 5 if persist else 6 if split else 0
-        N.call("sa_conv2d_k3_wino4_multi_gate", len(built), ctypes.addressof(arr), ctypes.addressof(gates),
-               shape, _stream(problems[0]["x"]))
+        _wino4_launch(len(built), arr, gates, shape, problems[0]["x"],
+                      sum(_wino4_blocks(**p) + 8 for p in plain))
     else:
         N.call("sa_conv2d_k3_wino4_multi" if f4 else "sa_conv2d_k3_wino_multi", len(built), ctypes.addressof(arr),
                _stream(problems[0]["x"]))
@@ -983,8 +1013,7 @@ def flow_head_update(h: torch.Tensor, U1: "WinoFilters", b1: torch.Tensor, w2: t
     gate = N.SaGateEpilogue(3)
     gate.head_w, gate.head_part, gate.head_part_bs = w2c.data_ptr(), part.data_ptr(), per
     _account("conv2d_wino4", 2.0 * 36 * Cin * U1.cout * B * ((H + 3) // 4) * ((W + 3) // 4))
-    N.call("sa_conv2d_k3_wino4_multi_gate", 1, ctypes.addressof(prob), ctypes.addressof(gate), 6 if split else 0,
-           _stream(h))
+    _wino4_launch(1, prob, gate, 6 if split else 0, h, _wino4_blocks(h, U1))
     _check(coords_x, "coords_x")
     N.call("sa_flow_head_reduce", part.data_ptr(), B, U1.cout, H, W, b2.data_ptr(), coords_x.data_ptr(),
            _ptr(flow), 0 if flow is None else _plane_bs(flow, "flow"), None, 0, _stream(h))
