@@ -411,6 +411,8 @@ def main():
                     help="F(4x4) convs on the split kernel (1) or fp32 MFMA (0); default: ops.W4_SPLIT")
     ap.add_argument("--direct-split", type=int, default=None, choices=[0, 1],
                     help="direct convs on split products (1) or fp32 MFMA (0); default: ops.DIRECT_SPLIT")
+    ap.add_argument("--split-guard", type=int, default=None, choices=[0, 1],
+                    help="the split kernel's f16 range guard (default ops.SPLIT_GUARD; 0 for A/B timing only)")
     ap.add_argument("--opts", default="",
                     help="ScheduleOptions overrides for A/B runs, e.g. fuse_flow_head=0,loop_parts=1")
     ap.add_argument("--offload-release", type=int, default=0, choices=[0, 1],
@@ -420,6 +422,8 @@ def main():
     ap.add_argument("--wino4-min-blocks", type=int, default=None,
                     help="F(4x4) for launches of at least this many blocks (default: ops._WINO4_MIN_BLOCKS)")
     args = ap.parse_args()
+    if args.split_guard is not None:
+        ops.SPLIT_GUARD = bool(args.split_guard)
     if args.batch is None:
         args.batch = 8 if args.config == "cfg4" else 4
     if args.wino4_min_blocks is not None:
@@ -713,6 +717,7 @@ def main():
         "execution_probe": probe,
         # split-kernel blocks the f16 range guard recomputed on fp32 MFMA during the timed steps
         "split_redo_blocks": redo_blocks,
+        "split_guard": bool(ops.SPLIT_GUARD),
         "schedule_overrides": args.opts or None,
         "box_state": {"before": state_before, "during": sampler.summary(), "after": state_after},
     }

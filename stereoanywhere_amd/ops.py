@@ -924,9 +924,13 @@ def _redo_workspace(x: torch.Tensor, blocks: int) -> torch.Tensor:
     return ws
 
 
+# the split kernel's f16 range guard (False: no workspace, no redo launch: A/B timing only)
+SPLIT_GUARD = True
+
+
 def _wino4_launch(n: int, arr, gates, shape: int, x: torch.Tensor, blocks: int) -> None:
     """sa_conv2d_k3_wino4_launch; the split shape (6) with its range-guard workspace."""
-    if shape == 6:
+    if shape == 6 and SPLIT_GUARD:
         ws = _redo_workspace(x, blocks)
         N.call("sa_conv2d_k3_wino4_launch", n, ctypes.addressof(arr), ctypes.addressof(gates), shape, ws.data_ptr(),
                ws.numel() - 1, _stream(x))
