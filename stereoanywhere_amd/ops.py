@@ -930,7 +930,8 @@ SPLIT_GUARD = True
 
 def _wino4_launch(n: int, arr, gates, shape: int, x: torch.Tensor, blocks: int) -> None:
     """sa_conv2d_k3_wino4_launch; the split shape (6) with its range-guard workspace."""
-    if shape == 6 and SPLIT_GUARD:
+    # (an A/B run's older library, SA_HIP_LIB, may predate the guard's entry point)
+    if shape == 6 and SPLIT_GUARD and hasattr(N.lib(), "sa_conv2d_k3_wino4_launch"):
         ws = _redo_workspace(x, blocks)
         N.call("sa_conv2d_k3_wino4_launch", n, ctypes.addressof(arr), ctypes.addressof(gates), shape, ws.data_ptr(),
                ws.numel() - 1, _stream(x))
