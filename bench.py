@@ -434,8 +434,11 @@ def main():
         ops.DIRECT_SPLIT = bool(args.direct_split)
 
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
-    r = D.init_from_env("nccl")
-    device = torch.device("cuda", r.local_rank)
+    # SA_DIST_BACKEND=gloo (and SA_DIST_SHARE_GPU=1): a multi-rank rehearsal of this code path on a
+    # single-GPU box (ranks share the GPU; the throughput is then meaningless)
+    r = D.init_from_env(os.environ.get("SA_DIST_BACKEND", "nccl"))
+    ngpu = torch.cuda.device_count()
+    device = torch.device("cuda", r.local_rank % ngpu if os.environ.get("SA_DIST_SHARE_GPU") == "1" else r.local_rank)
     torch.cuda.set_device(device)
     if r.world != args.gpus and r.is_main:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {r.world}", file=sys.stderr)

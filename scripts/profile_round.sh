@@ -16,5 +16,7 @@ exec_steps=(
   "trace1s:300:cd /tmp && rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof/trace1s -o run --output-format csv -- $SHORT --one-stream"
   "fetch:300:cd /tmp && rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/prof/fetch -o run --output-format csv -- $SHORT --one-stream"
   "write:300:cd /tmp && rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/prof/write -o run --output-format csv -- $SHORT --one-stream"
+  "trace5:400:cd /tmp && rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof/trace5 -o run --output-format csv -- python3 $R/bench.py --config cfg5 --steps 1 --warmup 1 --no-cpu-baseline --no-epe --one-stream"
+  "dist2:300:cd $R && SA_DIST_BACKEND=gloo SA_DIST_SHARE_GPU=1 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --config cfg4 --steps 2 --warmup 1 --no-epe > $R/gpurun_out/prof/dist2.log 2>&1"
 )
 bash "$R/scripts/gpu_steps.sh" "${exec_steps[@]}"
