@@ -24,8 +24,34 @@ def timeit(fn, reps=20):
     return a.elapsed_time(b) * 1000 / reps
 
 
+def plumbing(d):
+    """pool2x / interp of the update loop at configs[1]'s maps (B 4, level 08 136x240) and the
+    booster tiles' (B 25 tiles, 224x280): achieved GB/s of the planes read + written."""
+    g = torch.Generator(device="cpu").manual_seed(0)
+    for B, H, W in ((4, 136, 240), (25, 224, 280)):
+        h08, x16 = torch.randn(B, 128, H, W, generator=g).to(d), torch.empty(B, 256, H // 2, W // 2, device=d)
+        h16, x08 = torch.randn(B, 128, H // 2, W // 2, generator=g).to(d), torch.empty(B, 256, H, W, device=d)
+        h32, x32 = torch.empty(B, 128, H // 4, W // 4, device=d), torch.empty(B, 256, H // 4, W // 4, device=d)
+        for name, fn, nbytes in (
+                ("pool2x 08->16", lambda: ops.pool2x(h08, x16[:, :128]), (h08.numel() * 1.25) * 4),
+                ("pool2x 16->32", lambda: ops.pool2x(h16, x32[:, :128]), (h16.numel() * 1.25) * 4),
+                ("interp 16->08", lambda: ops.interp(h16, x08[:, 128:]), (h16.numel() * 5) * 4),
+                ("interp 32->16", lambda: ops.interp(h32, x16[:, 128:]), (h32.numel() * 5) * 4)):
+            t = timeit(fn)
+            print(f"B{B} {H}x{W} {name}: {t:8.1f} us  {nbytes / t / 1e3:7.0f} GB/s")
+        dst = x08[:, 128:]
+        t = timeit(lambda: dst.fill_(1.0))
+        print(f"B{B} fill of the interp 16->08 destination: {t:8.1f} us  {dst.numel() * 4 / t / 1e3:7.0f} GB/s")
+        t = timeit(lambda: dst.copy_(h08))
+        print(f"B{B} copy h08 -> that destination: {t:8.1f} us  {dst.numel() * 8 / t / 1e3:7.0f} GB/s")
+        t = timeit(lambda: torch.nn.functional.interpolate(h16, (H, W), mode="bilinear", align_corners=True))
+        print(f"B{B} torch interpolate 16->08: {t:8.1f} us")
+
+
 def main():
     d = torch.device("cuda", 0)
+    if "--plumbing" in sys.argv:
+        return plumbing(d)
     B, H, W = 4, 136, 240
     g = torch.Generator(device="cpu").manual_seed(0)
 

@@ -104,101 +104,120 @@ __global__ __launch_bounds__(256) void gru_out_kernel(const float *__restrict__ 
   stv<VEC>(h + b * h_bs + r, hv);
 }
 
-// F.avg_pool2d(x, 3, stride=2, padding=1), count_include_pad=True -> always / 9.
-// grid: x over output columns (64 per block), y over output rows (4 per block), z = (b, c)
-// (in_p / out_p: row pitches of the planes, >= W / Wo: columns beyond the width are not read
-// or written)
-__global__ __launch_bounds__(256) void pool2x_kernel(const float *__restrict__ in, long in_bs, int C, int H,
-                                                     int W, int Ho, int Wo, float *__restrict__ out, long out_bs,
-                                                     int in_p, int out_p) {
-  const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (x >= Wo || y >= Ho) return;
-  const int b = blockIdx.z / C, c = blockIdx.z % C;
-  const float *p = in + b * in_bs + (long)c * H * in_p;
-  float s = 0.f;
-  for (int dy = -1; dy <= 1; ++dy) {
-    const int yy = 2 * y + dy;
-    if (yy < 0 || yy >= H) continue;
-    for (int dx = -1; dx <= 1; ++dx) {
-      const int xx = 2 * x + dx;
-      if (xx < 0 || xx >= W) continue;
-      s += p[yy * in_p + xx];
-    }
+// pool2x / interp: grid y = one (image, channel) plane, grid x over a flat index of the
+// plane's output vectors (VEC consecutive outputs of one row, one VEC-wide store), FLAT_K
+// vectors per lane 256 apart (coalesced): every lane has work whatever the row width, and
+// the plane base is uniform (scalar) with 32-bit in-plane offsets.  The row of a vector is
+// umulhi(index, magic) (exact: index * nv < 2^32, checked on the host).  (The round-3
+// kernels mapped 64 lanes to a row segment and 4 rows to a workgroup: at the tiled configs'
+// widths, 70 / 140 / 280, up to half the lanes idled, at 1-1.5 TB/s.)
+constexpr int FLAT_K = 4;
+
+struct FlatGeo {
+  long in_bs, out_bs;
+  int C, H, W, Ho, Wo, in_p, out_p;
+  unsigned nv, per, magic;  // vectors per row and per plane; ceil(2^32 / nv)
+};
+
+__device__ __forceinline__ void flat_row(const FlatGeo &g, unsigned i, unsigned &y, unsigned &xv) {
+  y = g.nv == 1 ? i : __umulhi(i, g.magic);
+  xv = i - y * g.nv;
+}
+
+template <int VEC>
+__device__ __forceinline__ void st_vec(float *p, const float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    *reinterpret_cast<float4 *>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  } else if constexpr (VEC == 2) {
+    *reinterpret_cast<float2 *>(p) = make_float2(v[0], v[1]);
+  } else {
+    *p = v[0];
   }
-  out[b * out_bs + (long)c * Ho * out_p + y * out_p + x] = s / 9.0f;
 }
 
-// F.interpolate(bilinear, align_corners=True) (upsample_bilinear2d arithmetic); grid as pool2x
-__global__ __launch_bounds__(256) void interp_kernel(const float *__restrict__ in, long in_bs, int C, int H,
-                                                     int W, int Ho, int Wo, float sh, float sw,
-                                                     float *__restrict__ out, long out_bs, int in_p, int out_p) {
-  const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (x >= Wo || y >= Ho) return;
-  const int b = blockIdx.z / C, c = blockIdx.z % C;
-  const float *p = in + b * in_bs + (long)c * H * in_p;
-  const float ry = sh * (float)y, rx = sw * (float)x;
-  const int y0 = (int)ry, x0 = (int)rx;
-  const int yp = y0 < H - 1 ? 1 : 0, xp = x0 < W - 1 ? 1 : 0;
-  const float ly1 = ry - (float)y0, ly0 = 1.0f - ly1;
-  const float lx1 = rx - (float)x0, lx0 = 1.0f - lx1;
-  const float *r0 = p + y0 * in_p, *r1 = p + (y0 + yp) * in_p;
-  const float v = ly0 * (lx0 * r0[x0] + lx1 * r0[x0 + xp]) + ly1 * (lx0 * r1[x0] + lx1 * r1[x0 + xp]);
-  out[b * out_bs + (long)c * Ho * out_p + y * out_p + x] = v;
-}
-
-// interp_kernel with 4 consecutive outputs per thread and one float4 store (Wo % 4 == 0,
-// 16-byte aligned output planes: the update block's maps); per-output arithmetic identical
-// to interp_kernel. grid: x over quads of output columns (64 per block), y over rows (4)
-__global__ __launch_bounds__(256) void interp_v4_kernel(const float *__restrict__ in, long in_bs, int C, int H,
-                                                        int W, int Ho, int Wo, float sh, float sw,
-                                                        float *__restrict__ out, long out_bs, int in_p) {
-  const int xq = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (4 * xq >= Wo || y >= Ho) return;
-  const int b = blockIdx.z / C, c = blockIdx.z % C;
-  const float *p = in + b * in_bs + (long)c * H * in_p;
-  const float ry = sh * (float)y;
-  const int y0 = (int)ry;
-  const int yp = y0 < H - 1 ? 1 : 0;
-  const float ly1 = ry - (float)y0, ly0 = 1.0f - ly1;
-  const float *r0 = p + y0 * in_p, *r1 = p + (y0 + yp) * in_p;
-  float v[4];
+// F.avg_pool2d(x, 3, stride=2, padding=1), count_include_pad=True -> always / 9; each window
+// row summed as (left + centre) + right (an absent column adds an exact 0), rows in order.
+// VLOAD (W == 2 Wo, in_p % 4 == 0, 16-byte aligned planes): the window columns of a vector's
+// outputs, 2 VEC x0 - 1 .. 2 VEC x0 + 2 VEC - 1, as one scalar and VEC / 2 float4 loads per row.
+template <int VEC, bool VLOAD>
+__global__ __launch_bounds__(256) void pool2x_flat_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                          FlatGeo g) {
+  const unsigned b = blockIdx.y / (unsigned)g.C, c = blockIdx.y - b * (unsigned)g.C;
+  const float *p = in + b * g.in_bs + (long)c * g.H * g.in_p;
+  float *o = out + b * g.out_bs + (long)c * g.Ho * g.out_p;
+  const unsigned base = blockIdx.x * (256u * FLAT_K) + threadIdx.x;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float rx = sw * (float)(4 * xq + j);
-    const int x0 = (int)rx;
-    const int xp = x0 < W - 1 ? 1 : 0;
-    const float lx1 = rx - (float)x0, lx0 = 1.0f - lx1;
-    v[j] = ly0 * (lx0 * r0[x0] + lx1 * r0[x0 + xp]) + ly1 * (lx0 * r1[x0] + lx1 * r1[x0 + xp]);
+  for (int k = 0; k < FLAT_K; ++k) {
+    const unsigned i = base + k * 256u;
+    if (i >= g.per) return;
+    unsigned y, xv;
+    flat_row(g, i, y, xv);
+    const int x0 = 2 * VEC * (int)xv;
+    float s[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) s[j] = 0.f;
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int yy = 2 * (int)y + dy;
+      if (yy < 0 || yy >= g.H) continue;
+      const float *r = p + yy * g.in_p;
+      if constexpr (VLOAD && VEC >= 2) {
+        float w[2 * VEC + 1];
+        w[0] = x0 > 0 ? r[x0 - 1] : 0.0f;
+#pragma unroll
+        for (int q = 0; q < VEC / 2; ++q) {
+          const float4 t = *reinterpret_cast<const float4 *>(r + x0 + 4 * q);
+          w[1 + 4 * q] = t.x; w[2 + 4 * q] = t.y; w[3 + 4 * q] = t.z; w[4 + 4 * q] = t.w;
+        }
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) s[j] += (w[2 * j] + w[2 * j + 1]) + w[2 * j + 2];
+      } else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const int xx = x0 + 2 * j;
+          const float l = xx > 0 ? r[xx - 1] : 0.0f;
+          const float rt = xx + 1 < g.W ? r[xx + 1] : 0.0f;
+          s[j] += (l + r[xx]) + rt;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) s[j] = s[j] / 9.0f;
+    st_vec<VEC>(o + y * g.out_p + VEC * xv, s);
   }
-  *reinterpret_cast<float4 *>(out + b * out_bs + (long)c * Ho * Wo + y * Wo + 4 * xq) =
-      make_float4(v[0], v[1], v[2], v[3]);
 }
 
-// pool2x with 4 consecutive outputs per thread and one float4 store (W % 8 == 0, 16-byte
-// aligned planes: the update block's maps): the window columns of outputs 4q .. 4q + 3 are
-// 8q - 1 .. 8q + 7, one scalar and two float4 loads per input row instead of 12 scalar loads.
-__global__ __launch_bounds__(256) void pool2x_v4_kernel(const float *__restrict__ in, long in_bs, int C, int H, int W,
-                                                        int Ho, int Wo, float *__restrict__ out, long out_bs) {
-  const int xq = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (4 * xq >= Wo || y >= Ho) return;
-  const int b = blockIdx.z / C, c = blockIdx.z % C;
-  const float *p = in + b * in_bs + (long)c * H * W;
-  const int x0 = 8 * xq;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  for (int dy = -1; dy <= 1; ++dy) {
-    const int yy = 2 * y + dy;
-    if (yy < 0 || yy >= H) continue;
-    const float *r = p + yy * W;
-    const float4 a = *reinterpret_cast<const float4 *>(r + x0);   // x0 + 3 < W: Wo = W / 2
-    const float4 e = x0 + 4 < W ? *reinterpret_cast<const float4 *>(r + x0 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float m = x0 > 0 ? r[x0 - 1] : 0.0f;
-    s0 += (m + a.x) + a.y;
-    s1 += (a.y + a.z) + a.w;
-    s2 += (a.w + e.x) + e.y;
-    s3 += (e.y + e.z) + e.w;
+// F.interpolate(bilinear, align_corners=True) with upsample_bilinear2d's arithmetic:
+// source coordinate scale * dst, floor, the +1 neighbour clamped at the last row / column,
+// lambda weights, (lx0 * a + lx1 * b) per row, then the row blend.
+template <int VEC>
+__global__ __launch_bounds__(256) void interp_flat_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                          FlatGeo g, float sh, float sw) {
+  const unsigned b = blockIdx.y / (unsigned)g.C, c = blockIdx.y - b * (unsigned)g.C;
+  const float *p = in + b * g.in_bs + (long)c * g.H * g.in_p;
+  float *o = out + b * g.out_bs + (long)c * g.Ho * g.out_p;
+  const unsigned base = blockIdx.x * (256u * FLAT_K) + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < FLAT_K; ++k) {
+    const unsigned i = base + k * 256u;
+    if (i >= g.per) return;
+    unsigned y, xv;
+    flat_row(g, i, y, xv);
+    const float ry = sh * (float)y;
+    const int y0 = (int)ry;
+    const int yp = y0 < g.H - 1 ? 1 : 0;
+    const float ly1 = ry - (float)y0, ly0 = 1.0f - ly1;
+    const float *r0 = p + y0 * g.in_p, *r1 = p + (y0 + yp) * g.in_p;
+    float v[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float rx = sw * (float)(VEC * (int)xv + j);
+      const int x0 = (int)rx;
+      const int xp = x0 < g.W - 1 ? 1 : 0;
+      const float lx1 = rx - (float)x0, lx0 = 1.0f - lx1;
+      v[j] = ly0 * (lx0 * r0[x0] + lx1 * r0[x0 + xp]) + ly1 * (lx0 * r1[x0] + lx1 * r1[x0 + xp]);
+    }
+    st_vec<VEC>(o + y * g.out_p + VEC * xv, v);
   }
-  *reinterpret_cast<float4 *>(out + b * out_bs + (long)c * Ho * Wo + y * Wo + 4 * xq) =
-      make_float4(s0 / 9.0f, s1 / 9.0f, s2 / 9.0f, s3 / 9.0f);
 }
 
 __global__ __launch_bounds__(256) void relu_copy_kernel(const float *__restrict__ in, long in_bs, unsigned per,
@@ -285,22 +304,55 @@ extern "C" int sa_gru_out(const float *xc, long xc_bs, const float *bx, const fl
   return sa_gru_out_split(xc, xc_bs, bx, qh, nullptr, qh_bs, cq, c_bs, z, B, C, HW, h, h_bs, stream);
 }
 
+// the widest store the output rows allow (Wo, the row pitch, the batch stride and the base
+// all multiples of VEC floats)
+static int flat_vec(const float *out, int Wo, int out_p, long out_bs) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(out);
+  if (Wo % 4 == 0 && out_p % 4 == 0 && out_bs % 4 == 0 && (a & 15) == 0) return 4;
+  if (Wo % 2 == 0 && out_p % 2 == 0 && out_bs % 2 == 0 && (a & 7) == 0) return 2;
+  return 1;
+}
+
+static FlatGeo flat_geo(long in_bs, int in_p, int C, int H, int W, int Ho, int Wo, long out_bs, int out_p, int vec) {
+  FlatGeo g{in_bs, out_bs, C, H, W, Ho, Wo, in_p, out_p, 0u, 0u, 0u};
+  g.nv = (unsigned)(Wo / vec);
+  g.per = (unsigned)Ho * g.nv;
+  g.magic = g.nv > 1 ? (unsigned)(((1UL << 32) + g.nv - 1) / g.nv) : 0u;  // nv == 1: flat_row skips it
+  return g;
+}
+
+// umulhi(i, ceil(2^32 / nv)) == i / nv for i < per when per * nv < 2^32 (the rounding error
+// of the magic, < nv / 2^32 per unit of i, stays below 1 / nv)
+static bool flat_ok(const FlatGeo &g) { return (unsigned long)g.per * g.nv < (1UL << 32); }
+
+static dim3 flat_grid(const FlatGeo &g, int B) {
+  return dim3((g.per + 256u * FLAT_K - 1) / (256u * FLAT_K), (unsigned)(B * g.C));
+}
+
 extern "C" int sa_pool2x_p(const float *in, long in_bs, int in_pitch, int B, int C, int H, int W, float *out,
                            long out_bs, int out_pitch, void *stream) {
   SA_REQUIRE(in && out, "sa_pool2x: null pointer");
   SA_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0 && (long)B * C <= 65535, "sa_pool2x: bad shape");
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   SA_REQUIRE(in_pitch >= W && out_pitch >= Wo, "sa_pool2x: row pitch below the width");
-  SA_REQUIRE((long)H * in_pitch < (1L << 31), "sa_pool2x: plane too large");
+  SA_REQUIRE((long)H * in_pitch < (1L << 31) && (long)Ho * out_pitch < (1L << 31), "sa_pool2x: plane too large");
+  const int vec = flat_vec(out, Wo, out_pitch, out_bs);
+  // vector loads: W == 2 Wo (the window of the last vector ends at column W - 1), float4-aligned rows
+  const bool vload = vec >= 2 && W == 2 * Wo && in_pitch % 4 == 0 && in_bs % 4 == 0 && al16(in);
+  const FlatGeo g = flat_geo(in_bs, in_pitch, C, H, W, Ho, Wo, out_bs, out_pitch, vec);
+  SA_REQUIRE(flat_ok(g), "sa_pool2x: output plane shape unsupported (plane too large)");
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_PLUMBING, s);
-  if (in_pitch == W && out_pitch == Wo && W % 8 == 0 && Wo % 4 == 0 && al16(in) && al16(out) && in_bs % 4 == 0 &&
-      out_bs % 4 == 0)
-    pool2x_v4_kernel<<<dim3((Wo / 4 + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, out,
-                                                                                   out_bs);
+  if (vec == 4 && vload)
+    pool2x_flat_kernel<4, true><<<flat_grid(g, B), 256, 0, s>>>(in, out, g);
+  else if (vec == 4)
+    pool2x_flat_kernel<4, false><<<flat_grid(g, B), 256, 0, s>>>(in, out, g);
+  else if (vec == 2 && vload)
+    pool2x_flat_kernel<2, true><<<flat_grid(g, B), 256, 0, s>>>(in, out, g);
+  else if (vec == 2)
+    pool2x_flat_kernel<2, false><<<flat_grid(g, B), 256, 0, s>>>(in, out, g);
   else
-    pool2x_kernel<<<dim3((Wo + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, out, out_bs,
-                                                                            in_pitch, out_pitch);
+    pool2x_flat_kernel<1, false><<<flat_grid(g, B), 256, 0, s>>>(in, out, g);
   return sa::check_launch("sa_pool2x");
 }
 
@@ -317,17 +369,21 @@ extern "C" int sa_interp_bilinear_ac_p(const float *in, long in_bs, int in_pitch
   SA_REQUIRE(in_pitch >= W && out_pitch >= Wo, "sa_interp_bilinear_ac: row pitch below the width");
   SA_REQUIRE((long)H * in_pitch < (1L << 31) && (long)Ho * out_pitch < (1L << 31),
              "sa_interp_bilinear_ac: plane too large");
+
   // area_pixel_compute_scale(align_corners=True): (in - 1) / (out - 1), 0 for out == 1
   const float sh = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.0f;
   const float sw = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.0f;
+  const int vec = flat_vec(out, Wo, out_pitch, out_bs);
+  const FlatGeo g = flat_geo(in_bs, in_pitch, C, H, W, Ho, Wo, out_bs, out_pitch, vec);
+  SA_REQUIRE(flat_ok(g), "sa_interp_bilinear_ac: output plane shape unsupported (plane too large)");
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_PLUMBING, s);
-  if (out_pitch == Wo && Wo % 4 == 0 && al16(out) && out_bs % 4 == 0)
-    interp_v4_kernel<<<dim3((Wo / 4 + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, sh, sw,
-                                                                                   out, out_bs, in_pitch);
+  if (vec == 4)
+    interp_flat_kernel<4><<<flat_grid(g, B), 256, 0, s>>>(in, out, g, sh, sw);
+  else if (vec == 2)
+    interp_flat_kernel<2><<<flat_grid(g, B), 256, 0, s>>>(in, out, g, sh, sw);
   else
-    interp_kernel<<<dim3((Wo + 63) / 64, (Ho + 3) / 4, B * C), 256, 0, s>>>(in, in_bs, C, H, W, Ho, Wo, sh, sw, out,
-                                                                            out_bs, in_pitch, out_pitch);
+    interp_flat_kernel<1><<<flat_grid(g, B), 256, 0, s>>>(in, out, g, sh, sw);
   return sa::check_launch("sa_interp_bilinear_ac");
 }
 

@@ -438,8 +438,11 @@ def test_gru_gates_and_plumbing(H, W):
     ops.interp(y, odd)
     torch.testing.assert_close(odd, torch.nn.functional.interpolate(y, (9, 13), mode="bilinear",
                                                                     align_corners=True), atol=1e-6, rtol=0)
-    # the update block's map sizes (pool2x: the 4-wide float4 variant, W % 8 == 0)
-    for (hi, wi), (ho, wo) in (((136, 240), (68, 120)), ((68, 120), (34, 60))):
+    # the update block's map sizes: configs[1]'s (4-wide stores, float4 window loads), the tiled
+    # configs' (Wo = 140: 4-wide; 70: 2-wide stores with float4 window loads) and odd widths
+    # (W = 2 Wo - 1: scalar window loads; Wo = 35: 1-wide stores)
+    for (hi, wi), (ho, wo) in (((136, 240), (68, 120)), ((68, 120), (34, 60)), ((224, 280), (112, 140)),
+                               ((112, 140), (56, 70)), ((57, 71), (29, 36)), ((29, 69), (15, 35))):
         xs = g(rng.standard_normal((B, C, hi, wi)))
         pooled = torch.zeros(B, 2 * C, ho, wo, device=dev)
         ops.pool2x(xs, pooled[:, C:])
