@@ -186,6 +186,22 @@ int sa_pool2x_p(const float *in, long in_bs, int in_pitch, int B, int C, int H, 
                 long out_bs, int out_pitch, void *stream);
 int sa_interp_bilinear_ac_p(const float *in, long in_bs, int in_pitch, int B, int C, int H, int W,
                             int Ho, int Wo, float *out, long out_bs, int out_pitch, void *stream);
+/* Up to 4 independent pool2x / interp jobs (the pitched forms above) in ONE launch: the update
+ * loop's plumbing between two conv launches (update.py:124-132: pool2x(net[0]) and
+ * interp(net[2]) feed gru16; interp(net[1]) feeds gru08 and pool2x(net[1]) gru32).  pool2x:
+ * (Ho, Wo) must be ((H-1)/2+1, (W-1)/2+1).  Same results as the one-job entry points. */
+enum { SA_RESAMPLE_POOL2X = 0, SA_RESAMPLE_BILINEAR_AC = 1 };
+typedef struct SaResampleJob {
+  int kind;
+  const float *in;
+  long in_bs;
+  int in_pitch;
+  int B, C, H, W, Ho, Wo;
+  float *out;
+  long out_bs;
+  int out_pitch;
+} SaResampleJob;
+int sa_resample_multi(int njobs, const SaResampleJob *jobs, void *stream);
 int sa_relu_copy(const float *in, long in_bs, int B, int C, int HW, float *out, long out_bs,
                  void *stream);
 int sa_flow_update(float *coords_x, const float *delta, long delta_bs, int B, int H, int W,

@@ -39,6 +39,12 @@ def plumbing(d):
                 ("interp 32->16", lambda: ops.interp(h32, x16[:, 128:]), (h32.numel() * 5) * 4)):
             t = timeit(fn)
             print(f"B{B} {H}x{W} {name}: {t:8.1f} us  {nbytes / t / 1e3:7.0f} GB/s")
+        t = timeit(lambda: ops.resample_multi(("pool", h08, x16[:, :128], None, None),
+                                              ("interp", h32, x16[:, 128:], None, None)))
+        print(f"B{B} {H}x{W} multi pool 08->16 + interp 32->16: {t:8.1f} us")
+        t = timeit(lambda: ops.resample_multi(("interp", h16, x08[:, 128:], None, None),
+                                              ("pool", h16, x32[:, :128], None, None)))
+        print(f"B{B} {H}x{W} multi interp 16->08 + pool 16->32: {t:8.1f} us")
         dst = x08[:, 128:]
         t = timeit(lambda: dst.fill_(1.0))
         print(f"B{B} fill of the interp 16->08 destination: {t:8.1f} us  {dst.numel() * 4 / t / 1e3:7.0f} GB/s")

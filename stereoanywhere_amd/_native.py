@@ -36,6 +36,12 @@ class SaGateEpilogue(ctypes.Structure):
                 ("head_part_bs", L)]
 
 
+class SaResampleJob(ctypes.Structure):
+    """include/stereoanywhere_hip.h: one pool2x / interp job of sa_resample_multi."""
+    _fields_ = [("kind", I), ("in_", P), ("in_bs", L), ("in_pitch", I), ("B", I), ("C", I), ("H", I), ("W", I),
+                ("Ho", I), ("Wo", I), ("out", P), ("out_bs", L), ("out_pitch", I)]
+
+
 SIGNATURES = {
     "sa_abi_version": (I, []),
     "sa_last_error": (ctypes.c_char_p, []),
@@ -79,6 +85,7 @@ SIGNATURES = {
     "sa_interp_bilinear_ac": (I, [P, L, I, I, I, I, I, I, P, L, P]),
     "sa_pool2x_p": (I, [P, L, I, I, I, I, I, P, L, I, P]),
     "sa_interp_bilinear_ac_p": (I, [P, L, I, I, I, I, I, I, I, P, L, I, P]),
+    "sa_resample_multi": (I, [I, P, P]),
     "sa_relu_copy": (I, [P, L, I, I, I, P, L, P]),
     "sa_flow_update": (I, [P, P, L, I, I, I, P, L, P, L, P]),
     "sa_convex_upsample": (I, [P, P, L, I, I, I, I, P, P]),

@@ -140,12 +140,12 @@ __device__ __forceinline__ void st_vec(float *p, const float (&v)[VEC]) {
 // VLOAD (W == 2 Wo, in_p % 4 == 0, 16-byte aligned planes): the window columns of a vector's
 // outputs, 2 VEC x0 - 1 .. 2 VEC x0 + 2 VEC - 1, as one scalar and VEC / 2 float4 loads per row.
 template <int VEC, bool VLOAD>
-__global__ __launch_bounds__(256) void pool2x_flat_kernel(const float *__restrict__ in, float *__restrict__ out,
-                                                          FlatGeo g) {
-  const unsigned b = blockIdx.y / (unsigned)g.C, c = blockIdx.y - b * (unsigned)g.C;
+__device__ __forceinline__ void pool2x_flat_body(const float *__restrict__ in, float *__restrict__ out, const FlatGeo &g,
+                                                 unsigned bx, unsigned plane) {
+  const unsigned b = plane / (unsigned)g.C, c = plane - b * (unsigned)g.C;
   const float *p = in + b * g.in_bs + (long)c * g.H * g.in_p;
   float *o = out + b * g.out_bs + (long)c * g.Ho * g.out_p;
-  const unsigned base = blockIdx.x * (256u * FLAT_K) + threadIdx.x;
+  const unsigned base = bx * (256u * FLAT_K) + threadIdx.x;
 #pragma unroll
   for (int k = 0; k < FLAT_K; ++k) {
     const unsigned i = base + k * 256u;
@@ -184,6 +184,12 @@ __global__ __launch_bounds__(256) void pool2x_flat_kernel(const float *__restric
     for (int j = 0; j < VEC; ++j) s[j] = s[j] / 9.0f;
     st_vec<VEC>(o + y * g.out_p + VEC * xv, s);
   }
+}
+
+template <int VEC, bool VLOAD>
+__global__ __launch_bounds__(256) void pool2x_flat_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                          FlatGeo g) {
+  pool2x_flat_body<VEC, VLOAD>(in, out, g, blockIdx.x, blockIdx.y);
 }
 
 // F.interpolate(bilinear, align_corners=True) with upsample_bilinear2d's arithmetic:
@@ -227,13 +233,13 @@ __global__ __launch_bounds__(256) void interp_flat_kernel(const float *__restric
 // output.  grid: x = bands, y = planes; LDS: nr_cap rows x Wo (host-sized, <= 64 KiB).
 // magic_o: ceil(2^32 / Wo) for the horizontal pass's flat (row, column) index.
 template <int VEC>
-__global__ __launch_bounds__(256) void interp_band_kernel(const float *__restrict__ in, float *__restrict__ out,
-                                                          FlatGeo g, float sh, float sw, int RB, unsigned magic_o) {
-  extern __shared__ float hrow[];
-  const unsigned b = blockIdx.y / (unsigned)g.C, c = blockIdx.y - b * (unsigned)g.C;
+__device__ __forceinline__ void interp_band_body(const float *__restrict__ in, float *__restrict__ out, const FlatGeo &g,
+                                                 float sh, float sw, int RB, unsigned magic_o, unsigned bx,
+                                                 unsigned plane, float *hrow) {
+  const unsigned b = plane / (unsigned)g.C, c = plane - b * (unsigned)g.C;
   const float *p = in + b * g.in_bs + (long)c * g.H * g.in_p;
   float *o = out + b * g.out_bs + (long)c * g.Ho * g.out_p;
-  const int ya = blockIdx.x * RB, yb = min(ya + RB, g.Ho);
+  const int ya = (int)bx * RB, yb = min(ya + RB, g.Ho);
   const int r0 = (int)(sh * (float)ya);
   const int yl = (int)(sh * (float)(yb - 1));
   const int nr = yl + (yl < g.H - 1 ? 1 : 0) - r0 + 1;
@@ -262,6 +268,58 @@ __global__ __launch_bounds__(256) void interp_band_kernel(const float *__restric
 #pragma unroll
     for (int j = 0; j < VEC; ++j) v[j] = ly0 * h0[j] + ly1 * h1[j];
     st_vec<VEC>(o + y * g.out_p + VEC * xv, v);
+  }
+}
+
+template <int VEC>
+__global__ __launch_bounds__(256) void interp_band_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                          FlatGeo g, float sh, float sw, int RB, unsigned magic_o) {
+  extern __shared__ float hrow[];
+  interp_band_body<VEC>(in, out, g, sh, sw, RB, magic_o, blockIdx.x, blockIdx.y, hrow);
+}
+
+// Up to 4 independent pool2x / interp jobs in one launch (the update loop's plumbing between
+// two conv launches: pool(h08) + interp(h32) before gru16, interp(h16) + pool(h16) before
+// gru08): job j owns blocks [start[j], start[j + 1]), each block one (x-block, plane) of its
+// job's own launch shape, so the small jobs' launch tails overlap.
+struct ResampleJobDev {
+  const float *in;
+  float *out;
+  FlatGeo g;
+  float sh, sw;
+  int kind, vec, vload, RB;
+  unsigned magic_o, bx;  // x-blocks per plane
+};
+struct ResampleLaunch {
+  ResampleJobDev job[4];
+  unsigned start[5];
+  int njobs;
+};
+
+__global__ __launch_bounds__(256) void resample_multi_kernel(ResampleLaunch L) {
+  extern __shared__ float hrow[];
+  int j = 0;
+  while (j + 1 < L.njobs && blockIdx.x >= L.start[j + 1]) ++j;
+  const ResampleJobDev &J = L.job[j];
+  const unsigned local = blockIdx.x - L.start[j], plane = local / J.bx, bx = local - plane * J.bx;
+  if (J.kind == 0) {
+    if (J.vec == 4 && J.vload)
+      pool2x_flat_body<4, true>(J.in, J.out, J.g, bx, plane);
+    else if (J.vec == 4)
+      pool2x_flat_body<4, false>(J.in, J.out, J.g, bx, plane);
+    else if (J.vec == 2 && J.vload)
+      pool2x_flat_body<2, true>(J.in, J.out, J.g, bx, plane);
+    else if (J.vec == 2)
+      pool2x_flat_body<2, false>(J.in, J.out, J.g, bx, plane);
+    else
+      pool2x_flat_body<1, false>(J.in, J.out, J.g, bx, plane);
+  } else {
+    if (J.vec == 4)
+      interp_band_body<4>(J.in, J.out, J.g, J.sh, J.sw, J.RB, J.magic_o, bx, plane, hrow);
+    else if (J.vec == 2)
+      interp_band_body<2>(J.in, J.out, J.g, J.sh, J.sw, J.RB, J.magic_o, bx, plane, hrow);
+    else
+      interp_band_body<1>(J.in, J.out, J.g, J.sh, J.sw, J.RB, J.magic_o, bx, plane, hrow);
   }
 }
 
@@ -374,6 +432,20 @@ static dim3 flat_grid(const FlatGeo &g, int B) {
   return dim3((g.per + 256u * FLAT_K - 1) / (256u * FLAT_K), (unsigned)(B * g.C));
 }
 
+// The band interp's rows per block: RB output rows while their source rows' blends fit 64 KiB
+// of LDS (nr_cap bounds the rows a band touches: ceil(sh (RB - 1)) + 2, + 1 for float
+// rounding); false: the flat kernel (one output column, or rows too wide)
+static bool band_shape(float sh, int Ho, int Wo, int &RB, size_t &lds) {
+  if (Wo < 2) return false;
+  for (RB = 16; RB >= 2; RB /= 2) {
+    const int nr_cap = (int)ceilf(sh * (float)(RB - 1)) + 3;
+    lds = (size_t)nr_cap * Wo * sizeof(float);
+    if (lds <= 65536 && (unsigned long)nr_cap * Wo * Wo < (1UL << 32)) return true;
+  }
+  (void)Ho;
+  return false;
+}
+
 extern "C" int sa_pool2x_p(const float *in, long in_bs, int in_pitch, int B, int C, int H, int W, float *out,
                            long out_bs, int out_pitch, void *stream) {
   SA_REQUIRE(in && out, "sa_pool2x: null pointer");
@@ -423,14 +495,10 @@ extern "C" int sa_interp_bilinear_ac_p(const float *in, long in_bs, int in_pitch
   SA_REQUIRE(flat_ok(g), "sa_interp_bilinear_ac: output plane shape unsupported (plane too large)");
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_PLUMBING, s);
-  // band kernel: RB output rows per block while their source rows' blends fit 64 KiB of LDS
-  // (nr_cap bounds the rows a band touches: ceil(sh (RB - 1)) + 2, + 1 for float rounding)
-  for (int RB = 16; RB >= 2; RB /= 2) {
-    const int nr_cap = (int)ceilf(sh * (float)(RB - 1)) + 3;
-    const size_t lds = (size_t)nr_cap * Wo * sizeof(float);
-    if (lds > 65536 || (unsigned long)nr_cap * Wo * Wo >= (1UL << 32)) continue;
-    const unsigned magic_o = Wo > 1 ? (unsigned)(((1UL << 32) + Wo - 1) / Wo) : 0u;
-    if (Wo == 1) break;  // the flat kernel
+  int RB;
+  size_t lds;
+  if (band_shape(sh, Ho, Wo, RB, lds)) {
+    const unsigned magic_o = (unsigned)(((1UL << 32) + Wo - 1) / Wo);
     const dim3 grid((Ho + RB - 1) / RB, (unsigned)(B * C));
     if (vec == 4)
       interp_band_kernel<4><<<grid, 256, lds, s>>>(in, out, g, sh, sw, RB, magic_o);
@@ -447,6 +515,66 @@ extern "C" int sa_interp_bilinear_ac_p(const float *in, long in_bs, int in_pitch
   else
     interp_flat_kernel<1><<<flat_grid(g, B), 256, 0, s>>>(in, out, g, sh, sw);
   return sa::check_launch("sa_interp_bilinear_ac");
+}
+
+// sa_resample_multi: validates every job as sa_pool2x_p / sa_interp_bilinear_ac_p do, then one
+// launch; an interp job the band kernel cannot take runs on its own (flat kernel) first.
+extern "C" int sa_resample_multi(int njobs, const SaResampleJob *jobs, void *stream) {
+  SA_REQUIRE(njobs >= 1 && njobs <= 4 && jobs, "sa_resample_multi: 1..4 jobs");
+  ResampleLaunch L{};
+  size_t lds_max = 0;
+  unsigned total = 0;
+  int n = 0;
+  hipStream_t s = sa::as_stream(stream);
+  for (int i = 0; i < njobs; ++i) {
+    const SaResampleJob &q = jobs[i];
+    SA_REQUIRE(q.in && q.out, "sa_resample_multi: null pointer");
+    SA_REQUIRE(q.kind == SA_RESAMPLE_POOL2X || q.kind == SA_RESAMPLE_BILINEAR_AC, "sa_resample_multi: unknown kind");
+    SA_REQUIRE(q.B > 0 && q.C > 0 && q.H > 0 && q.W > 0 && (long)q.B * q.C <= 65535, "sa_resample_multi: bad shape");
+    int Ho = q.Ho, Wo = q.Wo;
+    if (q.kind == SA_RESAMPLE_POOL2X) {
+      const int ho = (q.H + 2 - 3) / 2 + 1, wo = (q.W + 2 - 3) / 2 + 1;
+      SA_REQUIRE(Ho == ho && Wo == wo, "sa_resample_multi: pool2x output size must be ((H-1)/2+1, (W-1)/2+1)");
+    }
+    SA_REQUIRE(Ho > 0 && Wo > 0 && q.in_pitch >= q.W && q.out_pitch >= Wo, "sa_resample_multi: row pitch below the width");
+    SA_REQUIRE((long)q.H * q.in_pitch < (1L << 31) && (long)Ho * q.out_pitch < (1L << 31),
+               "sa_resample_multi: plane too large");
+    const int vec = flat_vec(q.out, Wo, q.out_pitch, q.out_bs);
+    const FlatGeo g = flat_geo(q.in_bs, q.in_pitch, q.C, q.H, q.W, Ho, Wo, q.out_bs, q.out_pitch, vec);
+    SA_REQUIRE(flat_ok(g), "sa_resample_multi: output plane shape unsupported (plane too large)");
+    ResampleJobDev &J = L.job[n];
+    J.in = q.in;
+    J.out = q.out;
+    J.g = g;
+    J.kind = q.kind == SA_RESAMPLE_POOL2X ? 0 : 1;
+    J.vec = vec;
+    if (J.kind == 0) {
+      J.vload = vec >= 2 && q.W == 2 * Wo && q.in_pitch % 4 == 0 && q.in_bs % 4 == 0 && al16(q.in);
+      J.bx = (g.per + 256u * FLAT_K - 1) / (256u * FLAT_K);
+    } else {
+      J.sh = Ho > 1 ? (float)(q.H - 1) / (float)(Ho - 1) : 0.0f;
+      J.sw = Wo > 1 ? (float)(q.W - 1) / (float)(Wo - 1) : 0.0f;
+      size_t lds;
+      if (!band_shape(J.sh, Ho, Wo, J.RB, lds)) {
+        const int rc = sa_interp_bilinear_ac_p(q.in, q.in_bs, q.in_pitch, q.B, q.C, q.H, q.W, Ho, Wo, q.out, q.out_bs,
+                                               q.out_pitch, stream);
+        if (rc) return rc;
+        continue;
+      }
+      J.magic_o = (unsigned)(((1UL << 32) + Wo - 1) / Wo);
+      J.bx = (unsigned)((Ho + J.RB - 1) / J.RB);
+      if (lds > lds_max) lds_max = lds;
+    }
+    L.start[n] = total;
+    total += J.bx * (unsigned)(q.B * q.C);
+    ++n;
+  }
+  if (n == 0) return 0;
+  L.njobs = n;
+  L.start[n] = total;
+  sa::TimingScope ts(SA_K_PLUMBING, s);
+  resample_multi_kernel<<<total, 256, lds_max, s>>>(L);
+  return sa::check_launch("sa_resample_multi");
 }
 
 extern "C" int sa_interp_bilinear_ac(const float *in, long in_bs, int B, int C, int H, int W, int Ho, int Wo,

@@ -716,8 +716,6 @@ class StereoAnywhere(nn.Module):
         def pool(src, ks, dst, kd):
             ops.pool2x(src, dst, width=wid[ks], out_width=wid[kd])
 
-        def up(src, ks, dst, kd):
-            ops.interp(src, dst, width=wid[ks], out_width=wid[kd])
         pool(h16, "16", x32, "32")
         xc32, hzr32 = conv_group(*gate_x_h("32", x32, h32), name="pro32")
         gru_zr(2, "32", h32, xc32, hzr32)
@@ -727,8 +725,9 @@ class StereoAnywhere(nn.Module):
             # lookup of both pyramids + convc1 + ReLU in one kernel (sample 2b: stereo, 2b+1: mono)
             stereo_blk.lookup_conv1x1_into(coords_x, dw["c1_kc"], enc.convc1.bias, c1, other=mono_blk)
             fl = ops.conv2d_small(flow, dw["f1"], enc.convf1.bias, 64, 7, relu=True)
-            pool(h08, "08", x16[:, :128], "16")
-            up(h32, "32", x16[:, 128:], "16")
+            # pool2x(h08) and interp(h32) into gru16's input, one launch
+            ops.resample_multi(("pool", h08, x16[:, :128], wid["08"], wid["16"]),
+                               ("interp", h32, x16[:, 128:], wid["32"], wid["16"]))
             # gru16's x/h convs + the motion encoder's 3x3 convs (bias + ReLU in the epilogue,
             # written straight into the motion conv's input cat(convc2(stereo), convc2(mono),
             # convf2(convf1(flow))))
@@ -745,11 +744,12 @@ class StereoAnywhere(nn.Module):
             q_finish(1, "16", xc16, res[:len(qp)])
             yield   # half an iteration (the batch-parts schedule interleaves here)
             ops.flow_update(coords_x, None, None, x08[:, 126:128])
-            up(h16, "16", x08[:, 128:], "08")
+            # interp(h16) into gru08's input and (not last) pool2x(h16) into gru32's, one launch
+            ops.resample_multi(("interp", h16, x08[:, 128:], wid["16"], wid["08"]),
+                               *([] if last else [("pool", h16, x32, wid["16"], wid["32"])]))
             # gru08's x/h convs (+ gru32's of the next iteration), then the r*h convs
             probs = gate_x_h("08", x08, h08)
             if not last:
-                pool(h16, "16", x32, "32")
                 probs += gate_x_h("32", x32, h32)
             res = conv_group(*probs, name="zr08")
             xc08, hzr08 = res[:2]

@@ -463,6 +463,48 @@ def interp(x: torch.Tensor, out: torch.Tensor, width: Optional[int] = None,
     return out
 
 
+_RESAMPLE_MULTI_MAX = 1 << 26   # output elements (views count their own extent)
+
+
+def resample_multi(*jobs) -> None:
+    """Independent pool2x / interp jobs in one launch (sa_resample_multi): each job is
+    ("pool" | "interp", x, out, width, out_width) with the arguments of pool2x / interp."""
+    if not 1 <= len(jobs) <= 4:
+        raise RuntimeError("resample_multi: 1..4 jobs")
+    bad = [j[0] for j in jobs if j[0] not in ("pool", "interp")]
+    if bad:
+        raise RuntimeError(f"resample_multi: unknown job kind {bad[0]!r}")
+    if sum(out.numel() for _, _, out, _, _ in jobs) > _RESAMPLE_MULTI_MAX:
+        # big jobs fill the chip on their own: one launch each (the booster batch's pair took
+        # 291 / 293 us merged against 274 / 274 us as two launches; configs[1]'s 19.7 / 22.4 us
+        # against 28.7 / 29.0, scripts/bench_small.py --plumbing)
+        for kind, x, out, width, out_width in jobs:
+            (pool2x if kind == "pool" else interp)(x, out, width=width, out_width=out_width)
+        return
+    arr = (N.SaResampleJob * len(jobs))()
+    nbytes = 0.0
+    for j, (kind, x, out, width, out_width) in zip(arr, jobs):
+        B, C, H, Px = x.shape
+        W = width or Px
+        Bo, Co, Ho, Po = out.shape
+        Wo = out_width or Po
+        if (Bo, Co) != (B, C):
+            raise RuntimeError(f"resample_multi: {kind} batch/channels mismatch")
+        if kind == "pool":
+            if (Ho, Wo) != ((H - 1) // 2 + 1, (W - 1) // 2 + 1):
+                raise RuntimeError(f"resample_multi: pool out {tuple(out.shape)} (width {out_width}) != "
+                                   f"{(B, C, (H - 1) // 2 + 1, (W - 1) // 2 + 1)}")
+        if x.device != out.device:
+            raise RuntimeError("resample_multi: x and out on different devices")
+        j.kind = 0 if kind == "pool" else 1
+        j.in_, j.in_bs, j.in_pitch = x.data_ptr(), _pitched_bs(x, "x"), Px
+        j.B, j.C, j.H, j.W, j.Ho, j.Wo = B, C, H, W, Ho, Wo
+        j.out, j.out_bs, j.out_pitch = out.data_ptr(), _pitched_bs(out, "out"), Po
+        nbytes += 4.0 * B * C * (H * W + Ho * Wo)
+    N.call("sa_resample_multi", len(jobs), ctypes.addressof(arr), _stream(jobs[0][1]))
+    _account("gru_plumbing", nbytes)
+
+
 def relu_copy(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
     B, C, H, W = x.shape
     if tuple(out.shape) != (B, C, H, W):

@@ -456,6 +456,57 @@ def test_gru_gates_and_plumbing(H, W):
     torch.testing.assert_close(r, torch.relu(x))
 
 
+def test_resample_multi_equals_single_jobs():
+    """sa_resample_multi (pool2x / interp jobs in one launch) = the one-job entry points bit for
+    bit: dense and pitched planes, the update loop's two job sets, a 1-column interp (the flat
+    kernel beside the launch) and a 3-job launch."""
+    g = torch.Generator(device="cpu").manual_seed(7)
+
+    def r(*shape):
+        return torch.randn(*shape, generator=g).to(dev)
+    B, C = 2, 16
+    h08, h16, h32 = r(B, C, 112, 140), r(B, C, 56, 70), r(B, C, 28, 35)
+    # pitched 70- and 35-wide levels (row pitch 72 / 36), as the update loop keeps ragged levels
+    h16p = torch.zeros(B, C, 56, 72, device=dev)
+    h16p[..., :70] = h16
+    x16a, x16b = torch.zeros(B, 2 * C, 56, 72, device=dev), torch.zeros(B, 2 * C, 56, 72, device=dev)
+    ops.pool2x(h08, x16a[:, :C], out_width=70)
+    ops.interp(h32, x16a[:, C:], out_width=70)
+    ops.resample_multi(("pool", h08, x16b[:, :C], None, 70), ("interp", h32, x16b[:, C:], None, 70))
+    assert torch.equal(x16a, x16b)
+    x08a, x08b = torch.zeros(B, 2 * C, 112, 140, device=dev), torch.zeros(B, 2 * C, 112, 140, device=dev)
+    x32a, x32b = torch.zeros(B, C, 28, 36, device=dev), torch.zeros(B, C, 28, 36, device=dev)
+    ops.interp(h16p, x08a[:, C:], width=70)
+    ops.pool2x(h16p, x32a, width=70, out_width=35)
+    ops.resample_multi(("interp", h16p, x08b[:, C:], 70, None), ("pool", h16p, x32b, 70, 35))
+    assert torch.equal(x08a, x08b) and torch.equal(x32a, x32b)
+    col_a, col_b = torch.zeros(B, C, 9, 1, device=dev), torch.zeros(B, C, 9, 1, device=dev)
+    ops.interp(h32, col_a)
+    p_a, p_b = torch.zeros(B, C, 14, 18, device=dev), torch.zeros(B, C, 14, 18, device=dev)
+    ops.pool2x(h32, p_a)
+    u_a, u_b = torch.zeros(B, C, 61, 83, device=dev), torch.zeros(B, C, 61, 83, device=dev)
+    ops.interp(h32, u_a)
+    ops.resample_multi(("interp", h32, col_b, None, None), ("pool", h32, p_b, None, None),
+                       ("interp", h32, u_b, None, None))
+    assert torch.equal(col_a, col_b) and torch.equal(p_a, p_b) and torch.equal(u_a, u_b)
+    torch.testing.assert_close(u_b, torch.nn.functional.interpolate(h32, (61, 83), mode="bilinear",
+                                                                    align_corners=True), atol=1e-6, rtol=0)
+    with pytest.raises(RuntimeError, match="pool out"):
+        ops.resample_multi(("pool", h32, u_b, None, None))
+
+
+@pytest.mark.parametrize("hw,out", [((544, 960), (136, 240)), ((1120, 3008), (280, 752)), ((7, 5), (3, 2)),
+                                    ((68, 120), (136, 240))])
+def test_interp_band_down_and_up_vs_torch(hw, out):
+    """interp on the band kernel (downsampling as the mono maps are resized, model.py _forward,
+    and a width whose band must shrink) and on its fallbacks = torch's align_corners bilinear."""
+    g = torch.Generator(device="cpu").manual_seed(11)
+    x = torch.randn(2, 1, *hw, generator=g).to(dev)
+    y = ops.interp(x, torch.empty(2, 1, *out, device=dev))
+    torch.testing.assert_close(y, torch.nn.functional.interpolate(x, out, mode="bilinear", align_corners=True),
+                               atol=2e-6, rtol=0)
+
+
 def test_ops_reject_cpu_tensors():
     with pytest.raises(RuntimeError, match="GPU"):
         ops.corr_volume(torch.zeros(1, 4, 2, 8), torch.zeros(1, 4, 2, 8))
