@@ -1374,16 +1374,32 @@ __global__ __launch_bounds__(256) void flow_head_reduce_kernel(const float *__re
   const int ty1 = up ? ty0 - 1 : ty0 + 1, tx1 = lf ? tx0 - 1 : tx0 + 1;
   auto off = [&](int ty, int tx) { return ((long)(ty * tiles_w + tx) * RH + (y - (ty * BH - 1))) * RW + (x - (tx * BW - 1)); };
   const bool hy = up || dn, hx = lf || rt;
-  const long o0 = off(ty0, tx0), o1 = hx ? off(ty0, tx1) : 0, o2 = hy ? off(ty1, tx0) : 0,
-             o3 = hx && hy ? off(ty1, tx1) : 0;
+  // (absent neighbours read the pixel's own partial and add nothing: no branches between the loads)
+  const long o0 = off(ty0, tx0), o1 = hx ? off(ty0, tx1) : o0, o2 = hy ? off(ty1, tx0) : o0,
+             o3 = hx && hy ? off(ty1, tx1) : o0;
   float d = bias0[0];
   const float *pc = part + b * part_bs;
   const long cbs = (long)tiles_hw * RH * RW;
-  for (int cb = 0; cb < ncb; ++cb, pc += cbs) {
-    d += pc[o0];
-    if (hx) d += pc[o1];
-    if (hy) d += pc[o2];
-    if (hx && hy) d += pc[o3];
+  // 8 channel blocks' 32 loads go out together (clamped block index, summed only below ncb),
+  // then the sums in the fixed order
+  for (int cb0 = 0; cb0 < ncb; cb0 += 8) {
+    float a[8][4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float *q = pc + (long)min(cb0 + j, ncb - 1) * cbs;
+      a[j][0] = q[o0];
+      a[j][1] = q[o1];
+      a[j][2] = q[o2];
+      a[j][3] = q[o3];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool in = cb0 + j < ncb;
+      d = in ? d + a[j][0] : d;
+      d = in && hx ? d + a[j][1] : d;
+      d = in && hy ? d + a[j][2] : d;
+      d = in && hx && hy ? d + a[j][3] : d;
+    }
   }
   const long i = b * hw + r;
   const float c = cx[i] + d;
