@@ -56,6 +56,12 @@
 #ifndef SA_W4_GJB1
 #define SA_W4_GJB1 16  // the same for mode 1
 #endif
+#ifndef SA_W4_DUP
+#define SA_W4_DUP 0    // split kernel: each B operand (bhi, blo, bhi, blo) read as its (hi, lo) dword twice by one
+                       // ds_read2st64_b32 (filter image [g][k][n] per point and job) instead of register copies;
+                       // a column's pairs of points 0-2 / 3-5 are reloaded for the next column as soon as their
+                       // MFMAs are issued (the same 24 VGPRs as the copied form's bc / bn)
+#endif
 #ifndef SA_W4_PRIO
 #define SA_W4_PRIO 1   // s_setprio 1 for the point-half-1 waves (split kernel forward: 66.8 -> 66.5 ms/step, wino4 49.8 -> 49.0 ms, two interleaved passes)
 #endif
@@ -227,6 +233,33 @@ __device__ __forceinline__ f16x4 w4_split(const float x) {
 __device__ __forceinline__ float w4_unsplit(const float packed) {
   const f16x2 p = __builtin_bit_cast(f16x2, packed);
   return (float)p[0] + (float)p[1];
+}
+
+// (SA_W4_DUP) the dword at LDS byte address addr + 256 OFF into both registers of a pair: one
+// ds_read2st64_b32 with equal offsets.  Inline asm: the compiler does not count it in its LDS
+// waits, so every use is preceded by w4_lds_wait3 on the loaded pairs.
+template <int OFF>
+__device__ __forceinline__ f32x2 w4_lds_dup(unsigned addr) {
+  f32x2 r;
+  asm volatile("ds_read2st64_b32 %0, %1 offset0:%2 offset1:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+// the same with the offset as a value the unrolled loops make constant (the chain folds away)
+template <int N>
+__device__ __forceinline__ f32x2 w4_lds_dup_rt(unsigned addr, int off) {
+  if constexpr (N < 0) {
+    __builtin_unreachable();
+    return f32x2{0.f, 0.f};
+  } else {
+    if (off == N) return w4_lds_dup<N>(addr);
+    return w4_lds_dup_rt<N - 1>(addr, off);
+  }
+}
+// s_waitcnt lgkmcnt(CNT) tied to three points' pairs (both groups), so no use is scheduled above
+// it; CNT <= the LDS operations issued after those pairs' loads (LDS returns in order)
+template <int CNT>
+__device__ __forceinline__ void w4_lds_wait3(f32x2 &a0, f32x2 &a1, f32x2 &b0, f32x2 &b1, f32x2 &c0, f32x2 &c1) {
+  asm volatile("s_waitcnt lgkmcnt(%6)" : "+v"(a0), "+v"(a1), "+v"(b0), "+v"(b1), "+v"(c0), "+v"(c1) : "n"(CNT));
 }
 
 // Range guard of the split kernel: blocks whose f16 operands overflowed (|V| >= 65520 turns hi
@@ -686,7 +719,9 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   int PSv = PS, PGv = PG;
   asm volatile("" : "+s"(PSv), "+s"(PGv));
   const int pread = k * PSv * 4 + 4 * trow * PGv * 4 + 4 * tcol + 2;
-  const int uread = (k * 16 + m) * CG;
+  // (SA_W4_DUP: the split filter image is [g][k][n] per point and job, one 64-dword row per group)
+  constexpr bool DUP = SA_W4_DUP && (SPLIT || C::UNSPLIT) && !W4S_K32;
+  const int uread = DUP ? k * 16 + m : (k * 16 + m) * CG;
 
   // acc[i][jj][g]: point (row i, or 3 RH + i in a quadrant; column 3 HF + jj) of output-channel
   // group g
@@ -776,6 +811,9 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
         if constexpr (SPLIT && W4S_K32) {   // the K = 32 filter image [point][k][n][g][s], per channel
           const float *q = smem + cur * BUF + PBUF + (k * 16 + m) * 4 + (6 * i + 3 * HF + jj) * 256 + s;
           b[i] = f32xg{q[0], q[2]};
+        } else if constexpr (DUP) {   // (the redo kernel's fp32 products on the [g][k][n] image)
+          const float *q = ub + ((6 * i + 3 * HF + jj) * JPC + s) * SB;
+          b[i] = f32xg{q[0], q[64]};
         } else {
           b[i] = *reinterpret_cast<const f32xg *>(ub + ((6 * (QUAD ? 3 * RH + i : i) + 3 * HF + jj) * JPC + s) * SB);
         }
@@ -839,6 +877,67 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
 #if SA_W4_FENCE
           __builtin_amdgcn_sched_barrier(0);
 #endif
+        }
+      }
+      continue;
+    }
+    if constexpr (DUP && SPLIT) {
+      const unsigned ua = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float *)ub;
+      f32x2 P[6][2];   // the current column's pairs; points 0-2 / 3-5 refilled for the next column
+      auto ldp = [&](int s, int jj, int i0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = i0; i < i0 + 3; ++i)
+#pragma unroll
+          for (int g = 0; g < 2; ++g) P[i][g] = w4_lds_dup_rt<143>(ua, ((6 * i + 3 * HF + jj) * JPC + s) * 2 + g);
+      };
+      load_rows(0, 0, 6);
+      ldp(0, 0, 0);
+      ldp(0, 0, 3);
+#pragma unroll
+      for (int s = 0; s < JPC; ++s) {
+        if (s == 1) load_rows(1, 3, 6);
+        float t[6][3];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t[r]);
+        if (s + 1 < JPC) load_rows(1, 0, 3);
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) {
+          const bool more = s + 1 < JPC || jj < 2;
+          const int ns = jj < 2 ? s : s + 1, njj = jj < 2 ? jj + 1 : 0;
+          float v[6];
+          bt6(t[0][jj], t[1][jj], t[2][jj], t[3][jj], t[4][jj], t[5][jj], v);
+          f16x4 a[6];
+#pragma unroll
+          for (int i = 0; i < 6; ++i) a[i] = w4_split(v[i]);
+          w4_lds_wait3<6>(P[0][0], P[0][1], P[1][0], P[1][1], P[2][0], P[2][1]);   // points 3-5's pairs may stay out
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x16f16(a[i], __builtin_bit_cast(f16x4, P[i][0]), acc[i][jj][0], 0, 0, 0);
+            acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x16f16(a[i], __builtin_bit_cast(f16x4, P[i][1]), acc[i][jj][1], 0, 0, 0);
+          }
+#if SA_W4_FENCE
+          __builtin_amdgcn_sched_barrier(0);
+#endif
+          if (more) ldp(ns, njj, 0);
+          if (more)
+            w4_lds_wait3<6>(P[3][0], P[3][1], P[4][0], P[4][1], P[5][0], P[5][1]);   // the refill of 0-2 may stay out
+          else
+            w4_lds_wait3<0>(P[3][0], P[3][1], P[4][0], P[4][1], P[5][0], P[5][1]);
+#pragma unroll
+          for (int i = 3; i < 6; ++i) {
+            acc[i][jj][0] = __builtin_amdgcn_mfma_f32_16x16x16f16(a[i], __builtin_bit_cast(f16x4, P[i][0]), acc[i][jj][0], 0, 0, 0);
+            acc[i][jj][1] = __builtin_amdgcn_mfma_f32_16x16x16f16(a[i], __builtin_bit_cast(f16x4, P[i][1]), acc[i][jj][1], 0, 0, 0);
+          }
+#if SA_W4_FENCE
+          __builtin_amdgcn_sched_barrier(0);
+#endif
+          if (more) ldp(ns, njj, 3);
+          if (SA_W4_DIAG == 0 && SA_W4_SPREAD && s == 0 && kc + 1 < nchunks) {
+            issue_part(kc + 1, cur ^ 1, jj);
+#if SA_W4_FENCE
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+          }
         }
       }
       continue;
@@ -1344,6 +1443,8 @@ __global__ __launch_bounds__(256) void wino4s_weights_kernel(const float *__rest
       const int pt = 6 * a + b;
       if (W4S_K32)   // [Cout/32][Cin/8][36][4][16][2][2]: channel 8 chunk + 4 s + k at [k][n][g][s]
         U[(((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 4 + k) * 16 + n) * 4 + gg * 2 + s] = pr;
+      else if (SA_W4_DUP)   // [Cout/32][Cin/8][36][2][2][4][16]: [g][k][n] per point and job
+        U[(((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 2 + s) * 2 + gg) * 64 + k * 16 + n] = pr;
       else
         U[(((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 2 + s) * 4 + k) * 32 + n * 2 + gg] = pr;
     }
