@@ -25,7 +25,7 @@ FAMILIES = {
     # round 4: the families bench.py times separately (were "misc")
     "pyramid_from_volume_kernel": "mono_pyramid", "pyramid_from_strided_kernel": "mono_pyramid",
     "pool2x_kernel": "gru_plumbing", "pool2x_v4_kernel": "gru_plumbing", "interp_kernel": "gru_plumbing",
-    "pool2x_flat_kernel": "gru_plumbing", "interp_flat_kernel": "gru_plumbing", "interp_band_kernel": "gru_plumbing",
+    "pool2x_flat_kernel": "gru_plumbing", "interp_flat_kernel": "gru_plumbing", "interp_band_kernel": "gru_plumbing", "resample_multi_kernel": "gru_plumbing",
     "interp_v4_kernel": "gru_plumbing", "flow_update_kernel": "gru_plumbing", "relu_copy_kernel": "gru_plumbing",
     "flow_head_reduce_kernel": "gru_plumbing",
     "conv2d_k3_narrow_kernel": "conv2d_narrow", "conv2d_f1_mfma_kernel": "conv2d_small", "conv2d_small_kernel": "conv2d_small",
