@@ -190,7 +190,10 @@ int sa_interp_bilinear_ac_p(const float *in, long in_bs, int in_pitch, int B, in
  * loop's plumbing between two conv launches (update.py:124-132: pool2x(net[0]) and
  * interp(net[2]) feed gru16; interp(net[1]) feeds gru08 and pool2x(net[1]) gru32).  pool2x:
  * (Ho, Wo) must be ((H-1)/2+1, (W-1)/2+1).  Same results as the one-job entry points. */
-enum { SA_RESAMPLE_POOL2X = 0, SA_RESAMPLE_BILINEAR_AC = 1 };
+/* SA_RESAMPLE_FLOW_X: the motion encoder's flow planes from the coordinates, sa_flow_update with
+ * only flow_b: in = coords [B,1,H,W] (dense, batch stride in_bs), out = [B,2,H,W] planes (batch
+ * stride out_bs): out[0] = coords - x, out[1] = 0; C = 1, (Ho, Wo) = (H, W), pitches = W. */
+enum { SA_RESAMPLE_POOL2X = 0, SA_RESAMPLE_BILINEAR_AC = 1, SA_RESAMPLE_FLOW_X = 2 };
 typedef struct SaResampleJob {
   int kind;
   const float *in;

@@ -278,16 +278,33 @@ __global__ __launch_bounds__(256) void interp_band_kernel(const float *__restric
   interp_band_body<VEC>(in, out, g, sh, sw, RB, magic_o, blockIdx.x, blockIdx.y, hrow);
 }
 
+// the flow planes of the motion encoder's input from the coordinates (sa_flow_update with only
+// flow_b): out[b][0] = coords - x, out[b][1] = 0 (stereoanywhere.py:272-280, update.py:90)
+__device__ __forceinline__ void flow_x_body(const float *__restrict__ cx, float *__restrict__ out, const FlatGeo &g,
+                                            unsigned bx, unsigned b) {
+  const unsigned base = bx * (256u * FLAT_K) + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < FLAT_K; ++k) {
+    const unsigned r = base + k * 256u;
+    if (r >= g.per) return;
+    unsigned y, x;
+    flat_row(g, r, y, x);
+    const float fx = cx[b * g.in_bs + r] - (float)x;
+    out[b * g.out_bs + r] = fx;
+    out[b * g.out_bs + g.per + r] = 0.0f;
+  }
+}
+
 // Up to 4 independent pool2x / interp jobs in one launch (the update loop's plumbing between
 // two conv launches: pool(h08) + interp(h32) before gru16, interp(h16) + pool(h16) before
 // gru08): job j owns blocks [start[j], start[j + 1]), each block one (x-block, plane) of its
 // job's own launch shape, so the small jobs' launch tails overlap.
 struct ResampleJobDev {
-  const float *in;
+  const float *in;  // (flow job: the coordinates)
   float *out;
   FlatGeo g;
   float sh, sw;
-  int kind, vec, vload, RB;
+  int kind, vec, vload, RB;  // kind 0 pool2x, 1 interp, 2 flow planes
   unsigned magic_o, bx;  // x-blocks per plane
 };
 struct ResampleLaunch {
@@ -302,7 +319,9 @@ __global__ __launch_bounds__(256) void resample_multi_kernel(ResampleLaunch L) {
   while (j + 1 < L.njobs && blockIdx.x >= L.start[j + 1]) ++j;
   const ResampleJobDev &J = L.job[j];
   const unsigned local = blockIdx.x - L.start[j], plane = local / J.bx, bx = local - plane * J.bx;
-  if (J.kind == 0) {
+  if (J.kind == 2) {
+    flow_x_body(J.in, J.out, J.g, bx, plane);
+  } else if (J.kind == 0) {
     if (J.vec == 4 && J.vload)
       pool2x_flat_body<4, true>(J.in, J.out, J.g, bx, plane);
     else if (J.vec == 4)
@@ -529,9 +548,27 @@ extern "C" int sa_resample_multi(int njobs, const SaResampleJob *jobs, void *str
   for (int i = 0; i < njobs; ++i) {
     const SaResampleJob &q = jobs[i];
     SA_REQUIRE(q.in && q.out, "sa_resample_multi: null pointer");
-    SA_REQUIRE(q.kind == SA_RESAMPLE_POOL2X || q.kind == SA_RESAMPLE_BILINEAR_AC, "sa_resample_multi: unknown kind");
+    SA_REQUIRE(q.kind == SA_RESAMPLE_POOL2X || q.kind == SA_RESAMPLE_BILINEAR_AC || q.kind == SA_RESAMPLE_FLOW_X,
+               "sa_resample_multi: unknown kind");
     SA_REQUIRE(q.B > 0 && q.C > 0 && q.H > 0 && q.W > 0 && (long)q.B * q.C <= 65535, "sa_resample_multi: bad shape");
     int Ho = q.Ho, Wo = q.Wo;
+    if (q.kind == SA_RESAMPLE_FLOW_X) {
+      SA_REQUIRE(q.C == 1 && Ho == q.H && Wo == q.W && q.in_pitch == q.W && q.out_pitch == q.W &&
+                     q.in_bs >= (long)q.H * q.W && q.out_bs >= 2L * q.H * q.W && (long)q.H * q.W < (1L << 31),
+                 "sa_resample_multi: flow job needs dense [B,1,H,W] coordinates and [B,2,H,W] flow planes");
+      ResampleJobDev &J = L.job[n];
+      J.in = q.in;
+      J.out = q.out;
+      J.g = flat_geo(q.in_bs, q.W, 1, q.H, q.W, q.H, q.W, q.out_bs, q.W, 1);
+      SA_REQUIRE(flat_ok(J.g), "sa_resample_multi: flow plane too large");
+      J.kind = 2;
+      J.vec = 1;
+      J.bx = (J.g.per + 256u * FLAT_K - 1) / (256u * FLAT_K);
+      L.start[n] = total;
+      total += J.bx * (unsigned)q.B;
+      ++n;
+      continue;
+    }
     if (q.kind == SA_RESAMPLE_POOL2X) {
       const int ho = (q.H + 2 - 3) / 2 + 1, wo = (q.W + 2 - 3) / 2 + 1;
       SA_REQUIRE(Ho == ho && Wo == wo, "sa_resample_multi: pool2x output size must be ((H-1)/2+1, (W-1)/2+1)");

@@ -743,9 +743,10 @@ class StereoAnywhere(nn.Module):
                              name="q16")
             q_finish(1, "16", xc16, res[:len(qp)])
             yield   # half an iteration (the batch-parts schedule interleaves here)
-            ops.flow_update(coords_x, None, None, x08[:, 126:128])
+            # the flow planes of x08 (after the motion conv wrote its padding channels there),
             # interp(h16) into gru08's input and (not last) pool2x(h16) into gru32's, one launch
-            ops.resample_multi(("interp", h16, x08[:, 128:], wid["16"], wid["08"]),
+            ops.resample_multi(("flow_x", coords_x, x08[:, 126:128], None, None),
+                               ("interp", h16, x08[:, 128:], wid["16"], wid["08"]),
                                *([] if last else [("pool", h16, x32, wid["16"], wid["32"])]))
             # gru08's x/h convs (+ gru32's of the next iteration), then the r*h convs
             probs = gate_x_h("08", x08, h08)

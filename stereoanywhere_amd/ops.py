@@ -468,10 +468,11 @@ _RESAMPLE_MULTI_MAX = 1 << 26   # output elements (views count their own extent)
 
 def resample_multi(*jobs) -> None:
     """Independent pool2x / interp jobs in one launch (sa_resample_multi): each job is
-    ("pool" | "interp", x, out, width, out_width) with the arguments of pool2x / interp."""
+    ("pool" | "interp", x, out, width, out_width) with the arguments of pool2x / interp, or
+    ("flow_x", coords_x, flow_planes, None, None) = flow_update(coords_x, None, None, flow_planes)."""
     if not 1 <= len(jobs) <= 4:
         raise RuntimeError("resample_multi: 1..4 jobs")
-    bad = [j[0] for j in jobs if j[0] not in ("pool", "interp")]
+    bad = [j[0] for j in jobs if j[0] not in ("pool", "interp", "flow_x")]
     if bad:
         raise RuntimeError(f"resample_multi: unknown job kind {bad[0]!r}")
     if sum(out.numel() for _, _, out, _, _ in jobs) > _RESAMPLE_MULTI_MAX:
@@ -479,11 +480,24 @@ def resample_multi(*jobs) -> None:
         # 291 / 293 us merged against 274 / 274 us as two launches; configs[1]'s 19.7 / 22.4 us
         # against 28.7 / 29.0, scripts/bench_small.py --plumbing)
         for kind, x, out, width, out_width in jobs:
-            (pool2x if kind == "pool" else interp)(x, out, width=width, out_width=out_width)
+            if kind == "flow_x":
+                flow_update(x, None, None, out)
+            else:
+                (pool2x if kind == "pool" else interp)(x, out, width=width, out_width=out_width)
         return
     arr = (N.SaResampleJob * len(jobs))()
     nbytes = 0.0
     for j, (kind, x, out, width, out_width) in zip(arr, jobs):
+        if kind == "flow_x":   # flow_update(coords_x, None, None, out) as a job
+            _check(x, "coords_x")
+            B, _, H, W = x.shape
+            if x.shape[1] != 1 or tuple(out.shape) != (B, 2, H, W):
+                raise RuntimeError(f"resample_multi: flow job coords {tuple(x.shape)} / planes {tuple(out.shape)}")
+            j.kind, j.in_, j.in_bs, j.in_pitch = 2, x.data_ptr(), x.stride(0), W
+            j.B, j.C, j.H, j.W, j.Ho, j.Wo = B, 1, H, W, H, W
+            j.out, j.out_bs, j.out_pitch = out.data_ptr(), _plane_bs(out, "flow_b"), W
+            nbytes += 12.0 * B * H * W
+            continue
         B, C, H, Px = x.shape
         W = width or Px
         Bo, Co, Ho, Po = out.shape

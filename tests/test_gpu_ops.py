@@ -493,6 +493,12 @@ def test_resample_multi_equals_single_jobs():
                                                                     align_corners=True), atol=1e-6, rtol=0)
     with pytest.raises(RuntimeError, match="pool out"):
         ops.resample_multi(("pool", h32, u_b, None, None))
+    # the flow-plane job (flow_update with only flow_b) beside an interp, into channel slices
+    cx = r(B, 1, 56, 70) * 10 + torch.arange(70, device=dev, dtype=torch.float32)
+    buf_a, buf_b = torch.full((B, 4, 56, 70), 7.0, device=dev), torch.full((B, 4, 56, 70), 7.0, device=dev)
+    ops.flow_update(cx, None, None, buf_a[:, 1:3])
+    ops.resample_multi(("flow_x", cx, buf_b[:, 1:3], None, None), ("interp", h32, x16b[:, C:], None, 70))
+    assert torch.equal(buf_a, buf_b) and float(buf_b[:, 2].abs().max()) == 0.0
 
 
 @pytest.mark.parametrize("hw,out", [((544, 960), (136, 240)), ((1120, 3008), (280, 752)), ((7, 5), (3, 2)),
