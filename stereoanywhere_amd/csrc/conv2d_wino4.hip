@@ -62,6 +62,9 @@
                        // a column's pairs of points 0-2 / 3-5 are reloaded for the next column as soon as their
                        // MFMAs are issued (the same 24 VGPRs as the copied form's bc / bn)
 #endif
+#ifndef SA_W4_DMA_AT
+#define SA_W4_DMA_AT 0 // the next chunk's DMA part jj: 0 after column jj's MFMAs of the first job, 1 before its column pass
+#endif
 #ifndef SA_W4_PRIO
 #define SA_W4_PRIO 1   // s_setprio 1 for the point-half-1 waves (split kernel forward: 66.8 -> 66.5 ms/step, wino4 49.8 -> 49.0 ms, two interleaved passes)
 #endif
@@ -959,6 +962,12 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
       if (s + 1 < JPC) load_rows(1, 0, 3);
 #pragma unroll
       for (int jj = 0; jj < 3; ++jj) {
+        if (SA_W4_DMA_AT == 1 && SA_W4_DIAG == 0 && SA_W4_SPREAD && s == 0 && kc + 1 < nchunks) {
+          issue_part(kc + 1, cur ^ 1, jj);
+#if SA_W4_FENCE
+          __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
         if (SA_W4_DIAG != 7 && (s + 1 < JPC || jj < 2)) load_b(jj < 2 ? s : s + 1, jj < 2 ? jj + 1 : 0, bn);
         float v[6];
         if (SA_W4_DIAG == 5 || SA_W4_DIAG == 8) {   // timing only: no column pass
@@ -989,7 +998,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
 #if SA_W4_FENCE
         __builtin_amdgcn_sched_barrier(0);   // bound the scheduler's hoisting (register pressure)
 #endif
-        if (SA_W4_DIAG == 0 && SA_W4_SPREAD && s == 0 && kc + 1 < nchunks) {
+        if (SA_W4_DMA_AT == 0 && SA_W4_DIAG == 0 && SA_W4_SPREAD && s == 0 && kc + 1 < nchunks) {
           issue_part(kc + 1, cur ^ 1, jj);
 #if SA_W4_FENCE
           __builtin_amdgcn_sched_barrier(0);
