@@ -63,7 +63,10 @@
                        // MFMAs are issued (the same 24 VGPRs as the copied form's bc / bn)
 #endif
 #ifndef SA_W4_DMA_AT
-#define SA_W4_DMA_AT 0 // the next chunk's DMA part jj: 0 after column jj's MFMAs of the first job, 1 before its column pass
+#define SA_W4_DMA_AT 1 // the next chunk's DMA part jj: 0 after column jj's MFMAs of the first job, 1 before its
+                       // column pass (wino4 51.0 -> 50.1 ms/step, scripts/ab_w4_variants.sh), 2 all three parts
+                       // before column 0 (after the first job's row pass), 3 part 0 before the first job's row
+                       // pass, part jj + 1 before column jj
 #endif
 #ifndef SA_W4_PRIO
 #define SA_W4_PRIO 1   // s_setprio 1 for the point-half-1 waves (split kernel forward: 66.8 -> 66.5 ms/step, wino4 49.8 -> 49.0 ms, two interleaved passes)
@@ -950,6 +953,12 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
 #pragma unroll
     for (int s = 0; s < JPC; ++s) {
       if (s == 1) load_rows(1, 3, 6);
+      if (SA_W4_DMA_AT == 3 && SA_W4_DIAG == 0 && SA_W4_SPREAD && s == 0 && kc + 1 < nchunks) {
+        issue_part(kc + 1, cur ^ 1, 0);
+#if SA_W4_FENCE
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+      }
       float t[6][3];
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
@@ -962,8 +971,10 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
       if (s + 1 < JPC) load_rows(1, 0, 3);
 #pragma unroll
       for (int jj = 0; jj < 3; ++jj) {
-        if (SA_W4_DMA_AT == 1 && SA_W4_DIAG == 0 && SA_W4_SPREAD && s == 0 && kc + 1 < nchunks) {
-          issue_part(kc + 1, cur ^ 1, jj);
+        if (SA_W4_DMA_AT >= 1 && SA_W4_DIAG == 0 && SA_W4_SPREAD && s == 0 && kc + 1 < nchunks) {
+          if (SA_W4_DMA_AT == 1) issue_part(kc + 1, cur ^ 1, jj);
+          if (SA_W4_DMA_AT == 2 && jj == 0) issue(kc + 1, cur ^ 1);
+          if (SA_W4_DMA_AT == 3 && jj < 2) issue_part(kc + 1, cur ^ 1, jj + 1);
 #if SA_W4_FENCE
           __builtin_amdgcn_sched_barrier(0);
 #endif
