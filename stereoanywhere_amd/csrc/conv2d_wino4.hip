@@ -910,6 +910,12 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
         for (int jj = 0; jj < 3; ++jj) {
           const bool more = s + 1 < JPC || jj < 2;
           const int ns = jj < 2 ? s : s + 1, njj = jj < 2 ? jj + 1 : 0;
+          if (SA_W4_DMA_AT == 1 && SA_W4_DIAG == 0 && SA_W4_SPREAD && s == 0 && kc + 1 < nchunks) {
+            issue_part(kc + 1, cur ^ 1, jj);
+#if SA_W4_FENCE
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+          }
           float v[6];
           bt6(t[0][jj], t[1][jj], t[2][jj], t[3][jj], t[4][jj], t[5][jj], v);
           f16x4 a[6];
@@ -938,7 +944,7 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
           __builtin_amdgcn_sched_barrier(0);
 #endif
           if (more) ldp(ns, njj, 3);
-          if (SA_W4_DIAG == 0 && SA_W4_SPREAD && s == 0 && kc + 1 < nchunks) {
+          if (SA_W4_DMA_AT == 0 && SA_W4_DIAG == 0 && SA_W4_SPREAD && s == 0 && kc + 1 < nchunks) {
             issue_part(kc + 1, cur ^ 1, jj);
 #if SA_W4_FENCE
             __builtin_amdgcn_sched_barrier(0);
