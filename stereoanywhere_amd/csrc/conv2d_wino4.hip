@@ -68,6 +68,11 @@
                        // before column 0 (after the first job's row pass), 3 part 0 before the first job's row
                        // pass, part jj + 1 before column jj
 #endif
+#ifndef SA_W4_TGRP
+#define SA_W4_TGRP 1   // work-item order: groups of TGRP tiles, output-channel block outer within a group
+                       // (1: a tile's channel blocks adjacent).  The 32 blocks an XCD runs at once then share
+                       // ~TGRP tiles' patches and ~32 / TGRP channel blocks' filters in its L2
+#endif
 #ifndef SA_W4_PRIO
 #define SA_W4_PRIO 1   // s_setprio 1 for the point-half-1 waves (split kernel forward: 66.8 -> 66.5 ms/step, wino4 49.8 -> 49.0 ms, two interleaved passes)
 #endif
@@ -180,8 +185,26 @@ struct W4Prob {
   const float *in_m, *in_s, *in_t;
   int in_pstride, in_act;
   int pitch;               // row pitch of the input / output / gate planes (>= W, % 4 == 0; SaWinoProblem)
+  int ntiles;              // N * tiles_hw
 };
 constexpr int MAX_PROB = 8;
+
+// work item -> (output-channel block, tile in the image, image)
+__device__ __forceinline__ void w4_item(const unsigned wid, const int co_blocks, const int tiles_hw, const int ntiles,
+                                        int &cb, int &st, int &n) {
+  int gt;
+  if constexpr (SA_W4_TGRP <= 1) {
+    cb = wid % co_blocks;
+    gt = wid / co_blocks;
+  } else {
+    const int per = SA_W4_TGRP * co_blocks, g = wid / per, rem = wid - g * per, full = ntiles / SA_W4_TGRP;
+    const int sz = g < full ? SA_W4_TGRP : ntiles - full * SA_W4_TGRP;
+    cb = rem / sz;
+    gt = g * SA_W4_TGRP + (rem - cb * sz);
+  }
+  st = gt % tiles_hw;
+  n = gt / tiles_hw;
+}
 // GRU gate epilogues (SaGateEpilogue in the header), read by the store loop only
 struct W4Gate {
   int mode;
@@ -356,9 +379,8 @@ __device__ __forceinline__ void w4_issue_chunk0(const W4Prob &P, const unsigned 
   const int ltw = P.ltw, tw = 1 << ltw, tr = NT >> ltw;
   const int BH = 4 * tr, BW = 4 * tw, PG = tw + 2, PR = BH + 2, PS = PR * PG;
   const int co_blocks = P.co_blocks, tiles_hw = P.tiles_hw, tiles_w = P.tiles_w;
-  const int cb = wid % co_blocks;
-  const int st = (wid / co_blocks) % tiles_hw;
-  const int n = wid / (co_blocks * tiles_hw);
+  int cb, st, n;
+  w4_item(wid, co_blocks, tiles_hw, P.ntiles, cb, st, n);
   const int y0 = (st / tiles_w) * BH, x0 = (st % tiles_w) * BW;
   const int pitch = P.pitch, hw = H * pitch;
   const __amdgpu_buffer_rsrc_t xin = __builtin_amdgcn_make_buffer_rsrc(
@@ -646,9 +668,8 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int co_blocks = P.co_blocks, tiles_hw = P.tiles_hw, tiles_w = P.tiles_w;
-  const int cb = wid % co_blocks;
-  const int st = (wid / co_blocks) % tiles_hw;
-  const int n = wid / (co_blocks * tiles_hw);
+  int cb, st, n;
+  w4_item(wid, co_blocks, tiles_hw, P.ntiles, cb, st, n);
   const int y0 = (st / tiles_w) * BH, x0 = (st % tiles_w) * BW;
   const int co0 = cb * CO;
   const int pitch = P.pitch, hw = H * pitch;
@@ -1678,7 +1699,7 @@ extern "C" int sa_conv2d_k3_wino4_launch(int nprob, const SaWinoProblem *probs, 
     const int tiles_w = (q.W + bw - 1) / bw, tiles_h = (q.H + bh - 1) / bh;
     L.p[i] = W4Prob{q.in, q.in_bs, q.Cin, q.H, q.W, q.U, q.Cout, q.bias, q.relu, q.out, q.out_bs,
                     ltw, tiles_w, tiles_w * tiles_h, q.Cout / CO, q.stats_partial,
-                    q.in_m, q.in_s, q.in_t, q.in_pstride, q.in_act, pitch};
+                    q.in_m, q.in_s, q.in_t, q.in_pstride, q.in_act, pitch, q.N * tiles_w * tiles_h};
     L.gate[i] = W4Gate{};
     if (gates && gates[i].mode != 0) {
       const SaGateEpilogue &e = gates[i];
