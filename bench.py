@@ -407,6 +407,8 @@ def main():
                          "instrumented steps: rocprof per-launch times and PMC bytes comparable with the live ones)")
     ap.add_argument("--miopen-find", type=int, default=0,
                     help="let MIOpen time its conv algorithms per shape (torch cudnn.benchmark)")
+    ap.add_argument("--w4-split-small-cin", type=int, default=None,
+                    help="split F(4x4) launches with every Cin <= this on the 4-wave shape (ops.W4_SPLIT_SMALL_CIN)")
     ap.add_argument("--w4-split", type=int, default=None, choices=[0, 1],
                     help="F(4x4) convs on the split kernel (1) or fp32 MFMA (0); default: ops.W4_SPLIT")
     ap.add_argument("--direct-split", type=int, default=None, choices=[0, 1],
@@ -430,6 +432,8 @@ def main():
         ops._WINO4_MIN_BLOCKS = args.wino4_min_blocks
     if args.w4_split is not None:
         ops.W4_SPLIT = bool(args.w4_split)
+    if args.w4_split_small_cin is not None:
+        ops.W4_SPLIT_SMALL_CIN = args.w4_split_small_cin
     if args.direct_split is not None:
         ops.DIRECT_SPLIT = bool(args.direct_split)
 

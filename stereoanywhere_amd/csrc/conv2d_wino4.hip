@@ -114,7 +114,8 @@ struct W4Cfg {
   static constexpr int UBUF = NPT * KC * CO;                // filters per chunk (dwords)
   static constexpr int BUF = PBUF + UBUF;                   // one buffer: patch, then filters
   static constexpr int OPP = NT * 16 + 4;                   // output staging plane pitch (4 mod 32)
-  static constexpr int SMEM = 2 * BUF > CO * OPP ? 2 * BUF : CO * OPP;
+  // (past the output staging: the flow head's taps and the range guard's per-wave flags)
+  static constexpr int SMEM = 2 * BUF > CO * OPP + CO * 9 + 8 ? 2 * BUF : CO * OPP + CO * 9 + 8;
   static constexpr int PDMA = ((KC * PS_MAX + 63) / 64 + NW - 1) / NW;   // patch DMA pieces per wave
   static constexpr int UDMA = UBUF / 256;                   // filter DMA pieces (1 KiB) per chunk
   static constexpr int UPW = (UDMA + NW - 1) / NW;          // per wave
@@ -164,8 +165,13 @@ static_assert(!W4S_K32 || W4S_KC == 8, "the K = 32 split form takes a lane's two
 // 100-fold over the input patch.
 using W4Split = W4Cfg<8, W4S_KC, 32, false, true>;
 using W4SplitRedo = W4Cfg<8, W4S_KC, 32, false, false, true>;
+// the split products on the 4-wave shape (block_shape 7): 32 tiles, 4-channel chunks, two blocks
+// per CU, so one block's first-chunk wait and epilogue overlap the other's main loop
+using W4SplitSmall = W4Cfg<4, 4, 32, false, true>;
+using W4SplitRedoSmall = W4Cfg<4, 4, 32, false, false, true>;
 constexpr int W4S_LOG2 = 12;
 static_assert(2 * W4Small::SMEM * 4 <= 160 * 1024, "two small blocks per CU");
+static_assert(2 * (W4SplitSmall::SMEM * 4 + W4SplitSmall::AFF_MAX * 8) <= 160 * 1024, "two small split blocks per CU");
 static_assert(W4Wide::SMEM * 4 <= 160 * 1024, "one wide block per CU");
 
 struct W4Prob {
@@ -1339,9 +1345,8 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 || C::CO == 64 ? 1 : 2) void wi
 // split filters read as hi + lo), every block the preceding split launch queued in L.redo (the list
 // holds every block of the launch), then clears the count.  Launched after every guarded split
 // launch on its stream; with nothing queued it reads one word and exits.
-template <bool GATED, bool AFF>
-__global__ __launch_bounds__(W4SplitRedo::NTHR, 1) void wino_f4k3_redo_kernel(const W4Launch L) {
-  using C = W4SplitRedo;
+template <class C, bool GATED, bool AFF>
+__global__ __launch_bounds__(C::NTHR, 1) void wino_f4k3_redo_kernel(const W4Launch L) {
   __shared__ __attribute__((aligned(16))) float smem[C::SMEM];
   __shared__ float2 atab[AFF ? C::AFF_MAX : 1];
   const unsigned n = __atomic_load_n(L.redo, __ATOMIC_RELAXED);
@@ -1659,18 +1664,20 @@ extern "C" int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *pro
 extern "C" int sa_conv2d_k3_wino4_launch(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                                          int block_shape, unsigned *redo_ws, long redo_cap, void *stream) {
   SA_REQUIRE(nprob >= 1 && nprob <= MAX_PROB && probs, "sa_conv2d_k3_wino4_multi: 1..%d problems", MAX_PROB);
-  SA_REQUIRE(block_shape >= 0 && block_shape <= 6, "sa_conv2d_k3_wino4_multi: block_shape 0..6");
+  SA_REQUIRE(block_shape >= 0 && block_shape <= 7, "sa_conv2d_k3_wino4_multi: block_shape 0..7");
   // Large blocks unless the caller asks for small ones (block_shape 2) or wide ones (3: 64
   // output channels per block, filters from sa_conv2d_wino4_weights_cb(..., 64, ...)).  The
   // small shape measured 2-8% faster on standalone launches of Cin <= 128 with a few rounds of
   // blocks (qh08, convc2) but not faster in the forward as a blanket choice.
   // block_shape 4: the quadrant shape (W4Quad), also on the 64-channel filter layout
   // block_shape 6: the split kernel (W4Split; filters from sa_conv2d_wino4_weights_split)
+  // block_shape 7: the split kernel on the 4-wave shape (W4SplitSmall, the same split filters)
   const bool small = block_shape == 2, wide = block_shape == 3, quad = block_shape == 4, persist = block_shape == 5,
-             split = block_shape == 6;
-  const int nt = small || wide || quad ? W4Small::NT : W4Big::NT;
+             split = block_shape == 6, split_small = block_shape == 7;
+  const int nt = small || wide || quad || split_small ? W4Small::NT : W4Big::NT;
   const int CO = wide || quad ? 64 : 32;
-  const int aff_max = small ? W4Small::AFF_MAX : quad ? W4Quad::AFF_MAX : split ? W4Split::AFF_MAX : W4Big::AFF_MAX;
+  const int aff_max = small ? W4Small::AFF_MAX : quad ? W4Quad::AFF_MAX : split ? W4Split::AFF_MAX
+                    : split_small ? W4SplitSmall::AFF_MAX : W4Big::AFF_MAX;
   W4Launch L{};
   long total = 0;
   bool gated = false, aff = false;
@@ -1751,7 +1758,7 @@ extern "C" int sa_conv2d_k3_wino4_launch(int nprob, const SaWinoProblem *probs, 
   SA_REQUIRE(!(aff && gated), "sa_conv2d_k3_wino4: an input transform and a gate epilogue in one launch");
   // the split kernel's range guard: blocks whose operands overflowed queue themselves in redo_ws and
   // the redo kernel recomputes them on fp32 products (the list holds every block of the launch)
-  const bool guard = split && redo_ws;
+  const bool guard = (split || split_small) && redo_ws;
   if (guard) {
     SA_REQUIRE(redo_cap >= total && (reinterpret_cast<uintptr_t>(redo_ws) & 3) == 0,
                "sa_conv2d_k3_wino4: the redo workspace holds %ld entries, the launch has %ld blocks", redo_cap, total);
@@ -1775,9 +1782,17 @@ extern "C" int sa_conv2d_k3_wino4_launch(int nprob, const SaWinoProblem *probs, 
     : gated ? wino_f4k3_kernel<W4Split, true><<<(unsigned)total, W4Split::NTHR, 0, s>>>(L)
             : wino_f4k3_kernel<W4Split, false><<<(unsigned)total, W4Split::NTHR, 0, s>>>(L);
     if (guard)
-      aff     ? wino_f4k3_redo_kernel<false, true><<<1, W4SplitRedo::NTHR, 0, s>>>(L)
-      : gated ? wino_f4k3_redo_kernel<true, false><<<1, W4SplitRedo::NTHR, 0, s>>>(L)
-              : wino_f4k3_redo_kernel<false, false><<<1, W4SplitRedo::NTHR, 0, s>>>(L);
+      aff     ? wino_f4k3_redo_kernel<W4SplitRedo, false, true><<<1, W4SplitRedo::NTHR, 0, s>>>(L)
+      : gated ? wino_f4k3_redo_kernel<W4SplitRedo, true, false><<<1, W4SplitRedo::NTHR, 0, s>>>(L)
+              : wino_f4k3_redo_kernel<W4SplitRedo, false, false><<<1, W4SplitRedo::NTHR, 0, s>>>(L);
+  } else if (split_small) {
+    aff     ? wino_f4k3_kernel<W4SplitSmall, false, true><<<(unsigned)total, W4SplitSmall::NTHR, 0, s>>>(L)
+    : gated ? wino_f4k3_kernel<W4SplitSmall, true><<<(unsigned)total, W4SplitSmall::NTHR, 0, s>>>(L)
+            : wino_f4k3_kernel<W4SplitSmall, false><<<(unsigned)total, W4SplitSmall::NTHR, 0, s>>>(L);
+    if (guard)
+      aff     ? wino_f4k3_redo_kernel<W4SplitRedoSmall, false, true><<<1, W4SplitRedoSmall::NTHR, 0, s>>>(L)
+      : gated ? wino_f4k3_redo_kernel<W4SplitRedoSmall, true, false><<<1, W4SplitRedoSmall::NTHR, 0, s>>>(L)
+              : wino_f4k3_redo_kernel<W4SplitRedoSmall, false, false><<<1, W4SplitRedoSmall::NTHR, 0, s>>>(L);
   }
   else if (quad)
     aff     ? wino_f4k3_kernel<W4Quad, false, true><<<(unsigned)total, W4Quad::NTHR, 0, s>>>(L)

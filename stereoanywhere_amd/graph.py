@@ -39,7 +39,8 @@ class ForwardGraph:
         c_switches = (lib.sa_lookup_get_mfma(), lib.sa_softargmin_get_one_pass(), lib.sa_conv3d_wd_get_variant())
         return (tuple((tuple(x.shape), x.dtype, x.device) for x in xs), iters, dataclasses.astuple(m.opts),
                 m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_WIDE, ops.W4_QUAD, ops.W4_PERSIST, ops.W4_SPLIT,
-                                                   ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS, ops.SPLIT_GUARD), c_switches, args)
+                                                   ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS, ops.SPLIT_GUARD,
+                                                   ops.W4_SPLIT_SMALL_CIN), c_switches, args)
 
     def __call__(self, image2, image3, mde2, mde3, iters: int = 12, test_mode: bool = True):
         if not test_mode:

@@ -805,6 +805,10 @@ W4_QUAD = False
 # f16 x f16 products, fp32 accumulation) instead of fp32 MFMA: 1.06-1.22x per conv, 54.3 -> 60.4
 # pairs/s at configs[1] with EPE vs the reference 1.78e-5 (fp32 MFMA: 1.84e-5)
 W4_SPLIT = True
+# split launches whose problems all have Cin <= this on the 4-wave split shape (block_shape 7:
+# 32 tiles, 4-channel chunks, two blocks per CU, so one block's first-chunk wait and epilogue
+# overlap the other's main loop); 0: off
+W4_SPLIT_SMALL_CIN = 0
 # the split filters need |U * 2^12| < 65504; |U| <= max |weight| for F(4x4,3x3)'s G
 _W4_SPLIT_WMAX = 15.99
 # the direct convs (stems, stride-2 + 1x1) with split products (sa_conv_direct_split), derived
@@ -987,8 +991,8 @@ SPLIT_GUARD = True
 def _wino4_launch(n: int, arr, gates, shape: int, x: torch.Tensor, blocks: int) -> None:
     """sa_conv2d_k3_wino4_launch; the split shape (6) with its range-guard workspace."""
     # (an A/B run's older library, SA_HIP_LIB, may predate the guard's entry point)
-    if shape == 6 and SPLIT_GUARD and hasattr(N.lib(), "sa_conv2d_k3_wino4_launch"):
-        ws = _redo_workspace(x, blocks)
+    if shape in (6, 7) and SPLIT_GUARD and hasattr(N.lib(), "sa_conv2d_k3_wino4_launch"):
+        ws = _redo_workspace(x, 2 * blocks if shape == 7 else blocks)   # (7: half the tiles per block)
         N.call("sa_conv2d_k3_wino4_launch", n, ctypes.addressof(arr), ctypes.addressof(gates), shape, ws.data_ptr(),
                ws.numel() - 1, _stream(x))
     else:
@@ -1042,6 +1046,9 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
         gates = (N.SaGateEpilogue * len(built))(*[_gate_epilogue(p) if p.get("gate") else N.SaGateEpilogue()
                                                   for p in problems])
         shape = (4 if W4_QUAD else 3) if wide else 2 if small_blocks else 5 if persist else 6 if split else 0
+        if (shape == 6 and W4_SPLIT_SMALL_CIN and all(p["x"].shape[1] <= W4_SPLIT_SMALL_CIN for p in plain)
+                and not any(p.get("gate") and p["gate"]["mode"] == 3 for p in problems)):
+            shape = 7
         _wino4_launch(len(built), arr, gates, shape, problems[0]["x"],
                       sum(_wino4_blocks(**p) + 8 for p in plain))
     else:

@@ -55,6 +55,19 @@ def test_end_to_end_vs_reference(model, monkeypatch, name, H, W, D, iters, split
     assert e < 1e-3
 
 
+def test_end_to_end_split_small_shape_vs_reference(model, monkeypatch):
+    """Every split F(4x4) launch that allows it (no flow-head epilogue) on the 4-wave split shape
+    (ops.W4_SPLIT_SMALL_CIN, block_shape 7): the 544x960 / 22-iteration reference fixture."""
+    from stereoanywhere_amd import ops
+    monkeypatch.setattr(ops, "W4_SPLIT_SMALL_CIN", 4096)
+    fix = load_fixture("cfg2_544x960_it22.npz")
+    pair = regenerate_inputs(fix, 1, 544, 960, 192.0)
+    disp = run(model, pair, 22)
+    e = epe(disp, fix["disparity"])
+    print("split small shape EPE", e)
+    assert e < 1e-3
+
+
 def test_wide_input_vs_reference(model):
     """96x1152: W/4 = 288 > 256, the width class of the booster (1120), high_memory (1280) and
     kitti (1344) tiles; the mono pyramid is read from the hourglass layout in 256-wide

@@ -512,6 +512,29 @@ def test_wino4_split_weights_range(monkeypatch):
     assert float((got - ref).abs().max()) < 1e-4 * scale
 
 
+@pytest.mark.parametrize("Cin,Cout,H,W", [(64, 64, 68, 120), (128, 256, 36, 240), (256, 96, 20, 64)])
+def test_wino4_split_small_shape_matches_large(monkeypatch, Cin, Cout, H, W):
+    """The 4-wave split shape (block_shape 7: 32 tiles, 4-channel chunks, two blocks per CU) = the
+    8-wave split shape up to the accumulation order, with bias + ReLU and with an input
+    transform."""
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    monkeypatch.setattr(ops, "W4_SPLIT", True)
+    x = rnd(2, Cin, H, W, seed=Cin + H)
+    w, b = rnd(Cout, Cin, 3, 3, seed=Cout) / (3 * Cin ** 0.5), rnd(Cout, seed=5)
+    aff = ops.Affine(s=rnd(Cin, seed=6).abs() + 0.5, t=rnd(Cin, seed=7))
+    U = ops.wino_weights(w)
+    outs = []
+    for small in (0, 4096):
+        monkeypatch.setattr(ops, "W4_SPLIT_SMALL_CIN", small)
+        (y,), work = _run(monkeypatch, True, dict(x=x, U=U, bias=b, relu=True))
+        (ya,), _ = _run(monkeypatch, True, dict(x=x, U=U, in_aff=aff, in_act="relu"))
+        assert "conv2d_wino4" in work
+        outs.append((y, ya))
+    for a, c in zip(outs[0], outs[1]):
+        scale = float(a.abs().max())
+        assert float((a - c).abs().max()) < 2e-6 * scale
+
+
 def _redo_blocks(reset=True):
     from stereoanywhere_amd import _native as N
     n = int(N.lib().sa_split_redo_blocks(1 if reset else 0))
@@ -519,13 +542,16 @@ def _redo_blocks(reset=True):
     return n
 
 
+@pytest.mark.parametrize("small", [False, True])
 @pytest.mark.parametrize("mag", [300.0, 3000.0, 1e5])
-def test_wino4_split_range_guard(monkeypatch, mag):
+def test_wino4_split_range_guard(monkeypatch, mag, small):
     """Inputs whose transformed values pass the f16 range (|V| up to ~100 x the input): the split
     kernel's range guard recomputes those blocks on fp32 MFMA products inside the launch, so the
     output is finite and equals the fp32-product kernel; in-range blocks stay on the split path.
-    Only part of the image is scaled, so guarded and unguarded blocks share one launch."""
+    Only part of the image is scaled, so guarded and unguarded blocks share one launch.  small: the
+    4-wave split shape (block_shape 7) and its redo kernel."""
     monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    monkeypatch.setattr(ops, "W4_SPLIT_SMALL_CIN", 4096 if small else 0)
     x = rnd(2, 64, 36, 256, seed=3)
     x[0, :, 4:12, 70:90] *= mag   # one region of image 0
     w = rnd(96, 64, 3, 3, seed=4) / 24
@@ -546,17 +572,19 @@ def test_wino4_split_range_guard(monkeypatch, mag):
     # 2 x 36 x 256 at 16 x 64 px per block and 96 / 32 channel blocks: 2 x 3 x 4 x 3 = 72 blocks;
     # the scaled region overflows (|V| >= 65520) from mag ~ 300 on: a few blocks, never all
     if mag >= 3000:
-        assert 0 < redo < 72, redo
+        assert 0 < redo < (144 if small else 72), redo
 
 
-def test_wino4_split_range_guard_gate_and_input_transform(monkeypatch):
+@pytest.mark.parametrize("small", [False, True])
+def test_wino4_split_range_guard_gate_and_input_transform(monkeypatch, small):
     """The guard ahead of the epilogues: a mode-2 gate epilogue updating h IN PLACE, and an
     input-transform launch (the producer's norm on load scaled so the staged values overflow):
     finite, blocks redone, and as close to the float64 result as the fp32-product kernel.  (Winograd
     rounding scales with the largest value of a tile, so outputs of tiles that mix the scaled values
     with unit ones err by ~1e-7 of that value in either kernel: the two are compared through their
-    error against float64, not against each other.)"""
+    error against float64, not against each other.)  small: the 4-wave split shape."""
     monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    monkeypatch.setattr(ops, "W4_SPLIT_SMALL_CIN", 4096 if small else 0)
     B, hd, H, W = 2, 32, 16, 64
     g = torch.Generator(device="cpu").manual_seed(7)
 
