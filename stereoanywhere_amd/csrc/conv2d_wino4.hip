@@ -73,6 +73,12 @@
                        // (1: a tile's channel blocks adjacent).  The 32 blocks an XCD runs at once then share
                        // ~TGRP tiles' patches and ~32 / TGRP channel blocks' filters in its L2
 #endif
+#ifndef SA_W4_PPART
+#define SA_W4_PPART 0  // DMA pieces per part of the spread next-chunk DMA (0: 2, or 3 when a wave has more than 6)
+#endif
+#ifndef SA_W4_UFIRST
+#define SA_W4_UFIRST 0 // 1: a DMA part's filter pieces go out before its patch pieces
+#endif
 #ifndef SA_W4_PRIO
 #define SA_W4_PRIO 1   // s_setprio 1 for the point-half-1 waves (split kernel forward: 66.8 -> 66.5 ms/step, wino4 49.8 -> 49.0 ms, two interleaved passes)
 #endif
@@ -120,7 +126,7 @@ struct W4Cfg {
   static constexpr int UDMA = UBUF / 256;                   // filter DMA pieces (1 KiB) per chunk
   static constexpr int UPW = (UDMA + NW - 1) / NW;          // per wave
   static_assert(SMEM * 4 <= 160 * 1024, "LDS budget");
-  static constexpr int PPART = (PDMA > UPW ? PDMA : UPW) > 6 ? 3 : 2;   // DMA pieces per part
+  static constexpr int PPART = SA_W4_PPART ? SA_W4_PPART : (PDMA > UPW ? PDMA : UPW) > 6 ? 3 : 2;   // DMA pieces per part
   static_assert(PDMA <= 3 * PPART && UPW <= 3 * PPART, "three DMA parts");
   static_assert(OPP % 32 == 4, "conflict-free staging");
   // input (scale, shift) table of an input-transform launch in the LDS left over
@@ -723,15 +729,19 @@ __device__ __forceinline__ void w4_body(const W4Prob &P, const W4Gate *gate, con
   auto issue_part = [&](int chunk, int buf, int part) __attribute__((always_inline)) {
     float *pb = smem + buf * BUF;
     const int xs = chunk * KC * hw * 4;
+    float *ub = pb + PBUF;
+    const int us = u_chunk(chunk);
+    auto pieces_u = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < UPW; ++j)
+        if ((part < 0 || j / C::PPART == part) && wv + NWAVE * j < UDMA)
+          dma16(uin, ub + (wv + NWAVE * j) * 256, u_src(wv + NWAVE * j), us);
+    };
+    if (SA_W4_UFIRST) pieces_u();
 #pragma unroll
     for (int j = 0; j < PDMA; ++j)
       if ((part < 0 || j / C::PPART == part) && wv + NWAVE * j < npi) dma16(xin, pb + (wv + NWAVE * j) * 256, po[j], xs);
-    float *ub = pb + PBUF;
-    const int us = u_chunk(chunk);
-#pragma unroll
-    for (int j = 0; j < UPW; ++j)
-      if ((part < 0 || j / C::PPART == part) && wv + NWAVE * j < UDMA)
-        dma16(uin, ub + (wv + NWAVE * j) * 256, u_src(wv + NWAVE * j), us);
+    if (!SA_W4_UFIRST) pieces_u();
   };
   auto issue = [&](int chunk, int buf) __attribute__((always_inline)) { issue_part(chunk, buf, -1); };
   auto issue_p0 = [&]() __attribute__((always_inline)) {   // chunk 0's patch (its filters went first)
