@@ -407,6 +407,9 @@ def main():
                          "instrumented steps: rocprof per-launch times and PMC bytes comparable with the live ones)")
     ap.add_argument("--miopen-find", type=int, default=0,
                     help="let MIOpen time its conv algorithms per shape (torch cudnn.benchmark)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="graph instances in flight (PipelinedForward): consecutive batches overlap; 1: one "
+                         "forward at a time")
     ap.add_argument("--w4-split-small-cin", type=int, default=None,
                     help="split F(4x4) launches with every Cin <= this on the 4-wave shape (ops.W4_SPLIT_SMALL_CIN)")
     ap.add_argument("--w4-split", type=int, default=None, choices=[0, 1],
@@ -494,8 +497,8 @@ def main():
     if tiled is None and not args.no_graph and not args.one_stream:
         # the timed steps replay the whole forward from a hipGraph (inputs copied into its static
         # buffers each step): one host enqueue per forward instead of ~1.4k kernel launches
-        from stereoanywhere_amd.graph import ForwardGraph
-        runner = ForwardGraph(model)
+        from stereoanywhere_amd.graph import ForwardGraph, PipelinedForward
+        runner = ForwardGraph(model) if args.pipeline <= 1 else PipelinedForward(model, args.pipeline)
 
     def step():
         return runner(*x, iters=iters, test_mode=True)

@@ -71,3 +71,26 @@ class ForwardGraph:
         with torch.cuda.graph(g):
             self._out = self.model(*self._static, iters=iters, test_mode=True)[0]
         self._graph = g
+
+
+class PipelinedForward:
+    """``depth`` ForwardGraph instances (each with its own static buffers and memory pool) replayed
+    round-robin on ``depth`` streams: consecutive forwards of independent batches are in flight
+    together, so one batch's update loop overlaps the next batch's encoders and mono branch.
+    Same results as ForwardGraph; a returned tensor is ready on its instance's stream (synchronise
+    before reading it on another)."""
+
+    def __init__(self, model: torch.nn.Module, depth: int = 2):
+        if depth < 1:
+            raise ValueError("PipelinedForward: depth >= 1")
+        self.graphs = [ForwardGraph(model) for _ in range(depth)]
+        self.streams = [torch.cuda.Stream() for _ in range(depth)]
+        self._i = 0
+
+    def __call__(self, image2, image3, mde2, mde3, iters: int = 12, test_mode: bool = True):
+        i = self._i
+        self._i = (i + 1) % len(self.graphs)
+        s = self.streams[i]
+        s.wait_stream(torch.cuda.current_stream())   # the inputs (and anything else queued before)
+        with torch.cuda.stream(s):
+            return self.graphs[i](image2, image3, mde2, mde3, iters=iters, test_mode=test_mode)
