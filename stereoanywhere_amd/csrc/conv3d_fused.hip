@@ -39,9 +39,6 @@ constexpr int TW = 64;  // pointwise tiles along W
 constexpr int TH = 4;   // along H
 constexpr int TD = 4;   // output planes per thread along D
 constexpr int ROW = 64; // LDS row pitch (floats)
-#ifndef UPCAT_NDT
-#define UPCAT_NDT 4     // up-cat pointwise: D-tiles per block
-#endif
 
 struct InXform {
   const float *mean, *rstd;   // per (b, ci), or null
@@ -729,17 +726,8 @@ __global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__res
   const int ty = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // one H row per wave
   const int w0 = blockIdx.x * TWV, h0 = blockIdx.y * TH;
   const int w = w0 + tx_, h = h0 + ty;
-  const int b = blockIdx.z / tilesD;
+  const int b = blockIdx.z / tilesD, d0 = (blockIdx.z % tilesD) * TD;
   const long vol = (long)D * H * W;
-  float s[COUT], q[COUT];
-#pragma unroll
-  for (int c = 0; c < COUT; ++c) s[c] = q[c] = 0.0f;
-  // UPCAT_NDT D-tiles of TD planes per block, one statistics reduction at the end (the block
-  // statistics were ~30% of the instructions of a one-tile block)
-  for (int dt = 0; dt < UPCAT_NDT; ++dt) {
-  const int d0 = ((blockIdx.z % tilesD) * UPCAT_NDT + dt) * TD;
-  if (d0 >= D) break;
-  if (dt) __syncthreads();   // every thread's reads of the previous tile's footprint are done
   // upsample_trilinear3d(align_corners=True): source index floor(s * dst), monotone in dst
   const int dlo = (int)(sd * (float)d0), hlo = (int)(sh * (float)h0), wlo = (int)(sw * (float)w0);
   {
@@ -753,6 +741,9 @@ __global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__res
     }
   }
   __syncthreads();
+  float s[COUT], q[COUT];
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) s[c] = q[c] = 0.0f;
   const bool col_ok = tx_ < TWV && w < W && h < H;
   const int wc = min(w, W - 1), hc = min(h, H - 1);
   // Wa . Ta(a): all TD planes of this (h, w) column per input channel
@@ -850,7 +841,6 @@ __global__ __launch_bounds__(256) void pointwise_upcat_kernel(const float *__res
       }
     }
   }
-  }
   const int nparts = gridDim.x * gridDim.y * tilesD;
   const int blk = (blockIdx.z % tilesD) * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x;
   block_stats<COUT>(s, q, red, partial, b, nparts, blk, COUT);
@@ -918,9 +908,9 @@ inline dim3 conv_grid(int B, int Do, int Ho, int Wo, ConvGeo g, int &tilesD) {
   return dim3((Wo + g.valid_w() - 1) / g.valid_w(), (Ho + g.th - 1) / g.th, tilesD * B);
 }
 
-// up-cat pointwise tiles: UPCAT_NDT x TD x TH x TW, aligned, no halo
+// up-cat pointwise tiles: TD x TH x TW, aligned, no halo
 inline dim3 upcat_grid(int B, int D, int H, int W, int &tilesD) {
-  tilesD = (D + TD * UPCAT_NDT - 1) / (TD * UPCAT_NDT);
+  tilesD = (D + TD - 1) / TD;
   return dim3((W + TW - 1) / TW, (H + TH - 1) / TH, tilesD * B);
 }
 
