@@ -2,6 +2,7 @@
 """Throughput of the MI355X StereoAnywhere forward on synthetic 540x960 pairs.
 
     python bench.py [--gpus N --steps K --warmup W] [--config cfg2|cfg4|cfg3|cfg5]
+        (N > 1 without torchrun: bench.py starts the N ranks itself, one child process per GPU)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -387,6 +388,35 @@ TILED = {
 }
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def self_launch(gpus: int):
+    """``--gpus N`` (N > 1) outside torchrun: start N child ranks of this same command, one per GPU
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), wait for all of them and return
+    the first non-zero exit status (0 when every rank succeeded).  None: nothing to launch (N = 1, or
+    already a rank of a torchrun / self-launched world).  The parent touches no GPU: the children are
+    fresh interpreters started before any HIP call (no exec from a GPU process)."""
+    if gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import subprocess
+    port = _free_port()
+    procs = []
+    for rank in range(gpus):
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(gpus),
+                   LOCAL_WORLD_SIZE=str(gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [c for c in rcs if c != 0]
+    if bad:
+        print(f"bench: rank exit codes {rcs}", file=sys.stderr)
+    return bad[0] if bad else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -426,7 +456,30 @@ def main():
                          "timed beside it)")
     ap.add_argument("--wino4-min-blocks", type=int, default=None,
                     help="F(4x4) for launches of at least this many blocks (default: ops._WINO4_MIN_BLOCKS)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rendezvous only: every rank joins the process group and rank 0 prints the ranks that "
+                         "reported (checks the multi-rank launch without a model or a GPU)")
     args = ap.parse_args()
+    # --gpus N > 1 without a torchrun environment: this process becomes the launcher of N ranks
+    # (before anything touches the GPU); under torchrun the world size must match --gpus
+    rc = self_launch(args.gpus)
+    if rc is not None:
+        raise SystemExit(rc)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE {world_env}: the line would report "
+                         f"{world_env} GPU(s); launch with --nproc-per-node {args.gpus} (or without torchrun)")
+    if args.dry_run:
+        r = D.init_from_env(os.environ.get("SA_DIST_BACKEND", "nccl"))
+        if os.environ.get("SA_DIST_BACKEND", "nccl") == "nccl":
+            torch.cuda.set_device(r.local_rank)
+        dev = torch.device("cuda", r.local_rank) if os.environ.get("SA_DIST_BACKEND", "nccl") == "nccl" else None
+        got = D.gather_metrics(torch.tensor([[float(r.rank), float(r.world)]], dtype=torch.float64, device=dev), r)
+        D.barrier(r)
+        if r.is_main:
+            print(json.dumps({"dry_run": True, "n_gpus": r.world, "ranks": [int(v) for v in got[:, 0].tolist()],
+                              "worlds": sorted({int(v) for v in got[:, 1].tolist()})}))
+        return
     if args.split_guard is not None:
         ops.SPLIT_GUARD = bool(args.split_guard)
     if args.batch is None:
@@ -447,8 +500,6 @@ def main():
     ngpu = torch.cuda.device_count()
     device = torch.device("cuda", r.local_rank % ngpu if os.environ.get("SA_DIST_SHARE_GPU") == "1" else r.local_rank)
     torch.cuda.set_device(device)
-    if r.world != args.gpus and r.is_main:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {r.world}", file=sys.stderr)
 
     model = StereoAnywhere(dict(PUBLISHED)).eval()
     synth.load_seeded_weights(model, 0)
@@ -646,21 +697,25 @@ def main():
         secs = ms_tot / 1e3 / args.steps                      # per step
         if unit == "TFLOP/s":
             ach, peak, bound = amount / secs / 1e12, FP32_MFMA_PEAK_TFS, "mfma"
-            if (k == "conv2d_wino4" and ops.W4_SPLIT) or (k == "conv2d_direct" and ops.DIRECT_SPLIT):
-                # the split kernel's products: v_mfma_f32_16x16x16_f16 (16 cycles per SIMD) carries
-                # one 16x16x4 fp32 MFMA's products as hi/lo pairs (32 cycles): twice the fp32 rate
-                peak = SPLIT_MFMA_PEAK_TFS
+            split4 = (k == "conv2d_wino4" and ops.W4_SPLIT) or (k == "conv2d_direct" and ops.DIRECT_SPLIT)
+            if k == "conv2d_igemm":
+                # the implicit-GEMM conv issues three f16 MFMA products per fp32 product (hi*hi +
+                # hi*lo + lo*hi): its rate is the issued f16 flops against the guide's F16 dense peak
+                ach, peak = 3 * ach, F16_DENSE_PEAK_TFS
         else:
             ach, peak, bound = amount / secs / 1e9, HBM_PEAK_GBS, "hbm"
+            split4 = False
         kernels[k] = {"bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
                       "ms_per_step": ms_tot / args.steps, "launches_per_step": n_launch / args.steps,
                       "avg_launch_us": ms_tot * 1e3 / n_launch}
-        if peak == SPLIT_MFMA_PEAK_TFS:
-            # the same rate against the guide's peaks: the path's arithmetic type (fp32 products,
-            # 157.3 TF/s) and the f16 MFMA flops the kernel issues (4 f16 products per fp32 one)
-            # against the F16 dense peak (~2.5 PF)
-            kernels[k].update(frac_fp32_peak=ach / FP32_MFMA_PEAK_TFS, f16_issued_tflops=4 * ach,
-                              frac_f16_dense_peak=4 * ach / F16_DENSE_PEAK_TFS)
+        if split4:
+            # the split kernels' fp32 products (path type, peak 157.3 TF/s from the guide) also against
+            # the 16x16x16 f16 form's fp32-product rate (2x, self-derived) and as issued f16 flops (4
+            # f16 products per fp32 one) against the F16 dense peak (~2.5 PF)
+            kernels[k].update(split_peak=SPLIT_MFMA_PEAK_TFS, frac_split_peak=ach / SPLIT_MFMA_PEAK_TFS,
+                              f16_issued_tflops=4 * ach, frac_f16_dense_peak=4 * ach / F16_DENSE_PEAK_TFS)
+        if k == "conv2d_igemm":
+            kernels[k].update(fp32_product_tflops=ach / 3, direct_conv_tflops=ach / 3)
     dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
     roof = dict(kernels[dom])
     roof.update({"kernel": dom, "traffic": pmc_traffic(dom, args.batch) if tiled is None else None,
@@ -683,9 +738,13 @@ def main():
                          "(16/36 resp. 36/144 of the direct convolution's), so their direct-equivalent "
                          "rates are 2.25x resp. 4x achieved"
                          + ("; conv2d_wino4 / conv2d_direct run the split kernels (ops.W4_SPLIT, "
-                            "ops.DIRECT_SPLIT): their peak is the fp32-product rate of "
-                            "v_mfma_f32_16x16x16_f16 on hi/lo pairs, 2x the fp32 MFMA peak"
-                            if ops.W4_SPLIT or ops.DIRECT_SPLIT else "")})
+                            "ops.DIRECT_SPLIT): achieved = their fp32 products (exact f16 hi/lo pair "
+                            "products) against the guide's fp32 matrix peak 157.3 TF/s; split_peak "
+                            "(2x, the 16x16x16 f16 form) and the issued f16 flops vs the F16 dense peak "
+                            "are side fields" if ops.W4_SPLIT or ops.DIRECT_SPLIT else "")
+                         + "; conv2d_igemm (the implicit-GEMM 3x3 conv on 16x16x32 f16 MFMA) issues 3 "
+                           "f16 products per fp32 product: achieved = those issued flops vs the guide's "
+                           "F16 dense peak 2.5 PF (direct_conv_tflops = the fp32 products' rate)"})
     if tiled is None:
         metric, unit = "stereo pairs/sec @540x960 D=192 (1/2/4/8 GPU) + EPE vs reference", "pairs/s"
         if args.config == "cfg4":

@@ -462,6 +462,27 @@ int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const S
  * never carry the overflow.  redo_ws NULL: no guard.  Other block shapes ignore redo_ws. */
 int sa_conv2d_k3_wino4_launch(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                               int block_shape, unsigned *redo_ws, long redo_cap, void *stream);
+/* The same 3x3 / pad 1 convolutions as an implicit GEMM on v_mfma_f32_16x16x32_f16 with split
+ * operands (conv2d_igemm.hip): each product is hi*hi + hi*lo + lo*hi of f16 pairs (22-bit operands,
+ * exact products, fp32 accumulation).  sa_conv2d_igemm_weights arranges [Cout][Cin][3][3] (Cout %
+ * 128 == 0, Cin % 32 == 0) once as sa_conv2d_igemm_weights_size(Cout, Cin) dwords (16-byte
+ * aligned).  sa_conv2d_k3_igemm takes SaWinoProblem with U = those weights (any W; the row pitch %
+ * 4 == 0, 16-byte aligned outputs), the bias, ReLU, input transform (Cin <= 512) and InstanceNorm
+ * partials ([N*Cout][parts][2], parts = sa_conv2d_igemm_stat_parts(H, W)) of sa_conv2d_k3_wino_ex and
+ * the gate epilogues 1 / 2 of sa_conv2d_k3_wino4_multi_gate (mode 1 needs Cout % 256 == 0).
+ * Range guard: a block with an input (after its transform) outside the f16 range or not finite
+ * writes nothing and queues itself in redo_ws ([0] = count, zero-initialised, redo_cap >= the
+ * launch's blocks, left zeroed again by the fp32 redo kernel launched right after).  redo_ws NULL:
+ * no guard.  sa_conv2d_igemm_blocks: the workgroups of one problem. */
+long sa_conv2d_igemm_weights_size(int Cout, int Cin);
+int sa_conv2d_igemm_weights(const float *weight, int Cout, int Cin, void *out, void *stream);
+long sa_conv2d_igemm_stat_parts(int H, int W);
+long sa_conv2d_igemm_blocks(int N, int Cout, int H, int W);
+int sa_conv2d_k3_igemm(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates, unsigned *redo_ws,
+                       long redo_cap, void *stream);
+/* blocks the implicit-GEMM kernel's range guard recomputed in fp32 since the last reset (reset != 0
+ * clears), -1 on error; synchronises the device. */
+long sa_igemm_redo_blocks(int reset);
 /* Blocks of the split kernels (F(4x4) and sa_conv_direct_split) that the range guards recomputed on
  * fp32 MFMA since the last reset (reset != 0 clears the count), -1 on error; synchronises the
  * device. */
@@ -520,7 +541,8 @@ int sa_norm_act(const float *x, long x_bs, int B, int C, long hw, const float *m
 enum {
   SA_K_CORR_PYRAMID = 0, SA_K_LOOKUP, SA_K_MONO_VOLUME, SA_K_SOFTARGMIN, SA_K_LSQ,
   SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_NORM, SA_K_CONV2D, SA_K_CONV_DIRECT,
-  SA_K_CONV2D_W4, SA_K_SHEAR, SA_K_MONO_PYRAMID, SA_K_PLUMBING, SA_K_CONV_SMALL, SA_K_NARROW, SA_K_COUNT
+  SA_K_CONV2D_W4, SA_K_SHEAR, SA_K_MONO_PYRAMID, SA_K_PLUMBING, SA_K_CONV_SMALL, SA_K_NARROW, SA_K_CONV2D_IG,
+  SA_K_COUNT
 };
 /* Box-state probe (bench.py, outside timed regions; synchronises the device): `blocks` blocks of 4
  * waves run `iters` x 4 chained f16 MFMAs each; *mhz = the median over waves of the in-kernel shader

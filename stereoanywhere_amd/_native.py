@@ -103,6 +103,12 @@ SIGNATURES = {
     "sa_conv2d_k3_wino4_stat_parts": (L, [I, I]),
     "sa_conv2d_k3_wino4_multi": (I, [I, P, P]),
     "sa_conv2d_k3_wino4_multi_gate": (I, [I, P, P, I, P]),
+    "sa_conv2d_igemm_weights_size": (L, [I, I]),
+    "sa_conv2d_igemm_weights": (I, [P, I, I, P, P]),
+    "sa_conv2d_igemm_stat_parts": (L, [I, I]),
+    "sa_conv2d_igemm_blocks": (L, [I, I, I, I]),
+    "sa_conv2d_k3_igemm": (I, [I, P, P, P, L, P]),
+    "sa_igemm_redo_blocks": (L, [I]),
     "sa_conv_direct_weights": (I, [P, I, I, I, I, I, P, P]),
     "sa_conv_direct_weights_size": (L, [I, I, I, I, I]),
     "sa_conv_direct_weights_split": (I, [P, L, P, P]),
@@ -133,7 +139,7 @@ KERNEL_IDS = {
     "corr_volume_pyramid": 0, "corr_lookup": 1, "mono_masked_volume": 2, "softargmin_conf": 3,
     "weighted_lsq": 4, "gru_zr": 5, "gru_out": 6, "convex_upsample": 7, "misc": 8, "conv3d_fused": 9,
     "norm_act": 10, "conv2d_wino": 11, "conv2d_direct": 12, "conv2d_wino4": 13, "corr_shear": 14,
-    "mono_pyramid": 15, "gru_plumbing": 16, "conv2d_small": 17, "conv2d_narrow": 18,
+    "mono_pyramid": 15, "gru_plumbing": 16, "conv2d_small": 17, "conv2d_narrow": 18, "conv2d_igemm": 19,
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -19,12 +19,20 @@ class ForwardGraph:
     """Callable like StereoAnywhere.forward(image2, image3, mde2, mde3, iters, test_mode=True);
     returns (flow_up, None) with flow_up a fresh tensor (the graph's output buffer is reused)."""
 
+    _instances = 0
+
     def __init__(self, model: torch.nn.Module):
         self.model = model
         self._key = None
         self._graph: Optional[torch.cuda.CUDAGraph] = None
         self._static = None
         self._out = None
+        # this instance's capture stream and workspace scope: the split kernels' range-guard
+        # workspaces (ops._redo_workspace) baked into this graph are its own, so two instances
+        # replayed at the same time (PipelinedForward) never share a redo list
+        ForwardGraph._instances += 1
+        self._scope = ("graph", ForwardGraph._instances)
+        self._cap_stream: Optional[torch.cuda.Stream] = None
 
     def _make_key(self, xs, iters):
         m = self.model
@@ -36,7 +44,9 @@ class ForwardGraph:
         # model's flags
         args = tuple(sorted((k, repr(v)) for k, v in vars(m.args).items()))
         lib = N.lib()
-        c_switches = (lib.sa_lookup_get_mfma(), lib.sa_softargmin_get_one_pass(), lib.sa_conv3d_wd_get_variant())
+        # (an A/B run's older library, SA_HIP_LIB, may lack a getter: its switch reads as None)
+        c_switches = tuple(getattr(lib, name)() if hasattr(lib, name) else None
+                           for name in ("sa_lookup_get_mfma", "sa_softargmin_get_one_pass", "sa_conv3d_wd_get_variant"))
         return (tuple((tuple(x.shape), x.dtype, x.device) for x in xs), iters, dataclasses.astuple(m.opts),
                 m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_WIDE, ops.W4_QUAD, ops.W4_PERSIST, ops.W4_SPLIT,
                                                    ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS, ops.SPLIT_GUARD,
@@ -68,8 +78,15 @@ class ForwardGraph:
             self.model(*self._static, iters=iters, test_mode=True)
         cur.wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._out = self.model(*self._static, iters=iters, test_mode=True)[0]
+        if self._cap_stream is None:
+            self._cap_stream = torch.cuda.Stream()
+        from . import ops
+        prev, ops._REDO_SCOPE = ops._REDO_SCOPE, self._scope
+        try:
+            with torch.cuda.graph(g, stream=self._cap_stream):
+                self._out = self.model(*self._static, iters=iters, test_mode=True)[0]
+        finally:
+            ops._REDO_SCOPE = prev
         self._graph = g
 
 

@@ -970,11 +970,14 @@ def _gate_epilogue(p: dict) -> "N.SaGateEpilogue":
 # still name them
 _REDO_WS: dict = {}
 _REDO_OLD: list = []
+# set by graph.ForwardGraph while it captures: each graph instance bakes its own workspaces, so
+# graphs replayed concurrently on other streams (PipelinedForward) never share a redo list
+_REDO_SCOPE = None
 
 
 def _redo_workspace(x: torch.Tensor, blocks: int) -> torch.Tensor:
     st = torch.cuda.current_stream(x.device)
-    key = (x.device.index, st.cuda_stream)
+    key = (x.device.index, st.cuda_stream, _REDO_SCOPE)
     ws = _REDO_WS.get(key)
     if ws is None or ws.numel() < 1 + blocks:
         if ws is not None:

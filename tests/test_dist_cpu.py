@@ -128,3 +128,47 @@ def test_harness_and_tiles_sharded_equal_single_rank(world):
                                                                                           test_mode=True).numpy()
     for _, _, st in res:
         np.testing.assert_allclose(st, st1, rtol=1e-6, atol=1e-6)
+
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, extra_env=None, timeout=240):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env["SA_DIST_BACKEND"] = "gloo"
+    env.update(extra_env or {})
+    return subprocess.run([sys.executable, os.path.join(_ROOT, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launches_its_own_ranks(world):
+    """bench.py --gpus N outside torchrun starts N ranks itself (one child per GPU): every rank joins
+    the process group and reports world == N (the --dry-run rendezvous, gloo on the CPU)."""
+    import json
+    res = _bench(["--gpus", str(world), "--dry-run"])
+    assert res.returncode == 0, res.stderr
+    line = json.loads([ln for ln in res.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == world
+    assert line["ranks"] == list(range(world))
+    assert line["worlds"] == [world]
+
+
+def test_bench_world_size_mismatch_fails():
+    """Under a torchrun environment whose WORLD_SIZE differs from --gpus, bench.py exits non-zero
+    instead of reporting a line for the wrong GPU count."""
+    res = _bench(["--gpus", "4", "--dry-run"], dict(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0",
+                                                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port())))
+    assert res.returncode != 0
+    assert "WORLD_SIZE 2" in res.stderr
+
+
+def test_bench_failing_rank_fails_the_launch():
+    """Ranks that fail (here: a process-group backend that does not exist, seen only by the children:
+    the launcher itself joins no group) make the launcher exit non-zero."""
+    res = _bench(["--gpus", "2", "--dry-run"], dict(SA_DIST_BACKEND="no_such_backend"))
+    assert res.returncode != 0
+    assert "rank exit codes" in res.stderr
