@@ -440,8 +440,12 @@ def main():
     ap.add_argument("--pipeline", type=int, default=1,
                     help="graph instances in flight (PipelinedForward): consecutive batches overlap; 1: one "
                          "forward at a time")
-    ap.add_argument("--w4-split-small-cin", type=int, default=None,
-                    help="split F(4x4) launches with every Cin <= this on the 4-wave shape (ops.W4_SPLIT_SMALL_CIN)")
+    ap.add_argument("--igemm", type=int, default=None, choices=[0, 1],
+                    help="3x3 convs on the implicit-GEMM kernel where it applies (1) or on the Winograd kernels "
+                         "only (0); default: ops.IGEMM")
+    ap.add_argument("--igemm-max-work", type=int, default=None,
+                    help="implicit GEMM only for launches of at most this many output pixels x channels "
+                         "(ops.IGEMM_MAX_WORK)")
     ap.add_argument("--w4-split", type=int, default=None, choices=[0, 1],
                     help="F(4x4) convs on the split kernel (1) or fp32 MFMA (0); default: ops.W4_SPLIT")
     ap.add_argument("--direct-split", type=int, default=None, choices=[0, 1],
@@ -488,8 +492,10 @@ def main():
         ops._WINO4_MIN_BLOCKS = args.wino4_min_blocks
     if args.w4_split is not None:
         ops.W4_SPLIT = bool(args.w4_split)
-    if args.w4_split_small_cin is not None:
-        ops.W4_SPLIT_SMALL_CIN = args.w4_split_small_cin
+    if args.igemm is not None:
+        ops.IGEMM = bool(args.igemm)
+    if args.igemm_max_work is not None:
+        ops.IGEMM_MAX_WORK = args.igemm_max_work
     if args.direct_split is not None:
         ops.DIRECT_SPLIT = bool(args.direct_split)
 
@@ -677,6 +683,7 @@ def main():
     costs = step_costs(shape[0], shape[1], shape[2], iters)
     costs["conv2d_wino"] = ("TFLOP/s", work.get("conv2d_wino", 0.0))
     costs["conv2d_wino4"] = ("TFLOP/s", work.get("conv2d_wino4", 0.0))
+    costs["conv2d_igemm"] = ("TFLOP/s", work.get("conv2d_igemm", 0.0))
     costs["conv2d_direct"] = ("TFLOP/s", work.get("conv2d_direct", 0.0))
     costs["norm_act"] = ("GB/s", work.get("norm_act", 0.0))
     # the separate GRU gate kernels run only at levels whose width keeps the gates out of the
@@ -773,6 +780,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": ("f32 (" + " and ".join(n for n, on in (("F(4x4) Winograd-domain", ops.W4_SPLIT),
+                                                         ("implicit-GEMM 3x3", ops.IGEMM),
                                                          ("direct-conv", ops.DIRECT_SPLIT)) if on)
                   + " products as exact f16 hi/lo pair products on MFMA, fp32 accumulation; everything else "
                   "fp32)" if ops.W4_SPLIT or ops.DIRECT_SPLIT else "f32"), "data": "synthetic (seeded value-noise pairs, "

@@ -398,15 +398,9 @@ int sa_conv2d_k3_wino_multi(int nprob, const SaWinoProblem *probs, void *stream)
  * (16-byte aligned).  sa_conv2d_k3_wino4_multi takes SaWinoProblem with U = U4 and needs
  * W % 4 == 0 and 16-byte aligned input planes (in, in_bs % 4 == 0); an input transform
  * (in_m / in_s / in_t / in_pstride, in_act 0 or 1 = ReLU, as sa_conv2d_k3_wino_ex) needs
- * Cin <= 256 (block_shape 0) or 512 (2), no gate epilogue in the launch and not the wide
- * shape; bias, ReLU and the InstanceNorm partials
+ * Cin <= 256 (block_shape 0) or 512 (2) and no gate epilogue in the launch; bias, ReLU and the InstanceNorm partials
  * ([N*Cout][parts][2], parts = sa_conv2d_k3_wino4_stat_parts(H, W)) as sa_conv2d_k3_wino_ex. */
 int sa_conv2d_wino4_weights(const float *weight, int Cout, int Cin, float *U4, void *stream);
-/* U4 for the wide block shape (block_shape 3 of sa_conv2d_k3_wino4_multi_gate: 64 output
- * channels per block): co_block 64 lays the filters out [Cout/64][Cin/8][36][2][4][16][4]
- * (Cout % 64 == 0); co_block 32 is sa_conv2d_wino4_weights. */
-int sa_conv2d_wino4_weights_cb(const float *weight, int Cout, int Cin, int co_block, float *U4,
-                               void *stream);
 /* U4 for the split block shape (block_shape 6 of sa_conv2d_k3_wino4_multi_gate: the Winograd-domain
  * products on f16 MFMA with hi/lo operand pairs): 36*Cin*Cout dwords in U4's layout, each dword
  * the f16 pair (hi, lo) of U * 2^12 (hi in the low half).  Needs |weight| < 16 (U * 2^12
@@ -444,47 +438,40 @@ typedef struct SaGateEpilogue {
   long head_part_bs;
 } SaGateEpilogue;
 /* block_shape: 0 / 1 large blocks (8 waves, 64 Winograd tiles, one per CU), 2 small blocks (4
- * waves, 32 tiles, two per CU: shorter launches of few rounds fill the chip better), 3 wide
- * blocks (4 waves, 32 tiles x 64 output channels, one per CU; every problem's U from
- * sa_conv2d_wino4_weights_cb(..., 64, ...), Cout % 64 == 0, and Cout % 128 == 0 with a z/r gate),
- * 4 quadrant blocks (8 waves, 32 tiles x 64 output channels, the 64-channel U), 5 persistent large
- * blocks (the large shape, one block per CU walking the launch's work items; each item prefetches
- * the next item's first input-channel chunk under its own epilogue), 6 split large blocks (8 waves,
- * 64 tiles x 32 output channels, 4-channel chunks; every problem's U from
- * sa_conv2d_wino4_weights_split; the transformed inputs must stay below 65504 in magnitude). */
+ * waves, 32 tiles, two per CU: shorter launches of few rounds fill the chip better), 6 split large
+ * blocks (8 waves, 64 tiles x 32 output channels; every problem's U from
+ * sa_conv2d_wino4_weights_split; the transformed inputs must stay below 65504 in magnitude, see the
+ * guard of sa_conv2d_k3_wino4_launch).  Any other value is an error. */
 int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                                   int block_shape, void *stream);
-/* sa_conv2d_k3_wino4_multi_gate with the split kernel's range guard (block_shape 6): a block whose
- * f16 operands overflowed (|transformed input| >= 65520) writes nothing and queues itself in
- * redo_ws ([0] = count, then one entry per queued block; zero-initialised, redo_cap >= the launch's
- * blocks, left zeroed again), and a one-workgroup kernel launched right after on the same stream
- * recomputes those blocks on fp32 MFMA products (the split filters read as hi + lo), so results
- * never carry the overflow.  redo_ws NULL: no guard.  Other block shapes ignore redo_ws. */
+/* sa_conv2d_k3_wino4_multi_gate with the split kernel's range guard (block_shape 6, guard != 0): a
+ * block whose f16 operands overflowed (|transformed input| >= 65520, or an input not finite) writes
+ * nothing and recomputes its work item right away on fp32 MFMA products (the split filters read as
+ * hi + lo), so results never carry the overflow; every such block in parallel, no second launch.
+ * sa_split_redo_blocks counts them.  Other block shapes ignore guard. */
 int sa_conv2d_k3_wino4_launch(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
-                              int block_shape, unsigned *redo_ws, long redo_cap, void *stream);
+                              int block_shape, int guard, void *stream);
 /* The same 3x3 / pad 1 convolutions as an implicit GEMM on v_mfma_f32_16x16x32_f16 with split
  * operands (conv2d_igemm.hip): each product is hi*hi + hi*lo + lo*hi of f16 pairs (22-bit operands,
  * exact products, fp32 accumulation).  sa_conv2d_igemm_weights arranges [Cout][Cin][3][3] (Cout %
- * 128 == 0, Cin % 32 == 0) once as sa_conv2d_igemm_weights_size(Cout, Cin) dwords (16-byte
- * aligned).  sa_conv2d_k3_igemm takes SaWinoProblem with U = those weights (any W; the row pitch %
- * 4 == 0, 16-byte aligned outputs), the bias, ReLU, input transform (Cin <= 512) and InstanceNorm
- * partials ([N*Cout][parts][2], parts = sa_conv2d_igemm_stat_parts(H, W)) of sa_conv2d_k3_wino_ex and
- * the gate epilogues 1 / 2 of sa_conv2d_k3_wino4_multi_gate (mode 1 needs Cout % 256 == 0).
- * Range guard: a block with an input (after its transform) outside the f16 range or not finite
- * writes nothing and queues itself in redo_ws ([0] = count, zero-initialised, redo_cap >= the
- * launch's blocks, left zeroed again by the fp32 redo kernel launched right after).  redo_ws NULL:
- * no guard.  sa_conv2d_igemm_blocks: the workgroups of one problem. */
+ * 128 == 0, Cin % 32 == 0, |weight| < 16) once as sa_conv2d_igemm_weights_size(Cout, Cin) dwords
+ * (16-byte aligned).  sa_conv2d_k3_igemm takes SaWinoProblem with U = those weights (any W; the
+ * row pitch % 4 == 0, 16-byte aligned outputs), the bias, ReLU, input transform (Cin <= 512) and
+ * InstanceNorm partials ([N*Cout][parts][2], parts = sa_conv2d_igemm_stat_parts(H, W)) of
+ * sa_conv2d_k3_wino_ex and the gate epilogues 1 / 2 of sa_conv2d_k3_wino4_multi_gate (mode 1 needs
+ * Cout % 256 == 0).  Range guard (guard != 0): a block with a finite input (after its transform)
+ * of magnitude >= 65504 writes nothing and recomputes its work item with its inputs scaled by a
+ * power of two that brings them into the f16 range (exact; the accumulators scaled back), counted
+ * by sa_split_redo_blocks; inputs that are not finite give NaN outputs.
+ * sa_conv2d_igemm_blocks: the workgroups of one problem. */
 long sa_conv2d_igemm_weights_size(int Cout, int Cin);
 int sa_conv2d_igemm_weights(const float *weight, int Cout, int Cin, void *out, void *stream);
 long sa_conv2d_igemm_stat_parts(int H, int W);
 long sa_conv2d_igemm_blocks(int N, int Cout, int H, int W);
-int sa_conv2d_k3_igemm(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates, unsigned *redo_ws,
-                       long redo_cap, void *stream);
-/* blocks the implicit-GEMM kernel's range guard recomputed in fp32 since the last reset (reset != 0
- * clears), -1 on error; synchronises the device. */
-long sa_igemm_redo_blocks(int reset);
-/* Blocks of the split kernels (F(4x4) and sa_conv_direct_split) that the range guards recomputed on
- * fp32 MFMA since the last reset (reset != 0 clears the count), -1 on error; synchronises the
+int sa_conv2d_k3_igemm(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates, int guard,
+                       void *stream);
+/* Blocks of the split kernels (F(4x4), the implicit GEMM and sa_conv_direct_split) that the range
+ * guards recomputed since the last reset (reset != 0 clears the count), -1 on error; synchronises the
  * device. */
 long sa_split_redo_blocks(int reset);
 /* The flow head fused (gate mode 3 above): floats of the partial-sum buffer of a conv over

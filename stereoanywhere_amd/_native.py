@@ -69,7 +69,7 @@ SIGNATURES = {
     "sa_softargmin_set_one_pass": (None, [I]),
     "sa_softargmin_get_one_pass": (I, []),
     "sa_split_redo_blocks": (L, [I]),
-    "sa_conv2d_k3_wino4_launch": (I, [I, P, P, I, P, L, P]),
+    "sa_conv2d_k3_wino4_launch": (I, [I, P, P, I, I, P]),
     "sa_flow_head_part_size": (L, [I, I, I, I]),
     "sa_clock_probe": (I, [I, I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "sa_flow_head_reduce": (I, [P, I, I, I, I, P, P, P, L, P, L, P]),
@@ -98,7 +98,6 @@ SIGNATURES = {
     "sa_conv2d_k3_wino_ex": (I, [P, L, I, I, I, I, P, I, P, I, P, P, P, I, I, P, L, P, P]),
     "sa_conv2d_k3_wino_multi": (I, [I, P, P]),
     "sa_conv2d_wino4_weights": (I, [P, I, I, P, P]),
-    "sa_conv2d_wino4_weights_cb": (I, [P, I, I, I, P, P]),
     "sa_conv2d_wino4_weights_split": (I, [P, I, I, P, P]),
     "sa_conv2d_k3_wino4_stat_parts": (L, [I, I]),
     "sa_conv2d_k3_wino4_multi": (I, [I, P, P]),
@@ -107,8 +106,7 @@ SIGNATURES = {
     "sa_conv2d_igemm_weights": (I, [P, I, I, P, P]),
     "sa_conv2d_igemm_stat_parts": (L, [I, I]),
     "sa_conv2d_igemm_blocks": (L, [I, I, I, I]),
-    "sa_conv2d_k3_igemm": (I, [I, P, P, P, L, P]),
-    "sa_igemm_redo_blocks": (L, [I]),
+    "sa_conv2d_k3_igemm": (I, [I, P, P, I, P]),
     "sa_conv_direct_weights": (I, [P, I, I, I, I, I, P, P]),
     "sa_conv_direct_weights_size": (L, [I, I, I, I, I]),
     "sa_conv_direct_weights_split": (I, [P, L, P, P]),

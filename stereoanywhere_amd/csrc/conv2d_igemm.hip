@@ -101,8 +101,7 @@ struct IgLaunch {
   unsigned end[MAX_PROB];
   unsigned nblk[MAX_PROB];
   int nprob;
-  unsigned *redo;   // range guard: [0] = count, then (problem << 27 | work item) per skipped block
-  unsigned redo_cap;
+  int guard;   // range guard (a block with a finite input beyond the f16 range recomputes itself scaled)
 };
 
 __device__ unsigned g_ig_redo_blocks;
@@ -263,7 +262,7 @@ __device__ __forceinline__ void ig_emit(const IgProb &P, const IgGate *gate, flo
 // One work item (128 output channels x one pixel tile of one image).
 template <class C, bool GATED, bool AFF>
 __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, const unsigned wid, char *smem,
-                                        float2 *atab, unsigned *redo, const unsigned redo_cap, const unsigned tag) {
+                                        float2 *atab, const bool guard) {
   constexpr int NTHR = C::NTHR, TW = C::TW, TH = C::TH, PC = C::PC, NPIX = C::NPIX, PLANE = C::PLANE,
                 XBUF = C::XBUF, XJOBS = C::XJOBS, NCF = C::NCF, NPF = C::NPF, FPR = C::FPR, RPW = C::RPW,
                 WSTEP = C::WSTEP, OPP = C::OPP;
@@ -285,7 +284,6 @@ __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, con
   const __amdgpu_buffer_rsrc_t xin = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float *>(P.in + (long)n * P.in_bs), (short)0, Cin * hw * 4, 0x00020000);
   unsigned xoff[XJOBS];
-  int xdst[XJOBS], xgrp[XJOBS];
   bool xin_img[XJOBS];
 #pragma unroll
   for (int j = 0; j < XJOBS; ++j) {
@@ -295,12 +293,18 @@ __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, con
     const bool ok = J < 4 * NPIX && y >= 0 && y < H && x >= 0 && x < W;
     xin_img[j] = ok;
     xoff[j] = ok ? (unsigned)((8 * g * hw + y * pitch + x) * 4) : IG_OOB;
-    // (a slot-less lane writes the spare entry past the planes: branch-free, never read)
-    xdst[j] = J < 4 * NPIX ? (g * PLANE + q) * 16 : 8 * PLANE * 16;
-    xgrp[j] = g < 4 ? g : 3;
   }
+  // job j's LDS entry (group g, pixel q) = J + g (PLANE - NPIX), recomputed at its write (registers);
+  // a slot-less lane writes the spare entry past the planes (branch-free, never read)
+  auto xdst = [&](const int j) __attribute__((always_inline)) {
+    const int J = tid + NTHR * j, g = J / NPIX;
+    return J < 4 * NPIX ? (J + g * (PLANE - NPIX)) * 16 : 8 * PLANE * 16;
+  };
   float xv[2][8];   // two jobs in flight (a job's loads go out three tap positions before its write)
-  bool bad = false;   // an operand outside the f16 range (or not finite): the block goes to the redo list
+  // range guard: a finite operand outside the f16 range; the largest finite magnitude staged
+  bool bad = false;
+  float xmax = 0.0f;
+  float xscale = 1.0f;   // the recompute pass's power-of-two input scale
   auto xload = [&](const int j, const int chunk) __attribute__((always_inline)) {
     const int cs = chunk * KCH * hw * 4;
 #pragma unroll
@@ -317,17 +321,22 @@ __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, con
       float v = xv[j & 1][e];
       if constexpr (AFF) {
         if (xin_img[j]) {
-          const float2 ab = atab[chunk * KCH + 8 * xgrp[j] + e];
+          const float2 ab = atab[chunk * KCH + 8 * ((tid + NTHR * j) / NPIX) + e];
           v = fmaxf(v * ab.x + ab.y, act_floor);
         }
       }
-      bad |= !(__builtin_fabsf(v) < 65504.0f);
+      const float a = __builtin_fabsf(v);
+      const bool fin = a < INFINITY;   // (false for NaN too)
+      bad |= fin && a >= 65504.0f;
+      xmax = fmaxf(xmax, fin ? a : 0.0f);
+      v *= xscale;
       const _Float16 h = (_Float16)v;
       hi[e] = h;
       lo[e] = (_Float16)(v - (float)h);
     }
-    *reinterpret_cast<f16x8 *>(buf + xdst[j]) = hi;
-    *reinterpret_cast<f16x8 *>(buf + xdst[j] + 4 * PLANE * 16) = lo;
+    const int d = xdst(j);
+    *reinterpret_cast<f16x8 *>(buf + d) = hi;
+    *reinterpret_cast<f16x8 *>(buf + d + 4 * PLANE * 16) = lo;
   };
 
   // ---- weights: A operands straight from L2, two taps ahead ----
@@ -365,6 +374,12 @@ __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, con
     __syncthreads();
   }
 
+  // Pass 0 on the inputs as they are; pass 1 (block-uniform, only when pass 0 staged a finite value
+  // beyond the f16 range) on the inputs times 2^-k, which brings the block's largest one below 2^15
+  // (exact scaling; the accumulators are scaled back by 2^k).
+  f32x4 acc[NCF][NPF];
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
   // prologue: chunk 0's patch, then the first two taps' weights
 #pragma unroll
   for (int j = 0; j < XJOBS; ++j) {
@@ -376,7 +391,6 @@ __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, con
   wload(wr[0], toff);
   wload(wr[1], toff + 1 >= 9 ? toff - 8 : toff + 1);
 
-  f32x4 acc[NCF][NPF];
 #pragma unroll
   for (int cf = 0; cf < NCF; ++cf)
 #pragma unroll
@@ -395,7 +409,8 @@ __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, con
   for (int kc = 0; kc < nchunks; ++kc) {
     const char *xb = smem + (kc & 1) * XBUF + xlane;
     char *xn = smem + ((kc + 1) & 1) * XBUF;
-    const int kn = kc + 1 < nchunks ? kc + 1 : kc;
+    const bool more = kc + 1 < nchunks;
+    const int kn = more ? kc + 1 : kc;
 #pragma unroll
     for (int pos = 0; pos < 9; ++pos) {
       // the tap at this position: the pixel-half-1 waves (SIMD partners of the half-0 waves) run the
@@ -408,7 +423,9 @@ __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, con
       // loads (top of 2j + 3; job 3 at the end of position 8).  So the loads issued after this
       // position's weights are the next position's weights and, after an even position, a patch
       // job; on an odd position that waits for the job loaded at the end of p - 3 as well.
-      if ((pos & 1) && (pos - 1) / 2 < XJOBS) {
+      if (pos == 8 && !more) {   // the last chunk issues no weights past its end: nothing younger
+        wait_w(std::integral_constant<int, 0>{}, w);
+      } else if ((pos & 1) && (pos - 1) / 2 < XJOBS) {
         wait_w(std::integral_constant<int, 12>{}, w);
         if (pos >= 3 && (pos - 3) / 2 < XJOBS) {
           wait_x(std::integral_constant<int, 12>{}, xv[((pos - 3) / 2) & 1]);   // (ties the job's registers)
@@ -422,33 +439,39 @@ __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, con
         }
       }
       const char *xt = xb + ((tap / 3) * PC + tap % 3) * 16;
-      f16x8 bh[NPF], bl[NPF];
+      // the 8 pixel fragments in two halves of 4 (the B operands of a half: 32 VGPRs), each
+      // half's products hi*hi, hi*lo, lo*hi over its 4 x 2 tiles (consecutive MFMAs on different
+      // accumulators)
 #pragma unroll
-      for (int f = 0; f < NPF; ++f) {
-        const int qf = (f / FPR) * PC + (f % FPR) * 16;
-        bh[f] = *reinterpret_cast<const f16x8 *>(xt + qf * 16);
-        bl[f] = *reinterpret_cast<const f16x8 *>(xt + qf * 16 + 4 * PLANE * 16);
-      }
-      if constexpr (IG_DIAG == 5) {
+      for (int hf = 0; hf < 2; ++hf) {
+        f16x8 bh[NPF / 2], bl[NPF / 2];
 #pragma unroll
-        for (int f = 0; f < NPF; ++f)
-          acc[0][f][0] += (float)(bh[f][0] + bl[f][1] + w[0][0][f & 7] + w[1][1][f & 7]);
-      } else {
+        for (int u = 0; u < NPF / 2; ++u) {
+          const int f = hf * (NPF / 2) + u, qf = (f / FPR) * PC + (f % FPR) * 16;
+          bh[u] = *reinterpret_cast<const f16x8 *>(xt + qf * 16);
+          bl[u] = *reinterpret_cast<const f16x8 *>(xt + qf * 16 + 4 * PLANE * 16);
+        }
+        if constexpr (IG_DIAG == 5) {
 #pragma unroll
-      for (int f = 0; f < NPF; ++f)
+          for (int u = 0; u < NPF / 2; ++u)
+            acc[0][hf * 4 + u][0] += (float)(bh[u][0] + bl[u][1] + w[0][0][u] + w[1][1][u]);
+        } else {
 #pragma unroll
-        for (int cf = 0; cf < NCF; ++cf)
-          acc[cf][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[0][cf], bh[f], acc[cf][f], 0, 0, 0);
+          for (int u = 0; u < NPF / 2; ++u)
 #pragma unroll
-      for (int f = 0; f < NPF; ++f)
+            for (int cf = 0; cf < NCF; ++cf)
+              acc[cf][hf * 4 + u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[0][cf], bh[u], acc[cf][hf * 4 + u], 0, 0, 0);
 #pragma unroll
-        for (int cf = 0; cf < NCF; ++cf)
-          acc[cf][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[0][cf], bl[f], acc[cf][f], 0, 0, 0);
+          for (int u = 0; u < NPF / 2; ++u)
 #pragma unroll
-      for (int f = 0; f < NPF; ++f)
+            for (int cf = 0; cf < NCF; ++cf)
+              acc[cf][hf * 4 + u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[0][cf], bl[u], acc[cf][hf * 4 + u], 0, 0, 0);
 #pragma unroll
-        for (int cf = 0; cf < NCF; ++cf)
-          acc[cf][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[1][cf], bh[f], acc[cf][f], 0, 0, 0);
+          for (int u = 0; u < NPF / 2; ++u)
+#pragma unroll
+            for (int cf = 0; cf < NCF; ++cf)
+              acc[cf][hf * 4 + u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[1][cf], bh[u], acc[cf][hf * 4 + u], 0, 0, 0);
+        }
       }
       if (!(pos & 1) && pos / 2 < XJOBS && IG_DIAG != 2 && IG_DIAG != 4) xload(pos / 2, kn);
       {
@@ -458,7 +481,9 @@ __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, con
           c2 += 1;
         }
         t2 = t2 >= 9 ? t2 - 9 : t2;
-        if (IG_DIAG != 1 && IG_DIAG != 4) wload(wr[(pos + 2) % 3], c2 * 9 + t2);
+        // (past the last chunk nothing is loaded: an asm load left in flight into registers the
+        // compiler considers dead could land on whatever it reuses them for)
+        if (IG_DIAG != 1 && IG_DIAG != 4 && (pos < 7 || more)) wload(wr[(pos + 2) % 3], c2 * 9 + t2);
         else {   // (diagnostic: the same random operands, no loads)
 #pragma unroll
           for (int hl = 0; hl < 2; ++hl)
@@ -473,20 +498,28 @@ __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, con
     }
     if (IG_DIAG != 3 && IG_DIAG != 4) __syncthreads();   // chunk kc + 1's patch is written; chunk kc's buffer is free
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing (dummy) prefetches
-
-  // range guard: a block with an operand outside the f16 range writes nothing and queues itself
-  if (__syncthreads_or(bad)) {
-    if (redo && tid == 0) {
-      const unsigned slot = atomicAdd(redo, 1u);
-      if (slot < redo_cap) redo[1 + slot] = tag;
-    }
-    return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (nothing in flight past the loop)
+  if (pass == 1 || !guard || !__syncthreads_or(bad)) break;
+  // the block's largest finite input: wave maxima through LDS (the patch buffers are free)
+  {
+    float *red = reinterpret_cast<float *>(smem);
+    const float wmax = sa::wave_max_dpp(xmax);
+    if (lane == 0) red[wv] = wmax;
+    __syncthreads();
+    float m = red[0];
+#pragma unroll
+    for (int w = 1; w < C::NW; ++w) m = fmaxf(m, red[w]);
+    int e;
+    (void)frexpf(m, &e);             // m < 2^e
+    xscale = ldexpf(1.0f, 15 - e);   // m * xscale < 2^15
+    __syncthreads();
+    if (tid == 0) atomicAdd(&g_ig_redo_blocks, 1u);
+  }
   }
 
   // accumulators -> LDS planes [channel][pixel] (times 2^-12)
   float *ot = reinterpret_cast<float *>(smem);
-  constexpr float inv = 1.0f / (float)(1 << IG_LOG2);
+  const float inv = 1.0f / ((float)(1 << IG_LOG2) * xscale);
 #pragma unroll
   for (int cf = 0; cf < NCF; ++cf)
 #pragma unroll
@@ -513,10 +546,10 @@ __global__ __launch_bounds__(512, 1) void ig_kernel(const IgLaunch L) {
   __shared__ float2 atab[AFF ? 512 : 1];
   const unsigned wid = sa::xcd_remap(g - base, nb);
   const IgGate *gp = GATED ? &L.gate[pi] : nullptr;
-  const unsigned tag = ((unsigned)pi << 27) | wid;
-  if (P.ltw == 4) ig_body<IgCfg<4>, GATED, AFF>(P, gp, wid, smem, atab, L.redo, L.redo_cap, tag);
-  else if (P.ltw == 5) ig_body<IgCfg<5>, GATED, AFF>(P, gp, wid, smem, atab, L.redo, L.redo_cap, tag);
-  else ig_body<IgCfg<6>, GATED, AFF>(P, gp, wid, smem, atab, L.redo, L.redo_cap, tag);
+  const bool guard = L.guard != 0;
+  if (P.ltw == 4) ig_body<IgCfg<4>, GATED, AFF>(P, gp, wid, smem, atab, guard);
+  else if (P.ltw == 5) ig_body<IgCfg<5>, GATED, AFF>(P, gp, wid, smem, atab, guard);
+  else ig_body<IgCfg<6>, GATED, AFF>(P, gp, wid, smem, atab, guard);
 }
 
 // w[co][ci][3][3] -> [Cout/128][Cin/32][9][hl][co/16 % 8][g][co % 16][8] f16 of w * 2^12
@@ -579,8 +612,7 @@ extern "C" long sa_conv2d_igemm_blocks(int N, int Cout, int H, int W) {
   return (long)N * parts * (Cout / 128);
 }
 
-extern "C" long sa_igemm_redo_blocks(int reset) {
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
+long sa_igemm_redo_blocks_internal(int reset) {   // (sa_split_redo_blocks adds it up; synchronised there)
   unsigned v = 0;
   if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_ig_redo_blocks), sizeof v) != hipSuccess) return -1;
   if (reset) {
@@ -590,8 +622,8 @@ extern "C" long sa_igemm_redo_blocks(int reset) {
   return (long)v;
 }
 
-extern "C" int sa_conv2d_k3_igemm(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
-                                  unsigned *redo_ws, long redo_cap, void *stream) {
+extern "C" int sa_conv2d_k3_igemm(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates, int guard,
+                                  void *stream) {
   SA_REQUIRE(nprob >= 1 && nprob <= MAX_PROB && probs, "sa_conv2d_k3_igemm: 1..%d problems", MAX_PROB);
   IgLaunch L{};
   long total = 0;
@@ -647,12 +679,7 @@ extern "C" int sa_conv2d_k3_igemm(int nprob, const SaWinoProblem *probs, const S
   }
   L.nprob = nprob;
   SA_REQUIRE(!(aff && gated), "sa_conv2d_k3_igemm: an input transform and a gate epilogue in one launch");
-  if (redo_ws) {
-    SA_REQUIRE(redo_cap >= total && (reinterpret_cast<uintptr_t>(redo_ws) & 3) == 0,
-               "sa_conv2d_k3_igemm: the redo workspace holds %ld entries, the launch has %ld blocks", redo_cap, total);
-    L.redo = redo_ws;
-    L.redo_cap = (unsigned)redo_cap;
-  }
+  L.guard = guard ? 1 : 0;
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV2D_IG, s);
   aff     ? ig_kernel<false, true><<<(unsigned)total, 512, 0, s>>>(L)

@@ -27,11 +27,11 @@ class ForwardGraph:
         self._graph: Optional[torch.cuda.CUDAGraph] = None
         self._static = None
         self._out = None
-        # this instance's capture stream and workspace scope: the split kernels' range-guard
-        # workspaces (ops._redo_workspace) baked into this graph are its own, so two instances
-        # replayed at the same time (PipelinedForward) never share a redo list
+        # this instance's own capture stream (not torch's shared default capture stream).  The
+        # captured launches hold no per-stream workspace: the split kernels' range guards recompute
+        # an overflowed block inside its own launch, so graph instances replayed at the same time on
+        # different streams (PipelinedForward) share no state
         ForwardGraph._instances += 1
-        self._scope = ("graph", ForwardGraph._instances)
         self._cap_stream: Optional[torch.cuda.Stream] = None
 
     def _make_key(self, xs, iters):
@@ -48,9 +48,9 @@ class ForwardGraph:
         c_switches = tuple(getattr(lib, name)() if hasattr(lib, name) else None
                            for name in ("sa_lookup_get_mfma", "sa_softargmin_get_one_pass", "sa_conv3d_wd_get_variant"))
         return (tuple((tuple(x.shape), x.dtype, x.device) for x in xs), iters, dataclasses.astuple(m.opts),
-                m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_WIDE, ops.W4_QUAD, ops.W4_PERSIST, ops.W4_SPLIT,
-                                                   ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS, ops.SPLIT_GUARD,
-                                                   ops.W4_SPLIT_SMALL_CIN), c_switches, args)
+                m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_SPLIT, ops.IGEMM, ops.IGEMM_MAX_WORK,
+                                                   ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS, ops.SPLIT_GUARD),
+                c_switches, args)
 
     def __call__(self, image2, image3, mde2, mde3, iters: int = 12, test_mode: bool = True):
         if not test_mode:
@@ -80,13 +80,8 @@ class ForwardGraph:
         g = torch.cuda.CUDAGraph()
         if self._cap_stream is None:
             self._cap_stream = torch.cuda.Stream()
-        from . import ops
-        prev, ops._REDO_SCOPE = ops._REDO_SCOPE, self._scope
-        try:
-            with torch.cuda.graph(g, stream=self._cap_stream):
-                self._out = self.model(*self._static, iters=iters, test_mode=True)[0]
-        finally:
-            ops._REDO_SCOPE = prev
+        with torch.cuda.graph(g, stream=self._cap_stream):
+            self._out = self.model(*self._static, iters=iters, test_mode=True)[0]
         self._graph = g
 
 

@@ -777,38 +777,31 @@ def conv2d_k3_narrow(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch
 
 
 class WinoFilters:
-    """Transformed filters of one 3x3 conv for both fused Winograd kernels: ``u2`` for
-    F(2x2,3x3) (conv2d_wino.hip), ``u4`` for F(4x4,3x3) (conv2d_wino4.hip) in 32-channel
-    blocks, ``u4w`` in the wide shape's 64-channel blocks (None unless Cout % 64 == 0) and
-    ``u4s`` as the split kernel's f16 hi/lo pairs (None unless W4_SPLIT when derived)."""
-    __slots__ = ("u2", "u4", "u4w", "u4s", "cin", "cout")
+    """Derived filters of one 3x3 conv for the fused Winograd kernels and the implicit GEMM:
+    ``u2`` for F(2x2,3x3) (conv2d_wino.hip), ``u4`` for F(4x4,3x3) (conv2d_wino4.hip) in 32-channel
+    blocks, ``u4s`` as the split F(4x4) kernel's f16 hi/lo pairs (None unless W4_SPLIT when derived)
+    and ``uig`` as the implicit-GEMM kernel's split weights (conv2d_igemm.hip; None unless IGEMM,
+    Cout % 128 == 0 and Cin % 32 == 0)."""
+    __slots__ = ("u2", "u4", "u4s", "uig", "cin", "cout")
 
-    def __init__(self, u2: torch.Tensor, u4: torch.Tensor, cin: int, cout: int, u4w: Optional[torch.Tensor] = None,
-                 u4s: Optional[torch.Tensor] = None):
-        self.u2, self.u4, self.u4w, self.u4s, self.cin, self.cout = u2, u4, u4w, u4s, cin, cout
+    def __init__(self, u2: torch.Tensor, u4: torch.Tensor, cin: int, cout: int, u4s: Optional[torch.Tensor] = None,
+                 uig: Optional[torch.Tensor] = None):
+        self.u2, self.u4, self.u4s, self.uig, self.cin, self.cout = u2, u4, u4s, uig, cin, cout
 
 
 # False keeps every 3x3 conv on the F(2x2,3x3) kernel (set by A/B scripts and tests)
 _WINO4 = True
-# F(4x4) launches on the wide block shape (64 output channels per block, one wave per SIMD)
-# where every problem allows it (Cout % 64; Cout % 128 with a z/r gate)
-W4_WIDE = False
-# F(4x4) launches of the default (8-wave) shape on its persistent kernel (block_shape 5): one block
-# per CU walking the launch's work items, each prefetching the next item's first chunk under its
-# own epilogue
-W4_PERSIST = False
-# F(4x4) launches on the quadrant block shape (block_shape 4: 32 tiles x 64 output channels,
-# two waves per SIMD, each wave one quadrant of the 6 x 6 points) where every problem allows it
-W4_QUAD = False
 # F(4x4) launches of the default shape on the split kernel (block_shape 6): the Winograd-domain
 # products on v_mfma_f32_16x16x16_f16 with f16 hi/lo operand pairs (22 significant bits, exact
 # f16 x f16 products, fp32 accumulation) instead of fp32 MFMA: 1.06-1.22x per conv, 54.3 -> 60.4
 # pairs/s at configs[1] with EPE vs the reference 1.78e-5 (fp32 MFMA: 1.84e-5)
 W4_SPLIT = True
-# split launches whose problems all have Cin <= this on the 4-wave split shape (block_shape 7:
-# 32 tiles, 4-channel chunks, two blocks per CU, so one block's first-chunk wait and epilogue
-# overlap the other's main loop); 0: off
-W4_SPLIT_SMALL_CIN = 0
+# 3x3 launches on the implicit-GEMM kernel (conv2d_igemm.hip: direct convolution on
+# v_mfma_f32_16x16x32_f16, three f16 products per fp32 product) where every problem allows it
+# (Cout % 128, Cin % 32; gate modes 1 / 2) and the launch's total output pixels x Cout is at most
+# IGEMM_MAX_WORK (None: no limit; see conv2d_k3_multi)
+IGEMM = True
+IGEMM_MAX_WORK = None
 # the split filters need |U * 2^12| < 65504; |U| <= max |weight| for F(4x4,3x3)'s G
 _W4_SPLIT_WMAX = 15.99
 # the direct convs (stems, stride-2 + 1x1) with split products (sa_conv_direct_split), derived
@@ -834,17 +827,18 @@ def wino_weights(weight: torch.Tensor) -> WinoFilters:
     N.call("sa_conv2d_wino_weights", weight.data_ptr(), Cout, Cin, u2.data_ptr(), _stream(weight))
     u4 = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.float32)
     N.call("sa_conv2d_wino4_weights", weight.data_ptr(), Cout, Cin, u4.data_ptr(), _stream(weight))
-    u4w = None
-    if (W4_WIDE or W4_QUAD) and Cout % 64 == 0 and Cin % 8 == 0:   # the 64-channel layout only when it may run
-        u4w = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.float32)
-        N.call("sa_conv2d_wino4_weights_cb", weight.data_ptr(), Cout, Cin, 64, u4w.data_ptr(), _stream(weight))
     u4s = None
     # (a conv whose filters exceed the split kernel's f16 range keeps u4s = None: its launches run
     # the fp32-product kernel, conv2d_k3_multi)
     if W4_SPLIT and Cout % 32 == 0 and Cin % 8 == 0 and split_range_ok(weight):
         u4s = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.int32)
         N.call("sa_conv2d_wino4_weights_split", weight.data_ptr(), Cout, Cin, u4s.data_ptr(), _stream(weight))
-    return WinoFilters(u2, u4, Cin, Cout, u4w, u4s)
+    uig = None
+    if IGEMM and Cout % 128 == 0 and Cin % 32 == 0 and split_range_ok(weight):
+        uig = torch.empty((int(N.lib().sa_conv2d_igemm_weights_size(Cout, Cin)),), device=weight.device,
+                          dtype=torch.int32)
+        N.call("sa_conv2d_igemm_weights", weight.data_ptr(), Cout, Cin, uig.data_ptr(), _stream(weight))
+    return WinoFilters(u2, u4, Cin, Cout, u4s, uig)
 
 
 # largest Cin of an F(4x4,3x3) launch with an input transform (its (scale, shift) table fills the
@@ -883,8 +877,8 @@ _WINO4_MIN_BLOCKS = 128
 
 def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] = None, relu: bool = False,
                   out: Optional[torch.Tensor] = None, in_aff: Optional[Affine] = None, in_act=None,
-                  stats: bool = False, f4: bool = False, out_cout: Optional[int] = None, wide: bool = False,
-                  width: Optional[int] = None, split: bool = False):
+                  stats: bool = False, f4: bool = False, out_cout: Optional[int] = None,
+                  width: Optional[int] = None, split: bool = False, ig: bool = False):
     """out_cout: channels of ``out`` when the epilogue writes fewer than Cout there (gate mode 1).
     width: the image width when x (and out, and the gate planes) are PITCHED planes [.., H, P]
     whose columns width .. P - 1 are zero (F(4x4) only; the outputs' pad columns stay zero)."""
@@ -895,8 +889,8 @@ def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] 
     W = P if width is None else width
     if not 0 < W <= P:
         raise RuntimeError(f"conv2d_k3: width {W} outside the plane pitch {P}")
-    if W != P and not f4:
-        raise RuntimeError("conv2d_k3: pitched planes need the F(4x4,3x3) kernel")
+    if W != P and not (f4 or ig):
+        raise RuntimeError("conv2d_k3: pitched planes need the F(4x4,3x3) or the implicit-GEMM kernel")
     Cout = U.cout
     if U.cin != Cin:
         raise RuntimeError(f"conv2d_k3: U has {U.cin} input channels, x has {Cin}")
@@ -906,16 +900,19 @@ def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] 
     if tuple(out.shape) != (B, out_cout or Cout, H, P):
         raise RuntimeError("conv2d_k3: out shape mismatch")
     m, s, t, ps = (in_aff or Affine()).args(Cin)
-    parts_fn = N.lib().sa_conv2d_k3_wino4_stat_parts if f4 else N.lib().sa_conv2d_k3_wino_stat_parts
+    parts_fn = (N.lib().sa_conv2d_igemm_stat_parts if ig else N.lib().sa_conv2d_k3_wino4_stat_parts if f4
+                else N.lib().sa_conv2d_k3_wino_stat_parts)
     parts = int(parts_fn(H, W)) if stats else 0
     partial = torch.empty((B * Cout * parts * 2,), device=x.device, dtype=torch.float64) if stats else None
-    Uf = (U.u4w if wide else U.u4s if split else U.u4) if f4 else U.u2
+    Uf = U.uig if ig else (U.u4s if split else U.u4) if f4 else U.u2
     prob = N.SaWinoProblem(x.data_ptr(), bs, B, Cin, H, W, Uf.data_ptr(), Cout, _ptr(bias),
                            1 if relu else 0, m, s, t, ps, ACT[in_act], out.data_ptr(), _plane_bs(out, "out"),
                            _ptr(partial), P if P != W else 0)
     # Winograd-domain products actually executed: 36 per 4x4 tile (F4) or 16 per 2x2 tile (F2)
-    # per (Cin, Cout) pair
-    if f4:
+    # per (Cin, Cout) pair; the implicit GEMM: the direct convolution's 9 per output
+    if ig:
+        _account("conv2d_igemm", 2.0 * 9 * Cin * Cout * B * H * W)   # logical W
+    elif f4:
         _account("conv2d_wino4", 2.0 * 36 * Cin * Cout * B * ((H + 3) // 4) * ((W + 3) // 4))   # logical W
     else:
         _account("conv2d_wino", 2.0 * 16 * Cin * Cout * B * ((H + 1) // 2) * ((W + 1) // 2))
@@ -964,42 +961,30 @@ def _gate_epilogue(p: dict) -> "N.SaGateEpilogue":
     return e
 
 
-# the split kernel's range-guard workspaces ([0] = count, then one entry per block of a launch), one per
-# HIP stream (launches on one stream run in order, and the guard's redo kernel leaves the count
-# zeroed), grown by replacement; superseded buffers stay referenced, since a captured hipGraph may
-# still name them
-_REDO_WS: dict = {}
-_REDO_OLD: list = []
-# set by graph.ForwardGraph while it captures: each graph instance bakes its own workspaces, so
-# graphs replayed concurrently on other streams (PipelinedForward) never share a redo list
-_REDO_SCOPE = None
-
-
-def _redo_workspace(x: torch.Tensor, blocks: int) -> torch.Tensor:
-    st = torch.cuda.current_stream(x.device)
-    key = (x.device.index, st.cuda_stream, _REDO_SCOPE)
-    ws = _REDO_WS.get(key)
-    if ws is None or ws.numel() < 1 + blocks:
-        if ws is not None:
-            _REDO_OLD.append(ws)
-        ws = torch.zeros((1 + max(blocks, 1 << 15),), device=x.device, dtype=torch.int32)
-        _REDO_WS[key] = ws
-    return ws
-
-
-# the split kernel's f16 range guard (False: no workspace, no redo launch: A/B timing only)
+# the split kernels' f16 range guards (False: no overflow check or recompute: A/B timing only)
 SPLIT_GUARD = True
 
 
-def _wino4_launch(n: int, arr, gates, shape: int, x: torch.Tensor, blocks: int) -> None:
-    """sa_conv2d_k3_wino4_launch; the split shape (6) with its range-guard workspace."""
-    # (an A/B run's older library, SA_HIP_LIB, may predate the guard's entry point)
-    if shape in (6, 7) and SPLIT_GUARD and hasattr(N.lib(), "sa_conv2d_k3_wino4_launch"):
-        ws = _redo_workspace(x, 2 * blocks if shape == 7 else blocks)   # (7: half the tiles per block)
-        N.call("sa_conv2d_k3_wino4_launch", n, ctypes.addressof(arr), ctypes.addressof(gates), shape, ws.data_ptr(),
-               ws.numel() - 1, _stream(x))
-    else:
-        N.call("sa_conv2d_k3_wino4_multi_gate", n, ctypes.addressof(arr), ctypes.addressof(gates), shape, _stream(x))
+def _wino4_launch(n: int, arr, gates, shape: int, x: torch.Tensor) -> None:
+    """sa_conv2d_k3_wino4_launch; the split shape (6) with its range guard (an overflowed block
+    recomputes itself on fp32 products inside the launch)."""
+    N.call("sa_conv2d_k3_wino4_launch", n, ctypes.addressof(arr), ctypes.addressof(gates), shape,
+           1 if (shape == 6 and SPLIT_GUARD) else 0, _stream(x))
+
+
+def _igemm_ok(p: dict, q: dict) -> bool:
+    """Whether the implicit-GEMM kernel takes problem p (q: its arguments without the gate):
+    its weights derived (Cout % 128, Cin % 32, |w| < 16), gate modes 1 (Cout % 256) or 2, an input
+    transform none / ReLU with Cin <= 512, plane pitches % 4 and 16-byte aligned outputs."""
+    U, x, out = q["U"], q["x"], q.get("out")
+    if not IGEMM or U.uig is None:
+        return False
+    g = p.get("gate")
+    if g and not (g["mode"] == 2 or (g["mode"] == 1 and U.cout % 256 == 0)):
+        return False
+    if (q.get("in_aff") is not None or q.get("in_act") is not None) and (x.shape[1] > 512 or ACT[q.get("in_act")] > 1):
+        return False
+    return (x.shape[3] % 4 == 0 and (out is None or (out.data_ptr() % 16 == 0 and out.stride(0) % 4 == 0)))
 
 
 def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
@@ -1017,6 +1002,24 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     for p, q in zip(problems, plain):
         if p.get("gate") and p["gate"]["mode"] == 1:
             q["out_cout"] = p["U"].cout // 2   # z only: r*h goes to the gate's out2
+    if not small_blocks:
+        igs = [_igemm_ok(p, q) for p, q in zip(problems, plain)]
+        if any(igs):
+            if not all(igs):   # the implicit-GEMM problems in a launch of their own, the others as before
+                res = [None] * len(problems)
+                for idx in ([i for i, k in enumerate(igs) if k], [i for i, k in enumerate(igs) if not k]):
+                    for i, r in zip(idx, conv2d_k3_multi(*[problems[i] for i in idx])):
+                        res[i] = r
+                return res
+            if IGEMM_MAX_WORK is None or sum(q["x"].shape[0] * q["x"].shape[2] * q["x"].shape[3] * q["U"].cout
+                                             for q in plain) <= IGEMM_MAX_WORK:
+                built = [_wino_problem(**q, ig=True) for q in plain]
+                arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
+                gates = (N.SaGateEpilogue * len(built))(*[_gate_epilogue(p) if p.get("gate") else N.SaGateEpilogue()
+                                                          for p in problems])
+                N.call("sa_conv2d_k3_igemm", len(built), ctypes.addressof(arr), ctypes.addressof(gates),
+                       1 if SPLIT_GUARD else 0, _stream(problems[0]["x"]))
+                return [b[1]() for b in built]
     oks = [_WINO4 and _wino4_ok(**p) for p in plain]
     if any(oks) and not all(oks):
         # a mixed group: the problems F(4x4) cannot take (W % 4 != 0, unaligned planes) go to a
@@ -1037,23 +1040,13 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     aff = any(p.get("in_aff") is not None or p.get("in_act") is not None for p in plain)
     if gated and aff:
         raise RuntimeError("conv2d_k3_multi: an input transform and a gate epilogue in one launch")
-    wide = (f4 and (W4_QUAD or (W4_WIDE and not aff)) and not small_blocks
-            and all(p["U"].u4w is not None for p in plain)
-            and all(p["U"].cout % 128 == 0 for p in problems if p.get("gate") and p["gate"]["mode"] == 1))
-    persist = f4 and W4_PERSIST and not (small_blocks or wide)
-    split = (f4 and W4_SPLIT and not (small_blocks or wide or persist)
-             and all(p["U"].u4s is not None for p in plain))
-    built = [_wino_problem(**p, f4=f4, wide=wide, split=split) for p in plain]
+    split = f4 and W4_SPLIT and not small_blocks and all(p["U"].u4s is not None for p in plain)
+    built = [_wino_problem(**p, f4=f4, split=split) for p in plain]
     arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
-    if f4 and (gated or small_blocks or wide or persist or split):
+    if f4 and (gated or small_blocks or split):
         gates = (N.SaGateEpilogue * len(built))(*[_gate_epilogue(p) if p.get("gate") else N.SaGateEpilogue()
                                                   for p in problems])
-        shape = (4 if W4_QUAD else 3) if wide else 2 if small_blocks else 5 if persist else 6 if split else 0
-        if (shape == 6 and W4_SPLIT_SMALL_CIN and all(p["x"].shape[1] <= W4_SPLIT_SMALL_CIN for p in plain)
-                and not any(p.get("gate") and p["gate"]["mode"] == 3 for p in problems)):
-            shape = 7
-        _wino4_launch(len(built), arr, gates, shape, problems[0]["x"],
-                      sum(_wino4_blocks(**p) + 8 for p in plain))
+        _wino4_launch(len(built), arr, gates, 2 if small_blocks else 6 if split else 0, problems[0]["x"])
     else:
         N.call("sa_conv2d_k3_wino4_multi" if f4 else "sa_conv2d_k3_wino_multi", len(built), ctypes.addressof(arr),
                _stream(problems[0]["x"]))
@@ -1084,7 +1077,7 @@ def flow_head_update(h: torch.Tensor, U1: "WinoFilters", b1: torch.Tensor, w2: t
     gate = N.SaGateEpilogue(3)
     gate.head_w, gate.head_part, gate.head_part_bs = w2c.data_ptr(), part.data_ptr(), per
     _account("conv2d_wino4", 2.0 * 36 * Cin * U1.cout * B * ((H + 3) // 4) * ((W + 3) // 4))
-    _wino4_launch(1, prob, gate, 6 if split else 0, h, _wino4_blocks(h, U1))
+    _wino4_launch(1, prob, gate, 6 if split else 0, h)
     _check(coords_x, "coords_x")
     N.call("sa_flow_head_reduce", part.data_ptr(), B, U1.cout, H, W, b2.data_ptr(), coords_x.data_ptr(),
            _ptr(flow), 0 if flow is None else _plane_bs(flow, "flow"), None, 0, _stream(h))

@@ -38,33 +38,29 @@ def test_tiny_case_and_intermediates(model):
     assert e < 1e-3
 
 
-@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("kernels", ["fp32", "split", "split_igemm"])
 @pytest.mark.parametrize("name,H,W,D,iters", [("cfg1_256x512_it8.npz", 256, 512, 64.0, 8),
                                                ("cfg2_544x960_it22.npz", 544, 960, 192.0, 22)])
-def test_end_to_end_vs_reference(model, monkeypatch, name, H, W, D, iters, split):
-    """split: every F(4x4) and direct conv on the f16 hi/lo split kernels (ops.W4_SPLIT,
-    ops.DIRECT_SPLIT) or all on fp32 MFMA products."""
+def test_end_to_end_vs_reference(model, monkeypatch, name, H, W, D, iters, kernels):
+    """kernels: every 3x3 conv on fp32 MFMA products (the F(4x4) / F(2x2) Winograd kernels, and the
+    direct convs); "split": the F(4x4) and direct convs on the f16 hi/lo split kernels (ops.W4_SPLIT,
+    ops.DIRECT_SPLIT); "split_igemm": and the 3x3 convs it takes on the implicit GEMM (ops.IGEMM:
+    16x16x32 f16 MFMA, three products)."""
     from stereoanywhere_amd import ops
-    monkeypatch.setattr(ops, "W4_SPLIT", split)
-    monkeypatch.setattr(ops, "DIRECT_SPLIT", split)
+    monkeypatch.setattr(ops, "W4_SPLIT", kernels != "fp32")
+    monkeypatch.setattr(ops, "DIRECT_SPLIT", kernels != "fp32")
+    monkeypatch.setattr(ops, "IGEMM", kernels == "split_igemm")
     fix = load_fixture(name)
     pair = regenerate_inputs(fix, 1, H, W, D)
-    disp = run(model, pair, iters)
+    ops.WORK = {}
+    try:
+        disp = run(model, pair, iters)
+        work = dict(ops.WORK)
+    finally:
+        ops.WORK = None
+    assert ("conv2d_igemm" in work) == (kernels == "split_igemm")
     e = epe(disp, fix["disparity"])
-    print(name, "split" if split else "fp32", "EPE", e, "max", float(np.abs(disp - fix["disparity"]).max()))
-    assert e < 1e-3
-
-
-def test_end_to_end_split_small_shape_vs_reference(model, monkeypatch):
-    """Every split F(4x4) launch that allows it (no flow-head epilogue) on the 4-wave split shape
-    (ops.W4_SPLIT_SMALL_CIN, block_shape 7): the 544x960 / 22-iteration reference fixture."""
-    from stereoanywhere_amd import ops
-    monkeypatch.setattr(ops, "W4_SPLIT_SMALL_CIN", 4096)
-    fix = load_fixture("cfg2_544x960_it22.npz")
-    pair = regenerate_inputs(fix, 1, 544, 960, 192.0)
-    disp = run(model, pair, 22)
-    e = epe(disp, fix["disparity"])
-    print("split small shape EPE", e)
+    print(name, kernels, "EPE", e, "max", float(np.abs(disp - fix["disparity"]).max()))
     assert e < 1e-3
 
 
@@ -127,6 +123,7 @@ def test_large_disparity_split_vs_fp32(model, monkeypatch):
     for split in (False, True):
         monkeypatch.setattr(ops, "W4_SPLIT", split)
         monkeypatch.setattr(ops, "DIRECT_SPLIT", split)
+        monkeypatch.setattr(ops, "IGEMM", split)
         out[split] = run(model, pb, 8)
     assert np.isfinite(out[True]).all() and np.isfinite(out[False]).all()
     assert float(np.abs(out[True]).max()) > 50.0   # the large-disparity regime is exercised
@@ -239,7 +236,7 @@ def test_loop_parts_match_one_stream(model, parts, offset):
                                     dict(small_launches=frozenset({"q16", "q08", "zr16", "zr08", "pro32"})),
                                     dict(direct_conv=False), dict(wino4=False),
                                     dict(shear_min_bytes=0), dict(sheared_producers=True, shear_min_bytes=0),
-                                    dict(persist=True), dict(fuse_flow_head=False)])
+                                    dict(igemm=False), dict(fuse_flow_head=False)])
 def test_schedule_options_vs_reference(change):
     """Every non-default launch schedule (stereoanywhere_amd.model.ScheduleOptions; ops._WINO4)
     computes the same forward: cfg1 against the reference's disparity."""
@@ -251,16 +248,16 @@ def test_schedule_options_vs_reference(change):
     m = m.cuda()
     change = dict(change)
     wino4 = change.pop("wino4", True)
-    persist = change.pop("persist", False)
+    igemm = change.pop("igemm", ops.IGEMM)
     m.opts = dataclasses.replace(m.opts, **change)
     fix = load_fixture("cfg1_256x512_it8.npz")
     pair = regenerate_inputs(fix, 1, 256, 512, 64.0)
-    old = ops._WINO4, ops.W4_PERSIST
-    ops._WINO4, ops.W4_PERSIST = wino4, persist
+    old = ops._WINO4, ops.IGEMM
+    ops._WINO4, ops.IGEMM = wino4, igemm
     try:
         disp = run(m, pair, 8)
     finally:
-        ops._WINO4, ops.W4_PERSIST = old
+        ops._WINO4, ops.IGEMM = old
     e = epe(disp, fix["disparity"])
     print(change, "wino4" if wino4 else "no wino4", "EPE", e)
     assert e < 1e-3

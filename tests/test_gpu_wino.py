@@ -11,6 +11,13 @@ pytestmark = pytest.mark.gpu
 dev = "cuda"
 
 
+@pytest.fixture(autouse=True)
+def _winograd_only(monkeypatch):
+    """These tests pin the Winograd kernels: the implicit GEMM (ops.IGEMM) would take every
+    problem with Cout % 128 == 0 (tests/test_gpu_igemm.py covers it)."""
+    monkeypatch.setattr(ops, "IGEMM", False)
+
+
 def rnd(*shape, seed=0):
     g = torch.Generator(device="cpu").manual_seed(seed)
     return torch.randn(*shape, generator=g).to(dev)
@@ -115,7 +122,7 @@ def test_wino4_matches_conv2d(monkeypatch, N, Cin, Cout, H, W, split):
         assert err_max < 1e-4 * scale and err_rms < 1e-5 * scale, (err_max, err_rms)
 
 
-@pytest.mark.parametrize("small", [False, True, "quad", "split"])
+@pytest.mark.parametrize("small", [False, True, "split"])
 def test_wino4_input_transform(monkeypatch, small):
     """The producer's norm + activation applied on load by the F(4x4) kernel (the LDS pass over
     each staged chunk): per-(image, channel) InstanceNorm + ReLU with output statistics on a
@@ -129,11 +136,9 @@ def test_wino4_input_transform(monkeypatch, small):
         return torch.randn(*s, generator=g).cuda()
     xa = r(2, 96, 37, 132) * 2 + 0.7           # channel slice [16, 80) of it
     xb, xc = r(3, 32, 20, 52) + 0.3, r(1, 64, 9, 36)
-    quad = small == "quad"   # the quadrant shape (64 output channels per block)
-    monkeypatch.setattr(ops, "W4_QUAD", quad)
     monkeypatch.setattr(ops, "W4_SPLIT", small == "split")
     small = small is True
-    wa, wb, wc = r(64, 64, 3, 3) / 24, r(128 if quad else 96, 32, 3, 3) / 17, r(64 if quad else 32, 64, 3, 3) / 24
+    wa, wb, wc = r(64, 64, 3, 3) / 24, r(96, 32, 3, 3) / 17, r(32, 64, 3, 3) / 24
     mean, rstd = ops.plane_stats(xa[:, 16:80])
     bn = torch.nn.BatchNorm2d(32).cuda().eval()
     with torch.no_grad():
@@ -220,18 +225,13 @@ def test_wino4_multi_stats_views(monkeypatch):
     torch.testing.assert_close(ye, F.conv2d(xe, wb, padding=1), atol=2e-5, rtol=1e-4)
 
 
-@pytest.mark.parametrize("wide", [False, True, "quad", "persist", "split"])
-def test_wino4_gru_gate_epilogues(monkeypatch, wide):
+@pytest.mark.parametrize("split", [False, True])
+def test_wino4_gru_gate_epilogues(monkeypatch, split):
     """ConvGRU gates in the F(4x4) epilogue (update.py:16-27) against the reference's expressions
     in torch fp32: mode 1 (convz | convr over cat(h, x) -> z, r*h) on channel views of one
     [h | x | r*h] buffer, beside a plain problem in the same launch; mode 2 (convq's r*h part ->
     the new state, in place on h).  Two levels' shapes (8 x 128 and 16 x 64 blocks)."""
-    # also on the wide and the quadrant block shapes (64 channels per block) and on the
-    # persistent kernel (two 16-channel epilogue passes)
-    monkeypatch.setattr(ops, "W4_WIDE", wide is True)
-    monkeypatch.setattr(ops, "W4_QUAD", wide == "quad")
-    monkeypatch.setattr(ops, "W4_PERSIST", wide == "persist")
-    monkeypatch.setattr(ops, "W4_SPLIT", wide == "split")
+    monkeypatch.setattr(ops, "W4_SPLIT", split)
     g = torch.Generator(device="cpu").manual_seed(42)
 
     def r(*s):
@@ -290,81 +290,6 @@ def test_wino4_small_block_shape(monkeypatch):
         torch.testing.assert_close(mean, ref.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
 
 
-@pytest.mark.parametrize("shape", ["wide", "quad"])
-@pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 64, 64, 20, 52), (1, 128, 256, 136, 240), (2, 16, 128, 9, 36),
-                                            (1, 384, 128, 34, 60), (4, 256, 384, 17, 120)])
-def test_wino4_wide_block_shape(monkeypatch, N, Cin, Cout, H, W, shape):
-    """The 64-channel block shapes (block_shape 3, wide: 32 tiles x 64 output channels, one wave
-    per SIMD; block_shape 4, quad: the same tile with two waves per SIMD, each on a quadrant of
-    the points; filters in 64-channel blocks) against torch: bias + ReLU, InstanceNorm
-    statistics, both tile geometries (8 x 64 and 4 x 128 px), a ragged last tile row and column."""
-    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
-    monkeypatch.setattr(ops, "W4_WIDE", shape == "wide")
-    monkeypatch.setattr(ops, "W4_QUAD", shape == "quad")
-    g = torch.Generator(device="cpu").manual_seed(Cin + Cout)
-    x = torch.randn(N, Cin, H, W, generator=g).cuda()
-    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)).cuda()
-    b = torch.randn(Cout, generator=g).cuda()
-    U = ops.wino_weights(w)
-    assert U.u4w is not None
-    ops.WORK = {}
-    try:
-        (out, (mean, rstd)), = ops.conv2d_k3_multi(dict(x=x, U=U, stats=True))
-        (outr,) = ops.conv2d_k3_multi(dict(x=x, U=U, bias=b, relu=True))
-        assert "conv2d_wino4" in ops.WORK
-    finally:
-        ops.WORK = None
-    ref = F.conv2d(x, w, padding=1)
-    scale = max(float(ref.pow(2).mean().sqrt()), 1.0)
-    assert float((out - ref).abs().max()) < 1e-4 * scale and float((out - ref).pow(2).mean().sqrt()) < 1e-5 * scale
-    torch.testing.assert_close(outr, torch.relu(F.conv2d(x, w, b, padding=1)), atol=1e-4 * scale, rtol=1e-4)
-    torch.testing.assert_close(mean, ref.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
-    torch.testing.assert_close(rstd, torch.rsqrt(ref.var(dim=(2, 3), unbiased=False) + 1e-5).flatten(),
-                               atol=1e-4, rtol=1e-4)
-
-
-def test_wino4_persistent_equals_one_shot(monkeypatch):
-    """The persistent F(4x4) kernel (block_shape 5: one block per CU walking the work items, the
-    next item's first chunk prefetched under the epilogue, outputs staged in two 16-channel
-    passes) computes the one-shot kernel's outputs bit for bit: a multi-problem launch mixing
-    both tile geometries and input-channel counts (so consecutive items of a block change
-    problem, geometry and buffer parity), bias + ReLU, channel-slice views, InstanceNorm
-    statistics, and an input-transform launch; more items than blocks."""
-    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
-    monkeypatch.setattr(ops, "W4_SPLIT", False)   # the one-shot fp32 kernel it shares its code with
-    g = torch.Generator(device="cpu").manual_seed(77)
-
-    def r(*s):
-        return torch.randn(*s, generator=g).cuda()
-    xa, xb, xc = r(4, 136, 136, 240), r(4, 64, 68, 120), r(3, 200, 34, 60)
-    wa, wb, wc = r(64, 128, 3, 3) / 34, r(96, 64, 3, 3) / 24, r(128, 200, 3, 3) / 42
-    ba = r(64)
-    probs = lambda: [dict(x=xa[:, 8:], U=ops.wino_weights(wa), bias=ba, relu=True),   # noqa: E731
-                     dict(x=xb, U=ops.wino_weights(wb), stats=True),
-                     dict(x=xc, U=ops.wino_weights(wc), bias=r(128) * 0)]
-    outs = {}
-    for persist in (False, True):
-        monkeypatch.setattr(ops, "W4_PERSIST", persist)
-        outs[persist] = ops.conv2d_k3_multi(*probs())
-    (a0, b0, c0), (a1, b1, c1) = outs[False], outs[True]
-    assert torch.equal(a0, a1) and torch.equal(c0, c1) and torch.equal(b0[0], b1[0])
-    torch.testing.assert_close(b0[1][0], b1[1][0], atol=1e-6, rtol=1e-6)   # IN mean / rstd
-    torch.testing.assert_close(b0[1][1], b1[1][1], atol=1e-6, rtol=1e-6)
-    torch.testing.assert_close(a1, torch.relu(F.conv2d(xa[:, 8:], wa, ba, padding=1)), atol=1e-4, rtol=1e-4)
-    # input transform (producer InstanceNorm + ReLU applied on load), per-plane parameters
-    x = r(8, 64, 136, 240)
-    w = r(64, 64, 3, 3) / 24
-    m, s_ = r(8 * 64) * 0.1, r(8 * 64).abs() + 0.5
-    res = {}
-    for persist in (False, True):
-        monkeypatch.setattr(ops, "W4_PERSIST", persist)
-        res[persist] = ops.conv2d_k3(x, ops.wino_weights(w), in_aff=ops.Affine(m, s_, None, per_plane=True),
-                                     in_act="relu")
-    assert torch.equal(res[False], res[True])
-    xn = torch.relu((x - m.view(8, 64, 1, 1)) * s_.view(8, 64, 1, 1))
-    torch.testing.assert_close(res[True], F.conv2d(xn, w, padding=1), atol=1e-4, rtol=1e-4)
-
-
 def _pitched(x, P):
     """x [B, C, H, W] -> [B, C, H, P] with zero columns W .. P - 1."""
     out = torch.zeros(*x.shape[:3], P, device=x.device)
@@ -372,15 +297,14 @@ def _pitched(x, P):
     return out
 
 
-@pytest.mark.parametrize("persist", [False, True, "split"])
-def test_wino4_pitched_planes(monkeypatch, persist):
+@pytest.mark.parametrize("split", [False, True])
+def test_wino4_pitched_planes(monkeypatch, split):
     """F(4x4) on pitched planes (SaWinoProblem.pitch: widths 70 and 42 padded to 72 and 44, the
     booster / middlebury tiles' 1/16 GRU level): the convolution of the first W columns, the pad
     columns of the outputs left zero, InstanceNorm statistics over the W columns only, beside a
     dense problem in the same launch."""
     monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
-    monkeypatch.setattr(ops, "W4_PERSIST", persist is True)
-    monkeypatch.setattr(ops, "W4_SPLIT", persist == "split")
+    monkeypatch.setattr(ops, "W4_SPLIT", split)
     g = torch.Generator(device="cpu").manual_seed(91)
 
     def r(*s):
@@ -512,29 +436,6 @@ def test_wino4_split_weights_range(monkeypatch):
     assert float((got - ref).abs().max()) < 1e-4 * scale
 
 
-@pytest.mark.parametrize("Cin,Cout,H,W", [(64, 64, 68, 120), (128, 256, 36, 240), (256, 96, 20, 64)])
-def test_wino4_split_small_shape_matches_large(monkeypatch, Cin, Cout, H, W):
-    """The 4-wave split shape (block_shape 7: 32 tiles, 4-channel chunks, two blocks per CU) = the
-    8-wave split shape up to the accumulation order, with bias + ReLU and with an input
-    transform."""
-    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
-    monkeypatch.setattr(ops, "W4_SPLIT", True)
-    x = rnd(2, Cin, H, W, seed=Cin + H)
-    w, b = rnd(Cout, Cin, 3, 3, seed=Cout) / (3 * Cin ** 0.5), rnd(Cout, seed=5)
-    aff = ops.Affine(s=rnd(Cin, seed=6).abs() + 0.5, t=rnd(Cin, seed=7))
-    U = ops.wino_weights(w)
-    outs = []
-    for small in (0, 4096):
-        monkeypatch.setattr(ops, "W4_SPLIT_SMALL_CIN", small)
-        (y,), work = _run(monkeypatch, True, dict(x=x, U=U, bias=b, relu=True))
-        (ya,), _ = _run(monkeypatch, True, dict(x=x, U=U, in_aff=aff, in_act="relu"))
-        assert "conv2d_wino4" in work
-        outs.append((y, ya))
-    for a, c in zip(outs[0], outs[1]):
-        scale = float(a.abs().max())
-        assert float((a - c).abs().max()) < 2e-6 * scale
-
-
 def _redo_blocks(reset=True):
     from stereoanywhere_amd import _native as N
     n = int(N.lib().sa_split_redo_blocks(1 if reset else 0))
@@ -542,16 +443,14 @@ def _redo_blocks(reset=True):
     return n
 
 
-@pytest.mark.parametrize("small", [False, True])
 @pytest.mark.parametrize("mag", [300.0, 3000.0, 1e5])
-def test_wino4_split_range_guard(monkeypatch, mag, small):
+def test_wino4_split_range_guard(monkeypatch, mag):
     """Inputs whose transformed values pass the f16 range (|V| up to ~100 x the input): the split
-    kernel's range guard recomputes those blocks on fp32 MFMA products inside the launch, so the
-    output is finite and equals the fp32-product kernel; in-range blocks stay on the split path.
-    Only part of the image is scaled, so guarded and unguarded blocks share one launch.  small: the
-    4-wave split shape (block_shape 7) and its redo kernel."""
+    kernel's range guard recomputes those blocks on fp32 MFMA products inside the launch (each
+    overflowed block itself, right after its split pass), so the output is finite and equals the
+    fp32-product kernel; in-range blocks stay on the split path.  Only part of the image is scaled,
+    so guarded and unguarded blocks share one launch."""
     monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
-    monkeypatch.setattr(ops, "W4_SPLIT_SMALL_CIN", 4096 if small else 0)
     x = rnd(2, 64, 36, 256, seed=3)
     x[0, :, 4:12, 70:90] *= mag   # one region of image 0
     w = rnd(96, 64, 3, 3, seed=4) / 24
@@ -572,19 +471,17 @@ def test_wino4_split_range_guard(monkeypatch, mag, small):
     # 2 x 36 x 256 at 16 x 64 px per block and 96 / 32 channel blocks: 2 x 3 x 4 x 3 = 72 blocks;
     # the scaled region overflows (|V| >= 65520) from mag ~ 300 on: a few blocks, never all
     if mag >= 3000:
-        assert 0 < redo < (144 if small else 72), redo
+        assert 0 < redo < 72, redo
 
 
-@pytest.mark.parametrize("small", [False, True])
-def test_wino4_split_range_guard_gate_and_input_transform(monkeypatch, small):
+def test_wino4_split_range_guard_gate_and_input_transform(monkeypatch):
     """The guard ahead of the epilogues: a mode-2 gate epilogue updating h IN PLACE, and an
     input-transform launch (the producer's norm on load scaled so the staged values overflow):
     finite, blocks redone, and as close to the float64 result as the fp32-product kernel.  (Winograd
     rounding scales with the largest value of a tile, so outputs of tiles that mix the scaled values
     with unit ones err by ~1e-7 of that value in either kernel: the two are compared through their
-    error against float64, not against each other.)  small: the 4-wave split shape."""
+    error against float64, not against each other.)"""
     monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
-    monkeypatch.setattr(ops, "W4_SPLIT_SMALL_CIN", 4096 if small else 0)
     B, hd, H, W = 2, 32, 16, 64
     g = torch.Generator(device="cpu").manual_seed(7)
 
@@ -627,6 +524,42 @@ def test_wino4_split_range_guard_gate_and_input_transform(monkeypatch, small):
     print("input transform: split err", res[True][2], "fp32 err", res[False][2], "redone", res[True][1])
     assert torch.isfinite(res[True][0]).all() and res[True][1] > 0
     assert res[True][2] <= 2.5 * res[False][2] + 1e-6 * float(ref.abs().max())
+
+
+def test_wino4_split_range_guard_whole_launch(monkeypatch):
+    """The guard's worst case: every block of an xc08-sized launch (256 -> 384 channels at 136 x 240,
+    B = 4; inputs ~1e4, so every tile's transformed values overflow f16) recomputes itself on fp32
+    products inside the launch, in parallel: the result equals the fp32-product kernel's, and the
+    launch takes at most twice the fp32 kernel's time (split pass + fp32 pass per block)."""
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    x = rnd(4, 256, 136, 240, seed=11) * 1e4
+    w = rnd(384, 256, 3, 3, seed=12) / 48
+    t = {}
+    outs = {}
+    for split in (False, True):
+        monkeypatch.setattr(ops, "W4_SPLIT", split)
+        U = ops.wino_weights(w)
+        _redo_blocks()
+        (y,), work = _run(monkeypatch, True, dict(x=x, U=U))
+        assert "conv2d_wino4" in work
+        outs[split] = (y, _redo_blocks())
+        ops.conv2d_k3(x, U)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            ops.conv2d_k3(x, U)
+        e1.record()
+        torch.cuda.synchronize()
+        t[split] = e0.elapsed_time(e1) / 5
+    blocks = 4 * (-(-136 // 8)) * (-(-240 // 128)) * (384 // 32)
+    print(f"whole-launch overflow: {outs[True][1]} of {blocks} blocks redone; split {t[True]:.3f} ms, "
+          f"fp32 {t[False]:.3f} ms")
+    assert outs[True][1] >= blocks // 2 and outs[False][1] == 0
+    assert torch.isfinite(outs[True][0]).all()
+    scale = float(outs[False][0].abs().max())
+    assert float((outs[True][0] - outs[False][0]).abs().max()) < 1e-5 * scale
+    assert t[True] <= 2.0 * t[False] + 0.05, t
 
 
 @pytest.mark.parametrize("split", [False, True])
