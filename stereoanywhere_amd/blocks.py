@@ -1,5 +1,8 @@
-"""Dense convolution blocks that stay on PyTorch / MIOpen (fp32) in this tier.
+"""The model's convolution modules as parameter containers under the reference's names.
 
+The eval forward does not call their forward(): model.py / encoders.py run the convolutions on
+the HIP kernels (Winograd, implicit GEMM, direct, 3-D fused) with weights derived from these
+parameters; the module forwards remain for the training-mode path (batch-statistics BatchNorm).
 Module and parameter names reproduce the reference's state-dict layout exactly
 (tests/golden/state_dict_keys.json, 390 entries) so reference checkpoints load with
 ``strict=True`` after stripping DataParallel's ``module.`` prefix (test.py:142-152):

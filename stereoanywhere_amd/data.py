@@ -148,5 +148,10 @@ class SyntheticPairs:
 
     def __getitem__(self, i):
         p = synth.synthetic_pair(self.h, self.w, self.d, self.seed0 + i)
+        # occlusion mask (1 = occluded) as the Middlebury / Booster loaders give it: the left-view
+        # pixels whose match x - d falls outside the right image, so the harness's occ / noc metric
+        # columns are evaluated (without a mask they are NaN: guided_metrics, losses.py:311-333)
+        occ = (np.arange(self.w, dtype=np.float32)[None, :] - p["disp"] < 0).astype(np.uint8)[None]
         return {"im2": p["left"], "im3": p["right"], "im2_mono": p["mono_left"], "im3_mono": p["mono_right"],
-                "gt": p["disp"][None], "validgt": np.ones((1, self.h, self.w), np.uint8), "name": f"synthetic{i}"}
+                "gt": p["disp"][None], "validgt": np.ones((1, self.h, self.w), np.uint8), "maskocc": occ,
+                "name": f"synthetic{i}"}

@@ -314,7 +314,8 @@ class StereoAnywhere(nn.Module):
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 mono = self._mono_branch(dw, mde2, mde3, mde_lr, m2l, m3l, n2, n3, B, H4, W4)
-        # ---- context + feature encoders: convs on MIOpen fp32, epilogues fused (encoders.py)
+        # ---- context + feature encoders: 3x3 convs on the HIP Winograd / implicit-GEMM kernels,
+        # stems and stride-2 convs on the direct kernel, epilogues fused (encoders.py)
         if self.cnet.training or self.fnet.training:  # batch-statistics BatchNorm: module path
             cl = self.cnet(mde2.repeat(1, 3, 1, 1))
             hid = [torch.tanh(x[0]).contiguous() for x in cl]

@@ -87,6 +87,11 @@ def select_tiling_parameters(default_tile: int = 1024, default_overlap: int = 25
         return TilingParameters(min_tile, min_tile // 4)
     torch.cuda.synchronize(device)
     stats = torch.cuda.memory_stats(device)
+    # Deliberate parity with the reference (memory_utils.py:27-28): it reads the keys
+    # "reserved_bytes.all" / "allocated_bytes.all", which torch.cuda.memory_stats() does not have
+    # (its keys are "reserved_bytes.all.current" etc.), so `used` is always 0 and the tile size
+    # follows the total memory.  Kept so the tiling, and with it the output, equals the
+    # reference's; on an MI355X (288 GB) either reading gives the default 1024 / 256.
     used = max(stats.get("reserved_bytes.all", 0), stats.get("allocated_bytes.all", 0))
     free_mb = max(torch.cuda.get_device_properties(device).total_memory - used, 0) / 2 ** 20
     if free_mb <= 0:

@@ -21,7 +21,8 @@ def test_cli_disparity_is_the_model_forward_and_csv(tmp_path):
             "--monomodel", "synthetic", "--use_truncate_vol", "--use_aggregate_mono_vol", "--csv_path", csvp,
             "--maxdisp", "48", "--outdir", str(tmp_path / "out"), "--tries", "2"]
     mean = cli.main(args)
-    assert all(np.isfinite(mean[k]) for k in harness.METRIC_ORDER[:10])
+    # all 30 columns: the synthetic pairs carry an occlusion mask (data.SyntheticPairs)
+    assert all(np.isfinite(mean[k]) for k in harness.METRIC_ORDER), {k: mean[k] for k in harness.METRIC_ORDER}
     lines = open(csvp).read().splitlines()
     assert len(lines) == 2 and lines[0].split(",")[10:] == [k.upper() for k in harness.METRIC_ORDER]
     assert lines[1].split(",")[:10] == ["synthetic", "dataset/oak_dataset/", "synthetic", "None", "stereoanywhere",
@@ -84,5 +85,6 @@ def test_mapreduce_cli_tiled_with_guidance(tmp_path):
     mean = mr.main(["--dataset", "synthetic", "--synthetic_size", "200x320", "--synthetic_count", "1", "--iters", "3",
                     "--monomodel", "synthetic", "--tile_width", "192", "--tile_height", "128", "--overlap", "64",
                     "--use_global_guidance", "--maxdisp", "48", "--csv_path", csvp])
-    assert all(np.isfinite(mean[k]) for k in harness.METRIC_ORDER[:10])
+    # all 30 columns: the synthetic pairs carry an occlusion mask (data.SyntheticPairs)
+    assert all(np.isfinite(mean[k]) for k in harness.METRIC_ORDER), {k: mean[k] for k in harness.METRIC_ORDER}
     assert len(open(csvp).read().splitlines()) == 2
