@@ -58,7 +58,7 @@ def main():
         gates = N.SaGateEpilogue()
 
         def ig():
-            N.call("sa_conv2d_k3_igemm", 1, ctypes.addressof(prob), ctypes.addressof(gates), None, 0, 0)
+            N.call("sa_conv2d_k3_igemm", 1, ctypes.addressof(prob), ctypes.addressof(gates), 0, 0)
         U = ops.wino_weights(w)
 
         def w4():

@@ -240,21 +240,21 @@ class Hourglass(nn.Module):
         # the masked volume by its one-hot records (ops.OneHotVolume) or materialised
         orig = masked if isinstance(masked, ops.OneHotVolume) else ops.VolAct(masked)
         r = ops.conv3d(orig, fw["d00"], 16, stride=2, slope=slope)                  # down_layers[0][0]
-        r = ops.conv3d_wd(r, fw["d01_wd"], 16, slope=slope)                         # down_layers[0][1]
+        r = ops.conv3d_s1(r, fw["d01_wd"], fw.get("d01_mf"), 16, slope=slope)      # down_layers[0][1]
         down0 = gated(r, self.feature_atts[0], 1)
         r = ops.conv3d(down0, fw["d10"], 32, stride=2, slope=slope)                 # down_layers[1][0]
         r = ops.conv3d_wd(r, fw["d11_wd"], 32, slope=slope)                         # down_layers[1][1]
         down1 = gated(r, self.feature_atts[1], 2)
         # up-cat convs: the low-res branch is projected to the output channels, then upsampled
         r = ops.conv3d_pointwise_upcat(down0, down1, *fw["a10"], 16, slope=slope)  # agg_layers[1][0]
-        r = ops.conv3d_wd(r, fw["a11_wd"], 16, slope=slope)                         # agg_layers[1][1]
-        r = ops.conv3d_wd(r, fw["a12_wd"], 16, slope=slope)                         # agg_layers[1][2]
+        r = ops.conv3d_s1(r, fw["a11_wd"], fw.get("a11_mf"), 16, slope=slope)      # agg_layers[1][1]
+        r = ops.conv3d_s1(r, fw["a12_wd"], fw.get("a12_mf"), 16, slope=slope)      # agg_layers[1][2]
         x = gated(r, self.feature_atts_up[1], 1)
         r = ops.conv3d_pointwise_upcat(orig, x, *fw["fa0"], 8, slope=slope)         # final_agg[0]
-        # the stride-1 convs (8 channels at full, 16 at half, 32 at quarter resolution): F(4,3)
-        # Winograd along D
-        r = ops.conv3d_wd(r, fw["fa1_wd"], 8, slope=slope)                          # final_agg[1]
-        r = ops.conv3d_wd(r, fw["fa2_wd"], 8, slope=slope)                          # final_agg[2]
+        # the stride-1 convs: 8 -> 8 at full and 16 -> 16 at half resolution on split-f16 MFMA
+        # (conv3d_mfma.hip), 32 -> 32 and the gated classifier pair on F(4,3) Winograd along D
+        r = ops.conv3d_s1(r, fw["fa1_wd"], fw.get("fa1_mf"), 8, slope=slope)       # final_agg[1]
+        r = ops.conv3d_s1(r, fw["fa2_wd"], fw.get("fa2_mf"), 8, slope=slope)       # final_agg[2]
         r = gated(r, self.final_feature_atts_up, 0)
         vol = ops.conv3d_wd(r, fw["cls_wd"], 2, slope=slope, stats=False).raw       # both classifiers
         return vol[:, 0:1], vol[:, 1:2]
@@ -274,9 +274,10 @@ class Hourglass(nn.Module):
         fa1, fa2, cls = k3(self.final_agg[1].conv.weight), k3(self.final_agg[2].conv.weight), k3(classifiers)
         d01, a11, a12 = (k3(self.down_layers[0][1].conv.weight), k3(self.agg_layers[1][1].conv.weight),
                          k3(self.agg_layers[1][2].conv.weight))
-        wd = ops.conv3d_wd_weights
+        wd, mf = ops.conv3d_wd_weights, ops.conv3d_mf_weights
         return dict(
             fa1_wd=wd(fa1), fa2_wd=wd(fa2), cls_wd=wd(cls), d01_wd=wd(d01), a11_wd=wd(a11), a12_wd=wd(a12),
+            fa1_mf=mf(fa1), fa2_mf=mf(fa2), d01_mf=mf(d01), a11_mf=mf(a11), a12_mf=mf(a12),
             d11_wd=wd(k3(self.down_layers[1][1].conv.weight)),
             d00=k3(self.down_layers[0][0].conv.weight), d01=k3(self.down_layers[0][1].conv.weight),
             d10=k3(self.down_layers[1][0].conv.weight), d11=k3(self.down_layers[1][1].conv.weight),

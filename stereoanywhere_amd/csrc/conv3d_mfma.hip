@@ -1,0 +1,393 @@
+// Stride-1 3x3x3 convolutions of the hourglass (final_agg[1..2]: 8 -> 8 at full resolution,
+// down_layers[0][1] / agg_layers[1][1..2]: 16 -> 16 at half resolution; hourglass.py:13-91,
+// BasicConv3d submodule.py:25-53) as an implicit GEMM on v_mfma_f32_16x16x32_f16 with split
+// operands.
+//
+// Precision: every activation v = T(x) (the producer's InstanceNorm + LeakyReLU applied on load)
+// is split into f16 hi + lo (22 significant bits); every weight is scaled by 2^12 and split the
+// same way.  Each MFMA K-step accumulates hi*hi + hi*lo + lo*hi in fp32: the f16 products are
+// exact, so the sum carries ~2^-22 relative error per term - the fp32 kernels' accuracy.  No
+// range guard is needed: an InstanceNorm'ed value satisfies sum(v^2) = n var / (var + eps) <= n
+// over its n = D*H*W voxels, so |v| <= sqrt(n) < 2^15 for n < 2^30 (the host requires it), and
+// LeakyReLU only shrinks it; weights with |w| * 2^12 >= 2^15 are refused by ops.py.
+//
+// GEMM mapping (one wave, one MFMA): M = 16 consecutive output columns w, N = 16 output
+// channels x planes, K = 32 = 4 groups of 8 input channels at one input plane:
+//   * 8 -> 8: N = (2 output planes dd, 8 co), K = 4 input planes e (the pair's 3-tap D windows
+//     span 4 planes; B(e, dd) = W[kd = e - dd], zero outside 0..2): 9 K-steps per plane pair;
+//   * 16 -> 16: N = 16 co, K = (2 planes x 2 channel halves): 2 K-steps per (kh, kw), the second
+//     half-empty (its empty lanes read a zero block).
+// B (the weights) is stationary in registers for the whole kernel (72 / 144 VGPRs); A is read
+// from LDS with one ds_read_b128 per lane per operand half, at immediate offsets from a per-step
+// base: zero address arithmetic in the MFMA loop.
+//
+// Dataflow: a block owns a TH x 64 tile of (h, w) over a range of DR output planes and streams
+// the volume along D through a ring of staged input planes in LDS (the input is read once per
+// block plus a (TH+2)/TH halo in H, mostly served from L2 by the neighbouring tiles that the
+// XCD-grouped block order keeps on the same XCD).  Planes for the next step are loaded into
+// registers at the top of a step and transformed, split and written to LDS after its MFMAs.
+// Layout [B, C, D, H, W] throughout (D = W2, W = W1), as conv3d_fused.hip.
+#include <cmath>
+
+#include "sa_common.h"
+
+#pragma clang fp contract(fast)
+
+namespace {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
+
+constexpr float kWScale = 4096.0f;   // 2^12: weights -> f16 range
+constexpr int kThreads = 512;
+
+template <int CIN, int COUT>
+struct MfCfg {
+  static constexpr int DD = COUT == 8 ? 2 : 1;        // output planes per step (N = DD x co)
+  static constexpr int NCG = CIN / 8;                  // 8-channel groups
+  static constexpr int NG = (DD + 2) * NCG;            // K groups (plane, channel group) per (kh, kw)
+  static constexpr int KS = (NG + 3) / 4;              // MFMA K-steps per (kh, kw)
+  static constexpr bool ZERO = KS * 4 > NG;            // some lanes of the last K-step are empty
+  static constexpr int TH = CIN == 8 ? 8 : 4;          // output rows per block
+  static constexpr int TW = 64;                        // output columns per block
+  static constexpr int NWAVE = kThreads / 64;
+  static constexpr int MT = 4 * TH / NWAVE;            // 16-column tiles per wave
+  static constexpr int WPR = NWAVE / TH;               // waves per output row
+  static constexpr int ROWS = TH + 2, COLS = TW + 2;
+  static constexpr int PLANE = (ROWS * COLS + 15) / 16 * 16;   // 16-B entries, a multiple of 256 B
+  static constexpr int RING = 2 * DD + 2;              // planes in use (DD + 2) + filling (DD)
+  static constexpr int SLOT = NCG * 2 * PLANE;         // entries per ring slot: [cg][hl][entry]
+  static constexpr int ENTRIES = RING * SLOT + (ZERO ? 2 * PLANE : 0);
+  static constexpr int JOBS = NCG * ROWS * COLS;       // 8-channel staging jobs per plane
+  static constexpr int JPT = (JOBS * DD + kThreads - 1) / kThreads;   // jobs per thread per step
+  static_assert(ENTRIES * 16 <= 150 * 1024, "LDS");
+  static_assert(MT * WPR * 16 == TW, "tiling");
+};
+
+// n-th column of the B fragment -> (output plane offset, output channel)
+template <int COUT>
+__host__ __device__ inline void n_split(int n, int &dd, int &co) {
+  if (COUT == 8) {
+    dd = n >> 3;
+    co = n & 7;
+  } else {
+    dd = 0;
+    co = n;
+  }
+}
+
+// [Cin][27][Cout] fp32 (ops.conv3d layout) -> the per-lane B fragments [9 (kh,kw)][KS][hl][64][8]
+template <int CIN, int COUT>
+__global__ void mf_weights_kernel(const float *__restrict__ w, f16x8 *__restrict__ tab) {
+  using C = MfCfg<CIN, COUT>;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // ((khw * KS + t) * 64 + lane)
+  if (i >= 9 * C::KS * 64) return;
+  const int lane = i & 63, t = (i >> 6) % C::KS, khw = (i >> 6) / C::KS;
+  const int n = lane & 15, G = 4 * t + (lane >> 4);
+  int dd, co;
+  n_split<COUT>(n, dd, co);
+  const int e = G / C::NCG, cg = G % C::NCG, kd = e - dd;
+  f16x8 hi, lo;
+  for (int j = 0; j < 8; ++j) {
+    float v = 0.0f;
+    if (G < C::NG && kd >= 0 && kd <= 2) v = w[((8 * cg + j) * 27 + kd * 9 + khw) * COUT + co] * kWScale;
+    const _Float16 h = (_Float16)v;
+    hi[j] = h;
+    lo[j] = (_Float16)(v - (float)h);
+  }
+  tab[((khw * C::KS + t) * 2 + 0) * 64 + lane] = hi;
+  tab[((khw * C::KS + t) * 2 + 1) * 64 + lane] = lo;
+}
+
+template <int CIN, int COUT>
+__global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3d_mf_kernel(const float *__restrict__ in, int D, int H, int W,
+                                                                const f16x8 *__restrict__ wtab,
+                                                                const float *__restrict__ mean,
+                                                                const float *__restrict__ rstd, float slope,
+                                                                float *__restrict__ out, double *__restrict__ partial,
+                                                                int tilesW, int tilesH, int tilesD, int DR) {
+  using C = MfCfg<CIN, COUT>;
+  __shared__ f16x8 lds[C::ENTRIES];
+  __shared__ float2 nrm[CIN];
+  __shared__ double red[C::NWAVE][COUT][2];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wid = (int)sa::xcd_remap(blockIdx.x, gridDim.x);
+  const int bx = wid % tilesW, by = (wid / tilesW) % tilesH, dz = (wid / (tilesW * tilesH)) % tilesD;
+  const int b = wid / (tilesW * tilesH * tilesD);
+  const int w0 = bx * C::TW, h0 = by * C::TH, d0 = dz * DR, d1 = min(d0 + DR, D);
+  const long HW = (long)H * W;
+
+  if (tid < CIN) nrm[tid] = make_float2(mean[b * CIN + tid], rstd[b * CIN + tid]);
+  if constexpr (C::ZERO)
+    for (int i = tid; i < 2 * C::PLANE; i += kThreads) lds[C::RING * C::SLOT + i] = f16x8{};
+
+  // B fragments for the whole kernel
+  f16x8 bw[9][C::KS][2];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int t = 0; t < C::KS; ++t)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) bw[k][t][hl] = wtab[((k * C::KS + t) * 2 + hl) * 64 + lane];
+  __syncthreads();   // nrm
+
+  // staging: job J of plane p -> (cg, row, col) of the (TH + 2) x 66 window at (h0 - 1, w0 - 1)
+  auto job_src = [&](int J, int p, long &src, bool &ok, int &dst, int &cg) {
+    cg = J / (C::ROWS * C::COLS);
+    const int e = J % (C::ROWS * C::COLS), row = e / C::COLS, col = e % C::COLS;
+    const int h = h0 - 1 + row, w = w0 - 1 + col;
+    ok = p >= 0 && p < D && h >= 0 && h < H && w >= 0 && w < W;
+    src = ok ? (((long)b * CIN + 8 * cg) * D + p) * HW + (long)h * W + w : 0;
+    dst = ((((p + C::RING) % C::RING) * C::NCG + cg) * 2) * C::PLANE + e;
+  };
+  auto put = [&](const float (&x)[8], bool ok, int dst, int cg) {
+    f16x8 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float2 nr = nrm[8 * cg + j];
+      float v = (x[j] - nr.x) * nr.y;
+      v = v > 0.0f ? v : v * slope;
+      v = ok ? v : 0.0f;   // zero padding of the activated input
+      const _Float16 h = (_Float16)v;
+      hi[j] = h;
+      lo[j] = (_Float16)(v - (float)h);
+    }
+    lds[dst] = hi;
+    lds[dst + C::PLANE] = lo;
+  };
+  // (a padding job reads channel j of voxel 0, in bounds, and put() zeroes it)
+  auto load8 = [&](long src, float (&x)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = in[src + (long)j * D * HW];
+  };
+
+  // prologue: planes d0 - 1 .. d0 + DD
+  for (int J = tid; J < (C::DD + 2) * C::JOBS; J += kThreads) {
+    long src;
+    bool ok;
+    int dst, cg;
+    job_src(J % C::JOBS, d0 - 1 + J / C::JOBS, src, ok, dst, cg);
+    float x[8];
+    load8(src, x);
+    put(x, ok, dst, cg);
+  }
+  __syncthreads();
+
+  // this wave's output row and columns; the lane's A row (m) and K group (g)
+  const int r = wv / C::WPR, mt0 = (wv % C::WPR) * C::MT;
+  const int m = lane & 15, g = lane >> 4;
+  const int h = h0 + r;
+  int dd_l, co_l;
+  n_split<COUT>(m, dd_l, co_l);   // the lane's accumulator column n = lane & 15
+  const int wl = w0 + 16 * mt0 + 4 * g;   // + 16 mt + j: the lane's accumulator rows
+  const bool vec = (W & 3) == 0;
+  double s_acc = 0.0, q_acc = 0.0;
+
+  for (int dout = d0; dout < d1; dout += C::DD) {
+    const bool more = dout + C::DD < d1;
+    // next step's planes dout + DD + 1 .. dout + 2 DD -> registers
+    float xs[C::JPT][8];
+    long srcs[C::JPT];
+    bool oks[C::JPT];
+    int dsts[C::JPT], cgs[C::JPT];
+#pragma unroll
+    for (int k = 0; k < C::JPT; ++k) {
+      const int J = tid + k * kThreads;
+      srcs[k] = 0;
+      oks[k] = false;
+      dsts[k] = -1;
+      cgs[k] = 0;
+      if (more && J < C::DD * C::JOBS) {
+        job_src(J % C::JOBS, dout + C::DD + 1 + J / C::JOBS, srcs[k], oks[k], dsts[k], cgs[k]);
+        load8(srcs[k], xs[k]);
+      }
+    }
+
+    // the lane's A bases per K-step: group G = 4 t + g -> (plane e, channel group cg)
+    int base[C::KS];
+#pragma unroll
+    for (int t = 0; t < C::KS; ++t) {
+      const int G = 4 * t + g, e = G / C::NCG, cg = G % C::NCG;
+      const int slot = (dout - 1 + e + C::RING) % C::RING;
+      base[t] = G < C::NG ? ((slot * C::NCG + cg) * 2) * C::PLANE : C::RING * C::SLOT;
+      base[t] += r * C::COLS + 16 * mt0 + m;
+    }
+    f32x4 acc[C::MT];
+#pragma unroll
+    for (int u = 0; u < C::MT; ++u) acc[u] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    // A fragments one (kh, kw, t) step ahead: the MFMAs of a step overlap the next step's reads
+    constexpr int NK = 9 * C::KS;
+    f16x8 ah[2][C::MT], al[2][C::MT];
+    auto fetch = [&](int kk, f16x8 (&h_)[C::MT], f16x8 (&l_)[C::MT]) {
+      const int t = kk % C::KS, k = kk / C::KS, kh = k / 3, kw = k % 3;
+#pragma unroll
+      for (int u = 0; u < C::MT; ++u) {
+        const f16x8 *a = lds + base[t] + kh * C::COLS + kw + 16 * u;
+        h_[u] = a[0];
+        l_[u] = a[C::PLANE];
+      }
+    };
+    fetch(0, ah[0], al[0]);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * C::MT, 0);
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      const int cur = kk & 1;
+      if (kk + 1 < NK) fetch(kk + 1, ah[cur ^ 1], al[cur ^ 1]);
+      const int t = kk % C::KS, k = kk / C::KS;
+#pragma unroll
+      for (int u = 0; u < C::MT; ++u) {
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cur][u], bw[k][t][0], acc[u], 0, 0, 0);
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cur][u], bw[k][t][1], acc[u], 0, 0, 0);
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[cur][u], bw[k][t][0], acc[u], 0, 0, 0);
+      }
+      // (the default schedule sinks every read next to its MFMA and waits on it)
+      if (kk + 1 < NK) __builtin_amdgcn_sched_group_barrier(0x100, 2 * C::MT, 0);   // DS reads
+      __builtin_amdgcn_sched_group_barrier(0x008, 3 * C::MT, 0);                     // MFMAs
+    }
+
+    // epilogue: the lane holds out[b][co][dout + dd][h][wl + 16 u + j], j = 0..3
+    const int d = dout + dd_l;
+    if (d < d1 && h < H) {
+      float s = 0.0f, q = 0.0f;
+      float *o = out + (((long)b * COUT + co_l) * D + d) * HW + (long)h * W;
+#pragma unroll
+      for (int u = 0; u < C::MT; ++u) {
+        const int w = wl + 16 * u;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = acc[u][j] * (1.0f / kWScale);
+        if (vec && w + 3 < W) {
+          *reinterpret_cast<float4 *>(o + w) = make_float4(v[0], v[1], v[2], v[3]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            s += v[j];
+            q += v[j] * v[j];
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (w + j < W) {
+              o[w + j] = v[j];
+              s += v[j];
+              q += v[j] * v[j];
+            }
+        }
+      }
+      s_acc += (double)s;
+      q_acc += (double)q;
+    }
+
+    // next step's planes -> LDS (their slots held planes only the previous step read)
+    if (more) {
+#pragma unroll
+      for (int k = 0; k < C::JPT; ++k)
+        if (dsts[k] >= 0) put(xs[k], oks[k], dsts[k], cgs[k]);
+    }
+    __syncthreads();
+  }
+
+  // InstanceNorm partials: lanes n, n + 16, n + 32, n + 48 (and n + 8 for the plane pairs)
+  // share an output channel
+  if (partial) {
+#pragma unroll
+    for (int o = COUT == 8 ? 8 : 16; o < 64; o <<= 1) {
+      s_acc += __shfl_xor(s_acc, o);
+      q_acc += __shfl_xor(q_acc, o);
+    }
+    if (lane < COUT) {
+      red[wv][lane][0] = s_acc;
+      red[wv][lane][1] = q_acc;
+    }
+    __syncthreads();
+    if (tid < COUT) {
+      double a = 0.0, e = 0.0;
+#pragma unroll
+      for (int k = 0; k < C::NWAVE; ++k) {
+        a += red[k][tid][0];
+        e += red[k][tid][1];
+      }
+      const int nparts = tilesW * tilesH * tilesD;
+      const int blk = (dz * tilesH + by) * tilesW + bx;
+      double *p = partial + (((long)b * COUT + tid) * nparts + blk) * 2;
+      p[0] = a;
+      p[1] = e;
+    }
+  }
+}
+
+int g_mf_dr = 0;   // sa_conv3d_mf_set_planes: 0 = automatic
+
+struct MfGeo {
+  int tilesW, tilesH, tilesD, DR;
+};
+
+inline bool mf_shape(int Cin, int Cout) { return (Cin == 8 && Cout == 8) || (Cin == 16 && Cout == 16); }
+
+MfGeo mf_geo(int B, int Cin, int D, int H, int W) {
+  const int th = Cin == 8 ? 8 : 4, dd = Cin == 8 ? 2 : 1;
+  MfGeo g{(W + 63) / 64, (H + th - 1) / th, 1, 0};
+  int dr = g_mf_dr > 0 ? g_mf_dr : D;
+  if (g_mf_dr <= 0) {
+    // halve the planes per block until the grid fills the chip ~8 times (or 8 planes)
+    const long per = (long)B * g.tilesW * g.tilesH;
+    while (dr > 8 && per * ((D + dr - 1) / dr) < 8 * 256) dr = (dr + 1) / 2;
+  }
+  dr = (dr + dd - 1) / dd * dd;
+  g.DR = dr;
+  g.tilesD = (D + dr - 1) / dr;
+  return g;
+}
+
+}  // namespace
+
+extern "C" void sa_conv3d_mf_set_planes(int planes) { g_mf_dr = planes; }
+
+extern "C" long sa_conv3d_mf_weights_size(int Cin, int Cout) {
+  if (!mf_shape(Cin, Cout)) return -1;
+  const int ks = Cin == 8 ? MfCfg<8, 8>::KS : MfCfg<16, 16>::KS;
+  return 9L * ks * 2 * 64 * 16;
+}
+
+extern "C" int sa_conv3d_mf_weights(const float *weight, int Cin, int Cout, void *table, void *stream) {
+  SA_REQUIRE(weight && table, "sa_conv3d_mf_weights: null pointer");
+  SA_REQUIRE(mf_shape(Cin, Cout), "sa_conv3d_mf_weights: built for 8 -> 8 and 16 -> 16 (got %d -> %d)", Cin, Cout);
+  hipStream_t s = sa::as_stream(stream);
+  f16x8 *t = reinterpret_cast<f16x8 *>(table);
+  if (Cin == 8)
+    mf_weights_kernel<8, 8><<<(9 * MfCfg<8, 8>::KS * 64 + 255) / 256, 256, 0, s>>>(weight, t);
+  else
+    mf_weights_kernel<16, 16><<<(9 * MfCfg<16, 16>::KS * 64 + 255) / 256, 256, 0, s>>>(weight, t);
+  return sa::check_launch("sa_conv3d_mf_weights");
+}
+
+extern "C" long sa_conv3d_mf_stat_parts(int B, int Cin, int Cout, int D, int H, int W) {
+  if (!mf_shape(Cin, Cout) || B <= 0 || D <= 0 || H <= 0 || W <= 0) return -1;
+  const MfGeo g = mf_geo(B, Cin, D, H, W);
+  return (long)g.tilesW * g.tilesH * g.tilesD;
+}
+
+extern "C" int sa_conv3d_mf(const float *in, int B, int Cin, int D, int H, int W, const void *table, int Cout,
+                            const float *in_mean, const float *in_rstd, float slope, float *out,
+                            double *stats_partial, void *stream) {
+  SA_REQUIRE(in && table && out && in_mean && in_rstd, "sa_conv3d_mf: null pointer");
+  SA_REQUIRE(B > 0 && D > 0 && H > 0 && W > 0, "sa_conv3d_mf: empty shape");
+  SA_REQUIRE(mf_shape(Cin, Cout), "sa_conv3d_mf: built for 8 -> 8 and 16 -> 16 (got %d -> %d)", Cin, Cout);
+  // |InstanceNorm'ed value| <= sqrt(voxels) < 2^15: the f16 hi part cannot overflow
+  SA_REQUIRE((long)D * H * W < (1L << 30), "sa_conv3d_mf: a channel volume must hold < 2^30 voxels");
+  SA_REQUIRE((long)B * Cin * D * H * W < (1L << 62), "sa_conv3d_mf: size");
+  const MfGeo g = mf_geo(B, Cin, D, H, W);
+  const long blocks = (long)B * g.tilesW * g.tilesH * g.tilesD;
+  SA_REQUIRE(blocks < (1L << 31), "sa_conv3d_mf: grid");
+  hipStream_t s = sa::as_stream(stream);
+  sa::TimingScope ts(SA_K_CONV3D, s);
+  const f16x8 *t = reinterpret_cast<const f16x8 *>(table);
+  if (Cin == 8)
+    conv3d_mf_kernel<8, 8><<<(unsigned)blocks, kThreads, 0, s>>>(in, D, H, W, t, in_mean, in_rstd, slope, out,
+                                                                 stats_partial, g.tilesW, g.tilesH, g.tilesD, g.DR);
+  else
+    conv3d_mf_kernel<16, 16><<<(unsigned)blocks, kThreads, 0, s>>>(in, D, H, W, t, in_mean, in_rstd, slope, out,
+                                                                   stats_partial, g.tilesW, g.tilesH, g.tilesD, g.DR);
+  return sa::check_launch("sa_conv3d_mf");
+}

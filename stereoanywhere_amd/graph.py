@@ -49,7 +49,7 @@ class ForwardGraph:
                            for name in ("sa_lookup_get_mfma", "sa_softargmin_get_one_pass", "sa_conv3d_wd_get_variant"))
         return (tuple((tuple(x.shape), x.dtype, x.device) for x in xs), iters, dataclasses.astuple(m.opts),
                 m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_SPLIT, ops.IGEMM, ops.IGEMM_MAX_WORK,
-                                                   ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS, ops.SPLIT_GUARD),
+                                                   ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS, ops.SPLIT_GUARD, ops.CONV3D_MFMA),
                 c_switches, args)
 
     def __call__(self, image2, image3, mde2, mde3, iters: int = 12, test_mode: bool = True):

@@ -647,6 +647,53 @@ def conv3d_wd(x: "VolAct", w_wd: torch.Tensor, cout: int, slope: float = 0.01, s
     return VolAct(out, norm, act=stats)
 
 
+# the stride-1 hourglass convs 8 -> 8 and 16 -> 16 on the split-f16 MFMA kernel (conv3d_mfma.hip)
+# instead of the F(4,3)-along-D VALU kernel (conv3d_wd)
+CONV3D_MFMA = True
+_MF_MAX_W = 8.0   # |w| * 2^12 < 2^15: the split weight's hi part stays in f16 range
+
+
+def conv3d_mf_weights(w_t: torch.Tensor):
+    """[Cin][27][Cout] 3x3x3 kernel (ops.conv3d layout) -> sa_conv3d_mf's B-fragment table, or
+    None when the shape has no MFMA kernel or a weight is out of the split range."""
+    _check(w_t, "w_t")
+    cin, _, cout = w_t.shape
+    n = int(N.lib().sa_conv3d_mf_weights_size(cin, cout))
+    if n < 0 or not bool((w_t.abs() < _MF_MAX_W).all()):
+        return None
+    table = torch.empty((n,), device=w_t.device, dtype=torch.uint8)
+    N.call("sa_conv3d_mf_weights", w_t.data_ptr(), cin, cout, table.data_ptr(), _stream(table))
+    return table
+
+
+def conv3d_mf(x: "VolAct", table: torch.Tensor, cout: int, slope: float = 0.01, stats: bool = True) -> "VolAct":
+    """ops.conv3d at stride 1 for 8 -> 8 and 16 -> 16 on split-f16 MFMA (sa_conv3d_mf); the
+    input must carry an InstanceNorm + LeakyReLU and no gate; table from conv3d_mf_weights."""
+    _check(x.raw, "x")
+    if x.norm is None or not x.act or x.gate is not None:
+        raise ValueError("conv3d_mf: built for an InstanceNorm + LeakyReLU producer without gate")
+    B, Cin, D, H, W = x.raw.shape
+    out = torch.empty((B, cout, D, H, W), device=x.raw.device, dtype=torch.float32)
+    parts = int(N.lib().sa_conv3d_mf_stat_parts(B, Cin, cout, D, H, W))
+    if parts < 0:
+        raise ValueError(f"conv3d_mf: no kernel for {Cin} -> {cout}")
+    partial = torch.empty((B * cout * parts * 2,), device=out.device, dtype=torch.float64) if stats else None
+    mean, rstd = x.norm
+    N.call("sa_conv3d_mf", x.raw.data_ptr(), B, Cin, D, H, W, table.data_ptr(), cout, mean.data_ptr(),
+           rstd.data_ptr(), slope, out.data_ptr(), _ptr(partial), _stream(out))
+    norm = instnorm_finalize(partial, B * cout, parts, D * H * W) if stats else None
+    return VolAct(out, norm, act=stats)
+
+
+def conv3d_s1(x: "VolAct", w_wd: torch.Tensor, table, cout: int, slope: float = 0.01,
+              stats: bool = True) -> "VolAct":
+    """The hourglass's stride-1 conv: conv3d_mf where it applies (CONV3D_MFMA, a table, no gate),
+    else conv3d_wd."""
+    if CONV3D_MFMA and table is not None and x.gate is None and x.norm is not None and x.act:
+        return conv3d_mf(x, table, cout, slope, stats)
+    return conv3d_wd(x, w_wd, cout, slope, stats)
+
+
 def _conv3d_onehot(x: OneHotVolume, w_t: torch.Tensor, cout: int, stride: int, stats: bool):
     _check(w_t, "w_t")
     B, nb, D, H, W = x.shape
