@@ -119,9 +119,13 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
   const int w0 = bx * C::TW, h0 = by * C::TH, d0 = dz * DR, d1 = min(d0 + DR, D);
   const long HW = (long)H * W;
 
-  if (tid < CIN) nrm[tid] = make_float2(mean[b * CIN + tid], rstd[b * CIN + tid]);
-  if constexpr (C::ZERO)
-    for (int i = tid; i < 2 * C::PLANE; i += kThreads) lds[C::RING * C::SLOT + i] = f16x8{};
+  // T(x) = lrelu(x * rstd - mean * rstd); the whole ring starts zeroed: entries outside H x W
+  // (the zero padding) are never written again
+  if (tid < CIN) {
+    const float rs = rstd[b * CIN + tid];
+    nrm[tid] = make_float2(rs, -mean[b * CIN + tid] * rs);
+  }
+  for (int i = tid; i < C::ENTRIES; i += kThreads) lds[i] = f16x8{};
 
   // B fragments for the whole kernel
   f16x8 bw[9][C::KS][2];
@@ -131,47 +135,66 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
     for (int t = 0; t < C::KS; ++t)
 #pragma unroll
       for (int hl = 0; hl < 2; ++hl) bw[k][t][hl] = wtab[((k * C::KS + t) * 2 + hl) * 64 + lane];
-  __syncthreads();   // nrm
 
-  // staging: job J of plane p -> (cg, row, col) of the (TH + 2) x 66 window at (h0 - 1, w0 - 1)
-  auto job_src = [&](int J, int p, long &src, bool &ok, int &dst, int &cg) {
-    cg = J / (C::ROWS * C::COLS);
-    const int e = J % (C::ROWS * C::COLS), row = e / C::COLS, col = e % C::COLS;
-    const int h = h0 - 1 + row, w = w0 - 1 + col;
-    ok = p >= 0 && p < D && h >= 0 && h < H && w >= 0 && w < W;
-    src = ok ? (((long)b * CIN + 8 * cg) * D + p) * HW + (long)h * W + w : 0;
-    dst = ((((p + C::RING) % C::RING) * C::NCG + cg) * 2) * C::PLANE + e;
-  };
-  auto put = [&](const float (&x)[8], bool ok, int dst, int cg) {
-    f16x8 hi, lo;
+  // the thread's staging jobs, the same for every group of DD planes: job J = tid + 512 k ->
+  // (plane q of the group, channel group cg, entry (row, col) of the (TH+2) x 66 window at
+  // (h0 - 1, w0 - 1)); jobs outside H x W are dropped
+  long joff[C::JPT];
+  int jdst[C::JPT], jq[C::JPT], jcg[C::JPT];
+  bool jok[C::JPT];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float2 nr = nrm[8 * cg + j];
-      float v = (x[j] - nr.x) * nr.y;
-      v = v > 0.0f ? v : v * slope;
-      v = ok ? v : 0.0f;   // zero padding of the activated input
-      const _Float16 h = (_Float16)v;
-      hi[j] = h;
-      lo[j] = (_Float16)(v - (float)h);
+  for (int k = 0; k < C::JPT; ++k) {
+    const int J = tid + k * kThreads;
+    const int q = J / C::JOBS, r_ = J % C::JOBS, cg = r_ / (C::ROWS * C::COLS), e = r_ % (C::ROWS * C::COLS);
+    const int hh = h0 - 1 + e / C::COLS, ww = w0 - 1 + e % C::COLS;
+    jok[k] = J < C::DD * C::JOBS && hh >= 0 && hh < H && ww >= 0 && ww < W;
+    joff[k] = jok[k] ? ((long)b * CIN + 8 * cg) * D * HW + (long)hh * W + ww : 0;
+    jdst[k] = cg * 2 * C::PLANE + e;
+    jq[k] = q;
+    jcg[k] = cg;
+  }
+  // planes p0 .. p0 + DD - 1: loads into registers, then transform + split into their ring slots
+  auto stage_load = [&](int p0, float (&x)[C::JPT][8]) {
+#pragma unroll
+    for (int k = 0; k < C::JPT; ++k) {
+      const int p = p0 + jq[k];
+      if (jok[k] && p >= 0 && p < D) {
+        const float *src = in + joff[k] + (long)p * HW;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[k][j] = src[(long)j * D * HW];
+      }
     }
-    lds[dst] = hi;
-    lds[dst + C::PLANE] = lo;
   };
-  // (a padding job reads channel j of voxel 0, in bounds, and put() zeroes it)
-  auto load8 = [&](long src, float (&x)[8]) {
+  auto stage_put = [&](int p0, const float (&x)[C::JPT][8]) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = in[src + (long)j * D * HW];
+    for (int k = 0; k < C::JPT; ++k) {
+      if (!jok[k]) continue;
+      const int p = p0 + jq[k];
+      f16x8 hi{}, lo{};
+      if (p >= 0 && p < D) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float2 nr = nrm[8 * jcg[k] + j];
+          float v = __builtin_fmaf(x[k][j], nr.x, nr.y);
+          v = fmaxf(v, v * slope);   // LeakyReLU for 0 <= slope <= 1 (NaN stays NaN)
+          const _Float16 h = (_Float16)v;
+          hi[j] = h;
+          lo[j] = (_Float16)(v - (float)h);
+        }
+      }
+      const int dst = ((p + C::RING) % C::RING) * C::SLOT + jdst[k];
+      lds[dst] = hi;
+      lds[dst + C::PLANE] = lo;
+    }
   };
+  __syncthreads();   // nrm, ring zeroed
 
   // prologue: planes d0 - 1 .. d0 + DD
-  for (int J = tid; J < (C::DD + 2) * C::JOBS; J += kThreads) {
-    long src;
-    bool ok;
-    int dst, cg;
-    job_src(J % C::JOBS, d0 - 1 + J / C::JOBS, src, ok, dst, cg);
-    float x[8];
-    load8(src, x);
-    put(x, ok, dst, cg);
+#pragma unroll 1
+  for (int p0 = d0 - 1; p0 < d0 + C::DD + 1; p0 += C::DD) {
+    float x[C::JPT][8];
+    stage_load(p0, x);
+    stage_put(p0, x);
   }
   __syncthreads();
 
@@ -189,21 +212,7 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
     const bool more = dout + C::DD < d1;
     // next step's planes dout + DD + 1 .. dout + 2 DD -> registers
     float xs[C::JPT][8];
-    long srcs[C::JPT];
-    bool oks[C::JPT];
-    int dsts[C::JPT], cgs[C::JPT];
-#pragma unroll
-    for (int k = 0; k < C::JPT; ++k) {
-      const int J = tid + k * kThreads;
-      srcs[k] = 0;
-      oks[k] = false;
-      dsts[k] = -1;
-      cgs[k] = 0;
-      if (more && J < C::DD * C::JOBS) {
-        job_src(J % C::JOBS, dout + C::DD + 1 + J / C::JOBS, srcs[k], oks[k], dsts[k], cgs[k]);
-        load8(srcs[k], xs[k]);
-      }
-    }
+    if (more) stage_load(dout + C::DD + 1, xs);
 
     // the lane's A bases per K-step: group G = 4 t + g -> (plane e, channel group cg)
     int base[C::KS];
@@ -280,11 +289,7 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
     }
 
     // next step's planes -> LDS (their slots held planes only the previous step read)
-    if (more) {
-#pragma unroll
-      for (int k = 0; k < C::JPT; ++k)
-        if (dsts[k] >= 0) put(xs[k], oks[k], dsts[k], cgs[k]);
-    }
+    if (more) stage_put(dout + C::DD + 1, xs);
     __syncthreads();
   }
 
@@ -376,6 +381,7 @@ extern "C" int sa_conv3d_mf(const float *in, int B, int Cin, int D, int H, int W
   SA_REQUIRE(mf_shape(Cin, Cout), "sa_conv3d_mf: built for 8 -> 8 and 16 -> 16 (got %d -> %d)", Cin, Cout);
   // |InstanceNorm'ed value| <= sqrt(voxels) < 2^15: the f16 hi part cannot overflow
   SA_REQUIRE((long)D * H * W < (1L << 30), "sa_conv3d_mf: a channel volume must hold < 2^30 voxels");
+  SA_REQUIRE(slope >= 0.0f && slope <= 1.0f, "sa_conv3d_mf: LeakyReLU slope must lie in [0, 1]");
   SA_REQUIRE((long)B * Cin * D * H * W < (1L << 62), "sa_conv3d_mf: size");
   const MfGeo g = mf_geo(B, Cin, D, H, W);
   const long blocks = (long)B * g.tilesW * g.tilesH * g.tilesD;
