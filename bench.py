@@ -443,6 +443,9 @@ def main():
     ap.add_argument("--igemm", type=int, default=None, choices=[0, 1],
                     help="3x3 convs on the implicit-GEMM kernel where it applies (1) or on the Winograd kernels "
                          "only (0); default: ops.IGEMM")
+    ap.add_argument("--conv3d-mfma", type=int, default=None, choices=[0, 1],
+                    help="the hourglass's stride-1 8->8 / 16->16 convs on split-f16 MFMA (1) or on the F(4,3) "
+                         "VALU kernel (0); default: ops.CONV3D_MFMA")
     ap.add_argument("--igemm-max-work", type=int, default=None,
                     help="implicit GEMM only for launches of at most this many output pixels x channels "
                          "(ops.IGEMM_MAX_WORK)")
@@ -494,6 +497,8 @@ def main():
         ops.W4_SPLIT = bool(args.w4_split)
     if args.igemm is not None:
         ops.IGEMM = bool(args.igemm)
+    if args.conv3d_mfma is not None:
+        ops.CONV3D_MFMA = bool(args.conv3d_mfma)
     if args.igemm_max_work is not None:
         ops.IGEMM_MAX_WORK = args.igemm_max_work
     if args.direct_split is not None:

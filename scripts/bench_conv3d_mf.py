@@ -3,7 +3,7 @@
 over a sweep of planes per block, against the F(4,3)-along-D kernel (sa_conv3d_wd); time (HIP
 events around `reps` launches), effective HBM rate of the algorithmic bytes (input + output once)
 and max |difference| between the two.
-usage: python scripts/bench_conv3d_mf.py [reps] [--planes=a,b,...]"""
+usage: python scripts/bench_conv3d_mf.py [reps] [--planes=a,b,...] [--only=final_agg|agg16]"""
 import os
 import sys
 
@@ -30,12 +30,17 @@ def timed(fn, reps):
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else 10
     planes = [0]
+    only = None
     for a in sys.argv[1:]:
         if a.startswith("--planes="):
             planes = [int(v) for v in a.split("=", 1)[1].split(",")]
+        if a.startswith("--only="):
+            only = a.split("=", 1)[1]
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     for cin, (B, D, H, W), tag in SHAPES:
+        if only and tag != only:
+            continue
         x = torch.randn(B, cin, D, H, W, device=dev)
         mean = torch.randn(B * cin, device=dev) * 0.1
         rstd = torch.rand(B * cin, device=dev) + 0.5

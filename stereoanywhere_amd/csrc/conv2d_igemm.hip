@@ -423,9 +423,7 @@ __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, con
       // loads (top of 2j + 3; job 3 at the end of position 8).  So the loads issued after this
       // position's weights are the next position's weights and, after an even position, a patch
       // job; on an odd position that waits for the job loaded at the end of p - 3 as well.
-      if (pos == 8 && !more) {   // the last chunk issues no weights past its end: nothing younger
-        wait_w(std::integral_constant<int, 0>{}, w);
-      } else if ((pos & 1) && (pos - 1) / 2 < XJOBS) {
+      if ((pos & 1) && (pos - 1) / 2 < XJOBS) {
         wait_w(std::integral_constant<int, 12>{}, w);
         if (pos >= 3 && (pos - 3) / 2 < XJOBS) {
           wait_x(std::integral_constant<int, 12>{}, xv[((pos - 3) / 2) & 1]);   // (ties the job's registers)
@@ -481,9 +479,10 @@ __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, con
           c2 += 1;
         }
         t2 = t2 >= 9 ? t2 - 9 : t2;
-        // (past the last chunk nothing is loaded: an asm load left in flight into registers the
-        // compiler considers dead could land on whatever it reuses them for)
-        if (IG_DIAG != 1 && IG_DIAG != 4 && (pos < 7 || more)) wload(wr[(pos + 2) % 3], c2 * 9 + t2);
+        // (past the last chunk: clamped re-reads, so that every position's wait count is static;
+        // no branch on `more` around a wait: the compiler once merged such paths with register
+        // copies of loads still in flight, scripts/check_asm_loads.py)
+        if (IG_DIAG != 1 && IG_DIAG != 4) wload(wr[(pos + 2) % 3], c2 * 9 + t2);
         else {   // (diagnostic: the same random operands, no loads)
 #pragma unroll
           for (int hl = 0; hl < 2; ++hl)
@@ -498,7 +497,17 @@ __device__ __forceinline__ void ig_body(const IgProb &P, const IgGate *gate, con
     }
     if (IG_DIAG != 3 && IG_DIAG != 4) __syncthreads();   // chunk kc + 1's patch is written; chunk kc's buffer is free
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (nothing in flight past the loop)
+  // nothing in flight past the loop; the wait names every register an asm load may still be
+  // writing (so none of them is dead, copied or reused before it)
+  asm volatile("s_waitcnt vmcnt(0)"
+               : "+v"(wr[0][0][0]), "+v"(wr[0][0][1]), "+v"(wr[0][1][0]), "+v"(wr[0][1][1]), "+v"(wr[1][0][0]),
+                 "+v"(wr[1][0][1]), "+v"(wr[1][1][0]), "+v"(wr[1][1][1]), "+v"(wr[2][0][0]), "+v"(wr[2][0][1]),
+                 "+v"(wr[2][1][0]), "+v"(wr[2][1][1])
+               :
+               : "memory");
+  asm volatile("" : "+v"(xv[0][0]), "+v"(xv[0][1]), "+v"(xv[0][2]), "+v"(xv[0][3]), "+v"(xv[0][4]), "+v"(xv[0][5]),
+               "+v"(xv[0][6]), "+v"(xv[0][7]), "+v"(xv[1][0]), "+v"(xv[1][1]), "+v"(xv[1][2]), "+v"(xv[1][3]),
+               "+v"(xv[1][4]), "+v"(xv[1][5]), "+v"(xv[1][6]), "+v"(xv[1][7]));
   if (pass == 1 || !guard || !__syncthreads_or(bad)) break;
   // the block's largest finite input: wave maxima through LDS (the patch buffers are free)
   {

@@ -42,10 +42,11 @@
                        // 8 neither row nor column pass (no input transform)
 #endif
 #ifndef SA_W4_GJB
-#define SA_W4_GJB 8    // gate-epilogue store iterations whose plane loads go out together (mode 2)
+#define SA_W4_GJB 4    // gate-epilogue store iterations whose plane loads go out together (mode 2)
 #endif
 #ifndef SA_W4_GJB1
-#define SA_W4_GJB1 16  // the same for mode 1
+#define SA_W4_GJB1 8   // the same for mode 1 (8 / 16 measured the same, 49.99 vs 50.01 ms/step, but
+                       // with them the range guard's second body made the gated kernel spill 2 KiB)
 #endif
 
 namespace {
@@ -66,11 +67,8 @@ constexpr int NPT = 36;                   // transform points
 // (Measured slower and removed, in git history: a wide 64-channel shape, a quadrant shape, a
 // persistent kernel, the split products on the small shape, and the K = 32 / duplicated-read split
 // forms)
-template <int NW_, int KC_, bool SPLIT_ = false, bool UNSPLIT_ = false>
+template <int NW_, int KC_, bool SPLIT_ = false>
 struct W4Cfg {
-  // UNSPLIT: fp32 MFMA products with the split kernel's (hi, lo) filter dwords read as hi + lo (the
-  // range guard's recompute of an overflowed block, wino_f4k3_kernel)
-  static constexpr bool UNSPLIT = UNSPLIT_;
   // SPLIT: the products on f16 MFMA with hi/lo operand pairs (W4Split below)
   static constexpr bool SPLIT = SPLIT_;
   static constexpr int NW = NW_, NTHR = 64 * NW_, TG = NW_ / 2, NT = 16 * TG, KC = KC_, JPC = KC_ / 4;
@@ -164,7 +162,7 @@ struct W4Launch {
   unsigned end[MAX_PROB];
   unsigned nblk[MAX_PROB];
   int nprob;
-  int guard;   // the split kernel's range guard (an overflowed block recomputes itself on fp32 products)
+  int guard;   // the split kernel's range guard (an overflowed block runs again on scaled inputs)
 };
 
 // x as the f16 A operand (hi, hi, lo, lo): hi = f16(x), lo = f16(x - hi) (x - hi is exact in
@@ -175,12 +173,6 @@ __device__ __forceinline__ f16x4 w4_split(const float x) {
   asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(__builtin_bit_cast(unsigned, hh)), "v"(x));
   const f16x2 ll = __builtin_convertvector(f32x2{l, l}, f16x2);
   return __builtin_shufflevector(hh, ll, 0, 1, 2, 3);
-}
-
-// the fp32 value w * 2^12 of a split filter dword (hi, lo): hi + lo is exact in fp32 (22 bits)
-__device__ __forceinline__ float w4_unsplit(const float packed) {
-  const f16x2 p = __builtin_bit_cast(f16x2, packed);
-  return (float)p[0] + (float)p[1];
 }
 
 // Range guard of the split kernel: blocks whose f16 operands overflowed (|V| >= 65520 turns hi
@@ -484,10 +476,15 @@ __device__ unsigned long long g_w4_clock[65536][10];   // + [8] chunk 0 issued, 
 
 // One work item: the block's 64 tiles x 32 output channels (HF: this wave's point-column half).
 // Returns true (block-uniform) when the split kernel's range guard found an overflow: nothing was
-// written, and the caller recomputes the item on fp32 products.
+// written, and the caller runs the item again with xscale = 0: the body then scans the block's input
+// patch (every chunk, from global memory; after the producer's transform), takes the power of two
+// xscale that brings 100 max|d| >= max|V| below 2^15, multiplies the staged patch by it (the same
+// in-LDS pass as the input transform) and the accumulators by 1 / xscale: the same split products
+// on exactly scaled operands.  (A second, fp32 instantiation of the body in the same kernel made the
+// register allocator spill the gated split kernel: wino4 49.8 -> 79.0 ms/step.)
 template <class C, int HF, int LTW, bool GATED, bool AFF>
 __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, const unsigned wid, float *smem,
-                                        float2 *atab, const bool guard = false) {
+                                        float2 *atab, const bool guard = false, float xscale = 1.0f) {
   constexpr int NWAVE = C::NW, NTHR = C::NTHR, KC = C::KC, JPC = C::JPC, NT = C::NT, PDMA = C::PDMA,
                 UDMA = C::UDMA, UPW = C::UPW, UBUF = C::UBUF, BUF = C::BUF, PBUF = C::PBUF, OPP = C::OPP,
                 CO = C::CO, CG = C::CG, SB = C::SB, NR = C::NR;
@@ -546,6 +543,44 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
     po[j] = ok ? (ci * hw + y * pitch + x) * 4 : 0x7ffffff0;   // out of range: the load returns 0
     pc[j] = ok && wv + NWAVE * j < (KC * PS + 63) / 64 ? ci : -1;
   }
+  if constexpr (C::SPLIT) {
+    if (xscale == 0.0f) {   // the range guard's second pass: the scale from the block's largest input
+      float *red = smem;   // (patch buffer 0: only chunk 0's filters are in flight, into the filter area)
+      const char *ib = reinterpret_cast<const char *>(P.in + (long)n * P.in_bs);
+      float mx = 0.0f;
+#pragma unroll 1
+      for (int kc = 0; kc < nchunks; ++kc)
+#pragma unroll
+        for (int j = 0; j < PDMA; ++j) {
+          if (pc[j] < 0) continue;
+          const f32x4 v = *reinterpret_cast<const f32x4 *>(ib + po[j] + (long)kc * KC * hw * 4);
+          float a = 1.0f, b = 0.0f, fl = -INFINITY;
+          if constexpr (AFF) {
+            const int pi = n * P.in_pstride + kc * KC + pc[j];
+            const float m0 = P.in_m ? P.in_m[pi] : 0.0f, t0 = P.in_t ? P.in_t[pi] : 0.0f;
+            a = P.in_s ? P.in_s[pi] : 1.0f;
+            b = t0 - m0 * a;
+            fl = P.in_act ? 0.0f : -INFINITY;
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float t = __builtin_fabsf(fmaxf(v[e] * a + b, fl));
+            mx = fmaxf(mx, t < INFINITY ? t : 0.0f);
+          }
+        }
+      mx = sa::wave_max_dpp(mx);
+      if (lane == 0) red[wv] = mx;
+      __syncthreads();
+      mx = red[0];
+#pragma unroll
+      for (int w = 1; w < NWAVE; ++w) mx = fmaxf(mx, red[w]);
+      __syncthreads();   // (before chunk 0's patch DMA lands there)
+      int e2;
+      (void)frexpf(100.0f * mx, &e2);   // 100 max|d| < 2^e2
+      xscale = mx > 0.0f ? ldexpf(1.0f, 15 - e2) : 1.0f;
+    }
+  }
+  const bool scaled = xscale != 1.0f;
   // the chunk's DMAs in three parts (part -1: all at once), spread over the first job's three
   // column phases (each piece costs tens of issue cycles; clustered after the barrier they
   // would delay the first reads)
@@ -611,7 +646,7 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
     for (int c = tid; c < Cin; c += NTHR) {
       const int pi = n * P.in_pstride + c;
       const float m0 = P.in_m ? P.in_m[pi] : 0.0f, sc = P.in_s ? P.in_s[pi] : 1.0f, t0 = P.in_t ? P.in_t[pi] : 0.0f;
-      atab[c] = make_float2(sc, t0 - m0 * sc);
+      atab[c] = make_float2(sc * xscale, (t0 - m0 * sc) * xscale);   // (ReLU commutes with a scale > 0)
     }
     __syncthreads();
   }
@@ -636,7 +671,21 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
         }
       }
     }
-    if (SA_W4_DIAG < 3 || AFF) __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
+    if constexpr (SPLIT && !AFF) {
+      if (scaled) {   // the range guard's second pass: this lane's staged groups times xscale
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        float *pbuf = smem + cur * BUF + (wv * 64 + lane) * 4;
+        // (one group at a time: the accumulators are live here)
+#pragma unroll 1
+        for (int j = 0; j < PDMA; ++j) {
+          if (wv + NWAVE * j < npi) {
+            f32x4 *q = reinterpret_cast<f32x4 *>(pbuf + NWAVE * j * 256);
+            *q = *q * xscale;
+          }
+        }
+      }
+    }
+    if (SA_W4_DIAG < 3 || AFF || scaled) __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
 #ifdef SA_W4_CLOCK
     if (kc == 0 && HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][4] = __builtin_amdgcn_s_memtime();
 #endif
@@ -713,7 +762,7 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
           for (int i = 0; i < NR; ++i)
 #pragma unroll
             for (int g = 0; g < CG; ++g)
-              acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], C::UNSPLIT ? w4_unsplit(bc[i][g]) : bc[i][g],
+              acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], bc[i][g],
                                                                     acc[i][jj][g], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);   // bound the scheduler's hoisting (register pressure)
@@ -727,13 +776,14 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
 #ifdef SA_W4_CLOCK
   if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][5] = __builtin_amdgcn_s_memtime();
 #endif
-  if constexpr (SPLIT || C::UNSPLIT) {   // the filters' 2^W4S_LOG2 (exact)
+  if constexpr (SPLIT) {   // the filters' 2^W4S_LOG2 and the inputs' xscale (exact)
+    const float inv_scale = 1.0f / ((float)(1 << W4S_LOG2) * xscale);
 #pragma unroll
     for (int i = 0; i < NR; ++i)
 #pragma unroll
       for (int jj = 0; jj < 3; ++jj)
 #pragma unroll
-        for (int g = 0; g < CG; ++g) acc[i][jj][g] *= 1.0f / (1 << W4S_LOG2);
+        for (int g = 0; g < CG; ++g) acc[i][jj][g] *= inv_scale;
   }
 
   // ---- output transform.  Lane holds tiles tg * 16 + 4 (lane >> 4) + i of output channels
@@ -804,9 +854,9 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
   if constexpr (SPLIT) {
     // Range guard: an f16 operand overflow (|V| >= 65520: hi = inf, lo = -inf) makes every product
     // of that value NaN, and so the staged outputs it feeds (checked before the ReLU).  Such a
-    // block writes nothing (its epilogue may update h in place) and recomputes its item on fp32
-    // MFMA products right away (wino_f4k3_kernel): no list, no second launch, every overflowed
-    // block in parallel.  Genuine NaN inputs take the same path and give the fp32 kernel's NaN.
+    // block writes nothing (its epilogue may update h in place) and runs its item again right away
+    // on exactly scaled inputs (wino_f4k3_kernel, w4_body's xscale): no list, no second launch,
+    // every overflowed block in parallel.  Genuine NaN inputs take the same path and give NaN.
     // One int per wave past the output planes and the flow head's taps (nothing else uses that
     // LDS after the main loop).
     static_assert(C::CO * C::OPP + C::CO * 9 + NWAVE <= C::SMEM, "range guard flags");
@@ -832,6 +882,9 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
   return false;
 }
 
+#ifndef SA_W4_REDO
+#define SA_W4_REDO 1
+#endif
 template <class C, bool GATED, bool AFF = false>
 __global__ __launch_bounds__(C::NTHR, C::NW == 8 ? 1 : 2) void wino_f4k3_kernel(const W4Launch L) {
   // problem of the block from its raw id (ranges padded to multiples of 8: every XCD gets an
@@ -843,7 +896,6 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 ? 1 : 2) void wino_f4k3_kernel(
   int pi = 0;
 #pragma unroll
   for (int i = 1; i < MAX_PROB; ++i) pi += (i < L.nprob && g >= L.end[i - 1]) ? 1 : 0;
-  const W4Prob &P = L.p[pi];
   const unsigned base = pi ? L.end[pi - 1] : 0u, nb = L.nblk[pi];
   if (g - base >= nb) return;
   __shared__ __attribute__((aligned(16))) float smem[C::SMEM];
@@ -854,30 +906,36 @@ __global__ __launch_bounds__(C::NTHR, C::NW == 8 ? 1 : 2) void wino_f4k3_kernel(
 #endif
   // the first half of the waves takes point columns 0-2, the second half 3-5 (wave-uniform)
   const unsigned wid = sa::xcd_remap(g - base, nb);
-  const W4Gate *gp = GATED ? &L.gate[pi] : nullptr;
   const bool guard = C::SPLIT && L.guard;
+  // the range guard: an overflowed block (block-uniform) runs its item again on scaled inputs
+  const W4Prob &P = L.p[pi];
+  const W4Gate *gp = GATED ? &L.gate[pi] : nullptr;
   bool over;
-#define SA_W4_B(CC_, HF_, LTW_) w4_body<CC_, HF_, LTW_, GATED, AFF>(P, gp, wid, smem, atab, guard)
-  if (threadIdx.x < C::NTHR / 2) over = P.ltw == 4 ? SA_W4_B(C, 0, 4) : SA_W4_B(C, 0, 5);
-  else over = P.ltw == 4 ? SA_W4_B(C, 1, 4) : SA_W4_B(C, 1, 5);
-  if constexpr (C::SPLIT) {
-    // the range guard: an overflowed block (block-uniform) recomputes its item on fp32 MFMA products
-    // with the split filters read as hi + lo (W4SplitRedo: the same LDS layout and epilogues)
+#define SA_W4_B(CC_, HF_, LTW_, G_, XS_) w4_body<CC_, HF_, LTW_, GATED, AFF>(P, gp, wid, smem, atab, G_, XS_)
+  if (threadIdx.x < C::NTHR / 2) over = P.ltw == 4 ? SA_W4_B(C, 0, 4, guard, 1.0f) : SA_W4_B(C, 0, 5, guard, 1.0f);
+  else over = P.ltw == 4 ? SA_W4_B(C, 1, 4, guard, 1.0f) : SA_W4_B(C, 1, 5, guard, 1.0f);
+  if constexpr (C::SPLIT && SA_W4_REDO) {
     if (over) {
-      using R = W4Cfg<C::NW, C::KC, false, true>;
-      static_assert(R::SMEM <= C::SMEM, "the recompute's LDS");
       __syncthreads();   // the first pass's LDS reads are over
       if (threadIdx.x == 0) atomicAdd(&g_w4_redo_blocks, 1u);
+      // the second pass's arguments through opaque copies: nothing of it is hoisted (CSE'd) into
+      // the first pass, whose registers stay its own
+      int pil = __builtin_amdgcn_readfirstlane(pi);
+      unsigned widl = __builtin_amdgcn_readfirstlane(wid);
+      asm volatile("" : "+s"(pil), "+s"(widl));
+      const W4Prob &P2 = L.p[pil];
+      const W4Gate *gp2 = GATED ? &L.gate[pil] : nullptr;
+#define SA_W4_B2(HF_, LTW_) w4_body<C, HF_, LTW_, GATED, AFF>(P2, gp2, widl, smem, atab, false, 0.0f)
       if (threadIdx.x < C::NTHR / 2) {
-        if (P.ltw == 4) SA_W4_B(R, 0, 4);
-        else SA_W4_B(R, 0, 5);
+        if (P2.ltw == 4) SA_W4_B2(0, 4);
+        else SA_W4_B2(0, 5);
       } else {
-        if (P.ltw == 4) SA_W4_B(R, 1, 4);
-        else SA_W4_B(R, 1, 5);
+        if (P2.ltw == 4) SA_W4_B2(1, 4);
+        else SA_W4_B2(1, 5);
       }
+#undef SA_W4_B2
     }
   }
-  (void)over;
 #undef SA_W4_B
 #ifdef SA_W4_CLOCK
   if (threadIdx.x == 0 && g < 65536) {
@@ -1191,7 +1249,7 @@ extern "C" int sa_conv2d_k3_wino4_launch(int nprob, const SaWinoProblem *probs, 
   }
   L.nprob = nprob;
   SA_REQUIRE(!(aff && gated), "sa_conv2d_k3_wino4: an input transform and a gate epilogue in one launch");
-  // the split kernel's range guard: a block whose operands overflowed recomputes itself on fp32 products
+  // the split kernel's range guard: a block whose operands overflowed runs again on scaled inputs
   L.guard = split && guard ? 1 : 0;
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV2D_W4, s);

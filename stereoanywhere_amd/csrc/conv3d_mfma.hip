@@ -139,7 +139,12 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
   // the thread's staging jobs, the same for every group of DD planes: job J = tid + 512 k ->
   // (plane q of the group, channel group cg, entry (row, col) of the (TH+2) x 66 window at
   // (h0 - 1, w0 - 1)); jobs outside H x W are dropped
-  long joff[C::JPT];
+  // the image's volume through a buffer resource: 32-bit offsets (< 2^32 bytes per image, checked
+  // by the host), channel j of a job's group as the scalar offset j * D*H*W*4
+  const __amdgpu_buffer_rsrc_t src_img = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(in + (long)b * CIN * D * HW), (short)0, (int)((long)CIN * D * HW * 4), 0x00020000);
+  const int chan_bytes = (int)(D * HW * 4);
+  unsigned joff[C::JPT];
   int jdst[C::JPT], jq[C::JPT], jcg[C::JPT];
   bool jok[C::JPT];
 #pragma unroll
@@ -148,7 +153,7 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
     const int q = J / C::JOBS, r_ = J % C::JOBS, cg = r_ / (C::ROWS * C::COLS), e = r_ % (C::ROWS * C::COLS);
     const int hh = h0 - 1 + e / C::COLS, ww = w0 - 1 + e % C::COLS;
     jok[k] = J < C::DD * C::JOBS && hh >= 0 && hh < H && ww >= 0 && ww < W;
-    joff[k] = jok[k] ? ((long)b * CIN + 8 * cg) * D * HW + (long)hh * W + ww : 0;
+    joff[k] = jok[k] ? (unsigned)((8 * cg * (long)D * HW + (long)hh * W + ww) * 4) : 0u;
     jdst[k] = cg * 2 * C::PLANE + e;
     jq[k] = q;
     jcg[k] = cg;
@@ -159,9 +164,10 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
     for (int k = 0; k < C::JPT; ++k) {
       const int p = p0 + jq[k];
       if (jok[k] && p >= 0 && p < D) {
-        const float *src = in + joff[k] + (long)p * HW;
+        const unsigned vo = joff[k] + (unsigned)(p * HW * 4);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x[k][j] = src[(long)j * D * HW];
+        for (int j = 0; j < 8; ++j)
+          x[k][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(src_img, vo, j * chan_bytes, 0));
       }
     }
   };
@@ -208,11 +214,15 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
   const bool vec = (W & 3) == 0;
   double s_acc = 0.0, q_acc = 0.0;
 
-  for (int dout = d0; dout < d1; dout += C::DD) {
-    const bool more = dout + C::DD < d1;
-    // next step's planes dout + DD + 1 .. dout + 2 DD -> registers
-    float xs[C::JPT][8];
-    if (more) stage_load(dout + C::DD + 1, xs);
+  // step i (output planes dout = d0 + DD i ..): its top issues the loads of step i + 2's new planes,
+  // its end writes step i + 1's (loaded during step i - 1) into the ring: two steps of loads in
+  // flight, alternating between two register sets
+  const int nsteps = (d1 - d0 + C::DD - 1) / C::DD;
+  float xa[C::JPT][8], xb[C::JPT][8];
+  if (nsteps > 1) stage_load(d0 + C::DD + 1, xa);
+  auto step = [&](const int i, float (&xload)[C::JPT][8], float (&xput)[C::JPT][8]) __attribute__((always_inline)) {
+    const int dout = d0 + C::DD * i;
+    if (i + 2 < nsteps) stage_load(dout + 2 * C::DD + 1, xload);
 
     // the lane's A bases per K-step: group G = 4 t + g -> (plane e, channel group cg)
     int base[C::KS];
@@ -288,9 +298,14 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
       q_acc += (double)q;
     }
 
-    // next step's planes -> LDS (their slots held planes only the previous step read)
-    if (more) stage_put(dout + C::DD + 1, xs);
+    // step i + 1's planes -> LDS (their slots held planes only step i - 1 read)
+    if (i + 1 < nsteps) stage_put(dout + C::DD + 1, xput);
     __syncthreads();
+  };
+#pragma unroll 1
+  for (int i = 0; i < nsteps; i += 2) {
+    step(i, xb, xa);
+    if (i + 1 < nsteps) step(i + 1, xa, xb);
   }
 
   // InstanceNorm partials: lanes n, n + 16, n + 32, n + 48 (and n + 8 for the plane pairs)
@@ -382,6 +397,7 @@ extern "C" int sa_conv3d_mf(const float *in, int B, int Cin, int D, int H, int W
   // |InstanceNorm'ed value| <= sqrt(voxels) < 2^15: the f16 hi part cannot overflow
   SA_REQUIRE((long)D * H * W < (1L << 30), "sa_conv3d_mf: a channel volume must hold < 2^30 voxels");
   SA_REQUIRE(slope >= 0.0f && slope <= 1.0f, "sa_conv3d_mf: LeakyReLU slope must lie in [0, 1]");
+  SA_REQUIRE((long)Cin * D * H * W * 4 < (1L << 31), "sa_conv3d_mf: an image's volume must hold < 2^31 bytes");
   SA_REQUIRE((long)B * Cin * D * H * W < (1L << 62), "sa_conv3d_mf: size");
   const MfGeo g = mf_geo(B, Cin, D, H, W);
   const long blocks = (long)B * g.tilesW * g.tilesH * g.tilesD;

@@ -689,7 +689,9 @@ def conv3d_s1(x: "VolAct", w_wd: torch.Tensor, table, cout: int, slope: float = 
               stats: bool = True) -> "VolAct":
     """The hourglass's stride-1 conv: conv3d_mf where it applies (CONV3D_MFMA, a table, no gate),
     else conv3d_wd."""
-    if CONV3D_MFMA and table is not None and x.gate is None and x.norm is not None and x.act:
+    B, Cin, D, H, W = x.raw.shape
+    if (CONV3D_MFMA and table is not None and x.gate is None and x.norm is not None and x.act
+            and Cin * D * H * W * 4 < 2 ** 31 and D * H * W < 2 ** 30):
         return conv3d_mf(x, table, cout, slope, stats)
     return conv3d_wd(x, w_wd, cout, slope, stats)
 
@@ -846,8 +848,12 @@ W4_SPLIT = True
 # 3x3 launches on the implicit-GEMM kernel (conv2d_igemm.hip: direct convolution on
 # v_mfma_f32_16x16x32_f16, three f16 products per fp32 product) where every problem allows it
 # (Cout % 128, Cin % 32; gate modes 1 / 2) and the launch's total output pixels x Cout is at most
-# IGEMM_MAX_WORK (None: no limit; see conv2d_k3_multi)
-IGEMM = True
+# IGEMM_MAX_WORK (None: no limit; see conv2d_k3_multi).  Off by default, by measurement (round 5,
+# one box, same library): the forward at configs[1] 61.2 ms/step on F(4x4) only, 62.1 with every
+# eligible conv on the implicit GEMM (its MFMA load draws the clock to ~2.2 GHz against ~2.33), 61.9
+# with it on the 1/32-level launches only (IGEMM_MAX_WORK 3e6, where it is 1.2-1.3x per conv
+# standalone); DESIGN.md section 0
+IGEMM = False
 IGEMM_MAX_WORK = None
 # the split filters need |U * 2^12| < 65504; |U| <= max |weight| for F(4x4,3x3)'s G
 _W4_SPLIT_WMAX = 15.99
@@ -1019,6 +1025,9 @@ def _wino4_launch(n: int, arr, gates, shape: int, x: torch.Tensor) -> None:
            1 if (shape == 6 and SPLIT_GUARD) else 0, _stream(x))
 
 
+_IG_GATED = _IG_AFF = _IG_MULTI = True   # (diagnostic switches: problem kinds the implicit GEMM takes)
+
+
 def _igemm_ok(p: dict, q: dict) -> bool:
     """Whether the implicit-GEMM kernel takes problem p (q: its arguments without the gate):
     its weights derived (Cout % 128, Cin % 32, |w| < 16), gate modes 1 (Cout % 256) or 2, an input
@@ -1027,6 +1036,8 @@ def _igemm_ok(p: dict, q: dict) -> bool:
     if not IGEMM or U.uig is None:
         return False
     g = p.get("gate")
+    if (g and not _IG_GATED) or ((q.get("in_aff") is not None or q.get("in_act") is not None) and not _IG_AFF):
+        return False
     if g and not (g["mode"] == 2 or (g["mode"] == 1 and U.cout % 256 == 0)):
         return False
     if (q.get("in_aff") is not None or q.get("in_act") is not None) and (x.shape[1] > 512 or ACT[q.get("in_act")] > 1):
@@ -1049,7 +1060,7 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     for p, q in zip(problems, plain):
         if p.get("gate") and p["gate"]["mode"] == 1:
             q["out_cout"] = p["U"].cout // 2   # z only: r*h goes to the gate's out2
-    if not small_blocks:
+    if not small_blocks and (_IG_MULTI or len(problems) == 1):
         igs = [_igemm_ok(p, q) for p, q in zip(problems, plain)]
         if any(igs):
             if not all(igs):   # the implicit-GEMM problems in a launch of their own, the others as before

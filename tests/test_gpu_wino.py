@@ -528,9 +528,10 @@ def test_wino4_split_range_guard_gate_and_input_transform(monkeypatch):
 
 def test_wino4_split_range_guard_whole_launch(monkeypatch):
     """The guard's worst case: every block of an xc08-sized launch (256 -> 384 channels at 136 x 240,
-    B = 4; inputs ~1e4, so every tile's transformed values overflow f16) recomputes itself on fp32
-    products inside the launch, in parallel: the result equals the fp32-product kernel's, and the
-    launch takes at most twice the fp32 kernel's time (split pass + fp32 pass per block)."""
+    B = 4; inputs ~1e4, so every tile's transformed values overflow f16) runs its item again on
+    exactly scaled inputs inside the launch, in parallel: the result equals the fp32-product
+    kernel's within the split kernel's own accuracy (~1e-5 of the output scale, as
+    test_wino4_matches_conv2d), and the launch takes at most twice the fp32 kernel's time."""
     monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
     x = rnd(4, 256, 136, 240, seed=11) * 1e4
     w = rnd(384, 256, 3, 3, seed=12) / 48
@@ -558,7 +559,7 @@ def test_wino4_split_range_guard_whole_launch(monkeypatch):
     assert outs[True][1] >= blocks // 2 and outs[False][1] == 0
     assert torch.isfinite(outs[True][0]).all()
     scale = float(outs[False][0].abs().max())
-    assert float((outs[True][0] - outs[False][0]).abs().max()) < 1e-5 * scale
+    assert float((outs[True][0] - outs[False][0]).abs().max()) < 5e-5 * scale
     assert t[True] <= 2.0 * t[False] + 0.05, t
 
 
