@@ -408,6 +408,16 @@ typedef struct SaWinoProblem {
    * zero padding) and kept zero in every output.  F(4x4) only (pitch % 4 == 0): a GRU level
    * whose width is not a multiple of 4 runs on it with its planes padded to a multiple of 4. */
   int pitch;
+  /* residual epilogue (F(4x4) only; no statistics, no gate): out = oact(act(conv + bias) + skip'),
+   * skip' = skip_act(skip * skip_s + skip_t) per output channel (NULL skip_s / skip_t = 1 / 0),
+   * act = ReLU iff relu, skip_act / out_act 1 = ReLU; skip [N, Cout, H, pitch] with batch stride
+   * skip_bs, 16-byte aligned.  skip = NULL: the plain epilogue.  (The closing
+   * relu(relu(N2(c2)) + N3(skip)) of a BatchNorm residual block, extractor.py:41-60, with N2 folded
+   * into the conv.) */
+  const float *skip;
+  long skip_bs;
+  const float *skip_s, *skip_t;
+  int skip_act, out_act;
 } SaWinoProblem;
 int sa_conv2d_k3_wino_multi(int nprob, const SaWinoProblem *probs, void *stream);
 

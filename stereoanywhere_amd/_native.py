@@ -26,7 +26,8 @@ class SaWinoProblem(ctypes.Structure):
     """include/stereoanywhere_hip.h: one convolution of sa_conv2d_k3_wino_multi."""
     _fields_ = [("in_", P), ("in_bs", L), ("N", I), ("Cin", I), ("H", I), ("W", I), ("U", P), ("Cout", I),
                 ("bias", P), ("relu", I), ("in_m", P), ("in_s", P), ("in_t", P), ("in_pstride", I),
-                ("in_act", I), ("out", P), ("out_bs", L), ("stats_partial", P), ("pitch", I)]
+                ("in_act", I), ("out", P), ("out_bs", L), ("stats_partial", P), ("pitch", I),
+                ("skip", P), ("skip_bs", L), ("skip_s", P), ("skip_t", P), ("skip_act", I), ("out_act", I)]
 
 
 class SaGateEpilogue(ctypes.Structure):

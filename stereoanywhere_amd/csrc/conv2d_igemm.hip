@@ -640,6 +640,7 @@ extern "C" int sa_conv2d_k3_igemm(int nprob, const SaWinoProblem *probs, const S
   for (int i = 0; i < nprob; ++i) {
     const SaWinoProblem &q = probs[i];
     SA_REQUIRE(q.in && q.U && q.out && q.N > 0 && q.H > 0 && q.W > 0, "sa_conv2d_k3_igemm: bad arguments");
+    SA_REQUIRE(!q.skip, "sa_conv2d_k3_igemm: the residual epilogue is F(4x4) only");
     SA_REQUIRE(q.Cin % KCH == 0 && q.Cout % 128 == 0,
                "sa_conv2d_k3_igemm: needs Cin %% 32 == 0 and Cout %% 128 == 0 (got %d, %d)", q.Cin, q.Cout);
     const int pitch = q.pitch ? q.pitch : q.W;

@@ -491,6 +491,7 @@ namespace {
 // validate one problem and fill its kernel descriptor; returns its CG (0 on error)
 int wino_prob(const SaWinoProblem &q, WinoProb &P, bool &aff) {
   SA_REQUIRE(q.pitch == 0 || q.pitch == q.W, "sa_conv2d_k3_wino: pitched planes are F(4x4) only");
+  SA_REQUIRE(!q.skip, "sa_conv2d_k3_wino: the residual epilogue is F(4x4) only");
   SA_REQUIRE(q.in && q.U && q.out && q.N > 0 && q.H > 0 && q.W > 0, "sa_conv2d_k3_wino: bad arguments");
   SA_REQUIRE(q.Cin % KC == 0 && q.Cout % 32 == 0,
              "sa_conv2d_k3_wino: needs Cin %% 8 == 0 and Cout %% 32 == 0 (got %d, %d)", q.Cin, q.Cout);

@@ -128,6 +128,11 @@ struct W4Prob {
   const float *in_m, *in_s, *in_t;
   int in_pstride, in_act;
   int pitch;               // row pitch of the input / output / gate planes (>= W, % 4 == 0; SaWinoProblem)
+  // residual epilogue (SaWinoProblem skip ...): out = oact(act(conv + bias) + skip_act(skip * s + t))
+  const float *skip;
+  long skip_bs;
+  const float *skip_s, *skip_t;
+  int skip_act, out_act;
 };
 constexpr int MAX_PROB = 8;
 
@@ -305,6 +310,30 @@ __device__ __forceinline__ void w4_emit(const W4Prob &P, const W4Gate *gate, con
   float *dst = P.out + (long)n * P.out_bs;
   constexpr int NJ = (NCH * NT * 16) / (4 * NTHR);
   auto plain_stores = [&]() __attribute__((always_inline)) {
+    if (P.skip) {   // residual epilogue: oact(act(conv + bias) + skip_act(skip * s + t))
+      const float *sk = P.skip + (long)n * P.skip_bs;
+#pragma unroll 4
+      for (int j = 0; j < NJ; ++j) {
+        const int i4 = tid + NTHR * j;
+        const int c = i4 / (NT * 4), p = (i4 % (NT * 4)) * 4, r = p >> lbw, cx = p & (BW - 1);
+        const int y = y0 + r, x = x0 + cx;
+        if (y < H && x < W) {
+          const long off = (long)(cb0 + c) * hw + (long)y * pitch + x;
+          const f32x4 sv = *reinterpret_cast<const f32x4 *>(sk + off);
+          const float ss = P.skip_s ? P.skip_s[cb0 + c] : 1.0f, st_ = P.skip_t ? P.skip_t[cb0 + c] : 0.0f;
+          f32x4 v = *reinterpret_cast<const f32x4 *>(ot + c * OPP + p);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float a = sv[e] * ss + st_;
+            if (P.skip_act) a = fmaxf(a, 0.0f);
+            v[e] = v[e] + a;
+            if (P.out_act) v[e] = fmaxf(v[e], 0.0f);
+          }
+          *reinterpret_cast<f32x4 *>(dst + off) = tail0(v, x);
+        }
+      }
+      return;
+    }
 #pragma unroll 4
     for (int j = 0; j < NJ; ++j) {
       const int i4 = tid + NTHR * j;
@@ -1199,9 +1228,16 @@ extern "C" int sa_conv2d_k3_wino4_launch(int nprob, const SaWinoProblem *probs, 
                "sa_conv2d_k3_wino4: an image or the filter bank exceeds the 2 GB buffer-descriptor range");
     const int ltw = w4_ltw(q.H, q.W), bw = 4 << ltw, bh = 4 * (nt >> ltw);
     const int tiles_w = (q.W + bw - 1) / bw, tiles_h = (q.H + bh - 1) / bh;
+    if (q.skip) {
+      SA_REQUIRE(!q.stats_partial && !(gates && gates[i].mode != 0) && (reinterpret_cast<uintptr_t>(q.skip) & 15) == 0 &&
+                     q.skip_bs % 4 == 0 && (q.skip_act == 0 || q.skip_act == 1) && (q.out_act == 0 || q.out_act == 1),
+                 "sa_conv2d_k3_wino4: a residual epilogue takes no statistics or gate and a 16-byte aligned skip "
+                 "plane (skip_act none or ReLU)");
+    }
     L.p[i] = W4Prob{q.in, q.in_bs, q.Cin, q.H, q.W, q.U, q.Cout, q.bias, q.relu, q.out, q.out_bs,
                     ltw, tiles_w, tiles_w * tiles_h, q.Cout / CO, q.stats_partial,
-                    q.in_m, q.in_s, q.in_t, q.in_pstride, q.in_act, pitch};
+                    q.in_m, q.in_s, q.in_t, q.in_pstride, q.in_act, pitch,
+                    q.skip, q.skip_bs, q.skip_s, q.skip_t, q.skip_act, q.out_act};
     L.gate[i] = W4Gate{};
     if (gates && gates[i].mode != 0) {
       const SaGateEpilogue &e = gates[i];

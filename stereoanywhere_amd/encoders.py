@@ -161,7 +161,7 @@ def _materialize(x) -> torch.Tensor:
 
 def residual_block(blk: nn.Module, name: str, x, fin: _Finisher) -> torch.Tensor:
     w1, w2 = blk.conv1.weight.data_ptr(), blk.conv2.weight.data_ptr()
-    pending = None
+    pending = d_pre = None
     if isinstance(x, tuple):
         if blk.downsample is None and blk.conv1.stride == (1, 1) and w1 in _WINO and w2 in _WINO:
             x, pending = x
@@ -175,6 +175,11 @@ def residual_block(blk: nn.Module, name: str, x, fin: _Finisher) -> torch.Tensor
         r = ops.conv_direct(x, direct[0], 3, 2, blk.conv1.out_channels, wd=direct[1], stats=fin.instance)
         c1, d = r[0], r[1]
         s1, sd = r[2] if fin.instance else (None, None)
+        if not fin.instance:
+            y = _residual_close(c1, blk.conv2, d, fin.affine(name + ".norm3", d),
+                                in_aff=fin.affine(name + ".norm1", c1))
+            if y is not None:
+                return y
         c2, s2 = _conv_k3(c1, blk.conv2, fin, in_aff=fin.affine(name + ".norm1", c1, s1))
         return ops.norm_act(c2, fin.affine(name + ".norm2", c2, s2), act_in="relu", skip=d,
                             skip_aff=fin.affine(name + ".norm3", d, sd), act_out="relu", out=c2)
@@ -183,6 +188,10 @@ def residual_block(blk: nn.Module, name: str, x, fin: _Finisher) -> torch.Tensor
         # eval BatchNorm: norm1 + ReLU in conv1's epilogue (folded weights), so conv2 reads y1
         # on the F(4x4) kernel without a norm_act pass in between
         y1 = ops.conv2d_k3(x, fold[0], fold[1], relu=True, in_aff=pending, in_act=pact)
+        if blk.downsample is None:
+            y = _residual_close(y1, blk.conv2, x, pending, pact)
+            if y is not None:
+                return y
         c2, s2 = _conv_k3(y1, blk.conv2, fin)
     elif w1 in _WINO and w2 in _WINO:
         # y1 = relu(N1(c1)) is never written: conv2 applies it while loading c1
@@ -190,6 +199,13 @@ def residual_block(blk: nn.Module, name: str, x, fin: _Finisher) -> torch.Tensor
         c2, s2 = _conv_k3(c1, blk.conv2, fin, in_aff=fin.affine(name + ".norm1", c1, s1))
     else:
         c1 = _conv(x, blk.conv1)
+        if not fin.instance and blk.downsample is not None:
+            # (MIOpen's stride-2 conv1: norm1 + ReLU on conv2's load, the close in its epilogue)
+            d_pre = _conv(x, blk.downsample[0])
+            y = _residual_close(c1, blk.conv2, d_pre, fin.affine(name + ".norm3", d_pre),
+                                in_aff=fin.affine(name + ".norm1", c1))
+            if y is not None:
+                return y
         y1 = ops.norm_act(c1, fin.affine(name + ".norm1", c1), act_in="relu", out=c1)
         if w2 in _WINO:
             c2, s2 = _conv_k3(y1, blk.conv2, fin)
@@ -198,7 +214,7 @@ def residual_block(blk: nn.Module, name: str, x, fin: _Finisher) -> torch.Tensor
     a2 = fin.affine(name + ".norm2", c2, s2)
     if blk.downsample is None:
         return ops.norm_act(c2, a2, act_in="relu", skip=x, skip_aff=pending, skip_act=pact, act_out="relu", out=c2)
-    d = _conv(x, blk.downsample[0])
+    d = d_pre if d_pre is not None else _conv(x, blk.downsample[0])
     return ops.norm_act(c2, a2, act_in="relu", skip=d, skip_aff=fin.affine(name + ".norm3", d), act_out="relu",
                         out=c2)
 
@@ -222,6 +238,11 @@ def residual_blocks_grouped(blks, names, xs, fin: _Finisher) -> List[torch.Tenso
     if all(f is not None for f in folds) and ops.wino4_applies(xs[0], U2[0], *zip(xs[1:], U2[1:])):
         # eval BatchNorm folded into conv1 (residual_block): y1 straight from the epilogue
         y1 = ops.conv2d_k3_multi(*[dict(x=x, U=f[0], bias=f[1], relu=True) for x, f in zip(xs, folds)])
+        folds2 = [_FOLD.get(b.conv2.weight.data_ptr()) for b in blks]
+        if all(f is not None for f in folds2) and all(x.shape[1] == b.conv2.out_channels for x, b in zip(xs, blks)):
+            # norm2 folded into conv2, the close relu(relu(.) + x) in its epilogue
+            return ops.conv2d_k3_multi(*[dict(x=y, U=f[0], bias=f[1], relu=True, skip=x, out_act="relu")
+                                         for y, f, x in zip(y1, folds2, xs)])
         r2 = stage([b.conv2 for b in blks], y1, [None] * len(blks))
     else:
         r1 = stage([b.conv1 for b in blks], list(xs), [None] * len(blks))
@@ -303,20 +324,67 @@ def cnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
 
 
 def fold_table(enc: nn.Module) -> FoldTable:
-    """conv1 of every residual block of a BatchNorm encoder whose conv1 qualifies for Winograd,
-    with its eval norm1 folded in: y = (c + b - mu) g / sqrt(var + eps) + beta = conv(x; s W) +
-    (t - s m), s = g / sqrt(var + eps), m = mu - b, t = beta (bn_affine)."""
+    """conv1 and conv2 of every residual block of a BatchNorm encoder that qualify for Winograd,
+    with their eval norm1 / norm2 folded in: y = (c + b - mu) g / sqrt(var + eps) + beta =
+    conv(x; s W) + (t - s m), s = g / sqrt(var + eps), m = mu - b, t = beta (bn_affine).  (conv2
+    folded: the block's closing relu(relu(N2(c2)) + skip) is conv2's residual epilogue.)"""
     if not isinstance(enc.norm1, nn.BatchNorm2d):
         return {}
     t: FoldTable = {}
     with torch.no_grad():
         for blk in enc.modules():
-            if hasattr(blk, "conv1") and hasattr(blk, "norm2") and isinstance(blk.norm1, nn.BatchNorm2d) \
-                    and wino_eligible(blk.conv1):
-                a = bn_affine(blk.norm1, blk.conv1.bias)
-                w = (blk.conv1.weight * a.s[:, None, None, None]).contiguous()
-                t[blk.conv1.weight.data_ptr()] = (ops.wino_weights(w), (a.t - a.s * a.m).contiguous())
+            if not (hasattr(blk, "conv1") and hasattr(blk, "norm2")):
+                continue
+            for conv, norm in ((blk.conv1, blk.norm1), (blk.conv2, blk.norm2)):
+                if isinstance(norm, nn.BatchNorm2d) and wino_eligible(conv):
+                    a = bn_affine(norm, conv.bias)
+                    w = (conv.weight * a.s[:, None, None, None]).contiguous()
+                    t[conv.weight.data_ptr()] = (ops.wino_weights(w), (a.t - a.s * a.m).contiguous())
     return t
+
+
+# per-channel (scale, shift) of an affine (x - m) s + t as x s + (t - m s), for the residual
+# epilogue's skip term; cached per affine (BatchNorm tables live as long as the derived weights)
+_SKIP_ST: Dict[int, Tuple[torch.Tensor, torch.Tensor, "ops.Affine"]] = {}
+
+
+def _skip_st(aff: Optional["ops.Affine"]):
+    if aff is None:
+        return None, None
+    hit = _SKIP_ST.get(id(aff))
+    if hit is not None and hit[2] is aff:
+        return hit[0], hit[1]
+    with torch.no_grad():
+        s = aff.s
+        t = aff.t if aff.t is not None else torch.zeros_like(s)
+        if aff.m is not None:
+            t = t - aff.m * s
+        st = (s.contiguous(), t.contiguous())
+    _SKIP_ST[id(aff)] = (st[0], st[1], aff)
+    return st
+
+
+def _residual_close(y1: torch.Tensor, conv2: nn.Conv2d, skip: torch.Tensor, skip_aff=None, skip_act=None,
+                    in_aff=None):
+    """BatchNorm block close in conv2's epilogue: relu(relu(N2(conv2(y1))) + skip_act(skip_aff(skip)))
+    with N2 folded into conv2 (fold_table); in_aff: y1's own norm + ReLU applied on load.  None when
+    conv2 has no folded filters or the F(4x4) kernel does not take the shapes (the caller then
+    runs conv2 + norm_act)."""
+    fold = _FOLD.get(conv2.weight.data_ptr())
+    if fold is None or skip_aff is not None and (skip_aff.per_plane or skip_aff.s is None):
+        return None
+    if in_aff is not None and y1.shape[1] > ops._WINO4_AFF_CIN:
+        return None
+    # (F(4x4) at any size: the residual epilogue is only there)
+    if not (ops._WINO4 and ops._wino4_ok(y1, in_aff=in_aff, in_act="relu" if in_aff is not None else None)
+            and skip.stride(1) == skip.shape[2] * skip.shape[3]
+            and tuple(skip.shape) == (y1.shape[0], conv2.out_channels, y1.shape[2], y1.shape[3])
+            and skip.data_ptr() % 16 == 0 and skip.stride(0) % 4 == 0):
+        return None
+    ss, st = _skip_st(skip_aff)
+    return ops.conv2d_k3(y1, fold[0], fold[1], relu=True, in_aff=in_aff,
+                         in_act="relu" if in_aff is not None else None, skip=skip, skip_s=ss, skip_t=st,
+                         skip_act=skip_act, out_act="relu")
 
 
 def bn_table(enc: nn.Module) -> Dict[str, ops.Affine]:

@@ -931,10 +931,14 @@ _WINO4_MIN_BLOCKS = 128
 def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] = None, relu: bool = False,
                   out: Optional[torch.Tensor] = None, in_aff: Optional[Affine] = None, in_act=None,
                   stats: bool = False, f4: bool = False, out_cout: Optional[int] = None,
-                  width: Optional[int] = None, split: bool = False, ig: bool = False):
+                  width: Optional[int] = None, split: bool = False, ig: bool = False,
+                  skip: Optional[torch.Tensor] = None, skip_s: Optional[torch.Tensor] = None,
+                  skip_t: Optional[torch.Tensor] = None, skip_act=None, out_act=None):
     """out_cout: channels of ``out`` when the epilogue writes fewer than Cout there (gate mode 1).
     width: the image width when x (and out, and the gate planes) are PITCHED planes [.., H, P]
-    whose columns width .. P - 1 are zero (F(4x4) only; the outputs' pad columns stay zero)."""
+    whose columns width .. P - 1 are zero (F(4x4) only; the outputs' pad columns stay zero).
+    skip: the residual epilogue (F(4x4) only): out = out_act(act(conv + bias) + skip_act(skip *
+    skip_s + skip_t)), skip_s / skip_t per output channel (SaWinoProblem skip)."""
     bs = _plane_bs(x, "x")
     if not isinstance(U, WinoFilters):
         raise RuntimeError("conv2d_k3: U must come from ops.wino_weights")
@@ -961,6 +965,17 @@ def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] 
     prob = N.SaWinoProblem(x.data_ptr(), bs, B, Cin, H, W, Uf.data_ptr(), Cout, _ptr(bias),
                            1 if relu else 0, m, s, t, ps, ACT[in_act], out.data_ptr(), _plane_bs(out, "out"),
                            _ptr(partial), P if P != W else 0)
+    if skip is not None:
+        if not f4 or ig or stats:
+            raise RuntimeError("conv2d_k3: the residual epilogue needs the F(4x4) kernel and no statistics")
+        if tuple(skip.shape) != (B, Cout, H, P) or skip.stride(1) != H * P:
+            raise RuntimeError(f"conv2d_k3: skip must be [{B}, {Cout}, {H}, {P}] planes")
+        for v in (skip_s, skip_t):
+            if v is not None:
+                _check(v, "skip_s / skip_t")
+        prob.skip, prob.skip_bs = skip.data_ptr(), _plane_bs(skip, "skip")
+        prob.skip_s, prob.skip_t = _ptr(skip_s), _ptr(skip_t)
+        prob.skip_act, prob.out_act = ACT[skip_act], ACT[out_act]
     # Winograd-domain products actually executed: 36 per 4x4 tile (F4) or 16 per 2x2 tile (F2)
     # per (Cin, Cout) pair; the implicit GEMM: the direct convolution's 9 per output
     if ig:
@@ -1033,7 +1048,7 @@ def _igemm_ok(p: dict, q: dict) -> bool:
     its weights derived (Cout % 128, Cin % 32, |w| < 16), gate modes 1 (Cout % 256) or 2, an input
     transform none / ReLU with Cin <= 512, plane pitches % 4 and 16-byte aligned outputs."""
     U, x, out = q["U"], q["x"], q.get("out")
-    if not IGEMM or U.uig is None:
+    if not IGEMM or U.uig is None or q.get("skip") is not None:
         return False
     g = p.get("gate")
     if (g and not _IG_GATED) or ((q.get("in_aff") is not None or q.get("in_act") is not None) and not _IG_AFF):
@@ -1094,7 +1109,10 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     ok4 = all(oks)
     if gated and not ok4:
         raise RuntimeError("conv2d_k3_multi: gate epilogues need the F(4x4,3x3) kernel (gate_f4_ok)")
-    f4 = ok4 and (gated or sum(_wino4_blocks(**p) for p in plain) >= _WINO4_MIN_BLOCKS)
+    has_skip = any(p.get("skip") is not None for p in plain)
+    if has_skip and not ok4:
+        raise RuntimeError("conv2d_k3_multi: a residual epilogue needs the F(4x4,3x3) kernel")
+    f4 = ok4 and (gated or has_skip or sum(_wino4_blocks(**p) for p in plain) >= _WINO4_MIN_BLOCKS)
     aff = any(p.get("in_aff") is not None or p.get("in_act") is not None for p in plain)
     if gated and aff:
         raise RuntimeError("conv2d_k3_multi: an input transform and a gate epilogue in one launch")
@@ -1150,12 +1168,13 @@ def gate_f4_ok(*xs: torch.Tensor) -> bool:
 
 def conv2d_k3(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = None, relu: bool = False,
               out: Optional[torch.Tensor] = None, in_aff: Optional[Affine] = None, in_act=None,
-              stats: bool = False):
+              stats: bool = False, **residual):
     """3x3 / pad 1 conv via fused Winograd (U from wino_weights); + bias, optional ReLU.
     in_aff / in_act: the producer's norm + activation applied to x while it is loaded.
-    stats: also return the output's InstanceNorm (mean, rstd) per (image, channel)."""
+    stats: also return the output's InstanceNorm (mean, rstd) per (image, channel).
+    residual: skip / skip_s / skip_t / skip_act / out_act of _wino_problem's residual epilogue."""
     return conv2d_k3_multi(dict(x=x, U=U, bias=bias, relu=relu, out=out, in_aff=in_aff, in_act=in_act,
-                                stats=stats))[0]
+                                stats=stats, **residual))[0]
 
 
 def conv_direct_weights(weight: torch.Tensor, stride: int, with_ds: bool = False,

@@ -105,10 +105,14 @@ def _encoders():
     return fnet.to(dev).eval(), cnet.to(dev).eval()
 
 
-@pytest.mark.parametrize("use_wino,use_direct", [(False, False), (True, False), (True, True)])
-def test_fused_encoders_match_modules(use_wino, use_direct):
+@pytest.mark.parametrize("use_wino,use_direct,use_fold", [(False, False, False), (True, False, False),
+                                                           (True, True, False), (True, True, True),
+                                                           (True, False, True)])
+def test_fused_encoders_match_modules(use_wino, use_direct, use_fold):
     """Module forward vs the fused encoders: epilogue passes only (MIOpen convs), and with the
-    Winograd convs applying norm + ReLU on load and producing the InstanceNorm statistics."""
+    Winograd convs applying norm + ReLU on load and producing the InstanceNorm statistics; with
+    the BatchNorm folds (the model's path), the context encoder's residual blocks close in conv2's
+    residual epilogue instead of a norm_act pass."""
     fnet, cnet = _encoders()
     x = rnd(2, 3, 64, 96, seed=21).clamp(-1, 1)
     with torch.no_grad():
@@ -120,7 +124,15 @@ def test_fused_encoders_match_modules(use_wino, use_direct):
         got_f = encoders.fnet_forward(fnet, x, encoders.bn_table(fnet), wino, direct)
         torch.testing.assert_close(got_f, ref_f, atol=1e-4, rtol=1e-4)
         ref_c = cnet(x)
-        got_c = encoders.cnet_forward(cnet, x, encoders.bn_table(cnet), wino, direct)
+        fold = encoders.fold_table(cnet) if use_fold else None
+        ops.WORK = {}
+        got_c = encoders.cnet_forward(cnet, x, encoders.bn_table(cnet), wino, direct, fold)
+        work, ops.WORK = ops.WORK, {}
+        if use_fold:
+            # the blocks the F(4x4) kernel takes close in conv2's epilogue: fewer norm_act bytes
+            encoders.cnet_forward(cnet, x, encoders.bn_table(cnet), wino, direct, None)
+            assert work.get("norm_act", 0.0) < 0.5 * ops.WORK.get("norm_act", 0.0), (work, ops.WORK)
+        ops.WORK = None
         heads = [cnet.outputs08, cnet.outputs16, cnet.outputs32]
         for lvl in range(3):
             for j in range(2):
@@ -151,3 +163,30 @@ def test_wino_input_affine_and_stats():
         w2 = rnd(96, Cin, 3, 3, seed=34) / (3 * Cin ** 0.5)
         got = ops.conv2d_k3(x, ops.wino_weights(w2), in_aff=encoders.bn_affine(bn, None), in_act="relu")
         torch.testing.assert_close(got, F.conv2d(torch.relu(bn(x)), w2, padding=1), atol=2e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("skip_aff,skip_act", [(False, False), (True, False), (True, True)])
+def test_wino4_residual_epilogue(monkeypatch, split, skip_aff, skip_act):
+    """conv2d_k3's residual epilogue (the BatchNorm block close, extractor.py:41-60):
+    relu(relu(conv + b) + skip_act(skip * s + t)) against torch, with an input transform in the
+    same launch and ragged H / W."""
+    monkeypatch.setattr(ops, "W4_SPLIT", split)
+    monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
+    x = rnd(2, 64, 37, 52, seed=5)
+    w = rnd(96, 64, 3, 3, seed=6) / 24
+    b = rnd(96, seed=7)
+    sk = rnd(2, 96, 37, 52, seed=8)
+    s = rnd(96, seed=9).abs() + 0.5 if skip_aff else None
+    t = rnd(96, seed=10) if skip_aff else None
+    am, asc = rnd(64, seed=11) * 0.1, rnd(64, seed=12).abs() + 0.5
+    U = ops.wino_weights(w)
+    got = ops.conv2d_k3(x, U, b, relu=True, in_aff=ops.Affine(am, asc), in_act="relu", skip=sk, skip_s=s,
+                        skip_t=t, skip_act="relu" if skip_act else None, out_act="relu")
+    xin = torch.relu((x - am[None, :, None, None]) * asc[None, :, None, None])
+    skv = sk * s[None, :, None, None] + t[None, :, None, None] if skip_aff else sk
+    if skip_act:
+        skv = torch.relu(skv)
+    ref = torch.relu(torch.relu(torch.nn.functional.conv2d(xin, w, b, padding=1)) + skv)
+    torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
+
