@@ -311,14 +311,16 @@ int sa_conv3d_wd(const float *in, int B, int Cin, int D, int H, int W, const flo
  * runs and tests. */
 void sa_conv3d_wd_set_variant(int variant);
 int sa_conv3d_wd_get_variant(void);
-/* The stride-1 hourglass convs 8 -> 8 (final_agg[1..2]) and 16 -> 16 (down_layers[0][1],
- * agg_layers[1][1..2]; hourglass.py:13-91, submodule.py:25-53) as an implicit GEMM on
+/* The stride-1 hourglass convs 8 -> 8 (final_agg[1..2]), 16 -> 16 (down_layers[0][1],
+ * agg_layers[1][1..2]) and 32 -> 32 (down_layers[1][1]; hourglass.py:13-91, submodule.py:25-53)
+ * as an implicit GEMM on
  * v_mfma_f32_16x16x32_f16 with split operands (csrc/conv3d_mfma.hip): same contract as
  * sa_conv3d_wd for an InstanceNorm + LeakyReLU producer without gate (in_mean / in_rstd per
  * (b, ci), required), fp32-level accuracy (hi/lo f16 activations, weights x 2^12 split the same
  * way; |w| < 8 required, which ops.py checks).
  *   sa_conv3d_mf_weights: [Cin][27][Cout] fp32 (ops.conv3d layout) -> the kernel's B-fragment
  *     table (sa_conv3d_mf_weights_size bytes, device memory; -1 for an unsupported shape).
+ *     Cin = Cout = 8, 16 or 32.
  *   sa_conv3d_mf: out [B, Cout, D, H, W] raw conv of T(in) (pad 1, no bias) + InstanceNorm
  *     partials [B*Cout][parts][2], parts = sa_conv3d_mf_stat_parts(B, Cin, Cout, D, H, W);
  *     D*H*W < 2^30.

@@ -12,7 +12,7 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from stereoanywhere_amd import _native as N, ops  # noqa: E402
 
-SHAPES = [(8, (4, 240, 136, 240), "final_agg"), (16, (4, 120, 68, 120), "agg16")]
+SHAPES = [(8, (4, 240, 136, 240), "final_agg"), (16, (4, 120, 68, 120), "agg16"), (32, (4, 60, 34, 60), "down32")]
 
 
 def timed(fn, reps):

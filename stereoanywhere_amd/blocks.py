@@ -243,7 +243,7 @@ class Hourglass(nn.Module):
         r = ops.conv3d_s1(r, fw["d01_wd"], fw.get("d01_mf"), 16, slope=slope)      # down_layers[0][1]
         down0 = gated(r, self.feature_atts[0], 1)
         r = ops.conv3d(down0, fw["d10"], 32, stride=2, slope=slope)                 # down_layers[1][0]
-        r = ops.conv3d_wd(r, fw["d11_wd"], 32, slope=slope)                         # down_layers[1][1]
+        r = ops.conv3d_s1(r, fw["d11_wd"], fw.get("d11_mf"), 32, slope=slope)      # down_layers[1][1]
         down1 = gated(r, self.feature_atts[1], 2)
         # up-cat convs: the low-res branch is projected to the output channels, then upsampled
         r = ops.conv3d_pointwise_upcat(down0, down1, *fw["a10"], 16, slope=slope)  # agg_layers[1][0]
@@ -251,8 +251,8 @@ class Hourglass(nn.Module):
         r = ops.conv3d_s1(r, fw["a12_wd"], fw.get("a12_mf"), 16, slope=slope)      # agg_layers[1][2]
         x = gated(r, self.feature_atts_up[1], 1)
         r = ops.conv3d_pointwise_upcat(orig, x, *fw["fa0"], 8, slope=slope)         # final_agg[0]
-        # the stride-1 convs: 8 -> 8 at full and 16 -> 16 at half resolution on split-f16 MFMA
-        # (conv3d_mfma.hip), 32 -> 32 and the gated classifier pair on F(4,3) Winograd along D
+        # the stride-1 convs (8 -> 8 at full, 16 -> 16 at half, 32 -> 32 at quarter resolution) on
+        # split-f16 MFMA (conv3d_mfma.hip), the gated classifier pair on F(4,3) Winograd along D
         r = ops.conv3d_s1(r, fw["fa1_wd"], fw.get("fa1_mf"), 8, slope=slope)       # final_agg[1]
         r = ops.conv3d_s1(r, fw["fa2_wd"], fw.get("fa2_mf"), 8, slope=slope)       # final_agg[2]
         r = gated(r, self.final_feature_atts_up, 0)
@@ -278,6 +278,7 @@ class Hourglass(nn.Module):
         return dict(
             fa1_wd=wd(fa1), fa2_wd=wd(fa2), cls_wd=wd(cls), d01_wd=wd(d01), a11_wd=wd(a11), a12_wd=wd(a12),
             fa1_mf=mf(fa1), fa2_mf=mf(fa2), d01_mf=mf(d01), a11_mf=mf(a11), a12_mf=mf(a12),
+            d11_mf=mf(k3(self.down_layers[1][1].conv.weight)),
             d11_wd=wd(k3(self.down_layers[1][1].conv.weight)),
             d00=k3(self.down_layers[0][0].conv.weight), d01=k3(self.down_layers[0][1].conv.weight),
             d10=k3(self.down_layers[1][0].conv.weight), d11=k3(self.down_layers[1][1].conv.weight),

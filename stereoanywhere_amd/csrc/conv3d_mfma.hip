@@ -1,5 +1,6 @@
 // Stride-1 3x3x3 convolutions of the hourglass (final_agg[1..2]: 8 -> 8 at full resolution,
-// down_layers[0][1] / agg_layers[1][1..2]: 16 -> 16 at half resolution; hourglass.py:13-91,
+// down_layers[0][1] / agg_layers[1][1..2]: 16 -> 16 at half, down_layers[1][1]: 32 -> 32 at quarter
+// resolution; hourglass.py:13-91,
 // BasicConv3d submodule.py:25-53) as an implicit GEMM on v_mfma_f32_16x16x32_f16 with split
 // operands.
 //
@@ -16,8 +17,10 @@
 //   * 8 -> 8: N = (2 output planes dd, 8 co), K = 4 input planes e (the pair's 3-tap D windows
 //     span 4 planes; B(e, dd) = W[kd = e - dd], zero outside 0..2): 9 K-steps per plane pair;
 //   * 16 -> 16: N = 16 co, K = (2 planes x 2 channel halves): 2 K-steps per (kh, kw), the second
-//     half-empty (its empty lanes read a zero block).
-// B (the weights) is stationary in registers for the whole kernel (72 / 144 VGPRs); A is read
+//     half-empty (its empty lanes read a zero block);
+//   * 32 -> 32: N = 16 co (a block computes one half of the outputs), K = 4 channel quarters at one
+//     plane: 3 K-steps per (kh, kw), 216 weight registers: 4 waves, one per SIMD.
+// B (the weights) is stationary in registers for the whole kernel (72 / 144 / 216); A is read
 // from LDS with one ds_read_b128 per lane per operand half, at immediate offsets from a per-step
 // base: zero address arithmetic in the MFMA loop.
 //
@@ -39,19 +42,24 @@ using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
 
 constexpr float kWScale = 4096.0f;   // 2^12: weights -> f16 range
-constexpr int kThreads = 512;
 
+// 8 -> 8 and 16 -> 16: 8 waves (two per SIMD); 32 -> 32: 4 waves, one per SIMD (its 216 weight
+// VGPRs), each block one 16-channel half of the outputs (NCH = 2)
 template <int CIN, int COUT>
 struct MfCfg {
   static constexpr int DD = COUT == 8 ? 2 : 1;        // output planes per step (N = DD x co)
+  static constexpr int NCO = 16 / DD;                  // output channels per block
+  static constexpr int NCH = COUT / NCO;               // output-channel blocks
   static constexpr int NCG = CIN / 8;                  // 8-channel groups
   static constexpr int NG = (DD + 2) * NCG;            // K groups (plane, channel group) per (kh, kw)
   static constexpr int KS = (NG + 3) / 4;              // MFMA K-steps per (kh, kw)
   static constexpr bool ZERO = KS * 4 > NG;            // some lanes of the last K-step are empty
   static constexpr int TH = CIN == 8 ? 8 : 4;          // output rows per block
-  static constexpr int TW = 64;                        // output columns per block
-  static constexpr int NWAVE = kThreads / 64;
-  static constexpr int MT = 4 * TH / NWAVE;            // 16-column tiles per wave
+  static constexpr int TW = CIN == 32 ? 32 : 64;       // output columns per block
+  static constexpr int NWAVE = CIN == 32 ? 4 : 8;
+  static constexpr int NTHR = 64 * NWAVE;
+  static constexpr int WPE = CIN == 32 ? 1 : 2;        // waves per SIMD (register budget)
+  static constexpr int MT = TH * TW / 16 / NWAVE;      // 16-column tiles per wave
   static constexpr int WPR = NWAVE / TH;               // waves per output row
   static constexpr int ROWS = TH + 2, COLS = TW + 2;
   static constexpr int PLANE = (ROWS * COLS + 15) / 16 * 16;   // 16-B entries, a multiple of 256 B
@@ -59,12 +67,13 @@ struct MfCfg {
   static constexpr int SLOT = NCG * 2 * PLANE;         // entries per ring slot: [cg][hl][entry]
   static constexpr int ENTRIES = RING * SLOT + (ZERO ? 2 * PLANE : 0);
   static constexpr int JOBS = NCG * ROWS * COLS;       // 8-channel staging jobs per plane
-  static constexpr int JPT = (JOBS * DD + kThreads - 1) / kThreads;   // jobs per thread per step
+  static constexpr int JPT = (JOBS * DD + NTHR - 1) / NTHR;   // jobs per thread per step
+  static constexpr int TAB = 9 * KS * 2 * 64;          // B fragments (f16x8) per output-channel block
   static_assert(ENTRIES * 16 <= 150 * 1024, "LDS");
   static_assert(MT * WPR * 16 == TW, "tiling");
 };
 
-// n-th column of the B fragment -> (output plane offset, output channel)
+// n-th column of the B fragment -> (output plane offset, output channel in the block's NCO)
 template <int COUT>
 __host__ __device__ inline void n_split(int n, int &dd, int &co) {
   if (COUT == 8) {
@@ -76,16 +85,18 @@ __host__ __device__ inline void n_split(int n, int &dd, int &co) {
   }
 }
 
-// [Cin][27][Cout] fp32 (ops.conv3d layout) -> the per-lane B fragments [9 (kh,kw)][KS][hl][64][8]
+// [Cin][27][Cout] fp32 (ops.conv3d layout) -> the per-lane B fragments
+// [NCH][9 (kh,kw)][KS][hl][64][8]
 template <int CIN, int COUT>
 __global__ void mf_weights_kernel(const float *__restrict__ w, f16x8 *__restrict__ tab) {
   using C = MfCfg<CIN, COUT>;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // ((khw * KS + t) * 64 + lane)
-  if (i >= 9 * C::KS * 64) return;
-  const int lane = i & 63, t = (i >> 6) % C::KS, khw = (i >> 6) / C::KS;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // ((ch * 9 + khw) * KS + t) * 64 + lane
+  if (i >= C::NCH * 9 * C::KS * 64) return;
+  const int lane = i & 63, t = (i >> 6) % C::KS, khw = (i >> 6) / C::KS % 9, ch = (i >> 6) / C::KS / 9;
   const int n = lane & 15, G = 4 * t + (lane >> 4);
   int dd, co;
   n_split<COUT>(n, dd, co);
+  co += ch * C::NCO;
   const int e = G / C::NCG, cg = G % C::NCG, kd = e - dd;
   f16x8 hi, lo;
   for (int j = 0; j < 8; ++j) {
@@ -95,12 +106,13 @@ __global__ void mf_weights_kernel(const float *__restrict__ w, f16x8 *__restrict
     hi[j] = h;
     lo[j] = (_Float16)(v - (float)h);
   }
-  tab[((khw * C::KS + t) * 2 + 0) * 64 + lane] = hi;
-  tab[((khw * C::KS + t) * 2 + 1) * 64 + lane] = lo;
+  tab[ch * C::TAB + ((khw * C::KS + t) * 2 + 0) * 64 + lane] = hi;
+  tab[ch * C::TAB + ((khw * C::KS + t) * 2 + 1) * 64 + lane] = lo;
 }
 
 template <int CIN, int COUT>
-__global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3d_mf_kernel(const float *__restrict__ in, int D, int H, int W,
+__global__ __launch_bounds__((MfCfg<CIN, COUT>::NTHR), 1)
+__attribute__((amdgpu_waves_per_eu(MfCfg<CIN, COUT>::WPE, MfCfg<CIN, COUT>::WPE))) void conv3d_mf_kernel(const float *__restrict__ in, int D, int H, int W,
                                                                 const f16x8 *__restrict__ wtab,
                                                                 const float *__restrict__ mean,
                                                                 const float *__restrict__ rstd, float slope,
@@ -109,13 +121,15 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
   using C = MfCfg<CIN, COUT>;
   __shared__ f16x8 lds[C::ENTRIES];
   __shared__ float2 nrm[CIN];
-  __shared__ double red[C::NWAVE][COUT][2];
+  __shared__ double red[C::NWAVE][C::NCO][2];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wid = (int)sa::xcd_remap(blockIdx.x, gridDim.x);
+  const int wid_ = (int)sa::xcd_remap(blockIdx.x, gridDim.x);
+  const int ch = wid_ % C::NCH, wid = wid_ / C::NCH;   // (an output-channel block's neighbours share its input)
   const int bx = wid % tilesW, by = (wid / tilesW) % tilesH, dz = (wid / (tilesW * tilesH)) % tilesD;
   const int b = wid / (tilesW * tilesH * tilesD);
+  wtab += ch * C::TAB;
   const int w0 = bx * C::TW, h0 = by * C::TH, d0 = dz * DR, d1 = min(d0 + DR, D);
   const long HW = (long)H * W;
 
@@ -125,7 +139,7 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
     const float rs = rstd[b * CIN + tid];
     nrm[tid] = make_float2(rs, -mean[b * CIN + tid] * rs);
   }
-  for (int i = tid; i < C::ENTRIES; i += kThreads) lds[i] = f16x8{};
+  for (int i = tid; i < C::ENTRIES; i += C::NTHR) lds[i] = f16x8{};
 
   // B fragments for the whole kernel
   f16x8 bw[9][C::KS][2];
@@ -149,7 +163,7 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
   bool jok[C::JPT];
 #pragma unroll
   for (int k = 0; k < C::JPT; ++k) {
-    const int J = tid + k * kThreads;
+    const int J = tid + k * C::NTHR;
     const int q = J / C::JOBS, r_ = J % C::JOBS, cg = r_ / (C::ROWS * C::COLS), e = r_ % (C::ROWS * C::COLS);
     const int hh = h0 - 1 + e / C::COLS, ww = w0 - 1 + e % C::COLS;
     jok[k] = J < C::DD * C::JOBS && hh >= 0 && hh < H && ww >= 0 && ww < W;
@@ -270,7 +284,7 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
     const int d = dout + dd_l;
     if (d < d1 && h < H) {
       float s = 0.0f, q = 0.0f;
-      float *o = out + (((long)b * COUT + co_l) * D + d) * HW + (long)h * W;
+      float *o = out + (((long)b * COUT + ch * C::NCO + co_l) * D + d) * HW + (long)h * W;
 #pragma unroll
       for (int u = 0; u < C::MT; ++u) {
         const int w = wl + 16 * u;
@@ -312,16 +326,16 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
   // share an output channel
   if (partial) {
 #pragma unroll
-    for (int o = COUT == 8 ? 8 : 16; o < 64; o <<= 1) {
+    for (int o = C::DD == 2 ? 8 : 16; o < 64; o <<= 1) {
       s_acc += __shfl_xor(s_acc, o);
       q_acc += __shfl_xor(q_acc, o);
     }
-    if (lane < COUT) {
+    if (lane < C::NCO) {
       red[wv][lane][0] = s_acc;
       red[wv][lane][1] = q_acc;
     }
     __syncthreads();
-    if (tid < COUT) {
+    if (tid < C::NCO) {
       double a = 0.0, e = 0.0;
 #pragma unroll
       for (int k = 0; k < C::NWAVE; ++k) {
@@ -330,7 +344,7 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
       }
       const int nparts = tilesW * tilesH * tilesD;
       const int blk = (dz * tilesH + by) * tilesW + bx;
-      double *p = partial + (((long)b * COUT + tid) * nparts + blk) * 2;
+      double *p = partial + (((long)b * COUT + ch * C::NCO + tid) * nparts + blk) * 2;
       p[0] = a;
       p[1] = e;
     }
@@ -343,15 +357,20 @@ struct MfGeo {
   int tilesW, tilesH, tilesD, DR;
 };
 
-inline bool mf_shape(int Cin, int Cout) { return (Cin == 8 && Cout == 8) || (Cin == 16 && Cout == 16); }
+inline bool mf_shape(int Cin, int Cout) {
+  return (Cin == 8 && Cout == 8) || (Cin == 16 && Cout == 16) || (Cin == 32 && Cout == 32);
+}
 
+// (tile sizes and blocks per output-channel set of MfCfg<Cin, Cin>)
 MfGeo mf_geo(int B, int Cin, int D, int H, int W) {
-  const int th = Cin == 8 ? 8 : 4, dd = Cin == 8 ? 2 : 1;
-  MfGeo g{(W + 63) / 64, (H + th - 1) / th, 1, 0};
+  const int th = Cin == 8 ? 8 : 4, tw = Cin == 32 ? 32 : 64, dd = Cin == 8 ? 2 : 1, nch = Cin == 32 ? 2 : 1;
+  const int waves = Cin == 32 ? 4 : 8;
+  MfGeo g{(W + tw - 1) / tw, (H + th - 1) / th, 1, 0};
   int dr = g_mf_dr > 0 ? g_mf_dr : D;
   if (g_mf_dr <= 0) {
-    // halve the planes per block until the grid fills the chip ~8 times (or 8 planes)
-    const long per = (long)B * g.tilesW * g.tilesH;
+    // halve the planes per block until the grid fills the chip ~8 times over (in waves: 8 per
+    // block-of-8-waves) or reaches 8 planes
+    const long per = (long)B * g.tilesW * g.tilesH * nch * waves / 8;
     while (dr > 8 && per * ((D + dr - 1) / dr) < 8 * 256) dr = (dr + 1) / 2;
   }
   dr = (dr + dd - 1) / dd * dd;
@@ -366,19 +385,23 @@ extern "C" void sa_conv3d_mf_set_planes(int planes) { g_mf_dr = planes; }
 
 extern "C" long sa_conv3d_mf_weights_size(int Cin, int Cout) {
   if (!mf_shape(Cin, Cout)) return -1;
-  const int ks = Cin == 8 ? MfCfg<8, 8>::KS : MfCfg<16, 16>::KS;
-  return 9L * ks * 2 * 64 * 16;
+  const int tab = Cin == 8 ? MfCfg<8, 8>::NCH * MfCfg<8, 8>::TAB
+                : Cin == 16 ? MfCfg<16, 16>::NCH * MfCfg<16, 16>::TAB : MfCfg<32, 32>::NCH * MfCfg<32, 32>::TAB;
+  return (long)tab * 16;
 }
 
 extern "C" int sa_conv3d_mf_weights(const float *weight, int Cin, int Cout, void *table, void *stream) {
   SA_REQUIRE(weight && table, "sa_conv3d_mf_weights: null pointer");
-  SA_REQUIRE(mf_shape(Cin, Cout), "sa_conv3d_mf_weights: built for 8 -> 8 and 16 -> 16 (got %d -> %d)", Cin, Cout);
+  SA_REQUIRE(mf_shape(Cin, Cout), "sa_conv3d_mf_weights: built for 8 -> 8, 16 -> 16 and 32 -> 32 (got %d -> %d)", Cin,
+             Cout);
   hipStream_t s = sa::as_stream(stream);
   f16x8 *t = reinterpret_cast<f16x8 *>(table);
-  if (Cin == 8)
-    mf_weights_kernel<8, 8><<<(9 * MfCfg<8, 8>::KS * 64 + 255) / 256, 256, 0, s>>>(weight, t);
-  else
-    mf_weights_kernel<16, 16><<<(9 * MfCfg<16, 16>::KS * 64 + 255) / 256, 256, 0, s>>>(weight, t);
+#define SA_MFW(CI)                                                                                              \
+  mf_weights_kernel<CI, CI><<<(MfCfg<CI, CI>::NCH * 9 * MfCfg<CI, CI>::KS * 64 + 255) / 256, 256, 0, s>>>(weight, t)
+  if (Cin == 8) SA_MFW(8);
+  else if (Cin == 16) SA_MFW(16);
+  else SA_MFW(32);
+#undef SA_MFW
   return sa::check_launch("sa_conv3d_mf_weights");
 }
 
@@ -393,23 +416,24 @@ extern "C" int sa_conv3d_mf(const float *in, int B, int Cin, int D, int H, int W
                             double *stats_partial, void *stream) {
   SA_REQUIRE(in && table && out && in_mean && in_rstd, "sa_conv3d_mf: null pointer");
   SA_REQUIRE(B > 0 && D > 0 && H > 0 && W > 0, "sa_conv3d_mf: empty shape");
-  SA_REQUIRE(mf_shape(Cin, Cout), "sa_conv3d_mf: built for 8 -> 8 and 16 -> 16 (got %d -> %d)", Cin, Cout);
+  SA_REQUIRE(mf_shape(Cin, Cout), "sa_conv3d_mf: built for 8 -> 8, 16 -> 16 and 32 -> 32 (got %d -> %d)", Cin, Cout);
   // |InstanceNorm'ed value| <= sqrt(voxels) < 2^15: the f16 hi part cannot overflow
   SA_REQUIRE((long)D * H * W < (1L << 30), "sa_conv3d_mf: a channel volume must hold < 2^30 voxels");
   SA_REQUIRE(slope >= 0.0f && slope <= 1.0f, "sa_conv3d_mf: LeakyReLU slope must lie in [0, 1]");
   SA_REQUIRE((long)Cin * D * H * W * 4 < (1L << 31), "sa_conv3d_mf: an image's volume must hold < 2^31 bytes");
   SA_REQUIRE((long)B * Cin * D * H * W < (1L << 62), "sa_conv3d_mf: size");
   const MfGeo g = mf_geo(B, Cin, D, H, W);
-  const long blocks = (long)B * g.tilesW * g.tilesH * g.tilesD;
+  const long blocks = (long)B * g.tilesW * g.tilesH * g.tilesD * (Cin == 32 ? 2 : 1);
   SA_REQUIRE(blocks < (1L << 31), "sa_conv3d_mf: grid");
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV3D, s);
   const f16x8 *t = reinterpret_cast<const f16x8 *>(table);
-  if (Cin == 8)
-    conv3d_mf_kernel<8, 8><<<(unsigned)blocks, kThreads, 0, s>>>(in, D, H, W, t, in_mean, in_rstd, slope, out,
-                                                                 stats_partial, g.tilesW, g.tilesH, g.tilesD, g.DR);
-  else
-    conv3d_mf_kernel<16, 16><<<(unsigned)blocks, kThreads, 0, s>>>(in, D, H, W, t, in_mean, in_rstd, slope, out,
-                                                                   stats_partial, g.tilesW, g.tilesH, g.tilesD, g.DR);
+#define SA_MF(CI)                                                                                             \
+  conv3d_mf_kernel<CI, CI><<<(unsigned)blocks, MfCfg<CI, CI>::NTHR, 0, s>>>(                                  \
+      in, D, H, W, t, in_mean, in_rstd, slope, out, stats_partial, g.tilesW, g.tilesH, g.tilesD, g.DR)
+  if (Cin == 8) SA_MF(8);
+  else if (Cin == 16) SA_MF(16);
+  else SA_MF(32);
+#undef SA_MF
   return sa::check_launch("sa_conv3d_mf");
 }

@@ -39,7 +39,8 @@ def _torch_input(v, slope=0.01):
     (8, 8, (2, 20, 12, 72), 0), (8, 8, (1, 13, 9, 130), 0), (8, 8, (2, 21, 17, 64), 4),
     (8, 8, (1, 5, 3, 8), 0), (8, 8, (1, 9, 10, 30), 6),
     (16, 16, (2, 15, 10, 66), 0), (16, 16, (1, 7, 9, 20), 3), (16, 16, (2, 24, 20, 128), 0),
-    (16, 16, (1, 11, 5, 62), 5)])
+    (16, 16, (1, 11, 5, 62), 5), (32, 32, (2, 9, 6, 40), 0), (32, 32, (1, 13, 9, 70), 4),
+    (32, 32, (4, 60, 34, 60), 0)])
 def test_conv3d_mf_matches_direct(cin, cout, shape, planes):
     """Ragged W (not a multiple of 4: the scalar store path), H (partial row tiles), D (odd plane
     counts, several D tiles via sa_conv3d_mf_set_planes, a ragged last tile)."""
@@ -58,7 +59,7 @@ def test_conv3d_mf_matches_direct(cin, cout, shape, planes):
     torch.testing.assert_close(a.norm[1], b.norm[1], atol=1e-5, rtol=1e-5)
 
 
-@pytest.mark.parametrize("cin,cout", [(8, 8), (16, 16)])
+@pytest.mark.parametrize("cin,cout", [(8, 8), (16, 16), (32, 32)])
 def test_conv3d_mf_vs_float64(cin, cout):
     """Accuracy against a float64 CPU conv of the same transformed input: the split-f16 products
     land at fp32 level (the direct fp32 kernel's error, within a small factor)."""
@@ -128,7 +129,7 @@ def _time(fn, reps=5):
     return e0.elapsed_time(e1) / reps
 
 
-@pytest.mark.parametrize("cin,shape", [(8, (4, 240, 136, 240)), (16, (4, 120, 68, 120))])
+@pytest.mark.parametrize("cin,shape", [(8, (4, 240, 136, 240)), (16, (4, 120, 68, 120)), (32, (4, 60, 34, 60))])
 def test_conv3d_mf_model_size_faster_than_wd(cin, shape):
     """At cfg2's volumes (final_agg at full, agg_layers at half resolution) the MFMA kernel agrees
     with the F(4,3) kernel and takes less time."""
