@@ -446,6 +446,9 @@ def main():
     ap.add_argument("--conv3d-mfma", type=int, default=None, choices=[0, 1],
                     help="the hourglass's stride-1 8->8 / 16->16 convs on split-f16 MFMA (1) or on the F(4,3) "
                          "VALU kernel (0); default: ops.CONV3D_MFMA")
+    ap.add_argument("--lookup-mfma", type=int, default=None, choices=[0, 1],
+                    help="the fused lookups' convc1 on fp32 MFMA (1) or on the VALU (0); default: the library's "
+                         "(sa_lookup_get_mfma)")
     ap.add_argument("--igemm-max-work", type=int, default=None,
                     help="implicit GEMM only for launches of at most this many output pixels x channels "
                          "(ops.IGEMM_MAX_WORK)")
@@ -499,6 +502,9 @@ def main():
         ops.IGEMM = bool(args.igemm)
     if args.conv3d_mfma is not None:
         ops.CONV3D_MFMA = bool(args.conv3d_mfma)
+    if args.lookup_mfma is not None:
+        from stereoanywhere_amd import _native as _N
+        _N.lib().sa_lookup_set_mfma(int(args.lookup_mfma))
     if args.igemm_max_work is not None:
         ops.IGEMM_MAX_WORK = args.igemm_max_work
     if args.direct_split is not None:

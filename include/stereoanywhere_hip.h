@@ -219,9 +219,10 @@ int sa_corr_lookup_conv1x1(const float *pyramid_a, const float *pyramid_b, int W
                            int B, int H, int W1, const float *weight_kc, const float *bias, int Cout,
                            float *out, void *stream);
 /* a10 on a disparity-sheared pyramid (csrc/corr_shear.hip): level l of image row (b, h) as
- * S_l[e][j] = C_l[j][(j >> l) - e + W_l - 1], e in [0, W_l + ((W1 - 1) >> l)), levels back to back
- * in a slice of sa_shear_slice_size floats per image row: a wave's neighbouring pixels then read
- * neighbouring addresses.  Cells whose k = (j >> l) - e + W_l - 1 falls outside [0, W_l) are not
+ * S_l[e][j] = C_l[j][(j >> l) - e + W_l - 1], e in [0, W_l + ((W1 - 1) >> l)), rows
+ * sa_shear_row_pitch(W1) = W1 rounded up to 32 floats apart (whole 128-byte lines per 32-pixel
+ * segment), levels back to back at sa_shear_level_offset in a slice of sa_shear_slice_size floats
+ * per image row: a wave's neighbouring pixels then read neighbouring addresses.  Cells whose k = (j >> l) - e + W_l - 1 falls outside [0, W_l) are not
  * written (the lookup's tap test gives the reference's zero padding there without using them).
  *   sa_corr_pyramid_shear: the row-layout pyramid [B*H*W1][row_stride] -> sheared [B*H][slice]
  *   sa_corr_volume_pyramid_sheared: sa_corr_volume_pyramid written sheared (C % 16 == 0, W1 and
@@ -234,7 +235,12 @@ int sa_corr_lookup_conv1x1(const float *pyramid_a, const float *pyramid_b, int W
  * slower): the same k-ordered fmaf chain either way.  For A/B runs and tests. */
 void sa_lookup_set_mfma(int on);
 int sa_lookup_get_mfma(void);
+/* the sheared lookup with both volumes in one thread (1, default: one tap grid, both volumes'
+ * gathers in flight together) or one volume per grid row (0).  For A/B runs and tests. */
+void sa_lookup_set_shear_dual(int on);
+int sa_lookup_get_shear_dual(void);
 long sa_shear_slice_size(int W1, int W2, int num_levels);
+long sa_shear_row_pitch(int W1);
 /* 1 when sa_corr_pyramid_shear + sa_corr_lookup_conv1x1_sheared take this geometry (B*H <= 65535,
  * W2 <= 511, 4 levels with the coarsest >= 2 wide), else 0: the caller keeps the row layout */
 int sa_corr_shear_supported(int B, int H, int W1, int W2, int num_levels);

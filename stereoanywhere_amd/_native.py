@@ -55,8 +55,11 @@ SIGNATURES = {
     "sa_corr_lookup": (I, [P, P, I, L, I, I, P, L, I, I, I, P, L, P]),
     "sa_corr_lookup_conv1x1": (I, [P, P, I, L, I, I, P, L, I, I, I, P, P, I, P, P]),
     "sa_lookup_set_mfma": (None, [I]),
+    "sa_lookup_set_shear_dual": (None, [I]),
+    "sa_lookup_get_shear_dual": (I, []),
     "sa_lookup_get_mfma": (I, []),
     "sa_shear_slice_size": (L, [I, I, I]),
+    "sa_shear_row_pitch": (L, [I]),
     "sa_corr_shear_supported": (I, [I, I, I, I, I]),
     "sa_shear_level_offset": (L, [I, I, I, I]),
     "sa_corr_pyramid_shear": (I, [P, L, I, I, I, I, I, P, P]),

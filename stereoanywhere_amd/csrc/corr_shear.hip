@@ -10,7 +10,10 @@
 //   e in [0, E_l), E_l = W_l + ((W1 - 1) >> l)   (all (j, k) pairs of the level, k = (j >> l) -
 //   e + W_l - 1; the entries with k outside [0, W_l) are left unwritten: the lookup's tap test
 //   selects the reference's zero padding there without reading them into the result)
-// so pixel j's cell k sits at row e = (j >> l) - k + W_l - 1, column j.  Neighbouring pixels
+// so pixel j's cell k sits at row e = (j >> l) - k + W_l - 1, column j.  Rows are P = W1 rounded
+// up to 32 floats apart (sa_shear_row_pitch), so a 32-pixel row segment starting at a multiple
+// of 32 is one whole 128-byte line: the producers write whole lines, never two halves from two
+// blocks.  Neighbouring pixels
 // at the same disparity read the same row e at neighbouring columns: one load instruction of
 // the wave is one or two row segments.  Storage ~2x the row layout; written once per forward
 // by sa_corr_pyramid_shear from the row-layout pyramid, read at every GRU iteration.
@@ -21,7 +24,7 @@ namespace {
 
 // the sheared slice of one image row (b, h): levels back to back, each E_l x W1 floats
 struct ShGeo {
-  int L, W1, W2;
+  int L, W1, W2, P;   // P: row pitch (floats)
   int wid[4], rows[4];
   long off[4];   // level offsets within a slice (floats)
   long slice;    // floats per slice, a multiple of 4
@@ -32,21 +35,22 @@ ShGeo shear_geo(int W1, int W2, int L) {
   g.L = L;
   g.W1 = W1;
   g.W2 = W2;
+  g.P = sa::shear_pitch(W1);
   long off = 0;
   for (int l = 0; l < L; ++l) {
     g.wid[l] = sa_pyramid_level_width(W2, l);
     g.rows[l] = g.wid[l] + ((W1 - 1) >> l);
     g.off[l] = off;
-    off += (long)g.rows[l] * W1;
+    off += (long)g.rows[l] * g.P;
   }
-  g.slice = (off + 3) / 4 * 4;
+  g.slice = off;   // (a multiple of 32)
   return g;
 }
 
 // one level of 32 consecutive pixel rows j of one slice: their W_l cells read once into LDS
 // (row-contiguous loads), then every row e of the level written along j (128-byte segments)
 constexpr int SH_J = 32;
-__global__ __launch_bounds__(256) void shear_kernel(const float *__restrict__ pyr, long rs, int W1, int off_l,
+__global__ __launch_bounds__(256) void shear_kernel(const float *__restrict__ pyr, long rs, int W1, int P, int off_l,
                                                     int Wl, int El, int lev, long slice_sz, long soff,
                                                     float *__restrict__ out) {
   extern __shared__ float tile[];   // [SH_J][Wl + 1]
@@ -67,12 +71,12 @@ __global__ __launch_bounds__(256) void shear_kernel(const float *__restrict__ py
   float *dst = out + slice * slice_sz + soff + j;
   for (int e = tid / SH_J; e < El; e += 256 / SH_J) {
     const int k = (j >> lev) - e + Wl - 1;
-    if (k >= 0 && k < Wl) dst[(long)e * W1] = tile[jl * pitch + k];
+    if (k >= 0 && k < Wl) dst[(long)e * P] = tile[jl * pitch + k];
   }
 }
 
 struct ShLGeo {
-  int H, W1;
+  int H, W1, P;
   long cbs;
   long slice;
   int wid[4], rows[4];
@@ -80,26 +84,33 @@ struct ShLGeo {
 };
 
 // lookup_c1_vec_kernel (corr_lookup.hip) on the sheared pyramid: the same per-tap grid
-// arithmetic, the window's cells gathered by one load each from the rows e of column j
-template <int L, int R, int COUT, bool MF = false>
-__global__ __launch_bounds__(256) void lookup_c1_shear_kernel(const float *__restrict__ sa, const float *__restrict__ sb,
+// arithmetic, the window's cells gathered by one load each from the rows e of column j.
+// DUAL: one thread takes its pixel in both volumes (grid.y = 1): the tap grid is computed once,
+// both volumes' gathers are in flight together, and each convc1 weight is loaded once for both
+// (half the waves, each with twice the independent work).
+template <int L, int R, int COUT, bool MF = false, bool DUAL = false>
+__global__ __launch_bounds__(256, (DUAL ? 2 : 1)) void lookup_c1_shear_kernel(const float *__restrict__ sa, const float *__restrict__ sb,
                                                               const float *__restrict__ cx, ShLGeo g, int npix,
                                                               const float *__restrict__ wt,
                                                               const float *__restrict__ bias, int nvol,
                                                               float *__restrict__ out) {
   constexpr int K = 2 * R + 1, NT = L * K, WIN = 2 * R + 4;   // cells x_-R - 1 .. x_-R + 2R + 2
+  constexpr int NV = DUAL ? 2 : 1;
   static_assert(!MF || COUT == 64, "MFMA convc1: 64 outputs");
   __shared__ float c1lds[MF ? 4 : 1][MF ? NT * sa::C1_PITCH : 1];
   const int p0 = blockIdx.x * 256 + threadIdx.x;
   if (!MF && p0 >= npix) return;
   const int p = p0 < npix ? p0 : npix - 1;   // (MFMA: the whole wave takes part)
-  const int v = blockIdx.y;
+  const int v0 = DUAL ? 0 : blockIdx.y;
   const int hw = g.H * g.W1;
   const int b = p / hw, rem = p - b * hw;
   const int h = rem / g.W1, j = rem - h * g.W1;
   const float x = cx[(long)b * g.cbs + rem];
-  const float *__restrict__ S = (v ? sb : sa) + ((long)b * g.H + h) * g.slice + j;
-  float f[NT];
+  const long soff = ((long)b * g.H + h) * g.slice + j;
+  const float *__restrict__ S[NV];
+  S[0] = (v0 ? sb : sa) + soff;
+  if constexpr (DUAL) S[NV - 1] = sb + soff;
+  float f[NV][NT];
 #pragma unroll
   for (int l = 0; l < L; ++l) {
     const int Wl = g.wid[l], El = g.rows[l];
@@ -121,53 +132,77 @@ __global__ __launch_bounds__(256) void lookup_c1_shear_kernel(const float *__res
     }
     // cell k = xi[0] - 1 + c sits at row e = (j >> l) - k + Wl - 1 of column j
     const int e0 = (j >> l) - xi[0] + Wl;
-    const float *__restrict__ lv = S + g.off[l];
-    float cell[WIN];
+    float cell[NV][WIN];
 #pragma unroll
-    for (int c = 0; c < WIN; ++c) {
-      const int e = e0 - c;
-      cell[c] = (unsigned)e < (unsigned)El ? lv[(long)e * g.W1] : 0.0f;
+    for (int vv = 0; vv < NV; ++vv) {
+      const float *__restrict__ lv = S[vv] + g.off[l];
+#pragma unroll
+      for (int c = 0; c < WIN; ++c) {
+        const int e = e0 - c;
+        cell[vv][c] = (unsigned)e < (unsigned)El ? lv[(long)e * g.P] : 0.0f;
+      }
     }
 #pragma unroll
-    for (int t = 0; t < K; ++t) {
-      const int d = xi[t] - xi[0] - t;   // -1, 0 or +1 (fp32 rounding of the grid position)
-      const float c0 = d == 0 ? cell[t + 1] : d < 0 ? cell[t] : cell[t + 2];
-      const float c1 = d == 0 ? cell[t + 2] : d < 0 ? cell[t + 1] : cell[t + 3 < WIN ? t + 3 : WIN - 1];
-      const float v0 = (xi[t] >= 0 && xi[t] <= Wl - 1) ? c0 : 0.0f;
-      const float v1 = (xi[t] + 1 >= 0 && xi[t] + 1 <= Wl - 1) ? c1 : 0.0f;
-      const float w = wgt[t];
-      f[l * K + t] = v0 * (1.0f - w) + v1 * w;
-    }
+    for (int vv = 0; vv < NV; ++vv)
+#pragma unroll
+      for (int t = 0; t < K; ++t) {
+        const int d = xi[t] - xi[0] - t;   // -1, 0 or +1 (fp32 rounding of the grid position)
+        const float c0 = d == 0 ? cell[vv][t + 1] : d < 0 ? cell[vv][t] : cell[vv][t + 2];
+        const float c1 = d == 0 ? cell[vv][t + 2] : d < 0 ? cell[vv][t + 1] : cell[vv][t + 3 < WIN ? t + 3 : WIN - 1];
+        const float a0 = (xi[t] >= 0 && xi[t] <= Wl - 1) ? c0 : 0.0f;
+        const float a1 = (xi[t] + 1 >= 0 && xi[t] + 1 <= Wl - 1) ? c1 : 0.0f;
+        const float w = wgt[t];
+        f[vv][l * K + t] = a0 * (1.0f - w) + a1 * w;
+      }
   }
   if constexpr (MF) {
     const int lane = threadIdx.x & 63;
     sa::C1Weights<NT> w;
     sa::c1_load_weights<NT>(wt, bias, lane, w);
     const int wp0 = p0 - lane;
-    sa::c1_mfma<NT>(f, w, c1lds[threadIdx.x >> 6], lane, [&](int q, int gq, const auto &r) {
-      sa::c1_store4(out, wp0 + 16 * q + 4 * (lane >> 4), 16 * gq + (lane & 15), hw, nvol, v, npix, r);
-    });
+#pragma unroll
+    for (int vv = 0; vv < NV; ++vv)
+      sa::c1_mfma<NT>(f[vv], w, c1lds[threadIdx.x >> 6], lane, [&](int q, int gq, const auto &r) {
+        sa::c1_store4(out, wp0 + 16 * q + 4 * (lane >> 4), 16 * gq + (lane & 15), hw, nvol, v0 + vv, npix, r);
+      });
     return;
   }
-  float *__restrict__ o = out + ((long)b * nvol + v) * COUT * hw + rem;
-#pragma unroll 4
+  // (both volumes' channels c0 .. c0 + 7 together in DUAL: each weight is loaded once)
+  float *__restrict__ o = out + ((long)b * nvol + v0) * COUT * hw + rem;
+#pragma unroll(DUAL ? 2 : 4)
   for (int c0 = 0; c0 < COUT; c0 += 8) {
-    float acc[8];
+    float acc[NV][8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) acc[c] = bias[c0 + c];
+    for (int vv = 0; vv < NV; ++vv)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[vv][c] = bias[c0 + c];
 #pragma unroll
     for (int k = 0; k < NT; ++k) {
 #pragma unroll
-      for (int c = 0; c < 8; ++c) acc[c] = fmaf(wt[k * COUT + c0 + c], f[k], acc[c]);
+      for (int c = 0; c < 8; ++c) {
+        const float wk = wt[k * COUT + c0 + c];
+#pragma unroll
+        for (int vv = 0; vv < NV; ++vv) acc[vv][c] = fmaf(wk, f[vv][k], acc[vv][c]);
+      }
     }
 #pragma unroll
-    for (int c = 0; c < 8; ++c) o[(long)(c0 + c) * hw] = fmaxf(acc[c], 0.0f);
+    for (int vv = 0; vv < NV; ++vv)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) o[((long)vv * COUT + c0 + c) * hw] = fmaxf(acc[vv][c], 0.0f);
   }
 }
 
 }  // namespace
 
 extern "C" int sa_lookup_get_mfma();
+
+namespace {
+int g_shear_dual = 1;   // both volumes per thread in the sheared lookup (A/B switch)
+}
+extern "C" void sa_lookup_set_shear_dual(int on) { g_shear_dual = on ? 1 : 0; }
+extern "C" int sa_lookup_get_shear_dual() { return g_shear_dual; }
+
+extern "C" long sa_shear_row_pitch(int W1) { return W1 > 0 ? sa::shear_pitch(W1) : -1; }
 
 extern "C" long sa_shear_slice_size(int W1, int W2, int num_levels) {
   if (W1 <= 0 || W2 <= 0 || num_levels < 1 || num_levels > 4) return -1;
@@ -205,7 +240,7 @@ extern "C" int sa_corr_pyramid_shear(const float *pyramid, long row_stride, int 
   for (int l = 0; l < num_levels; ++l) {
     const dim3 grid((unsigned)((W1 + SH_J - 1) / SH_J), 1u, (unsigned)(B * H));
     const size_t lds = (size_t)SH_J * (g.wid[l] + 1) * sizeof(float);
-    shear_kernel<<<grid, 256, lds, s>>>(pyramid, row_stride, W1, sa_pyramid_level_offset(W2, l), g.wid[l], g.rows[l],
+    shear_kernel<<<grid, 256, lds, s>>>(pyramid, row_stride, W1, g.P, sa_pyramid_level_offset(W2, l), g.wid[l], g.rows[l],
                                         l, g.slice, g.off[l], sheared);
   }
   return sa::check_launch("sa_corr_pyramid_shear");
@@ -229,6 +264,7 @@ extern "C" int sa_corr_lookup_conv1x1_sheared(const float *sheared_a, const floa
   ShLGeo g{};
   g.H = H;
   g.W1 = W1;
+  g.P = sg.P;
   g.cbs = coords_bstride;
   g.slice = sg.slice;
   for (int l = 0; l < 4; ++l) {
@@ -239,12 +275,19 @@ extern "C" int sa_corr_lookup_conv1x1_sheared(const float *sheared_a, const floa
   const int nvol = sheared_b ? 2 : 1;
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_LOOKUP, s);
-  dim3 grid((unsigned)((npix + 255) / 256), nvol);
-  if (sa_lookup_get_mfma())
-    lookup_c1_shear_kernel<4, 4, 64, true><<<grid, 256, 0, s>>>(sheared_a, sheared_b ? sheared_b : sheared_a, coords_x,
-                                                                g, (int)npix, weight_kc, bias, nvol, out);
-  else
-    lookup_c1_shear_kernel<4, 4, 64><<<grid, 256, 0, s>>>(sheared_a, sheared_b ? sheared_b : sheared_a, coords_x, g,
-                                                          (int)npix, weight_kc, bias, nvol, out);
+  const bool dual = nvol == 2 && g_shear_dual;
+  dim3 grid((unsigned)((npix + 255) / 256), dual ? 1 : nvol);
+  const float *sbb = sheared_b ? sheared_b : sheared_a;
+#define SA_LK(MF_, DU_) \
+  lookup_c1_shear_kernel<4, 4, 64, MF_, DU_><<<grid, 256, 0, s>>>(sheared_a, sbb, coords_x, g, (int)npix, weight_kc, \
+                                                                  bias, nvol, out)
+  if (sa_lookup_get_mfma()) {
+    if (dual) SA_LK(true, true);
+    else SA_LK(true, false);
+  } else {
+    if (dual) SA_LK(false, true);
+    else SA_LK(false, false);
+  }
+#undef SA_LK
   return sa::check_launch("sa_corr_lookup_conv1x1_sheared");
 }

@@ -197,41 +197,37 @@ __device__ __forceinline__ void v2_dma16(__amdgpu_buffer_rsrc_t r, float *lds, i
 struct ShOut {
   float *base;
   long slice;
+  int pitch;   // row pitch (floats, a multiple of 32)
   long off[4];
   int rows[4];
 };
 
-// Level l of a 64-pixel (j) x (64 >> l)-cell (k) tile staged in LDS as T_l[jl][kl] (pitch 64 >> l,
-// the levels back to back: T_l at 64 * (128 - (128 >> l))... see tile_off), written as its
-// sheared rows: row e of the level takes, at column j, the cell kk = (j >> l) - e + W_l - 1 when
-// it lies in this tile and in the level; the wave's 64 lanes are the tile's 64 pixels, so each row
-// segment is one coalesced store.  The LDS reads T_l[jl][(jl >> l) - e'] are conflict-free (the
-// lane's address is jl (64 >> l) + (jl >> l), distinct mod 64 banks).  Cells of the level outside
-// [0, W_l) are not written (the sheared lookup's tap test never uses them).
-__device__ __forceinline__ int sh_tile_off(int l) { return 64 * (128 - (128 >> l)); }   // 0, 4096, 6144, 7168
-
-__device__ __forceinline__ void sh_write_tile(const ShOut &so, long slice_idx, const float *T, int nlev, const int *wid,
-                                              int W1, int j0, int k0l0, int wv, int nw, int lane) {
-  const int j = j0 + lane;
-  float *sl = so.base + slice_idx * so.slice;
-  for (int l = 0; l < nlev; ++l) {
-    const int Wl = wid[l], NK = 64 >> l, K = k0l0 >> l;
-    const int El = so.rows[l];
-    int emin = (j0 >> l) - (K + NK - 1) + Wl - 1, emax = ((j0 + 63) >> l) - K + Wl - 1;
-    emin = max(emin, 0);
-    emax = min(emax, El - 1);
-    const float *Tl = T + sh_tile_off(l) + lane * NK;
-    float *dst = sl + so.off[l] + j;
-    const int jsh = j >> l;
-    for (int e = emin + wv; e <= emax; e += nw) {
-      const int kk = jsh - e + Wl - 1;
-      if (j < W1 && kk >= K && kk < K + NK && kk < Wl) dst[(long)e * W1] = Tl[kk - K];
-    }
+// The sheared rows of one 32-pixel round: level l's cells of pixels [jr0, jr0 + 32) and cells
+// [K, KE) staged in LDS as Tl[jl][kk - K] (pitch pl, odd: the lane reads Tl[jl][(jr0 + jl >> l) - e
+// + W_l - 1 - K] fall in distinct banks), written as rows e of the level: lanes 0-31 row e,
+// lanes 32-63 row e + 1, each a whole 128-byte line (the row pitch is a multiple of 32 floats and
+// jr0 of 32).  Only the rows holding a cell of [K, KE) are visited; cells outside the level are
+// not written (the sheared lookup's tap test never uses them).
+__device__ __forceinline__ void sh_write_round(const ShOut &so, float *sl, const float *Tl, int pl, int l, int Wl,
+                                               int K, int KE, int W1, int jr0, int wv, int nw, int lane) {
+  const int jh = lane & 31, j = jr0 + jh;
+  const int jr1 = min(jr0 + 32, W1);
+  int emin = (jr0 >> l) - (KE - 1) + Wl - 1, emax = ((jr1 - 1) >> l) - K + Wl - 1;
+  emin = max(emin, 0);
+  emax = min(emax, so.rows[l] - 1);
+  const int jsh = j >> l;
+  float *dst = sl + so.off[l] + j;
+  const float *src = Tl + jh * pl - K;
+#pragma unroll 2
+  for (int e = emin + 2 * wv + (lane >> 5); e <= emax; e += 2 * nw) {
+    const int kk = jsh - e + Wl - 1;
+    if (j < jr1 && kk >= K && kk < KE) dst[(long)e * so.pitch] = src[kk];
   }
 }
 
 template <bool TRUNC, bool POW2, bool SHEAR = false>
-__global__ __launch_bounds__(256, 4) void corr_pyramid_v2_kernel(const float *__restrict__ f2, const float *__restrict__ f3,
+// (the sheared epilogue holds the cells while it stages them: 3 blocks per CU, no spill)
+__global__ __launch_bounds__(256, (SHEAR ? 3 : 4)) void corr_pyramid_v2_kernel(const float *__restrict__ f2, const float *__restrict__ f3,
                                                               Geo g, int jblocks, int kblocks, int kstep, float sqrt_c,
                                                               float inv_c, const float *__restrict__ tdisp,
                                                               const float *__restrict__ tconf, float atten,
@@ -329,31 +325,68 @@ __global__ __launch_bounds__(256, 4) void corr_pyramid_v2_kernel(const float *__
     }
   }
   if constexpr (SHEAR) {
-    // the (row, 64-cell group) tiles through LDS (the panels are free after this barrier), then
-    // written as sheared rows
+    // two rounds of 32 pixels (waves 2r, 2r + 1 hold pixels 32r .. 32r + 31) through the (now
+    // free) panel buffers: the round's level-0 cells staged and written as whole-line sheared rows
+    // (sh_write_round), then its level 1..3 cells formed from the staged ones (the row path's
+    // averaging order) into the same space and written the same way
+    constexpr int P0 = 257, P1 = 129, P2 = 65, P3 = 33;   // LDS pitches (odd)
+    constexpr int O2 = 32 * P1, O3 = O2 + 32 * P2;
+    static_assert(32 * P0 <= 2 * V2_BUF && O3 + 32 * P3 <= 32 * P0, "round tiles fit the panel buffers");
     float *T = smem;
-    static_assert(64 * 120 <= 2 * V2_BUF, "sheared tiles fit the panel buffers");
+    float *sl = so.base + ((long)b * g.H + h) * so.slice;
+    const int tid = threadIdx.x, pj = tid & 31, pc = tid >> 5;   // level pass: pixel pj, cells 32 pc ..
+    // the cells in place (the truncation's per-pixel inputs die here)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[gg][t][i] = cell(gg, i, t, j0 + 16 * w + 4 * (lane >> 4) + i, k0 + 64 * gg + 4 * n, dj[i], mj[i]);
 #pragma unroll 1
-    for (int gg = 0; gg < ngroups; ++gg) {
-      __syncthreads();
+    for (int r = 0; r < 2; ++r) {
+      const int jr0 = j0 + 32 * r;
+      if (jr0 >= g.W1) break;   // block-uniform
+      __syncthreads();   // the panels / the previous round's tiles are free
+      if ((w >> 1) == r) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int jl = 16 * w + 4 * (lane >> 4) + i, j = j0 + jl;
-        const int P = k0 + 64 * gg + 4 * n;
-        float v[4];
+        for (int i = 0; i < 4; ++i) {
+          const int jl = 16 * (w & 1) + 4 * (lane >> 4) + i;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] = cell(gg, i, t, j, P, dj[i], mj[i]);
-        *reinterpret_cast<f32x4v *>(T + jl * 64 + 4 * n) = f32x4v{v[0], v[1], v[2], v[3]};
-        const float l1a = (v[0] + v[1]) * 0.5f, l1b = (v[2] + v[3]) * 0.5f;
-        T[sh_tile_off(1) + jl * 32 + 2 * n] = l1a;
-        T[sh_tile_off(1) + jl * 32 + 2 * n + 1] = l1b;
-        const float l2 = (l1a + l1b) * 0.5f;
-        T[sh_tile_off(2) + jl * 16 + n] = l2;
-        const float l3 = (l2 + __shfl_xor(l2, 1)) * 0.5f;
-        if ((n & 1) == 0) T[sh_tile_off(3) + jl * 8 + n / 2] = l3;
+          for (int gg = 0; gg < 4; ++gg) {
+            if (gg >= ngroups) break;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+              T[jl * P0 + 64 * gg + 4 * n + t] = acc[gg][t][i];
+          }
+        }
       }
       __syncthreads();
-      sh_write_tile(so, (long)b * g.H + h, T, g.nlev, g.wid, g.W1, j0, k0 + 64 * gg, w, 4, lane);
+      sh_write_round(so, sl, T, P0, 0, g.wid[0], k0, min(kend, g.wid[0]), g.W1, jr0, w, 4, lane);
+      if (g.nlev < 2) continue;
+      float c1[16], c2[8], c3[4];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const float *t0 = T + pj * P0 + 32 * pc + 2 * u;
+        c1[u] = (t0[0] + t0[1]) * 0.5f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) c2[u] = (c1[2 * u] + c1[2 * u + 1]) * 0.5f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) c3[u] = (c2[2 * u] + c2[2 * u + 1]) * 0.5f;
+      __syncthreads();   // level-0 rows read
+#pragma unroll
+      for (int u = 0; u < 16; ++u) T[pj * P1 + 16 * pc + u] = c1[u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) T[O2 + pj * P2 + 8 * pc + u] = c2[u];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) T[O3 + pj * P3 + 4 * pc + u] = c3[u];
+      __syncthreads();
+#pragma unroll 1
+      for (int l = 1; l < g.nlev; ++l) {
+        const int pl = l == 1 ? P1 : l == 2 ? P2 : P3, ol = l == 1 ? 0 : l == 2 ? O2 : O3;
+        sh_write_round(so, sl, T + ol, pl, l, g.wid[l], k0 >> l, min(kend >> l, g.wid[l]), g.W1, jr0, w, 4, lane);
+      }
     }
     return;
   }
@@ -444,13 +477,9 @@ __global__ __launch_bounds__(256) void pyramid_from_volume_kernel(const float *_
 // (a pair / quad / octet of level-0 cells) lies inside one chunk.
 constexpr int PT_J = 64, PT_CHUNK = 256, PT_PITCH = PT_CHUNK + 4;   // 16-byte aligned rows
 
-// SHEAR: the chunk's cells go out as sheared rows (ShOut) instead: row e of level l takes at
-// pixel j (a lane per pixel of the block) the cell kk = (j >> l) - e + W_l - 1 when it lies in
-// this chunk, formed from the staged level-0 cells with the row path's averaging order.
-template <bool SHEAR = false>
 __global__ __launch_bounds__(256) void pyramid_from_strided_kernel(const float *__restrict__ vol, long sb, long sh,
                                                                    long sk, int H, int W1, int W2, Geo g,
-                                                                   float *__restrict__ pyr, ShOut so) {
+                                                                   float *__restrict__ pyr) {
   __shared__ __attribute__((aligned(16))) float tile[PT_J * PT_PITCH];
   const int j0 = blockIdx.x * PT_J, h = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -482,47 +511,6 @@ __global__ __launch_bounds__(256) void pyramid_from_strided_kernel(const float *
       tile[(jq + 3) * PT_PITCH + (k ^ swz(jq + 3))] = q[i].w;
     }
     __syncthreads();
-    if constexpr (SHEAR) {
-      const int jj = lane, j = j0 + jj;
-      const float *trow = tile + jj * PT_PITCH;
-      const int sw = swz(jj);
-      auto c0v = [&](int k) __attribute__((always_inline)) { return trow[(k - c0) ^ sw]; };
-      float *sl = so.base + ((long)b * H + h) * so.slice;
-      for (int l = 0; l < g.nlev; ++l) {
-        const int Wl = g.wid[l], K = c0 >> l, KE = min((c0 + cw) >> l, Wl);
-        int emin = (j0 >> l) - (KE - 1) + Wl - 1, emax = ((j0 + PT_J - 1) >> l) - K + Wl - 1;
-        emin = max(emin, 0);
-        emax = min(emax, so.rows[l] - 1);
-        float *dst = sl + so.off[l] + j;
-        const int jsh = j >> l;
-        for (int e = emin + wv; e <= emax; e += 4) {
-          const int kk = jsh - e + Wl - 1;
-          if (j < W1 && kk >= K && kk < KE) {
-            const int k = kk << l;
-            float x;
-            if (l == 0) {
-              x = c0v(k);
-            } else {
-              // (v0 + v1) / 2, then pairs of those, as the row path's l1 / l2 / l3
-              float a[8];
-#pragma unroll
-              for (int q = 0; q < 8; ++q) a[q] = q < (1 << l) ? c0v(k + q) : 0.0f;
-              float b1[4];
-#pragma unroll
-              for (int q = 0; q < 4; ++q) b1[q] = (a[2 * q] + a[2 * q + 1]) * 0.5f;
-              if (l == 1) {
-                x = b1[0];
-              } else {
-                const float c2a = (b1[0] + b1[1]) * 0.5f, c2b = (b1[2] + b1[3]) * 0.5f;
-                x = l == 2 ? c2a : (c2a + c2b) * 0.5f;
-              }
-            }
-            dst[(long)e * W1] = x;
-          }
-        }
-      }
-      continue;
-    }
     // a lane per 4 consecutive cells: level 0 as one float4, levels 1-2 in registers, level 3
     // from the neighbour lane
     const int lb = 4 * lane, base = c0 + lb;
@@ -555,6 +543,75 @@ __global__ __launch_bounds__(256) void pyramid_from_strided_kernel(const float *
         if (g.nlev > 2 && base / 4 < g.wid[2]) dst[g.off[2] + base / 4] = l2;
         if (g.nlev > 3 && (lane & 1) == 0 && base / 8 < g.wid[3]) dst[g.off[3] + base / 8] = l3;
       }
+    }
+  }
+}
+
+// The same pyramid written in the disparity-sheared layout (ShOut): a block stages 32 pixels x a
+// 256-cell W2 chunk of one (b, h) in LDS (loads coalesced along W1), writes the chunk's level-0
+// cells as whole-line sheared rows (sh_write_round), forms its level 1..3 cells from the staged
+// ones (the row path's averaging order) into the same LDS space and writes those rows.  Any W2,
+// chunk by chunk (a chunk starts at a multiple of 8: every coarser cell lies inside one).
+constexpr int PS_J = 32, PS_CHUNK = 256;
+__global__ __launch_bounds__(256) void pyramid_from_strided_sheared_kernel(const float *__restrict__ vol, long sb,
+                                                                           long sh, long sk, int H, int W1, int W2,
+                                                                           Geo g, ShOut so) {
+  constexpr int P0 = 257, P1 = 129, P2 = 65, P3 = 33;   // LDS pitches (odd: conflict-free row reads)
+  constexpr int O2 = 32 * P1, O3 = O2 + 32 * P2;
+  static_assert(O3 + 32 * P3 <= 32 * P0, "the level tiles reuse the level-0 tile");
+  __shared__ float T[32 * P0];
+  const int jr0 = blockIdx.x * PS_J, h = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float *src = vol + b * sb + h * sh + jr0;
+  float *sl = so.base + ((long)b * H + h) * so.slice;
+  // loads: thread t takes pixels 4 (t % 8) .. + 3 of cells 32 i + t / 8 (W1 % 4 == 0: a quad is
+  // wholly inside or outside)
+  const int tq = tid & 7, tk = tid >> 3, jq = 4 * tq;
+  const bool qok = jr0 + jq < W1;
+  // level pass: thread t forms pixel t % 32's coarser cells from level-0 cells 32 (t / 32) .. + 31
+  const int pj = tid & 31, pc = tid >> 5;
+  for (int c0 = 0; c0 < W2; c0 += PS_CHUNK) {
+    const int cw = min(PS_CHUNK, W2 - c0);
+    if (c0 > 0) __syncthreads();   // the previous chunk's rows are written
+    float4 q[PS_CHUNK / 32];
+#pragma unroll
+    for (int i = 0; i < PS_CHUNK / 32; ++i) {
+      const int k = 32 * i + tk;
+      q[i] = (qok && k < cw) ? *reinterpret_cast<const float4 *>(src + (long)(c0 + k) * sk + jq)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < PS_CHUNK / 32; ++i) {
+      const int k = 32 * i + tk;
+      T[(jq + 0) * P0 + k] = q[i].x;
+      T[(jq + 1) * P0 + k] = q[i].y;
+      T[(jq + 2) * P0 + k] = q[i].z;
+      T[(jq + 3) * P0 + k] = q[i].w;
+    }
+    __syncthreads();
+    sh_write_round(so, sl, T, P0, 0, g.wid[0], c0, min(c0 + cw, g.wid[0]), W1, jr0, wv, 4, lane);
+    if (g.nlev < 2) continue;
+    float c1[16], c2[8], c3[4];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const float *t0 = T + pj * P0 + 32 * pc + 2 * u;
+      c1[u] = (t0[0] + t0[1]) * 0.5f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) c2[u] = (c1[2 * u] + c1[2 * u + 1]) * 0.5f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) c3[u] = (c2[2 * u] + c2[2 * u + 1]) * 0.5f;
+    __syncthreads();   // level-0 rows read
+#pragma unroll
+    for (int u = 0; u < 16; ++u) T[pj * P1 + 16 * pc + u] = c1[u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) T[O2 + pj * P2 + 8 * pc + u] = c2[u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) T[O3 + pj * P3 + 4 * pc + u] = c3[u];
+    __syncthreads();
+    for (int l = 1; l < g.nlev; ++l) {
+      const int pl = l == 1 ? P1 : l == 2 ? P2 : P3, ol = l == 1 ? 0 : l == 2 ? O2 : O3;
+      sh_write_round(so, sl, T + ol, pl, l, g.wid[l], c0 >> l, min((c0 + cw) >> l, g.wid[l]), W1, jr0, wv, 4, lane);
     }
   }
 }
@@ -704,7 +761,7 @@ extern "C" int sa_corr_pyramid_from_volume_strided(const float *volume, int B, i
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_MONO_PYRAMID, s);
   pyramid_from_strided_kernel<<<dim3((unsigned)((W1 + PT_J - 1) / PT_J), (unsigned)H, (unsigned)B), 256, 0, s>>>(
-      volume, sb, sh, sk, H, W1, W2, g, pyramid, ShOut{});
+      volume, sb, sh, sk, H, W1, W2, g, pyramid);
   return sa::check_launch("sa_corr_pyramid_from_volume_strided");
 }
 
@@ -713,6 +770,7 @@ ShOut make_shout(float *sheared, int W1, int W2, int nlev) {
   ShOut so{};
   so.base = sheared;
   so.slice = sa_shear_slice_size(W1, W2, nlev);
+  so.pitch = (int)sa_shear_row_pitch(W1);
   for (int l = 0; l < 4; ++l) {
     so.off[l] = l < nlev ? sa_shear_level_offset(W1, W2, nlev, l) : 0;
     so.rows[l] = l < nlev ? sa_pyramid_level_width(W2, l) + ((W1 - 1) >> l) : 0;
@@ -734,7 +792,7 @@ extern "C" int sa_corr_pyramid_from_volume_strided_sheared(const float *volume, 
   Geo g = make_geo(1, 1, 1, W2, num_levels, 0);
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_MONO_PYRAMID, s);
-  pyramid_from_strided_kernel<true><<<dim3((unsigned)((W1 + PT_J - 1) / PT_J), (unsigned)H, (unsigned)B), 256, 0, s>>>(
-      volume, sb, sh, sk, H, W1, W2, g, nullptr, make_shout(sheared, W1, W2, num_levels));
+  pyramid_from_strided_sheared_kernel<<<dim3((unsigned)((W1 + PS_J - 1) / PS_J), (unsigned)H, (unsigned)B), 256, 0,
+                                        s>>>(volume, sb, sh, sk, H, W1, W2, g, make_shout(sheared, W1, W2, num_levels));
   return sa::check_launch("sa_corr_pyramid_from_volume_strided_sheared");
 }

@@ -24,6 +24,10 @@ struct TimingScope {
 
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
+// row pitch of the disparity-sheared pyramid (corr_shear.hip): W1 rounded up to 32 floats, so a
+// 32-pixel row segment starting at a multiple of 32 is one 128-byte line
+inline int shear_pitch(int W1) { return (W1 + 31) / 32 * 32; }
+
 inline int check_launch(const char *what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {

@@ -94,20 +94,22 @@ class ScheduleOptions:
     # one load instruction of a wave reads one or two row segments; the row layout spreads
     # it over 64 cache lines); False: the row-layout lookup
     sheared_lookup: bool = True
-    # ... when the stereo volume (B x H4 x W4 x W4 floats) is at least shear_min_bytes (the
-    # sheared lookup is 0.69x the row one at the booster tile batch, 1.03x at B = 4 x 240), as a
-    # copy pass from the row layout (sa_corr_pyramid_shear); True: the two pyramid producers write
-    # the sheared layout themselves (stereo: the volume + truncation + pyramid kernel; mono: the
-    # pyramid from the classifier output) -- measured slower: the diagonal row segments of a
-    # 64 x 64 tile end mid-sector, and the partial 4-byte writes cost the stereo producer 16.1
-    # instead of 3.0 ms at the booster batch, against 2.4 ms for the copy pass
-    # Memory: a sheared copy is ~2x its row-layout pyramid (~3.75x the volume), so the GRU loop
-    # holds ~7.5x the volume instead of ~3.75x; each row pyramid is released right after its copy
-    # (the stereo one before the mono pyramid is built), which bounds the build at ~9.4x (e.g.
-    # 16.5 GB for cfg5's 25-tile booster batch).  Geometries the sheared kernels do not take
+    # ... when the stereo volume (B x H4 x W4 x W4 floats) is at least shear_min_bytes, written
+    # by the two pyramid producers themselves (sheared_producers; stereo: the volume +
+    # truncation + pyramid kernel, mono: the pyramid from the classifier output), in rounds of 32
+    # pixels so that every sheared row segment is one whole 128-byte line (the row pitch is padded
+    # to 32 floats): the stereo producer 203 -> 227 us at cfg2 and 2.68 -> 2.97 ms at the booster
+    # batch (round 4's 64 x 64 diagonal tiles, whose segments ended mid-line: 1.27 / 16.3 ms), the
+    # lookup 58.7 -> 45.0 us per call in the cfg2 forward (counter bytes 1.2x its bytes model, row
+    # layout 2.3x).  sheared_producers=False: a copy pass from the row layout
+    # (sa_corr_pyramid_shear, ~190 us per pyramid at cfg2).
+    # Memory: a sheared pyramid is ~2x its row-layout one (~3.75x the volume), so the GRU loop
+    # holds ~7.5x the volume instead of ~3.75x (e.g. 14 GB for cfg5's 25-tile booster batch); the
+    # copy path releases each row pyramid right after its copy (the stereo one before the mono
+    # pyramid is built), which bounds it at ~9.4x.  Geometries the sheared kernels do not take
     # (ops.shear_supported: W4 > 511, B * H4 > 65535) keep the row layout.
-    sheared_producers: bool = False
-    shear_min_bytes: int = 1 << 30
+    sheared_producers: bool = True
+    shear_min_bytes: int = 0
     # a GRU level whose width is not a multiple of 4 keeps its planes padded to one (zero
     # columns) and runs on F(4x4) with the gates in the epilogue (False: separate gate kernels and
     # F(2x2) launches for that level)

@@ -168,7 +168,7 @@ def _sheared_valid_cells(sh, W1, W2, L=4):
         e = torch.arange(E, device=sh.device).view(E, 1)
         j = torch.arange(W1, device=sh.device).view(1, W1)
         k = (j >> l) - e + wids[l] - 1
-        idx = (o + e * W1 + j)[(k >= 0) & (k < wids[l])]
+        idx = (o + e * int(N.lib().sa_shear_row_pitch(W1)) + j)[(k >= 0) & (k < wids[l])]
         cols.append(sh[:, idx])
     return torch.cat(cols, 1)
 
@@ -227,17 +227,27 @@ def test_lookup_sheared_bit_exact(W1, W2):
                        c(ops.corr_lookup_conv1x1_sheared(sa, sb, W2, 4, 4, g(cx), g(wt), g(bias))))
         finally:
             N.lib().sa_lookup_set_mfma(0)   # (the default: convc1 on the VALU)
+    N.lib().sa_lookup_set_shear_dual(0)   # one volume per thread (default: both in one thread)
+    try:
+        single = c(ops.corr_lookup_conv1x1_sheared(sa, sb, W2, 4, 4, g(cx), g(wt), g(bias)))
+        one_vol = c(ops.corr_lookup_conv1x1_sheared(sa, None, W2, 4, 4, g(cx), g(wt), g(bias)))
+    finally:
+        N.lib().sa_lookup_set_shear_dual(1)
     row, sh = res[1]
     np.testing.assert_array_equal(sh, row)
     np.testing.assert_array_equal(res[0][0], row)
     np.testing.assert_array_equal(res[0][1], row)
+    np.testing.assert_array_equal(single, row)
+    np.testing.assert_array_equal(one_vol, row[0::2])
     # the sheared copy holds every level cell once (other entries are never read)
     _, offs, wids = ops.pyramid_geometry(W2, 4)
     sa_h = c(sa)
     for l in range(4):
         o = int(N.lib().sa_shear_level_offset(W1, W2, 4, l))
         E = wids[l] + ((W1 - 1) >> l)
-        lvl = sa_h[:, o:o + E * W1].reshape(B * H, E, W1)
+        P = int(N.lib().sa_shear_row_pitch(W1))
+        assert P % 32 == 0 and W1 <= P < W1 + 32
+        lvl = sa_h[:, o:o + E * P].reshape(B * H, E, P)
         ref = c(pa)[:, offs[l]:offs[l] + wids[l]].reshape(B * H, W1, wids[l])
         j = np.arange(W1)
         for k in (0, wids[l] - 1, wids[l] // 2):
