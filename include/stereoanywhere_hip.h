@@ -542,6 +542,18 @@ int sa_conv_direct_weights_split(const float *arranged, long n, void *out, void 
 int sa_conv_direct_split(const float *in, long in_bs, int N, int Cin, int H, int W, int K, int S, const void *wg,
                          const void *wd, int Cout, float *out, long out_bs, float *out_ds, long out_ds_bs,
                          double *part, double *part_ds, void *stream);
+/* The stride-2 3x3 conv + fused 1x1 downsample of a residual block's output that was never
+ * written (extractor.py:22-60: the feature encoder's stage boundary): the conv input is
+ * relu(relu((c2 - mean) * rstd) + skip) per (image, channel) plane (mean / rstd [N*Cin], the
+ * block's InstanceNorm of its conv2 output c2; skip the block input), formed while the patch is
+ * staged with sa_norm_act's arithmetic, zero padding outside the image.  wg / wd as for
+ * sa_conv_direct (split = 0) or sa_conv_direct_split (split = 1).  Replaces the block's closing
+ * sa_norm_act pass.  sa_conv_direct_close_supported: 1 when a kernel exists (Cout = 96). */
+int sa_conv_direct_close_supported(int K, int S, int Cout);
+int sa_conv_direct_close(const float *c2, long c2_bs, const float *skip, long skip_bs, const float *mean,
+                         const float *rstd, int N, int Cin, int H, int W, int K, int S, const void *wg,
+                         const void *wd, int split, int Cout, float *out, long out_bs, float *out_ds,
+                         long out_ds_bs, double *part, double *part_ds, void *stream);
 
 /* Epilogues of the MIOpen 2-D convs (encoders extractor.py:6-300, update block update.py:64-110).
  * sa_plane_stats: InstanceNorm2d statistics (biased variance, eps) of each (b, c) plane of

@@ -117,6 +117,8 @@ SIGNATURES = {
     "sa_conv_direct_stat_parts": (L, [I, I]),
     "sa_conv_direct": (I, [P, L, I, I, I, I, I, I, P, P, I, P, L, P, L, P, P, P]),
     "sa_conv_direct_split": (I, [P, L, I, I, I, I, I, I, P, P, I, P, L, P, L, P, P, P]),
+    "sa_conv_direct_close_supported": (I, [I, I, I]),
+    "sa_conv_direct_close": (I, [P, L, P, L, P, P, I, I, I, I, I, I, P, P, I, I, P, L, P, L, P, P, P]),
     "sa_plane_stats": (I, [P, L, I, I, L, F, P, P, P]),
     "sa_norm_act": (I, [P, L, I, I, L, P, P, P, I, I, P, L, P, P, P, I, I, I, P, L, P]),
     "sa_conv3d_upcat_stat_parts": (L, [I, I, I]),

@@ -16,6 +16,10 @@
 //   output = raw conv (no bias: the encoders fold it into the following norm) and optional
 //            float64 InstanceNorm partials per (image, channel, block), as the Winograd conv
 //            writes them (sa_instnorm_finalize)
+//   close  = (CL, sa_conv_direct_close) the input is a residual block's output not yet written:
+//            relu(relu((c2 - mean) * rstd) + skip) per (image, channel) plane, formed while the
+//            patch is staged (c2 and skip loaded at the same offsets; zero padding outside the
+//            image), the arithmetic of sa_norm_act's pass exactly (no contraction)
 #include "sa_common.h"
 
 #pragma clang fp contract(fast)
@@ -80,6 +84,8 @@ struct DCfg {
 struct DirArgs {
   const float *in;
   long in_bs;
+  const float *skip, *cm, *cs;   // CL: the close's skip planes and per-(image, channel) mean / rstd
+  long skip_bs;
   int Cin, H, W, Ho, Wo;
   const float *wg, *wd;   // arranged weights (sa_conv_direct_weights layout)
   int Cout, co_blocks, tiles_w, tiles, nchunks;
@@ -88,11 +94,20 @@ struct DirArgs {
   double *part, *part_ds;
 };
 
-template <int K, int S, int KC, int NTL, bool DS, bool SP = false>
+// relu(relu((v - m) * s) + k) as sa_norm_act computes it (separate rounding of each operation)
+__device__ __forceinline__ float close_value(float v, float m, float s, float k) {
+#pragma clang fp contract(off)
+  const float y = fmaxf((v - m) * s + 0.0f, 0.0f);
+  return fmaxf(y + k, 0.0f);
+}
+
+template <int K, int S, int KC, int NTL, bool DS, bool SP = false, bool CL = false>
 __global__ __launch_bounds__(512, DS ? 2 : 4) void conv_direct_kernel(const DirArgs a) {
   using C = DCfg<K, S, KC, NTL, DS>;
   constexpr int NC = C::NC, NCP = C::NCP, PLANE = C::PLANE, PWP = C::PWP;
   __shared__ __attribute__((aligned(16))) float sm[C::SMEM];
+  // CL: the (mean, rstd) of the staged chunk's channels, double-buffered by chunk parity
+  __shared__ float ctab[CL ? 2 : 1][CL ? 2 * KC : 1];
   float *sx = sm, *sw = sm + C::XN, *sd = sw + KC * C::KK * NCP;
   constexpr int SPARE = C::SMEM - 4;   // slot-less threads commit here (never read)
   const int tid = threadIdx.x, lane = tid & 63;
@@ -142,12 +157,23 @@ __global__ __launch_bounds__(512, DS ? 2 : 4) void conv_direct_kernel(const DirA
     const int row = (4 * i) / NC, col = (4 * i) % NC;
     wl[j] = i < WQ ? row * NCP + col : SPARE;
   }
-  float xr[C::XPT];
+  const __amdgpu_buffer_rsrc_t kin = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(CL ? a.skip + (long)n * a.skip_bs : src), (short)0, (int)((long)a.Cin * hw * 4), 0x00020000);
+  float xr[C::XPT], kr[CL ? C::XPT : 1];
+  float tv = 0.0f;   // CL: this thread's entry of the next chunk's (mean, rstd) table (tid < 2 KC)
   f32x4 wr[C::WPT];
   auto fetch = [&](int chunk) __attribute__((always_inline)) {
     const int xs = chunk * KC * (int)hw * 4;
 #pragma unroll
     for (int j = 0; j < C::XPT; ++j) xr[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xin, xoff[j], xs, 0));
+    if constexpr (CL) {
+#pragma unroll
+      for (int j = 0; j < C::XPT; ++j) kr[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(kin, xoff[j], xs, 0));
+      if (tid < 2 * KC) {
+        const int c = min(chunk * KC + tid % KC, a.Cin - 1);
+        tv = (tid < KC ? a.cm : a.cs)[(long)n * a.Cin + c];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < C::WPT; ++j) {
       const auto v = wds[j] ? __builtin_amdgcn_raw_buffer_load_b128(din, woff[j], chunk * C::DN * 4, 0)
@@ -155,9 +181,20 @@ __global__ __launch_bounds__(512, DS ? 2 : 4) void conv_direct_kernel(const DirA
       wr[j] = f32x4{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3])};
     }
   };
-  auto commit = [&]() __attribute__((always_inline)) {
+  auto put_tab = [&](int chunk) __attribute__((always_inline)) {
+    if (CL && tid < 2 * KC) ctab[CL ? chunk & 1 : 0][tid] = tv;
+  };
+  auto commit = [&](int chunk) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < C::XPT; ++j) sx[xl[j]] = xr[j];
+    for (int j = 0; j < C::XPT; ++j) {
+      float v = xr[j];
+      if constexpr (CL) {
+        const int cl = min((tid + 512 * j) / PLANE, KC - 1);
+        const float *tb = ctab[chunk & 1];
+        v = xoff[j] == OOB ? 0.0f : close_value(v, tb[cl], tb[KC + cl], kr[j]);
+      }
+      sx[xl[j]] = v;
+    }
 #pragma unroll
     for (int j = 0; j < C::WPT; ++j) *reinterpret_cast<f32x4 *>(sw + wl[j]) = wr[j];
   };
@@ -175,7 +212,11 @@ __global__ __launch_bounds__(512, DS ? 2 : 4) void conv_direct_kernel(const DirA
   const int bbase = kq * NCP + ml;
 
   fetch(0);
-  commit();
+  if constexpr (CL) {
+    put_tab(0);
+    __syncthreads();
+  }
+  commit(0);
   __syncthreads();
 #pragma unroll 1
   for (int chunk = 0; chunk < a.nchunks; ++chunk) {
@@ -204,9 +245,10 @@ __global__ __launch_bounds__(512, DS ? 2 : 4) void conv_direct_kernel(const DirA
         for (int t = 0; t < NTL; ++t) prod(sd[bbase + ci0 * NCP + t * 16], &acc[0][NTL + t]);
       }
     }
+    if (CL && chunk + 1 < a.nchunks) put_tab(chunk + 1);   // (its buffer was last read two chunks ago)
     __syncthreads();
     if (chunk + 1 < a.nchunks) {
-      commit();
+      commit(chunk + 1);
       __syncthreads();
     }
   }
@@ -231,7 +273,11 @@ __global__ __launch_bounds__(512, DS ? 2 : 4) void conv_direct_kernel(const DirA
 #pragma unroll 1
       for (int chunk = 0; chunk < a.nchunks; ++chunk) {
         fetch(chunk);
-        commit();
+        if constexpr (CL) {
+          put_tab(chunk);
+          __syncthreads();
+        }
+        commit(chunk);
         __syncthreads();
 #pragma unroll 1
         for (int s = 0; s < C::KSTEPS; ++s) {
@@ -429,21 +475,25 @@ extern "C" long sa_conv_direct_stat_parts(int Ho, int Wo) {
 template <bool SP>
 static int conv_direct_launch(const float *in, long in_bs, int N, int Cin, int H, int W, int K, int S,
                               const float *wg, const float *wd, int Cout, float *out, long out_bs, float *out_ds,
-                              long out_ds_bs, double *part, double *part_ds, void *stream) {
+                              long out_ds_bs, double *part, double *part_ds, void *stream,
+                              const float *skip = nullptr, long skip_bs = 0, const float *cm = nullptr,
+                              const float *cs = nullptr) {
   int KC = 0, NTL = 0;
-  const bool ds = wd != nullptr;
+  const bool ds = wd != nullptr, cl = skip != nullptr;
   SA_REQUIRE(in && wg && out && N > 0 && Cin > 0 && H > 0 && W > 0, "sa_conv_direct: bad arguments");
   SA_REQUIRE(!ds || out_ds, "sa_conv_direct: downsample weights without an output");
   SA_REQUIRE(K != 1 && pick(K, S, Cout, KC, NTL) && ds == (S == 2),
              "sa_conv_direct: no kernel for K=%d S=%d Cout=%d ds=%d", K, S, Cout, (int)ds);
   SA_REQUIRE((long)Cin * H * W < (1L << 31), "sa_conv_direct: image too large");
   SA_REQUIRE(Cin % KC == 0 || Cin <= KC, "sa_conv_direct: Cin must be a multiple of %d (or at most %d)", KC, KC);
+  SA_REQUIRE(!cl || (cm && cs && K == 3 && Cin % KC == 0),
+             "sa_conv_direct_close: needs mean / rstd, a 3x3 stride-2 conv and Cin %% %d == 0", KC);
   const int p = K / 2;
   const int Ho = (H + 2 * p - K) / S + 1, Wo = (W + 2 * p - K) / S + 1;
   const int tiles_w = (Wo + DOTW - 1) / DOTW, tiles = tiles_w * ((Ho + DOTH - 1) / DOTH);
   const int co_blocks = Cout / (16 * NTL);
-  const DirArgs a{in, in_bs, Cin, H, W, Ho, Wo, wg, wd, Cout, co_blocks, tiles_w, tiles, (Cin + KC - 1) / KC,
-                  out, out_ds, out_bs, out_ds_bs, part, part_ds};
+  const DirArgs a{in, in_bs, skip, cm, cs, skip_bs, Cin, H, W, Ho, Wo, wg, wd, Cout, co_blocks, tiles_w, tiles,
+                  (Cin + KC - 1) / KC, out, out_ds, out_bs, out_ds_bs, part, part_ds};
   const long nblk = (long)N * tiles * co_blocks;
   SA_REQUIRE(nblk < (1L << 31), "sa_conv_direct: grid too large");
   hipStream_t s = sa::as_stream(stream);
@@ -451,8 +501,11 @@ static int conv_direct_launch(const float *in, long in_bs, int N, int Cin, int H
   if (K == 7) {
     conv_direct_kernel<7, 1, 4, 4, false, SP><<<(unsigned)nblk, 512, 0, s>>>(a);
   } else if (NTL == 6) {
-    conv_direct_kernel<3, 2, 8, 6, true, SP><<<(unsigned)nblk, 512, 0, s>>>(a);
+    if (cl) conv_direct_kernel<3, 2, 8, 6, true, SP, true><<<(unsigned)nblk, 512, 0, s>>>(a);
+    else conv_direct_kernel<3, 2, 8, 6, true, SP><<<(unsigned)nblk, 512, 0, s>>>(a);
   } else {
+    // (no close form here: staging the skip too would spill the 128-channel kernel's registers)
+    SA_REQUIRE(!cl, "sa_conv_direct_close: no close form for Cout = %d", Cout);
     conv_direct_kernel<3, 2, 8, 8, true, SP><<<(unsigned)nblk, 512, 0, s>>>(a);
   }
   return sa::check_launch("sa_conv_direct");
@@ -472,4 +525,27 @@ extern "C" int sa_conv_direct_split(const float *in, long in_bs, int N, int Cin,
   return conv_direct_launch<true>(in, in_bs, N, Cin, H, W, K, S, static_cast<const float *>(wg),
                                   static_cast<const float *>(wd), Cout, out, out_bs, out_ds, out_ds_bs, part, part_ds,
                                   stream);
+}
+
+// 1 when sa_conv_direct_close has a kernel for this conv (the 96-channel stride-2 3x3 + downsample)
+extern "C" int sa_conv_direct_close_supported(int K, int S, int Cout) {
+  int KC = 0, NTL = 0;
+  return K == 3 && S == 2 && pick(K, S, Cout, KC, NTL) && NTL == 6 ? 1 : 0;
+}
+
+// The stride-2 3x3 conv + 1x1 downsample (sa_conv_direct / _split, split != 0) of a residual
+// block's output that was not written: the input is relu(relu((c2 - mean) * rstd) + skip), mean /
+// rstd per (image, channel) ([N][Cin]), formed while the patch is staged (sa_norm_act's arithmetic)
+extern "C" int sa_conv_direct_close(const float *c2, long c2_bs, const float *skip, long skip_bs, const float *mean,
+                                    const float *rstd, int N, int Cin, int H, int W, int K, int S, const void *wg,
+                                    const void *wd, int split, int Cout, float *out, long out_bs, float *out_ds,
+                                    long out_ds_bs, double *part, double *part_ds, void *stream) {
+  SA_REQUIRE(skip, "sa_conv_direct_close: null skip");
+  if (split)
+    return conv_direct_launch<true>(c2, c2_bs, N, Cin, H, W, K, S, static_cast<const float *>(wg),
+                                    static_cast<const float *>(wd), Cout, out, out_bs, out_ds, out_ds_bs, part, part_ds,
+                                    stream, skip, skip_bs, mean, rstd);
+  return conv_direct_launch<false>(c2, c2_bs, N, Cin, H, W, K, S, static_cast<const float *>(wg),
+                                   static_cast<const float *>(wd), Cout, out, out_bs, out_ds, out_ds_bs, part, part_ds,
+                                   stream, skip, skip_bs, mean, rstd);
 }

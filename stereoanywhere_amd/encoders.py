@@ -27,6 +27,10 @@ import torch.nn.functional as F
 from . import ops
 
 
+# the feature encoder's stage outputs formed by the next stage's stride-2 direct conv while it
+# stages its input (_Close; False: each stage's last block writes its output in a norm_act pass)
+FNET_LAZY_CLOSE = True
+
 # Winograd-transformed filters of the eligible 3x3 convs (ops.conv2d_k3), keyed by the
 # module's weight storage; filled by StereoAnywhere._weights()
 WinoTable = Dict[int, torch.Tensor]
@@ -152,27 +156,51 @@ def _conv_k3(x: torch.Tensor, conv: nn.Conv2d, fin: _Finisher, in_aff=None):
 Pending = Tuple[torch.Tensor, "ops.Affine"]
 
 
+class _Close:
+    """A feature-encoder stage's last block output relu(relu(N2(c2)) + skip) (InstanceNorm
+    statistics of c2 in ``aff``) not yet written: the next stage's stride-2 direct conv forms it
+    while staging its input (ops.conv_direct close=...), so the block's closing norm_act pass and
+    its output tensor disappear; any other consumer materialises it (_materialize)."""
+    __slots__ = ("c2", "aff", "skip")
+
+    def __init__(self, c2, aff, skip):
+        self.c2, self.aff, self.skip = c2, aff, skip
+
+
 def _materialize(x) -> torch.Tensor:
     if isinstance(x, tuple):
         raw, aff = x
         return ops.norm_act(raw, aff, act_in="relu", out=raw)
+    if isinstance(x, _Close):
+        return ops.norm_act(x.c2, x.aff, act_in="relu", skip=x.skip, act_out="relu", out=x.c2)
     return x
 
 
-def residual_block(blk: nn.Module, name: str, x, fin: _Finisher) -> torch.Tensor:
+def residual_block(blk: nn.Module, name: str, x, fin: _Finisher, lazy: bool = False):
+    """lazy: an InstanceNorm block without downsample may return its output as a _Close."""
     w1, w2 = blk.conv1.weight.data_ptr(), blk.conv2.weight.data_ptr()
     pending = d_pre = None
+    direct = _DIRECT.get(w1)
+    close = None
+    if isinstance(x, _Close):
+        if (direct is not None and w2 in _WINO and fin.instance and _direct_fills_chip(x.c2, blk.conv1)
+                and ops.conv_direct_close_supported(3, 2, blk.conv1.out_channels)):
+            close = x
+            x = x.c2
+        else:
+            x = _materialize(x)
     if isinstance(x, tuple):
         if blk.downsample is None and blk.conv1.stride == (1, 1) and w1 in _WINO and w2 in _WINO:
             x, pending = x
         else:
             x = _materialize(x)
     pact = "relu" if pending is not None else None
-    direct = _DIRECT.get(w1)
     if direct is not None and w2 in _WINO and _direct_fills_chip(x, blk.conv1):
         # stride-2 conv1 and the 1x1 downsample in one direct-MFMA launch (raw outputs, IN
-        # statistics in its epilogue); conv2 applies norm1 + ReLU while loading conv1's output
-        r = ops.conv_direct(x, direct[0], 3, 2, blk.conv1.out_channels, wd=direct[1], stats=fin.instance)
+        # statistics in its epilogue); conv2 applies norm1 + ReLU while loading conv1's output.
+        # With a _Close input the previous block's output is formed while staging.
+        cl = None if close is None else (close.skip, close.aff.m, close.aff.s)
+        r = ops.conv_direct(x, direct[0], 3, 2, blk.conv1.out_channels, wd=direct[1], stats=fin.instance, close=cl)
         c1, d = r[0], r[1]
         s1, sd = r[2] if fin.instance else (None, None)
         if not fin.instance:
@@ -213,6 +241,8 @@ def residual_block(blk: nn.Module, name: str, x, fin: _Finisher) -> torch.Tensor
             c2, s2 = _conv(y1, blk.conv2), None
     a2 = fin.affine(name + ".norm2", c2, s2)
     if blk.downsample is None:
+        if lazy and fin.instance and pending is None and a2.t is None and a2.m is not None and a2.s is not None:
+            return _Close(c2, a2, x)
         return ops.norm_act(c2, a2, act_in="relu", skip=x, skip_aff=pending, skip_act=pact, act_out="relu", out=c2)
     d = d_pre if d_pre is not None else _conv(x, blk.downsample[0])
     return ops.norm_act(c2, a2, act_in="relu", skip=d, skip_aff=fin.affine(name + ".norm3", d), act_out="relu",
@@ -272,10 +302,11 @@ def _stem(enc: nn.Module, x: torch.Tensor, fin: _Finisher) -> Pending:
     return c, fin.affine("norm1", c, stats)
 
 
-def _stage(seq: nn.Sequential, name: str, x, fin: _Finisher) -> torch.Tensor:
+def _stage(seq: nn.Sequential, name: str, x, fin: _Finisher, lazy_out: bool = False):
+    """lazy_out: the last block's output may stay a _Close for the next stage's first block."""
     for i, blk in enumerate(seq):
-        x = residual_block(blk, f"{name}.{i}", x, fin)
-    return _materialize(x)
+        x = residual_block(blk, f"{name}.{i}", x, fin, lazy=lazy_out and i == len(seq) - 1)
+    return x if lazy_out else _materialize(x)
 
 
 def _install(wino: Optional[WinoTable], direct: Optional[DirectTable], fold: Optional[FoldTable] = None) -> None:
@@ -294,7 +325,8 @@ def fnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
     fin = _Finisher("instance" if isinstance(enc.norm1, nn.InstanceNorm2d) else "batch", table)
     x = _stem(enc, x, fin)
     for s in ("layer1", "layer2", "layer3"):
-        x = _stage(getattr(enc, s), s, x, fin)
+        # (layer1 / layer2 outputs: the next stage's stride-2 direct conv may form them on load)
+        x = _stage(getattr(enc, s), s, x, fin, lazy_out=FNET_LAZY_CLOSE and s != "layer3")
     return F.conv2d(x, enc.conv2.weight, enc.conv2.bias)
 
 

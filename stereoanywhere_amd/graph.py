@@ -37,7 +37,7 @@ class ForwardGraph:
     def _make_key(self, xs, iters):
         m = self.model
         m._weights()   # the derived weights of the current parameter version
-        from . import ops
+        from . import encoders, ops
         from . import _native as N
         # everything that picks the captured kernels: the schedule, the module-level kernel
         # switches and the library's own A/B switches (set by A/B scripts and tests) and the
@@ -50,7 +50,8 @@ class ForwardGraph:
                                          "sa_lookup_get_shear_dual"))
         return (tuple((tuple(x.shape), x.dtype, x.device) for x in xs), iters, dataclasses.astuple(m.opts),
                 m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_SPLIT, ops.IGEMM, ops.IGEMM_MAX_WORK,
-                                                   ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS, ops.SPLIT_GUARD, ops.CONV3D_MFMA),
+                                                   ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS, ops.SPLIT_GUARD, ops.CONV3D_MFMA,
+                                                   encoders.FNET_LAZY_CLOSE),
                 c_switches, args)
 
     def __call__(self, image2, image3, mde2, mde3, iters: int = 12, test_mode: bool = True):

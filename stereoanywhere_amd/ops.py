@@ -1202,11 +1202,19 @@ def conv_direct_weights(weight: torch.Tensor, stride: int, with_ds: bool = False
     return out
 
 
+def conv_direct_close_supported(K: int, stride: int, Cout: int) -> bool:
+    """Whether conv_direct takes ``close`` for this conv (sa_conv_direct_close_supported)."""
+    return bool(N.lib().sa_conv_direct_close_supported(K, stride, Cout))
+
+
 def conv_direct(x: torch.Tensor, wg: torch.Tensor, K: int, stride: int, Cout: int,
-                wd: Optional[torch.Tensor] = None, stats: bool = False):
+                wd: Optional[torch.Tensor] = None, stats: bool = False, close=None):
     """KxK conv (padding K//2, no bias) on fp32 MFMA: the 7x7 stems and the stride-2 3x3 conv
     with its fused 1x1 stride-2 downsample (wd).  Returns [out, (out_ds)] and, with stats,
-    the InstanceNorm (mean, rstd) of each output after it."""
+    the InstanceNorm (mean, rstd) of each output after it.
+    close = (skip, mean, rstd): x is a residual block's raw conv2 output and the conv's input is
+    the block's output relu(relu((x - mean) * rstd) + skip), formed while staging
+    (sa_conv_direct_close; conv_direct_close_supported)."""
     bs = _plane_bs(x, "x")
     if wg.dtype == torch.int32:   # split (hi, lo) pairs (conv_direct_weights under DIRECT_SPLIT)
         if wg.device.type != "cuda" or not wg.is_contiguous():
@@ -1226,9 +1234,21 @@ def conv_direct(x: torch.Tensor, wg: torch.Tensor, K: int, stride: int, Cout: in
     split = wg.dtype == torch.int32
     if wd is not None and (wd.dtype == torch.int32) != split:
         raise RuntimeError("conv_direct: wg and wd must both be split or both fp32 (conv_direct_weights)")
-    N.call("sa_conv_direct_split" if split else "sa_conv_direct", x.data_ptr(), bs, B, Cin, H, W, K, stride,
-           wg.data_ptr(), _ptr(wd), Cout, out.data_ptr(), Cout * Ho * Wo, _ptr(out_ds), Cout * Ho * Wo, _ptr(pa),
-           _ptr(pd), _stream(x))
+    if close is not None:
+        skip, mean, rstd = close
+        if tuple(skip.shape) != (B, Cin, H, W):
+            raise RuntimeError("conv_direct: close skip shape mismatch")
+        for t, nm in ((mean, "mean"), (rstd, "rstd")):
+            _check(t, nm)
+            if t.numel() != B * Cin:
+                raise RuntimeError(f"conv_direct: close {nm} must have B*Cin entries")
+        N.call("sa_conv_direct_close", x.data_ptr(), bs, skip.data_ptr(), _plane_bs(skip, "skip"), mean.data_ptr(),
+               rstd.data_ptr(), B, Cin, H, W, K, stride, wg.data_ptr(), _ptr(wd), int(split), Cout, out.data_ptr(),
+               Cout * Ho * Wo, _ptr(out_ds), Cout * Ho * Wo, _ptr(pa), _ptr(pd), _stream(x))
+    else:
+        N.call("sa_conv_direct_split" if split else "sa_conv_direct", x.data_ptr(), bs, B, Cin, H, W, K, stride,
+               wg.data_ptr(), _ptr(wd), Cout, out.data_ptr(), Cout * Ho * Wo, _ptr(out_ds), Cout * Ho * Wo, _ptr(pa),
+               _ptr(pd), _stream(x))
     # products executed: the stem's channels padded to the kernel's chunk of 4
     cin_x = -(-Cin // 4) * 4 if K == 7 else Cin
     _account("conv2d_direct", 2.0 * B * Cout * cin_x * K * K * Ho * Wo

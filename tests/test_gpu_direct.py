@@ -52,6 +52,32 @@ def test_stride2_with_downsample(monkeypatch, B, Cin, Cout, H, W, split):
     torch.testing.assert_close(sd[0], ref_d.mean(dim=(2, 3)).flatten(), atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("B,H,W", [(2, 34, 70), (1, 27, 45), (3, 16, 32)])
+def test_stride2_close_on_load(monkeypatch, B, H, W, split):
+    """The block output relu(relu((c2 - mean) * rstd) + skip) formed while the patch is staged
+    (sa_conv_direct_close) gives exactly the conv of the materialised output (ops.norm_act: the
+    same arithmetic), outputs and InstanceNorm statistics; zero padding stays zero; a 128-channel
+    conv has no close form."""
+    monkeypatch.setattr(ops, "DIRECT_SPLIT", split)
+    Cin, Cout = 64, 96
+    c2 = rnd(B, Cin, H, W, seed=6) * 3 + 0.5
+    skip = torch.relu(rnd(B, Cin, H, W, seed=7))
+    mean = rnd(B * Cin, seed=8) * 0.3
+    rstd = torch.rand(B * Cin, device=dev) + 0.2
+    w = rnd(Cout, Cin, 3, 3, seed=9) / (3 * Cin ** 0.5)
+    wd = rnd(Cout, Cin, 1, 1, seed=10) / Cin ** 0.5
+    wg_, wd_ = ops.conv_direct_weights(w, 2), ops.conv_direct_weights(wd, 2, with_ds=True)
+    y = ops.norm_act(c2, ops.Affine(mean, rstd, None, per_plane=True), act_in="relu", skip=skip, act_out="relu")
+    ref = ops.conv_direct(y, wg_, 3, 2, Cout, wd=wd_, stats=True)
+    got = ops.conv_direct(c2, wg_, 3, 2, Cout, wd=wd_, stats=True, close=(skip, mean, rstd))
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+    for (m0, r0), (m1, r1) in zip(got[2], ref[2]):
+        assert torch.equal(m0, m1) and torch.equal(r0, r1)
+    torch.testing.assert_close(got[0], F.conv2d(y, w, stride=2, padding=1), atol=2e-5, rtol=1e-4)
+    assert ops.conv_direct_close_supported(3, 2, 96) and not ops.conv_direct_close_supported(3, 2, 128)
+
+
 def test_unsupported_shapes_raise():
     x = rnd(1, 12, 16, 16)
     with pytest.raises(RuntimeError):
