@@ -192,14 +192,97 @@ __global__ __launch_bounds__(256, (DUAL ? 2 : 1)) void lookup_c1_shear_kernel(co
   }
 }
 
+// The same lookup + convc1 with the work spread over a block's 256 threads for 64 pixels: phase 1
+// gives each (volume, level) of a pixel to its own thread (4 or 8 tasks per pixel: 12 gathers and
+// the 9 taps each), the taps go to LDS as [volume][tap][pixel]; phase 2 gives each thread 16 of the
+// 64 convc1 outputs of one pixel in every volume (the same k-ordered fmaf chains, weights uniform
+// per wave).  Four times the waves of lookup_c1_shear_kernel with a fraction of its registers:
+// the gathers and the output stores of many more waves overlap.
+template <int L, int R, int COUT>
+__global__ __launch_bounds__(256) void lookup_c1_shear_lds_kernel(const float *__restrict__ sa,
+                                                                  const float *__restrict__ sb,
+                                                                  const float *__restrict__ cx, ShLGeo g, int npix,
+                                                                  const float *__restrict__ wt,
+                                                                  const float *__restrict__ bias, int nvol,
+                                                                  float *__restrict__ out) {
+  constexpr int K = 2 * R + 1, NT = L * K, WIN = 2 * R + 4, PX = 64, CG = COUT / 4;
+  static_assert(COUT % 4 == 0, "four channel groups");
+  __shared__ float ft[2][NT][PX];
+  const int tid = threadIdx.x, px = tid & (PX - 1);
+  const int grp = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar weight loads
+  const int p0 = blockIdx.x * PX + px;
+  const int p = p0 < npix ? p0 : npix - 1;
+  const int hw = g.H * g.W1;
+  const int b = p / hw, rem = p - b * hw;
+  const int h = rem / g.W1, j = rem - h * g.W1;
+  const float x = cx[(long)b * g.cbs + rem];
+  const long soff = ((long)b * g.H + h) * g.slice + j;
+  // phase 1: tasks (volume, level) = grp, grp + 4 (wave-uniform)
+  for (int task = grp; task < nvol * L; task += 4) {
+    const int v = task / L, l = task % L;
+    const int Wl = g.wid[l], El = g.rows[l];
+    const float xl = x / (float)(1 << l);
+    const float denom = (float)(Wl - 1);
+    const float sf = (float)(Wl - 1) / 2.0f;
+    int xi[K];
+    float wgt[K];
+#pragma unroll
+    for (int t = -R; t <= R; ++t) {
+      const float x0 = (float)t + xl;
+      const float xg = 2.0f * x0 / denom - 1.0f;
+      const float ix = (xg + 1.0f) * sf;
+      float xw = floorf(ix);
+      wgt[t + R] = ix - xw;
+      xw = fminf(fmaxf(xw, -16777216.0f), 16777216.0f);
+      xi[t + R] = (int)xw;
+    }
+    const int e0 = (j >> l) - xi[0] + Wl;
+    const float *__restrict__ lv = (v ? sb : sa) + soff + g.off[l];
+    float cell[WIN];
+#pragma unroll
+    for (int c = 0; c < WIN; ++c) {
+      const int e = e0 - c;
+      cell[c] = (unsigned)e < (unsigned)El ? lv[(long)e * g.P] : 0.0f;
+    }
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const int d = xi[t] - xi[0] - t;
+      const float c0 = d == 0 ? cell[t + 1] : d < 0 ? cell[t] : cell[t + 2];
+      const float c1 = d == 0 ? cell[t + 2] : d < 0 ? cell[t + 1] : cell[t + 3 < WIN ? t + 3 : WIN - 1];
+      const float a0 = (xi[t] >= 0 && xi[t] <= Wl - 1) ? c0 : 0.0f;
+      const float a1 = (xi[t] + 1 >= 0 && xi[t] + 1 <= Wl - 1) ? c1 : 0.0f;
+      const float w = wgt[t];
+      ft[v][l * K + t][px] = a0 * (1.0f - w) + a1 * w;
+    }
+  }
+  __syncthreads();
+  if (p0 >= npix) return;
+  // phase 2: channels CG * grp .. + CG - 1, one volume after the other (16 accumulators)
+  const int c0 = CG * grp;
+  for (int v = 0; v < nvol; ++v) {
+    float acc[CG];
+#pragma unroll
+    for (int c = 0; c < CG; ++c) acc[c] = bias[c0 + c];
+#pragma unroll 4
+    for (int k = 0; k < NT; ++k) {
+      const float f = ft[v][k][px];
+#pragma unroll
+      for (int c = 0; c < CG; ++c) acc[c] = fmaf(wt[k * COUT + c0 + c], f, acc[c]);
+    }
+    float *__restrict__ o = out + (((long)b * nvol + v) * COUT + c0) * hw + rem;
+#pragma unroll
+    for (int c = 0; c < CG; ++c) o[(long)c * hw] = fmaxf(acc[c], 0.0f);
+  }
+}
+
 }  // namespace
 
 extern "C" int sa_lookup_get_mfma();
 
 namespace {
-int g_shear_dual = 1;   // both volumes per thread in the sheared lookup (A/B switch)
+int g_shear_dual = 2;   // sheared lookup form: 0 one volume per thread, 1 both, 2 spread over the block (A/B)
 }
-extern "C" void sa_lookup_set_shear_dual(int on) { g_shear_dual = on ? 1 : 0; }
+extern "C" void sa_lookup_set_shear_dual(int on) { g_shear_dual = on < 0 ? 0 : on > 2 ? 2 : on; }
 extern "C" int sa_lookup_get_shear_dual() { return g_shear_dual; }
 
 extern "C" long sa_shear_row_pitch(int W1) { return W1 > 0 ? sa::shear_pitch(W1) : -1; }
@@ -275,9 +358,15 @@ extern "C" int sa_corr_lookup_conv1x1_sheared(const float *sheared_a, const floa
   const int nvol = sheared_b ? 2 : 1;
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_LOOKUP, s);
+  const float *sbb = sheared_b ? sheared_b : sheared_a;
+  if (g_shear_dual == 2 && !sa_lookup_get_mfma()) {
+    lookup_c1_shear_lds_kernel<4, 4, 64><<<(unsigned)((npix + 63) / 64), 256, 0, s>>>(sheared_a, sbb, coords_x, g,
+                                                                                     (int)npix, weight_kc, bias, nvol,
+                                                                                     out);
+    return sa::check_launch("sa_corr_lookup_conv1x1_sheared");
+  }
   const bool dual = nvol == 2 && g_shear_dual;
   dim3 grid((unsigned)((npix + 255) / 256), dual ? 1 : nvol);
-  const float *sbb = sheared_b ? sheared_b : sheared_a;
 #define SA_LK(MF_, DU_) \
   lookup_c1_shear_kernel<4, 4, 64, MF_, DU_><<<grid, 256, 0, s>>>(sheared_a, sbb, coords_x, g, (int)npix, weight_kc, \
                                                                   bias, nvol, out)

@@ -227,18 +227,21 @@ def test_lookup_sheared_bit_exact(W1, W2):
                        c(ops.corr_lookup_conv1x1_sheared(sa, sb, W2, 4, 4, g(cx), g(wt), g(bias))))
         finally:
             N.lib().sa_lookup_set_mfma(0)   # (the default: convc1 on the VALU)
-    N.lib().sa_lookup_set_shear_dual(0)   # one volume per thread (default: both in one thread)
+    forms = {}   # 0: one volume per thread, 1: both in one thread, 2 (default): spread over the block
     try:
-        single = c(ops.corr_lookup_conv1x1_sheared(sa, sb, W2, 4, 4, g(cx), g(wt), g(bias)))
-        one_vol = c(ops.corr_lookup_conv1x1_sheared(sa, None, W2, 4, 4, g(cx), g(wt), g(bias)))
+        for form in (0, 1, 2):
+            N.lib().sa_lookup_set_shear_dual(form)
+            forms[form] = (c(ops.corr_lookup_conv1x1_sheared(sa, sb, W2, 4, 4, g(cx), g(wt), g(bias))),
+                           c(ops.corr_lookup_conv1x1_sheared(sa, None, W2, 4, 4, g(cx), g(wt), g(bias))))
     finally:
-        N.lib().sa_lookup_set_shear_dual(1)
+        N.lib().sa_lookup_set_shear_dual(2)
     row, sh = res[1]
     np.testing.assert_array_equal(sh, row)
     np.testing.assert_array_equal(res[0][0], row)
     np.testing.assert_array_equal(res[0][1], row)
-    np.testing.assert_array_equal(single, row)
-    np.testing.assert_array_equal(one_vol, row[0::2])
+    for form, (both, one_vol) in forms.items():
+        np.testing.assert_array_equal(both, row, err_msg=f"form {form}")
+        np.testing.assert_array_equal(one_vol, row[0::2], err_msg=f"form {form}")
     # the sheared copy holds every level cell once (other entries are never read)
     _, offs, wids = ops.pyramid_geometry(W2, 4)
     sa_h = c(sa)
