@@ -217,8 +217,12 @@ __global__ __launch_bounds__(256) void lookup_c1_shear_lds_kernel(const float *_
   const int h = rem / g.W1, j = rem - h * g.W1;
   const float x = cx[(long)b * g.cbs + rem];
   const long soff = ((long)b * g.H + h) * g.slice + j;
-  // phase 1: tasks (volume, level) = grp, grp + 4 (wave-uniform)
-  for (int task = grp; task < nvol * L; task += 4) {
+  // phase 1: tasks (volume, level) = grp, grp + 4 (wave-uniform; unrolled: both tasks' gathers
+  // in flight together)
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int task = grp + 4 * tt;
+    if (task >= nvol * L) break;
     const int v = task / L, l = task % L;
     const int Wl = g.wid[l], El = g.rows[l];
     const float xl = x / (float)(1 << l);
