@@ -181,8 +181,9 @@ __device__ __forceinline__ f16x4 w4_split(const float x) {
 }
 
 // Range guard of the split kernel: blocks whose f16 operands overflowed (|V| >= 65520 turns hi
-// into inf, so every product of that value, and the outputs it feeds, are NaN) skip their epilogue
-// and are recomputed on fp32 MFMA by wino_f4k3_redo_kernel; this counts them (sa_split_redo_blocks)
+// into inf, so every product of that value, and the outputs it feeds, are NaN) run their item
+// again inside the launch on exactly scaled inputs (w4_body's xscale); this counts them
+// (sa_split_redo_blocks)
 __device__ unsigned g_w4_redo_blocks;
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, float *lds, int voff, int soff) {

@@ -279,6 +279,35 @@ def test_forward_graph_replays_the_forward(model):
         assert float((got - ref).abs().max()) < 1e-4
 
 
+def test_pipelined_forward_equals_forward_graph(model):
+    """graph.PipelinedForward (two ForwardGraph instances, each capturing on its own stream, replayed
+    round-robin on two streams with both forwards in flight) returns what one ForwardGraph returns
+    for each batch, bit for bit, with the split kernels' range guard firing in both (a pair scaled
+    so that F(4x4) blocks overflow f16 and recompute in-kernel)."""
+    from stereoanywhere_amd.graph import ForwardGraph, PipelinedForward
+    pf, fg = PipelinedForward(model, depth=2), ForwardGraph(model)
+    batches = []
+    for seed, scale in ((31, 1.0), (32, 3e3), (33, 1.0), (34, 3e3)):
+        pb = synth.synthetic_batch(2, 128, 256, 48.0, seed0=seed)
+        x = [torch.from_numpy(pb[k]).cuda() for k in ("left", "right", "mono_left", "mono_right")]
+        batches.append([t * scale for t in x])   # (the mono maps feed the BatchNorm context encoder)
+    from stereoanywhere_amd import _native as N
+    N.lib().sa_split_redo_blocks(1)
+    with torch.no_grad():
+        ref = [fg(*x, iters=3)[0].clone() for x in batches]
+        torch.cuda.synchronize()
+        got = []
+        for x in batches:   # consecutive batches overlap on the two streams
+            out = pf(*x, iters=3)[0]
+            with torch.cuda.stream(pf.streams[(pf._i - 1) % len(pf.graphs)]):
+                got.append(out.clone())   # (before that instance's next replay reuses the buffer)
+        torch.cuda.synchronize()
+    assert N.lib().sa_split_redo_blocks(1) > 0   # the guard fired
+    for r, g_ in zip(ref, got):
+        assert torch.isfinite(r).all()
+        assert torch.equal(r, g_)
+
+
 @pytest.mark.parametrize("name,over", [("vd1", dict(vol_downsample=1)), ("aggstereo", dict(use_aggregate_stereo_vol=True)),
                                        ("rawmono", dict(use_aggregate_mono_vol=False)),
                                        ("addhg2", dict(n_additional_hourglass=2))])
