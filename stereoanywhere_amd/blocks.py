@@ -242,7 +242,7 @@ class Hourglass(nn.Module):
         r = ops.conv3d(orig, fw["d00"], 16, stride=2, slope=slope)                  # down_layers[0][0]
         r = ops.conv3d_s1(r, fw["d01_wd"], fw.get("d01_mf"), 16, slope=slope)      # down_layers[0][1]
         down0 = gated(r, self.feature_atts[0], 1)
-        r = ops.conv3d(down0, fw["d10"], 32, stride=2, slope=slope)                 # down_layers[1][0]
+        r = ops.conv3d_s2(down0, fw["d10"], fw.get("d10_mf"), 32, slope=slope)    # down_layers[1][0]
         r = ops.conv3d_s1(r, fw["d11_wd"], fw.get("d11_mf"), 32, slope=slope)      # down_layers[1][1]
         down1 = gated(r, self.feature_atts[1], 2)
         # up-cat convs: the low-res branch is projected to the output channels, then upsampled
@@ -279,6 +279,7 @@ class Hourglass(nn.Module):
             fa1_wd=wd(fa1), fa2_wd=wd(fa2), cls_wd=wd(cls), d01_wd=wd(d01), a11_wd=wd(a11), a12_wd=wd(a12),
             fa1_mf=mf(fa1), fa2_mf=mf(fa2), d01_mf=mf(d01), a11_mf=mf(a11), a12_mf=mf(a12),
             d11_mf=mf(k3(self.down_layers[1][1].conv.weight)),
+            d10_mf=ops.conv3d_s2mf_weights(k3(self.down_layers[1][0].conv.weight)),
             d11_wd=wd(k3(self.down_layers[1][1].conv.weight)),
             d00=k3(self.down_layers[0][0].conv.weight), d01=k3(self.down_layers[0][1].conv.weight),
             d10=k3(self.down_layers[1][0].conv.weight), d11=k3(self.down_layers[1][1].conv.weight),

@@ -696,6 +696,39 @@ def conv3d_s1(x: "VolAct", w_wd: torch.Tensor, table, cout: int, slope: float = 
     return conv3d_wd(x, w_wd, cout, slope, stats)
 
 
+def conv3d_s2mf_weights(w_t: torch.Tensor):
+    """[16][27][32] 3x3x3 kernel (ops.conv3d layout) of the hourglass's stride-2 16 -> 32 conv ->
+    sa_conv3d_s2mf's B-fragment table; None for other shapes or a weight out of the split range."""
+    _check(w_t, "w_t")
+    cin, _, cout = w_t.shape
+    if (cin, cout) != (16, 32) or not bool((w_t.abs() < _MF_MAX_W).all()):
+        return None
+    table = torch.empty((int(N.lib().sa_conv3d_s2mf_weights_size()),), device=w_t.device, dtype=torch.uint8)
+    N.call("sa_conv3d_s2mf_weights", w_t.data_ptr(), table.data_ptr(), _stream(table))
+    return table
+
+
+def conv3d_s2(x: "VolAct", w_t: torch.Tensor, table, cout: int, slope: float = 0.01, stats: bool = True) -> "VolAct":
+    """The hourglass's stride-2 conv (down_layers[1][0]): 16 -> 32 on split-f16 MFMA
+    (sa_conv3d_s2mf; CONV3D_MFMA, a table from conv3d_s2mf_weights, an InstanceNorm + LeakyReLU
+    producer without gate), else ops.conv3d at stride 2."""
+    if (CONV3D_MFMA and table is not None and isinstance(x, VolAct) and x.gate is None and x.norm is not None
+            and x.act and x.raw.shape[1] == 16 and cout == 32):
+        _check(x.raw, "x")
+        B, Cin, D, H, W = x.raw.shape
+        if Cin * D * H * W < 2 ** 31 and D * H * W < 2 ** 30:
+            Do, Ho, Wo = (D - 1) // 2 + 1, (H - 1) // 2 + 1, (W - 1) // 2 + 1
+            out = torch.empty((B, cout, Do, Ho, Wo), device=x.raw.device, dtype=torch.float32)
+            parts = int(N.lib().sa_conv3d_s2mf_stat_parts(Do, Ho, Wo))
+            partial = torch.empty((B * cout * parts * 2,), device=out.device, dtype=torch.float64) if stats else None
+            mean, rstd = x.norm
+            N.call("sa_conv3d_s2mf", x.raw.data_ptr(), B, D, H, W, table.data_ptr(), mean.data_ptr(),
+                   rstd.data_ptr(), slope, out.data_ptr(), _ptr(partial), _stream(out))
+            norm = instnorm_finalize(partial, B * cout, parts, Do * Ho * Wo) if stats else None
+            return VolAct(out, norm, act=stats)
+    return conv3d(x, w_t, cout, stride=2, slope=slope, stats=stats)
+
+
 def _conv3d_onehot(x: OneHotVolume, w_t: torch.Tensor, cout: int, stride: int, stats: bool):
     _check(w_t, "w_t")
     B, nb, D, H, W = x.shape

@@ -144,3 +144,57 @@ def test_conv3d_mf_model_size_faster_than_wd(cin, shape):
     t_wd = _time(lambda: ops.conv3d_wd(v, wwd, cin))
     print(f"conv3d {cin}->{cin} {shape}: mfma {t_mf * 1e3:.0f} us, wd {t_wd * 1e3:.0f} us")
     assert t_mf < t_wd
+
+
+@pytest.mark.parametrize("shape", [(2, 20, 12, 72), (1, 13, 9, 31), (2, 9, 17, 66), (1, 3, 3, 5), (4, 120, 68, 120)])
+def test_conv3d_s2mf_matches_direct(shape):
+    """The stride-2 16 -> 32 conv (down_layers[1][0]) on split-f16 MFMA (sa_conv3d_s2mf) against the
+    direct fp32 fused conv at stride 2 (sa_conv3d) and torch's conv3d: odd D / H / W (ragged output
+    tiles: Ho not a multiple of 4, Wo not of 16 or 4: the scalar store path), the model's size
+    (cfg2's half-resolution volume), InstanceNorm statistics; and the model's dispatch
+    (ops.conv3d_s2) takes it."""
+    v, w = _case(16, 32, shape, sum(shape))
+    table = ops.conv3d_s2mf_weights(w)
+    assert table is not None
+    a = ops.conv3d_s2(v, w, table, 32)
+    b = ops.conv3d(v, w, 32, stride=2)
+    assert a.raw.shape == b.raw.shape
+    scale = float(b.raw.abs().max())
+    torch.testing.assert_close(a.raw, b.raw, atol=2e-6 * scale, rtol=1e-5)
+    torch.testing.assert_close(a.norm[0], b.norm[0], atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(a.norm[1], b.norm[1], atol=1e-5, rtol=1e-5)
+    if shape[0] * shape[1] * shape[2] * shape[3] < 10 ** 5:
+        ref = torch.nn.functional.conv3d(_torch_input(v).double(), w.double().permute(2, 0, 1).reshape(32, 16, 3, 3, 3),
+                                         stride=2, padding=1)
+        torch.testing.assert_close(a.raw.double(), ref, atol=2e-6 * scale, rtol=1e-5)
+
+
+def test_conv3d_s2mf_falls_back():
+    """Weights out of the split range, other channel counts or a gated input keep the fp32 kernel."""
+    v, w = _case(16, 32, (1, 9, 6, 20), 7)
+    assert ops.conv3d_s2mf_weights(w * 100) is None
+    assert ops.conv3d_s2mf_weights(torch.zeros(8, 27, 16, device=dev)) is None
+    b = ops.conv3d(v, w, 32, stride=2)
+    a = ops.conv3d_s2(v, w, None, 32)
+    assert torch.equal(a.raw, b.raw)
+
+
+def test_conv3d_s2mf_faster_than_direct():
+    """At cfg2's half-resolution volume the MFMA form beats the fp32 direct kernel."""
+    v, w = _case(16, 32, (4, 120, 68, 120), 3)
+    table = ops.conv3d_s2mf_weights(w)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / 5
+    t_mf = timed(lambda: ops.conv3d_s2(v, w, table, 32))
+    t_d = timed(lambda: ops.conv3d(v, w, 32, stride=2))
+    print(f"stride-2 16 -> 32 at 4x120x68x120: MFMA {t_mf * 1e3:.1f} us, direct {t_d * 1e3:.1f} us")
+    assert t_mf < t_d
