@@ -340,7 +340,8 @@ int sa_conv3d_mf(const float *in, int B, int Cin, int D, int H, int W, const voi
 void sa_conv3d_mf_set_planes(int planes);
 /* The hourglass's stride-2 16 -> 32 conv (down_layers[1][0], hourglass.py:27-33, submodule.py:25-53)
  * on the same split-f16 MFMA: in [B][16][D][H][W] with the producer's InstanceNorm (mean / rstd
- * [B*16]) + LeakyReLU(slope) applied on load, out [B][32][Do][Ho][Wo] (Do = (D-1)/2+1, ...) and
+ * [B*16]) + LeakyReLU(slope) and the optional feature-attention gate (sa_conv3d's gate_l / gate_r)
+ * applied on load, out [B][32][Do][Ho][Wo] (Do = (D-1)/2+1, ...) and
  * optional float64 InstanceNorm partials [B*32][sa_conv3d_s2mf_stat_parts][2];
  * sa_conv3d_s2mf_weights turns the [16][27][32] kernel into its sa_conv3d_s2mf_weights_size-byte
  * table (|w| < 8).  Needs D*H*W < 2^30. */
@@ -348,7 +349,8 @@ long sa_conv3d_s2mf_weights_size(void);
 int sa_conv3d_s2mf_weights(const float *weight, void *table, void *stream);
 long sa_conv3d_s2mf_stat_parts(int Do, int Ho, int Wo);
 int sa_conv3d_s2mf(const float *in, int B, int D, int H, int W, const void *table, const float *mean,
-                   const float *rstd, float slope, float *out, double *partial, void *stream);
+                   const float *rstd, float slope, const float *gate_l, const float *gate_r, float *out,
+                   double *partial, void *stream);
 /* The hourglass's two readers of the masked mono volume (down_layers[0][0], hourglass.py:27-33;
  * final_agg[0] over cat(orig, up(x)), hourglass.py:326-328) on the one-hot volume given by its
  * records (sa_mono_bin_records; rec_l [B,H,W] of the left pixels = the volume's W axis, rec_r

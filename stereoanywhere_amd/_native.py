@@ -137,7 +137,7 @@ SIGNATURES = {
     "sa_conv3d_s2mf_weights_size": (L, []),
     "sa_conv3d_s2mf_weights": (I, [P, P, P]),
     "sa_conv3d_s2mf_stat_parts": (L, [I, I, I]),
-    "sa_conv3d_s2mf": (I, [P, I, I, I, I, P, P, P, F, P, P, P]),
+    "sa_conv3d_s2mf": (I, [P, I, I, I, I, P, P, P, F, P, P, P, P, P]),
     "sa_conv3d_onehot_stat_parts": (L, [I, I, I]),
     "sa_conv3d_onehot": (I, [P, P, I, I, I, I, I, I, F, P, I, P, P, P]),
     "sa_conv3d_pointwise_upcat_onehot": (I, [P, P, I, F, P, I, I, I, I, I, I, I, P, I, P, P, P]),

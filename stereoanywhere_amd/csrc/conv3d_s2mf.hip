@@ -9,7 +9,8 @@
 // row and channel half.
 // Tile = one output plane x 4 rows x 16 columns x 32 channels; a block of 4 waves stages the tile's
 // input footprint (3 planes x 9 rows x 33 columns x 16 channels, the producer's InstanceNorm +
-// LeakyReLU applied and split into f16 hi / lo while staging) in LDS as 16-byte entries of 8
+// LeakyReLU and the feature-attention gate gl[b,c,h,w] * gr[b,c,h,d] applied and split into
+// f16 hi / lo while staging) in LDS as 16-byte entries of 8
 // channels, [channel group][hl][plane][row][column]; wave w computes channel half w & 1 of rows
 // 2 (w >> 1) and 2 (w >> 1) + 1 with its half's 28 B fragments resident in registers for the
 // whole kernel.  The grid is persistent (two blocks per CU loop over the tiles) so the weights are
@@ -56,6 +57,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_s2mf_kernel(const float *__rest
                                                              int Do, int Ho, int Wo, const f16x8 *__restrict__ tab,
                                                              const float *__restrict__ mean,
                                                              const float *__restrict__ rstd, float slope,
+                                                             const float *__restrict__ gl,
+                                                             const float *__restrict__ gr,
                                                              float *__restrict__ out, double *__restrict__ partial,
                                                              int tilesW, int tilesH, int ntiles) {
   __shared__ f16x8 lds[S2_ENT];
@@ -92,15 +95,22 @@ __global__ __launch_bounds__(256, 2) void conv3d_s2mf_kernel(const float *__rest
         const int id = id0 + p, ih = ih0 + r, iw = iw0 + c;
         const bool ok = id >= 0 && id < D && ih >= 0 && ih < H && iw >= 0 && iw < W;
         const float *src = in + ((long)b * S2_CIN + 8 * cg) * DHW + (ok ? (long)id * HW + (long)ih * W + iw : 0);
-        float x[8];
+        float x[8], gt[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] = ok ? src[(long)j * DHW] : 0.0f;
+        if (gl) {   // (block-uniform) the gate of (b, c, h, w) x (b, c, h, d), as InXform's pg
+          const long bc = (long)b * S2_CIN + 8 * cg;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            gt[j] = ok ? gl[((bc + j) * H + ih) * W + iw] * gr[((bc + j) * H + ih) * D + id] : 0.0f;
+        }
         f16x8 hi, lo;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float2 nr = nrm[8 * cg + j];
           float v = fmaf(x[j], nr.x, nr.y);
           v = fmaxf(v, v * slope);
+          if (gl) v = gt[j] * v;
           v = ok ? v : 0.0f;
           const _Float16 h = (_Float16)v;
           hi[j] = h;
@@ -193,12 +203,15 @@ extern "C" long sa_conv3d_s2mf_stat_parts(int Do, int Ho, int Wo) {
   return (long)Do * ((Ho + S2_TR - 1) / S2_TR) * ((Wo + S2_TC - 1) / S2_TC);
 }
 
-// out = conv3d(lrelu((x - mean) * rstd), W, stride 2, padding 1) for 16 -> 32 channels; x
-// [B][16][D][H][W], mean / rstd [B*16] (the producer's InstanceNorm), out [B][32][Do][Ho][Wo] with
+// out = conv3d([gl * gr *] lrelu((x - mean) * rstd), W, stride 2, padding 1) for 16 -> 32 channels;
+// x [B][16][D][H][W], mean / rstd [B*16] (the producer's InstanceNorm), optional gate maps
+// gate_l [B*16][H][W] and gate_r [B*16][H][D] (sa_conv3d's), out [B][32][Do][Ho][Wo] with
 // Do = (D - 1) / 2 + 1 etc.; partial: optional float64 (sum, sum of squares) per (b, co, tile)
 extern "C" int sa_conv3d_s2mf(const float *in, int B, int D, int H, int W, const void *table, const float *mean,
-                              const float *rstd, float slope, float *out, double *partial, void *stream) {
+                              const float *rstd, float slope, const float *gate_l, const float *gate_r, float *out,
+                              double *partial, void *stream) {
   SA_REQUIRE(in && table && mean && rstd && out, "sa_conv3d_s2mf: null pointer");
+  SA_REQUIRE((gate_l == nullptr) == (gate_r == nullptr), "sa_conv3d_s2mf: both gate maps or none");
   SA_REQUIRE(B > 0 && D > 0 && H > 0 && W > 0, "sa_conv3d_s2mf: empty shape");
   SA_REQUIRE((long)S2_CIN * D * H * W < (1L << 31) && (long)D * H * W < (1L << 30),
              "sa_conv3d_s2mf: volume too large (the split range needs D*H*W < 2^30)");
@@ -211,6 +224,6 @@ extern "C" int sa_conv3d_s2mf(const float *in, int B, int D, int H, int W, const
   sa::TimingScope ts(SA_K_CONV3D, s);
   const unsigned grid = (unsigned)std::min<long>(ntiles, 512);   // two persistent blocks per CU
   conv3d_s2mf_kernel<<<grid, 256, 0, s>>>(in, D, H, W, Do, Ho, Wo, static_cast<const f16x8 *>(table), mean, rstd,
-                                          slope, out, partial, tilesW, tilesH, (int)ntiles);
+                                          slope, gate_l, gate_r, out, partial, tilesW, tilesH, (int)ntiles);
   return sa::check_launch("sa_conv3d_s2mf");
 }

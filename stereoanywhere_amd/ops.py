@@ -711,8 +711,8 @@ def conv3d_s2mf_weights(w_t: torch.Tensor):
 def conv3d_s2(x: "VolAct", w_t: torch.Tensor, table, cout: int, slope: float = 0.01, stats: bool = True) -> "VolAct":
     """The hourglass's stride-2 conv (down_layers[1][0]): 16 -> 32 on split-f16 MFMA
     (sa_conv3d_s2mf; CONV3D_MFMA, a table from conv3d_s2mf_weights, an InstanceNorm + LeakyReLU
-    producer without gate), else ops.conv3d at stride 2."""
-    if (CONV3D_MFMA and table is not None and isinstance(x, VolAct) and x.gate is None and x.norm is not None
+    producer, optionally gated), else ops.conv3d at stride 2."""
+    if (CONV3D_MFMA and table is not None and isinstance(x, VolAct) and x.norm is not None
             and x.act and x.raw.shape[1] == 16 and cout == 32):
         _check(x.raw, "x")
         B, Cin, D, H, W = x.raw.shape
@@ -722,8 +722,9 @@ def conv3d_s2(x: "VolAct", w_t: torch.Tensor, table, cout: int, slope: float = 0
             parts = int(N.lib().sa_conv3d_s2mf_stat_parts(Do, Ho, Wo))
             partial = torch.empty((B * cout * parts * 2,), device=out.device, dtype=torch.float64) if stats else None
             mean, rstd = x.norm
+            gl, gr = x.gate if x.gate is not None else (None, None)
             N.call("sa_conv3d_s2mf", x.raw.data_ptr(), B, D, H, W, table.data_ptr(), mean.data_ptr(),
-                   rstd.data_ptr(), slope, out.data_ptr(), _ptr(partial), _stream(out))
+                   rstd.data_ptr(), slope, _ptr(gl), _ptr(gr), out.data_ptr(), _ptr(partial), _stream(out))
             norm = instnorm_finalize(partial, B * cout, parts, Do * Ho * Wo) if stats else None
             return VolAct(out, norm, act=stats)
     return conv3d(x, w_t, cout, stride=2, slope=slope, stats=stats)

@@ -146,14 +146,19 @@ def test_conv3d_mf_model_size_faster_than_wd(cin, shape):
     assert t_mf < t_wd
 
 
-@pytest.mark.parametrize("shape", [(2, 20, 12, 72), (1, 13, 9, 31), (2, 9, 17, 66), (1, 3, 3, 5), (4, 120, 68, 120)])
-def test_conv3d_s2mf_matches_direct(shape):
+@pytest.mark.parametrize("shape,gated", [((2, 20, 12, 72), False), ((1, 13, 9, 31), True), ((2, 9, 17, 66), True),
+                                         ((1, 3, 3, 5), False), ((4, 120, 68, 120), True)])
+def test_conv3d_s2mf_matches_direct(shape, gated):
     """The stride-2 16 -> 32 conv (down_layers[1][0]) on split-f16 MFMA (sa_conv3d_s2mf) against the
     direct fp32 fused conv at stride 2 (sa_conv3d) and torch's conv3d: odd D / H / W (ragged output
     tiles: Ho not a multiple of 4, Wo not of 16 or 4: the scalar store path), the model's size
-    (cfg2's half-resolution volume), InstanceNorm statistics; and the model's dispatch
-    (ops.conv3d_s2) takes it."""
+    (cfg2's half-resolution volume, gated by the feature attention as the model's input is),
+    InstanceNorm statistics; and the model's dispatch (ops.conv3d_s2) takes it."""
     v, w = _case(16, 32, shape, sum(shape))
+    if gated:   # the feature-attention gate gl[b, c, h, w] * gr[b, c, h, d] (sa_conv3d's)
+        B, D, H, W = shape
+        rng = np.random.default_rng(D * H)
+        v = v.with_gate((g(rng.random((B * 16, H, W))), g(rng.random((B * 16, H, D)))))
     table = ops.conv3d_s2mf_weights(w)
     assert table is not None
     a = ops.conv3d_s2(v, w, table, 32)
@@ -163,7 +168,7 @@ def test_conv3d_s2mf_matches_direct(shape):
     torch.testing.assert_close(a.raw, b.raw, atol=2e-6 * scale, rtol=1e-5)
     torch.testing.assert_close(a.norm[0], b.norm[0], atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(a.norm[1], b.norm[1], atol=1e-5, rtol=1e-5)
-    if shape[0] * shape[1] * shape[2] * shape[3] < 10 ** 5:
+    if shape[0] * shape[1] * shape[2] * shape[3] < 10 ** 5 and not gated:
         ref = torch.nn.functional.conv3d(_torch_input(v).double(), w.double().permute(2, 0, 1).reshape(32, 16, 3, 3, 3),
                                          stride=2, padding=1)
         torch.testing.assert_close(a.raw.double(), ref, atol=2e-6 * scale, rtol=1e-5)
