@@ -449,6 +449,9 @@ def main():
     ap.add_argument("--lookup-mfma", type=int, default=None, choices=[0, 1],
                     help="the fused lookups' convc1 on fp32 MFMA (1) or on the VALU (0); default: the library's "
                          "(sa_lookup_get_mfma)")
+    ap.add_argument("--lookup-form", type=int, default=None, choices=[0, 1, 2, 3],
+                    help="the sheared lookup's work split (sa_lookup_set_shear_dual): 0 one volume per "
+                         "thread, 1 both, 2 spread over a 4-wave block (default), 3 over 8 waves")
     ap.add_argument("--igemm-max-work", type=int, default=None,
                     help="implicit GEMM only for launches of at most this many output pixels x channels "
                          "(ops.IGEMM_MAX_WORK)")
@@ -505,6 +508,9 @@ def main():
     if args.lookup_mfma is not None:
         from stereoanywhere_amd import _native as _N
         _N.lib().sa_lookup_set_mfma(int(args.lookup_mfma))
+    if args.lookup_form is not None:
+        from stereoanywhere_amd import _native as _N
+        _N.lib().sa_lookup_set_shear_dual(int(args.lookup_form))
     if args.igemm_max_work is not None:
         ops.IGEMM_MAX_WORK = args.igemm_max_work
     if args.direct_split is not None:

@@ -235,8 +235,9 @@ int sa_corr_lookup_conv1x1(const float *pyramid_a, const float *pyramid_b, int W
  * slower): the same k-ordered fmaf chain either way.  For A/B runs and tests. */
 void sa_lookup_set_mfma(int on);
 int sa_lookup_get_mfma(void);
-/* the sheared lookup with both volumes in one thread (1, default: one tap grid, both volumes'
- * gathers in flight together) or one volume per grid row (0).  For A/B runs and tests. */
+/* the sheared lookup's work split: 3 (default) / 2 spread over an 8 / 4-wave block per 64 pixels
+ * (a thread per (pixel, volume, level) gathers the taps into LDS, then a thread per (pixel, channel
+ * group) runs convc1), 1 both volumes in one thread, 0 one volume per thread.  A/B and tests. */
 void sa_lookup_set_shear_dual(int on);
 int sa_lookup_get_shear_dual(void);
 long sa_shear_slice_size(int W1, int W2, int num_levels);

@@ -76,13 +76,13 @@ def main():
             from stereoanywhere_amd import _native as N
             t_form = {}
             try:
-                for form in (0, 1):
+                for form in (0, 1, 2):
                     N.lib().sa_lookup_set_shear_dual(form)
                     t_form[form] = timeit(lambda: ops.corr_lookup_conv1x1_sheared(sa, sb, W, 4, 4, cx, wt, bias,
                                                                                   out=out), reps)
                     same = same and torch.equal(out, o_row)
             finally:
-                N.lib().sa_lookup_set_shear_dual(2)
+                N.lib().sa_lookup_set_shear_dual(3)
             N.lib().sa_lookup_set_mfma(1)
             try:
                 t_shm = timeit(lambda: ops.corr_lookup_conv1x1_sheared(sa, sb, W, 4, 4, cx, wt, bias, out=out), reps)
@@ -92,7 +92,7 @@ def main():
             alg = B * H * W * (2 * 4 * 10 * 4 + 4 + 2 * 64 * 4)
             print(f"{name} lookup+convc1 (cell {cell}, amp {amp}): row {t_row:.1f} us ({alg / t_row / 1e6:.2f} TB/s "
                   f"of the bytes model), sheared {t_sh:.1f} us ({alg / t_sh / 1e6:.2f} TB/s; one volume per thread "
-                  f"{t_form[0]:.1f}, both {t_form[1]:.1f}); convc1 on MFMA: row "
+                  f"{t_form[0]:.1f}, both {t_form[1]:.1f}, over 4 waves {t_form[2]:.1f}); convc1 on MFMA: row "
                   f"{t_rowm:.1f}, sheared {t_shm:.1f} us; bit-exact {same}", flush=True)
         del f2, f3, pa, sa, ref
         torch.cuda.empty_cache()

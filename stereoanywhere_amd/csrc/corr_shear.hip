@@ -198,15 +198,16 @@ __global__ __launch_bounds__(256, (DUAL ? 2 : 1)) void lookup_c1_shear_kernel(co
 // 64 convc1 outputs of one pixel in every volume (the same k-ordered fmaf chains, weights uniform
 // per wave).  Four times the waves of lookup_c1_shear_kernel with a fraction of its registers:
 // the gathers and the output stores of many more waves overlap.
-template <int L, int R, int COUT>
-__global__ __launch_bounds__(256) void lookup_c1_shear_lds_kernel(const float *__restrict__ sa,
+template <int L, int R, int COUT, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void lookup_c1_shear_lds_kernel(const float *__restrict__ sa,
                                                                   const float *__restrict__ sb,
                                                                   const float *__restrict__ cx, ShLGeo g, int npix,
                                                                   const float *__restrict__ wt,
                                                                   const float *__restrict__ bias, int nvol,
                                                                   float *__restrict__ out) {
-  constexpr int K = 2 * R + 1, NT = L * K, WIN = 2 * R + 4, PX = 64, CG = COUT / 4;
-  static_assert(COUT % 4 == 0, "four channel groups");
+  constexpr int K = 2 * R + 1, NT = L * K, WIN = 2 * R + 4, PX = 64, CG = COUT / NW;
+  constexpr int TPT = (2 * L + NW - 1) / NW;   // (volume, level) tasks per thread
+  static_assert(COUT % NW == 0, "NW channel groups");
   __shared__ float ft[2][NT][PX];
   const int tid = threadIdx.x, px = tid & (PX - 1);
   const int grp = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar weight loads
@@ -217,11 +218,11 @@ __global__ __launch_bounds__(256) void lookup_c1_shear_lds_kernel(const float *_
   const int h = rem / g.W1, j = rem - h * g.W1;
   const float x = cx[(long)b * g.cbs + rem];
   const long soff = ((long)b * g.H + h) * g.slice + j;
-  // phase 1: tasks (volume, level) = grp, grp + 4 (wave-uniform; unrolled: both tasks' gathers
-  // in flight together)
+  // phase 1: tasks (volume, level) = grp, grp + NW (wave-uniform; unrolled: a thread's tasks'
+  // gathers in flight together)
 #pragma unroll
-  for (int tt = 0; tt < 2; ++tt) {
-    const int task = grp + 4 * tt;
+  for (int tt = 0; tt < TPT; ++tt) {
+    const int task = grp + NW * tt;
     if (task >= nvol * L) break;
     const int v = task / L, l = task % L;
     const int Wl = g.wid[l], El = g.rows[l];
@@ -284,9 +285,9 @@ __global__ __launch_bounds__(256) void lookup_c1_shear_lds_kernel(const float *_
 extern "C" int sa_lookup_get_mfma();
 
 namespace {
-int g_shear_dual = 2;   // sheared lookup form: 0 one volume per thread, 1 both, 2 spread over the block (A/B)
+int g_shear_dual = 3;   // sheared lookup form: 0 one volume per thread, 1 both, 2 / 3 spread over a 4 / 8-wave block
 }
-extern "C" void sa_lookup_set_shear_dual(int on) { g_shear_dual = on < 0 ? 0 : on > 2 ? 2 : on; }
+extern "C" void sa_lookup_set_shear_dual(int on) { g_shear_dual = on < 0 ? 0 : on > 3 ? 3 : on; }
 extern "C" int sa_lookup_get_shear_dual() { return g_shear_dual; }
 
 extern "C" long sa_shear_row_pitch(int W1) { return W1 > 0 ? sa::shear_pitch(W1) : -1; }
@@ -363,10 +364,13 @@ extern "C" int sa_corr_lookup_conv1x1_sheared(const float *sheared_a, const floa
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_LOOKUP, s);
   const float *sbb = sheared_b ? sheared_b : sheared_a;
-  if (g_shear_dual == 2 && !sa_lookup_get_mfma()) {
-    lookup_c1_shear_lds_kernel<4, 4, 64><<<(unsigned)((npix + 63) / 64), 256, 0, s>>>(sheared_a, sbb, coords_x, g,
-                                                                                     (int)npix, weight_kc, bias, nvol,
-                                                                                     out);
+  if (g_shear_dual >= 2 && !sa_lookup_get_mfma()) {
+    if (g_shear_dual == 3)
+      lookup_c1_shear_lds_kernel<4, 4, 64, 8><<<(unsigned)((npix + 63) / 64), 512, 0, s>>>(
+          sheared_a, sbb, coords_x, g, (int)npix, weight_kc, bias, nvol, out);
+    else
+      lookup_c1_shear_lds_kernel<4, 4, 64><<<(unsigned)((npix + 63) / 64), 256, 0, s>>>(
+          sheared_a, sbb, coords_x, g, (int)npix, weight_kc, bias, nvol, out);
     return sa::check_launch("sa_corr_lookup_conv1x1_sheared");
   }
   const bool dual = nvol == 2 && g_shear_dual;

@@ -227,14 +227,15 @@ def test_lookup_sheared_bit_exact(W1, W2):
                        c(ops.corr_lookup_conv1x1_sheared(sa, sb, W2, 4, 4, g(cx), g(wt), g(bias))))
         finally:
             N.lib().sa_lookup_set_mfma(0)   # (the default: convc1 on the VALU)
-    forms = {}   # 0: one volume per thread, 1: both in one thread, 2 (default): spread over the block
+    forms = {}   # 0: one volume per thread, 1: both in one thread, 2 / 3 (default): spread over 4 / 8 waves
+    default = N.lib().sa_lookup_get_shear_dual()
     try:
-        for form in (0, 1, 2):
+        for form in (0, 1, 2, 3):
             N.lib().sa_lookup_set_shear_dual(form)
             forms[form] = (c(ops.corr_lookup_conv1x1_sheared(sa, sb, W2, 4, 4, g(cx), g(wt), g(bias))),
                            c(ops.corr_lookup_conv1x1_sheared(sa, None, W2, 4, 4, g(cx), g(wt), g(bias))))
     finally:
-        N.lib().sa_lookup_set_shear_dual(2)
+        N.lib().sa_lookup_set_shear_dual(default)
     row, sh = res[1]
     np.testing.assert_array_equal(sh, row)
     np.testing.assert_array_equal(res[0][0], row)
