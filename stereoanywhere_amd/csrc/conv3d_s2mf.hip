@@ -13,8 +13,9 @@
 // f16 hi / lo while staging) in LDS as 16-byte entries of 8
 // channels, [channel group][hl][plane][row][column]; wave w computes channel half w & 1 of rows
 // 2 (w >> 1) and 2 (w >> 1) + 1 with its half's 28 B fragments resident in registers for the
-// whole kernel.  The grid is persistent (two blocks per CU loop over the tiles) so the weights are
-// loaded once per block.  InstanceNorm partials (float64) per (image, channel, tile).
+// whole kernel.  The grid is persistent (two blocks per CU, each a contiguous run of tiles with the
+// output plane fastest) so the weights are loaded once per block and the gate's (h, w) factors once
+// per run of planes.  InstanceNorm partials (float64) per (image, channel, tile).
 // Layout [B, C, D, H, W] (D = W2, W = W1), as conv3d_fused.hip.
 #include "sa_common.h"
 
@@ -63,6 +64,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_s2mf_kernel(const float *__rest
                                                              int tilesW, int tilesH, int ntiles) {
   __shared__ f16x8 lds[S2_ENT];
   __shared__ float2 nrm[S2_CIN];
+  // the tile's gate factors, staged once per tile: gl [ch][row][column], gr [ch][row][plane]
+  __shared__ float gls[S2_CIN * S2_PPL], grs[S2_CIN * S2_PR * 3];
   __shared__ double red[2][2][16][2];   // [half][wave pair][channel][sum, sum of squares]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -75,18 +78,39 @@ __global__ __launch_bounds__(256, 2) void conv3d_s2mf_kernel(const float *__rest
   const long HW = (long)H * W, DHW = (long)D * HW;
   const int per_image = Do * tilesH * tilesW;
   const int m = lane & 15, g = lane >> 4, cgl = g & 1, tsel = g >> 1;
-  // consecutive tiles (neighbouring halos) on one XCD: the start tile from the XCD-grouped block id
-  for (int tile = (int)sa::xcd_remap(blockIdx.x, gridDim.x); tile < ntiles; tile += gridDim.x) {
-    const int tx = tile % tilesW, ty = (tile / tilesW) % tilesH, od = (tile / (tilesW * tilesH)) % Do;
+  // a block takes a contiguous run of tiles, output planes fastest: the gate factors (which do not
+  // depend on the plane) are staged once per run of one (image, row tile, column tile); runs of
+  // neighbouring blocks on one XCD (the XCD-grouped block id)
+  const int chunk = (ntiles + gridDim.x - 1) / gridDim.x;
+  const int t0 = (int)sa::xcd_remap(blockIdx.x, gridDim.x) * chunk, t1 = min(t0 + chunk, ntiles);
+  int gkey = -1;
+  for (int tile = t0; tile < t1; ++tile) {
+    const int od = tile % Do, rest = tile / Do;
+    const int tx = rest % tilesW, ty = (rest / tilesW) % tilesH;
     const int b = tile / per_image;
+    const int id0 = 2 * od - 1, ih0 = 2 * ty * S2_TR - 1, iw0 = 2 * tx * S2_TC - 1;
     __syncthreads();   // the previous tile's LDS reads and reductions are done
     if (tid < S2_CIN) {
       const float rs = rstd[b * S2_CIN + tid];
       nrm[tid] = make_float2(rs, -mean[b * S2_CIN + tid] * rs);
     }
+    if (gl && rest != gkey) {   // (block-uniform) gl: once per run of planes
+      gkey = rest;
+      for (int i = tid; i < S2_CIN * S2_PPL; i += 256) {
+        const int ch = i / S2_PPL, rc = i % S2_PPL, ih = ih0 + rc / S2_PC, iw = iw0 + rc % S2_PC;
+        const bool ok = ih >= 0 && ih < H && iw >= 0 && iw < W;
+        gls[i] = ok ? gl[(((long)b * S2_CIN + ch) * H + ih) * W + iw] : 0.0f;
+      }
+    }
+    if (gl) {   // gr: the tile's 3 input planes
+      for (int i = tid; i < S2_CIN * S2_PR * 3; i += 256) {
+        const int ch = i / (S2_PR * 3), rp = i % (S2_PR * 3), ih = ih0 + rp / 3, id = id0 + rp % 3;
+        const bool ok = ih >= 0 && ih < H && id >= 0 && id < D;
+        grs[i] = ok ? gr[(((long)b * S2_CIN + ch) * H + ih) * D + id] : 0.0f;
+      }
+    }
     __syncthreads();
-    // staging: T(x) = lrelu(x * rstd - mean * rstd), zero outside the volume (the padding)
-    const int id0 = 2 * od - 1, ih0 = 2 * ty * S2_TR - 1, iw0 = 2 * tx * S2_TC - 1;
+    // staging: T(x) = [gl gr] lrelu(x * rstd - mean * rstd), zero outside the volume (the padding)
 #pragma unroll
     for (int q = 0; q < S2_JPT; ++q) {
       const int job = tid + 256 * q;
@@ -99,10 +123,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_s2mf_kernel(const float *__rest
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] = ok ? src[(long)j * DHW] : 0.0f;
         if (gl) {   // (block-uniform) the gate of (b, c, h, w) x (b, c, h, d), as InXform's pg
-          const long bc = (long)b * S2_CIN + 8 * cg;
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            gt[j] = ok ? gl[((bc + j) * H + ih) * W + iw] * gr[((bc + j) * H + ih) * D + id] : 0.0f;
+            gt[j] = gls[(8 * cg + j) * S2_PPL + r * S2_PC + c] * grs[((8 * cg + j) * S2_PR + r) * 3 + p];
         }
         f16x8 hi, lo;
 #pragma unroll
