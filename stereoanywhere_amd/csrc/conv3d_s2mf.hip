@@ -83,9 +83,13 @@ __global__ __launch_bounds__(256, 2) void conv3d_s2mf_kernel(const float *__rest
   // neighbouring blocks on one XCD (the XCD-grouped block id)
   const int chunk = (ntiles + gridDim.x - 1) / gridDim.x;
   const int t0 = (int)sa::xcd_remap(blockIdx.x, gridDim.x) * chunk, t1 = min(t0 + chunk, ntiles);
-  int gkey = -1;
+  int gkey = -1, prev = -2;
   for (int tile = t0; tile < t1; ++tile) {
     const int od = tile % Do, rest = tile / Do;
+    // input plane id lives in LDS plane slot (id + 3) % 3: the next output plane of a run reuses
+    // the last input plane of this one and stages only its two new planes
+    const bool reuse = tile == prev + 1 && od > 0;
+    prev = tile;
     const int tx = rest % tilesW, ty = (rest / tilesW) % tilesH;
     const int b = tile / per_image;
     const int id0 = 2 * od - 1, ih0 = 2 * ty * S2_TR - 1, iw0 = 2 * tx * S2_TC - 1;
@@ -111,11 +115,12 @@ __global__ __launch_bounds__(256, 2) void conv3d_s2mf_kernel(const float *__rest
     }
     __syncthreads();
     // staging: T(x) = [gl gr] lrelu(x * rstd - mean * rstd), zero outside the volume (the padding)
+    const int np = reuse ? 2 : 3, p0 = 3 - np, njobs = 2 * np * S2_PPL;
 #pragma unroll
     for (int q = 0; q < S2_JPT; ++q) {
       const int job = tid + 256 * q;
-      if (job < S2_JOBS) {
-        const int c = job % S2_PC, r = (job / S2_PC) % S2_PR, p = (job / S2_PPL) % 3, cg = job / (3 * S2_PPL);
+      if (job < njobs) {
+        const int c = job % S2_PC, r = (job / S2_PC) % S2_PR, p = p0 + (job / S2_PPL) % np, cg = job / (np * S2_PPL);
         const int id = id0 + p, ih = ih0 + r, iw = iw0 + c;
         const bool ok = id >= 0 && id < D && ih >= 0 && ih < H && iw >= 0 && iw < W;
         const float *src = in + ((long)b * S2_CIN + 8 * cg) * DHW + (ok ? (long)id * HW + (long)ih * W + iw : 0);
@@ -139,19 +144,23 @@ __global__ __launch_bounds__(256, 2) void conv3d_s2mf_kernel(const float *__rest
           hi[j] = h;
           lo[j] = (_Float16)(v - (float)h);
         }
-        lds[((cg * 2 + 0) * 3 + p) * S2_PPL + r * S2_PC + c] = hi;
-        lds[((cg * 2 + 1) * 3 + p) * S2_PPL + r * S2_PC + c] = lo;
+        const int sl = (id + 3) % 3;
+        lds[((cg * 2 + 0) * 3 + sl) * S2_PPL + r * S2_PC + c] = hi;
+        lds[((cg * 2 + 1) * 3 + sl) * S2_PPL + r * S2_PC + c] = lo;
       }
     }
     __syncthreads();
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const int slot0 = (id0 + 3) % 3;   // LDS plane slot of the kd = 0 input plane (uniform)
 #pragma unroll
     for (int s = 0; s < S2_KS; ++s) {
       const int tap = min(2 * s + tsel, 26);   // (tap 27: zero weights, any finite A)
-      const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+      const int kh = (tap / 3) % 3, kw = tap % 3;
+      const int sk = slot0 + (tsel ? min(2 * s + 1, 26) / 9 : (2 * s) / 9);
+      const int pk = (sk >= 3 ? sk - 3 : sk) * S2_PPL;   // the tap's input plane slot
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        const int base = (cgl * 2 * 3 + kd) * S2_PPL + (2 * (2 * rh + mt) + kh) * S2_PC + 2 * m + kw;
+        const int base = cgl * 2 * 3 * S2_PPL + pk + (2 * (2 * rh + mt) + kh) * S2_PC + 2 * m + kw;
         const f16x8 ahi = lds[base], alo = lds[base + 3 * S2_PPL];
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bw[s][0], acc[mt], 0, 0, 0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bw[s][1], acc[mt], 0, 0, 0);
