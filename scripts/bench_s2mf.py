@@ -26,8 +26,10 @@ def timed(fn, reps=5):
 def main():
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
-    for B, D, H, W in ((4, 120, 68, 120), (25, 120, 68, 120), (1, 140, 112, 140), (4, 140, 112, 140),
-                       (25, 140, 112, 140)):
+    shapes = ((4, 120, 68, 120), (25, 120, 68, 120), (1, 140, 112, 140), (4, 140, 112, 140), (25, 140, 112, 140))
+    if len(sys.argv) > 1:   # one shape by index (PMC runs)
+        shapes = (shapes[int(sys.argv[1])],)
+    for B, D, H, W in shapes:
         x = torch.randn(B, 16, D, H, W, device=dev, generator=g)
         mean = torch.randn(B * 16, device=dev, generator=g) * 0.1
         rstd = torch.rand(B * 16, device=dev, generator=g) + 0.5
