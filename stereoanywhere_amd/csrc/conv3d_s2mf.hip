@@ -145,8 +145,11 @@ __global__ __launch_bounds__(256, 2) void conv3d_s2mf_kernel(const float *__rest
           lo[j] = (_Float16)(v - (float)h);
         }
         const int sl = (id + 3) % 3;
-        lds[((cg * 2 + 0) * 3 + sl) * S2_PPL + r * S2_PC + c] = hi;
-        lds[((cg * 2 + 1) * 3 + sl) * S2_PPL + r * S2_PC + c] = lo;
+        // columns stored even ones first, then odd ones: the stride-2 reads of a K-step hit
+        // consecutive entries (2 m + kw -> m + kw / 2, or 17 + m for kw = 1)
+        const int cs = (c & 1) ? 17 + (c >> 1) : (c >> 1);
+        lds[((cg * 2 + 0) * 3 + sl) * S2_PPL + r * S2_PC + cs] = hi;
+        lds[((cg * 2 + 1) * 3 + sl) * S2_PPL + r * S2_PC + cs] = lo;
       }
     }
     __syncthreads();
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_s2mf_kernel(const float *__rest
       const int pk = (sk >= 3 ? sk - 3 : sk) * S2_PPL;   // the tap's input plane slot
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        const int base = cgl * 2 * 3 * S2_PPL + pk + (2 * (2 * rh + mt) + kh) * S2_PC + 2 * m + kw;
+        const int base = cgl * 2 * 3 * S2_PPL + pk + (2 * (2 * rh + mt) + kh) * S2_PC + m + (kw == 1 ? 17 : kw >> 1);
         const f16x8 ahi = lds[base], alo = lds[base + 3 * S2_PPL];
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bw[s][0], acc[mt], 0, 0, 0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bw[s][1], acc[mt], 0, 0, 0);
