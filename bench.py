@@ -299,25 +299,39 @@ def _time_oracle(sd, H, W, iters, D, runs):
     return sorted(times)
 
 
-def cpu_baseline(iters: int, H: int, W: int, runs: int = 3):
+def cpu_baseline(iters: int, H: int, W: int, runs: int = 3, cfg1: bool = True):
     """The oracle restatement (parity-pinned to the reference) on the box's host threads:
     one warm-up, then the median of ``runs`` single-pair forwards, at the bench shape and
-    at cfg1 (256x512, 8 iterations)."""
+    (cfg1) at configs[0] (256x512, 8 iterations)."""
     from oracle import model_ref as M
 
     share = host_cpu_share()
     torch.set_num_threads(share["threads"])
     sd = M.load_state_dict_seeded(0)
     ts = _time_oracle(sd, H, W, iters, 192.0, runs)
-    t1 = _time_oracle(sd, 256, 512, 8, 64.0, runs)
-    med, med1 = ts[len(ts) // 2], t1[len(t1) // 2]
-    return {"value": 1.0 / med, "unit": "pairs/s", "cores": torch.get_num_threads(), "kind": "port",
-            "cpu_model": cpu_model(), "cpu_share": share,
-            "sample": f"1 pair 1x{H}x{W}, {iters} iters, oracle (torch CPU convs + numpy hot path); "
-                      f"1 warm-up + median of {runs}: {', '.join(f'{x:.2f}' for x in ts)} s",
-            "cfg1": {"value": 1.0 / med1, "unit": "pairs/s",
-                     "sample": f"1 pair 1x256x512, 8 iters; 1 warm-up + median of {runs}: "
-                               f"{', '.join(f'{x:.2f}' for x in t1)} s"}}
+    med = ts[len(ts) // 2]
+    res = {"value": 1.0 / med, "unit": "pairs/s", "cores": torch.get_num_threads(), "kind": "port",
+           "cpu_model": cpu_model(), "cpu_share": share,
+           "sample": f"1 pair 1x{H}x{W}, {iters} iters, oracle (torch CPU convs + numpy hot path); "
+                     f"1 warm-up + median of {runs}: {', '.join(f'{x:.2f}' for x in ts)} s"}
+    if cfg1:
+        t1 = _time_oracle(sd, 256, 512, 8, 64.0, runs)
+        res["cfg1"] = {"value": 1.0 / t1[len(t1) // 2], "unit": "pairs/s",
+                       "sample": f"1 pair 1x256x512, 8 iters; 1 warm-up + median of {runs}: "
+                                 f"{', '.join(f'{x:.2f}' for x in t1)} s"}
+    return res
+
+
+def rank_report(per_rank_s, steps: int, gather_ms: float, gather_bytes: int, backend: str) -> dict:
+    """N > 1: what makes the line explain itself (the only data-path collective is the
+    metric all_gather after the timed region): each rank's timed-region length per step (the value
+    divides by the slowest), which rank that was, and the all_gather's own latency and size.
+    per_rank_s: each rank's own K steps, from the opening barrier to its own device sync (before the
+    closing barrier, which equalises the bracketed times)."""
+    ms = [t / steps * 1e3 for t in per_rank_s]
+    slow = max(range(len(ms)), key=lambda i: ms[i])
+    return {"per_rank_ms_per_step": ms, "slowest_rank": slow, "spread": max(ms) / min(ms),
+            "gather_ms": gather_ms, "gather_bytes": gather_bytes, "backend": backend}
 
 
 def cpu_baseline_tile(cfg, iters: int, runs: int = 3):
@@ -397,10 +411,12 @@ def _free_port() -> int:
 
 def self_launch(gpus: int):
     """``--gpus N`` (N > 1) outside torchrun: start N child ranks of this same command, one per GPU
-    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), wait for all of them and return
-    the first non-zero exit status (0 when every rank succeeded).  None: nothing to launch (N = 1, or
-    already a rank of a torchrun / self-launched world).  The parent touches no GPU: the children are
-    fresh interpreters started before any HIP call (no exec from a GPU process)."""
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), poll them and return the first
+    non-zero exit status (0 when every rank succeeded).  As torchrun does, the first rank that fails
+    ends the others (SIGTERM, then SIGKILL after a grace period): the survivors would otherwise block
+    for ever in a collective with the dead rank.  None: nothing to launch (N = 1, or already a rank of
+    a torchrun / self-launched world).  The parent touches no GPU: the children are fresh
+    interpreters started before any HIP call (no exec from a GPU process)."""
     if gpus <= 1 or "WORLD_SIZE" in os.environ:
         return None
     import subprocess
@@ -410,11 +426,30 @@ def self_launch(gpus: int):
         env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(gpus),
                    LOCAL_WORLD_SIZE=str(gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [c for c in rcs if c != 0]
-    if bad:
+    import time
+    first_bad = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [c for c in rcs if c not in (None, 0)]
+        if bad and first_bad is None:
+            first_bad = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            deadline = time.monotonic() + 15.0
+            while any(p.poll() is None for p in procs) and time.monotonic() < deadline:
+                time.sleep(0.1)
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            rcs = [p.wait() for p in procs]
+        if all(c is not None for c in rcs):
+            break
+        time.sleep(0.1)
+    if first_bad is not None or any(c != 0 for c in rcs):
         print(f"bench: rank exit codes {rcs}", file=sys.stderr)
-    return bad[0] if bad else 0
+        return first_bad if first_bad is not None else next(c for c in rcs if c != 0)
+    return 0
 
 
 def main():
@@ -440,9 +475,6 @@ def main():
     ap.add_argument("--pipeline", type=int, default=1,
                     help="graph instances in flight (PipelinedForward): consecutive batches overlap; 1: one "
                          "forward at a time")
-    ap.add_argument("--igemm", type=int, default=None, choices=[0, 1],
-                    help="3x3 convs on the implicit-GEMM kernel where it applies (1) or on the Winograd kernels "
-                         "only (0); default: ops.IGEMM")
     ap.add_argument("--conv3d-mfma", type=int, default=None, choices=[0, 1],
                     help="the hourglass's stride-1 8->8 / 16->16 convs on split-f16 MFMA (1) or on the F(4,3) "
                          "VALU kernel (0); default: ops.CONV3D_MFMA")
@@ -451,10 +483,7 @@ def main():
                          "(sa_lookup_get_mfma)")
     ap.add_argument("--lookup-form", type=int, default=None, choices=[0, 1, 2, 3],
                     help="the sheared lookup's work split (sa_lookup_set_shear_dual): 0 one volume per "
-                         "thread, 1 both, 2 spread over a 4-wave block (default), 3 over 8 waves")
-    ap.add_argument("--igemm-max-work", type=int, default=None,
-                    help="implicit GEMM only for launches of at most this many output pixels x channels "
-                         "(ops.IGEMM_MAX_WORK)")
+                         "thread, 1 both, 2 spread over a 4-wave block, 3 over 8 waves (the library's default)")
     ap.add_argument("--w4-split", type=int, default=None, choices=[0, 1],
                     help="F(4x4) convs on the split kernel (1) or fp32 MFMA (0); default: ops.W4_SPLIT")
     ap.add_argument("--direct-split", type=int, default=None, choices=[0, 1],
@@ -487,11 +516,29 @@ def main():
         if os.environ.get("SA_DIST_BACKEND", "nccl") == "nccl":
             torch.cuda.set_device(r.local_rank)
         dev = torch.device("cuda", r.local_rank) if os.environ.get("SA_DIST_BACKEND", "nccl") == "nccl" else None
+        if os.environ.get("SA_DRYRUN_FAIL_RANK") == str(r.rank):   # (tests: a rank that dies after joining)
+            raise SystemExit(3)
+        # the timed-region bookkeeping of a real run on stand-in steps (rank r sleeps 5 (r + 1) ms per step)
+        D.barrier(r)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            time.sleep(5e-3 * (r.rank + 1))
+        own = time.perf_counter() - t0
+        D.barrier(r)
+        per_rank = D.gather_scalars(own, r, dev)
+        tg = time.perf_counter()
         got = D.gather_metrics(torch.tensor([[float(r.rank), float(r.world)]], dtype=torch.float64, device=dev), r)
+        gather_ms = (time.perf_counter() - tg) * 1e3
         D.barrier(r)
         if r.is_main:
-            print(json.dumps({"dry_run": True, "n_gpus": r.world, "ranks": [int(v) for v in got[:, 0].tolist()],
-                              "worlds": sorted({int(v) for v in got[:, 1].tolist()})}))
+            line = {"dry_run": True, "n_gpus": r.world, "ranks": [int(v) for v in got[:, 0].tolist()],
+                    "worlds": sorted({int(v) for v in got[:, 1].tolist()})}
+            if r.world > 1:
+                line["rank_timing"] = rank_report(per_rank, args.steps, gather_ms, got.numel() * 8,
+                                                  os.environ.get("SA_DIST_BACKEND", "nccl"))
+            if not args.no_cpu_baseline:   # (a tiny oracle sample: the key's plumbing, not a baseline)
+                line["cpu_baseline"] = cpu_baseline(1, 64, 128, runs=1, cfg1=False)
+            print(json.dumps(line))
         return
     if args.split_guard is not None:
         ops.SPLIT_GUARD = bool(args.split_guard)
@@ -501,8 +548,6 @@ def main():
         ops._WINO4_MIN_BLOCKS = args.wino4_min_blocks
     if args.w4_split is not None:
         ops.W4_SPLIT = bool(args.w4_split)
-    if args.igemm is not None:
-        ops.IGEMM = bool(args.igemm)
     if args.conv3d_mfma is not None:
         ops.CONV3D_MFMA = bool(args.conv3d_mfma)
     if args.lookup_mfma is not None:
@@ -511,8 +556,6 @@ def main():
     if args.lookup_form is not None:
         from stereoanywhere_amd import _native as _N
         _N.lib().sa_lookup_set_shear_dual(int(args.lookup_form))
-    if args.igemm_max_work is not None:
-        ops.IGEMM_MAX_WORK = args.igemm_max_work
     if args.direct_split is not None:
         ops.DIRECT_SPLIT = bool(args.direct_split)
 
@@ -622,6 +665,7 @@ def main():
             for _ in range(args.steps):
                 out = step()
             torch.cuda.synchronize()
+            own = time.perf_counter() - t0   # this rank's own steps (before waiting for the others)
             D.barrier(r)
             elapsed = time.perf_counter() - t0
         redo_blocks = int(N.lib().sa_split_redo_blocks(1))
@@ -686,12 +730,17 @@ def main():
         N.timing_enable(False)
         model.stream_overlap = not args.one_stream
         log(f"instrumented {args.steps} steps in {elapsed_ev:.3f} s")
+        per_rank = D.gather_scalars(own, r, device)
         elapsed = D.max_over_ranks(elapsed, r, device)
-        # per-unit metrics gathered once, after the timed region (the only collective)
+        # per-unit metrics gathered once, after the timed region (the only data-path collective)
         disp = out[0] if isinstance(out, tuple) else out
         disp = -disp[:, 0] if tiled is None else disp[:, 0]
         local = torch.stack([disp.mean((1, 2)), disp.amin((1, 2)), disp.amax((1, 2))], 1).double()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
         allm = D.gather_metrics(local, r)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3
 
     total_units = units * r.world * args.steps
     if not r.is_main:
@@ -700,7 +749,6 @@ def main():
     costs = step_costs(shape[0], shape[1], shape[2], iters)
     costs["conv2d_wino"] = ("TFLOP/s", work.get("conv2d_wino", 0.0))
     costs["conv2d_wino4"] = ("TFLOP/s", work.get("conv2d_wino4", 0.0))
-    costs["conv2d_igemm"] = ("TFLOP/s", work.get("conv2d_igemm", 0.0))
     costs["conv2d_direct"] = ("TFLOP/s", work.get("conv2d_direct", 0.0))
     costs["norm_act"] = ("GB/s", work.get("norm_act", 0.0))
     # the separate GRU gate kernels run only at levels whose width keeps the gates out of the
@@ -722,10 +770,6 @@ def main():
         if unit == "TFLOP/s":
             ach, peak, bound = amount / secs / 1e12, FP32_MFMA_PEAK_TFS, "mfma"
             split4 = (k == "conv2d_wino4" and ops.W4_SPLIT) or (k == "conv2d_direct" and ops.DIRECT_SPLIT)
-            if k == "conv2d_igemm":
-                # the implicit-GEMM conv issues three f16 MFMA products per fp32 product (hi*hi +
-                # hi*lo + lo*hi): its rate is the issued f16 flops against the guide's F16 dense peak
-                ach, peak = 3 * ach, F16_DENSE_PEAK_TFS
         else:
             ach, peak, bound = amount / secs / 1e9, HBM_PEAK_GBS, "hbm"
             split4 = False
@@ -738,8 +782,6 @@ def main():
             # f16 products per fp32 one) against the F16 dense peak (~2.5 PF)
             kernels[k].update(split_peak=SPLIT_MFMA_PEAK_TFS, frac_split_peak=ach / SPLIT_MFMA_PEAK_TFS,
                               f16_issued_tflops=4 * ach, frac_f16_dense_peak=4 * ach / F16_DENSE_PEAK_TFS)
-        if k == "conv2d_igemm":
-            kernels[k].update(fp32_product_tflops=ach / 3, direct_conv_tflops=ach / 3)
     dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
     roof = dict(kernels[dom])
     roof.update({"kernel": dom, "traffic": pmc_traffic(dom, args.batch) if tiled is None else None,
@@ -766,9 +808,7 @@ def main():
                             "products) against the guide's fp32 matrix peak 157.3 TF/s; split_peak "
                             "(2x, the 16x16x16 f16 form) and the issued f16 flops vs the F16 dense peak "
                             "are side fields" if ops.W4_SPLIT or ops.DIRECT_SPLIT else "")
-                         + "; conv2d_igemm (the implicit-GEMM 3x3 conv on 16x16x32 f16 MFMA) issues 3 "
-                           "f16 products per fp32 product: achieved = those issued flops vs the guide's "
-                           "F16 dense peak 2.5 PF (direct_conv_tflops = the fp32 products' rate)"})
+})
     if tiled is None:
         metric, unit = "stereo pairs/sec @540x960 D=192 (1/2/4/8 GPU) + EPE vs reference", "pairs/s"
         if args.config == "cfg4":
@@ -797,7 +837,6 @@ def main():
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": ("f32 (" + " and ".join(n for n, on in (("F(4x4) Winograd-domain", ops.W4_SPLIT),
-                                                         ("implicit-GEMM 3x3", ops.IGEMM),
                                                          ("direct-conv", ops.DIRECT_SPLIT)) if on)
                   + " products as exact f16 hi/lo pair products on MFMA, fp32 accumulation; everything else "
                   "fp32)" if ops.W4_SPLIT or ops.DIRECT_SPLIT else "f32"), "data": "synthetic (seeded value-noise pairs, "
@@ -826,7 +865,10 @@ def main():
         res["epe_vs_reference"] = (epe_vs_reference(model, device) if tiled is None
                                    else epe_vs_reference_tiled(model, device, args.config))
         log(f"EPE vs reference {res['epe_vs_reference']:.3g}")
-    if r.world == 1 and not args.no_cpu_baseline:
+    if r.world > 1:
+        res["rank_timing"] = rank_report(per_rank, args.steps, gather_ms, allm.numel() * 8,
+                                         os.environ.get("SA_DIST_BACKEND", "nccl"))
+    if not args.no_cpu_baseline:   # (rank 0, after every collective: the other ranks are not held)
         log("cpu baseline (oracle, bounded sample) ...")
         res["cpu_baseline"] = cpu_baseline(iters, Hp, Wp) if tiled is None else cpu_baseline_tile(tiled, iters)
     print(json.dumps(res))

@@ -24,6 +24,20 @@
 extern "C" {
 #endif
 
+/* ABI version of this header.  Bumped whenever an entry point's signature or a struct passed by
+ * pointer or in an array changes (INTEGRATION.md lists the breaks).  A host checks at load time
+ * that sa_abi_version() == SA_ABI_VERSION and that sa_struct_size(SA_STRUCT_*) equals its own
+ * sizeof: the arrays of SaWinoProblem / SaGateEpilogue / SaResampleJob are read at the library's
+ * stride, so a host built against another layout would hand over misread fields.
+ *   6: round 6 (the implicit-GEMM entry points removed; sa_struct_size, sa_conv3d_mf_get_planes)
+ *   5: SaWinoProblem gained the residual-epilogue fields (skip ... out_act); sa_conv2d_k3_wino4_launch
+ *      took a guard flag; sa_conv2d_wino4_weights_cb removed */
+#define SA_ABI_VERSION 6
+enum { SA_STRUCT_WINO_PROBLEM = 0, SA_STRUCT_GATE_EPILOGUE = 1, SA_STRUCT_RESAMPLE_JOB = 2 };
+int sa_abi_version(void);
+/* sizeof the struct `which` (SA_STRUCT_*) as the library was built, -1 for an unknown id */
+long sa_struct_size(int which);
+
 enum {
   SA_OK = 0,
   SA_E_ARG = -1,        /* bad shape / null pointer / unsupported size           */
@@ -31,7 +45,6 @@ enum {
   SA_E_RUNTIME = -3     /* other HIP runtime failure (events, memset)            */
 };
 
-int sa_abi_version(void);
 const char *sa_last_error(void);
 
 /* ----------------------------------------------------------------------------------
@@ -339,6 +352,7 @@ int sa_conv3d_mf(const float *in, int B, int Cin, int D, int H, int W, const voi
                  const float *in_mean, const float *in_rstd, float slope, float *out,
                  double *stats_partial, void *stream);
 void sa_conv3d_mf_set_planes(int planes);
+int sa_conv3d_mf_get_planes(void);
 /* The hourglass's stride-2 16 -> 32 conv (down_layers[1][0], hourglass.py:27-33, submodule.py:25-53)
  * on the same split-f16 MFMA: in [B][16][D][H][W] with the producer's InstanceNorm (mean / rstd
  * [B*16]) + LeakyReLU(slope) and the optional feature-attention gate (sa_conv3d's gate_l / gate_r)
@@ -502,26 +516,7 @@ int sa_conv2d_k3_wino4_multi_gate(int nprob, const SaWinoProblem *probs, const S
  * sa_split_redo_blocks counts them.  Other block shapes ignore guard. */
 int sa_conv2d_k3_wino4_launch(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates,
                               int block_shape, int guard, void *stream);
-/* The same 3x3 / pad 1 convolutions as an implicit GEMM on v_mfma_f32_16x16x32_f16 with split
- * operands (conv2d_igemm.hip): each product is hi*hi + hi*lo + lo*hi of f16 pairs (22-bit operands,
- * exact products, fp32 accumulation).  sa_conv2d_igemm_weights arranges [Cout][Cin][3][3] (Cout %
- * 128 == 0, Cin % 32 == 0, |weight| < 16) once as sa_conv2d_igemm_weights_size(Cout, Cin) dwords
- * (16-byte aligned).  sa_conv2d_k3_igemm takes SaWinoProblem with U = those weights (any W; the
- * row pitch % 4 == 0, 16-byte aligned outputs), the bias, ReLU, input transform (Cin <= 512) and
- * InstanceNorm partials ([N*Cout][parts][2], parts = sa_conv2d_igemm_stat_parts(H, W)) of
- * sa_conv2d_k3_wino_ex and the gate epilogues 1 / 2 of sa_conv2d_k3_wino4_multi_gate (mode 1 needs
- * Cout % 256 == 0).  Range guard (guard != 0): a block with a finite input (after its transform)
- * of magnitude >= 65504 writes nothing and recomputes its work item with its inputs scaled by a
- * power of two that brings them into the f16 range (exact; the accumulators scaled back), counted
- * by sa_split_redo_blocks; inputs that are not finite give NaN outputs.
- * sa_conv2d_igemm_blocks: the workgroups of one problem. */
-long sa_conv2d_igemm_weights_size(int Cout, int Cin);
-int sa_conv2d_igemm_weights(const float *weight, int Cout, int Cin, void *out, void *stream);
-long sa_conv2d_igemm_stat_parts(int H, int W);
-long sa_conv2d_igemm_blocks(int N, int Cout, int H, int W);
-int sa_conv2d_k3_igemm(int nprob, const SaWinoProblem *probs, const SaGateEpilogue *gates, int guard,
-                       void *stream);
-/* Blocks of the split kernels (F(4x4), the implicit GEMM and sa_conv_direct_split) that the range
+/* Blocks of the split kernels (F(4x4) and sa_conv_direct_split) that the range
  * guards recomputed since the last reset (reset != 0 clears the count), -1 on error; synchronises the
  * device. */
 long sa_split_redo_blocks(int reset);
@@ -591,7 +586,7 @@ int sa_norm_act(const float *x, long x_bs, int B, int C, long hw, const float *m
 enum {
   SA_K_CORR_PYRAMID = 0, SA_K_LOOKUP, SA_K_MONO_VOLUME, SA_K_SOFTARGMIN, SA_K_LSQ,
   SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_NORM, SA_K_CONV2D, SA_K_CONV_DIRECT,
-  SA_K_CONV2D_W4, SA_K_SHEAR, SA_K_MONO_PYRAMID, SA_K_PLUMBING, SA_K_CONV_SMALL, SA_K_NARROW, SA_K_CONV2D_IG,
+  SA_K_CONV2D_W4, SA_K_SHEAR, SA_K_MONO_PYRAMID, SA_K_PLUMBING, SA_K_CONV_SMALL, SA_K_NARROW,
   SA_K_COUNT
 };
 /* Box-state probe (bench.py, outside timed regions; synchronises the device): `blocks` blocks of 4

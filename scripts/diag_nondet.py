@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run-to-run determinism of the forward at cfg2 (batch 4, 540x960, 22 iterations): the same eager
 forward three times per setting, max |difference| of the disparity between runs, for the kernel
-switches given as name=value pairs of ops module flags (e.g. IGEMM=0 CONV3D_MFMA=1) and the
+switches given as name=value pairs of ops module flags (e.g. W4_SPLIT=0 CONV3D_MFMA=1) and the
 model's stream overlap (overlap=0/1).
 usage: python scripts/diag_nondet.py [iters] [FLAG=v ...] [overlap=0|1]"""
 import os

@@ -30,7 +30,7 @@ FAMILIES = {
     "flow_head_reduce_kernel": "gru_plumbing",
     "conv2d_k3_narrow_kernel": "conv2d_narrow", "conv2d_f1_mfma_kernel": "conv2d_small", "conv2d_small_kernel": "conv2d_small",
     # round 5: the 3-D split-f16 MFMA conv and the implicit-GEMM 3x3 conv
-    "conv3d_mf_kernel": "conv3d_fused", "ig_kernel": "conv2d_igemm",
+    "conv3d_mf_kernel": "conv3d_fused",
     # the sheared layout's producers and the block-spread lookup
     "lookup_c1_shear_lds_kernel": "corr_lookup", "pyramid_from_strided_sheared_kernel": "mono_pyramid",
 }

@@ -106,11 +106,6 @@ SIGNATURES = {
     "sa_conv2d_k3_wino4_stat_parts": (L, [I, I]),
     "sa_conv2d_k3_wino4_multi": (I, [I, P, P]),
     "sa_conv2d_k3_wino4_multi_gate": (I, [I, P, P, I, P]),
-    "sa_conv2d_igemm_weights_size": (L, [I, I]),
-    "sa_conv2d_igemm_weights": (I, [P, I, I, P, P]),
-    "sa_conv2d_igemm_stat_parts": (L, [I, I]),
-    "sa_conv2d_igemm_blocks": (L, [I, I, I, I]),
-    "sa_conv2d_k3_igemm": (I, [I, P, P, I, P]),
     "sa_conv_direct_weights": (I, [P, I, I, I, I, I, P, P]),
     "sa_conv_direct_weights_size": (L, [I, I, I, I, I]),
     "sa_conv_direct_weights_split": (I, [P, L, P, P]),
@@ -134,6 +129,8 @@ SIGNATURES = {
     "sa_conv3d_mf_stat_parts": (L, [I, I, I, I, I, I]),
     "sa_conv3d_mf": (I, [P, I, I, I, I, I, P, I, P, P, F, P, P, P]),
     "sa_conv3d_mf_set_planes": (None, [I]),
+    "sa_conv3d_mf_get_planes": (I, []),
+    "sa_struct_size": (L, [I]),
     "sa_conv3d_s2mf_weights_size": (L, []),
     "sa_conv3d_s2mf_weights": (I, [P, P, P]),
     "sa_conv3d_s2mf_stat_parts": (L, [I, I, I]),
@@ -152,7 +149,7 @@ KERNEL_IDS = {
     "corr_volume_pyramid": 0, "corr_lookup": 1, "mono_masked_volume": 2, "softargmin_conf": 3,
     "weighted_lsq": 4, "gru_zr": 5, "gru_out": 6, "convex_upsample": 7, "misc": 8, "conv3d_fused": 9,
     "norm_act": 10, "conv2d_wino": 11, "conv2d_direct": 12, "conv2d_wino4": 13, "corr_shear": 14,
-    "mono_pyramid": 15, "gru_plumbing": 16, "conv2d_small": 17, "conv2d_narrow": 18, "conv2d_igemm": 19,
+    "mono_pyramid": 15, "gru_plumbing": 16, "conv2d_small": 17, "conv2d_narrow": 18,
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -189,8 +186,29 @@ def lib() -> ctypes.CDLL:
                 raise NativeError(f"{LIB_PATH} does not export {name}")
             fn.restype = res
             fn.argtypes = args
+        _check_abi(h)
         _lib = h
     return _lib
+
+
+# include/stereoanywhere_hip.h SA_ABI_VERSION: the library must be built from the same header as
+# these bindings (the struct arrays are read at the library's stride)
+ABI_VERSION = 6
+
+
+def _check_abi(h) -> None:
+    if not hasattr(h, "sa_abi_version"):
+        if os.environ.get("SA_HIP_LIB"):   # an older library of an A/B run
+            return
+        raise NativeError(f"{LIB_PATH} has no sa_abi_version: rebuild it (`make`)")
+    v = int(h.sa_abi_version())
+    if v != ABI_VERSION:
+        raise NativeError(f"{LIB_PATH} implements ABI version {v}, these bindings {ABI_VERSION}: rebuild it")
+    for which, st in ((0, SaWinoProblem), (1, SaGateEpilogue), (2, SaResampleJob)):
+        got = int(h.sa_struct_size(which))
+        if got != ctypes.sizeof(st):
+            raise NativeError(f"{LIB_PATH}: {st.__name__} is {got} bytes in the library, "
+                              f"{ctypes.sizeof(st)} in the bindings")
 
 
 def call(name: str, *args) -> None:

@@ -39,7 +39,8 @@
 #define SA_W4_DIAG 0   // timing diagnostics only (wrong results): 1 no DMA in the loop, 2 no
                        // transform / MFMA, 3 no DMA and no barrier in the loop, 4 as 3 and no
                        // DMA at all, 5 no column pass, 6 no row pass, 7 no filter reads in the loop,
-                       // 8 neither row nor column pass (no input transform)
+                       // 8 neither row nor column pass (no input transform), 9 the loop waits for
+                       // chunk kc - 1's DMAs only (the floor of a ring that issues two chunks ahead)
 #endif
 #ifndef SA_W4_GJB
 #define SA_W4_GJB 4    // gate-epilogue store iterations whose plane loads go out together (mode 2)
@@ -717,7 +718,18 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
         }
       }
     }
-    if (SA_W4_DIAG < 3 || AFF || scaled) __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
+    if (SA_W4_DIAG == 9 && !AFF && !scaled) {
+      // timing only: wait for chunk kc - 1's DMAs, not chunk kc's (every wave issues >= 9 pieces
+      // per chunk), i.e. the floor of a ring that issues each chunk two chunks ahead
+      if (kc == 0)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else if (SA_W4_DIAG < 3 || AFF || scaled) {
+      __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
+    }
 #ifdef SA_W4_CLOCK
     if (kc == 0 && HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][4] = __builtin_amdgcn_s_memtime();
 #endif
@@ -768,7 +780,7 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
         // the next chunk's DMA part jj goes out before column jj's pass of the first job (the
         // chunk time is bound by the DMA's latency: one column earlier than after its MFMAs,
         // wino4 51.0 -> 50.1 ms/step; all parts at once delay the row reads)
-        if (SA_W4_DIAG == 0 && s == 0 && kc + 1 < nchunks) {
+        if ((SA_W4_DIAG == 0 || SA_W4_DIAG == 9) && s == 0 && kc + 1 < nchunks) {
           issue_part(kc + 1, cur ^ 1, jj);
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -1161,9 +1173,8 @@ extern "C" int sa_flow_head_reduce(const float *part, int N, int Cout, int H, in
 }
 
 long sa_direct_redo_blocks_internal(int reset);   // conv_direct.hip
-long sa_igemm_redo_blocks_internal(int reset);    // conv2d_igemm.hip
 
-// blocks of the split kernels (F(4x4), direct and the implicit GEMM) that the range guards recomputed
+// blocks of the split kernels (F(4x4) and direct) that the range guards recomputed
 // since the last reset; synchronises the device (tests and bench.py, outside timed regions)
 extern "C" long sa_split_redo_blocks(int reset) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
@@ -1173,8 +1184,8 @@ extern "C" long sa_split_redo_blocks(int reset) {
     const unsigned z = 0;
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_w4_redo_blocks), &z, sizeof z) != hipSuccess) return -1;
   }
-  const long d = sa_direct_redo_blocks_internal(reset), g = sa_igemm_redo_blocks_internal(reset);
-  return d < 0 || g < 0 ? -1 : (long)v + d + g;
+  const long d = sa_direct_redo_blocks_internal(reset);
+  return d < 0 ? -1 : (long)v + d;
 }
 
 // InstanceNorm partial count: the small blocks' tiling (a large block writes its two halves)

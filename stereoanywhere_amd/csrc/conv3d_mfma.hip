@@ -382,6 +382,7 @@ MfGeo mf_geo(int B, int Cin, int D, int H, int W) {
 }  // namespace
 
 extern "C" void sa_conv3d_mf_set_planes(int planes) { g_mf_dr = planes; }
+extern "C" int sa_conv3d_mf_get_planes() { return g_mf_dr; }
 
 extern "C" long sa_conv3d_mf_weights_size(int Cin, int Cout) {
   if (!mf_shape(Cin, Cout)) return -1;

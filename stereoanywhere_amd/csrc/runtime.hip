@@ -29,8 +29,7 @@ const char *g_names[SA_K_COUNT] = {"corr_volume_pyramid", "corr_lookup", "mono_m
                                    "gru_out",             "convex_upsample", "misc",
                                    "conv3d_fused",        "norm_act",
                                    "conv2d_wino", "conv2d_direct", "conv2d_wino4", "corr_shear",
-                                   "mono_pyramid", "gru_plumbing", "conv2d_small", "conv2d_narrow",
-                                   "conv2d_igemm"};
+                                   "mono_pyramid", "gru_plumbing", "conv2d_small", "conv2d_narrow"};
 }  // namespace
 
 TimingScope::TimingScope(int kernel_id, hipStream_t s) : id(kernel_id), stream(s), on(false) {
@@ -59,8 +58,6 @@ TimingScope::~TimingScope() {
 }  // namespace sa
 
 extern "C" {
-
-int sa_abi_version(void) { return 1; }
 
 const char *sa_last_error(void) { return sa::g_err; }
 
@@ -123,3 +120,14 @@ const char *sa_kernel_name(int kernel_id) {
 }
 
 }  // extern "C"
+
+extern "C" int sa_abi_version(void) { return SA_ABI_VERSION; }   // (1 through round 5)
+
+extern "C" long sa_struct_size(int which) {
+  switch (which) {
+    case SA_STRUCT_WINO_PROBLEM: return (long)sizeof(SaWinoProblem);
+    case SA_STRUCT_GATE_EPILOGUE: return (long)sizeof(SaGateEpilogue);
+    case SA_STRUCT_RESAMPLE_JOB: return (long)sizeof(SaResampleJob);
+    default: return -1;
+  }
+}

@@ -64,6 +64,17 @@ def gather_metrics(local: torch.Tensor, r: Rank) -> torch.Tensor:
     return torch.cat([b[: int(s.item())] for b, s in zip(bufs, sizes)], 0)
 
 
+def gather_scalars(value: float, r: Rank, device) -> list:
+    """all_gather of one float per rank -> [rank 0's, rank 1's, ...] on every rank (the per-rank
+    timed-region lengths of bench.py: a slow rank shows as such, not only as the max)."""
+    if r.world == 1:
+        return [float(value)]
+    t = torch.tensor([value], device=device, dtype=torch.float64)
+    out = [torch.zeros_like(t) for _ in range(r.world)]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
 def max_over_ranks(value: float, r: Rank, device) -> float:
     if r.world == 1:
         return value

@@ -316,6 +316,7 @@ def _install(wino: Optional[WinoTable], direct: Optional[DirectTable], fold: Opt
     _DIRECT.update(direct or {})
     _FOLD.clear()
     _FOLD.update(fold or {})
+    _SKIP_ST.clear()   # (entries hold the previous tables' Affine objects alive)
 
 
 def fnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],

@@ -19,8 +19,6 @@ class ForwardGraph:
     """Callable like StereoAnywhere.forward(image2, image3, mde2, mde3, iters, test_mode=True);
     returns (flow_up, None) with flow_up a fresh tensor (the graph's output buffer is reused)."""
 
-    _instances = 0
-
     def __init__(self, model: torch.nn.Module):
         self.model = model
         self._key = None
@@ -31,7 +29,6 @@ class ForwardGraph:
         # captured launches hold no per-stream workspace: the split kernels' range guards recompute
         # an overflowed block inside its own launch, so graph instances replayed at the same time on
         # different streams (PipelinedForward) share no state
-        ForwardGraph._instances += 1
         self._cap_stream: Optional[torch.cuda.Stream] = None
 
     def _make_key(self, xs, iters):
@@ -47,11 +44,11 @@ class ForwardGraph:
         # (an A/B run's older library, SA_HIP_LIB, may lack a getter: its switch reads as None)
         c_switches = tuple(getattr(lib, name)() if hasattr(lib, name) else None
                            for name in ("sa_lookup_get_mfma", "sa_softargmin_get_one_pass", "sa_conv3d_wd_get_variant",
+                                         "sa_conv3d_mf_get_planes",
                                          "sa_lookup_get_shear_dual"))
         return (tuple((tuple(x.shape), x.dtype, x.device) for x in xs), iters, dataclasses.astuple(m.opts),
-                m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_SPLIT, ops.IGEMM, ops.IGEMM_MAX_WORK,
-                                                   ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS, ops.SPLIT_GUARD, ops.CONV3D_MFMA,
-                                                   encoders.FNET_LAZY_CLOSE),
+                m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_SPLIT, ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS,
+                                                   ops.SPLIT_GUARD, ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE),
                 c_switches, args)
 
     def __call__(self, image2, image3, mde2, mde3, iters: int = 12, test_mode: bool = True):

@@ -185,8 +185,8 @@ class StereoAnywhere(nn.Module):
         """Derived tensors (split GRU kernels, permuted classifier kernels, folded BatchNorm),
         rebuilt when any parameter or buffer is modified or moved."""
         key = tuple((p.data_ptr(), p._version) for p in list(self.parameters()) + list(self.buffers()))
-        # (the split kernels' filters and the implicit GEMM's are derived only when on)
-        key += (self.opts.direct_conv, ops.W4_SPLIT, ops.DIRECT_SPLIT, ops.IGEMM)
+        # (the split kernels' filters are derived only when on)
+        key += (self.opts.direct_conv, ops.W4_SPLIT, ops.DIRECT_SPLIT)
         if self._derived_key != key:
             ub = self.update_block
             hd = self.args.context_dims

@@ -860,16 +860,13 @@ def conv2d_k3_narrow(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch
 
 
 class WinoFilters:
-    """Derived filters of one 3x3 conv for the fused Winograd kernels and the implicit GEMM:
-    ``u2`` for F(2x2,3x3) (conv2d_wino.hip), ``u4`` for F(4x4,3x3) (conv2d_wino4.hip) in 32-channel
-    blocks, ``u4s`` as the split F(4x4) kernel's f16 hi/lo pairs (None unless W4_SPLIT when derived)
-    and ``uig`` as the implicit-GEMM kernel's split weights (conv2d_igemm.hip; None unless IGEMM,
-    Cout % 128 == 0 and Cin % 32 == 0)."""
-    __slots__ = ("u2", "u4", "u4s", "uig", "cin", "cout")
+    """Derived filters of one 3x3 conv for the fused Winograd kernels: ``u2`` for F(2x2,3x3)
+    (conv2d_wino.hip), ``u4`` for F(4x4,3x3) (conv2d_wino4.hip) in 32-channel blocks and ``u4s`` as
+    the split F(4x4) kernel's f16 hi/lo pairs (None unless W4_SPLIT when derived)."""
+    __slots__ = ("u2", "u4", "u4s", "cin", "cout")
 
-    def __init__(self, u2: torch.Tensor, u4: torch.Tensor, cin: int, cout: int, u4s: Optional[torch.Tensor] = None,
-                 uig: Optional[torch.Tensor] = None):
-        self.u2, self.u4, self.u4s, self.uig, self.cin, self.cout = u2, u4, u4s, uig, cin, cout
+    def __init__(self, u2: torch.Tensor, u4: torch.Tensor, cin: int, cout: int, u4s: Optional[torch.Tensor] = None):
+        self.u2, self.u4, self.u4s, self.cin, self.cout = u2, u4, u4s, cin, cout
 
 
 # False keeps every 3x3 conv on the F(2x2,3x3) kernel (set by A/B scripts and tests)
@@ -879,16 +876,9 @@ _WINO4 = True
 # f16 x f16 products, fp32 accumulation) instead of fp32 MFMA: 1.06-1.22x per conv, 54.3 -> 60.4
 # pairs/s at configs[1] with EPE vs the reference 1.78e-5 (fp32 MFMA: 1.84e-5)
 W4_SPLIT = True
-# 3x3 launches on the implicit-GEMM kernel (conv2d_igemm.hip: direct convolution on
-# v_mfma_f32_16x16x32_f16, three f16 products per fp32 product) where every problem allows it
-# (Cout % 128, Cin % 32; gate modes 1 / 2) and the launch's total output pixels x Cout is at most
-# IGEMM_MAX_WORK (None: no limit; see conv2d_k3_multi).  Off by default, by measurement (round 5,
-# one box, same library): the forward at configs[1] 61.2 ms/step on F(4x4) only, 62.1 with every
-# eligible conv on the implicit GEMM (its MFMA load draws the clock to ~2.2 GHz against ~2.33), 61.9
-# with it on the 1/32-level launches only (IGEMM_MAX_WORK 3e6, where it is 1.2-1.3x per conv
-# standalone); DESIGN.md section 0
-IGEMM = False
-IGEMM_MAX_WORK = None
+# (round 5 built a split-f16 implicit-GEMM 3x3 conv on 16x16x32 MFMA, conv2d_igemm.hip: 0.88-1.02x
+# F(4x4) per conv at the model's shapes and slower in the forward, so it was off by default; round 6
+# deleted it)
 # the split filters need |U * 2^12| < 65504; |U| <= max |weight| for F(4x4,3x3)'s G
 _W4_SPLIT_WMAX = 15.99
 # the direct convs (stems, stride-2 + 1x1) with split products (sa_conv_direct_split), derived
@@ -920,12 +910,7 @@ def wino_weights(weight: torch.Tensor) -> WinoFilters:
     if W4_SPLIT and Cout % 32 == 0 and Cin % 8 == 0 and split_range_ok(weight):
         u4s = torch.empty((36 * Cin * Cout,), device=weight.device, dtype=torch.int32)
         N.call("sa_conv2d_wino4_weights_split", weight.data_ptr(), Cout, Cin, u4s.data_ptr(), _stream(weight))
-    uig = None
-    if IGEMM and Cout % 128 == 0 and Cin % 32 == 0 and split_range_ok(weight):
-        uig = torch.empty((int(N.lib().sa_conv2d_igemm_weights_size(Cout, Cin)),), device=weight.device,
-                          dtype=torch.int32)
-        N.call("sa_conv2d_igemm_weights", weight.data_ptr(), Cout, Cin, uig.data_ptr(), _stream(weight))
-    return WinoFilters(u2, u4, Cin, Cout, u4s, uig)
+    return WinoFilters(u2, u4, Cin, Cout, u4s)
 
 
 # largest Cin of an F(4x4,3x3) launch with an input transform (its (scale, shift) table fills the
@@ -965,7 +950,7 @@ _WINO4_MIN_BLOCKS = 128
 def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] = None, relu: bool = False,
                   out: Optional[torch.Tensor] = None, in_aff: Optional[Affine] = None, in_act=None,
                   stats: bool = False, f4: bool = False, out_cout: Optional[int] = None,
-                  width: Optional[int] = None, split: bool = False, ig: bool = False,
+                  width: Optional[int] = None, split: bool = False,
                   skip: Optional[torch.Tensor] = None, skip_s: Optional[torch.Tensor] = None,
                   skip_t: Optional[torch.Tensor] = None, skip_act=None, out_act=None):
     """out_cout: channels of ``out`` when the epilogue writes fewer than Cout there (gate mode 1).
@@ -980,8 +965,8 @@ def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] 
     W = P if width is None else width
     if not 0 < W <= P:
         raise RuntimeError(f"conv2d_k3: width {W} outside the plane pitch {P}")
-    if W != P and not (f4 or ig):
-        raise RuntimeError("conv2d_k3: pitched planes need the F(4x4,3x3) or the implicit-GEMM kernel")
+    if W != P and not f4:
+        raise RuntimeError("conv2d_k3: pitched planes need the F(4x4,3x3) kernel")
     Cout = U.cout
     if U.cin != Cin:
         raise RuntimeError(f"conv2d_k3: U has {U.cin} input channels, x has {Cin}")
@@ -991,16 +976,15 @@ def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] 
     if tuple(out.shape) != (B, out_cout or Cout, H, P):
         raise RuntimeError("conv2d_k3: out shape mismatch")
     m, s, t, ps = (in_aff or Affine()).args(Cin)
-    parts_fn = (N.lib().sa_conv2d_igemm_stat_parts if ig else N.lib().sa_conv2d_k3_wino4_stat_parts if f4
-                else N.lib().sa_conv2d_k3_wino_stat_parts)
+    parts_fn = N.lib().sa_conv2d_k3_wino4_stat_parts if f4 else N.lib().sa_conv2d_k3_wino_stat_parts
     parts = int(parts_fn(H, W)) if stats else 0
     partial = torch.empty((B * Cout * parts * 2,), device=x.device, dtype=torch.float64) if stats else None
-    Uf = U.uig if ig else (U.u4s if split else U.u4) if f4 else U.u2
+    Uf = (U.u4s if split else U.u4) if f4 else U.u2
     prob = N.SaWinoProblem(x.data_ptr(), bs, B, Cin, H, W, Uf.data_ptr(), Cout, _ptr(bias),
                            1 if relu else 0, m, s, t, ps, ACT[in_act], out.data_ptr(), _plane_bs(out, "out"),
                            _ptr(partial), P if P != W else 0)
     if skip is not None:
-        if not f4 or ig or stats:
+        if not f4 or stats:
             raise RuntimeError("conv2d_k3: the residual epilogue needs the F(4x4) kernel and no statistics")
         if tuple(skip.shape) != (B, Cout, H, P) or skip.stride(1) != H * P:
             raise RuntimeError(f"conv2d_k3: skip must be [{B}, {Cout}, {H}, {P}] planes")
@@ -1011,10 +995,8 @@ def _wino_problem(x: torch.Tensor, U: WinoFilters, bias: Optional[torch.Tensor] 
         prob.skip_s, prob.skip_t = _ptr(skip_s), _ptr(skip_t)
         prob.skip_act, prob.out_act = ACT[skip_act], ACT[out_act]
     # Winograd-domain products actually executed: 36 per 4x4 tile (F4) or 16 per 2x2 tile (F2)
-    # per (Cin, Cout) pair; the implicit GEMM: the direct convolution's 9 per output
-    if ig:
-        _account("conv2d_igemm", 2.0 * 9 * Cin * Cout * B * H * W)   # logical W
-    elif f4:
+    # per (Cin, Cout) pair
+    if f4:
         _account("conv2d_wino4", 2.0 * 36 * Cin * Cout * B * ((H + 3) // 4) * ((W + 3) // 4))   # logical W
     else:
         _account("conv2d_wino", 2.0 * 16 * Cin * Cout * B * ((H + 1) // 2) * ((W + 1) // 2))
@@ -1074,26 +1056,6 @@ def _wino4_launch(n: int, arr, gates, shape: int, x: torch.Tensor) -> None:
            1 if (shape == 6 and SPLIT_GUARD) else 0, _stream(x))
 
 
-_IG_GATED = _IG_AFF = _IG_MULTI = True   # (diagnostic switches: problem kinds the implicit GEMM takes)
-
-
-def _igemm_ok(p: dict, q: dict) -> bool:
-    """Whether the implicit-GEMM kernel takes problem p (q: its arguments without the gate):
-    its weights derived (Cout % 128, Cin % 32, |w| < 16), gate modes 1 (Cout % 256) or 2, an input
-    transform none / ReLU with Cin <= 512, plane pitches % 4 and 16-byte aligned outputs."""
-    U, x, out = q["U"], q["x"], q.get("out")
-    if not IGEMM or U.uig is None or q.get("skip") is not None:
-        return False
-    g = p.get("gate")
-    if (g and not _IG_GATED) or ((q.get("in_aff") is not None or q.get("in_act") is not None) and not _IG_AFF):
-        return False
-    if g and not (g["mode"] == 2 or (g["mode"] == 1 and U.cout % 256 == 0)):
-        return False
-    if (q.get("in_aff") is not None or q.get("in_act") is not None) and (x.shape[1] > 512 or ACT[q.get("in_act")] > 1):
-        return False
-    return (x.shape[3] % 4 == 0 and (out is None or (out.data_ptr() % 16 == 0 and out.stride(0) % 4 == 0)))
-
-
 def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     """Independent conv2d_k3 calls (each a dict of conv2d_k3's keyword arguments) in ONE launch:
     their blocks share the grid, so each conv's partly filled last round of blocks is filled by
@@ -1109,24 +1071,6 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     for p, q in zip(problems, plain):
         if p.get("gate") and p["gate"]["mode"] == 1:
             q["out_cout"] = p["U"].cout // 2   # z only: r*h goes to the gate's out2
-    if not small_blocks and (_IG_MULTI or len(problems) == 1):
-        igs = [_igemm_ok(p, q) for p, q in zip(problems, plain)]
-        if any(igs):
-            if not all(igs):   # the implicit-GEMM problems in a launch of their own, the others as before
-                res = [None] * len(problems)
-                for idx in ([i for i, k in enumerate(igs) if k], [i for i, k in enumerate(igs) if not k]):
-                    for i, r in zip(idx, conv2d_k3_multi(*[problems[i] for i in idx])):
-                        res[i] = r
-                return res
-            if IGEMM_MAX_WORK is None or sum(q["x"].shape[0] * q["x"].shape[2] * q["x"].shape[3] * q["U"].cout
-                                             for q in plain) <= IGEMM_MAX_WORK:
-                built = [_wino_problem(**q, ig=True) for q in plain]
-                arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
-                gates = (N.SaGateEpilogue * len(built))(*[_gate_epilogue(p) if p.get("gate") else N.SaGateEpilogue()
-                                                          for p in problems])
-                N.call("sa_conv2d_k3_igemm", len(built), ctypes.addressof(arr), ctypes.addressof(gates),
-                       1 if SPLIT_GUARD else 0, _stream(problems[0]["x"]))
-                return [b[1]() for b in built]
     oks = [_WINO4 and _wino4_ok(**p) for p in plain]
     if any(oks) and not all(oks):
         # a mixed group: the problems F(4x4) cannot take (W % 4 != 0, unaligned planes) go to a

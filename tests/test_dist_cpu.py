@@ -147,14 +147,23 @@ def _bench(args, extra_env=None, timeout=240):
 @pytest.mark.parametrize("world", [2, 3])
 def test_bench_launches_its_own_ranks(world):
     """bench.py --gpus N outside torchrun starts N ranks itself (one child per GPU): every rank joins
-    the process group and reports world == N (the --dry-run rendezvous, gloo on the CPU)."""
+    the process group and reports world == N (the --dry-run rendezvous, gloo on the CPU).  The line
+    explains itself at N > 1: each rank's timed-region ms per step (stand-in
+    steps: rank r sleeps 5 (r + 1) ms, so the last rank is the slowest), the metric all_gather's
+    latency and size, and the cpu_baseline key (a tiny oracle sample in the dry run)."""
     import json
-    res = _bench(["--gpus", str(world), "--dry-run"])
+    res = _bench(["--gpus", str(world), "--dry-run", "--steps", "3"])
     assert res.returncode == 0, res.stderr
     line = json.loads([ln for ln in res.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == world
     assert line["ranks"] == list(range(world))
     assert line["worlds"] == [world]
+    rt = line["rank_timing"]
+    assert len(rt["per_rank_ms_per_step"]) == world and rt["slowest_rank"] == world - 1
+    assert all(v >= 5.0 for v in rt["per_rank_ms_per_step"]) and rt["spread"] > 1.0
+    assert rt["gather_ms"] > 0 and rt["gather_bytes"] == world * 2 * 8 and rt["backend"] == "gloo"
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1
 
 
 def test_bench_world_size_mismatch_fails():
@@ -164,6 +173,18 @@ def test_bench_world_size_mismatch_fails():
                                                     MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port())))
     assert res.returncode != 0
     assert "WORLD_SIZE 2" in res.stderr
+
+
+def test_bench_rank_dying_after_init_ends_the_launch():
+    """a rank that dies after the rendezvous (here rank 1 exits right after
+    init_process_group) leaves the others waiting in a collective; the launcher ends them and exits
+    non-zero with the dead rank's code instead of hanging."""
+    import time
+    t0 = time.monotonic()
+    res = _bench(["--gpus", "3", "--dry-run"], dict(SA_DRYRUN_FAIL_RANK="1"), timeout=180)
+    assert res.returncode == 3, (res.returncode, res.stderr[-2000:])
+    assert "rank exit codes" in res.stderr
+    assert time.monotonic() - t0 < 120
 
 
 def test_bench_failing_rank_fails_the_launch():

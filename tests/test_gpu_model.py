@@ -38,18 +38,16 @@ def test_tiny_case_and_intermediates(model):
     assert e < 1e-3
 
 
-@pytest.mark.parametrize("kernels", ["fp32", "split", "split_igemm"])
+@pytest.mark.parametrize("kernels", ["fp32", "split"])
 @pytest.mark.parametrize("name,H,W,D,iters", [("cfg1_256x512_it8.npz", 256, 512, 64.0, 8),
                                                ("cfg2_544x960_it22.npz", 544, 960, 192.0, 22)])
 def test_end_to_end_vs_reference(model, monkeypatch, name, H, W, D, iters, kernels):
     """kernels: every 3x3 conv on fp32 MFMA products (the F(4x4) / F(2x2) Winograd kernels, and the
     direct convs); "split": the F(4x4) and direct convs on the f16 hi/lo split kernels (ops.W4_SPLIT,
-    ops.DIRECT_SPLIT); "split_igemm": and the 3x3 convs it takes on the implicit GEMM (ops.IGEMM:
-    16x16x32 f16 MFMA, three products)."""
+    ops.DIRECT_SPLIT)."""
     from stereoanywhere_amd import ops
     monkeypatch.setattr(ops, "W4_SPLIT", kernels != "fp32")
     monkeypatch.setattr(ops, "DIRECT_SPLIT", kernels != "fp32")
-    monkeypatch.setattr(ops, "IGEMM", kernels == "split_igemm")
     fix = load_fixture(name)
     pair = regenerate_inputs(fix, 1, H, W, D)
     ops.WORK = {}
@@ -58,7 +56,7 @@ def test_end_to_end_vs_reference(model, monkeypatch, name, H, W, D, iters, kerne
         work = dict(ops.WORK)
     finally:
         ops.WORK = None
-    assert ("conv2d_igemm" in work) == (kernels == "split_igemm")
+    assert "conv2d_wino4" in work and "conv2d_direct" in work
     e = epe(disp, fix["disparity"])
     print(name, kernels, "EPE", e, "max", float(np.abs(disp - fix["disparity"]).max()))
     assert e < 1e-3
@@ -123,7 +121,6 @@ def test_large_disparity_split_vs_fp32(model, monkeypatch):
     for split in (False, True):
         monkeypatch.setattr(ops, "W4_SPLIT", split)
         monkeypatch.setattr(ops, "DIRECT_SPLIT", split)
-        monkeypatch.setattr(ops, "IGEMM", split)
         out[split] = run(model, pb, 8)
     assert np.isfinite(out[True]).all() and np.isfinite(out[False]).all()
     assert float(np.abs(out[True]).max()) > 50.0   # the large-disparity regime is exercised
@@ -235,29 +232,33 @@ def test_loop_parts_match_one_stream(model, parts, offset):
                                     dict(mono_stream=False), dict(cnet_side=1), dict(cnet_side=0),
                                     dict(small_launches=frozenset({"q16", "q08", "zr16", "zr08", "pro32"})),
                                     dict(direct_conv=False), dict(wino4=False),
-                                    dict(shear_min_bytes=0), dict(sheared_producers=True, shear_min_bytes=0),
-                                    dict(igemm=False), dict(fuse_flow_head=False)])
+                                    dict(sheared_producers=False), dict(shear_min_bytes=1 << 62),
+                                    dict(fuse_flow_head=False), dict(conv3d_mfma=False),
+                                    dict(fnet_lazy_close=False)])
 def test_schedule_options_vs_reference(change):
-    """Every non-default launch schedule (stereoanywhere_amd.model.ScheduleOptions; ops._WINO4)
-    computes the same forward: cfg1 against the reference's disparity."""
+    """Every non-default launch schedule (stereoanywhere_amd.model.ScheduleOptions; ops._WINO4,
+    ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE) computes the same forward: cfg1 against the
+    reference's disparity.  (sheared_producers=False: the row-layout producers and the copy pass;
+    shear_min_bytes=2^62: the row-layout lookup.)"""
     import dataclasses
 
-    from stereoanywhere_amd import ops
+    from stereoanywhere_amd import encoders, ops
     m = StereoAnywhere(dict(PUBLISHED)).eval()
     synth.load_seeded_weights(m, 0)
     m = m.cuda()
     change = dict(change)
     wino4 = change.pop("wino4", True)
-    igemm = change.pop("igemm", ops.IGEMM)
+    mf = change.pop("conv3d_mfma", ops.CONV3D_MFMA)
+    lazy = change.pop("fnet_lazy_close", encoders.FNET_LAZY_CLOSE)
     m.opts = dataclasses.replace(m.opts, **change)
     fix = load_fixture("cfg1_256x512_it8.npz")
     pair = regenerate_inputs(fix, 1, 256, 512, 64.0)
-    old = ops._WINO4, ops.IGEMM
-    ops._WINO4, ops.IGEMM = wino4, igemm
+    old = ops._WINO4, ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE
+    ops._WINO4, ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE = wino4, mf, lazy
     try:
         disp = run(m, pair, 8)
     finally:
-        ops._WINO4, ops.IGEMM = old
+        ops._WINO4, ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE = old
     e = epe(disp, fix["disparity"])
     print(change, "wino4" if wino4 else "no wino4", "EPE", e)
     assert e < 1e-3

@@ -11,13 +11,6 @@ pytestmark = pytest.mark.gpu
 dev = "cuda"
 
 
-@pytest.fixture(autouse=True)
-def _winograd_only(monkeypatch):
-    """These tests pin the Winograd kernels: the implicit GEMM (ops.IGEMM) would take every
-    problem with Cout % 128 == 0 (tests/test_gpu_igemm.py covers it)."""
-    monkeypatch.setattr(ops, "IGEMM", False)
-
-
 def rnd(*shape, seed=0):
     g = torch.Generator(device="cpu").manual_seed(seed)
     return torch.randn(*shape, generator=g).to(dev)
@@ -531,12 +524,10 @@ def test_wino4_split_range_guard_whole_launch(monkeypatch):
     B = 4; inputs ~1e4, so every tile's transformed values overflow f16) runs its item again on
     exactly scaled inputs inside the launch, in parallel: the result equals the fp32-product
     kernel's within the split kernel's own accuracy (~1e-5 of the output scale, as
-    test_wino4_matches_conv2d), and the launch takes at most ~2x the fp32 kernel's time (split pass,
-    the scale scan and the scaled pass per block; bound 2.25x)."""
+    test_wino4_matches_conv2d).  Its time against the fp32 kernel: tests/test_perf_gpu.py (perf)."""
     monkeypatch.setattr(ops, "_WINO4_MIN_BLOCKS", 0)
     x = rnd(4, 256, 136, 240, seed=11) * 1e4
     w = rnd(384, 256, 3, 3, seed=12) / 48
-    t = {}
     outs = {}
     for split in (False, True):
         monkeypatch.setattr(ops, "W4_SPLIT", split)
@@ -545,24 +536,12 @@ def test_wino4_split_range_guard_whole_launch(monkeypatch):
         (y,), work = _run(monkeypatch, True, dict(x=x, U=U))
         assert "conv2d_wino4" in work
         outs[split] = (y, _redo_blocks())
-        ops.conv2d_k3(x, U)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(5):
-            ops.conv2d_k3(x, U)
-        e1.record()
-        torch.cuda.synchronize()
-        t[split] = e0.elapsed_time(e1) / 5
     blocks = 4 * (-(-136 // 8)) * (-(-240 // 128)) * (384 // 32)
-    print(f"whole-launch overflow: {outs[True][1]} of {blocks} blocks redone; split {t[True]:.3f} ms, "
-          f"fp32 {t[False]:.3f} ms")
+    print(f"whole-launch overflow: {outs[True][1]} of {blocks} blocks redone")
     assert outs[True][1] >= blocks // 2 and outs[False][1] == 0
     assert torch.isfinite(outs[True][0]).all()
     scale = float(outs[False][0].abs().max())
     assert float((outs[True][0] - outs[False][0]).abs().max()) < 5e-5 * scale
-    # (measured 2.05-2.1x: the second pass first rereads the block's input patch to pick its scale)
-    assert t[True] <= 2.25 * t[False] + 0.05, t
 
 
 @pytest.mark.parametrize("split", [False, True])

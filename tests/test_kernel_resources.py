@@ -1,12 +1,9 @@
 """Compile-time checks of the hot kernels (hipcc for gfx950, no GPU): no register spills (scratch)
 in the conv kernels whose second, rarely taken passes (the split kernels' range guards) share a
-body with the hot one, and no compiler copy or reuse of a register that a hand-scheduled inline-asm
-load is still writing (scripts/check_asm_loads.py: the implicit GEMM's weight / patch prefetches;
-such a copy made its results vary from run to run)."""
+body with the hot one, or whose register budget is near the limit (conv3d_s2mf: ~239 VGPRs)."""
 import os
 import re
 import subprocess
-import sys
 
 import pytest
 
@@ -38,19 +35,11 @@ def _compile(name, tmp_path, extra=()):
 
 @pytest.mark.parametrize("name,kernel,extra", [
     ("conv2d_wino4.hip", "wino_f4k3_kernel", ("-fno-slp-vectorize",)),
-    ("conv2d_igemm.hip", "ig_kernel", ()),
     ("conv3d_mfma.hip", "conv3d_mf_kernel", ()),
+    ("conv3d_s2mf.hip", "conv3d_s2mf_kernel", ()),
 ])
 def test_conv_kernels_do_not_spill(tmp_path, name, kernel, extra):
     usage, _ = _compile(name, tmp_path, extra)
     hot = {k: v for k, v in usage.items() if kernel in k}
     assert hot, sorted(usage)
     assert all(v == 0 for v in hot.values()), hot
-
-
-def test_igemm_asm_loads_have_no_in_flight_copies(tmp_path):
-    _, listing = _compile("conv2d_igemm.hip", tmp_path)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_asm_loads.py"), str(listing),
-                        "ig_kernel"], capture_output=True, text=True, timeout=120)
-    counts = [int(m) for m in re.findall(r": (\d+) suspicious instruction", r.stdout)]
-    assert len(counts) == 3 and all(c == 0 for c in counts), r.stdout[-3000:]
