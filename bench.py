@@ -488,6 +488,11 @@ def main():
                     help="F(4x4) convs on the split kernel (1) or fp32 MFMA (0); default: ops.W4_SPLIT")
     ap.add_argument("--direct-split", type=int, default=None, choices=[0, 1],
                     help="direct convs on split products (1) or fp32 MFMA (0); default: ops.DIRECT_SPLIT")
+    ap.add_argument("--direct-small", type=int, default=None, choices=[0, 1],
+                    help="the context encoder's small stride-2 stages on the direct kernel (1) or MIOpen (0); "
+                         "default: encoders.DIRECT_SMALL")
+    ap.add_argument("--conv1x1", type=int, default=None, choices=[0, 1],
+                    help="the 1x1 convs on sa_conv1x1 (1) or F.conv2d / rocBLAS (0); default: ops.CONV1X1")
     ap.add_argument("--split-guard", type=int, default=None, choices=[0, 1],
                     help="the split kernel's f16 range guard (default ops.SPLIT_GUARD; 0 for A/B timing only)")
     ap.add_argument("--opts", default="",
@@ -558,6 +563,11 @@ def main():
         _N.lib().sa_lookup_set_shear_dual(int(args.lookup_form))
     if args.direct_split is not None:
         ops.DIRECT_SPLIT = bool(args.direct_split)
+    if args.direct_small is not None:
+        from stereoanywhere_amd import encoders as _E
+        _E.DIRECT_SMALL = bool(args.direct_small)
+    if args.conv1x1 is not None:
+        ops.CONV1X1 = bool(args.conv1x1)
 
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
     # SA_DIST_BACKEND=gloo (and SA_DIST_SHARE_GPU=1): a multi-rank rehearsal of this code path on a
@@ -758,7 +768,7 @@ def main():
     # the update loop's plumbing (pool2x / interp / flow_update: planes read and written once),
     # flow_head.conv2 (256 -> 2 planes), the mono pyramid (volume read, levels written) and convf1
     # (7x7, 2 -> 64 channels on fp32 MFMA), each priced per call (ops._account)
-    for k_, u_ in (("gru_plumbing", "GB/s"), ("conv2d_narrow", "GB/s"), ("mono_pyramid", "GB/s"),
+    for k_, u_ in (("gru_plumbing", "GB/s"), ("conv2d_narrow", "GB/s"), ("mono_pyramid", "GB/s"), ("conv1x1", "GB/s"),
                    ("conv2d_small", "TFLOP/s")):
         costs[k_] = (u_, work.get(k_, 0.0))
     kernels = {}

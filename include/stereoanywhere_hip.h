@@ -520,6 +520,35 @@ int sa_conv2d_k3_wino4_launch(int nprob, const SaWinoProblem *probs, const SaGat
  * guards recomputed since the last reset (reset != 0 clears the count), -1 on error; synchronises the
  * device. */
 long sa_split_redo_blocks(int reset);
+/* 1x1 convolution (stride 1, no padding) as a GEMM on split-f16 MFMA (conv1x1.hip): the feature
+ * encoder's output conv (extractor.py:149) and the mask head's 1x1 (update.py:159-162, 191).
+ *   out[b][co][p] = scale * (bias[co] + sum_ci W[co][ci] x[b][ci][p]) over the flat H*W plane;
+ *   each product as hi*hi + hi*lo + lo*hi of f16 pairs (22-bit operands), fp32 accumulation.
+ * sa_conv1x1_weights: [Cout][Cin] fp32 -> the split weights (sa_conv1x1_weights_size(Cout, Cin)
+ *   bytes, 16-byte aligned; |weight| < 16).
+ * sa_conv1x1: x [B][Cin][H][W] (batch stride x_bs floats, 16-byte aligned, H*W % 4 == 0,
+ *   Cin % 32 == 0), bias [Cout] or NULL, out [B][Cout][H][W] (batch stride out_bs).  A block whose
+ *   inputs reach the f16 range (|x| >= 65504) recomputes its outputs with fp32 FMAs;
+ *   sa_conv1x1_redo_blocks counts those blocks (reset != 0 clears; synchronises the device). */
+long sa_conv1x1_weights_size(int Cout, int Cin);
+int sa_conv1x1_weights(const float *weight, int Cout, int Cin, void *out, void *stream);
+int sa_conv1x1(const float *x, long x_bs, int B, int Cin, int H, int W, const void *wsplit, int Cout,
+               const float *bias, float scale, float *out, long out_bs, void *stream);
+long sa_conv1x1_redo_blocks(int reset);
+/* The tiled harness's data movement (mapreduce_v2/tile_wrapper.py:226-236, 169-185, 188-189;
+ * tiler.hip):
+ * sa_tile_gather_pad: src [C][H][W] (dense) -> out [ntiles][C][th + pt + pb][tw + pl + pr], tile t
+ *   the rectangle at origin[2t] (row), origin[2t + 1] (column) (device int pairs), padded by edge
+ *   replication (torch.cat of the tile views, then F.pad(..., mode="replicate")), bit-exact copies.
+ * sa_tile_stitch: for every pixel of num / den [H][W], the ntiles entries tiles[3i .. 3i + 2] =
+ *   (row, column, slot) in order (a rectangle listed twice adds twice), each covering it adds
+ *   d * w to num and w to den, d = disp[slot * disp_ts + ty * dpitch + tx], w = wgt[ty * tw + tx];
+ *   finalize != 0 then writes num = den > 0 ? num / max(den, 1e-4) : num (den untouched).  The
+ *   reference's per-tile slice updates, per pixel in the same order: the same bits. */
+int sa_tile_gather_pad(const float *src, int C, int H, int W, const int *origin, int ntiles, int th, int tw,
+                       int pt, int pb, int pl, int pr, float *out, void *stream);
+int sa_tile_stitch(const float *disp, long disp_ts, int dpitch, const int *tiles, int ntiles, int th, int tw,
+                   const float *wgt, int H, int W, int finalize, float *num, float *den, void *stream);
 /* The flow head fused (gate mode 3 above): floats of the partial-sum buffer of a conv over
  * [N, Cout, H, W] (-1 on bad shapes), and the reduction that finishes it: delta = bias0 + the
  * sum of the partials at each pixel (conv2's channel 0), then as sa_flow_update: coords_x +=
@@ -587,7 +616,7 @@ enum {
   SA_K_CORR_PYRAMID = 0, SA_K_LOOKUP, SA_K_MONO_VOLUME, SA_K_SOFTARGMIN, SA_K_LSQ,
   SA_K_GRU_ZR, SA_K_GRU_OUT, SA_K_UPSAMPLE, SA_K_MISC, SA_K_CONV3D, SA_K_NORM, SA_K_CONV2D, SA_K_CONV_DIRECT,
   SA_K_CONV2D_W4, SA_K_SHEAR, SA_K_MONO_PYRAMID, SA_K_PLUMBING, SA_K_CONV_SMALL, SA_K_NARROW,
-  SA_K_COUNT
+  SA_K_CONV1X1, SA_K_COUNT
 };
 /* Box-state probe (bench.py, outside timed regions; synchronises the device): `blocks` blocks of 4
  * waves run `iters` x 4 chained f16 MFMAs each; *mhz = the median over waves of the in-kernel shader

@@ -45,6 +45,12 @@ class SaResampleJob(ctypes.Structure):
 
 SIGNATURES = {
     "sa_abi_version": (I, []),
+    "sa_conv1x1_weights_size": (L, [I, I]),
+    "sa_conv1x1_weights": (I, [P, I, I, P, P]),
+    "sa_conv1x1": (I, [P, L, I, I, I, I, P, I, P, F, P, L, P]),
+    "sa_conv1x1_redo_blocks": (L, [I]),
+    "sa_tile_gather_pad": (I, [P, I, I, I, P, I, I, I, I, I, I, I, P, P]),
+    "sa_tile_stitch": (I, [P, L, I, P, I, I, I, P, I, I, I, P, P, P]),
     "sa_last_error": (ctypes.c_char_p, []),
     "sa_pyramid_level_width": (I, [I, I]),
     "sa_pyramid_level_offset": (I, [I, I]),
@@ -149,7 +155,7 @@ KERNEL_IDS = {
     "corr_volume_pyramid": 0, "corr_lookup": 1, "mono_masked_volume": 2, "softargmin_conf": 3,
     "weighted_lsq": 4, "gru_zr": 5, "gru_out": 6, "convex_upsample": 7, "misc": 8, "conv3d_fused": 9,
     "norm_act": 10, "conv2d_wino": 11, "conv2d_direct": 12, "conv2d_wino4": 13, "corr_shear": 14,
-    "mono_pyramid": 15, "gru_plumbing": 16, "conv2d_small": 17, "conv2d_narrow": 18,
+    "mono_pyramid": 15, "gru_plumbing": 16, "conv2d_small": 17, "conv2d_narrow": 18, "conv1x1": 19,
 }
 
 _lib: Optional[ctypes.CDLL] = None

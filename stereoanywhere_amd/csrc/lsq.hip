@@ -122,44 +122,103 @@ __device__ __forceinline__ void hist_add(unsigned *h, unsigned bin, bool count) 
   if (act & me) atomicAdd(&h[bin], 1u);
 }
 
-// KPT > 0: the sample's keys (n <= KPT * LSQ_THREADS) stay in registers over the four
-// radix passes; KPT == 0: they are re-read from memory each pass.
-template <int KPT>
-__global__ __launch_bounds__(LSQ_THREADS) void lsq_kernel(const float *__restrict__ mde, const float *__restrict__ disp,
-                                                          const float *__restrict__ conf, int n, float q_lo,
-                                                          float q_hi, float *__restrict__ scale,
-                                                          float *__restrict__ shift) {
-  __shared__ unsigned hist[4][256];
-  __shared__ unsigned prefix[4];
-  __shared__ unsigned remain[4];
-  __shared__ double red[LSQ_THREADS / 64];
-  __shared__ float qv[2];
-  const int b = blockIdx.x;
-  const float *md = mde + (long)b * n, *dd = disp + (long)b * n, *cd = conf + (long)b * n;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+// ------------------------------------------------- weighted LSQ, one launch (round 6)
+// One workgroup of 1024 threads per sample, one launch for the whole batch.  The four order
+// statistics (floor / ceil ranks of the two linear quantiles) come from one pass over the keys
+// instead of four radix passes:
+//   A. a histogram of the top 15 bits of every key (relu'd values: sign 0, so 16384 bins of
+//      relative width 2^-6) in LDS; a wave per rank finds the rank's bin and the count below it
+//      (per-thread sums of 8 bins, then the bins of the one segment);
+//   B. the keys of the (at most 4, usually 2) selected bins and their indices are copied into an LDS
+//      pool at offsets known from the histogram (the pool holds 16384 keys: 25 % of a model sample);
+//      the same pass accumulates the normal equations of every key in a bin strictly between the
+//      lower and the upper quantile's bins (inside the band whatever the exact quantiles);
+//   C. a 9-bit and an 8-bit radix pass over each rank's bin (its pool slice) give the exact key;
+//      then the pooled keys inside the band add their terms (their mono / confidence values
+//      gathered by index).
+// A sample whose selected bins hold more keys than the pool (e.g. a quarter of the pixels at
+// one value) takes the four full 8-bit radix passes instead (lsq_select_radix below, the round-5
+// single-block algorithm) and a separate pass for the normal equations, in the same launch.
+// Every pass streams the sample's keys from memory (L2-resident after the first) in chunks of
+// L1_CH keys per thread whose loads are all in flight together: one load at a time, the pass
+// would wait a round trip per key.
+#ifdef SA_LSQ_CLOCK   // phase timestamps of block 0 (diagnostic builds)
+__device__ long long g_lsq_clock[8];
+#define LSQ_STAMP(i) \
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_lsq_clock[i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define LSQ_STAMP(i)
+#endif
+constexpr int L1_BINS = 16384, L1_SHIFT = 17, L1_POOL = 16384, L1_SEG = 8, L1_CH = 16;
 
-  unsigned keys[KPT > 0 ? KPT : 1];
-  if (KPT > 0) {
+// f(key, index, valid) over this thread's keys of dd[0 .. n), in chunks of L1_CH loads in flight
+template <class Fn>
+__device__ __forceinline__ void lsq_stream_keys(const float *__restrict__ dd, int n, Fn f) {
+  const int t = threadIdx.x;
+  for (int base = 0; base < n; base += L1_CH * LSQ_THREADS) {
+    unsigned k[L1_CH];
 #pragma unroll
-    for (int i = 0; i < KPT; ++i) {
-      const int j = t + i * LSQ_THREADS;
-      keys[i] = j < n ? key_of(dd[j]) : 0u;
+    for (int c = 0; c < L1_CH; ++c)   // (clamped, not predicated: a load under a branch waits at once)
+      k[c] = key_of(dd[min(base + c * LSQ_THREADS + t, n - 1)]);
+#pragma unroll
+    for (int c = 0; c < L1_CH; ++c) {
+      const int j = base + c * LSQ_THREADS + t;
+      f(k[c], j, j < n);
     }
   }
+}
 
-  // ranks of torch.quantile(linear): rank = q * (n - 1) in fp32
-  const float r_lo = q_lo * (float)(n - 1), r_hi = q_hi * (float)(n - 1);
-  if (t < 4) {
-    const float r = (t < 2) ? r_lo : r_hi;
-    const float idx = (t & 1) ? ceilf(r) : truncf(r);
-    remain[t] = (unsigned)idx;
-    prefix[t] = 0u;
+// a[i] of a 4-entry register array for a wave-uniform i < 4 (no dynamic indexing: that goes to scratch)
+template <class T>
+__device__ __forceinline__ T pick4(const T (&a)[4], int i) {
+  return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
+}
+
+// the first index i of cnt[0 .. 64 * PER) (LDS) whose inclusive prefix count exceeds rem, and the
+// count of the entries before it; every lane of the calling wave gets both
+template <int PER>
+__device__ __forceinline__ void wave_find(const unsigned *cnt, unsigned rem, int &idx, unsigned &below) {
+  const int lane = threadIdx.x & 63;
+  unsigned c[PER], tot = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    c[k] = cnt[lane * PER + k];
+    tot += c[k];
   }
+  unsigned inc = tot;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  const unsigned long long past = __ballot(inc > rem);
+  const int L = past ? __ffsll((long long)past) - 1 : 63;
+  unsigned acc = inc - tot;
+  int sel = PER - 1;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (acc + c[k] > rem) {
+      sel = k;
+      break;
+    }
+    acc += c[k];
+  }
+  idx = __shfl(L * PER + sel, L);
+  below = __shfl(acc, L);
+}
+
+// The round-5 single-block selection: four 8-bit radix passes over all n keys (re-read from
+// memory), ranks sharing a prefix share a histogram.  hist: LDS [4][256]; pre / rem: LDS [4]
+// (rem holds the ranks on entry, the keys' prefixes in pre on exit).
+__device__ __forceinline__ void lsq_select_radix(const float *__restrict__ dd, int n, unsigned *hist, unsigned *prefix,
+                                 unsigned *remain) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t < 4) prefix[t] = 0u;
+  __syncthreads();
   for (int pass = 0; pass < 4; ++pass) {
     const int shift_ = 24 - 8 * pass;
-    for (int i = t; i < 4 * 256; i += LSQ_THREADS) (&hist[0][0])[i] = 0u;
+    for (int i = t; i < 4 * 256; i += LSQ_THREADS) hist[i] = 0u;
     __syncthreads();
-    // ranks whose selected prefix so far equals an earlier rank's share its histogram
     unsigned pre[4];
     int src[4];
 #pragma unroll
@@ -169,89 +228,262 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq_kernel(const float *__restric
       for (int q = r - 1; q >= 0; --q)
         if (pre[q] == pre[r]) src[r] = q;
     }
-    auto count = [&](unsigned k, bool valid) {
+    lsq_stream_keys(dd, n, [&](unsigned k, int, bool valid) {
       const unsigned bin = (k >> shift_) & 255u;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (src[r] != r) continue;  // uniform
+        if (src[r] != r) continue;
         const bool match = valid && (pass == 0 || ((k ^ pre[r]) >> (shift_ + 8)) == 0u);
-        hist_add(hist[r], bin, match);
+        hist_add(hist + 256 * r, bin, match);
       }
-    };
-    if (KPT > 0) {
-#pragma unroll
-      for (int i = 0; i < KPT; ++i) count(keys[i], t + i * LSQ_THREADS < n);
-    } else {
-      for (int i0 = 0; i0 < n; i0 += LSQ_THREADS) {
-        const int i = i0 + t;
-        count(i < n ? key_of(dd[i]) : 0u, i < n);
-      }
-    }
+    });
     __syncthreads();
     if (wv < 4) {
-      // wave wv selects rank wv's digit: lane l owns bins 4l..4l+3; inclusive scan of the
-      // lane totals, the first lane whose running count passes the rank holds the digit
-      const unsigned *hr = hist[src[wv]];
-      const unsigned rem = remain[wv];
-      const unsigned c0 = hr[4 * lane], c1 = hr[4 * lane + 1], c2 = hr[4 * lane + 2], c3 = hr[4 * lane + 3];
-      unsigned inc = c0 + c1 + c2 + c3;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const unsigned u = __shfl_up(inc, o);
-        if (lane >= o) inc += u;
-      }
-      const unsigned long long past = __ballot(inc > rem);
-      const int L = past ? __ffsll((long long)past) - 1 : 63;
-      if (lane == L) {
-        unsigned acc = inc - (c0 + c1 + c2 + c3), sel = 4u * L + 3u;
-        const unsigned cs[4] = {c0, c1, c2, c3};
-        for (int k = 0; k < 4; ++k) {
-          if (acc + cs[k] > rem) {
-            sel = 4u * L + k;
-            break;
-          }
-          acc += cs[k];
-        }
-        remain[wv] = rem - acc;
-        prefix[wv] = pre[wv] | (sel << shift_);
+      int d;
+      unsigned below;
+      wave_find<4>(hist + 256 * pick4(src, wv), remain[wv], d, below);
+      if (lane == 0) {
+        remain[wv] -= below;
+        prefix[wv] = pick4(pre, wv) | ((unsigned)d << shift_);
       }
     }
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(LSQ_THREADS) void lsq1_kernel(const float *__restrict__ mde, const float *__restrict__ disp,
+                                                           const float *__restrict__ conf, int n, float q_lo,
+                                                           float q_hi, float *__restrict__ scale,
+                                                           float *__restrict__ shift) {
+  __shared__ unsigned hist[L1_BINS];           // pass A; then the pooled keys' indices
+  __shared__ unsigned pool[L1_POOL];           // the selected bins' keys
+  __shared__ unsigned seg[L1_BINS / L1_SEG];   // 8-bin sums; then [4][512] digit histograms
+  static_assert(L1_BINS / L1_SEG >= 4 * 512 && L1_BINS >= L1_POOL, "LDS reuse");
+  __shared__ unsigned s_bin[4], s_rem[4], s_off[4], s_cnt[4], s_pre[4], s_total;
+  __shared__ int s_list[4], s_fall;
+  __shared__ double red[LSQ_THREADS / 64];
+  __shared__ float qv[2];
+  const int b = blockIdx.x;
+  const float *md = mde + (long)b * n, *dd = disp + (long)b * n, *cd = conf + (long)b * n;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  LSQ_STAMP(7);
+
+  // ranks of torch.quantile(linear): rank = q * (n - 1) in fp32
+  const float r_lo = q_lo * (float)(n - 1), r_hi = q_hi * (float)(n - 1);
+  if (t < 4) {
+    const float r = (t < 2) ? r_lo : r_hi;
+    s_rem[t] = (unsigned)((t & 1) ? ceilf(r) : truncf(r));
+  }
+  for (int i = t; i < L1_BINS; i += LSQ_THREADS) hist[i] = 0u;
+  __syncthreads();
+  LSQ_STAMP(0);
+  // A: histogram of the top bits
+  lsq_stream_keys(dd, n, [&](unsigned k, int, bool v) { hist_add(hist, k >> L1_SHIFT, v); });
+  __syncthreads();
+  LSQ_STAMP(1);
+  {
+    unsigned sacc = 0;
+#pragma unroll
+    for (int k = 0; k < L1_SEG; ++k) sacc += hist[t * L1_SEG + k];
+    for (int q = t + LSQ_THREADS; q < L1_BINS / L1_SEG; q += LSQ_THREADS) {   // (L1_BINS / L1_SEG > LSQ_THREADS)
+      unsigned a2 = 0;
+#pragma unroll
+      for (int k = 0; k < L1_SEG; ++k) a2 += hist[q * L1_SEG + k];
+      seg[q] = a2;
+    }
+    seg[t] = sacc;
+  }
+  __syncthreads();
+  if (wv < 4) {   // wave r: rank r's bin and the keys below it
+    int sg;
+    unsigned below;
+    wave_find<L1_BINS / L1_SEG / 64>(seg, s_rem[wv], sg, below);
+    if (lane == 0) {
+      unsigned acc = below, rem = s_rem[wv];
+      int bin = sg * L1_SEG + L1_SEG - 1;
+      for (int k = 0; k < L1_SEG; ++k) {
+        const unsigned c = hist[sg * L1_SEG + k];
+        if (acc + c > rem) {
+          bin = sg * L1_SEG + k;
+          break;
+        }
+        acc += c;
+      }
+      s_bin[wv] = (unsigned)bin;
+      s_rem[wv] = rem - acc;   // the rank within its bin
+    }
+  }
+  __syncthreads();
+  if (t == 0) {   // pool slices of the distinct bins
+    unsigned off = 0;
+    int fall = 0;
+    for (int r = 0; r < 4; ++r) {
+      int src = r;
+      for (int q = r - 1; q >= 0; --q)
+        if (s_bin[q] == s_bin[r]) src = q;
+      s_list[r] = src;
+      if (src == r) {
+        s_off[r] = off;
+        s_cnt[r] = 0u;
+        off += hist[s_bin[r]];
+      }
+    }
+    fall = off > (unsigned)L1_POOL;
+    s_fall = fall;
+    s_total = off;
+  }
+  __syncthreads();
+  LSQ_STAMP(2);
+  const bool fall = s_fall != 0;
+  unsigned lb[4];
+  int lsrc[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    lb[r] = s_bin[r];
+    lsrc[r] = s_list[r];
+  }
+  double s11 = 0, s12 = 0, s22 = 0, t1 = 0, t2 = 0;
+  auto add_terms = [&](float d, float mv, float cv) __attribute__((always_inline)) {
+    const float m = fabsf(mv);
+    const float cc = fabsf(cv) * 0.9f + 0.1f;
+    const float w = sqrtf(cc);
+    const float a1 = m * w, y = fabsf(d) * w;
+    s11 += (double)a1 * a1;
+    s12 += (double)a1 * w;
+    s22 += (double)w * w;
+    t1 += (double)a1 * y;
+    t2 += (double)w * y;
+  };
+  if (!fall) {
+    // B: copy the selected bins' keys (and indices) into their pool slices (wave-aggregated
+    // appends); the normal equations of the keys strictly between the quantiles' bins
+    const unsigned in_lo = lb[1], in_hi = lb[2];   // (b0 <= b1 <= b2 <= b3)
+    auto append = [&](unsigned k, int j, bool valid) __attribute__((always_inline)) {
+      const unsigned bin = k >> L1_SHIFT;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (lsrc[r] != r) continue;   // (uniform)
+        const bool hit = valid && bin == lb[r];
+        const unsigned long long m = __ballot(hit);
+        if (!m) continue;
+        const int leader = __ffsll((long long)m) - 1;
+        unsigned base = 0;
+        if (lane == leader) base = atomicAdd(&s_cnt[r], (unsigned)__popcll(m));
+        base = __shfl(base, leader);
+        if (hit) {
+          const unsigned at = s_off[r] + base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+          pool[at] = k;
+          hist[at] = (unsigned)j;
+        }
+      }
+    };
+    for (int base = 0; base < n; base += 8 * LSQ_THREADS) {
+      unsigned kv[8];
+      float mv[8], cv[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {   // (clamped loads, all in flight together)
+        const int jc = min(base + c * LSQ_THREADS + t, n - 1);
+        kv[c] = key_of(dd[jc]);
+        mv[c] = md[jc];
+        cv[c] = cd[jc];
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int j = base + c * LSQ_THREADS + t;
+        const unsigned bin = kv[c] >> L1_SHIFT;
+        append(kv[c], j, j < n);
+        if (j < n && bin > in_lo && bin < in_hi) add_terms(__uint_as_float(kv[c]), mv[c], cv[c]);
+      }
+    }
+    __syncthreads();
+  LSQ_STAMP(3);
+    // C: the low 17 bits of each rank's key as a 9-bit and an 8-bit digit (seg reused as [4][512])
+    if (t < 4) s_pre[t] = lb[t] << L1_SHIFT;
+    for (int pass = 0; pass < 2; ++pass) {
+      const int sh = pass == 0 ? 8 : 0, bits = pass == 0 ? 9 : 8;   // bits 16..8, then 7..0
+      for (int i = t; i < 4 * 512; i += LSQ_THREADS) seg[i] = 0u;
+      __syncthreads();
+      unsigned pre[4];
+      int src[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pre[r] = s_pre[r];
+        src[r] = r;
+        for (int q = r - 1; q >= 0; --q)
+          if (pre[q] == pre[r]) src[r] = q;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (src[r] != r) continue;   // (uniform)
+        const int L = lsrc[r];
+        const unsigned cnt = s_cnt[L], off = s_off[L];
+        for (unsigned e0 = 0; e0 < cnt; e0 += LSQ_THREADS) {
+          const unsigned e = e0 + t;
+          const unsigned k = e < cnt ? pool[off + e] : 0u;
+          const bool match = e < cnt && (pass == 0 || ((k ^ pre[r]) >> (sh + bits)) == 0u);
+          hist_add(seg + 512 * r, (k >> sh) & ((1u << bits) - 1u), match);
+        }
+      }
+      __syncthreads();
+      if (wv < 4) {
+        int d;
+        unsigned below;
+        wave_find<8>(seg + 512 * pick4(src, wv), s_rem[wv], d, below);
+        if (lane == 0) {
+          s_rem[wv] -= below;
+          s_pre[wv] = pick4(pre, wv) | ((unsigned)d << sh);
+        }
+      }
+      __syncthreads();
+    }
+  } else {
+    if (t < 4) {
+      const float r = (t < 2) ? r_lo : r_hi;
+      s_rem[t] = (unsigned)((t & 1) ? ceilf(r) : truncf(r));
+    }
+    __syncthreads();
+    lsq_select_radix(dd, n, hist, s_pre, s_rem);
+  }
+  LSQ_STAMP(4);
   if (t < 2) {
     const float r = t == 0 ? r_lo : r_hi;
-    const float lo = __uint_as_float(prefix[2 * t]), hi = __uint_as_float(prefix[2 * t + 1]);
+    const float lo = __uint_as_float(s_pre[2 * t]), hi = __uint_as_float(s_pre[2 * t + 1]);
     qv[t] = lerp_ref(lo, hi, r - truncf(r));
   }
   __syncthreads();
+  LSQ_STAMP(5);
   const float qlo = qv[0], qhi = qv[1];
-  double s11 = 0, s12 = 0, s22 = 0, t1 = 0, t2 = 0;
-  auto accum = [&](int i, unsigned k) {
-    const float d = __uint_as_float(k);
-    if (qlo <= d && d <= qhi) {
-      const float m = fabsf(md[i]);
-      const float c = fabsf(cd[i]) * 0.9f + 0.1f;
-      const float w = sqrtf(c);
-      const float a1 = m * w, y = fabsf(d) * w;
-      s11 += (double)a1 * a1;
-      s12 += (double)a1 * w;
-      s22 += (double)w * w;
-      t1 += (double)a1 * y;
-      t2 += (double)w * y;
+  if (!fall) {   // the pooled keys inside the band
+    const unsigned total = s_total;
+    for (unsigned e = t; e < total; e += LSQ_THREADS) {
+      const float d = __uint_as_float(pool[e]);
+      if (qlo <= d && d <= qhi) {
+        const unsigned j = hist[e];
+        add_terms(d, md[j], cd[j]);
+      }
     }
-  };
-  if (KPT > 0) {
+  } else {   // (the fallback: every key against the band)
+    for (int base = 0; base < n; base += 8 * LSQ_THREADS) {
+      float dv[8], mv[8], cv[8];
 #pragma unroll
-    for (int u = 0; u < KPT; ++u)
-      if (t + u * LSQ_THREADS < n) accum(t + u * LSQ_THREADS, keys[u]);
-  } else {
-    for (int i = t; i < n; i += LSQ_THREADS) accum(i, key_of(dd[i]));
+      for (int c = 0; c < 8; ++c) {
+        const int j = base + c * LSQ_THREADS + t, jc = min(j, n - 1);
+        dv[c] = __uint_as_float(key_of(dd[jc]));
+        if (j >= n) dv[c] = -1.0f;   // (outside every band)
+        mv[c] = md[jc];
+        cv[c] = cd[jc];
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (qlo <= dv[c] && dv[c] <= qhi) add_terms(dv[c], mv[c], cv[c]);
+    }
   }
   s11 = block_sum(s11, red);
   s12 = block_sum(s12, red);
   s22 = block_sum(s22, red);
   t1 = block_sum(t1, red);
   t2 = block_sum(t2, red);
+  LSQ_STAMP(6);
   if (t == 0) {
     const double det = s11 * s22 - s12 * s12;
     double sc, sh;
@@ -356,7 +588,7 @@ __global__ __launch_bounds__(LSQ_BT) void lsq_hist_kernel(const float *__restric
   if (!s_last) return;
   __threadfence();
   if (wv < 4) {
-    const unsigned *hr = gh + 256 * src[wv];
+    const unsigned *hr = gh + 256 * pick4(src, wv);
     const unsigned rem = s_rem[wv];
     const unsigned c0 = ld_agent(hr + 4 * lane), c1 = ld_agent(hr + 4 * lane + 1);
     const unsigned c2 = ld_agent(hr + 4 * lane + 2), c3 = ld_agent(hr + 4 * lane + 3);
@@ -379,7 +611,7 @@ __global__ __launch_bounds__(LSQ_BT) void lsq_hist_kernel(const float *__restric
         acc += cs[k];
       }
       st->remain[wv] = rem - acc;
-      st->prefix[wv] = pre[wv] | (sel << shift_);
+      st->prefix[wv] = pick4(pre, wv) | (sel << shift_);
     }
   }
   __syncthreads();
@@ -516,10 +748,7 @@ extern "C" int sa_weighted_lsq(const float *mde, const float *disp, const float 
   SA_REQUIRE(q_lo >= 0.f && q_lo <= q_hi && q_hi <= 1.f, "sa_weighted_lsq: quantiles out of order");
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_LSQ, s);
-  if (n_per_b <= 32 * LSQ_THREADS)
-    lsq_kernel<32><<<B, LSQ_THREADS, 0, s>>>(mde, disp, conf, n_per_b, q_lo, q_hi, scale, shift);
-  else
-    lsq_kernel<0><<<B, LSQ_THREADS, 0, s>>>(mde, disp, conf, n_per_b, q_lo, q_hi, scale, shift);
+  lsq1_kernel<<<B, LSQ_THREADS, 0, s>>>(mde, disp, conf, n_per_b, q_lo, q_hi, scale, shift);
   return sa::check_launch("sa_weighted_lsq");
 }
 
@@ -568,3 +797,9 @@ extern "C" int sa_mono_scale_mirror(const float *m2, const float *m3, const floa
   mirror_kernel<<<nb, 256, 0, s>>>(sm2, sm3, dL, conf_l, H, W, in_bs, lrc_th, div, conf_th, npix, mirror, coords_x);
   return sa::check_launch("sa_mono_scale_mirror/mirror");
 }
+
+#ifdef SA_LSQ_CLOCK
+extern "C" int sa_lsq_clock_read(long long *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lsq_clock), sizeof(long long) * 8) == hipSuccess ? 0 : -1;
+}
+#endif

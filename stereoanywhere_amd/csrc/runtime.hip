@@ -29,7 +29,8 @@ const char *g_names[SA_K_COUNT] = {"corr_volume_pyramid", "corr_lookup", "mono_m
                                    "gru_out",             "convex_upsample", "misc",
                                    "conv3d_fused",        "norm_act",
                                    "conv2d_wino", "conv2d_direct", "conv2d_wino4", "corr_shear",
-                                   "mono_pyramid", "gru_plumbing", "conv2d_small", "conv2d_narrow"};
+                                   "mono_pyramid", "gru_plumbing", "conv2d_small", "conv2d_narrow",
+                                   "conv1x1"};
 }  // namespace
 
 TimingScope::TimingScope(int kernel_id, hipStream_t s) : id(kernel_id), stream(s), on(false) {

@@ -98,6 +98,28 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
   v += dpp_f32<0x143, 0xC>(0.0f, v);
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
+// N independent reductions with their DPP steps interleaved (the same tree per value: results equal
+// wave_max_dpp / wave_sum_dpp bit for bit), so the N dependency chains hide each other's latency
+template <int N>
+__device__ __forceinline__ void wave_max_dpp_n(float (&v)[N]) {
+#define SA_DPP_STEP(CTRL, RM)                                                     \
+  _Pragma("unroll") for (int i = 0; i < N; ++i) v[i] = fmaxf(v[i], dpp_f32<CTRL, RM>(-INFINITY, v[i]));
+  SA_DPP_STEP(0xB1, 0xF) SA_DPP_STEP(0x4E, 0xF) SA_DPP_STEP(0x141, 0xF) SA_DPP_STEP(0x140, 0xF)
+  SA_DPP_STEP(0x142, 0xA) SA_DPP_STEP(0x143, 0xC)
+#undef SA_DPP_STEP
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v[i]), 63));
+}
+template <int N>
+__device__ __forceinline__ void wave_sum_dpp_n(float (&v)[N]) {
+#define SA_DPP_STEP(CTRL, RM) \
+  _Pragma("unroll") for (int i = 0; i < N; ++i) v[i] += dpp_f32<CTRL, RM>(0.0f, v[i]);
+  SA_DPP_STEP(0xB1, 0xF) SA_DPP_STEP(0x4E, 0xF) SA_DPP_STEP(0x141, 0xF) SA_DPP_STEP(0x140, 0xF)
+  SA_DPP_STEP(0x142, 0xA) SA_DPP_STEP(0x143, 0xC)
+#undef SA_DPP_STEP
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v[i]), 63));
+}
 // fp64 sum; the total is in lane 63 only
 __device__ __forceinline__ double wave_sum_dpp_lane63(double v) {
   v += dpp_f64<0xB1>(v);

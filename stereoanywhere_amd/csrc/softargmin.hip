@@ -299,32 +299,52 @@ __global__ __launch_bounds__(1024) void sam_slice_kernel(const float *__restrict
       x[r][c] = (k < n && j < n) ? src[(long)k * g.sk + j] : -INFINITY;
     }
   }
-  // ---- right: per row k, softmax over j (estimate_right_*, utils.py:132-152, 162-170)
+  // ---- right: per row k, softmax over j (estimate_right_*, utils.py:132-152, 162-170).  Rows in
+  // groups of RG: each group's max / sum / accumulate reductions run as RG interleaved DPP chains
+  // (one row at a time, the wave waited on one chain's latency after another: round 6, 4 rows per
+  // group; the same operations per row, so the same bits)
   const float lw_r = g.log2W1;
+  constexpr int RG = NR % 4 == 0 ? 4 : NR % 3 == 0 ? 3 : NR % 2 == 0 ? 2 : 1;
 #pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const int k = w + 16 * r;
-    if (k >= n) continue;   // wave-uniform
-    float m = x[r][0];
+  for (int r0 = 0; r0 < NR; r0 += RG) {
+    if (w + 16 * r0 >= n) continue;   // wave-uniform (rows k >= n of a group: all -inf, unused)
+    float m[RG];
 #pragma unroll
-    for (int c = 1; c < NC; ++c) m = fmaxf(m, x[r][c]);
-    m = wave_max(m);
-    float e[NC], se = 0.f;
+    for (int u = 0; u < RG; ++u) {
+      m[u] = x[r0 + u][0];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      e[c] = exp_le0(x[r][c] - m);   // -inf (j >= n) -> 0
-      se += e[c];
+      for (int c = 1; c < NC; ++c) m[u] = fmaxf(m[u], x[r0 + u][c]);
     }
-    const float inv = 1.0f / wave_sum(se);
-    float acc = 0.f;
+    sa::wave_max_dpp_n(m);
+    float e[RG][NC], se[RG];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int j = lane + 64 * c;
-      const float p = e[c] * inv;
-      if (j < n) acc += conf ? p * log2_pos(p + 1e-6f) : p * (float)j;
+    for (int u = 0; u < RG; ++u) {
+      se[u] = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        e[u][c] = exp_le0(x[r0 + u][c] - m[u]);   // -inf (j >= n) -> 0
+        se[u] += e[u][c];
+      }
     }
-    acc = wave_sum(acc);
-    if (lane == 0) outR[ob + k] = conf ? 1.0f - (-acc) / lw_r : acc - (float)k;
+    sa::wave_sum_dpp_n(se);
+    float acc[RG];
+#pragma unroll
+    for (int u = 0; u < RG; ++u) {
+      const float inv = 1.0f / se[u];
+      acc[u] = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int j = lane + 64 * c;
+        const float p = e[u][c] * inv;
+        if (j < n) acc[u] += conf ? p * log2_pos(p + 1e-6f) : p * (float)j;
+      }
+    }
+    sa::wave_sum_dpp_n(acc);
+#pragma unroll
+    for (int u = 0; u < RG; ++u) {
+      const int k = w + 16 * (r0 + u);
+      if (lane == 0 && k < n) outR[ob + k] = conf ? 1.0f - (-acc[u]) / lw_r : acc[u] - (float)k;
+    }
   }
   // ---- left: per column j, softmax over k (estimate_left_*, utils.py:112-130, 154-161)
   auto column_total = [&](float *part, bool is_max) __attribute__((always_inline)) {

@@ -30,6 +30,9 @@ from . import ops
 # the feature encoder's stage outputs formed by the next stage's stride-2 direct conv while it
 # stages its input (_Close; False: each stage's last block writes its output in a norm_act pass)
 FNET_LAZY_CLOSE = True
+# the stride-2 blocks below one direct-conv block per CU (the context encoder's 1/16 and 1/32
+# stages) on the direct kernel too (True) or on MIOpen's finer grid (False, round 5's choice)
+DIRECT_SMALL = True
 
 # Winograd-transformed filters of the eligible 3x3 convs (ops.conv2d_k3), keyed by the
 # module's weight storage; filled by StereoAnywhere._weights()
@@ -84,7 +87,9 @@ def block_direct(blk: nn.Module) -> bool:
 
 def _direct_fills_chip(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     """The direct kernel runs one 8x32-output block per CU; below one block per CU (cnet's
-    1/16 and 1/32 stages) MIOpen's finer grid is faster."""
+    1/16 and 1/32 stages) MIOpen's finer grid was faster (DIRECT_SMALL = False keeps it there)."""
+    if DIRECT_SMALL:
+        return True
     B, _, H, W = x.shape
     Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
     nc = 96 if conv.out_channels == 96 else 128
@@ -320,14 +325,18 @@ def _install(wino: Optional[WinoTable], direct: Optional[DirectTable], fold: Opt
 
 
 def fnet_forward(enc: nn.Module, x: torch.Tensor, table: Dict[str, ops.Affine],
-                 wino: WinoTable = None, direct: DirectTable = None) -> torch.Tensor:
-    """BasicEncoder.forward (extractor.py:62-153) -> [N, 256, H/4, W/4]."""
+                 wino: WinoTable = None, direct: DirectTable = None,
+                 out_w: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """BasicEncoder.forward (extractor.py:62-153) -> [N, 256, H/4, W/4].  out_w: the output 1x1
+    conv's split weights (ops.conv1x1_weights; None: F.conv2d)."""
     _install(wino, direct)
     fin = _Finisher("instance" if isinstance(enc.norm1, nn.InstanceNorm2d) else "batch", table)
     x = _stem(enc, x, fin)
     for s in ("layer1", "layer2", "layer3"):
         # (layer1 / layer2 outputs: the next stage's stride-2 direct conv may form them on load)
         x = _stage(getattr(enc, s), s, x, fin, lazy_out=FNET_LAZY_CLOSE and s != "layer3")
+    if out_w is not None and x.shape[2] * x.shape[3] % 4 == 0:
+        return ops.conv1x1(x, out_w, enc.conv2.out_channels, enc.conv2.bias)
     return F.conv2d(x, enc.conv2.weight, enc.conv2.bias)
 
 

@@ -48,7 +48,8 @@ class ForwardGraph:
                                          "sa_lookup_get_shear_dual"))
         return (tuple((tuple(x.shape), x.dtype, x.device) for x in xs), iters, dataclasses.astuple(m.opts),
                 m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_SPLIT, ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS,
-                                                   ops.SPLIT_GUARD, ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE),
+                                                   ops.SPLIT_GUARD, ops.CONV3D_MFMA, ops.CONV1X1,
+                                                   encoders.FNET_LAZY_CLOSE, encoders.DIRECT_SMALL),
                 c_switches, args)
 
     def __call__(self, image2, image3, mde2, mde3, iters: int = 12, test_mode: bool = True):

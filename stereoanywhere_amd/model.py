@@ -186,7 +186,7 @@ class StereoAnywhere(nn.Module):
         rebuilt when any parameter or buffer is modified or moved."""
         key = tuple((p.data_ptr(), p._version) for p in list(self.parameters()) + list(self.buffers()))
         # (the split kernels' filters are derived only when on)
-        key += (self.opts.direct_conv, ops.W4_SPLIT, ops.DIRECT_SPLIT)
+        key += (self.opts.direct_conv, ops.W4_SPLIT, ops.DIRECT_SPLIT, ops.CONV1X1)
         if self._derived_key != key:
             ub = self.update_block
             hd = self.args.context_dims
@@ -237,7 +237,10 @@ class StereoAnywhere(nn.Module):
                          U_mot=ops.wino_weights(d["mot_w"]),
                          U_fh1=ops.wino_weights(ub.flow_head.conv1.weight.detach().contiguous()),
                          U_mask=ops.wino_weights(ub.mask[0].weight.detach().contiguous()),
-                         U_ctx=[ops.wino_weights(c.weight.detach().contiguous()) for c in self.context_zqr_convs])
+                         U_ctx=[ops.wino_weights(c.weight.detach().contiguous()) for c in self.context_zqr_convs],
+                         # the 1x1 convs on sa_conv1x1 (None: F.conv2d)
+                         c1_fnet=ops.conv1x1_weights(self.fnet.conv2.weight),
+                         c1_mask=ops.conv1x1_weights(ub.mask[2].weight))
                 cls = torch.cat([self._derived["cls_d"], self._derived["cls_c"]], 0)  # [2,8,3,3,3]
                 self._derived["hg"] = self.hourglass_mono.fused_weights(cls)
                 if self.args.use_aggregate_stereo_vol:
@@ -340,7 +343,7 @@ class StereoAnywhere(nn.Module):
             else:
                 hid, ctx = self._context(dw, mde2)
             fm = encoders.fnet_forward(self.fnet, torch.cat([image2, image3], 0), dw["bn_fnet"], dw["wino"],
-                                       dw["direct"])
+                                       dw["direct"], out_w=dw["c1_fnet"])
         fmap2, fmap3 = fm[:B].contiguous(), fm[B:].contiguous()
         if side is not None:
             main.wait_stream(side)
@@ -533,12 +536,21 @@ class StereoAnywhere(nn.Module):
         the mono maps at the volume's resolution (1/2^vol_downsample), then at 1/2^i for
         i = n_downsample .. 5."""
         a = self.args
+
+        def resized(m, i):   # F.interpolate(scale_factor=2^-i)'s output size: floor(size * 2^-i)
+            B, C, H, W = m.shape
+            return torch.empty((B, C, H >> i, W >> i), device=m.device, dtype=torch.float32)
+
         out = []
         for m in (mde2, mde3):
+            m = m.contiguous()
             if a.vol_downsample > 0:
-                m = F.interpolate(m, scale_factor=1 / 2 ** a.vol_downsample, mode="bilinear", align_corners=True)
-            out.append([F.interpolate(m, scale_factor=1 / 2 ** i, mode="bilinear", align_corners=True)
-                        for i in range(a.n_downsample, len(self.feature_channels))])
+                m = ops.interp(m, resized(m, a.vol_downsample))
+            levels = [resized(m, i) for i in range(a.n_downsample, len(self.feature_channels))]
+            # the levels as jobs of one resample launch each (align_corners bilinear, sa_resample_multi)
+            for k in range(0, len(levels), 4):
+                ops.resample_multi(*[("interp", m, o, None, None) for o in levels[k:k + 4]])
+            out.append(levels)
         return out
 
     def _masked_dense(self, vol, m2l, m3l, vd: int) -> torch.Tensor:
@@ -781,7 +793,10 @@ class StereoAnywhere(nn.Module):
                 # mask head (update.py:185-191): 3x3 conv + bias + ReLU on the Winograd kernel,
                 # then the 1x1 conv; x 0.25 as the reference scales it
                 m1 = ops.conv2d_k3(h08, dw["U_mask"], ub.mask[0].bias, relu=True)
-                mask = F.conv2d(m1, ub.mask[2].weight, ub.mask[2].bias).mul_(0.25)
+                if dw["c1_mask"] is not None:
+                    mask = ops.conv1x1(m1, dw["c1_mask"], ub.mask[2].out_channels, ub.mask[2].bias, 0.25)
+                else:
+                    mask = F.conv2d(m1, ub.mask[2].weight, ub.mask[2].bias).mul_(0.25)
                 flow_up = ops.convex_upsample(flow[:, 0:1].contiguous(), mask, 2 ** self.args.n_downsample)
             yield
         return flow_up, None

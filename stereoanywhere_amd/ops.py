@@ -1155,6 +1155,73 @@ def conv2d_k3(x: torch.Tensor, U: torch.Tensor, bias: Optional[torch.Tensor] = N
                                 stats=stats, **residual))[0]
 
 
+# the 1x1 convs (fnet's output conv, the mask head's 1x1) on sa_conv1x1 (False: F.conv2d, A/B runs)
+CONV1X1 = True
+
+
+def conv1x1_weights(weight: torch.Tensor) -> Optional[torch.Tensor]:
+    """[Cout, Cin, 1, 1] (or [Cout, Cin]) -> the split weights of sa_conv1x1 (f16 hi / lo planes of
+    w * 2^12), or None where the kernel does not take the conv (|w| >= 16, Cin % 32 != 0): the
+    caller keeps F.conv2d."""
+    w = weight.detach().reshape(weight.shape[0], -1).contiguous()
+    _check(w, "weight")
+    Cout, Cin = w.shape
+    if not CONV1X1 or Cin % 32 or not split_range_ok(w):
+        return None
+    out = torch.empty((int(N.lib().sa_conv1x1_weights_size(Cout, Cin)),), device=w.device, dtype=torch.uint8)
+    N.call("sa_conv1x1_weights", w.data_ptr(), Cout, Cin, out.data_ptr(), _stream(w))
+    return out
+
+
+def conv1x1(x: torch.Tensor, wsplit: torch.Tensor, Cout: int, bias: Optional[torch.Tensor] = None,
+            scale: float = 1.0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """scale * (F.conv2d(x, w, bias)) for a 1x1 stride-1 conv on split-f16 MFMA (sa_conv1x1; weights
+    from conv1x1_weights): the feature encoder's output conv and the mask head's 1x1."""
+    bs = _plane_bs(x, "x")
+    B, Cin, H, W = x.shape
+    if out is None:
+        out = torch.empty((B, Cout, H, W), device=x.device, dtype=torch.float32)
+    if tuple(out.shape) != (B, Cout, H, W):
+        raise RuntimeError("conv1x1: out shape mismatch")
+    if bias is not None:
+        _check(bias, "bias")
+    N.call("sa_conv1x1", x.data_ptr(), bs, B, Cin, H, W, wsplit.data_ptr(), Cout, _ptr(bias), float(scale),
+           out.data_ptr(), _plane_bs(out, "out"), _stream(x))
+    _account("conv1x1", 4.0 * B * (Cin + Cout) * H * W)   # bytes: x read once, out written once
+    return out
+
+
+# ----------------------------------------------------------------------- tiled harness (tiler.hip)
+def tile_gather_pad(src: torch.Tensor, origins: List[Tuple[int, int]], th: int, tw: int, pad) -> torch.Tensor:
+    """torch.cat of the [1, C, th, tw] views of src [1, C, H, W] at origins (row, column), then
+    F.pad(pad = [left, right, top, bottom], mode="replicate"), in one launch (sa_tile_gather_pad)."""
+    _check(src, "src")
+    _, C, H, W = src.shape
+    pl, pr, pt, pb = pad
+    org = torch.tensor([v for o in origins for v in o], dtype=torch.int32).to(src.device, non_blocking=True)
+    out = torch.empty((len(origins), C, th + pt + pb, tw + pl + pr), device=src.device, dtype=torch.float32)
+    N.call("sa_tile_gather_pad", src.data_ptr(), C, H, W, org.data_ptr(), len(origins), th, tw, pt, pb, pl, pr,
+           out.data_ptr(), _stream(src))
+    org.record_stream(torch.cuda.current_stream(src.device))
+    return out
+
+
+def tile_stitch(disp: torch.Tensor, tiles: List[Tuple[int, int, int]], wgt: torch.Tensor, H: int, W: int,
+                finalize: bool, num: torch.Tensor, den: torch.Tensor) -> None:
+    """The stitching loop of TileWrapper.forward in one launch (sa_tile_stitch): disp [n, 1, th, tw]
+    (a view with any row pitch), tiles = (row, column, slot in disp) in the reference's order."""
+    n, _, th, tw = disp.shape
+    if disp.stride(3) != 1:
+        raise RuntimeError("tile_stitch: disp rows must be contiguous")
+    _check(wgt, "wgt")
+    _check(num, "num")
+    _check(den, "den")
+    tl = torch.tensor([v for t in tiles for v in t], dtype=torch.int32).to(disp.device, non_blocking=True)
+    N.call("sa_tile_stitch", disp.data_ptr(), disp.stride(0), disp.stride(2), tl.data_ptr(), len(tiles), th, tw,
+           wgt.data_ptr(), H, W, 1 if finalize else 0, num.data_ptr(), den.data_ptr(), _stream(disp))
+    tl.record_stream(torch.cuda.current_stream(disp.device))
+
+
 def conv_direct_weights(weight: torch.Tensor, stride: int, with_ds: bool = False,
                         split: Optional[bool] = None) -> torch.Tensor:
     """[Cout, Cin, K, K] -> the direct-conv kernel's chunked layout (sa_conv_direct_weights).

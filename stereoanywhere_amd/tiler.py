@@ -38,6 +38,8 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from . import ops
+
 
 @dataclass(frozen=True)
 class TileSpec:
@@ -136,6 +138,13 @@ def blend_weight(height: int, width: int, device) -> torch.Tensor:
     gy, gx = torch.meshgrid(y, x, indexing="ij")
     w = torch.sin(torch.pi * torch.clamp(gy, 0, 1)) * torch.sin(torch.pi * torch.clamp(gx, 0, 1))
     return torch.clamp(w, min=1e-4)
+
+
+def _hip_tiles(*ts) -> bool:
+    """The GPU gather / stitch (ops.tile_gather_pad / tile_stitch) take float32 CUDA images of batch 1;
+    anything else (CPU tensors: the harness tests' mock models) keeps the torch ops."""
+    return all(t is None or (t.is_cuda and t.dtype == torch.float32 and t.dim() == 4 and t.shape[0] == 1)
+               for t in ts) and ts[0] is not None
 
 
 def guidance_blend(disp: torch.Tensor, guide: torch.Tensor, weight: float) -> torch.Tensor:
@@ -245,7 +254,34 @@ class TileWrapper(torch.nn.Module):
         def view(t, s):
             return None if t is None else t[:, :, s.y_start:s.y_end, s.x_start:s.x_end]
 
-        if self.batch_tiles and mine:
+        hip = _hip_tiles(left, right, mono_left, mono_right) and len({(s.height, s.width) for s in tiles}) == 1
+        if self.batch_tiles and mine and hip:
+            # the batch cut and replicate-padded on the GPU in one launch per tensor (sa_tile_gather_pad:
+            # the torch.cat + F.pad of the branch below, bit for bit)
+            th, tw = mine[0].height, mine[0].width
+            _pad = pad32(th, tw)
+            org = [(s.y_start, s.x_start) for s in mine]
+
+            def gp(t):
+                return None if t is None else ops.tile_gather_pad(t.contiguous(), org, th, tw, _pad)
+            disp = canonicalize(self.model(gp(left), gp(right), gp(mono_left), gp(mono_right), *args, **kw))
+            hd, wd = disp.shape[-2:]
+            outs = disp[..., _pad[2]:hd - _pad[3], _pad[0]:wd - _pad[1]]
+            if guide is None and outs.device == device and outs.shape[-2:] == (th, tw):
+                # the stitching loop below in one launch (sa_tile_stitch), same order, same bits
+                slot = {s: i for i, s in enumerate(mine)}
+                wgt = blend_weight(th, tw, device).contiguous()
+                listed = [(s.y_start, s.x_start, slot[s]) for s in tiles if s in slot]
+                ops.tile_stitch(outs, listed, wgt, H, W, self.world == 1, stitched.view(H, W), weight.view(H, W))
+                if self.world == 1:
+                    return stitched
+                import torch.distributed as dist
+                both = torch.cat([stitched, weight], 1)
+                dist.all_reduce(both)
+                stitched, weight = both[:, :1], both[:, 1:]
+                return torch.where(weight > 0, stitched / torch.clamp(weight, min=1e-4), stitched)
+            outs = list(outs.split(1, 0))
+        elif self.batch_tiles and mine:
             # every tile has the same size (tiles are pushed inside the image), so batch them
             outs = self._run(torch.cat([view(left, s) for s in mine]), torch.cat([view(right, s) for s in mine]),
                              None if mono_left is None else torch.cat([view(mono_left, s) for s in mine]),

@@ -234,10 +234,10 @@ def test_loop_parts_match_one_stream(model, parts, offset):
                                     dict(direct_conv=False), dict(wino4=False),
                                     dict(sheared_producers=False), dict(shear_min_bytes=1 << 62),
                                     dict(fuse_flow_head=False), dict(conv3d_mfma=False),
-                                    dict(fnet_lazy_close=False)])
+                                    dict(fnet_lazy_close=False), dict(direct_small=False), dict(conv1x1=False)])
 def test_schedule_options_vs_reference(change):
     """Every non-default launch schedule (stereoanywhere_amd.model.ScheduleOptions; ops._WINO4,
-    ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE) computes the same forward: cfg1 against the
+    ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE, encoders.DIRECT_SMALL, ops.CONV1X1) computes the same forward: cfg1 against the
     reference's disparity.  (sheared_producers=False: the row-layout producers and the copy pass;
     shear_min_bytes=2^62: the row-layout lookup.)"""
     import dataclasses
@@ -250,15 +250,18 @@ def test_schedule_options_vs_reference(change):
     wino4 = change.pop("wino4", True)
     mf = change.pop("conv3d_mfma", ops.CONV3D_MFMA)
     lazy = change.pop("fnet_lazy_close", encoders.FNET_LAZY_CLOSE)
+    dsmall = change.pop("direct_small", encoders.DIRECT_SMALL)
+    c1 = change.pop("conv1x1", ops.CONV1X1)
     m.opts = dataclasses.replace(m.opts, **change)
     fix = load_fixture("cfg1_256x512_it8.npz")
     pair = regenerate_inputs(fix, 1, 256, 512, 64.0)
-    old = ops._WINO4, ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE
-    ops._WINO4, ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE = wino4, mf, lazy
+    old = ops._WINO4, ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE, encoders.DIRECT_SMALL, ops.CONV1X1
+    ops._WINO4, ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE, encoders.DIRECT_SMALL, ops.CONV1X1 = \
+        wino4, mf, lazy, dsmall, c1
     try:
         disp = run(m, pair, 8)
     finally:
-        ops._WINO4, ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE = old
+        ops._WINO4, ops.CONV3D_MFMA, encoders.FNET_LAZY_CLOSE, encoders.DIRECT_SMALL, ops.CONV1X1 = old
     e = epe(disp, fix["disparity"])
     print(change, "wino4" if wino4 else "no wino4", "EPE", e)
     assert e < 1e-3

@@ -415,6 +415,28 @@ def test_convex_upsample(micro):
     np.testing.assert_allclose(out, micro["up.out"], atol=1e-5)
 
 
+@pytest.mark.parametrize("B,H,W", [(4, 136, 240), (2, 7, 13), (1, 1, 1)])
+def test_convex_upsample_pixel_kernel_bit_exact(B, H, W):
+    """f = 4 runs one thread per low-res pixel (convex_up_px_kernel); the per-output kernel (taken for
+    an output that is not 16-byte aligned, and for f != 4) computes the same operations: equal bit for
+    bit, with the mask a channel slice of a larger buffer (batch stride) and zero padding at borders."""
+    gen = torch.Generator(device="cpu").manual_seed(H * W)
+    flow = (torch.randn(B, 1, H, W, generator=gen) * 5).to(dev)
+    big = (torch.randn(B, 150, H, W, generator=gen) * 3).to(dev)
+    mask = big[:, 3:147]
+    a = torch.empty(B * 16 * H * W + 4, device=dev)
+    b = torch.empty(B * 16 * H * W + 4, device=dev)
+    from stereoanywhere_amd import _native as N
+    for buf, off in ((a, 0), (b, 1)):   # b + 1 float: not 16-byte aligned -> the per-output kernel
+        N.call("sa_convex_upsample", flow.data_ptr(), mask.data_ptr(), mask.stride(0), B, H, W, 4,
+               buf[off:].data_ptr(), 0)
+    torch.cuda.synchronize()
+    n = B * 16 * H * W
+    assert torch.equal(a[:n], b[1:n + 1])
+    ref = ops.convex_upsample(flow, mask, 4).reshape(-1)
+    assert torch.equal(ref, a[:n])
+
+
 @pytest.mark.parametrize("H,W", [(10, 12), (9, 13)])   # float4 and scalar (H*W % 4 != 0) paths
 def test_gru_gates_and_plumbing(H, W):
     rng = np.random.default_rng(9)

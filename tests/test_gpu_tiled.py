@@ -97,3 +97,38 @@ def test_cfg5_harness_booster_preset_with_offload(tmp_path):
     b = data.read_pfm(str(tmp_path / "synthetic0_disp.pfm"))
     assert a.shape == (1792, 2464) and np.isfinite(a).all()
     assert epe(a, b) < 1e-5
+
+
+class _GpuMock(torch.nn.Module):
+    """A deterministic per-tile 'model' on the GPU (negated disparity, position- and size-dependent)."""
+
+    def __init__(self):
+        super().__init__()
+        self.p = torch.nn.Parameter(torch.zeros(1, device="cuda"))
+        self.calls = []
+
+    def forward(self, l, r, ml, mr, iters=1, test_mode=True):
+        self.calls.append(tuple(l.shape))
+        H, W = l.shape[-2:]
+        ramp = torch.arange(W, dtype=torch.float32, device=l.device).view(1, 1, 1, W) / W
+        return -(40 * l[:, :1] - 10 * r[:, 1:2] + ml * 3 - mr + ramp + H / 100.0), None
+
+
+@pytest.mark.parametrize("H,W,th,tw,ov", [(300, 500, 160, 224, 64), (256, 416, 256, 224, 96), (200, 260, 96, 128, 32)])
+def test_tile_gather_and_stitch_equal_torch_path(monkeypatch, H, W, th, tw, ov):
+    """The GPU gather (sa_tile_gather_pad: cat + replicate pad) and stitch (sa_tile_stitch) equal
+    the torch path bit for bit: the padded batch the model sees and the stitched map, including
+    geometries whose enumeration lists a rectangle twice and ragged tiles (non-multiples of 32)."""
+    g = torch.Generator(device="cpu").manual_seed(H + W)
+    imgs = [torch.rand(1, c, H, W, generator=g).cuda() for c in (3, 3, 1, 1)]
+    out = {}
+    seen = {}
+    for hip in (True, False):
+        if not hip:
+            monkeypatch.setattr(tiler, "_hip_tiles", lambda *ts: False)
+        m = _GpuMock()
+        tw_ = tiler.TileWrapper(m, tile_width=tw, tile_height=th, overlap=ov, batch_tiles=True)
+        out[hip] = tw_(*imgs, iters=1, test_mode=True)
+        seen[hip] = m.calls
+    assert seen[True] == seen[False]
+    assert torch.equal(out[True], out[False]), float((out[True] - out[False]).abs().max())
