@@ -33,9 +33,16 @@ def main():
         f3 = torch.randn(B, 256, H, W, generator=g).to(d)
         td = (torch.rand(B, 1, H, W, generator=g) * 60).to(d)
         tc = torch.rand(B, 1, H, W, generator=g).to(d)
-        t = timeit(lambda: ops.corr_volume_pyramid(f2, f3, 4, td, tc, 0.9))
         fl = 2.0 * 256 * B * H * W * W
-        print(f"corr_volume_pyramid B={B} {H}x{W}: {t:7.1f} us  {fl / t / 1e6:6.1f} TF/s  frac {fl / t / 1e-6 / PEAK:.3f}")
+        from stereoanywhere_amd import _native as N
+        for sp in (1, 0):   # split products (the default) / fp32 MFMA products
+            N.lib().sa_corr_set_split(sp)
+            for name, fn in (("row", lambda: ops.corr_volume_pyramid(f2, f3, 4, td, tc, 0.9)),
+                             ("sheared", lambda: ops.corr_volume_pyramid_sheared(f2, f3, 4, td, tc, 0.9))):
+                t = timeit(fn)
+                print(f"corr_volume_pyramid {name:7s} split={sp} B={B} {H}x{W}: {t:7.1f} us  {fl / t / 1e6:6.1f} TF/s  "
+                      f"frac {fl / t / 1e-6 / PEAK:.3f} of the fp32 peak", flush=True)
+        N.lib().sa_corr_set_split(1)
 
 
 if __name__ == "__main__":

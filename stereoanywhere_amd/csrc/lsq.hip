@@ -113,8 +113,8 @@ __device__ __forceinline__ void hist_add(unsigned *h, unsigned bin, bool count) 
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     if (!act) return;
-    const int leader = __ffsll((long long)act) - 1;
-    const unsigned lb = __shfl(bin, leader);
+    const int leader = __ffsll((long long)act) - 1;   // (wave-uniform: a v_readlane, not an LDS round trip)
+    const unsigned lb = (unsigned)__builtin_amdgcn_readlane((int)bin, leader);
     const unsigned long long same = __ballot((act & me) && bin == lb);
     if ((int)(threadIdx.x & 63) == leader) atomicAdd(&h[lb], (unsigned)__popcll(same));
     act &= ~same;
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq1_kernel(const float *__restri
         const int leader = __ffsll((long long)m) - 1;
         unsigned base = 0;
         if (lane == leader) base = atomicAdd(&s_cnt[r], (unsigned)__popcll(m));
-        base = __shfl(base, leader);
+        base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
         if (hit) {
           const unsigned at = s_off[r] + base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
           pool[at] = k;

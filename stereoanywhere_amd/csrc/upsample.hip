@@ -4,11 +4,11 @@
 // mask logits mask[k*f*f + a*f + b] (k = 3x3 neighbour, row-major like F.unfold), then
 // the weighted sum of the zero-padded 3x3 neighbourhood of f*flow.
 //
-// convex_up_px_kernel (round 6, f = 4, the model's factor): one thread per LOW-RES pixel, all 16
-// sub-pixels: each of the 144 mask planes is read by a wave as 64 consecutive floats (whole 256-B
-// runs; one thread per output pixel read each plane in 64-B pieces, 4 planes interleaved, and
-// fetched ~1.3x the mask's bytes), the 3x3 flow neighbourhood once per pixel, and each output row
-// of 4 sub-pixels is one float4 store.  The same operations per output, in the same order:
+// convex_up_px_kernel (round 6, f = 4, the model's factor): one thread per low-res pixel and
+// sub-pixel row a (its 4 sub-pixels): each of the 144 mask planes is read by a wave as 64
+// consecutive floats (whole 256-B runs; one thread per output pixel read each plane in 64-B pieces,
+// 4 planes interleaved, and fetched ~1.3x the mask's bytes), its 36 logits all in flight together,
+// and the 4 outputs are one float4 store.  The same operations per output, in the same order:
 // bit-identical to convex_up_kernel (the other factors' path).
 #include "sa_common.h"
 
@@ -41,11 +41,17 @@ __global__ __launch_bounds__(256) void convex_up_px_kernel(const float *__restri
                                                            const float *__restrict__ mask, long mask_bs, int H,
                                                            int W, long n, float *__restrict__ out) {
   constexpr int f = 4;
+  // thread = (b, a, h, w), w fastest: a wave's lanes read 64 consecutive pixels of each mask plane
+  // and write 64 consecutive float4 of output row 4 h + a
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const long hw = (long)H * W;
-  const long b = i / hw;
-  const int r = (int)(i - b * hw), h = r / W, w = r - h * W;
+  const int w = (int)(i % W);
+  const long q = i / W;
+  const int h = (int)(q % H);
+  const int a = (int)((q / H) % f);
+  const long b = q / ((long)H * f);
+  const int r = h * W + w;
   const float *fl = flow + b * hw;
   float v[9];
 #pragma unroll
@@ -53,24 +59,20 @@ __global__ __launch_bounds__(256) void convex_up_px_kernel(const float *__restri
     const int yy = h + k / 3 - 1, xx = w + k % 3 - 1;
     v[k] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? (float)f * fl[(long)yy * W + xx] : 0.0f;
   }
-  const float *m = mask + b * mask_bs + r;
+  const float *m = mask + b * mask_bs + (long)(a * f) * hw + r;
   const long kstride = (long)f * f * hw;
+  float lg[f][9];
+#pragma unroll
+  for (int c = 0; c < f; ++c)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) lg[c][k] = m[k * kstride + (long)c * hw];
+  float4 o;
+  o.x = convex_px(lg[0], v);
+  o.y = convex_px(lg[1], v);
+  o.z = convex_px(lg[2], v);
+  o.w = convex_px(lg[3], v);
   const int Wo = W * f;
-  float *o = out + b * hw * f * f + (long)(h * f) * Wo + w * f;
-#pragma unroll 1
-  for (int a = 0; a < f; ++a) {
-    float lg[f][9];
-#pragma unroll
-    for (int c = 0; c < f; ++c)
-#pragma unroll
-      for (int k = 0; k < 9; ++k) lg[c][k] = m[k * kstride + (long)(a * f + c) * hw];
-    float4 q;
-    q.x = convex_px(lg[0], v);
-    q.y = convex_px(lg[1], v);
-    q.z = convex_px(lg[2], v);
-    q.w = convex_px(lg[3], v);
-    *reinterpret_cast<float4 *>(o + (long)a * Wo) = q;
-  }
+  *reinterpret_cast<float4 *>(out + b * hw * f * f + (long)(h * f + a) * Wo + w * f) = o;
 }
 
 __global__ __launch_bounds__(256) void convex_up_kernel(const float *__restrict__ flow,
@@ -123,7 +125,7 @@ extern "C" int sa_convex_upsample(const float *flow, const float *mask, long mas
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_UPSAMPLE, s);
   if (factor == 4 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
-    const long np = (long)B * H * W;
+    const long np = (long)B * H * W * 4;
     convex_up_px_kernel<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(flow, mask, mask_bs, H, W, np, out);
     return sa::check_launch("sa_convex_upsample");
   }
