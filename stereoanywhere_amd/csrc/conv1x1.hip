@@ -60,21 +60,13 @@ __global__ __launch_bounds__(C1_THR, 2) void conv1x1_kernel(const float *__restr
 
   // staging: thread tid loads 4 float4 per chunk: channel kk = tid / 32 + 8 i, pixels 4 (tid % 32) .. + 3
   const int sp = (tid & 31) * 4;
+  // (pixels past the plane's end load the plane's last group instead: unpredicated loads all stay in
+  // flight, a load under a branch would be waited for at once; those outputs are never stored)
+  const long pc = min(p0 + sp, P - 4);
   auto load_chunk = [&](int k0, f32x4 (&v)[4]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int kk = (tid >> 5) + 8 * i;
-      const long p = p0 + sp;
-      const float *src = xb + (long)(k0 + kk) * P + p;
-      if (p + 3 < P) {
-        v[i] = *reinterpret_cast<const f32x4 *>(src);
-      } else {
-        f32x4 t = {0.f, 0.f, 0.f, 0.f};
-        for (int e = 0; e < 4; ++e)
-          if (p + e < P) t[e] = src[e];
-        v[i] = t;
-      }
-    }
+    for (int i = 0; i < 4; ++i)
+      v[i] = *reinterpret_cast<const f32x4 *>(xb + (long)(k0 + (tid >> 5) + 8 * i) * P + pc);
   };
   auto stage = [&](const f32x4 (&v)[4]) __attribute__((always_inline)) {
 #pragma unroll
@@ -99,28 +91,24 @@ __global__ __launch_bounds__(C1_THR, 2) void conv1x1_kernel(const float *__restr
     for (int q = 0; q < 2; ++q) acc[c][q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nchunks = Cin / C1_K;
-  f32x4 xv[4];
-  f16x8 wh[4], wl[4];
-  load_chunk(0, xv);
-  load_w(0, wh, wl);
   // B operands: pixel (wave's 32) + 16 q + lane % 16, k = 8 (lane / 16) .. + 7
   const int bp = wv * 32 + (lane & 15), bk = (lane >> 4) * 8;
   bool bad = false;   // an input beyond the f16 range (|x| >= 65504: its hi half is inf)
-#pragma unroll 1
-  for (int kc = 0; kc < nchunks; ++kc) {
+  // two register sets, each chunk's loads issued two chunks ahead: chunk kc + 2's inputs as soon as
+  // chunk kc is staged, its weights once chunk kc's MFMAs have read theirs
+  f32x4 xa[4], xb2[4];
+  f16x8 wha[4], wla[4], whb[4], wlb[4];
+  load_chunk(0, xa);
+  load_w(0, wha, wla);
+  if (nchunks > 1) {
+    load_chunk(C1_K, xb2);
+    load_w(C1_K, whb, wlb);
+  }
+  auto step = [&](int kc, f32x4 (&xv)[4], f16x8 (&wh)[4], f16x8 (&wl)[4]) __attribute__((always_inline)) {
     __syncthreads();   // the previous chunk's B reads are done
     stage(xv);
     __syncthreads();
-    f16x8 wh_c[4], wl_c[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      wh_c[c] = wh[c];
-      wl_c[c] = wl[c];
-    }
-    if (kc + 1 < nchunks) {   // the next chunk's loads, in flight under this chunk's MFMAs
-      load_chunk((kc + 1) * C1_K, xv);
-      load_w((kc + 1) * C1_K, wh, wl);
-    }
+    if (kc + 2 < nchunks) load_chunk((kc + 2) * C1_K, xv);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       float v[8];
@@ -136,11 +124,17 @@ __global__ __launch_bounds__(C1_THR, 2) void conv1x1_kernel(const float *__restr
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        acc[c][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh_c[c], bh, acc[c][q], 0, 0, 0);
-        acc[c][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh_c[c], bl, acc[c][q], 0, 0, 0);
-        acc[c][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl_c[c], bh, acc[c][q], 0, 0, 0);
+        acc[c][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[c], bh, acc[c][q], 0, 0, 0);
+        acc[c][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[c], bl, acc[c][q], 0, 0, 0);
+        acc[c][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[c], bh, acc[c][q], 0, 0, 0);
       }
     }
+    if (kc + 2 < nchunks) load_w((kc + 2) * C1_K, wh, wl);
+  };
+#pragma unroll 1
+  for (int kc = 0; kc < nchunks; kc += 2) {
+    step(kc, xa, wha, wla);
+    if (kc + 1 < nchunks) step(kc + 1, xb2, whb, wlb);
   }
   float *ob = out + (long)b * out_bs;
   // D layout: lane holds rows 4 (lane / 16) .. + 3 (channels), column lane % 16 (pixel)

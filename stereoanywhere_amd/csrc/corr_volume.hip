@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256, (SHEAR ? 3 : 4)) void corr_pyramid_v2_kernel(c
             o[e] = v2_pair(v[e]);
             bad |= !(__builtin_fabsf(v[e]) < 65504.0f);
           }
-          reinterpret_cast<u32x4v *>(pbv)[threadIdx.x + 256 * i] = o;
+          pbv[threadIdx.x + 256 * i] = __builtin_bit_cast(f32x4v, o);   // (one type for the panel: no TBAA split)
         }
         __syncthreads();
       }
@@ -339,7 +339,10 @@ __global__ __launch_bounds__(256, (SHEAR ? 3 : 4)) void corr_pyramid_v2_kernel(c
             if (gg < ngroups) {
 #pragma unroll
               for (int t = 0; t < 4; ++t) {
-                const unsigned bp = __builtin_bit_cast(unsigned, bv[gg][t]);   // B = (hi, lo, hi, lo)
+                // B = (hi, lo, hi, lo).  (The element is copied out first: __builtin_bit_cast of a vector
+                // element lvalue reads element 0 with this compiler.)
+                const float be = bv[gg][t];
+                const unsigned bp = __float_as_uint(be);
                 const f16x4v Bv = __builtin_bit_cast(f16x4v, (u32x4v){bp, bp, 0u, 0u}.xy);
                 acc[gg][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A, Bv, acc[gg][t], 0, 0, 0);
               }

@@ -55,9 +55,10 @@ __global__ __launch_bounds__(256) void convex_up_px_kernel(const float *__restri
   const float *fl = flow + b * hw;
   float v[9];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
+  for (int k = 0; k < 9; ++k) {   // (clamped loads, then the zero padding as a select: no load under a branch)
     const int yy = h + k / 3 - 1, xx = w + k % 3 - 1;
-    v[k] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? (float)f * fl[(long)yy * W + xx] : 0.0f;
+    const float t = fl[(long)min(max(yy, 0), H - 1) * W + min(max(xx, 0), W - 1)];
+    v[k] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? (float)f * t : 0.0f;
   }
   const float *m = mask + b * mask_bs + (long)(a * f) * hw + r;
   const long kstride = (long)f * f * hw;
