@@ -784,8 +784,7 @@ def main():
         secs = ms_tot / 1e3 / args.steps                      # per step
         if unit == "TFLOP/s":
             ach, peak, bound = amount / secs / 1e12, FP32_MFMA_PEAK_TFS, "mfma"
-            split4 = ((k == "conv2d_wino4" and ops.W4_SPLIT) or (k == "conv2d_direct" and ops.DIRECT_SPLIT)
-                      or (k == "corr_volume_pyramid" and int(N.lib().sa_corr_get_split()) == 1))
+            split4 = (k == "conv2d_wino4" and ops.W4_SPLIT) or (k == "conv2d_direct" and ops.DIRECT_SPLIT)
         else:
             ach, peak, bound = amount / secs / 1e9, HBM_PEAK_GBS, "hbm"
             split4 = False
@@ -823,8 +822,7 @@ def main():
                             "ops.DIRECT_SPLIT): achieved = their fp32 products (exact f16 hi/lo pair "
                             "products) against the guide's fp32 matrix peak 157.3 TF/s; split_peak "
                             "(2x, the 16x16x16 f16 form) and the issued f16 flops vs the F16 dense peak "
-                            "are side fields; corr_volume_pyramid likewise (sa_corr_set_split, default on)"
-                            if ops.W4_SPLIT or ops.DIRECT_SPLIT else "")
+                            "are side fields" if ops.W4_SPLIT or ops.DIRECT_SPLIT else "")
 })
     if tiled is None:
         metric, unit = "stereo pairs/sec @540x960 D=192 (1/2/4/8 GPU) + EPE vs reference", "pairs/s"

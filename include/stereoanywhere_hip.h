@@ -265,14 +265,6 @@ int sa_corr_volume_pyramid_sheared(const float *fmap2, const float *fmap3, int B
                                    int W2, float sqrt_c, const float *trunc_disp,
                                    const float *trunc_conf, float atten, int num_levels,
                                    float *sheared, void *stream);
-/* The volume kernel's C contraction (the v2 kernel: C % 16 == 0, W1 and W2 % 4 == 0) on split
- * products (on != 0, the default): both feature values x 2^8 as f16 hi / lo pairs, each product as
- * the four exact f16 products on v_mfma_f32_16x16x16_f16, fp32 accumulation; a block holding a
- * feature of magnitude >= 255.9 recomputes on fp32 MFMA products (sa_corr_redo_blocks counts those
- * blocks since the last reset, synchronising the device).  on == 0: fp32 MFMA products throughout. */
-void sa_corr_set_split(int on);
-int sa_corr_get_split(void);
-long sa_corr_redo_blocks(int reset);
 int sa_corr_pyramid_from_volume_strided_sheared(const float *volume, int B, int H, int W1, int W2,
                                                 long sb, long sh, long sk, int num_levels,
                                                 float *sheared, void *stream);

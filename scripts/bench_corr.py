@@ -34,15 +34,11 @@ def main():
         td = (torch.rand(B, 1, H, W, generator=g) * 60).to(d)
         tc = torch.rand(B, 1, H, W, generator=g).to(d)
         fl = 2.0 * 256 * B * H * W * W
-        from stereoanywhere_amd import _native as N
-        for sp in (1, 0):   # split products (the default) / fp32 MFMA products
-            N.lib().sa_corr_set_split(sp)
-            for name, fn in (("row", lambda: ops.corr_volume_pyramid(f2, f3, 4, td, tc, 0.9)),
-                             ("sheared", lambda: ops.corr_volume_pyramid_sheared(f2, f3, 4, td, tc, 0.9))):
-                t = timeit(fn)
-                print(f"corr_volume_pyramid {name:7s} split={sp} B={B} {H}x{W}: {t:7.1f} us  {fl / t / 1e6:6.1f} TF/s  "
-                      f"frac {fl / t / 1e-6 / PEAK:.3f} of the fp32 peak", flush=True)
-        N.lib().sa_corr_set_split(1)
+        for name, fn in (("row", lambda: ops.corr_volume_pyramid(f2, f3, 4, td, tc, 0.9)),
+                         ("sheared", lambda: ops.corr_volume_pyramid_sheared(f2, f3, 4, td, tc, 0.9))):
+            t = timeit(fn)
+            print(f"corr_volume_pyramid {name:7s} B={B} {H}x{W}: {t:7.1f} us  {fl / t / 1e6:6.1f} TF/s  "
+                  f"frac {fl / t / 1e-6 / PEAK:.3f} of the fp32 peak", flush=True)
 
 
 if __name__ == "__main__":

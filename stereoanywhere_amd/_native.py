@@ -49,9 +49,6 @@ SIGNATURES = {
     "sa_conv1x1_weights": (I, [P, I, I, P, P]),
     "sa_conv1x1": (I, [P, L, I, I, I, I, P, I, P, F, P, L, P]),
     "sa_conv1x1_redo_blocks": (L, [I]),
-    "sa_corr_set_split": (None, [I]),
-    "sa_corr_get_split": (I, []),
-    "sa_corr_redo_blocks": (L, [I]),
     "sa_tile_gather_pad": (I, [P, I, I, I, P, I, I, I, I, I, I, I, P, P]),
     "sa_tile_stitch": (I, [P, L, I, P, I, I, I, P, I, I, I, P, P, P]),
     "sa_last_error": (ctypes.c_char_p, []),

@@ -187,25 +187,6 @@ constexpr int V2_J = 64, V2_K = 256, V2_KC = 16;
 constexpr int V2_ABUF = V2_KC * V2_J, V2_BBUF = V2_KC * V2_K, V2_BUF = V2_ABUF + V2_BBUF;
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x4v __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
-
-// Split products (round 6, g_corr_split): both panels' values x 2^8 as f16 pairs (hi = f16(v),
-// lo = f16(v - hi), v - hi exact in fp32), each channel's product as the four exact f16 products
-// hi hi + hi lo + lo hi + lo lo on v_mfma_f32_16x16x16_f16 (the K = 16 slots of a lane are one
-// channel), fp32 accumulation, the accumulators x 2^-16 after the loop (exact).  The B panel is split
-// in place in LDS once per block (each value once, not once per wave), the A value per lane in
-// registers.  A block with a value of magnitude >= 65504 / 2^8 recomputes on fp32 MFMA.
-constexpr float V2_SPLIT_SCALE = 256.0f;
-int g_corr_split = 1;
-__device__ unsigned g_corr_redo_blocks;
-
-__device__ __forceinline__ unsigned v2_pair(float x) {   // (hi, lo) of x as one dword
-  const f16x2v hh = __builtin_convertvector((f32x4v){x, x, 0.f, 0.f}.xy, f16x2v);
-  const float l = x - (float)hh[0];
-  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x4v){x, l, 0.f, 0.f}.xy, f16x2v));
-}
 
 __device__ __forceinline__ void v2_dma16(__amdgpu_buffer_rsrc_t r, float *lds, int voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)lds, 16, voff, 0, 0, 0);
@@ -244,7 +225,7 @@ __device__ __forceinline__ void sh_write_round(const ShOut &so, float *sl, const
   }
 }
 
-template <bool TRUNC, bool POW2, bool SHEAR = false, bool SPLIT = false>
+template <bool TRUNC, bool POW2, bool SHEAR = false>
 // (the sheared epilogue holds the cells while it stages them: 3 blocks per CU, no spill)
 __global__ __launch_bounds__(256, (SHEAR ? 3 : 4)) void corr_pyramid_v2_kernel(const float *__restrict__ f2, const float *__restrict__ f3,
                                                               Geo g, int jblocks, int kblocks, int kstep, float sqrt_c,
@@ -295,89 +276,33 @@ __global__ __launch_bounds__(256, (SHEAR ? 3 : 4)) void corr_pyramid_v2_kernel(c
   const int ar = (lane >> 4) * V2_J + 16 * w + (lane & 15);   // A[c = lane/16][16 w + lane%16]
   const int br = (lane >> 4) * V2_K + 4 * (lane & 15);         // B[c = lane/16][4 n .. 4 n + 3]
   const bool active = j0 + 16 * w < g.W1;                       // wave-uniform: rows left to compute
-  // the K loop, on split products (split) or fp32 MFMA
-  auto kloop = [&](const bool split) __attribute__((always_inline)) {
-    bool bad = false;
-    issue(0, 0);
+  // (round 6 built split-f16 products for this loop: the B panel split in place in LDS once per block,
+  // the A value per lane, v_mfma_f32_16x16x16_f16 with hi / lo pairs; measured 1.09x SLOWER at cfg2,
+  // 226 vs 208 us row layout, 243 vs 224 us sheared, and 1.25x at the booster batch: the in-place
+  // split pass, its extra barrier per chunk and the B-operand register copies cost more than the
+  // halved MFMA time.  Removed)
+  issue(0, 0);
 #pragma unroll 1
-    for (int kc = 0; kc < nchunks; ++kc) {
-      const int cur = kc & 1;
-      __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
-      if (kc + 1 < nchunks) issue(kc + 1, cur ^ 1);
-      if (SPLIT && split) {   // the B panel's values -> (hi, lo) dwords in place, each once per block
-        f32x4v *pbv = reinterpret_cast<f32x4v *>(smem + cur * V2_BUF + V2_ABUF);
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const int cur = kc & 1;
+    __syncthreads();   // chunk kc landed (vmcnt(0) precedes the barrier); buffer cur ^ 1 is free
+    if (kc + 1 < nchunks) issue(kc + 1, cur ^ 1);
+    if (!active) continue;
+    const float *pa = smem + cur * V2_BUF + ar, *pb = smem + cur * V2_BUF + V2_ABUF + br;
 #pragma unroll
-        for (int i = 0; i < V2_BBUF / 4 / 256; ++i) {
-          const f32x4v v = pbv[threadIdx.x + 256 * i] * V2_SPLIT_SCALE;
-          u32x4v o;
+    for (int s = 0; s < V2_KC / 4; ++s) {
+      const float a = pa[s * 4 * V2_J];
+      f32x4v bv[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            o[e] = v2_pair(v[e]);
-            bad |= !(__builtin_fabsf(v[e]) < 65504.0f);
-          }
-          pbv[threadIdx.x + 256 * i] = __builtin_bit_cast(f32x4v, o);   // (one type for the panel: no TBAA split)
-        }
-        __syncthreads();
-      }
-      if (!active) continue;
-      const float *pa = smem + cur * V2_BUF + ar, *pb = smem + cur * V2_BUF + V2_ABUF + br;
-#pragma unroll
-      for (int s = 0; s < V2_KC / 4; ++s) {
-        const float a = pa[s * 4 * V2_J];
-        f32x4v bv[4];
-#pragma unroll
-        for (int gg = 0; gg < 4; ++gg) bv[gg] = *reinterpret_cast<const f32x4v *>(pb + s * 4 * V2_K + 64 * gg);
-        if (SPLIT && split) {
-          const float as = a * V2_SPLIT_SCALE;
-          bad |= !(__builtin_fabsf(as) < 65504.0f);
-          const unsigned ap = v2_pair(as);   // (hi, lo) -> A = (hi, hi, lo, lo)
-          const f16x4v A = __builtin_bit_cast(
-              f16x4v, (u32x4v){__builtin_amdgcn_perm(ap, ap, 0x01000100u), __builtin_amdgcn_perm(ap, ap, 0x03020302u),
-                               0u, 0u}.xy);
-#pragma unroll
-          for (int gg = 0; gg < 4; ++gg)
-            if (gg < ngroups) {
-#pragma unroll
-              for (int t = 0; t < 4; ++t) {
-                // B = (hi, lo, hi, lo).  (The element is copied out first: __builtin_bit_cast of a vector
-                // element lvalue reads element 0 with this compiler.)
-                const float be = bv[gg][t];
-                const unsigned bp = __float_as_uint(be);
-                const f16x4v Bv = __builtin_bit_cast(f16x4v, (u32x4v){bp, bp, 0u, 0u}.xy);
-                acc[gg][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A, Bv, acc[gg][t], 0, 0, 0);
-              }
-            }
-        } else {
-#pragma unroll
-          for (int gg = 0; gg < 4; ++gg)
-            if (gg < ngroups) {
-#pragma unroll
-              for (int t = 0; t < 4; ++t)
-                acc[gg][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv[gg][t], acc[gg][t], 0, 0, 0);
-            }
-        }
-      }
-    }
-    return bad;
-  };
-  if constexpr (SPLIT) {
-    const bool bad = kloop(true);
-    if (__syncthreads_or(bad)) {   // a value beyond the split range: this block again on fp32 MFMA
-      if (threadIdx.x == 0) atomicAdd(&g_corr_redo_blocks, 1u);
+      for (int gg = 0; gg < 4; ++gg) bv[gg] = *reinterpret_cast<const f32x4v *>(pb + s * 4 * V2_K + 64 * gg);
 #pragma unroll
       for (int gg = 0; gg < 4; ++gg)
+        if (gg < ngroups) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[gg][t] = f32x4v{0.f, 0.f, 0.f, 0.f};
-      kloop(false);
-    } else {
-      constexpr float unscale = 1.0f / (V2_SPLIT_SCALE * V2_SPLIT_SCALE);
-#pragma unroll
-      for (int gg = 0; gg < 4; ++gg)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[gg][t] *= unscale;
+          for (int t = 0; t < 4; ++t)
+            acc[gg][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv[gg][t], acc[gg][t], 0, 0, 0);
+        }
     }
-  } else {
-    kloop(false);
   }
 
   // ---------------------------------------------------------------- epilogue
@@ -758,15 +683,10 @@ int corr_volume_pyramid_impl(const float *fmap2, const float *fmap3, int B, int 
     const unsigned nbu = (unsigned)nb;
     const int a2 = (int)f2_bytes, a3 = (int)f3_bytes;
     const ShOut so = sheared ? make_shout(sheared, W1, W2, num_levels) : ShOut{};
-#define SA_V2S(TR_, P2_, SH_, SP_)                                                                                  \
-  corr_pyramid_v2_kernel<TR_, P2_, SH_, SP_><<<nbu, 256, 0, s>>>(fmap2, fmap3, g, jblocks, kblocks, kstep, sqrt_c, \
-                                                                 inv, TR_ ? trunc_disp : nullptr,                  \
-                                                                 TR_ ? trunc_conf : nullptr, atten, pyramid, a2, a3, so)
-#define SA_V2(TR_, P2_, SH_)   \
-  if (g_corr_split)            \
-    SA_V2S(TR_, P2_, SH_, true); \
-  else                         \
-    SA_V2S(TR_, P2_, SH_, false)
+#define SA_V2(TR_, P2_, SH_)                                                                                        \
+  corr_pyramid_v2_kernel<TR_, P2_, SH_><<<nbu, 256, 0, s>>>(fmap2, fmap3, g, jblocks, kblocks, kstep, sqrt_c, inv, \
+                                                            TR_ ? trunc_disp : nullptr, TR_ ? trunc_conf : nullptr, \
+                                                            atten, pyramid, a2, a3, so)
     if (sheared) {
       if (tr && pow2) SA_V2(true, true, true);
       else if (tr) SA_V2(true, false, true);
@@ -779,7 +699,6 @@ int corr_volume_pyramid_impl(const float *fmap2, const float *fmap3, int B, int 
       else SA_V2(false, false, false);
     }
 #undef SA_V2
-#undef SA_V2S
     return sa::check_launch("sa_corr_volume_pyramid");
   }
   SA_REQUIRE(!sheared, "sa_corr_volume_pyramid_sheared: needs C %% 16 == 0, W1 and W2 %% 4 == 0, 16-byte aligned "
@@ -798,20 +717,6 @@ int corr_volume_pyramid_impl(const float *fmap2, const float *fmap3, int B, int 
   return sa::check_launch("sa_corr_volume_pyramid");
 }
 }  // namespace
-
-// the v2 kernel's split products (1, default) or fp32 MFMA products (0): A/B runs and tests
-extern "C" void sa_corr_set_split(int on) { g_corr_split = on ? 1 : 0; }
-extern "C" int sa_corr_get_split() { return g_corr_split; }
-extern "C" long sa_corr_redo_blocks(int reset) {
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  unsigned v = 0;
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_corr_redo_blocks), sizeof v) != hipSuccess) return -1;
-  if (reset) {
-    const unsigned z = 0;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_corr_redo_blocks), &z, sizeof z) != hipSuccess) return -1;
-  }
-  return v;
-}
 
 extern "C" int sa_corr_volume_pyramid(const float *fmap2, const float *fmap3, int B, int C, int H,
                                       int W1, int W2, float sqrt_c, const float *trunc_disp,

@@ -44,7 +44,7 @@ class ForwardGraph:
         # (an A/B run's older library, SA_HIP_LIB, may lack a getter: its switch reads as None)
         c_switches = tuple(getattr(lib, name)() if hasattr(lib, name) else None
                            for name in ("sa_lookup_get_mfma", "sa_softargmin_get_one_pass", "sa_conv3d_wd_get_variant",
-                                         "sa_conv3d_mf_get_planes", "sa_corr_get_split",
+                                         "sa_conv3d_mf_get_planes",
                                          "sa_lookup_get_shear_dual"))
         return (tuple((tuple(x.shape), x.dtype, x.device) for x in xs), iters, dataclasses.astuple(m.opts),
                 m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_SPLIT, ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS,

@@ -50,51 +50,6 @@ def test_corr_volume_and_pyramid(shape):
         np.testing.assert_allclose(lv, rv, atol=tol)
 
 
-@pytest.mark.parametrize("scale", [1.0, 1e-3, 40.0])
-def test_corr_split_products_vs_fp32(scale):
-    """The v2 volume kernel's split products (sa_corr_set_split(1), the default: features x 2^8 as f16
-    hi / lo pairs on 16x16x16 f16 MFMA) against its fp32-MFMA products: within the split operands'
-    2^-22 relative rounding, at unit, small (lo halves near the f16 subnormals) and large features;
-    no block falls back at these scales."""
-    from stereoanywhere_amd import _native as N
-    B, C, H, W1, W2 = 2, 256, 3, 240, 240
-    rng = np.random.default_rng(7)
-    f2 = g(rng.standard_normal((B, C, H, W1)).astype(np.float32) * scale)
-    f3 = g(rng.standard_normal((B, C, H, W2)).astype(np.float32) * scale)
-    out = {}
-    try:
-        for sp in (0, 1):
-            N.lib().sa_corr_set_split(sp)
-            N.lib().sa_corr_redo_blocks(1)
-            out[sp] = ops.corr_volume_pyramid(g(c(f2)), f3, 4)
-            assert N.lib().sa_corr_redo_blocks(1) == 0
-    finally:
-        N.lib().sa_corr_set_split(1)
-    ref = R.corr_volume(c(f2), c(f3))
-    tol = 4e-6 * np.abs(ref).max()
-    for l1, l0, rv in zip(levels_of(out[1], B, H, W1, W2), levels_of(out[0], B, H, W1, W2), R.corr_pyramid(ref, 4)):
-        np.testing.assert_allclose(l1, l0, atol=tol)   # (the row pitch's pad cells are never written)
-        np.testing.assert_allclose(l1, rv, atol=tol)
-
-
-def test_corr_split_range_guard():
-    """Features beyond the split range (|x| >= 65504 / 2^8) in one image row: that row's blocks
-    recompute on fp32 MFMA (counted), the rest stay split; the result equals the fp32 kernel's."""
-    from stereoanywhere_amd import _native as N
-    B, C, H, W = 1, 256, 4, 240
-    rng = np.random.default_rng(8)
-    f2 = rng.standard_normal((B, C, H, W)).astype(np.float32)
-    f3 = rng.standard_normal((B, C, H, W)).astype(np.float32)
-    f2[:, :, 1] *= 1000.0
-    N.lib().sa_corr_redo_blocks(1)
-    got = ops.corr_volume_pyramid(g(f2), g(f3), 4)
-    redone = int(N.lib().sa_corr_redo_blocks(1))
-    assert 0 < redone < 16   # (4 rows x 4 j blocks; the scaled row's blocks only)
-    ref = R.corr_volume(f2, f3)
-    lv0 = levels_of(got, B, H, W, W)[0]
-    np.testing.assert_allclose(lv0, ref, atol=4e-6 * np.abs(ref).max())
-
-
 def test_corr_volume_matches_reference_vector(micro):
     vol = c(ops.corr_volume(g(micro["corr.f2"]), g(micro["corr.f3"])))
     np.testing.assert_allclose(vol, micro["corr.out"], atol=2e-5)
