@@ -491,9 +491,6 @@ def main():
     ap.add_argument("--direct-small", type=int, default=None, choices=[0, 1],
                     help="the context encoder's small stride-2 stages on the direct kernel (1) or MIOpen (0); "
                          "default: encoders.DIRECT_SMALL")
-    ap.add_argument("--w4-fp32-cin64-px", type=int, default=None,
-                    help="F(4x4) launches with Cin <= 64 above this many output pixels on fp32 products "
-                         "(ops.W4_FP32_CIN64_PX; -1: none)")
     ap.add_argument("--conv1x1", type=int, default=None, choices=[0, 1],
                     help="the 1x1 convs on sa_conv1x1 (1) or F.conv2d / rocBLAS (0); default: ops.CONV1X1")
     ap.add_argument("--split-guard", type=int, default=None, choices=[0, 1],
@@ -571,8 +568,6 @@ def main():
         _E.DIRECT_SMALL = bool(args.direct_small)
     if args.conv1x1 is not None:
         ops.CONV1X1 = bool(args.conv1x1)
-    if args.w4_fp32_cin64_px is not None:
-        ops.W4_FP32_CIN64_PX = None if args.w4_fp32_cin64_px < 0 else args.w4_fp32_cin64_px
 
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
     # SA_DIST_BACKEND=gloo (and SA_DIST_SHARE_GPU=1): a multi-rank rehearsal of this code path on a

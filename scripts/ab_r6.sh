@@ -16,7 +16,6 @@ print(sys.argv[1], round(d["value"], 2), round(d["ms_per_step"], 2), "w4", round
 }
 for pass in 1 2; do
   run default$pass ""
-  run cin64fp32_$pass "--w4-fp32-cin64-px 500000"
   run directsmall0_$pass "--direct-small 0"
   run conv1x1off_$pass "--conv1x1 0"
 done

@@ -48,7 +48,7 @@ class ForwardGraph:
                                          "sa_lookup_get_shear_dual"))
         return (tuple((tuple(x.shape), x.dtype, x.device) for x in xs), iters, dataclasses.astuple(m.opts),
                 m.stream_overlap, m._derived_key, (ops._WINO4, ops.W4_SPLIT, ops.DIRECT_SPLIT, ops._WINO4_MIN_BLOCKS,
-                                                   ops.SPLIT_GUARD, ops.CONV3D_MFMA, ops.CONV1X1, ops.W4_FP32_CIN64_PX,
+                                                   ops.SPLIT_GUARD, ops.CONV3D_MFMA, ops.CONV1X1,
                                                    encoders.FNET_LAZY_CLOSE, encoders.DIRECT_SMALL),
                 c_switches, args)
 

@@ -1045,11 +1045,9 @@ def _gate_epilogue(p: dict) -> "N.SaGateEpilogue":
     return e
 
 
-# launches whose problems all have Cin <= 64 and more than this many output pixels run the fp32-product
-# F(4x4) kernel (None: the split kernel everywhere): fnet.layer1 (8 x 64 -> 64 at 272 x 480) measured
-# 1.03 ms fp32 against 1.13 ms split (8 chunks: the split kernel's longer prologue and epilogue are not
-# amortised), while convc2 (8 x 64 -> 64 at 136 x 240) is faster split (79 vs 94 us)
-W4_FP32_CIN64_PX = None
+# (round 6: fnet.layer1's plain 64 -> 64 shape measured 1.03 ms on the fp32-product kernel against
+# 1.13 ms split, but with its layer-1 launches on fp32 products the forward was slower, 61.0 / 61.3 vs
+# 60.7 ms/step in two interleaved passes: the split kernel stays on every F(4x4) launch)
 
 # the split kernels' f16 range guards (False: no overflow check or recompute: A/B timing only)
 SPLIT_GUARD = True
@@ -1100,10 +1098,7 @@ def conv2d_k3_multi(*problems, small_blocks: bool = False) -> list:
     aff = any(p.get("in_aff") is not None or p.get("in_act") is not None for p in plain)
     if gated and aff:
         raise RuntimeError("conv2d_k3_multi: an input transform and a gate epilogue in one launch")
-    split = (f4 and W4_SPLIT and not small_blocks and all(p["U"].u4s is not None for p in plain)
-             and not (W4_FP32_CIN64_PX is not None and all(
-                 p["x"].shape[1] <= 64 and p["x"].shape[0] * p["x"].shape[2] * p["x"].shape[3] > W4_FP32_CIN64_PX
-                 for p in plain)))
+    split = f4 and W4_SPLIT and not small_blocks and all(p["U"].u4s is not None for p in plain)
     built = [_wino_problem(**p, f4=f4, split=split) for p in plain]
     arr = (N.SaWinoProblem * len(built))(*[b[0] for b in built])
     if f4 and (gated or small_blocks or split):
