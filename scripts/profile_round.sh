@@ -9,6 +9,7 @@
 #   cfg3/4/5   the other configs' bench lines
 #   dist2      a 2-rank torchrun rehearsal of the bench on one GPU (gloo, ranks share the card)
 # Each step under its own limit; a fault or time-out ends the script (gpu_steps.sh).
+# usage: scripts/profile_round.sh [a|b|all]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 R=$(pwd)
 mkdir -p gpurun_out/prof
@@ -25,4 +26,9 @@ exec_steps=(
   "cfg5:420:python3 $R/bench.py --config cfg5 > $R/gpurun_out/prof/cfg5.log 2>&1; tail -n 1 $R/gpurun_out/prof/cfg5.log > $R/gpurun_out/prof/bench_cfg5.json"
   "dist2:300:cd $R && SA_DIST_BACKEND=gloo SA_DIST_SHARE_GPU=1 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --config cfg4 --steps 2 --warmup 1 --no-epe > $R/gpurun_out/prof/dist2.log 2>&1"
 )
-bash "$R/scripts/gpu_steps.sh" "${exec_steps[@]}"
+# part a / b (one gpurun call each: a call is limited to 20 minutes): the first five steps / the rest
+case "${1:-all}" in
+  a) bash "$R/scripts/gpu_steps.sh" "${exec_steps[@]:0:5}" ;;
+  b) bash "$R/scripts/gpu_steps.sh" "${exec_steps[@]:5}" ;;
+  *) bash "$R/scripts/gpu_steps.sh" "${exec_steps[@]}" ;;
+esac
