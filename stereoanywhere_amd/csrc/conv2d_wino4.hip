@@ -42,6 +42,9 @@
                        // 8 neither row nor column pass (no input transform), 9 the loop waits for
                        // chunk kc - 1's DMAs only (the floor of a ring that issues two chunks ahead)
 #endif
+#ifndef SA_W4_PAIR
+#define SA_W4_PAIR 1   // split kernel: a lane's two channels (jobs) in one MFMA pair (w4_pair_split, round 6)
+#endif
 #ifndef SA_W4_GJB
 #define SA_W4_GJB 4    // gate-epilogue store iterations whose plane loads go out together (mode 2)
 #endif
@@ -179,6 +182,25 @@ __device__ __forceinline__ f16x4 w4_split(const float x) {
   asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(__builtin_bit_cast(unsigned, hh)), "v"(x));
   const f16x2 ll = __builtin_convertvector(f32x2{l, l}, f16x2);
   return __builtin_shufflevector(hh, ll, 0, 1, 2, 3);
+}
+
+// The two channels of a lane's jobs (c and c + 4) as the A operands of one MFMA pair (SA_W4_PAIR):
+// ahi = (hi0, hi0, hi1, hi1), alo = (lo0, 0, lo1, 0) against B = (bhi0, blo0, bhi1, blo1), the two
+// channels' filter (hi, lo) dwords of one output channel read straight into a register pair by one
+// ds_read2_b32: ahi . B = hi0 bhi0 + hi0 blo0 + hi1 bhi1 + hi1 blo1, alo . B = lo0 bhi0 + lo1 bhi1,
+// i.e. per channel hi*bhi + hi*blo + lo*bhi (the dropped lo*lo term is below 2^-22 of the product).
+// The B operand needs no register copy (the one-channel form duplicates the (bhi, blo) dword: one
+// v_mov per MFMA, ~1 of the kernel's 5-7 VALU per MFMA) at the same MFMA and LDS instruction counts.
+__device__ __forceinline__ void w4_pair_split(const float x0, const float x1, f16x4 &ahi, f16x4 &alo) {
+  const f16x2 h0 = __builtin_convertvector(f32x2{x0, x0}, f16x2);
+  const f16x2 h1 = __builtin_convertvector(f32x2{x1, x1}, f16x2);
+  float l0, l1;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l0) : "v"(__builtin_bit_cast(unsigned, h0)), "v"(x0));
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l1) : "v"(__builtin_bit_cast(unsigned, h1)), "v"(x1));
+  const f16x2 q0 = __builtin_convertvector(f32x2{l0, 0.0f}, f16x2);
+  const f16x2 q1 = __builtin_convertvector(f32x2{l1, 0.0f}, f16x2);
+  ahi = __builtin_shufflevector(h0, h1, 0, 1, 2, 3);
+  alo = __builtin_shufflevector(q0, q1, 0, 1, 2, 3);
 }
 
 // Range guard of the split kernel: blocks whose f16 operands overflowed (|V| >= 65520 turns hi
@@ -760,6 +782,52 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
 #pragma unroll
       for (int i = 0; i < NR; ++i) b[i] = *reinterpret_cast<const f32xg *>(ub + ((6 * i + 3 * HF + jj) * JPC + s) * SB);
     };
+    if constexpr (SPLIT && SA_W4_PAIR != 0 && JPC == 2 && !AFF) {   // (the affine input variant spills with it)
+      // both jobs' row passes first, then per column both jobs' column passes feed one MFMA pair per
+      // (row, output-channel group) (w4_pair_split); the filter pairs of the next column are read
+      // under the current column's MFMAs
+      float t0[6][3], t1[6][3];
+      load_rows(0, 0, 6);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t0[r]);
+      load_rows(1, 0, 6);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t1[r]);
+      f32x2 pc_[NR][CG];
+      auto load_bp = [&](int jj, f32x2 (&b)[NR][CG]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+#pragma unroll
+          for (int g = 0; g < CG; ++g) {
+            const float *q = ub + (6 * i + 3 * HF + jj) * JPC * SB + g;
+            b[i][g] = f32x2{q[0], q[SB]};   // (job 0's and job 1's channel: one ds_read2_b32)
+          }
+      };
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) {
+        if ((SA_W4_DIAG == 0 || SA_W4_DIAG == 9) && kc + 1 < nchunks) {
+          issue_part(kc + 1, cur ^ 1, jj);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        load_bp(jj, pc_);   // (latency under the two column passes; a next-column prefetch spills)
+        float v0[6], v1[6];
+        bt6(t0[0][jj], t0[1][jj], t0[2][jj], t0[3][jj], t0[4][jj], t0[5][jj], v0);
+        bt6(t1[0][jj], t1[1][jj], t1[2][jj], t1[3][jj], t1[4][jj], t1[5][jj], v1);
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          f16x4 ahi, alo;
+          w4_pair_split(v0[i], v1[i], ahi, alo);
+#pragma unroll
+          for (int g = 0; g < CG; ++g) {
+            const f16x4 bp = __builtin_bit_cast(f16x4, pc_[i][g]);
+            acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x16f16(ahi, bp, acc[i][jj][g], 0, 0, 0);
+            acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x16f16(alo, bp, acc[i][jj][g], 0, 0, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);   // bound the scheduler's hoisting (register pressure)
+      }
+      continue;
+    }
     load_rows(0, 0, 6);
     load_b(0, 0, bc);
 #pragma unroll
