@@ -671,7 +671,7 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
   int PSv = PS, PGv = PG;
   asm volatile("" : "+s"(PSv), "+s"(PGv));
   const int pread = k * PSv * 4 + 4 * trow * PGv * 4 + 4 * tcol + 2;
-  const int uread = (k * 16 + m) * CG;
+  const int uread = (k * 16 + m) * CG * (SPLIT ? JPC : 1);   // (split: [k][n][g][job], wino4s_weights_kernel)
 
   // acc[i][jj][g]: point (row i, column 3 HF + jj) of output-channel group g
   f32x4 acc[NR][3][CG];
@@ -780,12 +780,19 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
     f32xg bc[NR], bn[NR];
     auto load_b = [&](int s, int jj, f32xg *b) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < NR; ++i) b[i] = *reinterpret_cast<const f32xg *>(ub + ((6 * i + 3 * HF + jj) * JPC + s) * SB);
+      for (int i = 0; i < NR; ++i) {
+        if constexpr (SPLIT) {   // (the job's dwords of both groups: one ds_read2_b32)
+          const float *q = ub + (6 * i + 3 * HF + jj) * JPC * SB + s;
+          b[i] = f32xg{q[0], q[JPC]};
+        } else {
+          b[i] = *reinterpret_cast<const f32xg *>(ub + ((6 * i + 3 * HF + jj) * JPC + s) * SB);
+        }
+      }
     };
     if constexpr (SPLIT && SA_W4_PAIR != 0 && JPC == 2 && !AFF) {   // (the affine input variant spills with it)
       // both jobs' row passes first, then per column both jobs' column passes feed one MFMA pair per
-      // (row, output-channel group) (w4_pair_split); the filter pairs of the next column are read
-      // under the current column's MFMAs
+      // (row, output-channel group) (w4_pair_split); a column's filter operands are read under its
+      // two column passes
       float t0[6][3], t1[6][3];
       load_rows(0, 0, 6);
 #pragma unroll
@@ -793,15 +800,10 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
       load_rows(1, 0, 6);
 #pragma unroll
       for (int r = 0; r < 6; ++r) bt6h<HF>(ra[r].y, rb[r].x, rb[r].y, rb[r].z, rb[r].w, rc[r].x, t1[r]);
-      f32x2 pc_[NR][CG];
-      auto load_bp = [&](int jj, f32x2 (&b)[NR][CG]) __attribute__((always_inline)) {
+      f32x4 pc_[NR];   // (group 0: job 0, job 1; group 1: job 0, job 1)
+      auto load_bp = [&](int jj, int i0, int i1, f32x4 (&b)[NR]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < NR; ++i)
-#pragma unroll
-          for (int g = 0; g < CG; ++g) {
-            const float *q = ub + (6 * i + 3 * HF + jj) * JPC * SB + g;
-            b[i][g] = f32x2{q[0], q[SB]};   // (job 0's and job 1's channel: one ds_read2_b32)
-          }
+        for (int i = i0; i < i1; ++i) b[i] = *reinterpret_cast<const f32x4 *>(ub + (6 * i + 3 * HF + jj) * JPC * SB);
       };
 #pragma unroll
       for (int jj = 0; jj < 3; ++jj) {
@@ -809,17 +811,19 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
           issue_part(kc + 1, cur ^ 1, jj);
           __builtin_amdgcn_sched_barrier(0);
         }
-        load_bp(jj, pc_);   // (latency under the two column passes; a next-column prefetch spills)
+        load_bp(jj, 0, NR / 2, pc_);   // (rows 0-2 under the column passes, 3-5 under rows 0-2's MFMAs:
+                                       // a whole column at once, or the next column's, spills)
         float v0[6], v1[6];
         bt6(t0[0][jj], t0[1][jj], t0[2][jj], t0[3][jj], t0[4][jj], t0[5][jj], v0);
         bt6(t1[0][jj], t1[1][jj], t1[2][jj], t1[3][jj], t1[4][jj], t1[5][jj], v1);
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
+          if (i == 1) load_bp(jj, NR / 2, NR, pc_);
           f16x4 ahi, alo;
           w4_pair_split(v0[i], v1[i], ahi, alo);
 #pragma unroll
           for (int g = 0; g < CG; ++g) {
-            const f16x4 bp = __builtin_bit_cast(f16x4, pc_[i][g]);
+            const f16x4 bp = __builtin_bit_cast(f16x4, g == 0 ? pc_[i].xy : pc_[i].zw);
             acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x16f16(ahi, bp, acc[i][jj][g], 0, 0, 0);
             acc[i][jj][g] = __builtin_amdgcn_mfma_f32_16x16x16f16(alo, bp, acc[i][jj][g], 0, 0, 0);
           }
@@ -1088,8 +1092,9 @@ __global__ __launch_bounds__(256) void wino4_weights_kernel(const float *__restr
 }
 
 // Filters of the split kernel (W4Split): U = G g G^T in fp64, times 2^W4S_LOG2, as the f16
-// pair hi = f16(u), lo = f16(u - hi) in one dword (hi in the low half), in the fp32 filters'
-// layout (wino4_weights_kernel).
+// pair hi = f16(u), lo = f16(u - hi) in one dword (hi in the low half); per (32-channel block,
+// 8-channel chunk, point) [k][n][g][job]: a lane's four operands of a point (both groups, both
+// jobs' channels k and k + 4) are one 16-byte LDS read, the MFMA pairs' B operands as they stand.
 __global__ __launch_bounds__(256) void wino4s_weights_kernel(const float *__restrict__ w, int Cout, int Cin,
                                                              unsigned *__restrict__ U) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1114,7 +1119,7 @@ __global__ __launch_bounds__(256) void wino4s_weights_kernel(const float *__rest
       const unsigned pr = (unsigned)__builtin_bit_cast(unsigned short, hi) |
                           ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
       const int pt = 6 * a + b;
-      U[(((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 2 + s) * 4 + k) * 32 + n * 2 + gg] = pr;
+      U[((((((long)cb * (Cin / 8) + chunk) * NPT + pt) * 4 + k) * 16 + n) * 2 + gg) * 2 + s] = pr;
     }
 }
 
