@@ -45,6 +45,12 @@
 #ifndef SA_W4_PAIR
 #define SA_W4_PAIR 1   // split kernel: a lane's two channels (jobs) in one MFMA pair (w4_pair_split, round 6)
 #endif
+#ifndef SA_W4_PAIR_AFF
+// the affine-input split kernel on the paired loop too: it spills 28 B per lane (loop-invariant values
+// around the main loop, one reload per chunk in the affine pass) and is still faster: forward
+// 58.7 -> 58.1 ms/step, two interleaved passes (profiles/ab/r06_w4_pair_ab.txt)
+#define SA_W4_PAIR_AFF 1
+#endif
 #ifndef SA_W4_GJB
 #define SA_W4_GJB 4    // gate-epilogue store iterations whose plane loads go out together (mode 2)
 #endif
@@ -585,7 +591,10 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
   }
   const int npi = (KC * PS + 63) >> 6;
   int po[PDMA];
-  int pc[PDMA];   // input transform: the group's channel in the chunk (-1: padding or idle lane)
+  // input transform: per piece j, 4 bits at 4j = the group's channel in the chunk + 1 (0: padding
+  // or an idle lane), one register for all pieces
+  unsigned pcs = 0;
+  static_assert(PDMA <= 8 && KC < 15, "4-bit channel fields");
 #pragma unroll
   for (int j = 0; j < PDMA; ++j) {
     const int s = (wv + NWAVE * j) * 64 + lane;
@@ -594,7 +603,7 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
     // (a pitched plane's columns W .. pitch - 1 are zero: they load as the right padding)
     const bool ok = s < KC * PS && y >= 0 && y < H && x >= 0 && x < pitch;
     po[j] = ok ? (ci * hw + y * pitch + x) * 4 : 0x7ffffff0;   // out of range: the load returns 0
-    pc[j] = ok && wv + NWAVE * j < (KC * PS + 63) / 64 ? ci : -1;
+    pcs |= (ok && wv + NWAVE * j < (KC * PS + 63) / 64 ? (unsigned)ci + 1u : 0u) << (4 * j);
   }
   if constexpr (C::SPLIT) {
     if (xscale == 0.0f) {   // the range guard's second pass: the scale from the block's largest input
@@ -607,11 +616,12 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
       for (int kc = 0; kc < nchunks; ++kc)
 #pragma unroll
         for (int j = 0; j < PDMA; ++j) {
-          if (pc[j] < 0) continue;
+          const int pcj = (int)((pcs >> (4 * j)) & 15u) - 1;
+          if (pcj < 0) continue;
           const f32x4 v = *reinterpret_cast<const f32x4 *>(ib + po[j] + (long)kc * KC * hw * 4);
           float a = 1.0f, b = 0.0f, fl = -INFINITY;
           if constexpr (AFF) {
-            const int pi = n * P.in_pstride + kc * KC + pc[j];
+            const int pi = n * P.in_pstride + kc * KC + pcj;
             const float m0 = P.in_m ? P.in_m[pi] : 0.0f, t0 = P.in_t ? P.in_t[pi] : 0.0f;
             a = P.in_s ? P.in_s[pi] : 1.0f;
             b = t0 - m0 * a;
@@ -716,9 +726,10 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
       float *pbuf = smem + cur * BUF;
 #pragma unroll
       for (int j = 0; j < PDMA; ++j) {
-        if (pc[j] >= 0) {
+        const int pcj = (int)((pcs >> (4 * j)) & 15u) - 1;
+        if (pcj >= 0) {
           f32x4 *q = reinterpret_cast<f32x4 *>(pbuf + ((wv + NWAVE * j) * 64 + lane) * 4);
-          const float2 ab = atab[kc * KC + pc[j]];
+          const float2 ab = atab[kc * KC + pcj];
           f32x4 v = *q;
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] * ab.x + ab.y, act_floor);
@@ -789,7 +800,7 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
         }
       }
     };
-    if constexpr (SPLIT && SA_W4_PAIR != 0 && JPC == 2 && !AFF) {   // (the affine input variant spills with it)
+    if constexpr (SPLIT && SA_W4_PAIR != 0 && JPC == 2 && (!AFF || SA_W4_PAIR_AFF)) {
       // both jobs' row passes first, then per column both jobs' column passes feed one MFMA pair per
       // (row, output-channel group) (w4_pair_split); a column's filter operands are read under its
       // two column passes

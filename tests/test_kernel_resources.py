@@ -42,4 +42,8 @@ def test_conv_kernels_do_not_spill(tmp_path, name, kernel, extra):
     usage, _ = _compile(name, tmp_path, extra)
     hot = {k: v for k, v in usage.items() if kernel in k}
     assert hot, sorted(usage)
-    assert all(v == 0 for v in hot.values()), hot
+    # the one measured exception: the split F(4x4) kernel with the affine input on the paired loop
+    # (SA_W4_PAIR_AFF) spills a few loop-invariant values and is faster than without (A/B in
+    # profiles/ab/r06_w4_pair_ab.txt); bounded, so a real regression still fails
+    allowed = {k: 32 for k in hot if "W4CfgILi8ELi8ELb1EEELb0ELb1E" in k}
+    assert all(v <= allowed.get(k, 0) for k, v in hot.items()), hot
