@@ -33,6 +33,11 @@ FAMILIES = {
     "conv3d_mf_kernel": "conv3d_fused",
     # the sheared layout's producers and the block-spread lookup
     "lookup_c1_shear_lds_kernel": "corr_lookup", "pyramid_from_strided_sheared_kernel": "mono_pyramid",
+    # round 6: the one-launch LSQ, the pixel-per-thread convex upsampling, the split 1x1 GEMM, the
+    # stride-2 3-D MFMA conv, the tiler's gather / stitch
+    "lsq1_kernel": "weighted_lsq", "convex_up_px_kernel": "convex_upsample", "conv1x1_kernel": "conv1x1",
+    "conv1x1_weights_kernel": "conv1x1", "conv3d_s2mf_kernel": "conv3d_fused",
+    "tile_gather_pad_kernel": "misc", "tile_stitch_kernel": "misc",
 }
 
 

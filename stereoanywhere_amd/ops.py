@@ -367,9 +367,9 @@ def softlrc_joint(disp: torch.Tensor, conf: Optional[torch.Tensor], lrc_th: floa
 def weighted_lsq(mde: torch.Tensor, disp: torch.Tensor, conf: torch.Tensor, q_lo: float = 0.2,
                  q_hi: float = 0.9, single_block: Optional[bool] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Per-sample (scale, shift) [B] of weighted_lsq over the flattened [B, ...] maps.
-    Spread over the GPU (sa_weighted_lsq_ws) or one workgroup per sample (single_block);
-    by default the former for up to 16 samples (B=4 at 2x136x240: 84 vs 156 us), the latter
-    above (B=64: 182 vs 709 us, where the global histogram atomics contend)."""
+    One launch, one workgroup per sample (sa_weighted_lsq, the default since round 6: B=4 at
+    2x136x240 73-77 vs ~100 us for the five-launch grid form, B=64 76 vs 714 us), or spread over
+    the GPU with a zeroed workspace (sa_weighted_lsq_ws, single_block=False)."""
     for t, nm in ((mde, "mde"), (disp, "disp"), (conf, "conf")):
         _check(t, nm)
     B = mde.shape[0]
@@ -377,7 +377,7 @@ def weighted_lsq(mde: torch.Tensor, disp: torch.Tensor, conf: torch.Tensor, q_lo
     scale = torch.empty(B, device=mde.device, dtype=torch.float32)
     shift = torch.empty(B, device=mde.device, dtype=torch.float32)
     if single_block is None:
-        single_block = B > 16
+        single_block = True
     if single_block:
         N.call("sa_weighted_lsq", mde.data_ptr(), disp.data_ptr(), conf.data_ptr(), B, n, q_lo, q_hi,
                scale.data_ptr(), shift.data_ptr(), _stream(mde))
