@@ -192,8 +192,9 @@ __device__ __forceinline__ f16x4 w4_split(const float x) {
 
 // The two channels of a lane's jobs (c and c + 4) as the A operands of one MFMA pair (SA_W4_PAIR):
 // ahi = (hi0, hi0, hi1, hi1), alo = (lo0, 0, lo1, 0) against B = (bhi0, blo0, bhi1, blo1), the two
-// channels' filter (hi, lo) dwords of one output channel read straight into a register pair by one
-// ds_read2_b32: ahi . B = hi0 bhi0 + hi0 blo0 + hi1 bhi1 + hi1 blo1, alo . B = lo0 bhi0 + lo1 bhi1,
+// channels' filter (hi, lo) dwords of one output channel, adjacent in the job-innermost LDS image
+// (one ds_read_b128 per point holds both groups' pairs): ahi . B = hi0 bhi0 + hi0 blo0 + hi1 bhi1 +
+// hi1 blo1, alo . B = lo0 bhi0 + lo1 bhi1,
 // i.e. per channel hi*bhi + hi*blo + lo*bhi (the dropped lo*lo term is below 2^-22 of the product).
 // The B operand needs no register copy (the one-channel form duplicates the (bhi, blo) dword: one
 // v_mov per MFMA, ~1 of the kernel's 5-7 VALU per MFMA) at the same MFMA and LDS instruction counts.

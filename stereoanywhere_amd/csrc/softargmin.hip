@@ -290,15 +290,21 @@ __global__ __launch_bounds__(1024) void sam_slice_kernel(const float *__restrict
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const long ob = (long)b * g.obs + (long)h * n;
   float x[NR][NC];
+  // unconditional loads of clamped cells, all issued before any arithmetic; the cells outside the
+  // slice become -inf only where they are first used (a load under the (k < n && j < n) predicate
+  // compiled to a branch around each load; a select right after the load, to a branch on the
+  // wave-uniform k < n with an immediate vmcnt(0) per load)
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
+    const int kc = min(w + 16 * r, n - 1);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[r][c] = src[(long)kc * g.sk + min(lane + 64 * c, n - 1)];
+  }
+  auto mask_row = [&](int r) __attribute__((always_inline)) {
     const int k = w + 16 * r;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int j = lane + 64 * c;
-      x[r][c] = (k < n && j < n) ? src[(long)k * g.sk + j] : -INFINITY;
-    }
-  }
+    for (int c = 0; c < NC; ++c) x[r][c] = (k < n && lane + 64 * c < n) ? x[r][c] : -INFINITY;
+  };
   // ---- right: per row k, softmax over j (estimate_right_*, utils.py:132-152, 162-170).  Rows in
   // groups of RG: each group's max / sum / accumulate reductions run as RG interleaved DPP chains
   // (one row at a time, the wave waited on one chain's latency after another: round 6, 4 rows per
@@ -308,6 +314,8 @@ __global__ __launch_bounds__(1024) void sam_slice_kernel(const float *__restrict
 #pragma unroll
   for (int r0 = 0; r0 < NR; r0 += RG) {
     if (w + 16 * r0 >= n) continue;   // wave-uniform (rows k >= n of a group: all -inf, unused)
+#pragma unroll
+    for (int u = 0; u < RG; ++u) mask_row(r0 + u);
     float m[RG];
 #pragma unroll
     for (int u = 0; u < RG; ++u) {
@@ -362,6 +370,9 @@ __global__ __launch_bounds__(1024) void sam_slice_kernel(const float *__restrict
     for (int c = 0; c < NC; ++c) part[c] = colv[lane + 64 * c < n ? lane + 64 * c : 0];
     __syncthreads();   // red / colv are reused by the next total
   };
+  // (the rows of the groups the right side skipped: masked here; the others again, a no-op)
+#pragma unroll
+  for (int r = 0; r < NR; ++r) mask_row(r);
   float q[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -541,6 +552,7 @@ bool launch_slices(const float *vd, const float *vc, const SGeo &g, int B, int n
   }
   SA_SLICE(8, 2)
   SA_SLICE(12, 3)
+  SA_SLICE(15, 4)   // (n = 240, the model's 1/4 width: no all-padding row per thread)
   SA_SLICE(16, 4)
   SA_SLICE(18, 5)
 #undef SA_SLICE
