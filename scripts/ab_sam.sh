@@ -5,17 +5,13 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
 mkdir -p gpurun_out/sam
 V=${1:-variants/samhead.so}
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_ops.py -k "softargmin or sam" \
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_ops.py tests/test_gpu_model.py -k "softargmin or sam or forward or epe or reference" \
   > gpurun_out/sam/tests.log 2>&1 || exit 1
 for pass in 1 2; do
-  echo "== in-tree $pass" >> gpurun_out/sam/bench.txt
-  timeout -k 10 120 python scripts/bench_sam.py >> gpurun_out/sam/bench.txt 2>&1 || exit 1
-  echo "== $V $pass" >> gpurun_out/sam/bench.txt
-  SA_HIP_LIB=$V timeout -k 10 120 python scripts/bench_sam.py >> gpurun_out/sam/bench.txt 2>&1 || exit 1
+  for shape in "4 136 240" "25 224 280"; do
+    echo "== in-tree $pass $shape" >> gpurun_out/sam/bench.txt
+    timeout -k 10 120 python scripts/bench_sam.py $shape >> gpurun_out/sam/bench.txt 2>&1 || exit 1
+    echo "== $V $pass $shape" >> gpurun_out/sam/bench.txt
+    SA_HIP_LIB=$V timeout -k 10 120 python scripts/bench_sam.py $shape >> gpurun_out/sam/bench.txt 2>&1 || exit 1
+  done
 done
-# the F(4x4) prologue with kernel arguments in device memory (first DMA ~2.8k cycles after start)
-if [ -f variants/clock.so ]; then
-  SA_HIP_LIB=variants/clock.so timeout -k 10 120 python scripts/w4_clock.py 4 128 128 136 240 > gpurun_out/sam/kernarg.txt 2>&1 || exit 1
-  HIP_FORCE_DEV_KERNARG=1 SA_HIP_LIB=variants/clock.so timeout -k 10 120 python scripts/w4_clock.py 4 128 128 136 240 >> gpurun_out/sam/kernarg.txt 2>&1 || exit 1
-  HIP_FORCE_DEV_KERNARG=0 SA_HIP_LIB=variants/clock.so timeout -k 10 120 python scripts/w4_clock.py 4 128 128 136 240 >> gpurun_out/sam/kernarg.txt 2>&1 || exit 1
-fi

@@ -120,6 +120,36 @@ __device__ __forceinline__ void wave_sum_dpp_n(float (&v)[N]) {
 #pragma unroll
   for (int i = 0; i < N; ++i) v[i] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v[i]), 63));
 }
+// Butterfly forms (gfx950): the four in-row DPP steps as above (every lane valid, so each folds into
+// the operation's DPP source), then v_permlane16_swap and v_permlane32_swap: each exchanges half
+// of the lanes between two copies of the value, so one operation on the pair completes the next
+// level and the total ends up in every lane (no row_bcast masks, identity moves or v_readlane).
+// A different addition order than wave_sum_dpp (not the same bits).
+template <int CTRL>
+__device__ __forceinline__ float dpp_all(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+template <bool MAX>
+__device__ __forceinline__ float bfly_op(float a, float b) { return MAX ? fmaxf(a, b) : a + b; }
+template <bool MAX, int N>
+__device__ __forceinline__ void wave_reduce_bfly_n(float (&v)[N]) {
+#define SA_BF_STEP(CTRL) _Pragma("unroll") for (int i = 0; i < N; ++i) v[i] = bfly_op<MAX>(v[i], dpp_all<CTRL>(v[i]));
+  SA_BF_STEP(0xB1) SA_BF_STEP(0x4E) SA_BF_STEP(0x141) SA_BF_STEP(0x140)
+#undef SA_BF_STEP
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const unsigned u = __builtin_bit_cast(unsigned, v[i]);
+    const auto p = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    v[i] = bfly_op<MAX>(__builtin_bit_cast(float, (unsigned)p[0]), __builtin_bit_cast(float, (unsigned)p[1]));
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const unsigned u = __builtin_bit_cast(unsigned, v[i]);
+    const auto p = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    v[i] = bfly_op<MAX>(__builtin_bit_cast(float, (unsigned)p[0]), __builtin_bit_cast(float, (unsigned)p[1]));
+  }
+}
+
 // fp64 sum; the total is in lane 63 only
 __device__ __forceinline__ double wave_sum_dpp_lane63(double v) {
   v += dpp_f64<0xB1>(v);

@@ -267,6 +267,11 @@ __global__ __launch_bounds__(256) void sam_strided_kernel(LineJob jd, LineJob jc
 // VALU-bound, not HBM-bound, with the library versions.
 __device__ __forceinline__ float exp_le0(float d) { return __builtin_amdgcn_exp2f(d * 1.44269504088896341f); }
 __device__ __forceinline__ float log2_pos(float y) { return __builtin_amdgcn_logf(y); }
+// exp(x - m) as exp2(x log2e - m log2e) with the row's m log2e formed once (one FMA per cell
+// instead of a subtract and a multiply; the rounding of m log2e is a common factor of the row,
+// which the normalisation removes)
+constexpr float SAM_L2E = 1.44269504088896341f;
+__device__ __forceinline__ float exp_shift(float x, float ml2e) { return __builtin_amdgcn_exp2f(fmaf(x, SAM_L2E, -ml2e)); }
 
 // One pass over each (b, h) slice: both reductions of a volume from one read.  A block of 1024
 // threads holds the slice's n x n cells in registers, element (k, j) at wave k % 16, slot
@@ -275,35 +280,36 @@ __device__ __forceinline__ float log2_pos(float y) { return __builtin_amdgcn_log
 // (softmax over k, per j) combines the 16 waves' column partials through LDS.  blockIdx.y
 // picks the volume (0: disparity, 1: confidence).  The two launches of the line kernels above
 // each read both volumes; this reads each once.
-template <int NR, int NC>
-__global__ __launch_bounds__(1024) void sam_slice_kernel(const float *__restrict__ vd, const float *__restrict__ vc,
-                                                         SGeo g, int n, float *dL, float *dR, float *cL, float *cR,
-                                                         int y0) {
-  __shared__ float red[16][NC * 64];
-  __shared__ float colv[NC * 64];
-  const int conf = y0 + (int)blockIdx.y;
-  const float *vol = conf ? vc : vd;
-  float *outL = conf ? cL : dL, *outR = conf ? cR : dR;
-  const int bh = blockIdx.x, b = bh / g.H, h = bh % g.H;
-  const float *src = vol + (long)b * g.sb + (long)h * g.sh;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const long ob = (long)b * g.obs + (long)h * n;
-  float x[NR][NC];
-  // unconditional loads of clamped cells, all issued before any arithmetic; the cells outside the
-  // slice become -inf only where they are first used (a load under the (k < n && j < n) predicate
-  // compiled to a branch around each load; a select right after the load, to a branch on the
-  // wave-uniform k < n with an immediate vmcnt(0) per load)
-#pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const int kc = min(w + 16 * r, n - 1);
-#pragma unroll
-    for (int c = 0; c < NC; ++c) x[r][c] = src[(long)kc * g.sk + min(lane + 64 * c, n - 1)];
-  }
+// A workgroup barrier for LDS exchanges only: the LDS operations complete, then s_barrier (a
+// __syncthreads also waits for every outstanding global load, here the prefetch kernel's DMAs
+// of the next slice)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// The reductions of one slice held in registers (x: cell (k, j) at row slot r = (k - w) / 16,
+// column slot c = (j - lane) / 64; cells outside the slice are masked here): the right side per row
+// within a wave, the left side per column through the 16 waves' LDS partials (red, colv).  CONF:
+// the confidence volume (entropy terms) or the disparity volume (index-weighted sums), a template
+// argument so neither volume's blocks evaluate the other's terms (with a run-time flag the
+// compiler formed both and selected: the log2 of every cell on the disparity volume too).
+// RT: the kind from the run-time flag rconf instead (one body for both volumes: the 18 x 5 slot
+// instance, whose two bodies would spill past its 128 VGPRs)
+template <int NR, int NC, bool CONF, bool RT = false>
+__device__ __forceinline__ void slice_reduce(float (&x)[NR][NC], float (&red)[16][NC * 64], float (&colv)[NC * 64],
+                                             const int n, const SGeo &g, float *outL, float *outR,
+                                             const long ob, const int w, const int lane, const int tid,
+                                             const bool rconf = false) {
+  const bool conf = RT ? rconf : CONF;
+  // cells outside the slice -> -inf; only the column slots that can reach past n and the rows past
+  // it (both wave-uniform tests) take the select
   auto mask_row = [&](int r) __attribute__((always_inline)) {
     const int k = w + 16 * r;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) x[r][c] = (k < n && lane + 64 * c < n) ? x[r][c] : -INFINITY;
+    for (int c = 0; c < NC; ++c)
+      if (k >= n || 64 * c + 63 >= n) x[r][c] = (k < n && lane + 64 * c < n) ? x[r][c] : -INFINITY;
   };
   // ---- right: per row k, softmax over j (estimate_right_*, utils.py:132-152, 162-170).  Rows in
   // groups of RG: each group's max / sum / accumulate reductions run as RG interleaved DPP chains
@@ -323,31 +329,33 @@ __global__ __launch_bounds__(1024) void sam_slice_kernel(const float *__restrict
 #pragma unroll
       for (int c = 1; c < NC; ++c) m[u] = fmaxf(m[u], x[r0 + u][c]);
     }
-    sa::wave_max_dpp_n(m);
+    sa::wave_reduce_bfly_n<true>(m);
     float e[RG][NC], se[RG];
 #pragma unroll
     for (int u = 0; u < RG; ++u) {
       se[u] = 0.f;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        e[u][c] = exp_le0(x[r0 + u][c] - m[u]);   // -inf (j >= n) -> 0
+        e[u][c] = exp_shift(x[r0 + u][c], m[u] * SAM_L2E);   // -inf (j >= n) -> 0
         se[u] += e[u][c];
       }
     }
-    sa::wave_sum_dpp_n(se);
+    sa::wave_reduce_bfly_n<false>(se);
     float acc[RG];
 #pragma unroll
     for (int u = 0; u < RG; ++u) {
-      const float inv = 1.0f / se[u];
+      const float inv = __builtin_amdgcn_rcpf(se[u]);   // (v_rcp_f32, 1 ulp; the IEEE division's 10 VALU)
       acc[u] = 0.f;
+      // (no j < n test: a masked cell has e = 0, so p = 0 and the term is an exact 0, log2 of
+      // 1e-6 being finite)
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int j = lane + 64 * c;
         const float p = e[u][c] * inv;
-        if (j < n) acc[u] += conf ? p * log2_pos(p + 1e-6f) : p * (float)j;
+        acc[u] = fmaf(p, conf ? log2_pos(p + 1e-6f) : (float)j, acc[u]);
       }
     }
-    sa::wave_sum_dpp_n(acc);
+    sa::wave_reduce_bfly_n<false>(acc);
 #pragma unroll
     for (int u = 0; u < RG; ++u) {
       const int k = w + 16 * (r0 + u);
@@ -358,21 +366,25 @@ __global__ __launch_bounds__(1024) void sam_slice_kernel(const float *__restrict
   auto column_total = [&](float *part, bool is_max) __attribute__((always_inline)) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) red[w][lane + 64 * c] = part[c];
-    __syncthreads();
+    lds_barrier();
     if (tid < n) {
       float t = red[0][tid];
 #pragma unroll
       for (int i = 1; i < 16; ++i) t = is_max ? fmaxf(t, red[i][tid]) : t + red[i][tid];
       colv[tid] = t;
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int c = 0; c < NC; ++c) part[c] = colv[lane + 64 * c < n ? lane + 64 * c : 0];
-    __syncthreads();   // red / colv are reused by the next total
+    lds_barrier();   // red / colv are reused by the next total
   };
-  // (the rows of the groups the right side skipped: masked here; the others again, a no-op)
+  // the rows of the groups the right side skipped (wave-uniform: none when 16 NR == n)
 #pragma unroll
-  for (int r = 0; r < NR; ++r) mask_row(r);
+  for (int r0 = 0; r0 < NR; r0 += RG)
+    if (w + 16 * r0 >= n) {
+#pragma unroll
+      for (int u = 0; u < RG; ++u) mask_row(r0 + u);
+    }
   float q[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -386,7 +398,7 @@ __global__ __launch_bounds__(1024) void sam_slice_kernel(const float *__restrict
     float se = 0.f;
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-      x[r][c] = exp_le0(x[r][c] - q[c]);   // rows k >= n: -inf -> 0
+      x[r][c] = exp_shift(x[r][c], q[c] * SAM_L2E);   // rows k >= n: -inf -> 0
       se += x[r][c];
     }
     q[c] = se;
@@ -394,26 +406,74 @@ __global__ __launch_bounds__(1024) void sam_slice_kernel(const float *__restrict
   column_total(q, false);   // q = column sum of exponentials
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    const float inv = 1.0f / q[c];
+    const float inv = __builtin_amdgcn_rcpf(q[c]);
     float acc = 0.f;
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
+    for (int r = 0; r < NR; ++r) {   // (rows k >= n: p = 0, as above)
       const int k = w + 16 * r;
       const float p = x[r][c] * inv;
-      if (k < n) acc += conf ? p * log2_pos(p + 1e-6f) : p * (float)k;
+      acc = fmaf(p, conf ? log2_pos(p + 1e-6f) : (float)k, acc);
     }
     q[c] = acc;
   }
   // the column totals of the accumulated terms, written by the threads that own column tid
 #pragma unroll
   for (int c = 0; c < NC; ++c) red[w][lane + 64 * c] = q[c];
-  __syncthreads();
+  lds_barrier();
   if (tid < n) {
     float acc = red[0][tid];
 #pragma unroll
     for (int i = 1; i < 16; ++i) acc += red[i][tid];
     outL[ob + tid] = conf ? 1.0f - (-acc) / g.log2W2 : (float)tid - acc;
   }
+}
+
+// loads of one slice + slice_reduce, per volume kind (the kernel branches once, before the loads:
+// with the branch after them the compiler shared values across both inlined bodies and spilled)
+template <int NR, int NC, bool CONF, bool RT = false>
+__device__ __forceinline__ void slice_one(const float *__restrict__ src, float (&red)[16][NC * 64],
+                                          float (&colv)[NC * 64], const int n, const SGeo &g, float *outL,
+                                          float *outR, const long ob, const int w, const int lane, const int tid,
+                                          const bool rconf = false) {
+  float x[NR][NC];
+  // unconditional loads of clamped cells, all issued before any arithmetic; the cells outside the
+  // slice become -inf only where they are first used (a load under the (k < n && j < n) predicate
+  // compiled to a branch around each load; a select right after the load, to a branch on the
+  // wave-uniform k < n with an immediate vmcnt(0) per load)
+  // (buffer loads: the row offset wave-uniform in an SGPR, the column offset per lane; 64-bit
+  // addresses cost a VALU add per load)
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(src), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int kc = min(w + 16 * r, n - 1);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      x[r][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, min(lane + 64 * c, n - 1) * 4,
+                                                                               kc * (int)g.sk * 4, 0));
+  }
+  slice_reduce<NR, NC, CONF, RT>(x, red, colv, n, g, outL, outR, ob, w, lane, tid, rconf);
+}
+
+template <int NR, int NC>
+__global__ __launch_bounds__(1024) void sam_slice_kernel(const float *__restrict__ vd, const float *__restrict__ vc,
+                                                         SGeo g, int n, float *dL, float *dR, float *cL, float *cR,
+                                                         int y0) {
+  __shared__ float red[16][NC * 64];
+  __shared__ float colv[NC * 64];
+  const int conf = y0 + (int)blockIdx.y;
+  const int bh = blockIdx.x, b = bh / g.H, h = bh % g.H;
+  const long so = (long)b * g.sb + (long)h * g.sh;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long ob = (long)b * g.obs + (long)h * n;
+  if constexpr (NR * NC > 64)
+    slice_one<NR, NC, false, true>(conf ? vc + so : vd + so, red, colv, n, g, conf ? cL : dL, conf ? cR : dR, ob, w,
+                                   lane, tid, conf != 0);
+  else if (conf)
+    slice_one<NR, NC, true>(vc + so, red, colv, n, g, cL, cR, ob, w, lane, tid);
+  else
+    slice_one<NR, NC, false>(vd + so, red, colv, n, g, dL, dR, ob, w, lane, tid);
 }
 
 #ifndef SA_SAM_DIAG
@@ -546,7 +606,7 @@ bool launch_slices(const float *vd, const float *vc, const SGeo &g, int B, int n
     return true;
   }
 #define SA_SLICE(NR_, NC_)                                                                          \
-  if (n <= 16 * NR_ && n <= 64 * NC_) {                                                             \
+  if (n <= 16 * NR_ && n <= 64 * NC_ && (long)(n - 1) * g.sk * 4 + (long)n * 4 < 0x7fffffffL) {     \
     sam_slice_kernel<NR_, NC_><<<grid, 1024, 0, s>>>(vd, vc, g, n, dL, dR, cL, cR, y0);           \
     return true;                                                                                    \
   }
@@ -590,7 +650,10 @@ int launch_side(LineJob jd, LineJob jc, const SGeo &g, int B, int left, hipStrea
 static int sa_softargmin_one_pass = 1;
 extern "C" void sa_softargmin_set_one_pass(int on) {
   // 0: the two line-kernel launches; 1 (default): the one-pass slice kernel; 2: the one-pass
-  // slice kernel with 16-byte rows where they apply (cfg2: 132 against 124 us, so not default)
+  // slice kernel with 16-byte rows where they apply (cfg2: 128 against 119 us, so not default).
+  // (Round 6 measured a persistent form that prefetches the next slice's first 144 rows into LDS
+  // by LDS-DMA while reducing the current one: 136.6 against 118.7 us.  The slice reductions, not
+  // the loads, bound this kernel: ~24 us of arithmetic per slice and volume, one block per CU.)
   sa_softargmin_one_pass = on ? 1 : 0;
   sa_softargmin_v4 = on == 2 ? 1 : 0;
 }
