@@ -24,7 +24,7 @@ torch.cuda.synchronize()
 nb = ops._wino4_blocks(x, U)
 fn = N.lib().sa_w4_clock_read
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-buf = np.zeros((min(nb, 65536), 10), dtype=np.uint64)
+buf = np.zeros((min(nb, 65536), 12), dtype=np.uint64)
 assert fn(buf.ctypes.data, buf.shape[0]) == 0
 d_t = (buf[:, 2] - buf[:, 0]).astype(np.float64)
 d_r = (buf[:, 3] - buf[:, 1]).astype(np.float64)
@@ -36,4 +36,5 @@ print(f"{nb} blocks: clock median {np.median(clk):.0f} MHz (p10 {np.percentile(c
       f"{np.median(buf[:, 6] - buf[:, 5]):.0f}, barrier + stats {np.median(buf[:, 7] - buf[:, 6]):.0f}, stores "
       f"{np.median(buf[:, 2] - buf[:, 7]):.0f}); first chunk: last wave started at "
       f"{np.median(buf[:, 9].astype(np.int64) - buf[:, 0].astype(np.int64)):.0f}, wave 0 issued it at "
-      f"{np.median(buf[:, 8] - buf[:, 0]):.0f}")
+      f"{np.median(buf[:, 8] - buf[:, 0]):.0f} (item decoded at {np.median(buf[:, 10] - buf[:, 0]):.0f}, chunk 0's filter DMA "
+      f"issued at {np.median(buf[:, 11] - buf[:, 0]):.0f})")

@@ -531,7 +531,8 @@ __device__ __forceinline__ void w4_flowhead(const W4Prob &P, const W4Gate &GT, f
 #ifdef SA_W4_CLOCK
 // diagnostic build only: per block (s_memtime, s_memrealtime) at the start and the end of wave 0,
 // then s_memtime after the first chunk's barrier and after the main loop
-__device__ unsigned long long g_w4_clock[65536][10];   // + [8] chunk 0 issued, [9] last wave's start
+__device__ unsigned long long g_w4_clock[65536][12];   // + [8] chunk 0 issued, [9] last wave's start,
+                                                      // [10] work item decoded, [11] chunk 0's filter DMA issued
 #endif
 
 // One work item: the block's 64 tiles x 32 output channels (HF: this wave's point-column half).
@@ -584,12 +585,18 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
   // patch DMA: the chunk's image is [channel][PR rows][PG groups of 4 floats], dense, starting
   // at (y0 - 1, x0 - 4); wave-instruction gi fills groups 64 gi .. 64 gi + 63 (lane-linear)
   // chunk 0's filters first: their offsets need no patch geometry
+#ifdef SA_W4_CLOCK
+  if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][10] = __builtin_amdgcn_s_memtime();
+#endif
   if (SA_W4_DIAG != 4) {
 #pragma unroll
     for (int j = 0; j < UPW; ++j)
       if (wv + NWAVE * j < UDMA)
         dma16(uin, smem + PBUF + (wv + NWAVE * j) * 256, u_src(wv + NWAVE * j), u_chunk(0));
   }
+#ifdef SA_W4_CLOCK
+  if (HF == 0 && tid == 0) g_w4_clock[blockIdx.x & 65535][11] = __builtin_amdgcn_s_memtime();
+#endif
   const int npi = (KC * PS + 63) >> 6;
   int po[PDMA];
   // input transform: per piece j, 4 bits at 4j = the group's channel in the chunk + 1 (0: padding
@@ -700,6 +707,8 @@ __device__ __forceinline__ bool w4_body(const W4Prob &P, const W4Gate *gate, con
   for (int k = 0; k < CG / 2; ++k) bpre[k] = P.bias ? P.bias[co0 + (2 * k + HF) * 16 + (lane & 15)] : 0.0f;
   // static priority for waves 4-7 (split kernel forward: 66.8 -> 66.5 ms/step, two interleaved passes)
   if (HF == 1) __builtin_amdgcn_s_setprio(1);
+  // (issuing each piece as soon as its offset is known, ~1.6k cycles earlier, did not land chunk 0
+  // any sooner: 6.6k vs 6.2k cycles at xc08, forward 59.6 vs 59.8 ms/step, scripts/w4_clock.py)
   if (SA_W4_DIAG != 4) issue_p0();
   // Input transform: v -> act(v * scale + shift), scale = s, shift = t - m * s per channel
   // (in_pstride 0) or per (image, channel) (in_pstride = Cin).  Each lane transforms the
@@ -1229,7 +1238,7 @@ extern "C" int sa_conv2d_wino4_weights_split(const float *weight, int Cout, int 
 
 #ifdef SA_W4_CLOCK
 extern "C" int sa_w4_clock_read(unsigned long long *out, int n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4_clock), sizeof(unsigned long long) * 10 * n) == hipSuccess ? 0 : -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4_clock), sizeof(unsigned long long) * 12 * n) == hipSuccess ? 0 : -1;
 }
 #endif
 
