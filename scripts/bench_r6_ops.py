@@ -20,8 +20,13 @@ n = 2 * H4 * W4
 m = torch.rand(B, n, device=dev, generator=g)
 d = (40 * m + 3) + 5 + torch.randn(B, n, device=dev, generator=g)
 c = torch.rand(B, n, device=dev, generator=g)
-for sb, name in ((True, "one launch"), (False, "round-5 grid form")):
-    print(f"weighted_lsq B={B} n={n} {name}: {timeit(lambda: ops.weighted_lsq(m, d, c, single_block=sb), 20):.1f} us")
+dz = d.clone()
+dz[:, : n // 2] = -1.0   # half the keys relu'd to 0 (the model's synthetic-weight disparities)
+dz = dz[:, torch.randperm(n, device=dev, generator=g)].contiguous()
+for dd, what in ((d, "positive keys"), (dz, "half zeros")):
+    for sb, name in ((True, "one launch"), (False, "round-5 grid form")):
+        print(f"weighted_lsq B={B} n={n} {what} {name}: "
+              f"{timeit(lambda: ops.weighted_lsq(m, dd, c, single_block=sb), 20):.1f} us")
 flow = torch.randn(B, 1, H4, W4, device=dev) * 5
 mask = torch.randn(B, 144, H4, W4, device=dev)
 t = timeit(lambda: ops.convex_upsample(flow, mask, 4), 20)

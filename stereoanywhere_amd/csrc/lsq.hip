@@ -150,6 +150,12 @@ __device__ long long g_lsq_clock[8];
 #define LSQ_STAMP(i)
 #endif
 constexpr int L1_BINS = 16384, L1_SHIFT = 17, L1_POOL = 16384, L1_SEG = 8, L1_CH = 16;
+// Bin 0 holds the exact zeros alone, bin b >= 1 the positive keys whose top bits are b - 1: the
+// relu'd zeros can be half of a sample (the model's synthetic-weight disparities; an edge's
+// out-of-view pixels), and a quantile among them is exactly 0 without pooling or a radix pass (in
+// one shared bin with the smallest positive keys they overflowed the pool: the four-pass fallback,
+// 177 against ~75 us).  The largest key (NaN 0x7fc00000) maps to bin 16353 < L1_BINS.
+__device__ __forceinline__ unsigned bin_of(unsigned k) { return k ? (k >> L1_SHIFT) + 1u : 0u; }
 
 // f(key, index, valid) over this thread's keys of dd[0 .. n), in chunks of L1_CH loads in flight
 template <class Fn>
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq1_kernel(const float *__restri
   __syncthreads();
   LSQ_STAMP(0);
   // A: histogram of the top bits
-  lsq_stream_keys(dd, n, [&](unsigned k, int, bool v) { hist_add(hist, k >> L1_SHIFT, v); });
+  lsq_stream_keys(dd, n, [&](unsigned k, int, bool v) { hist_add(hist, bin_of(k), v); });
   __syncthreads();
   LSQ_STAMP(1);
   {
@@ -325,7 +331,7 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq1_kernel(const float *__restri
       if (src == r) {
         s_off[r] = off;
         s_cnt[r] = 0u;
-        off += hist[s_bin[r]];
+        if (s_bin[r] != 0u) off += hist[s_bin[r]];   // (the zero bin is not pooled: its key is 0)
       }
     }
     fall = off > (unsigned)L1_POOL;
@@ -354,15 +360,27 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq1_kernel(const float *__restri
     t1 += (double)a1 * y;
     t2 += (double)w * y;
   };
+  // the zero keys' terms (d = 0: no t1 / t2 part), kept apart until the band is known: they are
+  // inside it iff the lower quantile is 0, possible only when the floor rank's bin is the zero bin
+  double z11 = 0, z12 = 0, z22 = 0;
+  const bool zero_lo = lb[0] == 0u;
+  auto add_zero = [&](float mv, float cv) __attribute__((always_inline)) {
+    const float m = fabsf(mv);
+    const float w = sqrtf(fabsf(cv) * 0.9f + 0.1f);
+    const float a1 = m * w;
+    z11 += (double)a1 * a1;
+    z12 += (double)a1 * w;
+    z22 += (double)w * w;
+  };
   if (!fall) {
     // B: copy the selected bins' keys (and indices) into their pool slices (wave-aggregated
     // appends); the normal equations of the keys strictly between the quantiles' bins
     const unsigned in_lo = lb[1], in_hi = lb[2];   // (b0 <= b1 <= b2 <= b3)
     auto append = [&](unsigned k, int j, bool valid) __attribute__((always_inline)) {
-      const unsigned bin = k >> L1_SHIFT;
+      const unsigned bin = bin_of(k);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (lsrc[r] != r) continue;   // (uniform)
+        if (lsrc[r] != r || lb[r] == 0u) continue;   // (uniform; the zero bin is not pooled)
         const bool hit = valid && bin == lb[r];
         const unsigned long long m = __ballot(hit);
         if (!m) continue;
@@ -390,15 +408,16 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq1_kernel(const float *__restri
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         const int j = base + c * LSQ_THREADS + t;
-        const unsigned bin = kv[c] >> L1_SHIFT;
+        const unsigned bin = bin_of(kv[c]);
         append(kv[c], j, j < n);
         if (j < n && bin > in_lo && bin < in_hi) add_terms(__uint_as_float(kv[c]), mv[c], cv[c]);
+        if (zero_lo && j < n && bin == 0u) add_zero(mv[c], cv[c]);
       }
     }
     __syncthreads();
   LSQ_STAMP(3);
     // C: the low 17 bits of each rank's key as a 9-bit and an 8-bit digit (seg reused as [4][512])
-    if (t < 4) s_pre[t] = lb[t] << L1_SHIFT;
+    if (t < 4) s_pre[t] = lb[t] ? (lb[t] - 1u) << L1_SHIFT : 0u;   // (a zero-bin rank: key 0, done)
     for (int pass = 0; pass < 2; ++pass) {
       const int sh = pass == 0 ? 8 : 0, bits = pass == 0 ? 9 : 8;   // bits 16..8, then 7..0
       for (int i = t; i < 4 * 512; i += LSQ_THREADS) seg[i] = 0u;
@@ -409,12 +428,12 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq1_kernel(const float *__restri
       for (int r = 0; r < 4; ++r) {
         pre[r] = s_pre[r];
         src[r] = r;
-        for (int q = r - 1; q >= 0; --q)
-          if (pre[q] == pre[r]) src[r] = q;
+        for (int q = r - 1; q >= 0; --q)   // (same bin too: a bin-1 rank's prefix is 0 like the zero bin's)
+          if (pre[q] == pre[r] && lb[q] == lb[r]) src[r] = q;
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (src[r] != r) continue;   // (uniform)
+        if (src[r] != r || lb[r] == 0u) continue;   // (uniform)
         const int L = lsrc[r];
         const unsigned cnt = s_cnt[L], off = s_off[L];
         for (unsigned e0 = 0; e0 < cnt; e0 += LSQ_THREADS) {
@@ -425,7 +444,7 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq1_kernel(const float *__restri
         }
       }
       __syncthreads();
-      if (wv < 4) {
+      if (wv < 4 && pick4(lb, wv) != 0u) {
         int d;
         unsigned below;
         wave_find<8>(seg + 512 * pick4(src, wv), s_rem[wv], d, below);
@@ -453,6 +472,11 @@ __global__ __launch_bounds__(LSQ_THREADS) void lsq1_kernel(const float *__restri
   __syncthreads();
   LSQ_STAMP(5);
   const float qlo = qv[0], qhi = qv[1];
+  if (!fall && zero_lo && qlo <= 0.0f) {   // the zeros are inside the band (d = 0 >= lo = 0)
+    s11 += z11;
+    s12 += z12;
+    s22 += z22;
+  }
   if (!fall) {   // the pooled keys inside the band
     const unsigned total = s_total;
     for (unsigned e = t; e < total; e += LSQ_THREADS) {

@@ -392,6 +392,30 @@ def test_weighted_lsq_quantile_band_vs_oracle(n, single_block):
     np.testing.assert_allclose(c(sh), rsh, rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("single_block", [False, True])
+@pytest.mark.parametrize("zfrac", [0.1999, 0.2, 0.2001, 0.5, 0.95])
+def test_weighted_lsq_zero_heavy(zfrac, single_block):
+    """Samples whose relu'd zeros reach the lower (and at 0.95 the upper) quantile, at the model's
+    n: the zero bin of the one-launch kernel (its key is 0 without pooling; the zeros' terms join
+    the band only when the lower quantile is 0), the floor / ceil ranks straddling the zeros'
+    end (0.2: rank 13055 is a zero, 13056 the next key), and in sample 1 denormal positives right
+    above the zeros (their bin's prefix is 0 like the zero bin's)."""
+    n, B = 65280, 2
+    rng = np.random.default_rng(int(zfrac * 1e4))
+    m = rng.random((B, n)).astype(np.float32)
+    d = (40 * m + 3 + rng.standard_normal((B, n))).astype(np.float32)
+    nz = int(round(zfrac * n))
+    d[:, :nz] = -rng.random(nz).astype(np.float32)
+    d[1, nz:nz + 50] = np.float32(1e-42)
+    perm = rng.permutation(n)
+    m, d = m[:, perm].copy(), d[:, perm].copy()
+    cf = rng.random((B, n)).astype(np.float32)
+    sc, sh = ops.weighted_lsq(g(m), g(d), g(cf), single_block=single_block)
+    rsc, rsh = R.weighted_lsq(m, d, cf)
+    np.testing.assert_allclose(c(sc), rsc, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(c(sh), rsh, rtol=1e-5, atol=1e-4)
+
+
 def test_mirror_and_coords():
     rng = np.random.default_rng(2)
     B, H, W = 2, 8, 40
