@@ -29,11 +29,12 @@ extern "C" {
  * that sa_abi_version() == SA_ABI_VERSION and that sa_struct_size(SA_STRUCT_*) equals its own
  * sizeof: the arrays of SaWinoProblem / SaGateEpilogue / SaResampleJob are read at the library's
  * stride, so a host built against another layout would hand over misread fields.
+ *   7: sa_feature_gates / SaFeatureGateJob added (additive: no earlier entry point changed)
  *   6: round 6 (the implicit-GEMM entry points removed; sa_struct_size, sa_conv3d_mf_get_planes)
  *   5: SaWinoProblem gained the residual-epilogue fields (skip ... out_act); sa_conv2d_k3_wino4_launch
  *      took a guard flag; sa_conv2d_wino4_weights_cb removed */
-#define SA_ABI_VERSION 6
-enum { SA_STRUCT_WINO_PROBLEM = 0, SA_STRUCT_GATE_EPILOGUE = 1, SA_STRUCT_RESAMPLE_JOB = 2 };
+#define SA_ABI_VERSION 7
+enum { SA_STRUCT_WINO_PROBLEM = 0, SA_STRUCT_GATE_EPILOGUE = 1, SA_STRUCT_RESAMPLE_JOB = 2, SA_STRUCT_FEATURE_GATE_JOB = 3 };
 int sa_abi_version(void);
 /* sizeof the struct `which` (SA_STRUCT_*) as the library was built, -1 for an unknown id */
 long sa_struct_size(int which);
@@ -218,6 +219,26 @@ typedef struct SaResampleJob {
   int out_pitch;
 } SaResampleJob;
 int sa_resample_multi(int njobs, const SaResampleJob *jobs, void *stream);
+
+/* a4 — the DoubleFeatureAtt gates of the hourglass (submodule.py:113-140; hourglass.py:66-91): per
+ * job and image, out[c] = sigmoid(b1[c] + sum_k w1[c][k] leaky(IN(conv3x3(in, w3[k])))) over 32
+ * hidden channels (conv3x3 with zero padding and no bias, InstanceNorm2d without affine, eps 1e-5,
+ * biased variance, LeakyReLU 0.01), in a one-channel plane [B][H][W] (image stride in_bs), w3
+ * [32][9], w1 [C][32], b1 [C] (NULL: 0), out [B][C][H][W] (image stride out_bs), C <= 64.  Up to
+ * SA_GATE_MAX_JOBS jobs in two launches; ws of sa_feature_gates_ws_size bytes (fp64 partial sums,
+ * no zeroing needed: every slot is written before it is read). */
+#define SA_GATE_MAX_JOBS 8
+typedef struct SaFeatureGateJob {
+  const float *in;
+  long in_bs;
+  int B, H, W;
+  const float *w3, *w1, *b1;
+  int C;
+  float *out;
+  long out_bs;
+} SaFeatureGateJob;
+long sa_feature_gates_ws_size(int njobs, const SaFeatureGateJob *jobs);
+int sa_feature_gates(int njobs, const SaFeatureGateJob *jobs, void *ws, void *stream);
 int sa_relu_copy(const float *in, long in_bs, int B, int C, int HW, float *out, long out_bs,
                  void *stream);
 int sa_flow_update(float *coords_x, const float *delta, long delta_bs, int B, int H, int W,

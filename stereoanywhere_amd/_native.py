@@ -43,7 +43,15 @@ class SaResampleJob(ctypes.Structure):
                 ("Ho", I), ("Wo", I), ("out", P), ("out_bs", L), ("out_pitch", I)]
 
 
+class SaFeatureGateJob(ctypes.Structure):
+    """include/stereoanywhere_hip.h: one DoubleFeatureAtt branch of sa_feature_gates."""
+    _fields_ = [("in_", P), ("in_bs", L), ("B", I), ("H", I), ("W", I), ("w3", P), ("w1", P), ("b1", P),
+                ("C", I), ("out", P), ("out_bs", L)]
+
+
 SIGNATURES = {
+    "sa_feature_gates_ws_size": (L, [I, P]),
+    "sa_feature_gates": (I, [I, P, P, P]),
     "sa_abi_version": (I, []),
     "sa_conv1x1_weights_size": (L, [I, I]),
     "sa_conv1x1_weights": (I, [P, I, I, P, P]),
@@ -199,7 +207,7 @@ def lib() -> ctypes.CDLL:
 
 # include/stereoanywhere_hip.h SA_ABI_VERSION: the library must be built from the same header as
 # these bindings (the struct arrays are read at the library's stride)
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 def _check_abi(h) -> None:
@@ -210,7 +218,7 @@ def _check_abi(h) -> None:
     v = int(h.sa_abi_version())
     if v != ABI_VERSION:
         raise NativeError(f"{LIB_PATH} implements ABI version {v}, these bindings {ABI_VERSION}: rebuild it")
-    for which, st in ((0, SaWinoProblem), (1, SaGateEpilogue), (2, SaResampleJob)):
+    for which, st in ((0, SaWinoProblem), (1, SaGateEpilogue), (2, SaResampleJob), (3, SaFeatureGateJob)):
         got = int(h.sa_struct_size(which))
         if got != ctypes.sizeof(st):
             raise NativeError(f"{LIB_PATH}: {st.__name__} is {got} bytes in the library, "

@@ -231,9 +231,28 @@ class Hourglass(nn.Module):
         normalised / gated / upsampled / concatenated volume is ever written."""
         from . import ops
         slope = self.final_agg[0].act_fn.negative_slope
+        # the four DoubleFeatureAtt gates (both sides) depend on the feature pyramid only: all eight
+        # branches in two launches up front (sa_feature_gates), not torch/MIOpen per branch
+        pre = {}
+        gw = fw.get("gates")
+        if gw is not None:
+            keys = (("fa0", 1), ("fa1", 2), ("fu1", 1), ("ffu", 0))
+            jobs = []
+            for key, lvl in keys:
+                wl, wr = gw[key]
+                jobs += [(fl[lvl].contiguous(), wl), (fr[lvl].contiguous(), wr)]
+            outs = ops.feature_gates(jobs)
+            pre = {id(att): (outs[2 * n], outs[2 * n + 1]) for n, att in enumerate(
+                (self.feature_atts[0], self.feature_atts[1], self.feature_atts_up[1], self.final_feature_atts_up))}
 
         def gated(v, att, i):
-            g = self._gate(att, fl[i], fr[i], v.raw.shape)
+            if id(att) in pre:
+                g = pre[id(att)]
+                D, H, W = v.raw.shape[2:]
+                if tuple(g[0].shape[2:]) != (H, W) or tuple(g[1].shape[2:]) != (H, D):
+                    g = None
+            else:
+                g = self._gate(att, fl[i], fr[i], v.raw.shape)
             if g is None:
                 raise RuntimeError("fused hourglass: feature pyramid does not match the volume")
             return v.with_gate(g)
@@ -275,7 +294,11 @@ class Hourglass(nn.Module):
         d01, a11, a12 = (k3(self.down_layers[0][1].conv.weight), k3(self.agg_layers[1][1].conv.weight),
                          k3(self.agg_layers[1][2].conv.weight))
         wd, mf = ops.conv3d_wd_weights, ops.conv3d_mf_weights
-        return dict(
+        fg = ops.feature_gate_weights
+        gates = {key: (fg(att.feat_att_left), fg(att.feat_att_right)) for key, att in (
+            ("fa0", self.feature_atts[0]), ("fa1", self.feature_atts[1]), ("fu1", self.feature_atts_up[1]),
+            ("ffu", self.final_feature_atts_up))}
+        return dict(gates=gates,
             fa1_wd=wd(fa1), fa2_wd=wd(fa2), cls_wd=wd(cls), d01_wd=wd(d01), a11_wd=wd(a11), a12_wd=wd(a12),
             fa1_mf=mf(fa1), fa2_mf=mf(fa2), d01_mf=mf(d01), a11_mf=mf(a11), a12_mf=mf(a12),
             d11_mf=mf(k3(self.down_layers[1][1].conv.weight)),

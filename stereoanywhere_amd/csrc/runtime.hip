@@ -129,6 +129,7 @@ extern "C" long sa_struct_size(int which) {
     case SA_STRUCT_WINO_PROBLEM: return (long)sizeof(SaWinoProblem);
     case SA_STRUCT_GATE_EPILOGUE: return (long)sizeof(SaGateEpilogue);
     case SA_STRUCT_RESAMPLE_JOB: return (long)sizeof(SaResampleJob);
+    case SA_STRUCT_FEATURE_GATE_JOB: return (long)sizeof(SaFeatureGateJob);
     default: return -1;
   }
 }

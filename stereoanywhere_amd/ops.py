@@ -519,6 +519,48 @@ def resample_multi(*jobs) -> None:
     _account("gru_plumbing", nbytes)
 
 
+def feature_gate_weights(branch) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
+    """(w3 [32, 9], w1 [C, 32], b1 [C]) of a DoubleFeatureAtt branch (BasicConv(1 -> 32, 3x3) +
+    Conv2d(32 -> C, 1x1)) for sa_feature_gates."""
+    conv, lin = branch[0].conv, branch[1]
+    if conv.weight.shape[1:] != (1, 3, 3) or conv.weight.shape[0] != 32 or lin.weight.shape[1:] != (32, 1, 1):
+        raise RuntimeError(f"feature_gate_weights: unsupported branch {tuple(conv.weight.shape)} / "
+                           f"{tuple(lin.weight.shape)}")
+    b1 = None if lin.bias is None else lin.bias.detach().float().contiguous()
+    return (conv.weight.detach().float().reshape(32, 9).contiguous(),
+            lin.weight.detach().float().reshape(lin.weight.shape[0], 32).contiguous(), b1)
+
+
+def feature_gates(jobs) -> list:
+    """The DoubleFeatureAtt branch outputs sigmoid(conv1x1(leaky(IN(conv3x3(feat))))) for up to 8
+    jobs (feat [B, 1, H, W], (w3, w1, b1) from feature_gate_weights) in two launches
+    (sa_feature_gates); returns a [B, C, H, W] tensor per job."""
+    if not 1 <= len(jobs) <= 8:
+        raise RuntimeError("feature_gates: 1..8 jobs")
+    arr = (N.SaFeatureGateJob * len(jobs))()
+    outs = []
+    nbytes = 0.0
+    for j, (x, (w3, w1, b1)) in zip(arr, jobs):
+        _check(x, "feat")
+        B, Cin, H, W = x.shape
+        if Cin != 1:
+            raise RuntimeError(f"feature_gates: one-channel features, got {tuple(x.shape)}")
+        for t, nm in ((w3, "w3"), (w1, "w1")):
+            _check(t, nm)
+        C = w1.shape[0]
+        out = torch.empty(B, C, H, W, device=x.device, dtype=torch.float32)
+        j.in_, j.in_bs, j.B, j.H, j.W = x.data_ptr(), x.stride(0), B, H, W
+        j.w3, j.w1, j.b1, j.C = w3.data_ptr(), w1.data_ptr(), _ptr(b1), C
+        j.out, j.out_bs = out.data_ptr(), out.stride(0)
+        outs.append(out)
+        nbytes += 4.0 * B * H * W * (2 + C)
+    ws = torch.empty(int(N.lib().sa_feature_gates_ws_size(len(jobs), ctypes.addressof(arr))), dtype=torch.uint8,
+                     device=jobs[0][0].device)
+    N.call("sa_feature_gates", len(jobs), ctypes.addressof(arr), ws.data_ptr(), _stream(jobs[0][0]))
+    _account("misc", nbytes)
+    return outs
+
+
 def relu_copy(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
     B, C, H, W = x.shape
     if tuple(out.shape) != (B, C, H, W):
