@@ -68,14 +68,19 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const float *__restri
 // MFMAs of all four 16-channel blocks); the B operands (weights, tap 4 j + k, channel 16 cb +
 // l % 16) stay in 100 VGPRs for the block's lifetime.  Accumulator lane l holds pixels
 // 4 (l / 16) .. + 3 of channel l % 16: one float4 store per (M-tile, channel block).
+// F1_CIN = 1: the model's call (round 6): the stereo flow's vertical channel is identically zero
+// (sa_flow_update / the flow_x resample job write 0), so its 49 taps only add exact zeros; with
+// them skipped (13 instead of 25 K steps) the sums are the same.
 using f32x4 = __attribute__((ext_vector_type(4))) float;
-constexpr int F1_K = 7, F1_CIN = 2, F1_TAPS = F1_CIN * F1_K * F1_K, F1_KS = (F1_TAPS + 3) / 4, F1_L = T + F1_K - 1;
+constexpr int F1_K = 7, F1_L = T + F1_K - 1;
 
+template <int F1_CIN>
 __global__ __launch_bounds__(256) void conv2d_f1_mfma_kernel(const float *__restrict__ in, long in_bs, int H, int W,
                                                              const float *__restrict__ wt,
                                                              const float *__restrict__ bias, int relu,
                                                              float *__restrict__ out, long out_bs) {
-  __shared__ float tile[F1_CIN * F1_L * F1_L + 4];
+  constexpr int F1_TAPS = F1_CIN * F1_K * F1_K, F1_KS = (F1_TAPS + 3) / 4;
+  __shared__ float tile[2 * F1_L * F1_L + 4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int x0 = blockIdx.x * T, y0 = blockIdx.y * T, b = blockIdx.z;
   const int m = lane & 15, kq = lane >> 4;
@@ -275,8 +280,10 @@ extern "C" int sa_conv2d_small(const float *in, long in_bs, int B, int Cin, int 
   hipStream_t s = sa::as_stream(stream);
   sa::TimingScope ts(SA_K_CONV_SMALL, s);
   const bool aligned = (reinterpret_cast<uintptr_t>(out) & 15) == 0 && out_bs % 4 == 0;
-  if (Cin == F1_CIN && aligned)
-    conv2d_f1_mfma_kernel<<<grid, 256, 0, s>>>(in, in_bs, H, W, weight, bias, relu, out, out_bs);
+  if (Cin == 2 && aligned)
+    conv2d_f1_mfma_kernel<2><<<grid, 256, 0, s>>>(in, in_bs, H, W, weight, bias, relu, out, out_bs);
+  else if (Cin == 1 && aligned)
+    conv2d_f1_mfma_kernel<1><<<grid, 256, 0, s>>>(in, in_bs, H, W, weight, bias, relu, out, out_bs);
   else
     conv2d_small_kernel<7, 64><<<grid, 256, 0, s>>>(in, in_bs, Cin, H, W, weight, bias, relu, out, out_bs);
   return sa::check_launch("sa_conv2d_small");

@@ -740,7 +740,9 @@ class StereoAnywhere(nn.Module):
             last = it == iters - 1
             # lookup of both pyramids + convc1 + ReLU in one kernel (sample 2b: stereo, 2b+1: mono)
             stereo_blk.lookup_conv1x1_into(coords_x, dw["c1_kc"], enc.convc1.bias, c1, other=mono_blk)
-            fl = ops.conv2d_small(flow, dw["f1"], enc.convf1.bias, 64, 7, relu=True)
+            # (the flow's vertical channel is identically zero, written so by flow_update: convf1
+            # over channel 0 alone adds the same products, without the 49 zero taps)
+            fl = ops.conv2d_small(flow[:, :1], dw["f1"], enc.convf1.bias, 64, 7, relu=True)
             # pool2x(h08) and interp(h32) into gru16's input, one launch
             ops.resample_multi(("pool", h08, x16[:, :128], wid["08"], wid["16"]),
                                ("interp", h32, x16[:, 128:], wid["32"], wid["16"]))

@@ -605,6 +605,24 @@ def _conv2d_small_case(B, H, W):
     torch.testing.assert_close(out, ref, atol=2e-5, rtol=1e-5)
 
 
+def test_conv2d_small_zero_channel_skipped_exactly():
+    """The model's convf1 call passes only the flow's x channel (its y channel is identically
+    zero): the one-channel MFMA kernel equals the two-channel kernel on the zero-padded input
+    value for value, at ragged and model sizes, and torch on the two-channel input."""
+    rng = np.random.default_rng(22)
+    for (B, H, W) in ((2, 37, 52), (4, 136, 240)):
+        x = torch.zeros(B, 2, H, W, device="cuda")
+        x[:, 0] = g(rng.standard_normal((B, H, W)) * 5)
+        w = g(rng.standard_normal((64, 2, 7, 7)) * 0.1)
+        b = g(rng.standard_normal(64) * 0.1)
+        wt = w.permute(1, 2, 3, 0).contiguous()
+        one = ops.conv2d_small(x[:, :1], wt, b, 64, 7, relu=True)
+        two = ops.conv2d_small(x, wt, b, 64, 7, relu=True)
+        assert torch.equal(one, two)
+        ref = torch.relu(torch.nn.functional.conv2d(x, w, b, padding=3))
+        torch.testing.assert_close(one, ref, atol=2e-5, rtol=1e-5)
+
+
 @pytest.mark.parametrize("shape", [(2, 24, 16, 32), (1, 60, 36, 44)])
 def test_fused_hourglass_matches_torch(shape):
     """The 12-launch fused hourglass + classifiers against the same module's torch path
