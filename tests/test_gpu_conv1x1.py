@@ -28,6 +28,9 @@ def _case(B, Cin, Cout, H, W, seed, xscale=1.0):
     (4, 256, 576, 136, 240, 0.25),   # the mask head's 1x1 at configs[1]
     (1, 32, 96, 5, 12, 1.0),         # ragged: 60 pixels (one partial tile), a partial channel block
     (3, 64, 70, 9, 28, 0.5),         # 252 pixels: two tiles, the second partial; Cout % 16 != 0
+    (2, 256, 40, 7, 36, 1.0),        # all-channel form: 3 channel tiles (one wave idle, passes padded)
+    (1, 96, 200, 6, 50, 1.0),        # Cin 96: the round-5 form (the all-channel form takes 64 / 128 / 256)
+    (1, 128, 1040, 4, 24, 1.0),      # Cout > 1024: the round-5 form
 ])
 def test_conv1x1_matches_conv2d(B, Cin, Cout, H, W, scale):
     x, w, b = _case(B, Cin, Cout, H, W, Cin + Cout)
@@ -42,6 +45,14 @@ def test_conv1x1_matches_conv2d(B, Cin, Cout, H, W, scale):
     print(f"{B}x{Cin}->{Cout} {H}x{W}: max|d| vs f64 {e64:.2e} (torch fp32 {e32:.2e}), scale {s:.1f}")
     assert e64 < 2e-6 * s
     assert N.lib().sa_conv1x1_redo_blocks(1) == 0
+
+
+@pytest.mark.parametrize("Cin,Cout", [(128, 256), (96, 64)])
+def test_conv1x1_no_bias(Cin, Cout):
+    x, w, _ = _case(2, Cin, Cout, 10, 30, 11)
+    got = ops.conv1x1(x, ops.conv1x1_weights(w), Cout, None, 0.25)
+    ref = F.conv2d(x.double(), w.double()) * 0.25
+    assert float((got.double() - ref).abs().max()) < 2e-6 * float(ref.abs().max())
 
 
 def test_conv1x1_batch_stride_views():
