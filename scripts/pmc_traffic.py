@@ -38,6 +38,8 @@ FAMILIES = {
     "lsq1_kernel": "weighted_lsq", "convex_up_px_kernel": "convex_upsample", "conv1x1_kernel": "conv1x1",
     "conv1x1_weights_kernel": "conv1x1", "conv3d_s2mf_kernel": "conv3d_fused",
     "tile_gather_pad_kernel": "misc", "tile_stitch_kernel": "misc",
+    # round 6 (late): the all-channel 1x1 form, the native feature gates (accounted as misc)
+    "conv1x1_v2_kernel": "conv1x1", "feature_gate_stats_kernel": "misc", "feature_gate_apply_kernel": "misc",
 }
 
 
