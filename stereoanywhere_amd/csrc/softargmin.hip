@@ -455,13 +455,20 @@ __device__ __forceinline__ void slice_one(const float *__restrict__ src, float (
   slice_reduce<NR, NC, CONF, RT>(x, red, colv, n, g, outL, outR, ob, w, lane, tid, rconf);
 }
 
+#ifndef SA_SAM_CONF_FIRST
+#define SA_SAM_CONF_FIRST 1   // 0: the disparity blocks first (the order before round 6's last change)
+#endif
+
 template <int NR, int NC>
 __global__ __launch_bounds__(1024) void sam_slice_kernel(const float *__restrict__ vd, const float *__restrict__ vc,
                                                          SGeo g, int n, float *dL, float *dR, float *cL, float *cR,
                                                          int y0) {
   __shared__ float red[16][NC * 64];
   __shared__ float colv[NC * 64];
-  const int conf = y0 + (int)blockIdx.y;
+  // with both volumes the confidence blocks (the costlier kind: a log2 per cell and side) take
+  // grid row 0, which the dispatcher issues first: the cheaper disparity blocks fill the last
+  // partial round of one-block-per-CU waves (1088 blocks at cfg2 = 4.25 rounds of 256 CUs)
+  const int conf = gridDim.y == 2 ? SA_SAM_CONF_FIRST ^ (int)blockIdx.y : y0 + (int)blockIdx.y;
   const int bh = blockIdx.x, b = bh / g.H, h = bh % g.H;
   const long so = (long)b * g.sb + (long)h * g.sh;
   const int tid = threadIdx.x, lane = tid & 63;
