@@ -12,7 +12,9 @@ FLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wn
 all: $(OUT)
 
 # packed-f32 SLP vectorisation of the transform math costs register moves and spills beside
-# the 144 MFMA accumulators (and packed VALU is no faster next to MFMAs)
+# the 144 MFMA accumulators (and packed VALU is no faster next to MFMAs).  Required, not a tuning
+# knob: built without it the split instances spill 72-96 B per lane and failed the GPU tests (round
+# 6); tests/test_kernel_resources.py checks this line and the no-spill build.
 build/conv2d_wino4.o: FLAGS += -fno-slp-vectorize
 
 build/%.o: stereoanywhere_amd/csrc/%.hip $(HDR)

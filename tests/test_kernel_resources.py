@@ -47,3 +47,10 @@ def test_conv_kernels_do_not_spill(tmp_path, name, kernel, extra):
     # profiles/ab/r06_w4_pair_ab.txt); bounded, so a real regression still fails
     allowed = {k: 32 for k in hot if "W4CfgILi8ELi8ELb1EEELb0ELb1E" in k}
     assert all(v <= allowed.get(k, 0) for k, v in hot.items()), hot
+
+
+def test_makefile_builds_wino4_without_slp_vectorize():
+    """The product build of conv2d_wino4.hip must keep -fno-slp-vectorize (the no-spill build the
+    check above compiles): without it the split instances spill and gave wrong results on the GPU."""
+    mk = open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "Makefile")).read()
+    assert any(line.startswith("build/conv2d_wino4.o:") and "-fno-slp-vectorize" in line for line in mk.splitlines())
