@@ -16,6 +16,9 @@ all: $(OUT)
 # knob: built without it the split instances spill 72-96 B per lane and failed the GPU tests (round
 # 6); tests/test_kernel_resources.py checks this line and the no-spill build.
 build/conv2d_wino4.o: FLAGS += -fno-slp-vectorize
+# LLVM's wave-priority pass (s_setprio raised until a wave's first memory loads are issued, then
+# lowered): conv2d_wino4 48.36 -> 47.42 ms/step, three interleaved passes (profiles/ab/r06_w4_wave_priority.txt)
+build/conv2d_wino4.o: FLAGS += -mllvm -amdgpu-set-wave-priority
 
 build/%.o: stereoanywhere_amd/csrc/%.hip $(HDR)
 	@mkdir -p build

@@ -34,7 +34,7 @@ def _compile(name, tmp_path, extra=()):
 
 
 @pytest.mark.parametrize("name,kernel,extra", [
-    ("conv2d_wino4.hip", "wino_f4k3_kernel", ("-fno-slp-vectorize",)),
+    ("conv2d_wino4.hip", "wino_f4k3_kernel", ("-fno-slp-vectorize", "-mllvm", "-amdgpu-set-wave-priority")),
     ("conv3d_mfma.hip", "conv3d_mf_kernel", ()),
     ("conv3d_s2mf.hip", "conv3d_s2mf_kernel", ()),
 ])
